@@ -1,0 +1,408 @@
+"""duckdb-fastlane_amd -- MI355X FastLanes scan path, Python binding.
+
+Thin ctypes view of the C-ABI in include/flsgpu.h and include/flswriter.h
+(libflsgpu.so, built in-tree by `make -C duckdb-fastlane_amd`).  It exists for
+tests and bench.py; the product boundary is the C-ABI itself, consumed by the
+C++ DuckDB glue in extension/.  There is no CPU fallback: if the shared library
+is missing, importing this package raises.
+
+Load with pkgload.load() (the directory name has a hyphen).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libflsgpu.so"
+
+if not LIB_PATH.exists():
+    raise ImportError(f"{LIB_PATH} not built: run `make -C {_HERE}` (hipcc --offload-arch=gfx950)")
+
+_lib = C.CDLL(str(LIB_PATH))
+
+# --- enums (include/flswriter.h) -------------------------------------------
+INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64 = 1, 2, 3, 4, 5, 6, 7, 8
+DATE, DECIMAL, VARCHAR = 10, 11, 20
+ENC_AUTO, ENC_FFOR, ENC_DELTA, ENC_DICT, ENC_RLE = 0, 1, 2, 3, 4
+
+NP_DTYPE = {INT8: np.int8, INT16: np.int16, INT32: np.int32, INT64: np.int64,
+            UINT8: np.uint8, UINT16: np.uint16, UINT32: np.uint32, UINT64: np.uint64,
+            DATE: np.int32, DECIMAL: np.int64}
+TYPE_NAMES = {INT8: "TINYINT", INT16: "SMALLINT", INT32: "INTEGER", INT64: "BIGINT",
+              UINT8: "UTINYINT", UINT16: "USMALLINT", UINT32: "UINTEGER", UINT64: "UBIGINT",
+              DATE: "DATE", DECIMAL: "DECIMAL", VARCHAR: "VARCHAR"}
+ROWGROUP = 65536
+
+
+class FlsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class ColumnInfo(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("type", C.c_uint8), ("width", C.c_uint8),
+                ("scale", C.c_uint8), ("out_bytes", C.c_uint8)]
+
+
+class RowGroup(C.Structure):
+    _fields_ = [("rowgroup", C.c_uint32), ("nrows", C.c_uint32), ("first_row", C.c_uint64),
+                ("ncols", C.c_uint32), ("columns", C.POINTER(C.c_void_p))]
+
+
+class DecodeStats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("values", C.c_uint64), ("packed_bytes", C.c_uint64),
+                ("meta_bytes", C.c_uint64), ("out_bytes", C.c_uint64), ("launches", C.c_uint32),
+                ("timed_launches", C.c_uint32), ("kernel_ms_total", C.c_double)]
+
+    @property
+    def algo_bytes(self) -> int:
+        return int(self.packed_bytes + self.meta_bytes + self.out_bytes)
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_P = C.c_void_p
+_sig("fls_last_error", C.c_char_p)
+_sig("fls_version", C.c_char_p)
+_sig("fls_device_count", C.c_int)
+_sig("fls_connect", C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(_P))
+_sig("fls_disconnect", None, _P)
+_sig("fls_read_fls", C.c_int, _P, C.c_char_p, C.POINTER(_P))
+_sig("fls_read_fls_image", C.c_int, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P))
+_sig("fls_table_close", None, _P)
+_sig("fls_table_ncols", C.c_uint32, _P)
+_sig("fls_table_nrows", C.c_uint64, _P)
+_sig("fls_table_row_offset", C.c_uint64, _P)
+_sig("fls_table_nrowgroups", C.c_uint32, _P)
+_sig("fls_table_rowgroup_rows", C.c_int64, _P, C.c_uint32)
+_sig("fls_table_column", C.c_int, _P, C.c_uint32, C.POINTER(ColumnInfo))
+_sig("fls_materialize", C.c_int, _P, C.c_uint32, C.POINTER(C.c_uint8), C.POINTER(RowGroup))
+_sig("fls_scan_begin", C.c_int, _P, C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32)
+_sig("fls_scan_next", C.c_int, _P, C.POINTER(RowGroup))
+_sig("fls_device_upload", C.c_int, _P, C.c_uint32, C.c_uint32)
+_sig("fls_device_decode", C.c_int, _P, C.POINTER(C.c_uint8))
+_sig("fls_device_sync", C.c_int, _P, C.POINTER(DecodeStats))
+_sig("fls_device_column", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64))
+_sig("fls_device_copy_out", C.c_int, _P, C.c_uint32, C.c_uint64, C.c_uint64, _P)
+_sig("fls_device_rows", C.c_uint64, _P)
+_sig("fls_writer_new", _P, C.c_uint64)
+_sig("fls_writer_free", None, _P)
+_sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8)
+_sig("fls_writer_add_rowgroup", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P))
+_sig("fls_writer_finish_file", C.c_int, _P, C.c_char_p)
+_sig("fls_writer_finish_image", C.c_int, _P, C.POINTER(_P), C.POINTER(C.c_uint64))
+_sig("fls_image_free", None, _P)
+_sig("fls_gen_nrows", C.c_int64, C.c_char_p, C.c_double, C.c_uint64)
+_sig("fls_gen_ncols", C.c_int, C.c_char_p)
+_sig("fls_gen_image", C.c_int, C.c_char_p, C.c_double, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int,
+     C.POINTER(_P), C.POINTER(C.c_uint64))
+_sig("fls_gen_values", C.c_int, C.c_char_p, C.c_double, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, _P)
+_sig("fls_gen_dict_string", C.c_char_p, C.c_char_p, C.c_int, C.c_uint32)
+
+lib = _lib
+
+
+def _check(rc: int) -> int:
+    if rc < 0:
+        raise FlsError(rc, (_lib.fls_last_error() or b"").decode(errors="replace"))
+    return rc
+
+
+def last_error() -> str:
+    return (_lib.fls_last_error() or b"").decode(errors="replace")
+
+
+def version() -> str:
+    return _lib.fls_version().decode()
+
+
+def device_count() -> int:
+    return _lib.fls_device_count()
+
+
+# --- images ------------------------------------------------------------------
+class Image:
+    """An .fls file image in host memory (library-allocated, freed on close)."""
+
+    def __init__(self, ptr: int, length: int):
+        self.ptr, self.len = ptr, length
+
+    def tobytes(self) -> bytes:
+        return C.string_at(self.ptr, self.len)
+
+    def view(self) -> np.ndarray:
+        return np.ctypeslib.as_array(C.cast(self.ptr, C.POINTER(C.c_uint8)), shape=(self.len,))
+
+    def write(self, path: str) -> None:
+        Path(path).write_bytes(self.tobytes())
+
+    def close(self) -> None:
+        if self.ptr:
+            _lib.fls_image_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.close()
+
+
+def _take_image(rc, p, n) -> Image:
+    _check(rc)
+    return Image(p.value, n.value)
+
+
+def gen_nrows(workload: str, scale: float = 1.0, nrows: int = 0) -> int:
+    return _check(_lib.fls_gen_nrows(workload.encode(), scale, nrows))
+
+
+def gen_image(workload: str, scale: float = 1.0, nrows: int = 0, rg_begin: int = 0,
+              rg_end: int | None = None, nthreads: int | None = None) -> Image:
+    if rg_end is None:
+        rg_end = 0xFFFFFFFF
+    if nthreads is None:
+        nthreads = min(16, os.cpu_count() or 1)
+    p, n = _P(), C.c_uint64()
+    rc = _lib.fls_gen_image(workload.encode(), scale, nrows, rg_begin, rg_end, nthreads, C.byref(p), C.byref(n))
+    return _take_image(rc, p, n)
+
+
+def gen_values(workload: str, col: int, row_begin: int, n: int, dtype, scale: float = 1.0,
+               nrows: int = 0) -> np.ndarray:
+    out = np.empty(n, dtype=dtype)
+    _check(_lib.fls_gen_values(workload.encode(), scale, nrows, col, row_begin, n, out.ctypes.data))
+    return out
+
+
+def gen_dict_string(workload: str, col: int, code: int) -> str | None:
+    s = _lib.fls_gen_dict_string(workload.encode(), col, code)
+    return None if s is None else s.decode()
+
+
+# --- writer ----------------------------------------------------------------
+def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0) -> Image:
+    """columns: list of (name, type, values, encoding[, width, scale]).
+    values: numpy int array for integer types, list of str/bytes for VARCHAR."""
+    w = _lib.fls_writer_new(row_offset)
+    try:
+        n = None
+        prepped = []
+        for spec in columns:
+            name, ty, vals, enc = spec[:4]
+            width, scale = (spec[4], spec[5]) if len(spec) > 4 else (0, 0)
+            _check(_lib.fls_writer_add_column(w, name.encode(), ty, width, scale, enc))
+            if ty == VARCHAR:
+                bs = [v.encode() if isinstance(v, str) else bytes(v) for v in vals]
+                prepped.append(("s", bs))
+                cnt = len(bs)
+            else:
+                arr = np.ascontiguousarray(np.asarray(vals).astype(NP_DTYPE[ty]))
+                prepped.append(("i", arr))
+                cnt = len(arr)
+            if n is None:
+                n = cnt
+            elif n != cnt:
+                raise ValueError("columns differ in length")
+        for r0 in range(0, n or 0, rowgroup):
+            r1 = min(n, r0 + rowgroup)
+            keep = []
+            data = (_P * len(prepped))()
+            offs = (_P * len(prepped))()
+            for c, (kind, v) in enumerate(prepped):
+                if kind == "i":
+                    part = np.ascontiguousarray(v[r0:r1])
+                    keep.append(part)
+                    data[c] = part.ctypes.data
+                else:
+                    sl = v[r0:r1]
+                    o = np.zeros(len(sl) + 1, dtype=np.uint32)
+                    o[1:] = np.cumsum([len(x) for x in sl], dtype=np.uint64).astype(np.uint32)
+                    buf = np.frombuffer(b"".join(sl) or b"\0", dtype=np.uint8).copy()
+                    keep += [o, buf]
+                    data[c] = buf.ctypes.data
+                    offs[c] = o.ctypes.data
+            _check(_lib.fls_writer_add_rowgroup(w, r1 - r0, data, offs))
+        p, ln = _P(), C.c_uint64()
+        rc = _lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln))
+        return _take_image(rc, p, ln)
+    finally:
+        _lib.fls_writer_free(w)
+
+
+# --- engine ----------------------------------------------------------------
+class Connection:
+    """fastlanes::connect() counterpart: a set of GPUs to shard row groups over."""
+
+    def __init__(self, devices=None):
+        h = _P()
+        if devices:
+            arr = (C.c_int * len(devices))(*devices)
+            _check(_lib.fls_connect(arr, len(devices), C.byref(h)))
+        else:
+            _check(_lib.fls_connect(None, 0, C.byref(h)))
+        self.h = h.value
+        self.devices = list(devices) if devices else [0]
+
+    def read_fls(self, path: str) -> "Table":
+        h = _P()
+        _check(_lib.fls_read_fls(self.h, str(path).encode(), C.byref(h)))
+        return Table(h.value, self)
+
+    def read_image(self, img, copy: bool = False) -> "Table":
+        h = _P()
+        if isinstance(img, Image):
+            _check(_lib.fls_read_fls_image(self.h, img.ptr, img.len, int(copy), C.byref(h)))
+            t = Table(h.value, self)
+            t._keep = img
+            return t
+        buf = bytes(img)
+        _check(_lib.fls_read_fls_image(self.h, buf, len(buf), 1, C.byref(h)))
+        return Table(h.value, self)
+
+    def close(self):
+        if self.h:
+            _lib.fls_disconnect(self.h)
+            self.h = None
+
+
+def _mask(t: "Table", cols) -> C.Array | None:
+    if cols is None:
+        return None
+    m = (C.c_uint8 * t.ncols)()
+    for c in cols:
+        m[c] = 1
+    return m
+
+
+class Table:
+    def __init__(self, h, conn):
+        self.h, self.conn, self._keep = h, conn, None
+
+    def close(self):
+        if self.h:
+            _lib.fls_table_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ncols(self) -> int:
+        return _lib.fls_table_ncols(self.h)
+
+    @property
+    def nrows(self) -> int:
+        return _lib.fls_table_nrows(self.h)
+
+    @property
+    def row_offset(self) -> int:
+        return _lib.fls_table_row_offset(self.h)
+
+    @property
+    def nrowgroups(self) -> int:
+        return _lib.fls_table_nrowgroups(self.h)
+
+    def rowgroup_rows(self, rg: int) -> int:
+        return _check(_lib.fls_table_rowgroup_rows(self.h, rg))
+
+    def column(self, c: int) -> ColumnInfo:
+        ci = ColumnInfo()
+        _check(_lib.fls_table_column(self.h, c, C.byref(ci)))
+        return ci
+
+    def schema(self):
+        out = []
+        for c in range(self.ncols):
+            ci = self.column(c)
+            out.append((ci.name.decode(), ci.type, ci.width, ci.scale, ci.out_bytes))
+        return out
+
+    # -- host-delivered decode (DataChunk path)
+    def _rg_arrays(self, rg: RowGroup, copy=True):
+        cols = []
+        sch = self.schema()
+        for c in range(rg.ncols):
+            p = rg.columns[c]
+            if not p:
+                cols.append(None)
+                continue
+            ob = sch[c][4]
+            a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(rg.nrows * ob,))
+            cols.append(a.copy() if copy else a)
+        return cols
+
+    def materialize(self, rg: int, cols=None):
+        out = RowGroup()
+        _check(_lib.fls_materialize(self.h, rg, _mask(self, cols), C.byref(out)))
+        return out.first_row, self._rg_arrays(out)
+
+    def scan(self, cols=None, rg_begin=0, rg_end=None):
+        if rg_end is None:
+            rg_end = self.nrowgroups
+        _check(_lib.fls_scan_begin(self.h, _mask(self, cols), rg_begin, rg_end))
+        out = RowGroup()
+        while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
+            yield out.first_row, self._rg_arrays(out)
+
+    # -- device-resident decode (bench)
+    def device_upload(self, rg_begin=0, rg_end=None):
+        if rg_end is None:
+            rg_end = self.nrowgroups
+        _check(_lib.fls_device_upload(self.h, rg_begin, rg_end))
+
+    def device_decode(self, cols=None):
+        _check(_lib.fls_device_decode(self.h, _mask(self, cols)))
+
+    def device_sync(self) -> DecodeStats:
+        st = DecodeStats()
+        _check(_lib.fls_device_sync(self.h, C.byref(st)))
+        return st
+
+    def device_column(self, c: int):
+        p, n = _P(), C.c_uint64()
+        _check(_lib.fls_device_column(self.h, c, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    @property
+    def device_rows(self) -> int:
+        return _lib.fls_device_rows(self.h)
+
+    def device_copy_out(self, c: int, row: int = 0, n: int | None = None) -> np.ndarray:
+        ob = self.column(c).out_bytes
+        if n is None:
+            n = self.device_rows - row
+        buf = np.empty(n * ob, dtype=np.uint8)
+        _check(_lib.fls_device_copy_out(self.h, c, row, n, buf.ctypes.data))
+        return buf
+
+
+def as_values(raw: np.ndarray, ty: int) -> np.ndarray:
+    """View decoded raw bytes of an integer column as its numpy dtype."""
+    return raw.view(NP_DTYPE[ty])
+
+
+def string_t_decode(raw: np.ndarray) -> list[bytes]:
+    """Decode DuckDB string_t records (host pointers dereferenced for >12 B)."""
+    rec = raw.reshape(-1, 16)
+    lens = rec[:, :4].copy().view(np.uint32).ravel()
+    out = []
+    for i in range(len(lens)):
+        n = int(lens[i])
+        if n <= 12:
+            out.append(bytes(rec[i, 4:4 + n]))
+        else:
+            ptr = int(rec[i, 8:16].copy().view(np.uint64)[0])
+            out.append(C.string_at(ptr, n))
+    return out

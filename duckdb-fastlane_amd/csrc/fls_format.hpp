@@ -1,0 +1,95 @@
+// fls_format.hpp -- on-disk / in-HBM layout of a FastLanes row-group file.
+//
+// The reference reads `.fls` files through cwida/FastLanes
+// (src/fastlanes_facade.cpp:33-56: connect -> read_fls -> get_rowgroup_reader
+// -> materialize).  That library's byte format is not available here (empty
+// submodule, .gitmodules:9-12), so this container is our own restatement of the
+// FastLanes layout (paper: 1024-value vectors, interleaved bit-packing, FFOR,
+// unified-transposed DELTA, DICT, FastLanes-RLE) designed so that the file body
+// can be uploaded to HBM verbatim and decoded in place: every column chunk is
+// 256-byte aligned, every packed vector 16-byte aligned, per-vector metadata is
+// a flat 32-byte record array.  DESIGN.md "Container format" is the spec.
+#pragma once
+#include <cstdint>
+
+namespace fls {
+
+constexpr uint32_t kVectorSize = 1024;      // values per FastLanes vector
+constexpr uint32_t kRowGroupSize = 65536;   // rows per row group (64 vectors);
+                                            // src/writer/write_fastlane_stream.cpp:21-24
+constexpr uint32_t kVectorsPerRowGroup = kRowGroupSize / kVectorSize;
+constexpr uint32_t kChunkAlign = 256;
+constexpr uint32_t kChunkMagic = 0x43534C46u;  // "FLSC"
+constexpr char kFileMagic[8] = {'F', 'L', 'S', 'A', 'M', 'D', '0', '1'};
+constexpr char kTailMagic[4] = {'F', 'L', 'S', 'F'};
+
+// Encodings (FastLanes expression kinds used on the north-star path)
+enum Encoding : uint8_t {
+    ENC_AUTO = 0,
+    ENC_FFOR = 1,   // fused frame-of-reference + interleaved bit-packing
+    ENC_DELTA = 2,  // unified-transposed delta, deltas FFOR-packed, per-lane bases
+    ENC_DICT = 3,   // dictionary codes FFOR-packed (T=32), per-row-group dictionary
+    ENC_RLE = 4,    // FastLanes-RLE: run values + DELTA(T=16) run-index vector
+};
+
+// Logical column types (cf. reference src/type_mapping.cpp:64-109)
+enum TypeId : uint8_t {
+    TY_INT8 = 1, TY_INT16 = 2, TY_INT32 = 3, TY_INT64 = 4,
+    TY_UINT8 = 5, TY_UINT16 = 6, TY_UINT32 = 7, TY_UINT64 = 8,
+    TY_DATE = 10,     // int32 days since 1970-01-01 (DuckDB date_t)
+    TY_DECIMAL = 11,  // int64 scaled integer (DuckDB DECIMAL(w<=18, s))
+    TY_VARCHAR = 20,  // dictionary strings, decoded to DuckDB string_t (16 B)
+};
+
+inline int type_value_bits(uint8_t t) {
+    switch (t) {
+    case TY_INT8: case TY_UINT8: return 8;
+    case TY_INT16: case TY_UINT16: return 16;
+    case TY_INT32: case TY_UINT32: case TY_DATE: return 32;
+    case TY_INT64: case TY_UINT64: case TY_DECIMAL: return 64;
+    default: return 0;
+    }
+}
+// bytes per decoded value in the output column (string_t = 16 B)
+inline int type_out_bytes(uint8_t t) { return t == TY_VARCHAR ? 16 : type_value_bits(t) / 8; }
+inline bool type_valid(uint8_t t) { return type_out_bytes(t) > 0; }
+
+struct ChunkHeader {          // 64 B, at the start of every column chunk
+    uint32_t magic;           // kChunkMagic
+    uint8_t enc;              // Encoding
+    uint8_t T;                // packing width of the bit-packed stream (8/16/32/64)
+    uint8_t vbits;            // value width in bits (0 for VARCHAR)
+    uint8_t is_str;           // 1 for VARCHAR dictionary
+    uint32_t nvec;            // vectors in this chunk (<= 64)
+    uint32_t nvals;           // rows in this chunk
+    uint64_t meta_off;        // VecMeta[nvec], relative to chunk start
+    uint64_t packed_off;      // packed area, relative to chunk start
+    uint64_t aux_off;         // aux area (bases / dictionary / run values)
+    uint64_t aux_len;
+    uint32_t dict_count;      // DICT: dictionary entries
+    uint32_t reserved0;
+    uint64_t reserved1;
+};
+struct VecMeta {              // 32 B per 1024-value vector
+    uint64_t packed_off;      // relative to packed area; multiple of 16; 128*bw bytes
+    int64_t for_base;         // frame of reference (sign-extended T-bit)
+    uint64_t aux_off;         // relative to aux area (DELTA bases, RLE bases+runs)
+    uint16_t nvals;           // 1..1024
+    uint8_t bw;               // bit width 0..T
+    uint8_t pad;
+    uint32_t aux_count;       // RLE: number of runs
+};
+static_assert(sizeof(ChunkHeader) == 64, "chunk header is 64 B");
+static_assert(sizeof(VecMeta) == 32, "vector meta is 32 B");
+static_assert(alignof(VecMeta) == 8 && alignof(ChunkHeader) == 8, "natural alignment, no padding");
+
+// Footer (little-endian):
+//   u32 version=1, u32 ncols, u64 nrows, u32 nrowgroups, u32 rowgroup_size,
+//   u64 row_offset,
+//   per column: u8 type, u8 width, u8 scale, u8 pad, u16 name_len, name[name_len]
+//   per row group: u32 nrows, per column {u64 chunk_off, u64 chunk_len}
+// File tail (16 B): u64 footer_off, u32 footer_len, "FLSF".
+constexpr uint32_t kFooterVersion = 1;
+constexpr uint32_t kFooterFixed = 32;
+
+}  // namespace fls

@@ -1,0 +1,143 @@
+// fls_reader.hpp -- footer / schema parser (Connection::read_fls counterpart,
+// reference src/fastlanes_facade.cpp:34).  Host only; validates every offset
+// so a corrupt file is reported as FLS_ERR_FORMAT instead of faulting a GPU.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fls_format.hpp"
+
+namespace fls {
+
+struct ColumnMeta {
+    std::string name;
+    uint8_t type, width, scale;
+};
+
+struct ChunkRef {
+    uint64_t off, len;
+    ChunkHeader hdr;
+};
+
+struct RowGroupMeta {
+    uint32_t nrows;
+    uint64_t first_row;            // relative to the file's first row
+    std::vector<ChunkRef> chunks;  // one per column
+};
+
+struct FileMeta {
+    uint64_t nrows = 0, row_offset = 0;
+    uint32_t rowgroup_size = kRowGroupSize;
+    std::vector<ColumnMeta> cols;
+    std::vector<RowGroupMeta> rgs;
+};
+
+// Parse and validate; returns empty string on success, else the reason.
+inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
+    auto rd = [&](uint64_t off, void *dst, size_t n) -> bool {
+        if (off > len || n > len - off) return false;
+        memcpy(dst, img + off, n);
+        return true;
+    };
+    if (len < 16 + 16 || memcmp(img, kFileMagic, 8) != 0) return "bad file magic";
+    if (memcmp(img + len - 4, kTailMagic, 4) != 0) return "bad tail magic";
+    uint64_t foff;
+    uint32_t flen;
+    rd(len - 16, &foff, 8);
+    rd(len - 8, &flen, 4);
+    if (foff > len - 16 || flen > len - 16 - foff || flen < kFooterFixed) return "bad footer offset";
+    uint64_t p = foff;
+    const uint64_t fend = foff + flen;
+    uint32_t ver, ncols, nrg, rgsz;
+    rd(p, &ver, 4);
+    rd(p + 4, &ncols, 4);
+    rd(p + 8, &m.nrows, 8);
+    rd(p + 16, &nrg, 4);
+    rd(p + 20, &rgsz, 4);
+    rd(p + 24, &m.row_offset, 8);
+    if (ver != kFooterVersion) return "unsupported footer version";
+    if (rgsz != kRowGroupSize) return "unsupported row-group size";
+    if (ncols == 0 || ncols > 4096) return "bad column count";
+    m.rowgroup_size = rgsz;
+    p += kFooterFixed;
+    m.cols.resize(ncols);
+    for (auto &c : m.cols) {
+        uint8_t d[4];
+        uint16_t nl;
+        if (p + 6 > fend || !rd(p, d, 4) || !rd(p + 4, &nl, 2) || p + 6 + nl > fend) return "truncated column descriptor";
+        c.type = d[0];
+        c.width = d[1];
+        c.scale = d[2];
+        if (!type_valid(c.type)) return "unsupported column type";
+        c.name.assign((const char *)img + p + 6, nl);
+        p += 6 + nl;
+    }
+    m.rgs.resize(nrg);
+    uint64_t rows = 0;
+    for (uint32_t r = 0; r < nrg; ++r) {
+        auto &rg = m.rgs[r];
+        if (p + 4 + 16ull * ncols > fend) return "truncated row-group descriptor";
+        rd(p, &rg.nrows, 4);
+        if (rg.nrows == 0 || rg.nrows > kRowGroupSize) return "bad row-group row count";
+        if (r + 1 < nrg && rg.nrows != kRowGroupSize) return "short row group before the last";
+        rg.first_row = rows;
+        rows += rg.nrows;
+        rg.chunks.resize(ncols);
+        for (uint32_t c = 0; c < ncols; ++c) {
+            auto &ch = rg.chunks[c];
+            rd(p + 4 + 16ull * c, &ch.off, 8);
+            rd(p + 12 + 16ull * c, &ch.len, 8);
+            if (ch.off > foff || ch.len > foff - ch.off || ch.len < sizeof(ChunkHeader) || ch.off % 16)
+                return "chunk out of bounds";
+            memcpy(&ch.hdr, img + ch.off, sizeof(ChunkHeader));
+            const ChunkHeader &h = ch.hdr;
+            if (h.magic != kChunkMagic) return "bad chunk magic";
+            if (h.nvals != rg.nrows || h.nvec != (rg.nrows + kVectorSize - 1) / kVectorSize) return "chunk row count mismatch";
+            if (h.T != 8 && h.T != 16 && h.T != 32 && h.T != 64) return "bad packing width";
+            if (h.enc < ENC_FFOR || h.enc > ENC_RLE) return "bad encoding";
+            const uint8_t ty = m.cols[c].type;
+            const bool is_str = ty == TY_VARCHAR;
+            if ((bool)h.is_str != is_str) return "chunk/column type mismatch";
+            if (is_str ? h.enc != ENC_DICT : h.vbits != type_value_bits(ty)) return "chunk/column type mismatch";
+            if ((h.enc == ENC_FFOR || h.enc == ENC_DELTA) && h.T != h.vbits) return "bad packing width";
+            if (h.enc == ENC_DICT && h.T != 32) return "bad dictionary code width";
+            if (h.enc == ENC_RLE && h.T != 16) return "bad run-index width";
+            if (h.meta_off + 32ull * h.nvec > ch.len || h.packed_off > ch.len || h.aux_off > ch.len ||
+                h.aux_len > ch.len - h.aux_off || h.packed_off % 16 || h.meta_off % 16 || h.aux_off % 16)
+                return "chunk layout out of bounds";
+            // per-vector validation: packed extents, widths, aux extents
+            for (uint32_t v = 0; v < h.nvec; ++v) {
+                VecMeta vm;
+                memcpy(&vm, img + ch.off + h.meta_off + 32ull * v, 32);
+                if (vm.bw > h.T || vm.nvals == 0 || vm.nvals > kVectorSize) return "bad vector meta";
+                if (v + 1 < h.nvec && vm.nvals != kVectorSize) return "short vector before the last";
+                if (vm.packed_off % 16 || h.packed_off + vm.packed_off + 128ull * vm.bw > h.aux_off) return "packed vector out of bounds";
+                if (h.enc == ENC_DELTA && (vm.aux_off % 16 || vm.aux_off + 128 > h.aux_len)) return "delta bases out of bounds";
+                if (h.enc == ENC_RLE) {
+                    if (vm.aux_off % 16 || vm.aux_count == 0 || vm.aux_count > kVectorSize ||
+                        vm.aux_off + 128 + (uint64_t)vm.aux_count * (h.vbits / 8) > h.aux_len)
+                        return "run values out of bounds";
+                }
+            }
+            if (h.enc == ENC_DICT) {
+                if (h.dict_count == 0) return "empty dictionary";
+                if (is_str) {
+                    uint64_t need = 4ull * (h.dict_count + 1);
+                    if (need > h.aux_len) return "dictionary out of bounds";
+                    uint32_t last;
+                    memcpy(&last, img + ch.off + h.aux_off + 4ull * h.dict_count, 4);
+                    if (need + last > h.aux_len) return "dictionary out of bounds";
+                } else if ((uint64_t)h.dict_count * (h.vbits / 8) > h.aux_len) {
+                    return "dictionary out of bounds";
+                }
+            }
+        }
+        p += 4 + 16ull * ncols;
+    }
+    if (rows != m.nrows) return "row count mismatch";
+    return "";
+}
+
+}  // namespace fls

@@ -1,0 +1,748 @@
+// fls_writer.cpp -- CPU FastLanes encoder + file assembler + seeded workloads.
+//
+// Encodes row groups of 65,536 rows (src/writer/write_fastlane_stream.cpp:21-24)
+// into 1024-value vectors with the FastLanes codecs the decode path supports:
+// FFOR, unified-transposed DELTA, DICT (int and string) and FastLanes-RLE.
+// This is the write path the reference only stubs
+// (src/writer/write_fastlane.cpp:227, src/include/fastlanes_facade.hpp:39-43)
+// and the producer of every benchmark / test input (fls_gen.hpp).
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/flsgpu.h"
+#include "../../include/flswriter.h"
+#include "fls_common.hpp"
+#include "fls_format.hpp"
+#include "fls_gen.hpp"
+
+namespace fls {
+
+std::string &last_error() {
+    static thread_local std::string e;
+    return e;
+}
+
+namespace {
+
+constexpr uint8_t kFLOrder[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+
+inline uint64_t tmask(int T) { return T >= 64 ? ~0ull : ((1ull << T) - 1ull); }
+inline int bitlen(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+inline int64_t sext(uint64_t v, int T) {
+    if (T >= 64) return (int64_t)v;
+    const uint64_t sign = 1ull << (T - 1);
+    v &= tmask(T);
+    return (int64_t)((v ^ sign) - sign);
+}
+// transposed position p -> original tuple index
+inline uint32_t tau(uint32_t p) { return 128u * kFLOrder[(p >> 4) & 7] + 16u * (p >> 7) + (p & 15); }
+
+struct TauTable {
+    uint16_t t[1024];
+    TauTable() { for (uint32_t p = 0; p < 1024; ++p) t[p] = (uint16_t)tau(p); }
+};
+const TauTable &tau_table() { static TauTable tt; return tt; }
+
+void put_word(uint8_t *dst, int T, uint64_t idx, uint64_t v) {
+    switch (T) {
+    case 8: dst[idx] = (uint8_t)v; break;
+    case 16: { uint16_t x = (uint16_t)v; memcpy(dst + 2 * idx, &x, 2); } break;
+    case 32: { uint32_t x = (uint32_t)v; memcpy(dst + 4 * idx, &x, 4); } break;
+    default: memcpy(dst + 8 * idx, &v, 8); break;
+    }
+}
+
+// Interleaved bit-packing of 1024 values in position order (lane-major
+// accumulation; lane L's k-th word goes to word index k*(1024/T)+L).
+void pack(int T, int W, const uint64_t *vals, uint8_t *dst) {
+    if (W == 0) return;
+    const int lanes = 1024 / T;
+    const uint64_t wm = tmask(W), tm = tmask(T);
+    for (int lane = 0; lane < lanes; ++lane) {
+        unsigned __int128 acc = 0;
+        int nbits = 0, k = 0;
+        for (int row = 0; row < T; ++row) {
+            acc |= (unsigned __int128)(vals[row * lanes + lane] & wm) << nbits;
+            nbits += W;
+            while (nbits >= T) {
+                put_word(dst, T, (uint64_t)k * lanes + lane, (uint64_t)acc & tm);
+                acc >>= T;
+                nbits -= T;
+                ++k;
+            }
+        }
+    }
+}
+
+// FFOR over 1024 unsigned T-bit values (already in position order).
+// Returns bw, sets base; u receives value - base (mod 2^T).
+int ffor_prepare(int T, const uint64_t *v, int64_t &base, uint64_t *u) {
+    int64_t mn = sext(v[0], T);
+    for (int i = 1; i < 1024; ++i) mn = std::min(mn, sext(v[i], T));
+    const uint64_t tm = tmask(T);
+    uint64_t mx = 0;
+    for (int i = 0; i < 1024; ++i) {
+        u[i] = (v[i] - (uint64_t)mn) & tm;
+        mx |= u[i];
+    }
+    base = mn;
+    return bitlen(mx);
+}
+
+struct VecOut {
+    VecMeta meta;
+    std::vector<uint8_t> packed;
+    std::vector<uint8_t> aux;  // per-vector aux (DELTA bases, RLE bases + runs)
+};
+
+void align_to(std::vector<uint8_t> &b, size_t a) {
+    while (b.size() % a) b.push_back(0);
+}
+
+// Assemble one chunk from encoded vectors + chunk-level aux (dictionary).
+std::vector<uint8_t> assemble_chunk(uint8_t enc, uint8_t T, uint8_t vbits, bool is_str,
+                                    uint32_t nvals, std::vector<VecOut> &vecs,
+                                    const std::vector<uint8_t> &chunk_aux, uint32_t dict_count) {
+    ChunkHeader h{};
+    h.magic = kChunkMagic;
+    h.enc = enc;
+    h.T = T;
+    h.vbits = vbits;
+    h.is_str = is_str ? 1 : 0;
+    h.nvec = (uint32_t)vecs.size();
+    h.nvals = nvals;
+    h.meta_off = sizeof(ChunkHeader);
+    size_t packed_total = 0;
+    for (auto &v : vecs) packed_total += v.packed.size();
+    size_t off = h.meta_off + sizeof(VecMeta) * vecs.size();
+    off = (off + 15) & ~size_t(15);
+    h.packed_off = off;
+    off += packed_total;
+    off = (off + 15) & ~size_t(15);
+    h.aux_off = off;
+    // aux: chunk-level dictionary first, then per-vector aux (8-B aligned)
+    std::vector<uint8_t> aux = chunk_aux;
+    align_to(aux, 16);
+    uint64_t poff = 0;
+    for (auto &v : vecs) {
+        v.meta.packed_off = poff;
+        poff += v.packed.size();
+        if (!v.aux.empty()) {
+            align_to(aux, 16);
+            v.meta.aux_off = aux.size();
+            aux.insert(aux.end(), v.aux.begin(), v.aux.end());
+        }
+    }
+    h.aux_len = aux.size();
+    h.dict_count = dict_count;
+    size_t total = h.aux_off + aux.size();
+    total = (total + kChunkAlign - 1) & ~size_t(kChunkAlign - 1);
+    std::vector<uint8_t> out(total, 0);
+    memcpy(out.data(), &h, sizeof(h));
+    for (size_t i = 0; i < vecs.size(); ++i) memcpy(out.data() + h.meta_off + 32 * i, &vecs[i].meta, 32);
+    size_t p = h.packed_off;
+    for (auto &v : vecs) {
+        if (!v.packed.empty()) memcpy(out.data() + p, v.packed.data(), v.packed.size());
+        p += v.packed.size();
+    }
+    if (!aux.empty()) memcpy(out.data() + h.aux_off, aux.data(), aux.size());
+    return out;
+}
+
+// load 1024 values of vector v (padding the tail with the last value)
+void load_vec(const uint64_t *vals, uint32_t n, uint32_t v, uint64_t *out, uint32_t &vn) {
+    const uint32_t b = v * 1024;
+    vn = std::min<uint32_t>(1024, n - b);
+    for (uint32_t i = 0; i < vn; ++i) out[i] = vals[b + i];
+    for (uint32_t i = vn; i < 1024; ++i) out[i] = vals[b + vn - 1];
+}
+
+// ---- integer chunk encoders (vals: n values as unsigned T-bit in uint64) --
+
+std::vector<uint8_t> enc_ffor(int T, const uint64_t *vals, uint32_t n) {
+    const uint32_t nvec = (n + 1023) / 1024;
+    std::vector<VecOut> vecs(nvec);
+    uint64_t v[1024], u[1024];
+    for (uint32_t k = 0; k < nvec; ++k) {
+        uint32_t vn;
+        load_vec(vals, n, k, v, vn);
+        int64_t base;
+        int W = ffor_prepare(T, v, base, u);
+        VecOut &o = vecs[k];
+        o.meta = VecMeta{};
+        o.meta.for_base = base;
+        o.meta.bw = (uint8_t)W;
+        o.meta.nvals = (uint16_t)vn;
+        o.packed.assign((size_t)128 * W, 0);
+        pack(T, W, u, o.packed.data());
+    }
+    return assemble_chunk(ENC_FFOR, (uint8_t)T, (uint8_t)T, false, n, vecs, {}, 0);
+}
+
+// deltas of one vector in the unified transposed layout; bases (128 B) out
+void delta_vector(int T, const uint64_t *v, uint64_t *pos_vals, uint8_t *bases) {
+    const uint64_t tm = tmask(T);
+    uint64_t d[1024];
+    const int nchains = 1024 / T;
+    for (int c = 0; c < nchains; ++c) {
+        const int blk = c / 16, l = c % 16;
+        const uint32_t i0 = (uint32_t)(blk * 16 * T + l);
+        put_word(bases, T, (uint64_t)c, v[i0]);
+        d[i0] = 0;
+        for (int k = 1; k < T; ++k) {
+            const uint32_t i = i0 + 16u * k;
+            d[i] = (v[i] - v[i - 16]) & tm;
+        }
+    }
+    const TauTable &tt = tau_table();
+    for (uint32_t p = 0; p < 1024; ++p) pos_vals[p] = d[tt.t[p]];
+}
+
+std::vector<uint8_t> enc_delta(int T, const uint64_t *vals, uint32_t n) {
+    const uint32_t nvec = (n + 1023) / 1024;
+    std::vector<VecOut> vecs(nvec);
+    uint64_t v[1024], pv[1024], u[1024];
+    for (uint32_t k = 0; k < nvec; ++k) {
+        uint32_t vn;
+        load_vec(vals, n, k, v, vn);
+        VecOut &o = vecs[k];
+        o.aux.assign(128, 0);
+        delta_vector(T, v, pv, o.aux.data());
+        int64_t base;
+        int W = ffor_prepare(T, pv, base, u);
+        o.meta = VecMeta{};
+        o.meta.for_base = base;
+        o.meta.bw = (uint8_t)W;
+        o.meta.nvals = (uint16_t)vn;
+        o.packed.assign((size_t)128 * W, 0);
+        pack(T, W, u, o.packed.data());
+    }
+    return assemble_chunk(ENC_DELTA, (uint8_t)T, (uint8_t)T, false, n, vecs, {}, 0);
+}
+
+// DICT codes (u32, T=32 packing) + chunk dictionary bytes
+std::vector<uint8_t> enc_dict_codes(const uint32_t *codes, uint32_t n, uint8_t vbits, bool is_str,
+                                    const std::vector<uint8_t> &dict, uint32_t dict_count) {
+    const uint32_t nvec = (n + 1023) / 1024;
+    std::vector<VecOut> vecs(nvec);
+    uint64_t v[1024], u[1024];
+    for (uint32_t k = 0; k < nvec; ++k) {
+        const uint32_t b = k * 1024, vn = std::min<uint32_t>(1024, n - b);
+        for (uint32_t i = 0; i < 1024; ++i) v[i] = codes[b + std::min(i, vn - 1)];
+        int64_t base;
+        int W = ffor_prepare(32, v, base, u);
+        VecOut &o = vecs[k];
+        o.meta = VecMeta{};
+        o.meta.for_base = base;
+        o.meta.bw = (uint8_t)W;
+        o.meta.nvals = (uint16_t)vn;
+        o.packed.assign((size_t)128 * W, 0);
+        pack(32, W, u, o.packed.data());
+    }
+    return assemble_chunk(ENC_DICT, 32, vbits, is_str, n, vecs, dict, dict_count);
+}
+
+std::vector<uint8_t> enc_dict_int(int T, const uint64_t *vals, uint32_t n) {
+    std::vector<uint64_t> uniq(vals, vals + n);
+    std::sort(uniq.begin(), uniq.end(), [T](uint64_t a, uint64_t b) { return sext(a, T) < sext(b, T); });
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    std::vector<uint32_t> codes(n);
+    std::unordered_map<uint64_t, uint32_t> idx;
+    idx.reserve(uniq.size() * 2);
+    for (uint32_t i = 0; i < uniq.size(); ++i) idx[uniq[i]] = i;
+    for (uint32_t i = 0; i < n; ++i) codes[i] = idx[vals[i]];
+    std::vector<uint8_t> dict((size_t)uniq.size() * (T / 8));
+    for (size_t i = 0; i < uniq.size(); ++i) put_word(dict.data(), T, i, uniq[i]);
+    return enc_dict_codes(codes.data(), n, (uint8_t)T, false, dict, (uint32_t)uniq.size());
+}
+
+std::vector<uint8_t> str_dict_bytes(const std::vector<std::string_view> &entries) {
+    std::vector<uint8_t> d(4 * (entries.size() + 1));
+    uint32_t off = 0;
+    for (size_t i = 0; i < entries.size(); ++i) {
+        memcpy(d.data() + 4 * i, &off, 4);
+        off += (uint32_t)entries[i].size();
+    }
+    memcpy(d.data() + 4 * entries.size(), &off, 4);
+    for (auto &e : entries) d.insert(d.end(), e.begin(), e.end());
+    return d;
+}
+
+std::vector<uint8_t> enc_dict_str(const uint32_t *offs, const char *bytes, uint32_t n) {
+    std::unordered_map<std::string_view, uint32_t> idx;
+    std::vector<std::string_view> entries;
+    std::vector<uint32_t> codes(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        std::string_view s(bytes + offs[i], offs[i + 1] - offs[i]);
+        auto it = idx.find(s);
+        if (it == idx.end()) {
+            it = idx.emplace(s, (uint32_t)entries.size()).first;
+            entries.push_back(s);
+        }
+        codes[i] = it->second;
+    }
+    return enc_dict_codes(codes.data(), n, 0, true, str_dict_bytes(entries), (uint32_t)entries.size());
+}
+
+// FastLanes-RLE: per vector run values + run-index vector (u16) DELTA-coded
+std::vector<uint8_t> enc_rle(int T, const uint64_t *vals, uint32_t n) {
+    const uint32_t nvec = (n + 1023) / 1024;
+    std::vector<VecOut> vecs(nvec);
+    uint64_t v[1024], idx[1024], pv[1024], u[1024];
+    for (uint32_t k = 0; k < nvec; ++k) {
+        uint32_t vn;
+        load_vec(vals, n, k, v, vn);
+        std::vector<uint64_t> runs;
+        for (int i = 0; i < 1024; ++i) {
+            if (i == 0 || v[i] != v[i - 1]) runs.push_back(v[i]);
+            idx[i] = runs.size() - 1;
+        }
+        VecOut &o = vecs[k];
+        o.aux.assign(128 + runs.size() * (T / 8), 0);
+        delta_vector(16, idx, pv, o.aux.data());
+        for (size_t r = 0; r < runs.size(); ++r) put_word(o.aux.data() + 128, T, r, runs[r]);
+        int64_t base;
+        int W = ffor_prepare(16, pv, base, u);
+        o.meta = VecMeta{};
+        o.meta.for_base = base;
+        o.meta.bw = (uint8_t)W;
+        o.meta.nvals = (uint16_t)vn;
+        o.meta.aux_count = (uint32_t)runs.size();
+        o.packed.assign((size_t)128 * W, 0);
+        pack(16, W, u, o.packed.data());
+    }
+    return assemble_chunk(ENC_RLE, 16, (uint8_t)T, false, n, vecs, {}, 0);
+}
+
+// estimated encoded bytes for ENC_AUTO
+size_t est_ffor(int T, const uint64_t *vals, uint32_t n) {
+    size_t b = 0;
+    uint64_t v[1024], u[1024];
+    for (uint32_t k = 0; k < (n + 1023) / 1024; ++k) {
+        uint32_t vn;
+        load_vec(vals, n, k, v, vn);
+        int64_t base;
+        b += 128 * (size_t)ffor_prepare(T, v, base, u) + 32;
+    }
+    return b;
+}
+size_t est_delta(int T, const uint64_t *vals, uint32_t n) {
+    size_t b = 0;
+    uint64_t v[1024], pv[1024], u[1024];
+    uint8_t bases[128];
+    for (uint32_t k = 0; k < (n + 1023) / 1024; ++k) {
+        uint32_t vn;
+        load_vec(vals, n, k, v, vn);
+        delta_vector(T, v, pv, bases);
+        int64_t base;
+        b += 128 * (size_t)ffor_prepare(T, pv, base, u) + 32 + 128;
+    }
+    return b;
+}
+size_t est_rle(int T, const uint64_t *vals, uint32_t n) {
+    size_t runs = 1;
+    for (uint32_t i = 1; i < n; ++i) runs += vals[i] != vals[i - 1];
+    if (runs * 4 > n) return SIZE_MAX;  // not worth it
+    // idx deltas over stride 16 are <= 16 -> at most 5 bits
+    return runs * (T / 8) + ((n + 1023) / 1024) * (32 + 128 + 128 * 5);
+}
+size_t est_dict(int T, const uint64_t *vals, uint32_t n) {
+    std::vector<uint64_t> s(vals, vals + n);
+    std::sort(s.begin(), s.end());
+    size_t d = std::unique(s.begin(), s.end()) - s.begin();
+    if (d > 65536) return SIZE_MAX;
+    return d * (T / 8) + ((n + 1023) / 1024) * (32 + 128 * (size_t)bitlen(d - 1 ? d - 1 : 0));
+}
+
+struct ColSpec {
+    std::string name;
+    uint8_t type, width, scale, enc;
+};
+
+}  // namespace
+
+// Encode one integer chunk with a chosen (or automatic) encoding.
+std::vector<uint8_t> encode_int_chunk(uint8_t type, uint8_t enc, const uint64_t *vals, uint32_t n) {
+    const int T = type_value_bits(type);
+    if (enc == ENC_AUTO) {
+        size_t best = est_ffor(T, vals, n);
+        enc = ENC_FFOR;
+        size_t d = est_delta(T, vals, n);
+        if (d < best) { best = d; enc = ENC_DELTA; }
+        size_t r = est_rle(T, vals, n);
+        if (r < best) { best = r; enc = ENC_RLE; }
+        size_t x = est_dict(T, vals, n);
+        if (x < best) { best = x; enc = ENC_DICT; }
+    }
+    switch (enc) {
+    case ENC_DELTA: return enc_delta(T, vals, n);
+    case ENC_DICT: return enc_dict_int(T, vals, n);
+    case ENC_RLE: return enc_rle(T, vals, n);
+    default: return enc_ffor(T, vals, n);
+    }
+}
+
+// ---- file assembly -------------------------------------------------------
+
+struct FileBuilder {
+    std::vector<ColSpec> cols;
+    uint64_t row_offset = 0;
+    struct RG {
+        uint32_t nrows;
+        std::vector<std::vector<uint8_t>> chunks;
+    };
+    std::vector<RG> rgs;
+
+    std::vector<uint8_t> footer(const std::vector<uint64_t> &chunk_offs) const {
+        std::vector<uint8_t> f;
+        auto put = [&f](const void *p, size_t n) { f.insert(f.end(), (const uint8_t *)p, (const uint8_t *)p + n); };
+        uint32_t ver = kFooterVersion, ncols = (uint32_t)cols.size(), nrg = (uint32_t)rgs.size(), rgsz = kRowGroupSize;
+        uint64_t nrows = 0;
+        for (auto &r : rgs) nrows += r.nrows;
+        put(&ver, 4); put(&ncols, 4); put(&nrows, 8); put(&nrg, 4); put(&rgsz, 4); put(&row_offset, 8);
+        for (auto &c : cols) {
+            uint8_t d[4] = {c.type, c.width, c.scale, 0};
+            put(d, 4);
+            uint16_t nl = (uint16_t)c.name.size();
+            put(&nl, 2);
+            put(c.name.data(), nl);
+        }
+        size_t k = 0;
+        for (auto &r : rgs) {
+            put(&r.nrows, 4);
+            for (size_t c = 0; c < cols.size(); ++c, ++k) {
+                uint64_t off = chunk_offs[k], len = r.chunks[c].size();
+                put(&off, 8);
+                put(&len, 8);
+            }
+        }
+        return f;
+    }
+
+    // Assemble into one malloc'ed image; chunk buffers are released as copied.
+    int finish(uint8_t **img, uint64_t *len, int nthreads) {
+        std::vector<uint64_t> offs;
+        uint64_t off = 256;  // 8 B magic + 8 B version, padded to the chunk alignment
+        for (auto &r : rgs)
+            for (auto &c : r.chunks) { offs.push_back(off); off += c.size(); }
+        std::vector<uint8_t> ft = footer(offs);
+        const uint64_t foot_off = off;
+        const uint64_t total = off + ft.size() + 16;
+        uint8_t *buf = (uint8_t *)malloc(total);
+        if (!buf) return fail(FLS_ERR_NOMEM, "out of host memory assembling %llu bytes", (unsigned long long)total);
+        memset(buf, 0, 256);
+        memcpy(buf, kFileMagic, 8);
+        uint64_t version = 1;
+        memcpy(buf + 8, &version, 8);
+        // parallel copy by row group
+        std::atomic<size_t> next{0};
+        std::vector<size_t> rg_first(rgs.size() + 1, 0);
+        for (size_t i = 0; i < rgs.size(); ++i) rg_first[i + 1] = rg_first[i] + rgs[i].chunks.size();
+        auto work = [&]() {
+            for (size_t r; (r = next.fetch_add(1)) < rgs.size();) {
+                for (size_t c = 0; c < rgs[r].chunks.size(); ++c) {
+                    auto &ch = rgs[r].chunks[c];
+                    memcpy(buf + offs[rg_first[r] + c], ch.data(), ch.size());
+                    std::vector<uint8_t>().swap(ch);
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+        memcpy(buf + foot_off, ft.data(), ft.size());
+        uint32_t flen = (uint32_t)ft.size();
+        memcpy(buf + foot_off + ft.size(), &foot_off, 8);
+        memcpy(buf + foot_off + ft.size() + 8, &flen, 4);
+        memcpy(buf + foot_off + ft.size() + 12, kTailMagic, 4);
+        *img = buf;
+        *len = total;
+        return 0;
+    }
+};
+
+// ---- seeded workloads ----------------------------------------------------
+
+namespace {
+
+const char *const kReturnFlag[] = {"A", "N", "R"};
+const char *const kLineStatus[] = {"F", "O"};
+const char *const kShipInstruct[] = {"DELIVER IN PERSON", "COLLECT COD", "NONE", "TAKE BACK RETURN"};
+const char *const kShipMode[] = {"REG AIR", "AIR", "RAIL", "SHIP", "TRUCK", "MAIL", "FOB"};
+
+struct Workload {
+    std::string name;
+    std::vector<ColSpec> cols;
+    uint64_t nrows;
+    gen::LineitemParams li;
+};
+
+uint64_t lineitem_rows(double sf) {
+    // dbgen row counts at the standard scale factors
+    if (sf == 0.01) return 60175;
+    if (sf == 0.1) return 600572;
+    if (sf == 1) return 6001215;
+    if (sf == 10) return 59986052;
+    if (sf == 100) return 600037902;
+    if (sf == 1000) return 5999989709ull;
+    return (uint64_t)(6000000.0 * sf + 0.5);
+}
+
+bool make_workload(const char *wl, double sf, uint64_t nrows, Workload &w) {
+    if (!wl) return false;
+    w.name = wl;
+    w.cols.clear();
+    if (w.name == "c1") {
+        w.cols = {{"value", TY_INT32, 0, 0, ENC_FFOR}};
+        w.nrows = nrows ? nrows : 1000000;
+    } else if (w.name == "c3") {
+        w.cols = {{"key", TY_INT64, 0, 0, ENC_DELTA}};
+        w.nrows = nrows ? nrows : 1000000000ull;
+    } else if (w.name == "c4") {
+        w.cols = {{"mode", TY_VARCHAR, 0, 0, ENC_DICT}};
+        w.nrows = nrows ? nrows : 1000000000ull;
+    } else if (w.name == "lineitem") {
+        if (!(sf > 0)) return false;
+        w.cols = {
+            {"l_orderkey", TY_INT64, 0, 0, ENC_DELTA},   {"l_partkey", TY_INT32, 0, 0, ENC_FFOR},
+            {"l_suppkey", TY_INT32, 0, 0, ENC_FFOR},     {"l_linenumber", TY_INT32, 0, 0, ENC_FFOR},
+            {"l_quantity", TY_DECIMAL, 15, 2, ENC_FFOR}, {"l_extendedprice", TY_DECIMAL, 15, 2, ENC_FFOR},
+            {"l_discount", TY_DECIMAL, 15, 2, ENC_FFOR}, {"l_tax", TY_DECIMAL, 15, 2, ENC_FFOR},
+            {"l_returnflag", TY_VARCHAR, 0, 0, ENC_DICT}, {"l_linestatus", TY_VARCHAR, 0, 0, ENC_DICT},
+            {"l_shipdate", TY_DATE, 0, 0, ENC_FFOR},     {"l_commitdate", TY_DATE, 0, 0, ENC_FFOR},
+            {"l_receiptdate", TY_DATE, 0, 0, ENC_FFOR},  {"l_shipinstruct", TY_VARCHAR, 0, 0, ENC_DICT},
+            {"l_shipmode", TY_VARCHAR, 0, 0, ENC_DICT},
+        };
+        w.nrows = nrows ? nrows : lineitem_rows(sf);
+        w.li.n_part = std::max<int64_t>(1, (int64_t)(200000.0 * sf + 0.5));
+        w.li.n_supp = std::max<int64_t>(4, (int64_t)(10000.0 * sf + 0.5));
+    } else {
+        return false;
+    }
+    w.li.seed = gen::kSeed;
+    w.li.nrows = w.nrows;
+    return true;
+}
+
+// dictionary (string table) of a generated VARCHAR column
+bool gen_dict(const Workload &w, int col, std::vector<std::string_view> &d) {
+    auto fill = [&d](const char *const *t, size_t n) { d.assign(t, t + n); };
+    if (w.name == "c4" && col == 0) { fill(kShipMode, 7); return true; }
+    if (w.name == "lineitem") {
+        switch (col) {
+        case 8: fill(kReturnFlag, 3); return true;
+        case 9: fill(kLineStatus, 2); return true;
+        case 13: fill(kShipInstruct, 4); return true;
+        case 14: fill(kShipMode, 7); return true;
+        }
+    }
+    return false;
+}
+
+// Fill raw values (sign-extended ints / codes) of all columns for rows
+// [row0, row0+n).  out[c] holds n uint64.
+void gen_rows(const Workload &w, uint64_t row0, uint32_t n, std::vector<std::vector<uint64_t>> &out) {
+    out.resize(w.cols.size());
+    for (auto &o : out) o.resize(n);
+    if (w.name == "c1") {
+        for (uint32_t i = 0; i < n; ++i) out[0][i] = (uint64_t)gen::c1_value(w.li.seed, row0 + i);
+    } else if (w.name == "c4") {
+        for (uint32_t i = 0; i < n; ++i) out[0][i] = (uint64_t)gen::c4_code(w.li.seed, row0 + i);
+    } else if (w.name == "c3") {
+        gen::OrderWalker ow;
+        ow.start(w.li.seed, row0);
+        for (uint32_t i = 0; i < n; ++i, ow.next()) out[0][i] = (uint64_t)gen::orderkey(ow.cur().order);
+    } else {
+        gen::OrderWalker ow;
+        ow.start(w.li.seed, row0);
+        gen::LineitemRow r;
+        for (uint32_t i = 0; i < n; ++i, ow.next()) {
+            gen::lineitem_row_at(w.li, row0 + i, ow.cur(), r);
+            for (int c = 0; c < gen::kLineitemCols; ++c) out[c][i] = (uint64_t)gen::lineitem_col(r, c);
+        }
+    }
+}
+
+std::vector<uint8_t> encode_gen_chunk(const Workload &w, int c, const std::vector<uint64_t> &vals) {
+    const ColSpec &cs = w.cols[c];
+    const uint32_t n = (uint32_t)vals.size();
+    if (cs.type == TY_VARCHAR) {
+        std::vector<std::string_view> d;
+        gen_dict(w, c, d);
+        std::vector<uint32_t> codes(vals.begin(), vals.end());
+        return enc_dict_codes(codes.data(), n, 0, true, str_dict_bytes(d), (uint32_t)d.size());
+    }
+    const int T = type_value_bits(cs.type);
+    std::vector<uint64_t> tv(vals);
+    for (auto &x : tv) x &= tmask(T);
+    return encode_int_chunk(cs.type, cs.enc, tv.data(), n);
+}
+
+}  // namespace
+}  // namespace fls
+
+using namespace fls;
+
+// ---- C-ABI ----------------------------------------------------------------
+
+struct fls_writer {
+    FileBuilder fb;
+};
+
+extern "C" {
+
+fls_writer *fls_writer_new(uint64_t row_offset) {
+    auto *w = new fls_writer();
+    w->fb.row_offset = row_offset;
+    return w;
+}
+
+void fls_writer_free(fls_writer *w) { delete w; }
+
+int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t width, uint8_t scale,
+                          uint8_t encoding) {
+    if (!w || !name) return fail(FLS_ERR_ARG, "fls_writer_add_column: NULL argument");
+    if (!type_valid(type)) return fail(FLS_ERR_ARG, "fls_writer_add_column: unsupported type %u", type);
+    if (encoding > ENC_RLE) return fail(FLS_ERR_ARG, "fls_writer_add_column: bad encoding %u", encoding);
+    if (type == TY_VARCHAR && encoding != ENC_AUTO && encoding != ENC_DICT)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: VARCHAR supports DICT only");
+    if (!w->fb.rgs.empty()) return fail(FLS_ERR_STATE, "fls_writer_add_column: after first row group");
+    if (strlen(name) > 65535) return fail(FLS_ERR_ARG, "column name too long");
+    w->fb.cols.push_back(ColSpec{name, type, width, scale, encoding});
+    return 0;
+}
+
+int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *data,
+                            const uint32_t *const *str_offsets) {
+    if (!w || !data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroup: NULL argument");
+    if (nrows == 0 || nrows > kRowGroupSize) return fail(FLS_ERR_ARG, "row group needs 1..65536 rows, got %u", nrows);
+    if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
+    FileBuilder::RG rg;
+    rg.nrows = nrows;
+    for (size_t c = 0; c < w->fb.cols.size(); ++c) {
+        const ColSpec &cs = w->fb.cols[c];
+        if (!data[c]) return fail(FLS_ERR_ARG, "column %zu: NULL data", c);
+        if (cs.type == TY_VARCHAR) {
+            if (!str_offsets || !str_offsets[c]) return fail(FLS_ERR_ARG, "column %zu: VARCHAR needs offsets", c);
+            const uint32_t *o = str_offsets[c];
+            for (uint32_t i = 0; i < nrows; ++i)
+                if (o[i + 1] < o[i]) return fail(FLS_ERR_ARG, "column %zu: offsets not monotone", c);
+            rg.chunks.push_back(enc_dict_str(o, (const char *)data[c], nrows));
+        } else {
+            const int T = type_value_bits(cs.type);
+            std::vector<uint64_t> v(nrows);
+            const uint8_t *p = (const uint8_t *)data[c];
+            for (uint32_t i = 0; i < nrows; ++i) {
+                uint64_t x = 0;
+                memcpy(&x, p + (size_t)i * (T / 8), T / 8);
+                v[i] = x;
+            }
+            rg.chunks.push_back(encode_int_chunk(cs.type, cs.enc, v.data(), nrows));
+        }
+    }
+    w->fb.rgs.push_back(std::move(rg));
+    return 0;
+}
+
+int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
+    if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
+    if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
+    return w->fb.finish(img, len, 1);
+}
+
+int fls_writer_finish_file(fls_writer *w, const char *path) {
+    uint8_t *img = nullptr;
+    uint64_t len = 0;
+    int rc = fls_writer_finish_image(w, &img, &len);
+    if (rc) return rc;
+    FILE *f = fopen(path, "wb");
+    if (!f) { free(img); return fail(FLS_ERR_IO, "cannot create %s", path); }
+    size_t wr = fwrite(img, 1, len, f);
+    fclose(f);
+    free(img);
+    if (wr != len) return fail(FLS_ERR_IO, "short write to %s", path);
+    return 0;
+}
+
+void fls_image_free(uint8_t *img) { free(img); }
+
+int64_t fls_gen_nrows(const char *workload, double scale, uint64_t nrows) {
+    Workload w;
+    if (!make_workload(workload, scale, nrows, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
+    return (int64_t)w.nrows;
+}
+
+int fls_gen_ncols(const char *workload) {
+    Workload w;
+    if (!make_workload(workload, 1.0, 0, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
+    return (int)w.cols.size();
+}
+
+int fls_gen_image(const char *workload, double scale, uint64_t nrows, uint32_t rg_begin, uint32_t rg_end,
+                  int nthreads, uint8_t **img, uint64_t *len) {
+    Workload w;
+    if (!make_workload(workload, scale, nrows, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
+    const uint64_t nrg_total = (w.nrows + kRowGroupSize - 1) / kRowGroupSize;
+    if (rg_end > nrg_total) rg_end = (uint32_t)nrg_total;
+    if (rg_begin > rg_end || !img || !len) return fail(FLS_ERR_ARG, "bad row-group range [%u,%u)", rg_begin, rg_end);
+    if (nthreads < 1) nthreads = 1;
+    FileBuilder fb;
+    fb.cols = w.cols;
+    fb.row_offset = (uint64_t)rg_begin * kRowGroupSize;
+    fb.rgs.resize(rg_end - rg_begin);
+    std::atomic<uint32_t> next{rg_begin};
+    auto work = [&]() {
+        std::vector<std::vector<uint64_t>> vals;
+        for (uint32_t rg; (rg = next.fetch_add(1)) < rg_end;) {
+            const uint64_t r0 = (uint64_t)rg * kRowGroupSize;
+            const uint32_t n = (uint32_t)std::min<uint64_t>(kRowGroupSize, w.nrows - r0);
+            gen_rows(w, r0, n, vals);
+            auto &out = fb.rgs[rg - rg_begin];
+            out.nrows = n;
+            out.chunks.resize(w.cols.size());
+            for (size_t c = 0; c < w.cols.size(); ++c) out.chunks[c] = encode_gen_chunk(w, (int)c, vals[c]);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    return fb.finish(img, len, nthreads);
+}
+
+int fls_gen_values(const char *workload, double scale, uint64_t nrows, int col, uint64_t row_begin, uint64_t n,
+                   void *out) {
+    Workload w;
+    if (!make_workload(workload, scale, nrows, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
+    if (col < 0 || col >= (int)w.cols.size() || !out) return fail(FLS_ERR_ARG, "bad column %d", col);
+    if (row_begin + n > w.nrows) return fail(FLS_ERR_ARG, "rows out of range");
+    const int vb = w.cols[col].type == TY_VARCHAR ? 4 : type_value_bits(w.cols[col].type) / 8;
+    std::vector<std::vector<uint64_t>> vals;
+    uint8_t *o = (uint8_t *)out;
+    for (uint64_t r = 0; r < n;) {
+        const uint32_t k = (uint32_t)std::min<uint64_t>(65536, n - r);
+        gen_rows(w, row_begin + r, k, vals);
+        for (uint32_t i = 0; i < k; ++i) memcpy(o + (r + i) * vb, &vals[col][i], vb);
+        r += k;
+    }
+    return 0;
+}
+
+const char *fls_gen_dict_string(const char *workload, int col, uint32_t code) {
+    Workload w;
+    if (!make_workload(workload, 1.0, 0, w)) return nullptr;
+    static thread_local std::vector<std::string_view> d;
+    if (!gen_dict(w, col, d) || code >= d.size()) return nullptr;
+    return d[code].data();  // entries are NUL-terminated literals
+}
+
+}  // extern "C"

@@ -1,0 +1,726 @@
+// flsgpu.hip -- host engine behind include/flsgpu.h.
+//
+// Replaces FastLanes' connect/read_fls/get_rowgroup_reader/materialize
+// (reference src/fastlanes_facade.cpp:33-56) with:
+//   * footer parse on the host (fls_reader.hpp) -- no GPU needed for schema;
+//   * device-resident mode: a shard of row groups is uploaded verbatim to HBM
+//     and decoded by ONE fused kernel launch per pass (bench / roofline);
+//   * streaming scan: row groups sharded contiguously over the connection's
+//     GPUs (no collectives: row groups are independent); per
+//     GPU a two-slot pipeline H2D(compressed batch) -> decode -> D2H(pinned)
+//     runs ahead of the consumer (DuckDB's scan thread).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/flsgpu.h"
+#include "fls_common.hpp"
+#include "fls_decode.hpp"
+#include "fls_format.hpp"
+#include "fls_reader.hpp"
+
+using namespace fls;
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(FLS_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                 \
+    } while (0)
+
+namespace {
+
+// DuckDB v1.3.2 string_t (16 B): len <= 12 inlined, else 4-byte prefix + pointer
+struct StrT {
+    uint32_t len;
+    char data[12];
+};
+static_assert(sizeof(StrT) == 16, "string_t is 16 B");
+
+StrT make_string_t(const char *p, uint32_t n) {
+    StrT s;
+    memset(&s, 0, sizeof(s));
+    s.len = n;
+    if (n <= 12) {
+        memcpy(s.data, p, n);
+    } else {
+        memcpy(s.data, p, 4);
+        memcpy(s.data + 4, &p, sizeof(p));
+    }
+    return s;
+}
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    int dev = -1;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n), dev(o.dev) { o.p = nullptr; o.n = 0; }
+    void release() {
+        if (p) {
+            int cur;
+            hipGetDevice(&cur);
+            hipSetDevice(dev);
+            hipFree(p);
+            hipSetDevice(cur);
+        }
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(int d, size_t count) {
+        if (count <= n && p && d == dev) return hipSuccess;
+        release();
+        dev = d;
+        n = count;
+        return hipMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)));
+    }
+    ~DevBuf() { release(); }
+};
+
+template <typename T>
+struct PinBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    PinBuf() = default;
+    PinBuf(const PinBuf &) = delete;
+    PinBuf &operator=(const PinBuf &) = delete;
+    PinBuf(PinBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    void release() {
+        if (p) hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        release();
+        n = count;
+        return hipHostMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)), hipHostMallocDefault);
+    }
+    ~PinBuf() { release(); }
+};
+
+}  // namespace
+
+struct fls_connection {
+    std::vector<int> devices;
+};
+
+namespace {
+
+// Per-chunk algorithmic byte accounting (roofline numerator).
+struct ByteCount {
+    uint64_t values = 0, packed = 0, meta = 0, out = 0;
+};
+
+// Byte range of the file covering row groups [rg0, rg1).
+void rg_byte_range(const FileMeta &m, uint32_t rg0, uint32_t rg1, uint64_t &lo, uint64_t &hi) {
+    lo = UINT64_MAX;
+    hi = 0;
+    for (uint32_t r = rg0; r < rg1; ++r)
+        for (auto &c : m.rgs[r].chunks) {
+            lo = std::min(lo, c.off);
+            hi = std::max(hi, c.off + c.len);
+        }
+    lo &= ~uint64_t(255);
+}
+
+// A shard of row groups uploaded to one GPU, with its VARCHAR string_t tables.
+struct DeviceShard {
+    int dev = -1;
+    uint32_t rg0 = 0, rg1 = 0;
+    uint64_t base = 0;                 // file offset of d_img[0]
+    DevBuf<uint8_t> img;               // compressed bytes of [rg0, rg1)
+    DevBuf<StrT> strtab;               // string_t tables of VARCHAR chunks
+    std::vector<uint64_t> strtab_off;  // per (rg - rg0) * ncols + col: index into strtab
+    DevBuf<uint32_t> err;
+};
+
+struct Slot {                       // one batch of row groups in flight
+    uint32_t rg0 = 0, nrg = 0;      // absolute row groups
+    bool busy = false;
+    std::vector<DevBuf<uint8_t>> d_out;   // per column
+    std::vector<PinBuf<uint8_t>> h_out;   // per column (pinned)
+    PinBuf<DevChunk> h_chunks;
+    DevBuf<DevChunk> d_chunks;
+    DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch
+    uint64_t in_base = 0;
+    hipEvent_t done = nullptr;
+};
+
+struct ScanDev {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    uint32_t rg0 = 0, rg1 = 0;      // row groups this GPU owns within the scan
+    uint32_t next_batch_rg = 0;     // next row group to enqueue
+    Slot slots[2];
+    DevBuf<StrT> strtab;
+    std::vector<uint64_t> strtab_off;
+    DevBuf<uint32_t> err;
+    int grid = 0;
+};
+
+struct ScanCtx {
+    bool active = false;
+    std::vector<uint8_t> mask;
+    uint32_t rg0 = 0, rg1 = 0, cur = 0;
+    uint32_t batch = 8;
+    std::vector<ScanDev> devs;
+    int release_dev = -1, release_slot = -1;   // slot to refill at the next call
+    std::vector<const void *> col_ptrs;
+};
+
+}  // namespace
+
+struct fls_table {
+    fls_connection *conn = nullptr;
+    std::vector<uint8_t> owned;
+    const uint8_t *img = nullptr;
+    uint64_t len = 0;
+    FileMeta meta;
+    std::vector<std::string> names;
+    bool registered = false;        // img pinned with hipHostRegister
+
+    // device-resident mode
+    DeviceShard shard;
+    std::vector<DevBuf<uint8_t>> d_out;  // per column, rows of [rg0, rg1)
+    DevBuf<DevChunk> d_chunks;
+    std::vector<DevChunk> h_chunks;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
+    uint32_t ev_used = 0;
+    int grid = 0;
+    uint64_t res_rows = 0, res_first_row = 0;
+    ByteCount last_bytes;
+    uint32_t launches = 0;
+    bool launched = false;
+
+    ScanCtx scan, mat;
+    ~fls_table();
+};
+
+namespace {
+
+int out_bytes_of(const fls_table *t, uint32_t c) { return type_out_bytes(t->meta.cols[c].type); }
+
+// Build host string_t tables for the VARCHAR chunks of [rg0, rg1) and upload.
+int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBuf<StrT> &tab,
+                  std::vector<uint64_t> &offs) {
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    offs.assign((size_t)(rg1 - rg0) * ncols, UINT64_MAX);
+    std::vector<StrT> host;
+    for (uint32_t r = rg0; r < rg1; ++r)
+        for (uint32_t c = 0; c < ncols; ++c) {
+            if (t->meta.cols[c].type != TY_VARCHAR) continue;
+            const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+            const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
+            const uint32_t n = ch.hdr.dict_count;
+            const char *bytes = (const char *)aux + 4ull * (n + 1);
+            offs[(size_t)(r - rg0) * ncols + c] = host.size();
+            for (uint32_t i = 0; i < n; ++i) {
+                uint32_t b0, b1;
+                memcpy(&b0, aux + 4ull * i, 4);
+                memcpy(&b1, aux + 4ull * (i + 1), 4);
+                host.push_back(make_string_t(bytes + b0, b1 - b0));
+            }
+        }
+    HIP_TRY(hipSetDevice(dev));
+    HIP_TRY(tab.alloc(dev, host.size()));
+    if (!host.empty()) HIP_TRY(hipMemcpy(tab.p, host.data(), host.size() * sizeof(StrT), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Describe chunk (rg, col) located at d_chunk_base (device) for the kernel.
+DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint8_t *d_chunk, const uint8_t *d_dict,
+                       uint8_t *d_out, ByteCount *bc) {
+    const ChunkRef &ch = t->meta.rgs[rg].chunks[col];
+    const ChunkHeader &h = ch.hdr;
+    DevChunk d;
+    memset(&d, 0, sizeof(d));
+    d.chunk = d_chunk;
+    d.out = d_out;
+    d.nvec = h.nvec;
+    d.dict_count = h.dict_count;
+    d.meta_off = (uint32_t)h.meta_off;
+    d.packed_off = (uint32_t)h.packed_off;
+    d.aux_off = (uint32_t)h.aux_off;
+    d.enc = h.enc;
+    d.T = h.T;
+    d.vbits = h.vbits;
+    d.ob = (uint8_t)out_bytes_of(t, col);
+    if (h.enc == ENC_DICT) d.dict = h.is_str ? d_dict : d_chunk + h.aux_off;
+    if (bc) {
+        bc->values += h.nvals;
+        bc->out += (uint64_t)h.nvals * d.ob;
+        bc->meta += 32ull * h.nvec;
+        const uint8_t *meta = t->img + ch.off + h.meta_off;
+        for (uint32_t v = 0; v < h.nvec; ++v) {
+            VecMeta vm;
+            memcpy(&vm, meta + 32ull * v, 32);
+            bc->packed += 128ull * vm.bw;
+            if (h.enc == ENC_DELTA) bc->meta += 128;
+            if (h.enc == ENC_RLE) bc->meta += 128 + (uint64_t)vm.aux_count * (h.vbits / 8);
+        }
+        if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? 16 : h.vbits / 8);
+    }
+    return d;
+}
+
+bool col_selected(const std::vector<uint8_t> &mask, uint32_t c) { return mask.empty() || mask[c]; }
+
+}  // namespace
+
+fls_table::~fls_table() {
+    if (stream) hipStreamDestroy(stream);
+    for (auto e : ev_pool) hipEventDestroy(e);
+    if (ev0) hipEventDestroy(ev0);
+    if (ev1) hipEventDestroy(ev1);
+    for (ScanCtx *s : {&scan, &mat})
+        for (auto &d : s->devs) {
+            hipSetDevice(d.dev);
+            if (d.stream) hipStreamSynchronize(d.stream);
+            for (auto &sl : d.slots)
+                if (sl.done) hipEventDestroy(sl.done);
+            if (d.stream) hipStreamDestroy(d.stream);
+        }
+    if (registered) hipHostUnregister((void *)img);
+}
+
+// ------------------------------------------------------------------------------
+// scan pipeline
+
+namespace {
+
+int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, uint32_t rg1) {
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    if (rg1 > t->meta.rgs.size() || rg0 > rg1) return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg0, rg1);
+    // tear down a previous scan on this context
+    for (auto &d : s.devs) {
+        hipSetDevice(d.dev);
+        if (d.stream) hipStreamSynchronize(d.stream);
+        for (auto &sl : d.slots) sl.busy = false;
+    }
+    s.mask.assign(ncols, 1);
+    if (col_mask)
+        for (uint32_t c = 0; c < ncols; ++c) s.mask[c] = col_mask[c] ? 1 : 0;
+    s.rg0 = rg0;
+    s.rg1 = rg1;
+    s.cur = rg0;
+    s.release_dev = s.release_slot = -1;
+    s.col_ptrs.assign(ncols, nullptr);
+    const auto &devs = t->conn->devices;
+    const uint32_t G = (uint32_t)devs.size(), nrg = rg1 - rg0;
+    if (s.devs.size() != G) {
+        for (auto &d : s.devs) {
+            hipSetDevice(d.dev);
+            for (auto &sl : d.slots)
+                if (sl.done) hipEventDestroy(sl.done);
+            if (d.stream) hipStreamDestroy(d.stream);
+        }
+        s.devs.clear();
+        s.devs.resize(G);
+    }
+    const char *b = getenv("FLS_SCAN_BATCH");
+    s.batch = b ? (uint32_t)std::max(1, atoi(b)) : 8u;
+    for (uint32_t g = 0; g < G; ++g) {
+        ScanDev &d = s.devs[g];
+        d.dev = devs[g];
+        HIP_TRY(hipSetDevice(d.dev));
+        if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        for (auto &sl : d.slots) {
+            if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+            sl.d_out.resize(ncols);
+            sl.h_out.resize(ncols);
+        }
+        d.rg0 = rg0 + (uint32_t)((uint64_t)nrg * g / G);
+        d.rg1 = rg0 + (uint32_t)((uint64_t)nrg * (g + 1) / G);
+        d.next_batch_rg = d.rg0;
+        if (!d.grid) d.grid = decode_grid_size();
+        int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off);
+        if (rc) return rc;
+        HIP_TRY(d.err.alloc(d.dev, 1));
+        HIP_TRY(hipMemsetAsync(d.err.p, 0, sizeof(uint32_t), d.stream));
+    }
+    s.active = true;
+    return 0;
+}
+
+// enqueue the next batch of device d into slot si
+int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
+    Slot &sl = d.slots[si];
+    if (d.next_batch_rg >= d.rg1) { sl.busy = false; return 0; }
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    sl.rg0 = d.next_batch_rg;
+    sl.nrg = std::min(s.batch, d.rg1 - sl.rg0);
+    d.next_batch_rg += sl.nrg;
+    HIP_TRY(hipSetDevice(d.dev));
+    // 1. H2D of the batch's compressed bytes
+    uint64_t lo, hi;
+    rg_byte_range(t->meta, sl.rg0, sl.rg0 + sl.nrg, lo, hi);
+    HIP_TRY(sl.d_in.alloc(d.dev, hi - lo));
+    sl.in_base = lo;
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, t->img + lo, hi - lo, hipMemcpyHostToDevice, d.stream));
+    // 2. decode into the slot's device columns
+    const uint64_t max_rows = (uint64_t)s.batch * kRowGroupSize;
+    uint32_t nsel = 0;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        if (!col_selected(s.mask, c)) continue;
+        ++nsel;
+        const uint64_t nb = max_rows * out_bytes_of(t, c);
+        HIP_TRY(sl.d_out[c].alloc(d.dev, nb));
+        HIP_TRY(sl.h_out[c].alloc(nb));
+    }
+    HIP_TRY(sl.h_chunks.alloc((size_t)nsel * sl.nrg));
+    HIP_TRY(sl.d_chunks.alloc(d.dev, (size_t)nsel * sl.nrg));
+    size_t k = 0;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        if (!col_selected(s.mask, c)) continue;
+        for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) {
+            const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+            const uint64_t so = d.strtab_off[(size_t)(r - d.rg0) * ncols + c];
+            const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
+            uint8_t *out = sl.d_out[c].p + (uint64_t)(r - sl.rg0) * kRowGroupSize * out_bytes_of(t, c);
+            sl.h_chunks.p[k++] = make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, nullptr);
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(launch_decode(sl.d_chunks.p, (uint32_t)k, d.err.p, d.grid, d.stream));
+    // 3. D2H into pinned host columns
+    const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
+                          t->meta.rgs[sl.rg0].first_row;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        if (!col_selected(s.mask, c)) continue;
+        HIP_TRY(hipMemcpyAsync(sl.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
+                               d.stream));
+    }
+    HIP_TRY(hipEventRecord(sl.done, d.stream));
+    sl.busy = true;
+    return 0;
+}
+
+int scan_start(fls_table *t, ScanCtx &s) {
+    for (auto &d : s.devs)
+        for (int si = 0; si < 2; ++si) {
+            int rc = enqueue_batch(t, s, d, si);
+            if (rc) return rc;
+        }
+    return 0;
+}
+
+int scan_next(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
+    if (!s.active) return fail(FLS_ERR_STATE, "scan not started");
+    // refill the slot the consumer has finished with
+    if (s.release_dev >= 0) {
+        ScanDev &d = s.devs[s.release_dev];
+        int rc = enqueue_batch(t, s, d, s.release_slot);
+        s.release_dev = s.release_slot = -1;
+        if (rc) return rc;
+    }
+    if (s.cur >= s.rg1) return 0;
+    const uint32_t rg = s.cur;
+    int g = -1, si = -1;
+    for (size_t i = 0; i < s.devs.size() && g < 0; ++i)
+        for (int j = 0; j < 2; ++j) {
+            const Slot &sl = s.devs[i].slots[j];
+            if (sl.busy && rg >= sl.rg0 && rg < sl.rg0 + sl.nrg) { g = (int)i; si = j; break; }
+        }
+    if (g < 0) return fail(FLS_ERR_STATE, "internal: row group %u not in flight", rg);
+    ScanDev &d = s.devs[g];
+    Slot &sl = d.slots[si];
+    HIP_TRY(hipSetDevice(d.dev));
+    HIP_TRY(hipEventSynchronize(sl.done));
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    for (uint32_t c = 0; c < ncols; ++c)
+        s.col_ptrs[c] = col_selected(s.mask, c)
+                            ? sl.h_out[c].p + (uint64_t)(rg - sl.rg0) * kRowGroupSize * out_bytes_of(t, c)
+                            : nullptr;
+    out->rowgroup = rg;
+    out->nrows = t->meta.rgs[rg].nrows;
+    out->first_row = t->meta.row_offset + t->meta.rgs[rg].first_row;
+    out->ncols = ncols;
+    out->columns = s.col_ptrs.data();
+    s.cur++;
+    if (rg + 1 == sl.rg0 + sl.nrg) {  // batch fully delivered: refill on next call
+        s.release_dev = g;
+        s.release_slot = si;
+    }
+    return 1;
+}
+
+int ensure_stream(fls_table *t, int dev) {
+    HIP_TRY(hipSetDevice(dev));
+    if (!t->stream) HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    if (!t->ev0) HIP_TRY(hipEventCreate(&t->ev0));
+    if (!t->ev1) HIP_TRY(hipEventCreate(&t->ev1));
+    return 0;
+}
+
+int open_common(fls_connection *conn, fls_table *t, fls_table **out) {
+    std::string why = parse_file(t->img, t->len, t->meta);
+    if (!why.empty()) {
+        delete t;
+        return fail(FLS_ERR_FORMAT, "not a valid FastLanes file: %s", why.c_str());
+    }
+    t->conn = conn;
+    for (auto &c : t->meta.cols) t->names.push_back(c.name);
+    *out = t;
+    if (debug_enabled())
+        fprintf(stderr, "DEBUG: FLS file opened: %zu columns, %llu rows, %zu row groups\n", t->meta.cols.size(),
+                (unsigned long long)t->meta.nrows, t->meta.rgs.size());
+    return 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------
+// C-ABI
+
+extern "C" {
+
+const char *fls_last_error(void) { return last_error().c_str(); }
+
+const char *fls_version(void) { return "fastlanes-mi355x 0.1.0 (gfx950)"; }
+
+int fls_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int fls_connect(const int *devices, int ndevices, fls_connection **out) {
+    if (!out) return fail(FLS_ERR_ARG, "fls_connect: NULL out");
+    auto *c = new fls_connection();
+    if (devices && ndevices > 0) c->devices.assign(devices, devices + ndevices);
+    else c->devices.push_back(0);
+    *out = c;
+    return 0;
+}
+
+void fls_disconnect(fls_connection *conn) { delete conn; }
+
+int fls_read_fls(fls_connection *conn, const char *path, fls_table **out) {
+    if (!conn || !path || !out) return fail(FLS_ERR_ARG, "fls_read_fls: NULL argument");
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(FLS_ERR_IO, "Failed to open FastLanes file: %s", path);
+    auto *t = new fls_table();
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    if (n < 0) { fclose(f); delete t; return fail(FLS_ERR_IO, "Failed to open FastLanes file: %s", path); }
+    t->owned.resize((size_t)n);
+    size_t rd = n ? fread(t->owned.data(), 1, (size_t)n, f) : 0;
+    fclose(f);
+    if (rd != (size_t)n) { delete t; return fail(FLS_ERR_IO, "short read of %s", path); }
+    t->img = t->owned.data();
+    t->len = (uint64_t)n;
+    return open_common(conn, t, out);
+}
+
+int fls_read_fls_image(fls_connection *conn, const void *img, uint64_t len, int copy, fls_table **out) {
+    if (!conn || !img || !out) return fail(FLS_ERR_ARG, "fls_read_fls_image: NULL argument");
+    auto *t = new fls_table();
+    if (copy) {
+        t->owned.assign((const uint8_t *)img, (const uint8_t *)img + len);
+        t->img = t->owned.data();
+    } else {
+        t->img = (const uint8_t *)img;
+    }
+    t->len = len;
+    return open_common(conn, t, out);
+}
+
+void fls_table_close(fls_table *t) { delete t; }
+
+uint32_t fls_table_ncols(const fls_table *t) { return t ? (uint32_t)t->meta.cols.size() : 0; }
+uint64_t fls_table_nrows(const fls_table *t) { return t ? t->meta.nrows : 0; }
+uint64_t fls_table_row_offset(const fls_table *t) { return t ? t->meta.row_offset : 0; }
+uint32_t fls_table_nrowgroups(const fls_table *t) { return t ? (uint32_t)t->meta.rgs.size() : 0; }
+int64_t fls_table_rowgroup_rows(const fls_table *t, uint32_t rg) {
+    if (!t || rg >= t->meta.rgs.size()) return fail(FLS_ERR_ARG, "row group %u out of range", rg);
+    return t->meta.rgs[rg].nrows;
+}
+
+int fls_table_column(const fls_table *t, uint32_t col, fls_column_info *out) {
+    if (!t || !out || col >= t->meta.cols.size()) return fail(FLS_ERR_ARG, "column %u out of range", col);
+    const ColumnMeta &c = t->meta.cols[col];
+    out->name = t->names[col].c_str();
+    out->type = c.type;
+    out->width = c.width;
+    out->scale = c.scale;
+    out->out_bytes = (uint8_t)type_out_bytes(c.type);
+    return 0;
+}
+
+int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowgroup *out) {
+    if (!t || !out) return fail(FLS_ERR_ARG, "fls_materialize: NULL argument");
+    if (rg >= t->meta.rgs.size()) return fail(FLS_ERR_ARG, "row group %u out of range", rg);
+    // a one-row-group scan on the GPU that owns rg in a full-table sharding
+    const uint32_t G = (uint32_t)t->conn->devices.size(), N = (uint32_t)t->meta.rgs.size();
+    uint32_t g = 0;
+    while (g + 1 < G && rg >= (uint64_t)N * (g + 1) / G) ++g;
+    fls_connection one;
+    one.devices = {t->conn->devices[g]};
+    fls_connection *saved = t->conn;
+    t->conn = &one;
+    int rc = scan_setup(t, t->mat, col_mask, rg, rg + 1);
+    if (!rc) rc = scan_start(t, t->mat);
+    t->conn = saved;
+    if (rc) return rc;
+    rc = scan_next(t, t->mat, out);
+    return rc == 1 ? 0 : (rc == 0 ? fail(FLS_ERR_STATE, "internal: empty materialize") : rc);
+}
+
+int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uint32_t rg_end) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_begin: NULL table");
+    int rc = scan_setup(t, t->scan, col_mask, rg_begin, rg_end);
+    if (rc) return rc;
+    return scan_start(t, t->scan);
+}
+
+int fls_scan_next(fls_table *t, fls_rowgroup *out) {
+    if (!t || !out) return fail(FLS_ERR_ARG, "fls_scan_next: NULL argument");
+    return scan_next(t, t->scan, out);
+}
+
+// ---- device-resident mode -------------------------------------------------
+
+int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_device_upload: NULL table");
+    if (rg_end > t->meta.rgs.size() || rg_begin >= rg_end)
+        return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg_begin, rg_end);
+    const int dev = t->conn->devices[0];
+    int rc = ensure_stream(t, dev);
+    if (rc) return rc;
+    DeviceShard &sh = t->shard;
+    sh.dev = dev;
+    sh.rg0 = rg_begin;
+    sh.rg1 = rg_end;
+    uint64_t lo, hi;
+    rg_byte_range(t->meta, rg_begin, rg_end, lo, hi);
+    sh.base = lo;
+    HIP_TRY(sh.img.alloc(dev, hi - lo));
+    HIP_TRY(hipMemcpy(sh.img.p, t->img + lo, hi - lo, hipMemcpyHostToDevice));
+    rc = build_strtabs(t, dev, rg_begin, rg_end, sh.strtab, sh.strtab_off);
+    if (rc) return rc;
+    HIP_TRY(sh.err.alloc(dev, 1));
+    HIP_TRY(hipMemset(sh.err.p, 0, sizeof(uint32_t)));
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    t->res_first_row = t->meta.rgs[rg_begin].first_row;
+    t->res_rows = t->meta.rgs[rg_end - 1].first_row + t->meta.rgs[rg_end - 1].nrows - t->res_first_row;
+    t->d_out.resize(ncols);
+    for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(t->d_out[c].alloc(dev, t->res_rows * out_bytes_of(t, c)));
+    if (!t->grid) t->grid = decode_grid_size();
+    t->h_chunks.clear();
+    t->launches = 0;
+    t->launched = false;
+    return 0;
+}
+
+int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_device_decode: NULL table");
+    DeviceShard &sh = t->shard;
+    if (sh.dev < 0 || !sh.img.p) return fail(FLS_ERR_STATE, "fls_device_decode before fls_device_upload");
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    std::vector<uint8_t> mask(ncols, 1);
+    if (col_mask)
+        for (uint32_t c = 0; c < ncols; ++c) mask[c] = col_mask[c] ? 1 : 0;
+    // column-major task order: concurrent waves stream one column's row groups
+    std::vector<DevChunk> chunks;
+    ByteCount bc;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        if (!mask[c]) continue;
+        for (uint32_t r = sh.rg0; r < sh.rg1; ++r) {
+            const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+            const uint64_t so = sh.strtab_off[(size_t)(r - sh.rg0) * ncols + c];
+            const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(sh.strtab.p + so);
+            uint8_t *out = t->d_out[c].p + (t->meta.rgs[r].first_row - t->res_first_row) * out_bytes_of(t, c);
+            chunks.push_back(make_devchunk(t, r, c, sh.img.p + (ch.off - sh.base), dict, out, &bc));
+        }
+    }
+    HIP_TRY(hipSetDevice(sh.dev));
+    const bool same = chunks.size() == t->h_chunks.size() &&
+                      !memcmp(chunks.data(), t->h_chunks.data(), chunks.size() * sizeof(DevChunk));
+    if (!same) {
+        HIP_TRY(hipStreamSynchronize(t->stream));
+        HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
+        HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
+        t->h_chunks = chunks;
+    }
+    if (t->ev_used + 2 > t->ev_pool.size()) {
+        for (int i = 0; i < 2; ++i) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            t->ev_pool.push_back(e);
+        }
+    }
+    hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
+    t->ev_used += 2;
+    HIP_TRY(hipEventRecord(e0, t->stream));
+    HIP_TRY(launch_decode(t->d_chunks.p, (uint32_t)chunks.size(), sh.err.p, t->grid, t->stream));
+    HIP_TRY(hipEventRecord(e1, t->stream));
+    t->last_bytes = bc;
+    t->launches++;
+    t->launched = true;
+    return 0;
+}
+
+int fls_device_sync(fls_table *t, fls_decode_stats *stats) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_device_sync: NULL table");
+    if (!t->stream) return fail(FLS_ERR_STATE, "nothing uploaded");
+    HIP_TRY(hipSetDevice(t->shard.dev));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, t->shard.err.p, sizeof(err), hipMemcpyDeviceToHost));
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        double total = 0;
+        float ms = 0;
+        for (uint32_t i = 0; i < t->ev_used; i += 2) {
+            HIP_TRY(hipEventElapsedTime(&ms, t->ev_pool[i], t->ev_pool[i + 1]));
+            total += ms;
+        }
+        stats->kernel_ms = ms;
+        stats->kernel_ms_total = total;
+        stats->timed_launches = t->ev_used / 2;
+        stats->values = t->last_bytes.values;
+        stats->packed_bytes = t->last_bytes.packed;
+        stats->meta_bytes = t->last_bytes.meta;
+        stats->out_bytes = t->last_bytes.out;
+        stats->launches = t->launches;
+    }
+    t->ev_used = 0;
+    if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
+    return 0;
+}
+
+int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbytes) {
+    if (!t || col >= t->d_out.size() || !t->d_out[col].p) return fail(FLS_ERR_ARG, "column %u not resident", col);
+    if (dev_ptr) *dev_ptr = t->d_out[col].p;
+    if (nbytes) *nbytes = t->res_rows * out_bytes_of(t, col);
+    return 0;
+}
+
+int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, void *host_dst) {
+    if (!t || col >= t->d_out.size() || !t->d_out[col].p || !host_dst) return fail(FLS_ERR_ARG, "column %u not resident", col);
+    if (row > t->res_rows || n > t->res_rows - row) return fail(FLS_ERR_ARG, "rows out of range");
+    const int ob = out_bytes_of(t, col);
+    HIP_TRY(hipSetDevice(t->shard.dev));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    HIP_TRY(hipMemcpy(host_dst, t->d_out[col].p + row * ob, n * ob, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+uint64_t fls_device_rows(const fls_table *t) { return t ? t->res_rows : 0; }
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+/*
+ * flsgpu.h -- C-ABI of the MI355X FastLanes decode engine (libflsgpu.so).
+ *
+ * This is the seam the reference's FastLanesFacade::Impl
+ * (src/fastlanes_facade.cpp:12-20) crosses into its decode library.  Each
+ * entry point names the cwida/FastLanes call it replaces:
+ *
+ *   fls_connect            fastlanes::connect()                src/fastlanes_facade.cpp:33
+ *   fls_read_fls           Connection::read_fls(path)          src/fastlanes_facade.cpp:34
+ *   fls_table_nrows/...    Rowgroup::RowCount()/ColCount()     src/fastlanes_facade.cpp:52-56,85
+ *   fls_table_column       Rowgroup::internal_rowgroup[c] type src/fastlanes_facade.cpp:112-183
+ *                          (typed schema: ext_fastlane::FastLanesFacade::
+ *                          getColumnTypes/getColumnNames,
+ *                          src/include/fastlanes_facade.hpp:34-35)
+ *   fls_materialize        TableReader::get_rowgroup_reader(rg)
+ *                          + RowgroupReader::materialize()     src/fastlanes_facade.cpp:41,48
+ *   fls_scan_begin/next    the row-group loop the reference never wrote
+ *                          (it decodes row group 0 only, :41)
+ *   fls_table_close/fls_disconnect  FastLanesFacade::closeFile  src/fastlanes_facade.cpp:202-210
+ *
+ * Conventions: plain pointers and sizes, no exceptions across the ABI; every
+ * function returns 0 (or a count) on success and a negative fls_status on
+ * error, with fls_last_error() holding a message for the calling thread.
+ * Decoded columns are DuckDB physical layouts: int8..int64 little-endian,
+ * DATE int32 days, DECIMAL int64 scaled, VARCHAR duckdb::string_t (16 B:
+ * u32 length + 12 inline bytes, or u32 length + 4-byte prefix + char* into a
+ * pinned host dictionary heap owned by the table).
+ * A table handle is used by one host thread at a time (DuckDB's scan thread,
+ * src/scanner/scan_fastlanes.cpp:43-45); internally there is one HIP stream
+ * set per GPU.
+ */
+#ifndef FLSGPU_H
+#define FLSGPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum fls_status {
+    FLS_OK = 0,
+    FLS_ERR_IO = -1,        /* cannot open / read the file */
+    FLS_ERR_FORMAT = -2,    /* not an .fls file or corrupt footer / chunk */
+    FLS_ERR_ARG = -3,       /* bad argument (index out of range, NULL) */
+    FLS_ERR_DEVICE = -4,    /* HIP runtime error or no usable GPU */
+    FLS_ERR_STATE = -5,     /* call out of order (e.g. decode before upload) */
+    FLS_ERR_NOMEM = -6
+} fls_status;
+
+typedef struct fls_connection fls_connection;
+typedef struct fls_table fls_table;
+
+typedef struct fls_column_info {
+    const char *name;   /* NUL-terminated, owned by the table */
+    uint8_t type;       /* enum fls_type (flswriter.h) */
+    uint8_t width;      /* DECIMAL width */
+    uint8_t scale;      /* DECIMAL scale */
+    uint8_t out_bytes;  /* bytes per decoded value (string_t = 16) */
+} fls_column_info;
+
+typedef struct fls_rowgroup {
+    uint32_t rowgroup;            /* row-group index within the table */
+    uint32_t nrows;
+    uint64_t first_row;           /* global row index of the first row */
+    uint32_t ncols;
+    const void *const *columns;   /* ncols pointers into pinned host memory;
+                                     NULL for columns not selected */
+} fls_rowgroup;
+
+typedef struct fls_decode_stats {
+    double kernel_ms;             /* duration of the last decode launch (HIP events) */
+    uint64_t values;              /* values decoded by that launch */
+    uint64_t packed_bytes;        /* algorithmic bytes read: bit-packed streams */
+    uint64_t meta_bytes;          /* per-vector metadata, bases, dictionaries, run values */
+    uint64_t out_bytes;           /* algorithmic bytes written: decoded columns */
+    uint32_t launches;            /* decode launches since upload */
+    uint32_t timed_launches;      /* launches since the previous fls_device_sync */
+    double kernel_ms_total;       /* sum of their kernel durations (HIP events on the
+                                     decode stream, one start/stop pair per launch) */
+} fls_decode_stats;
+
+const char *fls_last_error(void);
+const char *fls_version(void);
+/* Number of HIP devices visible (0 when there is no GPU). */
+int fls_device_count(void);
+
+/* fastlanes::connect(): devices = HIP ordinals to shard row groups over
+ * (NULL/0 = device 0). */
+int fls_connect(const int *devices, int ndevices, fls_connection **out);
+void fls_disconnect(fls_connection *conn);
+
+/* Connection::read_fls(): parse footer + schema (no GPU work). */
+int fls_read_fls(fls_connection *conn, const char *path, fls_table **out);
+/* Same over an in-memory image (copy=0: caller keeps img alive). */
+int fls_read_fls_image(fls_connection *conn, const void *img, uint64_t len, int copy, fls_table **out);
+void fls_table_close(fls_table *t);
+
+uint32_t fls_table_ncols(const fls_table *t);
+uint64_t fls_table_nrows(const fls_table *t);
+uint64_t fls_table_row_offset(const fls_table *t);
+uint32_t fls_table_nrowgroups(const fls_table *t);
+int64_t fls_table_rowgroup_rows(const fls_table *t, uint32_t rg);
+int fls_table_column(const fls_table *t, uint32_t col, fls_column_info *out);
+
+/* Decode the selected columns (col_mask[c] != 0; NULL = all) of one row group
+ * on the GPU that owns it and deliver them into pinned host buffers owned by
+ * the table, valid until the next materialize/scan call. */
+int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowgroup *out);
+
+/* Streaming scan over row groups [rg_begin, rg_end) in order: row groups are
+ * sharded contiguously over the connection's GPUs, uploaded once, decoded in
+ * batches and copied to pinned host memory ahead of the consumer. */
+int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uint32_t rg_end);
+/* 1 = a row group was delivered into *out, 0 = end of scan, <0 = error. */
+int fls_scan_next(fls_table *t, fls_rowgroup *out);
+
+/* ---- device-resident mode (HBM roofline measurement, bench.py) ---------
+ * Upload row groups [rg_begin, rg_end) of the table to the connection's first
+ * GPU and allocate HBM output columns for them. */
+int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end);
+/* Enqueue ONE decode launch over every resident vector of the selected
+ * columns (col_mask NULL = all) into HBM.  Asynchronous. */
+int fls_device_decode(fls_table *t, const uint8_t *col_mask);
+/* Wait for the table's GPU work; fills *stats if non-NULL (kernel_ms = last
+ * launch, kernel_ms_total over the launches since the previous sync). */
+int fls_device_sync(fls_table *t, fls_decode_stats *stats);
+/* HBM address and byte size of a resident output column. */
+int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbytes);
+/* Copy rows [row, row+n) (relative to the first resident row) of a decoded
+ * column into host memory. */
+int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, void *host_dst);
+/* Rows resident on the device. */
+uint64_t fls_device_rows(const fls_table *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,72 @@
+/*
+ * flswriter.h -- C-ABI of the CPU FastLanes writer and the seeded workload
+ * generators (libflsgpu.so).
+ *
+ * Reference interfaces this replaces / serves:
+ *   - ext_fastlane::FastLanesFacade::createFile / writeChunk / finalizeFile
+ *     (src/include/fastlanes_facade.hpp:39-43; declared, never implemented in
+ *     the reference) and the COPY ... TO 'x.fls' (FORMAT FLS) writer stub
+ *     (src/writer/write_fastlane_stream.cpp:65-314, row_group_size default
+ *     65,536 at :21-24).  Exposed as the copy function in SURVEY.md 8(f) row 1.
+ *   - the data file third_party/fastlanes/data/fls/data.fls that
+ *     test/sql/fastlane.test:15-66 scans (absent; regenerated synthetically).
+ *
+ * All functions return 0 on success and a negative fls_status on error;
+ * fls_last_error() (flsgpu.h) describes the last error of the calling thread.
+ */
+#ifndef FLSWRITER_H
+#define FLSWRITER_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fls_writer fls_writer;
+
+/* Column types (cf. reference src/type_mapping.cpp:64-109). */
+enum fls_type {
+    FLS_INT8 = 1, FLS_INT16 = 2, FLS_INT32 = 3, FLS_INT64 = 4,
+    FLS_UINT8 = 5, FLS_UINT16 = 6, FLS_UINT32 = 7, FLS_UINT64 = 8,
+    FLS_DATE = 10, FLS_DECIMAL = 11, FLS_VARCHAR = 20
+};
+/* Encodings; FLS_ENC_AUTO picks the smallest of the applicable ones per chunk. */
+enum fls_encoding { FLS_ENC_AUTO = 0, FLS_ENC_FFOR = 1, FLS_ENC_DELTA = 2, FLS_ENC_DICT = 3, FLS_ENC_RLE = 4 };
+
+/* New writer; row_offset = global index of the first row (shards). */
+fls_writer *fls_writer_new(uint64_t row_offset);
+void fls_writer_free(fls_writer *w);
+int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t width,
+                          uint8_t scale, uint8_t encoding);
+/* Append one row group of nrows (1..65536) rows.  Integer column c:
+ * data[c] -> nrows values of the column's width (1/2/4/8 B).  VARCHAR column c:
+ * data[c] -> concatenated bytes, str_offsets[c] -> nrows+1 uint32 offsets
+ * (str_offsets may be NULL when there is no VARCHAR column). */
+int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *data,
+                            const uint32_t *const *str_offsets);
+/* Assemble the file: to `path`, or into a malloc'ed buffer freed with
+ * fls_image_free. */
+int fls_writer_finish_file(fls_writer *w, const char *path);
+int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len);
+void fls_image_free(uint8_t *img);
+
+/* ---- seeded synthetic workloads (fls_gen.hpp) -------------------------
+ * workload: "c1", "lineitem", "c3", "c4".  scale: lineitem scale factor
+ * (ignored otherwise).  nrows: 0 = workload default (c1 1e6, c3/c4 1e9,
+ * lineitem dbgen row count for the scale).  Row groups [rg_begin, rg_end) of
+ * the full table are encoded into one image (a shard) using nthreads. */
+int64_t fls_gen_nrows(const char *workload, double scale, uint64_t nrows);
+int fls_gen_ncols(const char *workload);
+int fls_gen_image(const char *workload, double scale, uint64_t nrows, uint32_t rg_begin,
+                  uint32_t rg_end, int nthreads, uint8_t **img, uint64_t *len);
+/* Ground truth of column col for rows [row_begin, row_begin+n): integer columns
+ * in their value width, VARCHAR columns as uint32 dictionary codes. */
+int fls_gen_values(const char *workload, double scale, uint64_t nrows, int col,
+                   uint64_t row_begin, uint64_t n, void *out);
+/* Dictionary string `code` of VARCHAR column col (NULL if none). */
+const char *fls_gen_dict_string(const char *workload, int col, uint32_t code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

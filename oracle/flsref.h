@@ -1,0 +1,95 @@
+/*
+ * flsref.h -- CPU restatement of the FastLanes decode path (ORACLE).
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * or the timed CPU baseline.  The product (duckdb-fastlane_amd/) never links it.
+ *
+ * PARITY UNPINNED.  The reference (lmangani/duckdb-fastlane @ 2025-08-24)
+ * delegates every decode step to the cwida/FastLanes library
+ * (.gitmodules:9-12, branch `dev`, commit unknown, vcpkg port 0.1.0 at
+ * vcpkg_ports/fastlanes/vcpkg.json:3).  That submodule is empty in
+ * /root/reference and no .fls fixture exists (test/sql/fastlane.test:15-66
+ * needs third_party/fastlanes/data/fls/data.fls, absent), so neither the
+ * library nor its byte format can be executed or compared here.  This file
+ * restates the published FastLanes algorithm (Afroozeh & Boncz, "The
+ * FastLanes Compression Layout", VLDB 2023) over this repo's container
+ * format (DESIGN.md "Container format"), and is pinned by hand-computed
+ * known-answer tests, an independent numpy restatement (oracle/flsref_np.py)
+ * and the seeded generators' ground truth (integer codecs are lossless).
+ *
+ * Call sites of the replaced decode in the reference:
+ *   src/fastlanes_facade.cpp:33  fastlanes::connect()
+ *   src/fastlanes_facade.cpp:34  Connection::read_fls(path)
+ *   src/fastlanes_facade.cpp:41  TableReader::get_rowgroup_reader(0)
+ *   src/fastlanes_facade.cpp:48  RowgroupReader::materialize()   <- decode
+ *   src/fastlanes_facade.cpp:112-183  per-type column access
+ */
+#ifndef FLSREF_H
+#define FLSREF_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* --- layout primitives (paper section 3/4) --------------------------------- */
+
+/* Original tuple index stored at position p (0..1023) of the unified
+ * transposed layout.  FL_ORDER = {0,4,2,6,1,5,3,7}. */
+uint32_t flsref_tau(uint32_t p);
+
+/* Interleaved bit-unpack of one 1024-value vector: T in {8,16,32,64},
+ * 0 <= W <= T.  packed holds 128*W bytes (W words of T bits per lane,
+ * word k of lane L at word index k*(1024/T)+L).  out[p] = unsigned value at
+ * position p = row*(1024/T)+lane. */
+void flsref_unpack(int T, int W, const void *packed, uint64_t *out);
+
+/* Inverse of flsref_unpack (used only by tests to build KATs). */
+void flsref_pack(int T, int W, const uint64_t *in, void *packed);
+
+/* --- container decode ---------------------------------------------------- */
+
+typedef struct {
+    const uint8_t *img;
+    size_t len;
+    uint32_t ncols;
+    uint64_t nrows;
+    uint32_t nrowgroups;
+    uint32_t rowgroup_size;
+    uint64_t row_offset;
+    const uint8_t *footer;
+    uint32_t footer_len;
+} flsref_file;
+
+/* Parse the footer of an in-memory image.  Returns 0 on success. */
+int flsref_open(const void *img, size_t len, flsref_file *f);
+
+/* Column schema: logical type id, decimal width/scale, name (not NUL
+ * terminated; *name_len bytes). Returns 0 on success. */
+int flsref_column(const flsref_file *f, uint32_t col, int *type, int *width,
+                  int *scale, const char **name, int *name_len);
+
+/* Rows in row group rg (or -1 on error). */
+int64_t flsref_rowgroup_rows(const flsref_file *f, uint32_t rg);
+
+/* Decode column `col` of row group `rg`.
+ * Integer columns: out receives nrows values of the column's value width
+ *   (1/2/4/8 bytes, little-endian two's complement).
+ * VARCHAR columns: out receives nrows pairs {uint64 byte offset into the
+ *   image, uint64 length} naming each value's bytes inside the image.
+ * Returns number of rows decoded, or -1 on a malformed chunk. */
+int64_t flsref_decode(const flsref_file *f, uint32_t col, uint32_t rg, void *out);
+
+/* Decode every row group of `col` into out (rows concatenated).  Threads:
+ * nthreads > 1 decodes row groups in parallel (CPU baseline).  Returns rows. */
+int64_t flsref_decode_column(const flsref_file *f, uint32_t col, void *out, int nthreads);
+
+/* Bytes per output value of column col (1/2/4/8, or 16 for VARCHAR pairs). */
+int flsref_out_width(const flsref_file *f, uint32_t col);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
