@@ -406,3 +406,54 @@ def string_t_decode(raw: np.ndarray) -> list[bytes]:
             ptr = int(rec[i, 8:16].copy().view(np.uint64)[0])
             out.append(C.string_at(ptr, n))
     return out
+
+
+# --- full-size GPU verification (libflscheck.so; tests / bench support) ------
+_check_lib = None
+
+
+def _checklib():
+    global _check_lib
+    if _check_lib is None:
+        path = _HERE / "libflscheck.so"
+        if not path.exists():
+            raise ImportError(f"{path} not built")
+        lib_ = C.CDLL(str(path))
+        lib_.fls_check_workload.restype = C.c_int
+        lib_.fls_check_workload.argtypes = [C.c_char_p, C.c_double, C.c_uint64, C.c_uint64, C.c_uint64,
+                                            C.POINTER(_P), C.POINTER(C.c_uint8), C.c_int, C.POINTER(_P),
+                                            C.POINTER(C.c_uint64)]
+        lib_.fls_check_last_error.restype = C.c_char_p
+        _check_lib = lib_
+    return _check_lib
+
+
+def check_device_table(t: "Table", workload: str, scale: float = 1.0, nrows: int = 0) -> list[int]:
+    """Mismatching rows per column of t's resident decoded columns vs the
+    workload generator (computed on the GPU).  Call after device_sync()."""
+    lib_ = _checklib()
+    nc = t.ncols
+    total = gen_nrows(workload, scale, nrows)
+    cols = (_P * nc)()
+    obs = (C.c_uint8 * nc)()
+    dicts = (_P * nc)()
+    keep = []
+    for c in range(nc):
+        ptr, _ = t.device_column(c)
+        cols[c] = ptr
+        obs[c] = t.column(c).out_bytes
+        if obs[c] == 16:
+            words = []
+            k = 0
+            while (s := gen_dict_string(workload, c, k)) is not None:
+                words.append(s.encode())
+                k += 1
+            b = C.create_string_buffer(b"\0".join(words) + b"\0\0")
+            keep.append(b)
+            dicts[c] = C.cast(b, _P)
+    mism = (C.c_uint64 * nc)()
+    rc = lib_.fls_check_workload(workload.encode(), scale, total, t.row_offset, t.device_rows, cols, obs, nc,
+                                 dicts, mism)
+    if rc != 0:
+        raise FlsError(rc, lib_.fls_check_last_error().decode())
+    return list(mism)

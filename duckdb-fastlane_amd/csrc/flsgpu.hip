@@ -193,6 +193,7 @@ struct fls_table {
     std::vector<DevBuf<uint8_t>> d_out;  // per column, rows of [rg0, rg1)
     DevBuf<DevChunk> d_chunks;
     std::vector<DevChunk> h_chunks;
+    std::vector<uint8_t> dev_mask;     // column mask h_chunks was built for
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
@@ -622,6 +623,7 @@ int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
     for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(t->d_out[c].alloc(dev, t->res_rows * out_bytes_of(t, c)));
     if (!t->grid) t->grid = decode_grid_size();
     t->h_chunks.clear();
+    t->dev_mask.clear();
     t->launches = 0;
     t->launched = false;
     return 0;
@@ -635,27 +637,28 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     std::vector<uint8_t> mask(ncols, 1);
     if (col_mask)
         for (uint32_t c = 0; c < ncols; ++c) mask[c] = col_mask[c] ? 1 : 0;
-    // column-major task order: concurrent waves stream one column's row groups
-    std::vector<DevChunk> chunks;
-    ByteCount bc;
-    for (uint32_t c = 0; c < ncols; ++c) {
-        if (!mask[c]) continue;
-        for (uint32_t r = sh.rg0; r < sh.rg1; ++r) {
-            const ChunkRef &ch = t->meta.rgs[r].chunks[c];
-            const uint64_t so = sh.strtab_off[(size_t)(r - sh.rg0) * ncols + c];
-            const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(sh.strtab.p + so);
-            uint8_t *out = t->d_out[c].p + (t->meta.rgs[r].first_row - t->res_first_row) * out_bytes_of(t, c);
-            chunks.push_back(make_devchunk(t, r, c, sh.img.p + (ch.off - sh.base), dict, out, &bc));
-        }
-    }
     HIP_TRY(hipSetDevice(sh.dev));
-    const bool same = chunks.size() == t->h_chunks.size() &&
-                      !memcmp(chunks.data(), t->h_chunks.data(), chunks.size() * sizeof(DevChunk));
-    if (!same) {
+    if (mask != t->dev_mask || t->h_chunks.empty()) {
+        // (re)build the launch descriptor list: column-major task order, so
+        // concurrent waves stream one column's consecutive row groups
+        std::vector<DevChunk> chunks;
+        ByteCount bc;
+        for (uint32_t c = 0; c < ncols; ++c) {
+            if (!mask[c]) continue;
+            for (uint32_t r = sh.rg0; r < sh.rg1; ++r) {
+                const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+                const uint64_t so = sh.strtab_off[(size_t)(r - sh.rg0) * ncols + c];
+                const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(sh.strtab.p + so);
+                uint8_t *out = t->d_out[c].p + (t->meta.rgs[r].first_row - t->res_first_row) * out_bytes_of(t, c);
+                chunks.push_back(make_devchunk(t, r, c, sh.img.p + (ch.off - sh.base), dict, out, &bc));
+            }
+        }
         HIP_TRY(hipStreamSynchronize(t->stream));
         HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
         HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
-        t->h_chunks = chunks;
+        t->h_chunks.swap(chunks);
+        t->dev_mask = mask;
+        t->last_bytes = bc;
     }
     if (t->ev_used + 2 > t->ev_pool.size()) {
         for (int i = 0; i < 2; ++i) {
@@ -667,9 +670,8 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(launch_decode(t->d_chunks.p, (uint32_t)chunks.size(), sh.err.p, t->grid, t->stream));
+    HIP_TRY(launch_decode(t->d_chunks.p, (uint32_t)t->h_chunks.size(), sh.err.p, t->grid, t->stream));
     HIP_TRY(hipEventRecord(e1, t->stream));
-    t->last_bytes = bc;
     t->launches++;
     t->launched = true;
     return 0;

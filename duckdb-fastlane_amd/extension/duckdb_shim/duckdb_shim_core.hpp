@@ -1,0 +1,451 @@
+// duckdb_shim_core.hpp -- the slice of the DuckDB v1.3.2 C++ extension API the
+// FastLanes glue uses, declared from public knowledge of
+// DuckDB because the duckdb/ submodule is empty (.gitmodules:1-4).  It lets
+// the glue in ../ compile and run unchanged in this container; against a real
+// DuckDB v1.3.2 the glue compiles with DuckDB's own headers instead (same
+// include paths: "duckdb.hpp", "duckdb/function/table_function.hpp", ...).
+// Only the behaviour the glue and the tests observe is modelled: flat vectors,
+// Value casts to VARCHAR, string_t, table-function callbacks, replacement
+// scans, exceptions.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace duckdb {
+
+using std::move;
+using std::string;
+template <class T>
+using vector = std::vector<T>;
+template <class T, class D = std::default_delete<T>>
+using unique_ptr = std::unique_ptr<T, D>;
+template <class T>
+using shared_ptr = std::shared_ptr<T>;
+template <class T>
+using optional_ptr = T *;
+using idx_t = uint64_t;
+using column_t = uint64_t;
+using data_ptr_t = uint8_t *;
+
+constexpr idx_t STANDARD_VECTOR_SIZE = 2048;
+constexpr column_t COLUMN_IDENTIFIER_ROW_ID = (column_t)-1;
+
+template <class T, class... Args>
+unique_ptr<T> make_uniq(Args &&...args) {
+    return std::unique_ptr<T>(new T(std::forward<Args>(args)...));
+}
+template <class T, class... Args>
+shared_ptr<T> make_shared_ptr(Args &&...args) {
+    return std::make_shared<T>(std::forward<Args>(args)...);
+}
+
+// ---- exceptions ----------------------------------------------------------
+class Exception : public std::runtime_error {
+public:
+    explicit Exception(const string &msg) : std::runtime_error(msg) {}
+};
+class BinderException : public Exception {
+public:
+    explicit BinderException(const string &msg) : Exception(msg) {}
+};
+class IOException : public Exception {
+public:
+    explicit IOException(const string &msg) : Exception(msg) {}
+};
+class InvalidInputException : public Exception {
+public:
+    explicit InvalidInputException(const string &msg) : Exception(msg) {}
+};
+class InternalException : public Exception {
+public:
+    explicit InternalException(const string &msg) : Exception(msg) {}
+};
+class NotImplementedException : public Exception {
+public:
+    explicit NotImplementedException(const string &msg) : Exception(msg) {}
+};
+
+// ---- types -----------------------------------------------------------------
+enum class LogicalTypeId : uint8_t {
+    INVALID = 0, SQLNULL, BOOLEAN, TINYINT, SMALLINT, INTEGER, BIGINT, UTINYINT, USMALLINT, UINTEGER,
+    UBIGINT, DATE, FLOAT, DOUBLE, DECIMAL, VARCHAR, LIST
+};
+
+struct LogicalType {
+    LogicalType() : id_(LogicalTypeId::INVALID) {}
+    LogicalType(LogicalTypeId id) : id_(id) {}  // NOLINT (implicit like DuckDB)
+    LogicalTypeId id() const { return id_; }
+    bool operator==(const LogicalType &o) const {
+        if (id_ != o.id_) return false;
+        if (id_ == LogicalTypeId::DECIMAL) return width_ == o.width_ && scale_ == o.scale_;
+        if (id_ == LogicalTypeId::LIST) return child_ && o.child_ && *child_ == *o.child_;
+        return true;
+    }
+    bool operator!=(const LogicalType &o) const { return !(*this == o); }
+    static LogicalType DECIMAL(uint8_t w, uint8_t s) {
+        LogicalType t(LogicalTypeId::DECIMAL);
+        t.width_ = w;
+        t.scale_ = s;
+        return t;
+    }
+    static LogicalType LIST(const LogicalType &child) {
+        LogicalType t(LogicalTypeId::LIST);
+        t.child_ = std::make_shared<LogicalType>(child);
+        return t;
+    }
+    uint8_t Width() const { return width_; }
+    uint8_t Scale() const { return scale_; }
+    idx_t PhysicalSize() const;   // bytes per value in a flat vector
+    string ToString() const;
+
+    static const LogicalType SQLNULL, BOOLEAN, TINYINT, SMALLINT, INTEGER, BIGINT, UTINYINT, USMALLINT,
+        UINTEGER, UBIGINT, DATE, FLOAT, DOUBLE, VARCHAR;
+
+private:
+    LogicalTypeId id_;
+    uint8_t width_ = 0, scale_ = 0;
+    shared_ptr<LogicalType> child_;
+};
+
+// DuckDB string_t: 16 bytes, inlined up to 12 characters
+struct string_t {
+    static constexpr uint32_t INLINE_LENGTH = 12;
+    string_t() { memset(this, 0, sizeof(*this)); }
+    string_t(const char *data, uint32_t len) {
+        memset(this, 0, sizeof(*this));
+        value.inlined.length = len;
+        if (len <= INLINE_LENGTH) {
+            if (len) memcpy(value.inlined.inlined, data, len);
+        } else {
+            memcpy(value.pointer.prefix, data, 4);
+            value.pointer.ptr = const_cast<char *>(data);
+        }
+    }
+    uint32_t GetSize() const { return value.inlined.length; }
+    const char *GetData() const {
+        return GetSize() <= INLINE_LENGTH ? value.inlined.inlined : value.pointer.ptr;
+    }
+    string GetString() const { return string(GetData(), GetSize()); }
+    union {
+        struct {
+            uint32_t length;
+            char prefix[4];
+            char *ptr;
+        } pointer;
+        struct {
+            uint32_t length;
+            char inlined[12];
+        } inlined;
+    } value;
+};
+static_assert(sizeof(string_t) == 16, "string_t is 16 bytes");
+
+struct date_t {
+    int32_t days;
+};
+
+// ---- Value -----------------------------------------------------------------
+class Value {
+public:
+    Value() : type_(LogicalType::SQLNULL), is_null_(true) {}
+    Value(const string &s) : type_(LogicalType::VARCHAR), is_null_(false), str_(s) {}  // NOLINT
+    Value(const char *s) : Value(string(s)) {}                                          // NOLINT
+    static Value INTEGER(int32_t v) { return Value(LogicalType::INTEGER, (int64_t)v); }
+    static Value BIGINT(int64_t v) { return Value(LogicalType::BIGINT, v); }
+    static Value TINYINT(int8_t v) { return Value(LogicalType::TINYINT, (int64_t)v); }
+    static Value SMALLINT(int16_t v) { return Value(LogicalType::SMALLINT, (int64_t)v); }
+    static Value UTINYINT(uint8_t v) { return Value(LogicalType::UTINYINT, (int64_t)v); }
+    static Value USMALLINT(uint16_t v) { return Value(LogicalType::USMALLINT, (int64_t)v); }
+    static Value UINTEGER(uint32_t v) { return Value(LogicalType::UINTEGER, (int64_t)v); }
+    static Value UBIGINT(uint64_t v) { return Value(LogicalType::UBIGINT, (int64_t)v); }
+    static Value DATE(date_t d) { return Value(LogicalType::DATE, (int64_t)d.days); }
+    static Value DECIMAL(int64_t v, uint8_t w, uint8_t s) { return Value(LogicalType::DECIMAL(w, s), v); }
+    static Value FLOAT(float v) { Value x(LogicalType::FLOAT, 0); x.dbl_ = v; return x; }
+    static Value DOUBLE(double v) { Value x(LogicalType::DOUBLE, 0); x.dbl_ = v; return x; }
+    static Value LIST(const LogicalType &child, vector<Value> items) {
+        Value x(LogicalType::LIST(child), 0);
+        x.list_ = std::move(items);
+        return x;
+    }
+
+    const LogicalType &type() const { return type_; }
+    bool IsNull() const { return is_null_; }
+    template <class T>
+    T GetValue() const;
+    int64_t GetInt64() const { return int_; }
+    double GetDouble() const { return dbl_; }
+    const vector<Value> &ListChildren() const { return list_; }
+    // DuckDB's VARCHAR rendering of the value (the cast Vector::SetValue applies)
+    string ToString() const;
+
+private:
+    Value(LogicalType t, int64_t v) : type_(std::move(t)), is_null_(false), int_(v) {}
+    LogicalType type_;
+    bool is_null_;
+    int64_t int_ = 0;
+    double dbl_ = 0;
+    string str_;
+    vector<Value> list_;
+};
+template <>
+inline string Value::GetValue<string>() const { return is_null_ ? string() : (type_.id() == LogicalTypeId::VARCHAR ? str_ : ToString()); }
+template <>
+inline int64_t Value::GetValue<int64_t>() const { return int_; }
+template <>
+inline int32_t Value::GetValue<int32_t>() const { return (int32_t)int_; }
+template <>
+inline bool Value::GetValue<bool>() const { return int_ != 0; }
+
+// ---- vectors ---------------------------------------------------------------
+enum class VectorType : uint8_t { FLAT_VECTOR, CONSTANT_VECTOR };
+
+class Vector {
+public:
+    explicit Vector(LogicalType type, idx_t capacity = STANDARD_VECTOR_SIZE);
+    const LogicalType &GetType() const { return type_; }
+    void SetValue(idx_t index, const Value &val);
+    Value GetValue(idx_t index) const;
+    data_ptr_t GetData() { return data_.data(); }
+    const uint8_t *GetData() const { return data_.data(); }
+    bool RowIsValid(idx_t i) const { return valid_[i]; }
+    void SetValid(idx_t i, bool v) { valid_[i] = v; }
+    void SetVectorType(VectorType t) { vtype_ = t; }
+    VectorType GetVectorType() const { return vtype_; }
+    idx_t Capacity() const { return capacity_; }
+    void Reset();
+    // string heap owned by this vector (StringVector::AddString)
+    string_t AddString(const string &s);
+    void KeepAlive(shared_ptr<void> p) { keep_.push_back(std::move(p)); }
+
+private:
+    LogicalType type_;
+    idx_t capacity_;
+    vector<uint8_t> data_;
+    vector<bool> valid_;
+    std::deque<string> heap_;
+    vector<shared_ptr<void>> keep_;
+    VectorType vtype_ = VectorType::FLAT_VECTOR;
+};
+
+struct FlatVector {
+    template <class T>
+    static T *GetData(Vector &v) { return reinterpret_cast<T *>(v.GetData()); }
+    static void SetNull(Vector &v, idx_t i, bool is_null) { v.SetValid(i, !is_null); }
+};
+struct StringVector {
+    static string_t AddString(Vector &v, const string &s) { return v.AddString(s); }
+    static void AddBuffer(Vector &v, shared_ptr<void> keep) { v.KeepAlive(std::move(keep)); }
+};
+
+class DataChunk {
+public:
+    vector<Vector> data;
+    idx_t ColumnCount() const { return data.size(); }
+    idx_t size() const { return count_; }
+    void SetCardinality(idx_t n) { count_ = n; }
+    void InitializeEmpty(const vector<LogicalType> &types) {
+        data.clear();
+        for (auto &t : types) data.emplace_back(t);
+        count_ = 0;
+    }
+    void Initialize(const vector<LogicalType> &types) { InitializeEmpty(types); }
+    void Reset() {
+        for (auto &v : data) v.Reset();
+        count_ = 0;
+    }
+    vector<LogicalType> GetTypes() const {
+        vector<LogicalType> t;
+        for (auto &v : data) t.push_back(v.GetType());
+        return t;
+    }
+
+private:
+    idx_t count_ = 0;
+};
+
+// ---- functions -------------------------------------------------------------
+class ClientContext {};
+class ExecutionContext {
+public:
+    ClientContext &client;
+    explicit ExecutionContext(ClientContext &c) : client(c) {}
+};
+class DatabaseInstance;
+
+struct FunctionData {
+    virtual ~FunctionData() = default;
+    template <class T>
+    T &Cast() { return static_cast<T &>(*this); }
+    template <class T>
+    const T &Cast() const { return static_cast<const T &>(*this); }
+};
+struct TableFunctionData : public FunctionData {
+    vector<column_t> column_ids;
+};
+struct GlobalTableFunctionState {
+    virtual ~GlobalTableFunctionState() = default;
+    virtual idx_t MaxThreads() const { return 1; }
+    template <class T>
+    T &Cast() { return static_cast<T &>(*this); }
+};
+struct LocalTableFunctionState {
+    virtual ~LocalTableFunctionState() = default;
+    template <class T>
+    T &Cast() { return static_cast<T &>(*this); }
+};
+
+using named_parameter_map_t = std::unordered_map<string, Value>;
+using named_parameter_type_map_t = std::unordered_map<string, LogicalType>;
+
+struct TableFunctionBindInput {
+    vector<Value> &inputs;
+    named_parameter_map_t &named_parameters;
+};
+struct TableFunctionInitInput {
+    optional_ptr<const FunctionData> bind_data;
+    const vector<column_t> &column_ids;
+};
+struct TableFunctionInput {
+    optional_ptr<const FunctionData> bind_data;
+    optional_ptr<LocalTableFunctionState> local_state;
+    optional_ptr<GlobalTableFunctionState> global_state;
+};
+
+using table_function_bind_t = unique_ptr<FunctionData> (*)(ClientContext &, TableFunctionBindInput &,
+                                                           vector<LogicalType> &, vector<string> &);
+using table_function_init_global_t = unique_ptr<GlobalTableFunctionState> (*)(ClientContext &,
+                                                                             TableFunctionInitInput &);
+using table_function_init_local_t = unique_ptr<LocalTableFunctionState> (*)(ExecutionContext &,
+                                                                           TableFunctionInitInput &,
+                                                                           GlobalTableFunctionState *);
+using table_function_t = void (*)(ClientContext &, TableFunctionInput &, DataChunk &);
+
+class TableFunction {
+public:
+    TableFunction(string name, vector<LogicalType> arguments, table_function_t function,
+                  table_function_bind_t bind = nullptr, table_function_init_global_t init_global = nullptr,
+                  table_function_init_local_t init_local = nullptr)
+        : name(std::move(name)), arguments(std::move(arguments)), function(function), bind(bind),
+          init_global(init_global), init_local(init_local) {}
+    string name;
+    vector<LogicalType> arguments;
+    named_parameter_type_map_t named_parameters;
+    table_function_t function;
+    table_function_bind_t bind;
+    table_function_init_global_t init_global;
+    table_function_init_local_t init_local;
+    bool projection_pushdown = false;
+    bool filter_pushdown = false;
+    bool filter_prune = false;
+    void *in_out_function = nullptr;
+};
+
+struct ExpressionState {};
+using scalar_function_t = void (*)(DataChunk &, ExpressionState &, Vector &);
+class ScalarFunction {
+public:
+    ScalarFunction(string name, vector<LogicalType> arguments, LogicalType return_type, scalar_function_t fn)
+        : name(std::move(name)), arguments(std::move(arguments)), return_type(std::move(return_type)),
+          function(fn) {}
+    string name;
+    vector<LogicalType> arguments;
+    LogicalType return_type;
+    scalar_function_t function;
+};
+
+// ---- replacement scans -----------------------------------------------------
+class ParsedExpression {
+public:
+    virtual ~ParsedExpression() = default;
+};
+class ConstantExpression : public ParsedExpression {
+public:
+    explicit ConstantExpression(Value v) : value(std::move(v)) {}
+    Value value;
+};
+class FunctionExpression : public ParsedExpression {
+public:
+    FunctionExpression(string name, vector<unique_ptr<ParsedExpression>> children)
+        : function_name(std::move(name)), children(std::move(children)) {}
+    string function_name;
+    vector<unique_ptr<ParsedExpression>> children;
+};
+class TableRef {
+public:
+    virtual ~TableRef() = default;
+};
+class TableFunctionRef : public TableRef {
+public:
+    unique_ptr<ParsedExpression> function;
+};
+struct ReplacementScanInput {
+    string table_name;
+};
+struct ReplacementScanData {
+    virtual ~ReplacementScanData() = default;
+};
+using replacement_scan_t = unique_ptr<TableRef> (*)(ClientContext &, ReplacementScanInput &,
+                                                    optional_ptr<ReplacementScanData>);
+struct ReplacementScan {
+    ReplacementScan(replacement_scan_t fn) : function(fn) {}  // NOLINT
+    replacement_scan_t function;
+    static string GetFullPath(const ReplacementScanInput &input) { return input.table_name; }
+};
+
+struct DBConfig {
+    vector<ReplacementScan> replacement_scans;
+    static DBConfig &GetConfig(DatabaseInstance &db);
+};
+
+class DatabaseInstance {
+public:
+    DBConfig config;
+    std::multimap<string, TableFunction> table_functions;
+    std::multimap<string, ScalarFunction> scalar_functions;
+};
+
+class DuckDB {
+public:
+    explicit DuckDB(DatabaseInstance &db) : instance(&db, [](DatabaseInstance *) {}) {}
+    shared_ptr<DatabaseInstance> instance;
+    static const char *LibraryVersion() { return "v1.3.2"; }
+};
+
+class Extension {
+public:
+    virtual ~Extension() = default;
+    virtual void Load(DuckDB &db) = 0;
+    virtual std::string Name() = 0;
+    virtual std::string Version() const { return ""; }
+};
+
+struct ExtensionUtil {
+    static void RegisterFunction(DatabaseInstance &db, TableFunction fn) {
+        db.table_functions.emplace(fn.name, std::move(fn));
+    }
+    static void RegisterFunction(DatabaseInstance &db, ScalarFunction fn) {
+        db.scalar_functions.emplace(fn.name, std::move(fn));
+    }
+};
+
+struct StringUtil {
+    static string Lower(const string &s);
+    static bool EndsWith(const string &s, const string &suffix) {
+        return s.size() >= suffix.size() && s.compare(s.size() - suffix.size(), suffix.size(), suffix) == 0;
+    }
+};
+
+}  // namespace duckdb
+
+#ifndef DUCKDB_EXTENSION_API
+#define DUCKDB_EXTENSION_API __attribute__((visibility("default")))
+#endif

@@ -1,0 +1,30 @@
+/*
+ * flscheck.h -- full-size GPU verification of decoded columns against the
+ * seeded generators (libflscheck.so).  Test / bench support: it answers
+ * "is every decoded value of a 1e9-row / SF100 scan bit-exact?" without a host
+ * copy, by regenerating the ground truth (duckdb-fastlane_amd/csrc/fls_gen.hpp)
+ * on the GPU next to the decoded columns.  Not part of the decode product.
+ */
+#ifndef FLSCHECK_H
+#define FLSCHECK_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Compare decoded rows [0, n) -- global rows [row_begin, row_begin+n) of the
+ * workload -- of ncols columns resident on the current HIP device.
+ * d_cols[c]: device column (NULL = skip); out_bytes[c]: 1/2/4/8 or 16 for
+ * string_t; dicts[c]: for VARCHAR columns a NUL-separated, double-NUL-ended
+ * list of the dictionary strings (codes 0..7).  mismatches[c] receives the
+ * number of mismatching rows.  Returns 0, or -1 with fls_check_last_error(). */
+int fls_check_workload(const char *workload, double scale, uint64_t nrows_total, uint64_t row_begin,
+                       uint64_t n, const void *const *d_cols, const uint8_t *out_bytes, int ncols,
+                       const void *const *dicts, uint64_t *mismatches);
+const char *fls_check_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
