@@ -1,0 +1,196 @@
+// duckdb_shim.cpp -- implementation of the DuckDB v1.3.2 API slice declared in
+// duckdb_shim_core.hpp (flat vectors, Value -> VARCHAR casts, string heap).
+#include <algorithm>
+#include <cctype>
+#include <cstdio>
+
+#include "duckdb_shim_core.hpp"
+
+namespace duckdb {
+
+const LogicalType LogicalType::SQLNULL(LogicalTypeId::SQLNULL);
+const LogicalType LogicalType::BOOLEAN(LogicalTypeId::BOOLEAN);
+const LogicalType LogicalType::TINYINT(LogicalTypeId::TINYINT);
+const LogicalType LogicalType::SMALLINT(LogicalTypeId::SMALLINT);
+const LogicalType LogicalType::INTEGER(LogicalTypeId::INTEGER);
+const LogicalType LogicalType::BIGINT(LogicalTypeId::BIGINT);
+const LogicalType LogicalType::UTINYINT(LogicalTypeId::UTINYINT);
+const LogicalType LogicalType::USMALLINT(LogicalTypeId::USMALLINT);
+const LogicalType LogicalType::UINTEGER(LogicalTypeId::UINTEGER);
+const LogicalType LogicalType::UBIGINT(LogicalTypeId::UBIGINT);
+const LogicalType LogicalType::DATE(LogicalTypeId::DATE);
+const LogicalType LogicalType::FLOAT(LogicalTypeId::FLOAT);
+const LogicalType LogicalType::DOUBLE(LogicalTypeId::DOUBLE);
+const LogicalType LogicalType::VARCHAR(LogicalTypeId::VARCHAR);
+
+idx_t LogicalType::PhysicalSize() const {
+    switch (id_) {
+    case LogicalTypeId::BOOLEAN: case LogicalTypeId::TINYINT: case LogicalTypeId::UTINYINT: return 1;
+    case LogicalTypeId::SMALLINT: case LogicalTypeId::USMALLINT: return 2;
+    case LogicalTypeId::INTEGER: case LogicalTypeId::UINTEGER: case LogicalTypeId::DATE:
+    case LogicalTypeId::FLOAT: return 4;
+    case LogicalTypeId::BIGINT: case LogicalTypeId::UBIGINT: case LogicalTypeId::DOUBLE: return 8;
+    case LogicalTypeId::DECIMAL: return width_ <= 4 ? 2 : width_ <= 9 ? 4 : 8;
+    case LogicalTypeId::VARCHAR: return 16;
+    default: return 8;
+    }
+}
+
+string LogicalType::ToString() const {
+    switch (id_) {
+    case LogicalTypeId::SQLNULL: return "NULL";
+    case LogicalTypeId::BOOLEAN: return "BOOLEAN";
+    case LogicalTypeId::TINYINT: return "TINYINT";
+    case LogicalTypeId::SMALLINT: return "SMALLINT";
+    case LogicalTypeId::INTEGER: return "INTEGER";
+    case LogicalTypeId::BIGINT: return "BIGINT";
+    case LogicalTypeId::UTINYINT: return "UTINYINT";
+    case LogicalTypeId::USMALLINT: return "USMALLINT";
+    case LogicalTypeId::UINTEGER: return "UINTEGER";
+    case LogicalTypeId::UBIGINT: return "UBIGINT";
+    case LogicalTypeId::DATE: return "DATE";
+    case LogicalTypeId::FLOAT: return "FLOAT";
+    case LogicalTypeId::DOUBLE: return "DOUBLE";
+    case LogicalTypeId::DECIMAL: return "DECIMAL(" + std::to_string(width_) + "," + std::to_string(scale_) + ")";
+    case LogicalTypeId::VARCHAR: return "VARCHAR";
+    case LogicalTypeId::LIST: return (child_ ? child_->ToString() : string("?")) + "[]";
+    default: return "INVALID";
+    }
+}
+
+namespace {
+
+// civil-from-days (Howard Hinnant), DuckDB renders DATE as YYYY-MM-DD
+string date_to_string(int32_t days) {
+    int64_t z = (int64_t)days + 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const unsigned doe = (unsigned)(z - era * 146097);
+    const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t y = (int64_t)yoe + era * 400;
+    const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const unsigned mp = (5 * doy + 2) / 153;
+    const unsigned d = doy - (153 * mp + 2) / 5 + 1;
+    const unsigned m = mp < 10 ? mp + 3 : mp - 9;
+    y += (m <= 2);
+    char buf[32];
+    snprintf(buf, sizeof(buf), "%04lld-%02u-%02u", (long long)y, m, d);
+    return buf;
+}
+
+string decimal_to_string(int64_t v, uint8_t scale) {
+    if (scale == 0) return std::to_string(v);
+    const bool neg = v < 0;
+    uint64_t a = neg ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    uint64_t p = 1;
+    for (int i = 0; i < scale; ++i) p *= 10;
+    string frac = std::to_string(a % p);
+    frac.insert(0, scale - frac.size(), '0');
+    return (neg ? "-" : "") + std::to_string(a / p) + "." + frac;
+}
+
+// DuckDB prints doubles with the shortest round-tripping representation
+string double_to_string(double v) {
+    char buf[64];
+    for (int prec = 1; prec <= 17; ++prec) {
+        snprintf(buf, sizeof(buf), "%.*g", prec, v);
+        if (strtod(buf, nullptr) == v) break;
+    }
+    return buf;
+}
+
+}  // namespace
+
+string Value::ToString() const {
+    if (is_null_) return "NULL";
+    switch (type_.id()) {
+    case LogicalTypeId::VARCHAR: return str_;
+    case LogicalTypeId::BOOLEAN: return int_ ? "true" : "false";
+    case LogicalTypeId::UBIGINT: return std::to_string((uint64_t)int_);
+    case LogicalTypeId::DATE: return date_to_string((int32_t)int_);
+    case LogicalTypeId::DECIMAL: return decimal_to_string(int_, type_.Scale());
+    case LogicalTypeId::FLOAT: return double_to_string((float)dbl_);
+    case LogicalTypeId::DOUBLE: return double_to_string(dbl_);
+    case LogicalTypeId::LIST: {
+        string s = "[";
+        for (size_t i = 0; i < list_.size(); ++i) s += (i ? ", " : "") + list_[i].ToString();
+        return s + "]";
+    }
+    default: return std::to_string(int_);
+    }
+}
+
+Vector::Vector(LogicalType type, idx_t capacity)
+    : type_(std::move(type)), capacity_(capacity), data_(capacity * type_.PhysicalSize(), 0), valid_(capacity, true) {}
+
+void Vector::Reset() {
+    std::fill(valid_.begin(), valid_.end(), true);
+    heap_.clear();
+    keep_.clear();
+    vtype_ = VectorType::FLAT_VECTOR;
+}
+
+string_t Vector::AddString(const string &s) {
+    if (s.size() <= string_t::INLINE_LENGTH) return string_t(s.data(), (uint32_t)s.size());
+    heap_.push_back(s);
+    return string_t(heap_.back().data(), (uint32_t)heap_.back().size());
+}
+
+void Vector::SetValue(idx_t i, const Value &v) {
+    if (i >= capacity_) throw InternalException("Vector::SetValue out of range");
+    if (v.IsNull()) {
+        valid_[i] = false;
+        return;
+    }
+    valid_[i] = true;
+    uint8_t *p = data_.data() + i * type_.PhysicalSize();
+    switch (type_.id()) {
+    case LogicalTypeId::VARCHAR: {
+        // implicit cast to VARCHAR, as DuckDB's Vector::SetValue does
+        string_t s = AddString(v.GetValue<string>());
+        memcpy(p, &s, sizeof(s));
+        break;
+    }
+    case LogicalTypeId::FLOAT: { float f = (float)v.GetDouble(); memcpy(p, &f, 4); break; }
+    case LogicalTypeId::DOUBLE: { double d = v.GetDouble(); memcpy(p, &d, 8); break; }
+    default: {
+        int64_t x = v.GetInt64();
+        memcpy(p, &x, type_.PhysicalSize());
+    }
+    }
+}
+
+Value Vector::GetValue(idx_t i) const {
+    if (!valid_[i]) return Value();
+    const uint8_t *p = data_.data() + i * type_.PhysicalSize();
+    auto ld = [p](auto x) { memcpy(&x, p, sizeof(x)); return x; };
+    switch (type_.id()) {
+    case LogicalTypeId::VARCHAR: return Value(ld(string_t()).GetString());
+    case LogicalTypeId::TINYINT: return Value::TINYINT(ld(int8_t()));
+    case LogicalTypeId::SMALLINT: return Value::SMALLINT(ld(int16_t()));
+    case LogicalTypeId::INTEGER: return Value::INTEGER(ld(int32_t()));
+    case LogicalTypeId::BIGINT: return Value::BIGINT(ld(int64_t()));
+    case LogicalTypeId::UTINYINT: return Value::UTINYINT(ld(uint8_t()));
+    case LogicalTypeId::USMALLINT: return Value::USMALLINT(ld(uint16_t()));
+    case LogicalTypeId::UINTEGER: return Value::UINTEGER(ld(uint32_t()));
+    case LogicalTypeId::UBIGINT: return Value::UBIGINT(ld(uint64_t()));
+    case LogicalTypeId::DATE: return Value::DATE(date_t{ld(int32_t())});
+    case LogicalTypeId::FLOAT: return Value::FLOAT(ld(float()));
+    case LogicalTypeId::DOUBLE: return Value::DOUBLE(ld(double()));
+    case LogicalTypeId::DECIMAL: {
+        const idx_t w = type_.PhysicalSize();
+        int64_t x = w == 2 ? ld(int16_t()) : w == 4 ? ld(int32_t()) : ld(int64_t());
+        return Value::DECIMAL(x, type_.Width(), type_.Scale());
+    }
+    default: return Value();
+    }
+}
+
+DBConfig &DBConfig::GetConfig(DatabaseInstance &db) { return db.config; }
+
+string StringUtil::Lower(const string &s) {
+    string r(s);
+    std::transform(r.begin(), r.end(), r.begin(), [](unsigned char c) { return (char)std::tolower(c); });
+    return r;
+}
+
+}  // namespace duckdb
