@@ -1,207 +1,250 @@
-// fls_decode.hip -- MI355X (gfx950) FastLanes vector decode.
+// fls_decode.hip -- MI355X (gfx950) FastLanes vector decode, pipelined (v2).
 //
 // Replaces the decode inside RowgroupReader::materialize()
 // (reference src/fastlanes_facade.cpp:48) for the north-star codecs:
 // interleaved bit-unpack at every width, FFOR, unified-transposed DELTA,
 // DICT gather (integers and DuckDB string_t) and FastLanes-RLE.
 //
-// Work decomposition: one 64-lane wave decodes one 1024-value vector.
-//   1. stage: the vector's 128*W packed bytes are streamed HBM -> LDS with
-//      16 B/lane loads (1 KiB per wave-instruction), plus one zero word-row;
-//   2. unpack: lane handles 16-byte "chunks" ci (row R = ci/8, 16-byte column
-//      qc = ci%8 of the 128-byte word-row).  For any T the chunk's values are
-//      a funnel shift of word-rows k = R*W/T and k+1 (two ds_read_b128),
-//      computed with v_alignbit (T=32/64) or SWAR shifts (T=8/16), then masked;
-//      bit width W is a runtime, wave-uniform value (no 124-way template
-//      explosion, no runtime-indexed register arrays);
-//   3. FFOR stores chunk ci straight to output bytes [16ci, 16ci+16): the 64
-//      lanes of one store instruction write 1 KiB contiguously;
-//      DELTA / RLE scatter the chunk into LDS at its transposed position, scan
-//      the 1024/T lane chains (16 serial steps per lane + a wave shuffle across
-//      chain segments), add the lane bases and copy out with 16 B/lane stores;
-//      DICT / RLE gather through the dictionary / run values and store
-//      16 B/lane.
+// Work decomposition
+//   * a 64-lane wave owns whole column chunks (one column of one row group,
+//     <= 64 vectors), walking them grid-stride so every wave sees every column;
+//   * per chunk the 64 VecMeta records are loaded once, one per lane, and
+//     read with v_readlane when needed (no dependent metadata load per vector);
+//   * the chunk's (encoding, T, output width) selects a templated inner loop, so
+//     each loop body has a fixed instruction sequence and hipcc can count
+//     vmcnt exactly;
+//   * software pipeline, depth 1: while vector v is unpacked and stored, the
+//     packed bits (and DELTA lane bases) of vector v+1 are already in flight
+//     into registers.  gfx950's vmcnt counts stores and loads in issue order, so
+//     the prefetch is issued BEFORE v's stores: the wait for v+1's data never
+//     waits for v's stores;
+//   * unpack: a lane handles 16-byte chunks ci (row R = ci/8, 16-byte column
+//     qc = ci%8 of the 128-byte word-row) = funnel shift of word-rows R*W/T and
+//     +1 (two ds_read_b128 from the staged LDS copy); W is runtime/uniform;
+//   * FFOR stores chunk ci straight to output bytes [16ci, 16ci+16): one store
+//     instruction writes 1 KiB contiguously;
+//   * DELTA T=64 (BIGINT keys) is scanned entirely in registers: after the
+//     unpack a lane already holds 8 consecutive steps of 2 chains (segment
+//     FL_ORDER[lane/8]); in-lane prefix + a 3-step ds_bpermute scan across the
+//     8 segments + lane bases -> 8 x 16 B stores (128 B lines);
+//   * DELTA T<64 and RLE indices scatter into LDS at their transposed position
+//     and scan the 1024/T chains there; DICT codes go through LDS and gather
+//     from the dictionary (staged in LDS when small) with 16 B/lane stores.
 // The path is HBM-bound integer work: no MFMA.
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "fls_decode.hpp"
 #include "fls_format.hpp"
+#include "fls_unpack.hpp"
 
 namespace fls {
 namespace {
+using namespace dev;
 
-constexpr int kWaves = 4;                         // waves per 256-thread block
-constexpr int kPackedU4 = (128 * 64 + 128) / 16;  // max packed bytes (T=64,W=64) + pad row
-constexpr int kValBytes = 1024 * 8;               // max decoded vector (T=64)
+constexpr int kWaves = 4;  // waves per 256-thread block
 
-__device__ __forceinline__ void wave_sync() {
-    // one wave talks to itself through LDS: DS ops of a wave execute in order;
-    // the fences stop the compiler from moving LDS accesses across.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// address-space qualified views (global = 1, LDS = 3): see fls_unpack.hpp
+using gv4 = const FLS_GLOBAL v4u;
+using gu8 = const FLS_GLOBAL uint8_t;
+using ov4 = FLS_GLOBAL v4u;
+using ou8 = FLS_GLOBAL uint8_t;
+using lv4 = FLS_LDS v4u;
+using lu8 = FLS_LDS uint8_t;
 
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-
-__device__ __forceinline__ uint32_t tau(uint32_t p) {
-    // FL_ORDER = {0,4,2,6,1,5,3,7} is the 3-bit bit reversal
-    const uint32_t b = (p >> 4) & 7;
-    const uint32_t rb = ((b & 1) << 2) | (b & 2) | ((b >> 2) & 1);
-    return (rb << 7) | (((p >> 7) & 7) << 4) | (p & 15);
-}
-
-// ---- unpack one 16-byte chunk of T-bit values ------------------------------
 template <int T>
-__device__ __forceinline__ uint4 unpack_chunk(const uint4 *__restrict__ P, uint32_t W, uint32_t ci);
+struct UInt;
+template <> struct UInt<8> { using type = uint8_t; };
+template <> struct UInt<16> { using type = uint16_t; };
+template <> struct UInt<32> { using type = uint32_t; };
+template <> struct UInt<64> { using type = uint64_t; };
 
-template <>
-__device__ __forceinline__ uint4 unpack_chunk<32>(const uint4 *__restrict__ P, uint32_t W, uint32_t ci) {
-    const uint32_t R = ci >> 3, qc = ci & 7;
-    const uint32_t bit = R * W, k = bit >> 5, s = bit & 31;
-    const uint4 lo = P[k * 8 + qc], hi = P[(k + 1) * 8 + qc];
-    const uint32_t m = W >= 32 ? 0xFFFFFFFFu : ((1u << W) - 1u);
-    uint4 r;
-    r.x = __builtin_amdgcn_alignbit(hi.x, lo.x, s) & m;
-    r.y = __builtin_amdgcn_alignbit(hi.y, lo.y, s) & m;
-    r.z = __builtin_amdgcn_alignbit(hi.z, lo.z, s) & m;
-    r.w = __builtin_amdgcn_alignbit(hi.w, lo.w, s) & m;
-    return r;
-}
+__device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+// keep unrolled iterations in program order: bounds register pressure to one
+// iteration (the occupancy, not the ILP of one wave, hides latency here)
+__device__ __forceinline__ void seq() { __builtin_amdgcn_sched_barrier(0); }
+__device__ __forceinline__ uint32_t bitrev3(uint32_t g) { return ((g & 1) << 2) | (g & 2) | ((g >> 2) & 1); }
 
-template <>
-__device__ __forceinline__ uint4 unpack_chunk<64>(const uint4 *__restrict__ P, uint32_t W, uint32_t ci) {
-    const uint32_t R = ci >> 3, qc = ci & 7;
-    const uint32_t bit = R * W, k = bit >> 6, s = bit & 63, s5 = s & 31;
-    const uint4 lo = P[k * 8 + qc], hi = P[(k + 1) * 8 + qc];
-    const bool big = s >= 32;
-    const uint32_t mlo = W >= 32 ? 0xFFFFFFFFu : ((1u << W) - 1u);
-    const uint32_t mhi = W >= 64 ? 0xFFFFFFFFu : (W > 32 ? ((1u << (W - 32)) - 1u) : 0u);
-    uint4 r;
-    // lane 0 = (lo.y:lo.x), next word row (hi.y:hi.x); lane 1 = (.w:.z)
-    r.x = __builtin_amdgcn_alignbit(big ? hi.x : lo.y, big ? lo.y : lo.x, s5) & mlo;
-    r.y = __builtin_amdgcn_alignbit(big ? hi.y : hi.x, big ? hi.x : lo.y, s5) & mhi;
-    r.z = __builtin_amdgcn_alignbit(big ? hi.z : lo.w, big ? lo.w : lo.z, s5) & mlo;
-    r.w = __builtin_amdgcn_alignbit(big ? hi.w : hi.z, big ? hi.z : lo.w, s5) & mhi;
-    return r;
-}
-
-// SWAR funnel shift of packed 16-bit (or 8-bit) words inside a dword
-template <int T>
-__device__ __forceinline__ uint32_t swar_funnel(uint32_t lo, uint32_t hi, uint32_t s, uint32_t m1, uint32_t m2,
-                                                uint32_t mw) {
-    return (((lo >> s) & m1) | ((hi << (T - s)) & m2)) & mw;
-}
-
-template <>
-__device__ __forceinline__ uint4 unpack_chunk<16>(const uint4 *__restrict__ P, uint32_t W, uint32_t ci) {
-    const uint32_t R = ci >> 3, qc = ci & 7;
-    const uint32_t bit = R * W, k = bit >> 4, s = bit & 15;
-    const uint4 lo = P[k * 8 + qc], hi = P[(k + 1) * 8 + qc];
-    const uint32_t rep = 0x00010001u;
-    const uint32_t m1 = rep * (0xFFFFu >> s);
-    const uint32_t m2 = rep * ((0xFFFFu << (16 - s)) & 0xFFFFu);
-    const uint32_t mw = W >= 16 ? 0xFFFFFFFFu : rep * ((1u << W) - 1u);
-    uint4 r;
-    r.x = swar_funnel<16>(lo.x, hi.x, s, m1, m2, mw);
-    r.y = swar_funnel<16>(lo.y, hi.y, s, m1, m2, mw);
-    r.z = swar_funnel<16>(lo.z, hi.z, s, m1, m2, mw);
-    r.w = swar_funnel<16>(lo.w, hi.w, s, m1, m2, mw);
-    return r;
-}
-
-template <>
-__device__ __forceinline__ uint4 unpack_chunk<8>(const uint4 *__restrict__ P, uint32_t W, uint32_t ci) {
-    const uint32_t R = ci >> 3, qc = ci & 7;
-    const uint32_t bit = R * W, k = bit >> 3, s = bit & 7;
-    const uint4 lo = P[k * 8 + qc], hi = P[(k + 1) * 8 + qc];
-    const uint32_t rep = 0x01010101u;
-    const uint32_t m1 = rep * (0xFFu >> s);
-    const uint32_t m2 = rep * ((0xFFu << (8 - s)) & 0xFFu);
-    const uint32_t mw = W >= 8 ? 0xFFFFFFFFu : rep * ((1u << W) - 1u);
-    uint4 r;
-    r.x = swar_funnel<8>(lo.x, hi.x, s, m1, m2, mw);
-    r.y = swar_funnel<8>(lo.y, hi.y, s, m1, m2, mw);
-    r.z = swar_funnel<8>(lo.z, hi.z, s, m1, m2, mw);
-    r.w = swar_funnel<8>(lo.w, hi.w, s, m1, m2, mw);
-    return r;
-}
-
-// ---- frame-of-reference add on a 16-byte chunk (wrapping T-bit) ----------
-template <int T>
-__device__ __forceinline__ uint4 add_base(uint4 a, uint64_t base);
-
-template <>
-__device__ __forceinline__ uint4 add_base<64>(uint4 a, uint64_t base) {
-    const uint64_t v0 = (((uint64_t)a.y << 32) | a.x) + base;
-    const uint64_t v1 = (((uint64_t)a.w << 32) | a.z) + base;
-    return make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
-}
-template <>
-__device__ __forceinline__ uint4 add_base<32>(uint4 a, uint64_t base) {
-    const uint32_t b = (uint32_t)base;
-    return make_uint4(a.x + b, a.y + b, a.z + b, a.w + b);
-}
-__device__ __forceinline__ uint32_t swar_add(uint32_t a, uint32_t b, uint32_t hi) {
-    return ((a & ~hi) + (b & ~hi)) ^ ((a ^ b) & hi);
-}
-template <>
-__device__ __forceinline__ uint4 add_base<16>(uint4 a, uint64_t base) {
-    const uint32_t b = 0x00010001u * (uint32_t)(base & 0xFFFF), hi = 0x80008000u;
-    return make_uint4(swar_add(a.x, b, hi), swar_add(a.y, b, hi), swar_add(a.z, b, hi), swar_add(a.w, b, hi));
-}
-template <>
-__device__ __forceinline__ uint4 add_base<8>(uint4 a, uint64_t base) {
-    const uint32_t b = 0x01010101u * (uint32_t)(base & 0xFF), hi = 0x80808080u;
-    return make_uint4(swar_add(a.x, b, hi), swar_add(a.y, b, hi), swar_add(a.z, b, hi), swar_add(a.w, b, hi));
-}
-
-// ---- stores with tail guard ----------------------------------------------
-// store 16 bytes at out + off, or only the bytes below `limit`
-template <int EB>  // element bytes for the partial path
-__device__ __forceinline__ void store16(uint8_t *__restrict__ out, uint32_t off, uint32_t limit, uint4 v) {
-    if (off + 16 <= limit) {
-        *reinterpret_cast<uint4 *>(out + off) = v;
-        return;
+// per-lane copy of the chunk's VecMeta[lane]
+struct ChunkMetas {
+    uint32_t poff, blo, bhi, aoff, nvbw, acnt;
+};
+__device__ __forceinline__ ChunkMetas load_metas(const DevChunk &c, uint32_t lane) {
+    ChunkMetas m{0, 0, 0, 0, 0, 0};
+    if (lane < c.nvec) {
+        gv4 *p = reinterpret_cast<gv4 *>(gptr(c.chunk) + c.meta_off) + 2 * lane;
+        const v4u a = p[0], b = p[1];
+        m.poff = a.x;
+        m.blo = a.z;
+        m.bhi = a.w;
+        m.aoff = b.x;
+        m.nvbw = b.z;
+        m.acnt = b.w;
     }
-    if (off >= limit) return;
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    return m;
+}
+
+struct VecInfo {
+    uint32_t poff16;   // packed offset (uint4 units) inside the packed area
+    uint32_t W, nvals, aoff, acount;
+    uint64_t base;
+};
+__device__ __forceinline__ VecInfo vec_info(const ChunkMetas &m, uint32_t v) {
+    VecInfo x;
+    x.poff16 = rl(m.poff, v) >> 4;
+    x.base = ((uint64_t)rl(m.bhi, v) << 32) | rl(m.blo, v);
+    x.aoff = rl(m.aoff, v);
+    const uint32_t nb = rl(m.nvbw, v);
+    x.nvals = nb & 0xFFFF;
+    x.W = (nb >> 16) & 0xFF;
+    x.acount = rl(m.acnt, v);
+    return x;
+}
+
+// ---- packed-bit prefetch (registers) and staging (LDS) --------------------
+// L = T/8 = max uint4 per lane (W <= T -> 8W <= 8T uint4 per vector).  Every
+// lane issues exactly L loads (out-of-range lanes re-read a safe dummy line)
+// so the loop body's vmcnt arithmetic is static.
+template <int L>
+__device__ __forceinline__ void prefetch(gv4 *__restrict__ src, uint32_t n16, gv4 *__restrict__ dummy,
+                                         uint32_t lane, v4u (&r)[L]) {
 #pragma unroll
-    for (int e = 0; e < 16 / EB; ++e) {
-        const uint32_t o = off + e * EB;
-        if (o < limit) {
-            if (EB == 8) {
-                *reinterpret_cast<uint64_t *>(out + o) = ((uint64_t)w[2 * e + 1] << 32) | w[2 * e];
-            } else if (EB == 4) {
-                *reinterpret_cast<uint32_t *>(out + o) = w[e];
-            } else if (EB == 2) {
-                *reinterpret_cast<uint16_t *>(out + o) = (uint16_t)(w[e / 2] >> (16 * (e & 1)));
-            } else {
-                out[o] = (uint8_t)(w[e / 4] >> (8 * (e & 3)));
-            }
+    for (int i = 0; i < L; ++i) {
+        const uint32_t idx = lane + 64 * i;
+        r[i] = *(idx < n16 ? src + idx : dummy);
+    }
+}
+template <int L>
+__device__ __forceinline__ void stage(lv4 *__restrict__ P, const v4u (&r)[L], uint32_t n16, uint32_t lane) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const uint32_t idx = lane + 64 * i;
+        if (idx < n16) P[idx] = r[i];
+    }
+    if (lane < 8) P[n16 + lane] = mk4(0, 0, 0, 0);
+}
+
+// ---- per-path vector processing ---------------------------------------------
+// Each path: aux prefetch (registers, issued with the packed prefetch) and
+// vec<FULL>(...) writing one vector; FULL=false guards the partial tail.
+
+struct NoAux {
+    __device__ __forceinline__ void load(gu8 *, uint32_t) {}
+};
+
+template <int T, bool FULL>
+__device__ __forceinline__ void ffor_vec(const lv4 *__restrict__ P, uint32_t W, uint64_t base, ou8 *__restrict__ out,
+                                         uint32_t nvals, uint32_t lane) {
+    const uint32_t limit = nvals * (T / 8);
+#pragma unroll
+    for (uint32_t j = 0; j < T / 8; ++j) {
+        const uint32_t ci = lane + 64 * j;
+        const v4u v = add_base<T>(unpack_chunk<T>(P, W, ci), base);
+        if (FULL) reinterpret_cast<ov4 *>(out)[ci] = v;
+        else store16<T / 8>(out, 16 * ci, limit, v);
+        seq();
+    }
+}
+
+// DELTA T=64 bases: lane q = lane&7 needs chains 2q, 2q+1 -> one 16 B load
+struct Aux64 {
+    v4u b;
+    __device__ __forceinline__ void load(gu8 *bases, uint32_t lane) {
+        b = *reinterpret_cast<gv4 *>(bases + 16 * (lane & 7));
+    }
+};
+
+template <bool FULL>
+__device__ __forceinline__ void delta64_vec(const lv4 *__restrict__ P, uint32_t W, uint64_t base, const Aux64 &aux,
+                                            ou8 *__restrict__ out, uint32_t nvals, uint32_t lane) {
+    // chunk ci = lane + 64 j holds positions p = 16 R + 2q + e with R = g + 8 j
+    // (g = lane>>3, q = lane&7): tuple 16 (8 FL[g] + j) + 2q + e, i.e. steps
+    // 8 FL[g] + j of chains 2q, 2q+1 -- a contiguous 8-step segment s = FL[g].
+    const uint32_t g = lane >> 3, q = lane & 7, s = bitrev3(g);
+    uint64_t a0[8], a1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const v4u x = add_base<64>(unpack_chunk<64>(P, W, lane + 64 * j), base);
+        a0[j] = ((uint64_t)x.y << 32) | x.x;
+        a1[j] = ((uint64_t)x.w << 32) | x.z;
+        seq();
+    }
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+        a0[j] += a0[j - 1];
+        a1[j] += a1[j - 1];
+    }
+    // inclusive scan of segment totals in segment order; segment t lives in
+    // lane group FL[t] (FL is an involution)
+    uint64_t x0 = a0[7], x1 = a1[7];
+#pragma unroll
+    for (uint32_t d = 1; d < 8; d <<= 1) {
+        const uint32_t src = 8 * bitrev3((s - d) & 7) + q;
+        const uint64_t y0 = __shfl((unsigned long long)x0, (int)src, 64);
+        const uint64_t y1 = __shfl((unsigned long long)x1, (int)src, 64);
+        if (s >= d) {
+            x0 += y0;
+            x1 += y1;
         }
     }
+    const uint64_t p0 = x0 - a0[7] + (((uint64_t)aux.b.y << 32) | aux.b.x);
+    const uint64_t p1 = x1 - a1[7] + (((uint64_t)aux.b.w << 32) | aux.b.z);
+    const uint32_t limit = nvals * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint64_t v0 = p0 + a0[j], v1 = p1 + a1[j];
+        const v4u v = mk4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
+        const uint32_t off = 128 * (8 * s + j) + 16 * q;
+        if (FULL) *reinterpret_cast<ov4 *>(out + off) = v;
+        else store16<8>(out, off, limit, v);
+    }
 }
 
-// ---- LDS chain scan (DELTA / RLE index) -------------------------------------
-// vals: 1024 T-bit deltas in tuple order (LDS).  bases: 1024/T chain bases
-// (global).  In place: vals[i] = base[chain] + sum of the chain's deltas <= i.
+// DELTA T<64 / RLE index bases: lane's chain(s) base(s), loaded as registers
 template <int T>
-__device__ __forceinline__ void chain_scan(uint8_t *__restrict__ V, const uint8_t *__restrict__ bases, uint32_t lane) {
-    using UT = typename std::conditional<T == 64, uint64_t,
-               typename std::conditional<T == 32, uint32_t,
-               typename std::conditional<T == 16, uint16_t, uint8_t>::type>::type>::type;
-    UT *v = reinterpret_cast<UT *>(V);
-    const UT *b = reinterpret_cast<const UT *>(bases);
+struct AuxSmall {
+    uint32_t b0, b1;
+    __device__ __forceinline__ void load(gu8 *bases, uint32_t lane) {
+        if (T == 32) {
+            b0 = reinterpret_cast<const FLS_GLOBAL uint32_t *>(bases)[lane & 31];
+        } else if (T == 16) {
+            b0 = reinterpret_cast<const FLS_GLOBAL uint16_t *>(bases)[lane];
+        } else {
+            b0 = bases[lane];
+            b1 = bases[lane + 64];
+        }
+    }
+};
+
+// unpack + base into LDS at transposed (DELTA/RLE) or natural (DICT) position
+template <int T, bool TRANSPOSED>
+__device__ __forceinline__ void unpack_to_lds(const lv4 *__restrict__ P, uint32_t W, uint64_t base,
+                                              lu8 *__restrict__ V, uint32_t lane) {
+#pragma unroll
+    for (uint32_t j = 0; j < T / 8; ++j) {
+        const uint32_t ci = lane + 64 * j;
+        const v4u v = add_base<T>(unpack_chunk<T>(P, W, ci), base);
+        const uint32_t p0 = ci * (128 / T);
+        const uint32_t i0 = TRANSPOSED ? tau(p0) : p0;
+        *reinterpret_cast<lv4 *>(V + i0 * (T / 8)) = v;
+        seq();
+    }
+}
+
+// in-place chain scan in LDS (T = 8/16/32); bases from registers
+template <int T>
+__device__ __forceinline__ void chain_scan_lds(lu8 *__restrict__ V, const AuxSmall<T> &aux, uint32_t lane) {
+    using UT = typename UInt<T>::type;
+    FLS_LDS UT *v = reinterpret_cast<FLS_LDS UT *>(V);
     if (T == 8) {
-        // 128 chains of 8 steps: two chains per lane
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t c = lane + 64 * h;
             const uint32_t i0 = (c >> 4) * 128 + (c & 15);
-            UT acc = b[c];
+            UT acc = (UT)(h ? aux.b1 : aux.b0);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 acc = (UT)(acc + v[i0 + 16 * k]);
@@ -210,7 +253,7 @@ __device__ __forceinline__ void chain_scan(uint8_t *__restrict__ V, const uint8_
         }
         return;
     }
-    constexpr uint32_t nchains = 1024 / T;  // 16, 32, 64
+    constexpr uint32_t nchains = 1024 / T;  // 32 or 64
     const uint32_t c = lane % nchains, seg = lane / nchains;
     const uint32_t i0 = (c >> 4) * 16 * T + (c & 15) + 256 * seg;
     UT run[16];
@@ -220,202 +263,348 @@ __device__ __forceinline__ void chain_scan(uint8_t *__restrict__ V, const uint8_
         acc = (UT)(acc + v[i0 + 16 * j]);
         run[j] = acc;
     }
-    // exclusive prefix of segment totals across the lanes of one chain
-    uint64_t tot = (uint64_t)acc, x = tot;
-    if (nchains <= 32) {  // T >= 32: >= 2 segments
-        uint64_t y = __shfl_up((unsigned long long)x, nchains, 64);
-        if (seg >= 1) x += y;
-        if (nchains == 16) {
-            y = __shfl_up((unsigned long long)x, 32, 64);
-            if (seg >= 2) x += y;
-        }
+    uint32_t pre = 0;
+    if (nchains == 32) {  // two 16-step segments per chain
+        const uint32_t y = __shfl_up((uint32_t)acc, 32, 64);
+        pre = seg ? y : 0u;
     }
-    const UT pre = (UT)((x - tot) + (uint64_t)b[c]);
+    const UT p = (UT)(pre + aux.b0);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[i0 + 16 * j] = (UT)(pre + run[j]);
+    for (int j = 0; j < 16; ++j) v[i0 + 16 * j] = (UT)(p + run[j]);
 }
 
-// copy the decoded vector (tuple order, EB bytes each) from LDS to HBM
-template <int EB>
-__device__ __forceinline__ void copy_out(const uint8_t *__restrict__ V, uint8_t *__restrict__ out, uint32_t nvals,
+// 16 B/lane copy of a decoded vector (tuple order, EB bytes each) LDS -> HBM
+template <int EB, bool FULL>
+__device__ __forceinline__ void copy_out(const lu8 *__restrict__ V, ou8 *__restrict__ out, uint32_t nvals,
                                          uint32_t lane) {
     const uint32_t limit = nvals * EB;
 #pragma unroll
-    for (uint32_t ci = lane; ci < 64 * EB; ci += 64) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(V + 16 * ci);
-        store16<EB>(out, 16 * ci, limit, x);
+    for (uint32_t j = 0; j < EB; ++j) {
+        const uint32_t ci = lane + 64 * j;
+        const v4u x = *reinterpret_cast<const lv4 *>(V + 16 * ci);
+        if (FULL) reinterpret_cast<ov4 *>(out)[ci] = x;
+        else store16<EB>(out, 16 * ci, limit, x);
+        seq();
     }
 }
 
-// gather values through a table and store 16 B/lane.  idx(i) yields the
-// table index of tuple i, tab holds OB-byte entries.
-template <int OB, typename IdxF>
-__device__ __forceinline__ void gather_out(const uint8_t *__restrict__ tab, uint8_t *__restrict__ out, uint32_t nvals,
-                                           uint32_t lane, IdxF idx) {
+// gather OB-byte table entries by index and store 16 B/lane
+template <int OB, bool FULL, typename TabF, typename IdxF>
+__device__ __forceinline__ void gather_out(TabF tab, ou8 *__restrict__ out, uint32_t nvals, uint32_t lane, IdxF idx) {
     const uint32_t limit = nvals * OB;
     constexpr int per = 16 / OB;
 #pragma unroll
-    for (uint32_t oc = lane; oc < 64 * OB; oc += 64) {
+    for (uint32_t j = 0; j < OB; ++j) {
+        const uint32_t oc = lane + 64 * j;
         uint32_t w[4] = {0, 0, 0, 0};
         if (OB == 16) {
-            const uint4 e = reinterpret_cast<const uint4 *>(tab)[idx(oc)];
+            const v4u e = tab.v16(idx(oc));
             w[0] = e.x; w[1] = e.y; w[2] = e.z; w[3] = e.w;
         } else {
 #pragma unroll
             for (int e = 0; e < per; ++e) {
                 const uint32_t t = idx(oc * per + e);
                 if (OB == 8) {
-                    const uint64_t x = reinterpret_cast<const uint64_t *>(tab)[t];
+                    const uint64_t x = tab.u64(t);
                     w[2 * e] = (uint32_t)x;
                     w[2 * e + 1] = (uint32_t)(x >> 32);
                 } else if (OB == 4) {
-                    w[e] = reinterpret_cast<const uint32_t *>(tab)[t];
+                    w[e] = tab.u32(t);
                 } else if (OB == 2) {
-                    w[e / 2] |= (uint32_t)reinterpret_cast<const uint16_t *>(tab)[t] << (16 * (e & 1));
+                    w[e / 2] |= tab.u16(t) << (16 * (e & 1));
                 } else {
-                    w[e / 4] |= (uint32_t)tab[t] << (8 * (e & 3));
+                    w[e / 4] |= tab.u8(t) << (8 * (e & 3));
                 }
             }
         }
-        store16<OB == 16 ? 8 : OB>(out, 16 * oc, limit, make_uint4(w[0], w[1], w[2], w[3]));
+        const v4u v = mk4(w[0], w[1], w[2], w[3]);
+        if (FULL) reinterpret_cast<ov4 *>(out)[oc] = v;
+        else store16<OB == 16 ? 8 : OB>(out, 16 * oc, limit, v);
+        seq();
     }
 }
 
-struct VecCtx {
-    const uint4 *P;       // staged packed bits (LDS)
-    uint8_t *V;           // decoded vector scratch (LDS)
-    uint32_t W, nvals, lane;
-    uint64_t base;
+// table readers over an address space AS (LDS-staged or global dictionary)
+#define FLS_DEFINE_TAB(NAME, AS)                                                                          \
+    struct NAME {                                                                                         \
+        const AS uint8_t *p;                                                                              \
+        __device__ __forceinline__ v4u v16(uint32_t i) const { return reinterpret_cast<const AS v4u *>(p)[i]; } \
+        __device__ __forceinline__ uint64_t u64(uint32_t i) const {                                      \
+            return reinterpret_cast<const AS uint64_t *>(p)[i];                                           \
+        }                                                                                                 \
+        __device__ __forceinline__ uint32_t u32(uint32_t i) const {                                      \
+            return reinterpret_cast<const AS uint32_t *>(p)[i];                                           \
+        }                                                                                                 \
+        __device__ __forceinline__ uint32_t u16(uint32_t i) const {                                      \
+            return reinterpret_cast<const AS uint16_t *>(p)[i];                                           \
+        }                                                                                                 \
+        __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }                         \
+    };
+FLS_DEFINE_TAB(TabL, FLS_LDS)
+FLS_DEFINE_TAB(TabG, FLS_GLOBAL)
+#undef FLS_DEFINE_TAB
+
+// ---- the pipelined chunk loop ------------------------------------------------
+struct Lds {
+    lv4 *P;          // packed staging (p_bytes)
+    lu8 *V;          // decoded scratch; DICT: codes [0,4K) + staged dictionary
+    uint32_t v_bytes;
 };
 
-// FFOR: unpack + base, straight to HBM
-template <int T>
-__device__ __forceinline__ void do_ffor(const VecCtx &x, uint8_t *__restrict__ out) {
-    const uint32_t limit = x.nvals * (T / 8);
-#pragma unroll
-    for (uint32_t ci = x.lane; ci < 8 * T; ci += 64) {
-        const uint4 v = add_base<T>(unpack_chunk<T>(x.P, x.W, ci), x.base);
-        store16<T / 8>(out, 16 * ci, limit, v);
+// Path concept: T (packing width), Aux (registers prefetched with the packed
+// bits), aux_ptr(chunk, vec), template<bool FULL> vec(...).
+template <int T_>
+struct PathFfor {
+    __device__ __forceinline__ PathFfor(const DevChunk &, const Lds &, uint32_t, uint32_t *) {}
+    static constexpr int T = T_;
+    using Aux = NoAux;
+    __device__ __forceinline__ gu8 *aux_ptr(const DevChunk &, const VecInfo &) const { return nullptr; }
+    template <bool FULL>
+    __device__ __forceinline__ void vec(const Lds &s, const VecInfo &x, const Aux &, ou8 *out, uint32_t lane) const {
+        ffor_vec<T, FULL>(s.P, x.W, x.base, out, x.nvals, lane);
+    }
+};
+
+struct PathDelta64 {
+    __device__ __forceinline__ PathDelta64(const DevChunk &, const Lds &, uint32_t, uint32_t *) {}
+    static constexpr int T = 64;
+    using Aux = Aux64;
+    __device__ __forceinline__ gu8 *aux_ptr(const DevChunk &c, const VecInfo &x) const {
+        return gptr(c.chunk) + c.aux_off + x.aoff;
+    }
+    template <bool FULL>
+    __device__ __forceinline__ void vec(const Lds &s, const VecInfo &x, const Aux &a, ou8 *out, uint32_t lane) const {
+        delta64_vec<FULL>(s.P, x.W, x.base, a, out, x.nvals, lane);
+    }
+};
+
+template <int T_>
+struct PathDeltaSmall {
+    __device__ __forceinline__ PathDeltaSmall(const DevChunk &, const Lds &, uint32_t, uint32_t *) {}
+    static constexpr int T = T_;
+    using Aux = AuxSmall<T_>;
+    __device__ __forceinline__ gu8 *aux_ptr(const DevChunk &c, const VecInfo &x) const {
+        return gptr(c.chunk) + c.aux_off + x.aoff;
+    }
+    template <bool FULL>
+    __device__ __forceinline__ void vec(const Lds &s, const VecInfo &x, const Aux &a, ou8 *out, uint32_t lane) const {
+        unpack_to_lds<T, true>(s.P, x.W, x.base, s.V, lane);
+        wave_sync();
+        chain_scan_lds<T>(s.V, a, lane);
+        wave_sync();
+        copy_out<T / 8, FULL>(s.V, out, x.nvals, lane);
+    }
+};
+
+template <int OB, bool STAGED>
+struct PathDict {
+    static constexpr int T = 32;
+    using Aux = NoAux;
+    using Tab = typename std::conditional<STAGED, TabL, TabG>::type;
+    Tab tab;              // LDS-staged or global dictionary (OB-byte entries)
+    uint32_t count;
+    uint32_t *err;
+    __device__ __forceinline__ PathDict(const DevChunk &c, const Lds &s, uint32_t lane, uint32_t *e)
+        : count(c.dict_count), err(e) {
+        if constexpr (STAGED) {
+            // copy the small dictionary into LDS (V + 4 KiB): the gather stays on-chip
+            const uint32_t bytes = c.dict_count * OB;
+            lv4 *dst = reinterpret_cast<lv4 *>(s.V + 4096);
+            gu8 *src = gptr(c.dict);
+            if (((uintptr_t)c.dict & 15) == 0) {
+                for (uint32_t i = lane; i < (bytes + 15) / 16; i += 64) dst[i] = reinterpret_cast<gv4 *>(src)[i];
+            } else {
+                for (uint32_t i = lane; i < bytes; i += 64) s.V[4096 + i] = src[i];
+            }
+            wave_sync();
+            tab.p = s.V + 4096;
+        } else {
+            tab.p = gptr(c.dict);
+        }
+    }
+    __device__ __forceinline__ gu8 *aux_ptr(const DevChunk &, const VecInfo &) const { return nullptr; }
+    template <bool FULL>
+    __device__ __forceinline__ void vec(const Lds &s, const VecInfo &x, const Aux &, ou8 *out, uint32_t lane) const {
+        unpack_to_lds<32, false>(s.P, x.W, x.base, s.V, lane);
+        wave_sync();
+        const FLS_LDS uint32_t *codes = reinterpret_cast<const FLS_LDS uint32_t *>(s.V);
+        const uint32_t n = count;
+        bool bad = false;
+        gather_out<OB, FULL>(tab, out, x.nvals, lane, [&](uint32_t i) {
+            uint32_t k = codes[i];
+            if (k >= n) { bad = true; k = n - 1; }
+            return k;
+        });
+        if (bad) atomicOr(err, KERR_DICT_CODE);
+    }
+};
+
+template <int OB>
+struct PathRle {
+    static constexpr int T = 16;
+    using Aux = AuxSmall<16>;
+    gu8 *aux_base;
+    uint32_t *err;
+    __device__ __forceinline__ PathRle(const DevChunk &c, const Lds &, uint32_t, uint32_t *e)
+        : aux_base(gptr(c.chunk) + c.aux_off), err(e) {}
+    __device__ __forceinline__ gu8 *aux_ptr(const DevChunk &ch, const VecInfo &x) const {
+        return gptr(ch.chunk) + ch.aux_off + x.aoff;
+    }
+    template <bool FULL>
+    __device__ __forceinline__ void vec(const Lds &s, const VecInfo &x, const Aux &a, ou8 *out, uint32_t lane) const {
+        unpack_to_lds<16, true>(s.P, x.W, x.base, s.V, lane);
+        wave_sync();
+        chain_scan_lds<16>(s.V, a, lane);
+        wave_sync();
+        const FLS_LDS uint16_t *idx = reinterpret_cast<const FLS_LDS uint16_t *>(s.V);
+        const TabG runs{aux_base + x.aoff + 128};
+        const uint32_t n = x.acount;
+        bool bad = false;
+        gather_out<OB, FULL>(runs, out, x.nvals, lane, [&](uint32_t i) {
+            uint32_t r = idx[i];
+            if (r >= n) { bad = true; r = n - 1; }
+            return r;
+        });
+        if (bad) atomicOr(err, KERR_RUN_INDEX);
+    }
+};
+
+// One out-of-line function per path: each gets its own register allocation
+// (inlined into one switch, hipcc allocated the union of all paths: 292 VGPRs,
+// one wave per SIMD).  Arguments arrive in VGPRs, which a callee must assume
+// divergent, so everything uniform is re-established with readfirstlane.
+template <class Path>
+__device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generic, uint32_t lds_p, uint32_t lds_v,
+                                                    uint32_t v_bytes, uint32_t *err_generic) {
+    const uint64_t cp = (uint64_t)chunk_generic;
+    const FLS_GLOBAL DevChunk *cptr =
+        (const FLS_GLOBAL DevChunk *)((uint64_t)uni((uint32_t)(cp >> 32)) << 32 | uni((uint32_t)cp));
+    DevChunk c;
+    {
+        const FLS_GLOBAL v4u *q = reinterpret_cast<const FLS_GLOBAL v4u *>(cptr);
+        v4u *d = reinterpret_cast<v4u *>(&c);
+        d[0] = q[0];
+        d[1] = q[1];
+        d[2] = q[2];
+        d[3] = q[3];
+    }
+    Lds s;
+    s.P = (lv4 *)(size_t)uni(lds_p);
+    s.V = (lu8 *)(size_t)uni(lds_v);
+    s.v_bytes = uni(v_bytes);
+    const uint64_t ep = (uint64_t)err_generic;
+    uint32_t *err = (uint32_t *)((uint64_t)uni((uint32_t)(ep >> 32)) << 32 | uni((uint32_t)ep));
+    const uint32_t lane = __lane_id();
+    const Path path(c, s, lane, err);
+    constexpr int L = Path::T / 8;
+    using Aux = typename Path::Aux;
+    const uint32_t nvec = c.nvec;
+    const uint32_t ob = c.ob;
+    const ChunkMetas m = load_metas(c, lane);
+    gv4 *packed = reinterpret_cast<gv4 *>(gptr(c.chunk) + c.packed_off);
+    gv4 *dummy = reinterpret_cast<gv4 *>(gptr(c.chunk));
+    ou8 *out = gptr(c.out);
+    const uint32_t last_nvals = rl(m.nvbw, nvec - 1) & 0xFFFF;
+    const uint32_t nfull = last_nvals == kVectorSize ? nvec : nvec - 1;
+
+    v4u r[L];
+    Aux aux, aux_next;
+    VecInfo cur = vec_info(m, 0);
+    prefetch<L>(packed + cur.poff16, 8 * cur.W, dummy, lane, r);
+    aux.load(path.aux_ptr(c, cur), lane);
+    uint32_t v = 0;
+    if (nfull > 0) {
+        // peeled first iteration: the loop header then only sees the steady state
+        stage<L>(s.P, r, 8 * cur.W, lane);
+        VecInfo nxt = vec_info(m, nvec > 1 ? 1 : 0);
+        prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
+        aux_next.load(path.aux_ptr(c, nxt), lane);
+        wave_sync();
+        path.template vec<true>(s, cur, aux, out, lane);
+        cur = nxt;
+        aux = aux_next;
+        for (v = 1; v < nfull; ++v) {
+            wave_sync();
+            stage<L>(s.P, r, 8 * cur.W, lane);
+            nxt = vec_info(m, v + 1 < nvec ? v + 1 : v);
+            prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
+            aux_next.load(path.aux_ptr(c, nxt), lane);
+            wave_sync();
+            path.template vec<true>(s, cur, aux, out + (size_t)v * kVectorSize * ob, lane);
+            cur = nxt;
+            aux = aux_next;
+        }
+    }
+    if (nfull < nvec) {  // partial tail vector (only the last row group of a table)
+        wave_sync();
+        stage<L>(s.P, r, 8 * cur.W, lane);
+        wave_sync();
+        path.template vec<false>(s, cur, aux, out + (size_t)v * kVectorSize * ob, lane);
     }
 }
 
-// unpack + base into LDS at transposed (DELTA) or natural position
-template <int T, bool TRANSPOSED>
-__device__ __forceinline__ void unpack_to_lds(const VecCtx &x) {
-#pragma unroll
-    for (uint32_t ci = x.lane; ci < 8 * T; ci += 64) {
-        const uint4 v = add_base<T>(unpack_chunk<T>(x.P, x.W, ci), x.base);
-        const uint32_t p0 = ci * (128 / T);                     // first position of the chunk
-        const uint32_t i0 = TRANSPOSED ? tau(p0) : p0;          // its tuple index
-        *reinterpret_cast<uint4 *>(x.V + i0 * (T / 8)) = v;
-    }
-}
-
-template <int T>
-__device__ __forceinline__ void do_delta(const VecCtx &x, const uint8_t *__restrict__ bases, uint8_t *__restrict__ out) {
-    unpack_to_lds<T, true>(x);
-    wave_sync();
-    chain_scan<T>(x.V, bases, x.lane);
-    wave_sync();
-    copy_out<T / 8>(x.V, out, x.nvals, x.lane);
+template <class Path>
+__device__ __forceinline__ void call(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err) {
+    run_chunk<Path>(c, lp, lv, vb, err);
 }
 
 template <int OB>
-__device__ __forceinline__ void dict_gather(const VecCtx &x, const uint8_t *__restrict__ dict, uint32_t dict_count,
-                                            uint8_t *__restrict__ out, uint32_t *err) {
-    const uint32_t *codes = reinterpret_cast<const uint32_t *>(x.V);
-    bool bad = false;
-    gather_out<OB>(dict, out, x.nvals, x.lane, [&](uint32_t i) {
-        uint32_t c = codes[i];
-        if (c >= dict_count) { bad = true; c = dict_count - 1; }
-        return c;
-    });
-    if (bad) atomicOr(err, KERR_DICT_CODE);
+__device__ __forceinline__ void call_dict(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
+                                          uint32_t dict_count) {
+    if (dict_count * OB + 4096 <= vb) call<PathDict<OB, true>>(c, lp, lv, vb, err);
+    else call<PathDict<OB, false>>(c, lp, lv, vb, err);
 }
 
-template <int OB>
-__device__ __forceinline__ void rle_gather(const VecCtx &x, const uint8_t *__restrict__ runs, uint32_t nruns,
-                                           uint8_t *__restrict__ out, uint32_t *err) {
-    const uint16_t *idx = reinterpret_cast<const uint16_t *>(x.V);
-    bool bad = false;
-    gather_out<OB>(runs, out, x.nvals, x.lane, [&](uint32_t i) {
-        uint32_t r = idx[i];
-        if (r >= nruns) { bad = true; r = nruns - 1; }
-        return r;
-    });
-    if (bad) atomicOr(err, KERR_RUN_INDEX);
-}
-
-__global__ __launch_bounds__(256) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t ntasks,
-                                                     uint32_t *__restrict__ err) {
-    __shared__ uint4 lds_p[kWaves][kPackedU4];
-    __shared__ __attribute__((aligned(16))) uint8_t lds_v[kWaves][kValBytes];
-    const uint32_t lane = threadIdx.x & 63;
+__global__ __launch_bounds__(256, 4) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                        uint32_t *__restrict__ err, uint32_t p_bytes,
+                                                        uint32_t v_bytes) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     const uint32_t w = uni(threadIdx.x >> 6);
-    uint4 *P = lds_p[w];
-    uint8_t *V = lds_v[w];
+    const uint32_t lp = (uint32_t)(size_t)((lu8 *)lds_raw + w * (p_bytes + v_bytes));
+    const uint32_t lv = lp + p_bytes;
     const uint32_t stride = gridDim.x * kWaves;
-    for (uint32_t task = blockIdx.x * kWaves + w; task < ntasks; task += stride) {
-        const DevChunk &c = chunks[task >> 6];
-        const uint32_t v = task & 63;
-        if (v >= c.nvec) continue;
-        const VecMeta *vm = reinterpret_cast<const VecMeta *>(c.chunk + c.meta_off) + v;
-        const uint32_t W = vm->bw, nvals = vm->nvals;
-        const uint64_t base = (uint64_t)vm->for_base;
-        const uint8_t *aux = c.chunk + c.aux_off + vm->aux_off;
-        const uint4 *src = reinterpret_cast<const uint4 *>(c.chunk + c.packed_off + vm->packed_off);
-        uint8_t *out = c.out + (size_t)v * kVectorSize * c.ob;
-        // 1. stage packed bits (W word-rows of 128 B) + a zero pad row
-        wave_sync();
-        const uint32_t n16 = 8 * W;
-        for (uint32_t i = lane; i < n16; i += 64) P[i] = src[i];
-        if (lane < 8) P[n16 + lane] = make_uint4(0, 0, 0, 0);
-        wave_sync();
-        VecCtx x{P, V, W, nvals, lane, base};
-        switch (c.enc) {
+    for (uint32_t ci = blockIdx.x * kWaves + w; ci < nchunks; ci += stride) {
+        const DevChunk *cg = chunks + ci;
+        const FLS_GLOBAL DevChunk *c = gptr(cg);
+        const uint32_t nvec = c->nvec, dc = c->dict_count;
+        const uint32_t enc = c->enc, T = c->T, ob = c->ob;
+        if (nvec == 0) continue;
+        switch (enc) {
         case ENC_FFOR:
-            switch (c.T) {
-            case 64: do_ffor<64>(x, out); break;
-            case 32: do_ffor<32>(x, out); break;
-            case 16: do_ffor<16>(x, out); break;
-            default: do_ffor<8>(x, out); break;
+            switch (T) {
+            case 64: call<PathFfor<64>>(cg, lp, lv, v_bytes, err); break;
+            case 32: call<PathFfor<32>>(cg, lp, lv, v_bytes, err); break;
+            case 16: call<PathFfor<16>>(cg, lp, lv, v_bytes, err); break;
+            default: call<PathFfor<8>>(cg, lp, lv, v_bytes, err); break;
             }
             break;
         case ENC_DELTA:
-            switch (c.T) {
-            case 64: do_delta<64>(x, aux, out); break;
-            case 32: do_delta<32>(x, aux, out); break;
-            case 16: do_delta<16>(x, aux, out); break;
-            default: do_delta<8>(x, aux, out); break;
+            switch (T) {
+            case 64: call<PathDelta64>(cg, lp, lv, v_bytes, err); break;
+            case 32: call<PathDeltaSmall<32>>(cg, lp, lv, v_bytes, err); break;
+            case 16: call<PathDeltaSmall<16>>(cg, lp, lv, v_bytes, err); break;
+            default: call<PathDeltaSmall<8>>(cg, lp, lv, v_bytes, err); break;
             }
             break;
         case ENC_DICT:
-            unpack_to_lds<32, false>(x);
-            wave_sync();
-            switch (c.ob) {
-            case 16: dict_gather<16>(x, c.dict, c.dict_count, out, err); break;
-            case 8: dict_gather<8>(x, c.dict, c.dict_count, out, err); break;
-            case 4: dict_gather<4>(x, c.dict, c.dict_count, out, err); break;
-            case 2: dict_gather<2>(x, c.dict, c.dict_count, out, err); break;
-            default: dict_gather<1>(x, c.dict, c.dict_count, out, err); break;
+            switch (ob) {
+            case 16: call_dict<16>(cg, lp, lv, v_bytes, err, dc); break;
+            case 8: call_dict<8>(cg, lp, lv, v_bytes, err, dc); break;
+            case 4: call_dict<4>(cg, lp, lv, v_bytes, err, dc); break;
+            case 2: call_dict<2>(cg, lp, lv, v_bytes, err, dc); break;
+            default: call_dict<1>(cg, lp, lv, v_bytes, err, dc); break;
             }
             break;
-        case ENC_RLE: {
-            unpack_to_lds<16, true>(x);
-            wave_sync();
-            chain_scan<16>(V, aux, lane);
-            wave_sync();
-            const uint8_t *runs = aux + 128;
-            const uint32_t nruns = vm->aux_count;
-            switch (c.ob) {
-            case 8: rle_gather<8>(x, runs, nruns, out, err); break;
-            case 4: rle_gather<4>(x, runs, nruns, out, err); break;
-            case 2: rle_gather<2>(x, runs, nruns, out, err); break;
-            default: rle_gather<1>(x, runs, nruns, out, err); break;
+        case ENC_RLE:
+            switch (ob) {
+            case 8: call<PathRle<8>>(cg, lp, lv, v_bytes, err); break;
+            case 4: call<PathRle<4>>(cg, lp, lv, v_bytes, err); break;
+            case 2: call<PathRle<2>>(cg, lp, lv, v_bytes, err); break;
+            default: call<PathRle<1>>(cg, lp, lv, v_bytes, err); break;
             }
-        } break;
+            break;
         default:
-            if (lane == 0) atomicOr(err, KERR_BAD_DESC);
+            if ((threadIdx.x & 63) == 0) atomicOr(err, KERR_BAD_DESC);
             break;
         }
     }
@@ -423,25 +612,25 @@ __global__ __launch_bounds__(256) void decode_kernel(const DevChunk *__restrict_
 
 }  // namespace
 
-hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, int grid, hipStream_t stream) {
-    const uint64_t ntasks = (uint64_t)nchunks * 64;
-    if (ntasks == 0) return hipSuccess;
-    if (ntasks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint64_t need = (ntasks + kWaves - 1) / kWaves;
-    const int g = (int)std::min<uint64_t>(need, (uint64_t)grid);
-    hipLaunchKernelGGL(decode_kernel, dim3(g), dim3(64 * kWaves), 0, stream, d_chunks, (uint32_t)ntasks, d_err);
-    return hipGetLastError();
-}
-
-int decode_grid_size() {
-    int dev = 0, cus = 256, per_cu = 2;
+int decode_grid_size(uint32_t shmem_per_block) {
+    int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel, 64 * kWaves, 0) != hipSuccess)
-            per_cu = 2;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel, 64 * kWaves, shmem_per_block) !=
+            hipSuccess)
+            per_cu = 1;
     }
-    if (per_cu < 1) per_cu = 1;
-    return cus * per_cu;
+    return cus * std::max(1, per_cu);
+}
+
+hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
+                         hipStream_t stream) {
+    if (nchunks == 0) return hipSuccess;
+    const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
+    const int grid = std::min<int>(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), (nchunks + kWaves - 1) / kWaves);
+    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
+                       geom.p_bytes, geom.v_bytes);
+    return hipGetLastError();
 }
 
 }  // namespace fls

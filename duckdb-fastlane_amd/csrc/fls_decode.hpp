@@ -27,10 +27,30 @@ static_assert(sizeof(DevChunk) == 64, "DevChunk is 64 B");
 // error flags raised by the kernel (corrupt codes / run indices are clamped)
 enum : uint32_t { KERR_DICT_CODE = 1, KERR_RUN_INDEX = 2, KERR_BAD_DESC = 4 };
 
-// Launch the fused decode over ntasks = nchunks * 64 vector tasks.
-hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, int grid,
+// Per-launch LDS geometry: per-wave packed staging (>= 128*maxW + 128 bytes)
+// and decoded-vector scratch (path dependent), both multiples of 16; grid = 0
+// picks the resident grid for that LDS size.
+struct DecodeGeom {
+    uint32_t p_bytes = 256, v_bytes = 0;
+    int grid = 0;
+};
+
+// Launch the fused decode over every vector of nchunks chunks.
+hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream);
-// Resident-grid size for the decode kernel on the current device.
-int decode_grid_size();
+// Resident-grid size of the v2 kernel for the given dynamic LDS per block.
+int decode_grid_size(uint32_t shmem_per_block);
+// LDS bytes per wave the v2 kernel needs for one chunk (given its max width)
+inline void chunk_lds_need(uint8_t enc, uint8_t T, uint8_t ob, uint32_t dict_count, uint32_t max_w,
+                           uint32_t &p_bytes, uint32_t &v_bytes) {
+    p_bytes = 128 * max_w + 128;
+    v_bytes = 0;
+    if (enc == 2 /*DELTA*/ && T < 64) v_bytes = 128 * T;
+    if (enc == 4 /*RLE*/) v_bytes = 2048;
+    if (enc == 3 /*DICT*/) {
+        const uint32_t d = dict_count * ob;
+        v_bytes = 4096 + (d <= 4096 ? ((d + 15) & ~15u) : 0);
+    }
+}
 
 }  // namespace fls

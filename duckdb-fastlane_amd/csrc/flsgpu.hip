@@ -118,6 +118,7 @@ namespace {
 // Per-chunk algorithmic byte accounting (roofline numerator).
 struct ByteCount {
     uint64_t values = 0, packed = 0, meta = 0, out = 0;
+    DecodeGeom geom;   // max LDS need over the counted chunks
 };
 
 // Byte range of the file covering row groups [rg0, rg1).
@@ -258,20 +259,24 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
     d.vbits = h.vbits;
     d.ob = (uint8_t)out_bytes_of(t, col);
     if (h.enc == ENC_DICT) d.dict = h.is_str ? d_dict : d_chunk + h.aux_off;
-    if (bc) {
-        bc->values += h.nvals;
-        bc->out += (uint64_t)h.nvals * d.ob;
-        bc->meta += 32ull * h.nvec;
-        const uint8_t *meta = t->img + ch.off + h.meta_off;
-        for (uint32_t v = 0; v < h.nvec; ++v) {
-            VecMeta vm;
-            memcpy(&vm, meta + 32ull * v, 32);
-            bc->packed += 128ull * vm.bw;
-            if (h.enc == ENC_DELTA) bc->meta += 128;
-            if (h.enc == ENC_RLE) bc->meta += 128 + (uint64_t)vm.aux_count * (h.vbits / 8);
-        }
-        if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? 16 : h.vbits / 8);
+    bc->values += h.nvals;
+    bc->out += (uint64_t)h.nvals * d.ob;
+    bc->meta += 32ull * h.nvec;
+    const uint8_t *meta = t->img + ch.off + h.meta_off;
+    uint32_t max_w = 0;
+    for (uint32_t v = 0; v < h.nvec; ++v) {
+        VecMeta vm;
+        memcpy(&vm, meta + 32ull * v, 32);
+        bc->packed += 128ull * vm.bw;
+        max_w = std::max<uint32_t>(max_w, vm.bw);
+        if (h.enc == ENC_DELTA) bc->meta += 128;
+        if (h.enc == ENC_RLE) bc->meta += 128 + (uint64_t)vm.aux_count * (h.vbits / 8);
     }
+    if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? 16 : h.vbits / 8);
+    uint32_t pb, vb;
+    chunk_lds_need(h.enc, h.T, d.ob, h.dict_count, max_w, pb, vb);
+    bc->geom.p_bytes = std::max(bc->geom.p_bytes, pb);
+    bc->geom.v_bytes = std::max(bc->geom.v_bytes, vb);
     return d;
 }
 
@@ -344,7 +349,6 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         d.rg0 = rg0 + (uint32_t)((uint64_t)nrg * g / G);
         d.rg1 = rg0 + (uint32_t)((uint64_t)nrg * (g + 1) / G);
         d.next_batch_rg = d.rg0;
-        if (!d.grid) d.grid = decode_grid_size();
         int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off);
         if (rc) return rc;
         HIP_TRY(d.err.alloc(d.dev, 1));
@@ -382,6 +386,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     HIP_TRY(sl.h_chunks.alloc((size_t)nsel * sl.nrg));
     HIP_TRY(sl.d_chunks.alloc(d.dev, (size_t)nsel * sl.nrg));
     size_t k = 0;
+    ByteCount bc;
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
         for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) {
@@ -389,11 +394,11 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const uint64_t so = d.strtab_off[(size_t)(r - d.rg0) * ncols + c];
             const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
             uint8_t *out = sl.d_out[c].p + (uint64_t)(r - sl.rg0) * kRowGroupSize * out_bytes_of(t, c);
-            sl.h_chunks.p[k++] = make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, nullptr);
+            sl.h_chunks.p[k++] = make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc);
         }
     }
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(launch_decode(sl.d_chunks.p, (uint32_t)k, d.err.p, d.grid, d.stream));
+    HIP_TRY(launch_decode(sl.d_chunks.p, (uint32_t)k, d.err.p, bc.geom, d.stream));
     // 3. D2H into pinned host columns
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
@@ -621,7 +626,6 @@ int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
     t->res_rows = t->meta.rgs[rg_end - 1].first_row + t->meta.rgs[rg_end - 1].nrows - t->res_first_row;
     t->d_out.resize(ncols);
     for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(t->d_out[c].alloc(dev, t->res_rows * out_bytes_of(t, c)));
-    if (!t->grid) t->grid = decode_grid_size();
     t->h_chunks.clear();
     t->dev_mask.clear();
     t->launches = 0;
@@ -658,6 +662,7 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
         HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
         t->h_chunks.swap(chunks);
         t->dev_mask = mask;
+        bc.geom.grid = decode_grid_size(4 * (bc.geom.p_bytes + bc.geom.v_bytes));
         t->last_bytes = bc;
     }
     if (t->ev_used + 2 > t->ev_pool.size()) {
@@ -670,7 +675,7 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(launch_decode(t->d_chunks.p, (uint32_t)t->h_chunks.size(), sh.err.p, t->grid, t->stream));
+    HIP_TRY(launch_decode(t->d_chunks.p, (uint32_t)t->h_chunks.size(), sh.err.p, t->last_bytes.geom, t->stream));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;
     t->launched = true;
