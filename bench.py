@@ -46,6 +46,12 @@ def parse():
     return p.parse_args()
 
 
+def shard_range(nrg: int, rank: int, world: int):
+    """Contiguous row-group range of `rank`: concatenating the
+    ranks' ranges in rank order reproduces the table order; no collective."""
+    return nrg * rank // world, nrg * (rank + 1) // world
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -139,7 +145,7 @@ def main():
 
     nrows = fl.gen_nrows(args.workload, args.scale, args.rows)
     nrg = (nrows + 65535) // 65536
-    rg0, rg1 = nrg * rank // world, nrg * (rank + 1) // world
+    rg0, rg1 = shard_range(nrg, rank, world)
     t_gen = time.perf_counter()
     img = fl.gen_image(args.workload, args.scale, args.rows, rg0, rg1, nthreads)
     t_gen = time.perf_counter() - t_gen

@@ -1,0 +1,269 @@
+// fls_ext_harness.cpp -- a minimal DuckDB-style executor for the extension,
+// exported as a C-ABI so tests (and bench_e2e) can drive the glue exactly the
+// way DuckDB's binder and pipeline executor call table functions:
+//   lookup overload -> bind -> (projection pushdown) -> init_global ->
+//   init_local -> function() until an empty chunk.
+// It stands in for `duckdb` itself, which is absent from this container (the
+// duckdb/ submodule is empty, .gitmodules:1-4).  SQL-level operators the
+// reference test uses (COUNT, LIMIT, LIKE, LENGTH) are applied by the tests on
+// the returned rows.
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "duckdb.hpp"
+
+extern "C" void fastlane_init(duckdb::DatabaseInstance &db);
+
+using namespace duckdb;
+
+struct fls_ext_db {
+    DatabaseInstance db;
+    ClientContext ctx;
+};
+
+struct fls_ext_result {
+    std::vector<std::string> names, types;
+    std::vector<std::vector<std::string>> cells;  // row-major
+    std::vector<std::vector<char>> valid;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Query {
+    std::string fn;
+    vector<Value> args;
+    bool raw = false;  // call the bind callback with the arguments as given
+};
+
+bool resolve_replacement(fls_ext_db *d, const std::string &table, Query &q) {
+    for (auto &rs : d->db.config.replacement_scans) {
+        ReplacementScanInput in{table};
+        auto ref = rs.function(d->ctx, in, nullptr);
+        if (!ref) continue;
+        auto &tf = static_cast<TableFunctionRef &>(*ref);
+        auto &fe = static_cast<FunctionExpression &>(*tf.function);
+        q.fn = fe.function_name;
+        for (auto &c : fe.children) q.args.push_back(static_cast<ConstantExpression &>(*c).value);
+        return true;
+    }
+    return false;
+}
+
+// DuckDB's overload resolution, reduced to what these functions need: exact
+// type match first, then implicit casts of scalar arguments to VARCHAR.
+TableFunction *lookup(fls_ext_db *d, Query &q) {
+    auto range = d->db.table_functions.equal_range(q.fn);
+    if (range.first == range.second) throw BinderException("Table Function with name " + q.fn + " does not exist!");
+    if (q.raw) return &range.first->second;
+    for (auto it = range.first; it != range.second; ++it) {
+        auto &f = it->second;
+        if (f.arguments.size() != q.args.size()) continue;
+        bool ok = true;
+        for (size_t i = 0; i < q.args.size(); ++i) ok &= f.arguments[i] == q.args[i].type();
+        if (ok) return &f;
+    }
+    for (auto it = range.first; it != range.second; ++it) {
+        auto &f = it->second;
+        if (f.arguments.size() != q.args.size()) continue;
+        bool ok = true;
+        for (size_t i = 0; i < q.args.size(); ++i)
+            ok &= f.arguments[i] == LogicalType::VARCHAR && q.args[i].type().id() != LogicalTypeId::LIST;
+        if (!ok) continue;
+        for (auto &a : q.args) a = Value(a.ToString());  // implicit cast to VARCHAR
+        return &f;
+    }
+    std::string sig = q.fn + "(";
+    for (size_t i = 0; i < q.args.size(); ++i) sig += (i ? ", " : "") + q.args[i].type().ToString();
+    throw BinderException("No function matches the given name and argument types '" + sig + ")'");
+}
+
+// run the query; sink(chunk, column_ids) receives every produced chunk
+template <class Sink>
+void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limit, std::vector<std::string> &names,
+             std::vector<LogicalType> &types, Sink sink) {
+    TableFunction *f = lookup(d, q);
+    named_parameter_map_t named;
+    TableFunctionBindInput bin{q.args, named};
+    vector<LogicalType> rtypes;
+    vector<string> rnames;
+    auto bind = f->bind(d->ctx, bin, rtypes, rnames);
+    vector<column_t> ids;
+    if (proj.empty()) {
+        for (column_t c = 0; c < rtypes.size(); ++c) ids.push_back(c);
+    } else {
+        for (int p : proj) {
+            if (p < 0) ids.push_back(COLUMN_IDENTIFIER_ROW_ID);
+            else if ((size_t)p < rtypes.size()) ids.push_back((column_t)p);
+            else throw BinderException("projection index out of range");
+        }
+    }
+    // without pushdown the function produces every column and we project after
+    vector<column_t> fn_ids = ids;
+    if (!f->projection_pushdown) {
+        fn_ids.clear();
+        for (column_t c = 0; c < rtypes.size(); ++c) fn_ids.push_back(c);
+    }
+    TableFunctionInitInput iin{bind.get(), fn_ids};
+    auto gstate = f->init_global ? f->init_global(d->ctx, iin) : nullptr;
+    ExecutionContext ectx(d->ctx);
+    auto lstate = f->init_local ? f->init_local(ectx, iin, gstate.get()) : nullptr;
+    vector<LogicalType> chunk_types;
+    for (auto id : fn_ids) chunk_types.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? LogicalType::BIGINT : rtypes[id]);
+    for (auto id : ids) {
+        names.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? "rowid" : rnames[id]);
+        types.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? LogicalType::BIGINT : rtypes[id]);
+    }
+    std::vector<size_t> pick;  // output column -> chunk column
+    for (auto id : ids) {
+        size_t k = 0;
+        while (fn_ids[k] != id) ++k;
+        pick.push_back(k);
+    }
+    DataChunk chunk;
+    chunk.Initialize(chunk_types);
+    int64_t produced = 0;
+    while (limit < 0 || produced < limit) {
+        chunk.Reset();
+        TableFunctionInput tin{bind.get(), lstate.get(), gstate.get()};
+        f->function(d->ctx, tin, chunk);
+        if (chunk.size() == 0) break;
+        const idx_t take = limit < 0 ? chunk.size() : std::min<idx_t>(chunk.size(), (idx_t)(limit - produced));
+        sink(chunk, pick, take);
+        produced += (int64_t)take;
+    }
+}
+
+Query make_query(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list) {
+    Query q;
+    if (!fn) {
+        if (nargs != 1 || !resolve_replacement(d, args[0], q))
+            throw Exception("Catalog Error: Table with name " + std::string(nargs ? args[0] : "?") + " does not exist!");
+        return q;
+    }
+    q.fn = fn;
+    q.raw = as_list == 2;
+    if (as_list == 1) {
+        vector<Value> items;
+        for (int i = 0; i < nargs; ++i) items.push_back(Value(args[i] ? args[i] : ""));
+        q.args.push_back(Value::LIST(LogicalType::VARCHAR, items));
+    } else {
+        for (int i = 0; i < nargs; ++i) {
+            const std::string a = args[i] ? args[i] : "";
+            // "\x01" prefix marks an INTEGER literal (to exercise type checks)
+            if (!a.empty() && a[0] == '\x01') q.args.push_back(Value::INTEGER(std::atoi(a.c_str() + 1)));
+            else q.args.push_back(Value(a));
+        }
+    }
+    return q;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *fls_ext_last_error(void) { return g_err.c_str(); }
+
+fls_ext_db *fls_ext_open(void) {
+    auto *d = new fls_ext_db();
+    try {
+        fastlane_init(d->db);  // what DuckDB calls on LOAD fastlane
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        delete d;
+        return nullptr;
+    }
+    return d;
+}
+
+void fls_ext_close(fls_ext_db *d) { delete d; }
+
+int fls_ext_has_function(fls_ext_db *d, const char *name) { return d && d->db.table_functions.count(name) ? 1 : 0; }
+
+// an argument starting with '\x01' is an INTEGER literal (type errors).
+// as_list: 0 = scalar VARCHAR arguments, 1 = one LIST(VARCHAR) argument,
+// 2 = raw: bypass overload resolution and casts (reaches the bind checks).
+int fls_ext_query(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list, const int *proj,
+                  int nproj, int64_t limit, fls_ext_result **out) {
+    try {
+        Query q = make_query(d, fn, args, nargs, as_list);
+        auto *r = new fls_ext_result();
+        std::vector<LogicalType> types;
+        std::vector<int> pv(proj, proj + (proj ? nproj : 0));
+        execute(d, q, pv, limit, r->names, types, [r](DataChunk &c, const std::vector<size_t> &pick, idx_t n) {
+            for (idx_t i = 0; i < n; ++i) {
+                r->cells.emplace_back();
+                r->valid.emplace_back();
+                for (size_t k : pick) {
+                    Value v = c.data[k].GetValue(i);
+                    r->valid.back().push_back(!v.IsNull());
+                    r->cells.back().push_back(v.IsNull() ? std::string() : v.ToString());
+                }
+            }
+        });
+        for (auto &t : types) r->types.push_back(t.ToString());
+        *out = r;
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int64_t fls_ext_result_rows(const fls_ext_result *r) { return (int64_t)r->cells.size(); }
+int fls_ext_result_cols(const fls_ext_result *r) { return (int)r->names.size(); }
+const char *fls_ext_result_name(const fls_ext_result *r, int c) { return r->names[c].c_str(); }
+const char *fls_ext_result_type(const fls_ext_result *r, int c) { return r->types[c].c_str(); }
+const char *fls_ext_result_value(const fls_ext_result *r, int64_t row, int col) {
+    return r->valid[row][col] ? r->cells[row][col].c_str() : nullptr;
+}
+void fls_ext_result_free(fls_ext_result *r) { delete r; }
+
+// Stream a query without materialising it: rows, an order-dependent checksum
+// over the raw DataChunk bytes (string_t by content) and wall seconds.
+int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj, uint64_t *rows,
+                       uint64_t *checksum, double *seconds) {
+    try {
+        const char *args[1] = {path};
+        Query q = make_query(d, fn, args, 1, 0);
+        std::vector<std::string> names;
+        std::vector<LogicalType> types;
+        std::vector<int> pv(proj, proj + (proj ? nproj : 0));
+        uint64_t n = 0, h = 1469598103934665603ull;
+        auto t0 = std::chrono::steady_clock::now();
+        execute(d, q, pv, -1, names, types, [&](DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+            for (size_t k : pick) {
+                Vector &v = c.data[k];
+                if (v.GetType().id() == LogicalTypeId::VARCHAR) {
+                    const string_t *s = FlatVector::GetData<string_t>(v);
+                    for (idx_t i = 0; i < cnt; ++i) {
+                        const char *p = s[i].GetData();
+                        for (uint32_t j = 0; j < s[i].GetSize(); ++j) h = (h ^ (uint8_t)p[j]) * 1099511628211ull;
+                        h = (h ^ 0xFF) * 1099511628211ull;
+                    }
+                } else {
+                    const idx_t w = v.GetType().PhysicalSize();
+                    const uint8_t *p = v.GetData();
+                    for (idx_t i = 0; i < cnt * w; i += 8) {
+                        uint64_t x = 0;
+                        memcpy(&x, p + i, std::min<idx_t>(8, cnt * w - i));
+                        h = (h ^ x) * 1099511628211ull;
+                    }
+                }
+            }
+            n += cnt;
+        });
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        *rows = n;
+        *checksum = h;
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+}  // extern "C"

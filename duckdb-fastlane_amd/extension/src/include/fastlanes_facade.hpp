@@ -1,0 +1,49 @@
+//===----------------------------------------------------------------------===//
+//                         DuckDB - fastlane (MI355X)
+//
+// include/fastlanes_facade.hpp -- the richer facade the reference declares but
+// never implements (src/include/fastlanes_facade.hpp:23-48): typed schema,
+// row-major boxed reads, and the write path.  Same API; implemented in
+// scanner/ext_fastlanes_facade.cpp over the MI355X engine (reads) and the CPU
+// FastLanes writer (writes).  No FastLanes or HIP type appears here.
+//===----------------------------------------------------------------------===//
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "duckdb/common/types.hpp"
+#include "duckdb/common/types/data_chunk.hpp"
+
+namespace duckdb {
+namespace ext_fastlane {
+
+class FastLanesFacade {
+private:
+    class Impl;
+    std::unique_ptr<Impl> pImpl;
+
+public:
+    FastLanesFacade();
+    ~FastLanesFacade();
+
+    // Reading: all row groups, all columns, typed
+    bool openFile(const std::string &file_path);
+    std::vector<LogicalType> getColumnTypes();
+    std::vector<std::string> getColumnNames();
+    // next <= STANDARD_VECTOR_SIZE rows, row-major: values[row * ncols + col]
+    bool readNextChunk(std::vector<Value> &values, idx_t &rows_read);
+    void closeFile();
+
+    // Writing: 65,536-row row groups, encodings chosen per chunk
+    bool createFile(const std::string &file_path, const std::vector<LogicalType> &types,
+                    const std::vector<std::string> &names);
+    bool writeChunk(DataChunk &chunk);
+    void finalizeFile();
+
+    bool isValid() const;
+};
+
+}  // namespace ext_fastlane
+}  // namespace duckdb

@@ -1,0 +1,213 @@
+// ext_fastlanes_facade.cpp -- ext_fastlane::FastLanesFacade (declared at
+// reference src/include/fastlanes_facade.hpp:23-48, never implemented there).
+//
+// Reads stream every row group through the engine's GPU scan (fls_scan_*) and
+// box values row-major as the intended scanner expects
+// (src/scanner/scan_fastlanes.cpp:132-140).  Writes buffer DataChunks into
+// 65,536-row row groups (src/writer/write_fastlane_stream.cpp:21-24) and hand
+// them to the CPU FastLanes writer (include/flswriter.h).
+#include <cstring>
+#include <vector>
+
+#include "../../../../include/flsgpu.h"
+#include "../../../../include/flswriter.h"
+#include "../gpu_devices.hpp"
+#include "duckdb/common/vector.hpp"
+#include "fastlanes_facade.hpp"
+#include "type_mapping.hpp"
+
+namespace duckdb {
+namespace ext_fastlane {
+
+class FastLanesFacade::Impl {
+public:
+    // read side
+    fls_connection *conn = nullptr;
+    fls_table *table = nullptr;
+    std::vector<fls_column_info> cols;
+    fls_rowgroup rg{};
+    bool have_rg = false, eof = false;
+    idx_t rg_pos = 0;
+    // write side
+    fls_writer *writer = nullptr;
+    std::string out_path;
+    std::vector<LogicalType> wtypes;
+    std::vector<std::vector<uint8_t>> wcols;         // fixed-width buffered rows
+    std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
+    idx_t wrows = 0;
+
+    void close_read() {
+        if (table) fls_table_close(table);
+        if (conn) fls_disconnect(conn);
+        table = nullptr;
+        conn = nullptr;
+        have_rg = eof = false;
+        rg_pos = 0;
+    }
+    bool flush_rowgroup();
+    ~Impl() {
+        close_read();
+        if (writer) fls_writer_free(writer);
+    }
+};
+
+FastLanesFacade::FastLanesFacade() : pImpl(new Impl()) {}
+FastLanesFacade::~FastLanesFacade() = default;
+
+bool FastLanesFacade::openFile(const std::string &file_path) {
+    Impl &s = *pImpl;
+    s.close_read();
+    std::vector<int> devs = GpuDevices();
+    if (fls_connect(devs.data(), (int)devs.size(), &s.conn) != 0 ||
+        fls_read_fls(s.conn, file_path.c_str(), &s.table) != 0) {
+        s.close_read();
+        return false;
+    }
+    s.cols.resize(fls_table_ncols(s.table));
+    for (uint32_t c = 0; c < s.cols.size(); ++c) fls_table_column(s.table, c, &s.cols[c]);
+    return true;
+}
+
+std::vector<LogicalType> FastLanesFacade::getColumnTypes() {
+    std::vector<LogicalType> t;
+    for (auto &c : pImpl->cols) t.push_back(TypeMapping::FastLanesToDuckDB(c.type, c.width, c.scale));
+    return t;
+}
+
+std::vector<std::string> FastLanesFacade::getColumnNames() {
+    std::vector<std::string> n;
+    for (auto &c : pImpl->cols) n.emplace_back(c.name);
+    return n;
+}
+
+static Value BoxValue(const fls_column_info &ci, const void *col, idx_t row) {
+    const uint8_t *p = (const uint8_t *)col;
+    auto ld = [p, row](auto x) {
+        memcpy(&x, p + row * sizeof(x), sizeof(x));
+        return x;
+    };
+    switch (ci.type) {
+    case FLS_INT8: return Value::TINYINT(ld(int8_t()));
+    case FLS_INT16: return Value::SMALLINT(ld(int16_t()));
+    case FLS_INT32: return Value::INTEGER(ld(int32_t()));
+    case FLS_INT64: return Value::BIGINT(ld(int64_t()));
+    case FLS_UINT8: return Value::UTINYINT(ld(uint8_t()));
+    case FLS_UINT16: return Value::USMALLINT(ld(uint16_t()));
+    case FLS_UINT32: return Value::UINTEGER(ld(uint32_t()));
+    case FLS_UINT64: return Value::UBIGINT(ld(uint64_t()));
+    case FLS_DATE: return Value::DATE(date_t{ld(int32_t())});
+    case FLS_DECIMAL: return Value::DECIMAL(ld(int64_t()), ci.width ? ci.width : 18, ci.scale);
+    case FLS_VARCHAR: {
+        string_t s;
+        memcpy(&s, p + 16 * row, 16);
+        return Value(s.GetString());
+    }
+    default: return Value();
+    }
+}
+
+bool FastLanesFacade::readNextChunk(std::vector<Value> &values, idx_t &rows_read) {
+    Impl &s = *pImpl;
+    rows_read = 0;
+    values.clear();
+    if (!s.table || s.eof) return false;
+    if (!s.have_rg || s.rg_pos >= s.rg.nrows) {
+        if (!s.have_rg && fls_scan_begin(s.table, nullptr, 0, fls_table_nrowgroups(s.table)) != 0) return false;
+        s.have_rg = true;
+        const int rc = fls_scan_next(s.table, &s.rg);
+        if (rc != 1) {
+            s.eof = true;
+            return false;
+        }
+        s.rg_pos = 0;
+    }
+    const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, s.rg.nrows - s.rg_pos);
+    values.reserve(n * s.cols.size());
+    for (idx_t r = 0; r < n; ++r)
+        for (size_t c = 0; c < s.cols.size(); ++c) values.push_back(BoxValue(s.cols[c], s.rg.columns[c], s.rg_pos + r));
+    s.rg_pos += n;
+    rows_read = n;
+    return true;
+}
+
+void FastLanesFacade::closeFile() { pImpl->close_read(); }
+
+bool FastLanesFacade::isValid() const { return pImpl->table != nullptr || pImpl->writer != nullptr; }
+
+// ---- write path ------------------------------------------------------------
+
+bool FastLanesFacade::createFile(const std::string &file_path, const std::vector<LogicalType> &types,
+                                 const std::vector<std::string> &names) {
+    Impl &s = *pImpl;
+    if (types.size() != names.size() || types.empty()) return false;
+    if (s.writer) fls_writer_free(s.writer);
+    s.writer = fls_writer_new(0);
+    for (size_t c = 0; c < types.size(); ++c) {
+        const uint8_t ft = TypeMapping::DuckDBToFastLanes(types[c]);
+        if (!ft || fls_writer_add_column(s.writer, names[c].c_str(), ft, types[c].Width(), types[c].Scale(),
+                                         FLS_ENC_AUTO) != 0) {
+            fls_writer_free(s.writer);
+            s.writer = nullptr;
+            return false;
+        }
+    }
+    s.out_path = file_path;
+    s.wtypes = types;
+    s.wcols.assign(types.size(), {});
+    s.woffs.assign(types.size(), {0});
+    s.wrows = 0;
+    return true;
+}
+
+bool FastLanesFacade::Impl::flush_rowgroup() {
+    if (wrows == 0) return true;
+    std::vector<const void *> data(wtypes.size());
+    std::vector<const uint32_t *> offs(wtypes.size(), nullptr);
+    for (size_t c = 0; c < wtypes.size(); ++c) {
+        data[c] = wcols[c].empty() ? (const void *)"" : wcols[c].data();
+        if (wtypes[c].id() == LogicalTypeId::VARCHAR) offs[c] = woffs[c].data();
+    }
+    const bool ok = fls_writer_add_rowgroup(writer, (uint32_t)wrows, data.data(), offs.data()) == 0;
+    for (size_t c = 0; c < wtypes.size(); ++c) {
+        wcols[c].clear();
+        woffs[c].assign(1, 0);
+    }
+    wrows = 0;
+    return ok;
+}
+
+bool FastLanesFacade::writeChunk(DataChunk &chunk) {
+    Impl &s = *pImpl;
+    if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
+    for (idx_t r = 0; r < chunk.size(); ++r) {
+        for (size_t c = 0; c < s.wtypes.size(); ++c) {
+            Vector &v = chunk.data[c];
+            const LogicalType &t = s.wtypes[c];
+            if (t.id() == LogicalTypeId::VARCHAR) {
+                const std::string str = v.RowIsValid(r) ? v.GetValue(r).GetValue<string>() : std::string();
+                s.wcols[c].insert(s.wcols[c].end(), str.begin(), str.end());
+                s.woffs[c].push_back((uint32_t)s.wcols[c].size());
+            } else {
+                // NULLs have no encoding on this path: written as 0
+                const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
+                int64_t x = v.RowIsValid(r) ? v.GetValue(r).GetInt64() : 0;
+                const uint8_t *b = (const uint8_t *)&x;
+                s.wcols[c].insert(s.wcols[c].end(), b, b + w);
+            }
+        }
+        if (++s.wrows == 65536 && !s.flush_rowgroup()) return false;
+    }
+    return true;
+}
+
+void FastLanesFacade::finalizeFile() {
+    Impl &s = *pImpl;
+    if (!s.writer) return;
+    s.flush_rowgroup();
+    fls_writer_finish_file(s.writer, s.out_path.c_str());
+    fls_writer_free(s.writer);
+    s.writer = nullptr;
+}
+
+}  // namespace ext_fastlane
+}  // namespace duckdb

@@ -1,0 +1,192 @@
+// read_fastlanes.cpp -- `read_fastlanes(path | [paths])` over the MI355X engine.
+//
+// Bind reads only footers (no GPU): typed schema via TypeMapping.  InitGlobal
+// turns DuckDB's projected column_ids into the engine's column mask, so only
+// projected columns are uploaded, decoded and copied back.  Scan streams row
+// groups from fls_scan_next (GPU-sharded, decoded ahead into pinned host
+// memory) and fills STANDARD_VECTOR_SIZE-row DataChunks by memcpy of DuckDB's
+// physical layouts; string_t records point into the file image the global
+// state keeps alive.  Error texts follow src/scanner/scan_fastlanes.cpp:62-97.
+#include <cstring>
+
+#include "../../../../include/flsgpu.h"
+#include "../gpu_devices.hpp"
+#include "duckdb/common/exception.hpp"
+#include "duckdb/common/string_util.hpp"
+#include "duckdb/main/extension_util.hpp"
+#include "duckdb/parser/expression/constant_expression.hpp"
+#include "duckdb/parser/expression/function_expression.hpp"
+#include "duckdb/parser/tableref/table_function_ref.hpp"
+#include "table_function/read_fastlanes.hpp"
+#include "type_mapping.hpp"
+
+namespace duckdb {
+namespace ext_fastlane {
+
+namespace {
+
+struct OpenTable {
+    fls_connection *conn = nullptr;
+    fls_table *table = nullptr;
+    ~OpenTable() {
+        if (table) fls_table_close(table);
+        if (conn) fls_disconnect(conn);
+    }
+    bool open(const std::string &path) {
+        std::vector<int> devs = GpuDevices();
+        return fls_connect(devs.data(), (int)devs.size(), &conn) == 0 &&
+               fls_read_fls(conn, path.c_str(), &table) == 0;
+    }
+};
+
+struct ReadBindData : public TableFunctionData {
+    vector<string> files;
+    vector<LogicalType> types;
+    vector<string> names;
+    vector<fls_column_info> cols;
+};
+
+struct ReadGlobalState : public GlobalTableFunctionState {
+    vector<column_t> column_ids;
+    std::vector<uint8_t> mask;
+    idx_t file_idx = 0;
+    std::unique_ptr<OpenTable> cur;
+    fls_rowgroup rg{};
+    bool have_rg = false;
+    idx_t rg_pos = 0;
+    idx_t MaxThreads() const override { return 1; }
+};
+
+void CollectPaths(const Value &v, vector<string> &files, const char *fn) {
+    if (v.IsNull()) throw BinderException(string(fn) + " file paths must be strings");
+    if (v.type().id() == LogicalTypeId::LIST) {
+        for (auto &c : v.ListChildren()) CollectPaths(c, files, fn);
+        return;
+    }
+    if (v.type() != LogicalType::VARCHAR) throw BinderException(string(fn) + " file paths must be strings");
+    files.push_back(v.GetValue<string>());
+}
+
+unique_ptr<FunctionData> ReadBind(ClientContext &, TableFunctionBindInput &input, vector<LogicalType> &return_types,
+                                  vector<string> &names) {
+    auto bind = make_uniq<ReadBindData>();
+    for (auto &v : input.inputs) CollectPaths(v, bind->files, "read_fastlanes");
+    if (bind->files.empty()) throw BinderException("read_fastlanes requires at least one file path");
+    OpenTable t;
+    if (!t.open(bind->files[0])) throw BinderException("Failed to open FastLanes file: " + bind->files[0]);
+    const uint32_t n = fls_table_ncols(t.table);
+    bind->cols.resize(n);
+    for (uint32_t c = 0; c < n; ++c) {
+        fls_table_column(t.table, c, &bind->cols[c]);
+        bind->types.push_back(TypeMapping::FastLanesToDuckDB(bind->cols[c].type, bind->cols[c].width, bind->cols[c].scale));
+        bind->names.emplace_back(bind->cols[c].name);
+        bind->cols[c].name = nullptr;  // owned by the closed table
+    }
+    return_types = bind->types;
+    names = bind->names;
+    return std::move(bind);
+}
+
+unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFunctionInitInput &input) {
+    const auto &bind = input.bind_data->Cast<ReadBindData>();
+    auto state = make_uniq<ReadGlobalState>();
+    state->column_ids = input.column_ids;
+    state->mask.assign(bind.cols.size(), 0);
+    for (auto id : state->column_ids)
+        if (id != COLUMN_IDENTIFIER_ROW_ID && id < bind.cols.size()) state->mask[id] = 1;
+    // fail early on unreadable or schema-incompatible files
+    for (auto &f : bind.files) {
+        OpenTable t;
+        if (!t.open(f)) throw IOException("Failed to open FastLanes file: " + f);
+        bool same = fls_table_ncols(t.table) == bind.cols.size();
+        for (uint32_t c = 0; same && c < bind.cols.size(); ++c) {
+            fls_column_info ci;
+            fls_table_column(t.table, c, &ci);
+            same = ci.type == bind.cols[c].type && ci.width == bind.cols[c].width && ci.scale == bind.cols[c].scale;
+        }
+        if (!same) throw IOException("FastLanes file " + f + " does not match the schema of " + bind.files[0]);
+    }
+    return std::move(state);
+}
+
+// advance to a row group with rows left; false at the end of all files
+bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &st) {
+    while (true) {
+        if (st.cur && st.have_rg && st.rg_pos < st.rg.nrows) return true;
+        if (st.cur) {
+            const int rc = fls_scan_next(st.cur->table, &st.rg);
+            if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
+            if (rc == 1) {
+                st.have_rg = true;
+                st.rg_pos = 0;
+                continue;
+            }
+            st.cur.reset();
+            st.file_idx++;
+        }
+        if (st.file_idx >= bind.files.size()) return false;
+        st.cur = std::make_unique<OpenTable>();
+        if (!st.cur->open(bind.files[st.file_idx]))
+            throw IOException("Failed to open FastLanes file: " + bind.files[st.file_idx]);
+        if (fls_scan_begin(st.cur->table, st.mask.data(), 0, fls_table_nrowgroups(st.cur->table)) != 0)
+            throw IOException(string("FastLanes scan failed: ") + fls_last_error());
+        st.have_rg = false;
+    }
+}
+
+void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
+    const auto &bind = data.bind_data->Cast<ReadBindData>();
+    auto &st = data.global_state->Cast<ReadGlobalState>();
+    output.Reset();
+    if (!NextRowGroup(bind, st)) {
+        output.SetCardinality(0);
+        return;
+    }
+    const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, st.rg.nrows - st.rg_pos);
+    for (idx_t j = 0; j < output.ColumnCount(); ++j) {
+        const column_t id = j < st.column_ids.size() ? st.column_ids[j] : j;
+        Vector &vec = output.data[j];
+        if (id == COLUMN_IDENTIFIER_ROW_ID) {
+            int64_t *rid = FlatVector::GetData<int64_t>(vec);
+            for (idx_t i = 0; i < n; ++i) rid[i] = (int64_t)(st.rg.first_row + st.rg_pos + i);
+            continue;
+        }
+        const idx_t ob = bind.cols[id].out_bytes;
+        memcpy(vec.GetData(), (const uint8_t *)st.rg.columns[id] + st.rg_pos * ob, n * ob);
+    }
+    st.rg_pos += n;
+    output.SetCardinality(n);
+}
+
+unique_ptr<TableRef> ReadFastlanesReplacementScan(ClientContext &, ReplacementScanInput &input,
+                                                  optional_ptr<ReplacementScanData>) {
+    const string path = ReplacementScan::GetFullPath(input);
+    const string lower = StringUtil::Lower(path);
+    if (!StringUtil::EndsWith(lower, ".fls") && !StringUtil::EndsWith(lower, ".fastlane")) return nullptr;
+    auto ref = make_uniq<TableFunctionRef>();
+    vector<unique_ptr<ParsedExpression>> args;
+    args.push_back(make_uniq<ConstantExpression>(Value(path)));
+    ref->function = make_uniq<FunctionExpression>("read_fastlanes", std::move(args));
+    return std::move(ref);
+}
+
+}  // namespace
+
+TableFunction ReadFastlanesFunction() {
+    TableFunction fn("read_fastlanes", {LogicalType::VARCHAR}, ReadScan, ReadBind, ReadInitGlobal);
+    fn.projection_pushdown = true;
+    fn.filter_pushdown = false;
+    fn.filter_prune = false;
+    return fn;
+}
+
+void RegisterReadFastlanes(DatabaseInstance &db) {
+    TableFunction fn = ReadFastlanesFunction();
+    ExtensionUtil::RegisterFunction(db, fn);
+    fn.arguments = {LogicalType::LIST(LogicalType::VARCHAR)};
+    ExtensionUtil::RegisterFunction(db, fn);
+    DBConfig::GetConfig(db).replacement_scans.emplace_back(ReadFastlanesReplacementScan);
+}
+
+}  // namespace ext_fastlane
+}  // namespace duckdb

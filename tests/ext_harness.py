@@ -1,0 +1,87 @@
+"""ctypes driver for libfastlane_ext.so's mini DuckDB executor (tests only).
+
+Mirrors how DuckDB runs `SELECT <proj> FROM fn(args) LIMIT n` against the
+extension's table functions (see duckdb-fastlane_amd/extension/harness)."""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB = ROOT / "duckdb-fastlane_amd" / "libfastlane_ext.so"
+
+
+class ExtError(RuntimeError):
+    pass
+
+
+class Ext:
+    def __init__(self):
+        lib = C.CDLL(str(LIB))
+        lib.fls_ext_open.restype = C.c_void_p
+        lib.fls_ext_close.argtypes = [C.c_void_p]
+        lib.fls_ext_last_error.restype = C.c_char_p
+        lib.fls_ext_has_function.argtypes = [C.c_void_p, C.c_char_p]
+        lib.fls_ext_query.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                      C.POINTER(C.c_int), C.c_int, C.c_int64, C.POINTER(C.c_void_p)]
+        lib.fls_ext_result_rows.restype = C.c_int64
+        lib.fls_ext_result_rows.argtypes = [C.c_void_p]
+        lib.fls_ext_result_cols.argtypes = [C.c_void_p]
+        for f in ("fls_ext_result_name", "fls_ext_result_type"):
+            getattr(lib, f).restype = C.c_char_p
+            getattr(lib, f).argtypes = [C.c_void_p, C.c_int]
+        lib.fls_ext_result_value.restype = C.c_char_p
+        lib.fls_ext_result_value.argtypes = [C.c_void_p, C.c_int64, C.c_int]
+        lib.fls_ext_result_free.argtypes = [C.c_void_p]
+        lib.fls_ext_scan_count.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.c_int,
+                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        self.lib = lib
+        self.db = lib.fls_ext_open()
+        if not self.db:
+            raise ExtError(lib.fls_ext_last_error().decode())
+
+    def has_function(self, name: str) -> bool:
+        return bool(self.lib.fls_ext_has_function(self.db, name.encode()))
+
+    def query(self, fn, *args, as_list=False, raw=False, proj=None, limit=-1):
+        """Returns (names, types, rows) with rows as lists of str/None.
+        fn=None resolves args[0] through the replacement scans.
+        An int argument is passed as an INTEGER value (type errors)."""
+        a = (C.c_char_p * max(1, len(args)))(*[(b"\x01%d" % x) if isinstance(x, int) else str(x).encode()
+                                               for x in args])
+        p = (C.c_int * len(proj))(*proj) if proj else None
+        out = C.c_void_p()
+        mode = 2 if raw else int(as_list)
+        rc = self.lib.fls_ext_query(self.db, fn.encode() if fn else None, a, len(args), mode, p,
+                                    len(proj) if proj else 0, limit, C.byref(out))
+        if rc != 0:
+            raise ExtError(self.lib.fls_ext_last_error().decode())
+        r = out.value
+        try:
+            nc = self.lib.fls_ext_result_cols(r)
+            names = [self.lib.fls_ext_result_name(r, c).decode() for c in range(nc)]
+            types = [self.lib.fls_ext_result_type(r, c).decode() for c in range(nc)]
+            rows = []
+            for i in range(self.lib.fls_ext_result_rows(r)):
+                row = []
+                for c in range(nc):
+                    v = self.lib.fls_ext_result_value(r, i, c)
+                    row.append(None if v is None else v.decode())
+                rows.append(row)
+            return names, types, rows
+        finally:
+            self.lib.fls_ext_result_free(r)
+
+    def scan_count(self, fn, path, proj=None):
+        p = (C.c_int * len(proj))(*proj) if proj else None
+        rows, h, sec = C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = self.lib.fls_ext_scan_count(self.db, fn.encode(), str(path).encode(), p, len(proj) if proj else 0,
+                                         C.byref(rows), C.byref(h), C.byref(sec))
+        if rc != 0:
+            raise ExtError(self.lib.fls_ext_last_error().decode())
+        return rows.value, h.value, sec.value
+
+    def close(self):
+        if self.db:
+            self.lib.fls_ext_close(self.db)
+            self.db = None

@@ -1,0 +1,120 @@
+"""CPU writer (the .fls producer, reference write path stubs
+src/writer/write_fastlane*.cpp) round-trips through the oracle, for every
+encoding, type and the seeded workloads."""
+import numpy as np
+import pytest
+
+from helpers import INT_TYPE, SIGNED, width_sweep_values
+
+
+def roundtrip(fl, ref, cols):
+    img = fl.write_image(cols)
+    rf = ref.RefFile(img)
+    for c, spec in enumerate(cols):
+        ty, vals = spec[1], spec[2]
+        raw = np.concatenate([rf.decode(c, rg) for rg in range(rf.nrowgroups)])
+        if ty == fl.VARCHAR:
+            assert rf.strings(raw) == [v.encode() for v in vals]
+        else:
+            assert np.array_equal(raw.view(fl.NP_DTYPE[ty]), np.asarray(vals).astype(fl.NP_DTYPE[ty]))
+    return img, rf
+
+
+@pytest.mark.parametrize("enc", [1, 2, 3, 4, 0])
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_int_roundtrip(fl, ref, enc, T):
+    rng = np.random.default_rng(T * 10 + enc)
+    if enc == 3:  # dictionary: bounded cardinality
+        v = rng.integers(-100, 100, 5000).astype(SIGNED[T])
+    elif enc == 4:
+        v = np.repeat(rng.integers(-100, 100, 100), 50).astype(SIGNED[T])
+    else:
+        v = width_sweep_values(T, rng)
+    roundtrip(fl, ref, [("v", INT_TYPE[T], v, enc)])
+
+
+def test_unsigned_date_decimal(fl, ref):
+    rng = np.random.default_rng(1)
+    n = 70001
+    roundtrip(fl, ref, [("u8", fl.UINT8, rng.integers(0, 256, n), fl.ENC_AUTO),
+                        ("u64", fl.UINT64, rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2), fl.ENC_FFOR),
+                        ("d", fl.DATE, 8035 + rng.integers(0, 2557, n), fl.ENC_AUTO),
+                        ("m", fl.DECIMAL, rng.integers(-10**12, 10**12, n), fl.ENC_AUTO, 15, 2)])
+
+
+def test_strings(fl, ref):
+    rng = np.random.default_rng(2)
+    words = ["", "x", "ümlaut ✓", "a" * 300] + [f"s{i}" for i in range(3000)]
+    v = [words[i] for i in rng.integers(0, len(words), 140000)]
+    roundtrip(fl, ref, [("s", fl.VARCHAR, v, fl.ENC_DICT)])
+
+
+def test_auto_picks_compact_encodings(fl, ref):
+    n = 65536
+    cols = [("sorted", fl.INT64, np.arange(n) * 3 + 10**15, fl.ENC_AUTO),
+            ("runs", fl.INT32, np.repeat(np.random.default_rng(0).integers(-2**31, 2**31 - 1, n // 1000 + 1),
+                                         1000)[:n], fl.ENC_AUTO),
+            ("few", fl.INT64, (np.arange(n) % 3) * 10**17, fl.ENC_AUTO)]
+    img, rf = roundtrip(fl, ref, cols)
+    import struct
+    raw = img.tobytes()
+    encs = []
+    for c in range(3):
+        # chunk header encoding byte (offset 4) of row group 0
+        foff = struct.unpack_from("<Q", raw, len(raw) - 16)[0]
+        p = foff + 32
+        for _ in range(rf.ncols):
+            p += 6 + struct.unpack_from("<H", raw, p + 4)[0]
+        off = struct.unpack_from("<Q", raw, p + 4 + 16 * c)[0]
+        encs.append(raw[off + 4])
+    assert encs[0] == 2          # DELTA for a sorted run of keys
+    assert encs[1] in (3, 4)     # DICT or RLE for long runs
+    assert encs[2] == 3          # DICT for 3 distinct 64-bit values
+    assert img.len < n * 3       # well under one byte per value overall
+
+
+def test_writer_errors(fl):
+    with pytest.raises(fl.FlsError, match="VARCHAR supports DICT only"):
+        fl.write_image([("s", fl.VARCHAR, ["a"], fl.ENC_FFOR)])
+    with pytest.raises(fl.FlsError, match="unsupported type"):
+        fl.write_image([("x", 99, [1], fl.ENC_FFOR)])
+    with pytest.raises(ValueError):
+        fl.write_image([("a", fl.INT32, [1, 2], fl.ENC_FFOR), ("b", fl.INT32, [1], fl.ENC_FFOR)])
+
+
+@pytest.mark.parametrize("wl,scale,n", [("c1", 1, 0), ("c3", 1, 300000), ("c4", 1, 200000), ("lineitem", 0.01, 0)])
+def test_workloads_match_generator(fl, ref, wl, scale, n):
+    img = fl.gen_image(wl, scale, n)
+    rf = ref.RefFile(img)
+    for c in range(rf.ncols):
+        name, ty, _, _ = rf.column(c)
+        raw = rf.decode_column(c, 4)
+        if ty == fl.VARCHAR:
+            codes = fl.gen_values(wl, c, 0, rf.nrows, np.uint32, scale, n)
+            d = [fl.gen_dict_string(wl, c, k) for k in range(int(codes.max()) + 1)]
+            assert rf.strings(raw) == [d[k].encode() for k in codes], name
+        else:
+            assert np.array_equal(raw.view(fl.NP_DTYPE[ty]), fl.gen_values(wl, c, 0, rf.nrows, fl.NP_DTYPE[ty], scale, n)), name
+
+
+def test_lineitem_distributions(fl):
+    n = 60175
+    g = {c: fl.gen_values("lineitem", c, 0, n, t, 0.01) for c, t in
+         [(0, np.int64), (3, np.int32), (4, np.int64), (6, np.int64), (10, np.int32), (12, np.int32)]}
+    assert np.all(np.diff(g[0]) >= 0)                       # orderkey sorted
+    assert g[3].min() == 1 and g[3].max() == 7              # 1..7 lines per order
+    assert g[4].min() == 100 and g[4].max() == 5000         # quantity 1..50 (cents)
+    assert g[6].min() == 0 and g[6].max() == 10             # discount 0.00..0.10
+    assert g[10].min() >= 8036 and g[12].max() <= 10591 + 151
+    # keys dense 8 per 32
+    assert set((np.unique(g[0]) - 1) % 32) <= set(range(8))
+    assert fl.gen_nrows("lineitem", 100) == 600037902 and fl.gen_nrows("lineitem", 1) == 6001215
+
+
+def test_shard_images_concatenate(fl, ref):
+    """Row-group shards (what each rank encodes) reassemble the full table."""
+    full = ref.RefFile(fl.gen_image("c3", nrows=7 * 65536 + 123))
+    parts = [fl.gen_image("c3", nrows=7 * 65536 + 123, rg_begin=b, rg_end=e) for b, e in [(0, 3), (3, 5), (5, 8)]]
+    got = np.concatenate([ref.RefFile(p).decode_column(0) for p in parts])
+    assert np.array_equal(got, full.decode_column(0))
+    assert [ref.RefFile(p).f.row_offset for p in parts] == [0, 3 * 65536, 5 * 65536]
