@@ -27,7 +27,7 @@ def test_1e9_rows_bit_exact(fl, gpu, wl, rows):
     # the check must be able to fail: corrupt one decoded value and re-check
     p, n = t.device_column(0)
     import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libflsgpu.so already loaded
     bad = (ctypes.c_uint8 * 16)(*([0x5A] * 16))
     assert hip.hipMemcpy(ctypes.c_void_p(p + 16 * 12345), bad, 16 if wl == "c4" else 8, 1) == 0
     mism = fl.check_device_table(t, wl, 1.0, rows)
