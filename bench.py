@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--threads", type=int, default=0, help="host threads for encode / CPU baseline")
     p.add_argument("--verify-rowgroups", type=int, default=3)
+    p.add_argument("--no-traffic", action="store_true",
+                   help="skip the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -50,6 +53,43 @@ def shard_range(nrg: int, rank: int, world: int):
     """Contiguous row-group range of `rank`: concatenating the
     ranks' ranges in rank order reproduces the table order; no collective."""
     return nrg * rank // world, nrg * (rank + 1) // world
+
+
+def measure_traffic(args):
+    """HBM bytes per decode launch from rocprofv3 PMC counters, each counter in
+    its own pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950).
+    Runs as child processes BEFORE this process touches the GPU.  Corrections
+    per MI355X_MICROARCH.md (HBM/rocprofv3): counters are in KiB; FETCH_SIZE
+    reports half the bytes of 16 B/lane streaming reads -> x2."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"fls_pmc_{ctr.lower()}_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = ["rocprofv3", "--pmc", ctr, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
+               sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--steps", "2", "--warmup", "1",
+               "--workload", args.workload, "--scale", str(args.scale), "--rows", str(args.rows),
+               "--cpu-seconds", "0", "--verify-rowgroups", "0", "--no-traffic"]
+        try:
+            subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
+        except Exception as e:  # noqa: BLE001 - report, never fail the bench on profiling
+            return None, f"rocprofv3 {ctr} pass failed: {e}"
+        per = []
+        for path in Path(d).rglob("*counter_collection.csv"):
+            for r in csv.DictReader(open(path)):
+                if "decode_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
+                    per.append(float(r["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not per:
+            return None, f"no {ctr} samples"
+        vals[ctr] = sum(per) / len(per) * 1024.0  # KiB -> bytes, per launch
+    return 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"], \
+        f"rocprofv3 --pmc per launch: FETCH_SIZE x2 {2 * vals['FETCH_SIZE'] / 1e9:.3f} GB + " \
+        f"WRITE_SIZE {vals['WRITE_SIZE'] / 1e9:.3f} GB"
 
 
 def log(*a):
@@ -128,6 +168,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    traffic, traffic_note = None, "not measured (multi-rank run or --no-traffic)"
+    if world == 1 and not args.no_traffic and not args.pmc_child:
+        traffic, traffic_note = measure_traffic(args)
+        log(f"[traffic] {traffic_note}")
 
     import torch  # torch first: its HIP runtime is the one the engine binds to
     import torch.distributed as dist
@@ -228,7 +273,9 @@ def main():
             "config": cfg,
             "hbm_gbs": achieved * world,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic / 1e9 if traffic else None,
+                         "traffic_unit": "GB per launch (HBM, PMC)", "traffic_note": traffic_note,
                          "kernel": "fls::decode_kernel", "kernel_ms": avg_ms,
                          "algo_bytes_per_launch": algo,
                          "algo_bytes_split": {"packed": int(st.packed_bytes), "meta": int(st.meta_bytes),
