@@ -17,7 +17,8 @@ from pathlib import Path
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libflsgpu.so"
+# FLS_LIB selects an alternative in-tree build (A/B measurement of kernel variants)
+LIB_PATH = _HERE / os.environ.get("FLS_LIB", "libflsgpu.so")
 
 if not LIB_PATH.exists():
     raise ImportError(f"{LIB_PATH} not built: run `make -C {_HERE}` (hipcc --offload-arch=gfx950)")

@@ -65,7 +65,28 @@ template <> struct UInt<64> { using type = uint64_t; };
 __device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
 // keep unrolled iterations in program order: bounds register pressure to one
 // iteration (the occupancy, not the ILP of one wave, hides latency here)
+// full 16-byte output store (FLS_NT_STORE: non-temporal streaming store)
+__device__ __forceinline__ void st16(FLS_GLOBAL v4u *p, v4u v) {
+#ifdef FLS_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+// packed-bit load (FLS_NT_LOAD: non-temporal, read-once stream)
+__device__ __forceinline__ v4u ld16(const FLS_GLOBAL v4u *p) {
+#ifdef FLS_NT_LOAD
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
+#ifdef FLS_NO_SEQ
+__device__ __forceinline__ void seq() {}
+#else
 __device__ __forceinline__ void seq() { __builtin_amdgcn_sched_barrier(0); }
+#endif
 __device__ __forceinline__ uint32_t bitrev3(uint32_t g) { return ((g & 1) << 2) | (g & 2) | ((g >> 2) & 1); }
 
 // per-lane copy of the chunk's VecMeta[lane]
@@ -105,24 +126,29 @@ __device__ __forceinline__ VecInfo vec_info(const ChunkMetas &m, uint32_t v) {
 }
 
 // ---- packed-bit prefetch (registers) and staging (LDS) --------------------
-// L = T/8 = max uint4 per lane (W <= T -> 8W <= 8T uint4 per vector).  Every
-// lane issues exactly L loads (out-of-range lanes re-read a safe dummy line)
-// so the loop body's vmcnt arithmetic is static.
+// L = T/8 = max 16-byte loads per lane (W <= T -> 8W <= 8T per vector).  Load
+// instruction i is issued only when some lane needs it (a wave-uniform
+// branch on W); inside it, lanes past the end re-read a safe dummy line.  The
+// waits stay exact: what follows the prefetch (the stores) is fixed per path.
 template <int L>
 __device__ __forceinline__ void prefetch(gv4 *__restrict__ src, uint32_t n16, gv4 *__restrict__ dummy,
                                          uint32_t lane, v4u (&r)[L]) {
 #pragma unroll
     for (int i = 0; i < L; ++i) {
-        const uint32_t idx = lane + 64 * i;
-        r[i] = *(idx < n16 ? src + idx : dummy);
+        if (64 * i < n16) {
+            const uint32_t idx = lane + 64 * i;
+            r[i] = ld16(idx < n16 ? src + idx : dummy);
+        }
     }
 }
 template <int L>
 __device__ __forceinline__ void stage(lv4 *__restrict__ P, const v4u (&r)[L], uint32_t n16, uint32_t lane) {
 #pragma unroll
     for (int i = 0; i < L; ++i) {
-        const uint32_t idx = lane + 64 * i;
-        if (idx < n16) P[idx] = r[i];
+        if (64 * i < n16) {
+            const uint32_t idx = lane + 64 * i;
+            if (idx < n16) P[idx] = r[i];
+        }
     }
     if (lane < 8) P[n16 + lane] = mk4(0, 0, 0, 0);
 }
@@ -143,7 +169,7 @@ __device__ __forceinline__ void ffor_vec(const lv4 *__restrict__ P, uint32_t W, 
     for (uint32_t j = 0; j < T / 8; ++j) {
         const uint32_t ci = lane + 64 * j;
         const v4u v = add_base<T>(unpack_chunk<T>(P, W, ci), base);
-        if (FULL) reinterpret_cast<ov4 *>(out)[ci] = v;
+        if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, v);
         else store16<T / 8>(out, 16 * ci, limit, v);
         seq();
     }
@@ -198,7 +224,7 @@ __device__ __forceinline__ void delta64_vec(const lv4 *__restrict__ P, uint32_t 
         const uint64_t v0 = p0 + a0[j], v1 = p1 + a1[j];
         const v4u v = mk4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
         const uint32_t off = 128 * (8 * s + j) + 16 * q;
-        if (FULL) *reinterpret_cast<ov4 *>(out + off) = v;
+        if (FULL) st16(reinterpret_cast<ov4 *>(out + off), v);
         else store16<8>(out, off, limit, v);
     }
 }
@@ -282,7 +308,7 @@ __device__ __forceinline__ void copy_out(const lu8 *__restrict__ V, ou8 *__restr
     for (uint32_t j = 0; j < EB; ++j) {
         const uint32_t ci = lane + 64 * j;
         const v4u x = *reinterpret_cast<const lv4 *>(V + 16 * ci);
-        if (FULL) reinterpret_cast<ov4 *>(out)[ci] = x;
+        if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, x);
         else store16<EB>(out, 16 * ci, limit, x);
         seq();
     }
@@ -318,7 +344,7 @@ __device__ __forceinline__ void gather_out(TabF tab, ou8 *__restrict__ out, uint
             }
         }
         const v4u v = mk4(w[0], w[1], w[2], w[3]);
-        if (FULL) reinterpret_cast<ov4 *>(out)[oc] = v;
+        if (FULL) st16(reinterpret_cast<ov4 *>(out) + oc, v);
         else store16<OB == 16 ? 8 : OB>(out, 16 * oc, limit, v);
         seq();
     }
