@@ -260,7 +260,7 @@ class Connection:
 
     def read_image(self, img, copy: bool = False) -> "Table":
         h = _P()
-        if isinstance(img, Image):
+        if hasattr(img, "ptr") and hasattr(img, "len"):  # an Image (possibly from another loaded build)
             _check(_lib.fls_read_fls_image(self.h, img.ptr, img.len, int(copy), C.byref(h)))
             t = Table(h.value, self)
             t._keep = img

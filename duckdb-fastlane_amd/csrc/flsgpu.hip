@@ -154,6 +154,7 @@ struct Slot {                       // one batch of row groups in flight
     DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
 };
 
 struct ScanDev {
@@ -293,8 +294,11 @@ fls_table::~fls_table() {
         for (auto &d : s->devs) {
             hipSetDevice(d.dev);
             if (d.stream) hipStreamSynchronize(d.stream);
-            for (auto &sl : d.slots)
+            for (auto &sl : d.slots) {
+                if (sl.stream) hipStreamSynchronize(sl.stream);
                 if (sl.done) hipEventDestroy(sl.done);
+                if (sl.stream) hipStreamDestroy(sl.stream);
+            }
             if (d.stream) hipStreamDestroy(d.stream);
         }
     if (registered) hipHostUnregister((void *)img);
@@ -312,7 +316,10 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     for (auto &d : s.devs) {
         hipSetDevice(d.dev);
         if (d.stream) hipStreamSynchronize(d.stream);
-        for (auto &sl : d.slots) sl.busy = false;
+        for (auto &sl : d.slots) {
+            if (sl.stream) hipStreamSynchronize(sl.stream);
+            sl.busy = false;
+        }
     }
     s.mask.assign(ncols, 1);
     if (col_mask)
@@ -327,8 +334,10 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     if (s.devs.size() != G) {
         for (auto &d : s.devs) {
             hipSetDevice(d.dev);
-            for (auto &sl : d.slots)
+            for (auto &sl : d.slots) {
                 if (sl.done) hipEventDestroy(sl.done);
+                if (sl.stream) hipStreamDestroy(sl.stream);
+            }
             if (d.stream) hipStreamDestroy(d.stream);
         }
         s.devs.clear();
@@ -343,6 +352,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         for (auto &sl : d.slots) {
             if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+            if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
             sl.d_out.resize(ncols);
             sl.h_out.resize(ncols);
         }
@@ -353,6 +363,12 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         if (rc) return rc;
         HIP_TRY(d.err.alloc(d.dev, 1));
         HIP_TRY(hipMemsetAsync(d.err.p, 0, sizeof(uint32_t), d.stream));
+        HIP_TRY(hipStreamSynchronize(d.stream));
+    }
+    // pin the file image once so batch uploads are true async DMA
+    if (!t->registered && t->len > 0) {
+        if (hipHostRegister((void *)t->img, t->len, hipHostRegisterDefault) == hipSuccess) t->registered = true;
+        else (void)hipGetLastError();  // fall back to staged (pageable) copies
     }
     s.active = true;
     return 0;
@@ -372,7 +388,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     rg_byte_range(t->meta, sl.rg0, sl.rg0 + sl.nrg, lo, hi);
     HIP_TRY(sl.d_in.alloc(d.dev, hi - lo));
     sl.in_base = lo;
-    HIP_TRY(hipMemcpyAsync(sl.d_in.p, t->img + lo, hi - lo, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, t->img + lo, hi - lo, hipMemcpyHostToDevice, sl.stream));
     // 2. decode into the slot's device columns
     const uint64_t max_rows = (uint64_t)s.batch * kRowGroupSize;
     uint32_t nsel = 0;
@@ -397,17 +413,17 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             sl.h_chunks.p[k++] = make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc);
         }
     }
-    HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(launch_decode(sl.d_chunks.p, (uint32_t)k, d.err.p, bc.geom, d.stream));
+    HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
+    HIP_TRY(launch_decode(sl.d_chunks.p, (uint32_t)k, d.err.p, bc.geom, sl.stream));
     // 3. D2H into pinned host columns
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
         HIP_TRY(hipMemcpyAsync(sl.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
-                               d.stream));
+                               sl.stream));
     }
-    HIP_TRY(hipEventRecord(sl.done, d.stream));
+    HIP_TRY(hipEventRecord(sl.done, sl.stream));
     sl.busy = true;
     return 0;
 }

@@ -195,3 +195,22 @@ def test_corrupt_dictionary_code_is_reported(fl, ref, gpu):
     with pytest.raises(fl.FlsError, match="corrupt"):
         t.device_sync()
     del rf
+
+
+def test_scan_sharded_over_two_device_slots(fl, ref, gpu, monkeypatch):
+    """The in-process multi-GPU scan path (one stream + two-slot pipeline per
+    device, contiguous row-group ranges, in-order delivery) exercised with the
+    same GPU listed twice."""
+    monkeypatch.setenv("FLS_SCAN_BATCH", "2")
+    img = fl.gen_image("lineitem", 0.1)
+    rf = ref.RefFile(img)
+    conn = fl.Connection([0, 0])
+    t = conn.read_image(img)
+    got = list(t.scan(cols=[0, 5, 14]))
+    assert [r // 65536 for r, _ in got] == list(range(rf.nrowgroups))
+    for first, cols in got:
+        rg = first // 65536
+        assert np.array_equal(cols[0], rf.decode(0, rg)) and np.array_equal(cols[5], rf.decode(5, rg))
+    # materialize picks the owning device of the row group
+    first, cols = t.materialize(rf.nrowgroups - 1, cols=[0])
+    assert np.array_equal(cols[0], rf.decode(0, rf.nrowgroups - 1))
