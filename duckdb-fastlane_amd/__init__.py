@@ -101,6 +101,7 @@ _sig("fls_writer_new", _P, C.c_uint64)
 _sig("fls_writer_free", None, _P)
 _sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8)
 _sig("fls_writer_add_rowgroup", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P))
+_sig("fls_writer_set_rowgroup_size", C.c_int, _P, C.c_uint32)
 _sig("fls_writer_finish_file", C.c_int, _P, C.c_char_p)
 _sig("fls_writer_finish_image", C.c_int, _P, C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_image_free", None, _P)
@@ -195,6 +196,7 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0) -> Image
     values: numpy int array for integer types, list of str/bytes for VARCHAR."""
     w = _lib.fls_writer_new(row_offset)
     try:
+        _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))
         n = None
         prepped = []
         for spec in columns:

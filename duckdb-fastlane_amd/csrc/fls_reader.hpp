@@ -58,7 +58,7 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
     rd(p + 20, &rgsz, 4);
     rd(p + 24, &m.row_offset, 8);
     if (ver != kFooterVersion) return "unsupported footer version";
-    if (rgsz != kRowGroupSize) return "unsupported row-group size";
+    if (rgsz == 0 || rgsz > kRowGroupSize || rgsz % kVectorSize) return "unsupported row-group size";
     if (ncols == 0 || ncols > 4096) return "bad column count";
     m.rowgroup_size = rgsz;
     p += kFooterFixed;
@@ -80,8 +80,8 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
         auto &rg = m.rgs[r];
         if (p + 4 + 16ull * ncols > fend) return "truncated row-group descriptor";
         rd(p, &rg.nrows, 4);
-        if (rg.nrows == 0 || rg.nrows > kRowGroupSize) return "bad row-group row count";
-        if (r + 1 < nrg && rg.nrows != kRowGroupSize) return "short row group before the last";
+        if (rg.nrows == 0 || rg.nrows > rgsz) return "bad row-group row count";
+        if (r + 1 < nrg && rg.nrows != rgsz) return "short row group before the last";
         rg.first_row = rows;
         rows += rg.nrows;
         rg.chunks.resize(ncols);

@@ -395,6 +395,7 @@ std::vector<uint8_t> encode_int_chunk(uint8_t type, uint8_t enc, const uint64_t 
 struct FileBuilder {
     std::vector<ColSpec> cols;
     uint64_t row_offset = 0;
+    uint32_t rowgroup_size = kRowGroupSize;  // rows per row group (all but the last)
     struct RG {
         uint32_t nrows;
         std::vector<std::vector<uint8_t>> chunks;
@@ -404,7 +405,7 @@ struct FileBuilder {
     std::vector<uint8_t> footer(const std::vector<uint64_t> &chunk_offs) const {
         std::vector<uint8_t> f;
         auto put = [&f](const void *p, size_t n) { f.insert(f.end(), (const uint8_t *)p, (const uint8_t *)p + n); };
-        uint32_t ver = kFooterVersion, ncols = (uint32_t)cols.size(), nrg = (uint32_t)rgs.size(), rgsz = kRowGroupSize;
+        uint32_t ver = kFooterVersion, ncols = (uint32_t)cols.size(), nrg = (uint32_t)rgs.size(), rgsz = rowgroup_size;
         uint64_t nrows = 0;
         for (auto &r : rgs) nrows += r.nrows;
         put(&ver, 4); put(&ncols, 4); put(&nrows, 8); put(&nrg, 4); put(&rgsz, 4); put(&row_offset, 8);
@@ -624,8 +625,11 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
 int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *data,
                             const uint32_t *const *str_offsets) {
     if (!w || !data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroup: NULL argument");
-    if (nrows == 0 || nrows > kRowGroupSize) return fail(FLS_ERR_ARG, "row group needs 1..65536 rows, got %u", nrows);
+    if (nrows == 0 || nrows > w->fb.rowgroup_size)
+        return fail(FLS_ERR_ARG, "row group needs 1..%u rows, got %u", w->fb.rowgroup_size, nrows);
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
+    if (!w->fb.rgs.empty() && w->fb.rgs.back().nrows != w->fb.rowgroup_size)
+        return fail(FLS_ERR_STATE, "only the last row group may be short");
     FileBuilder::RG rg;
     rg.nrows = nrows;
     for (size_t c = 0; c < w->fb.cols.size(); ++c) {
@@ -650,6 +654,16 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
         }
     }
     w->fb.rgs.push_back(std::move(rg));
+    return 0;
+}
+
+int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows) {
+    if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_rowgroup_size: NULL writer");
+    if (rows == 0 || rows > kRowGroupSize || rows % kVectorSize)
+        return fail(FLS_ERR_ARG, "row group size must be a multiple of %u in [%u, %u], got %u", kVectorSize, kVectorSize,
+                    kRowGroupSize, rows);
+    if (!w->fb.rgs.empty()) return fail(FLS_ERR_STATE, "fls_writer_set_rowgroup_size: after first row group");
+    w->fb.rowgroup_size = rows;
     return 0;
 }
 

@@ -390,7 +390,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     sl.in_base = lo;
     HIP_TRY(hipMemcpyAsync(sl.d_in.p, t->img + lo, hi - lo, hipMemcpyHostToDevice, sl.stream));
     // 2. decode into the slot's device columns
-    const uint64_t max_rows = (uint64_t)s.batch * kRowGroupSize;
+    const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
     uint32_t nsel = 0;
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
@@ -409,7 +409,8 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const ChunkRef &ch = t->meta.rgs[r].chunks[c];
             const uint64_t so = d.strtab_off[(size_t)(r - d.rg0) * ncols + c];
             const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
-            uint8_t *out = sl.d_out[c].p + (uint64_t)(r - sl.rg0) * kRowGroupSize * out_bytes_of(t, c);
+            uint8_t *out = sl.d_out[c].p +
+                           (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * out_bytes_of(t, c);
             sl.h_chunks.p[k++] = make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc);
         }
     }
@@ -465,7 +466,8 @@ int scan_next(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     for (uint32_t c = 0; c < ncols; ++c)
         s.col_ptrs[c] = col_selected(s.mask, c)
-                            ? sl.h_out[c].p + (uint64_t)(rg - sl.rg0) * kRowGroupSize * out_bytes_of(t, c)
+                            ? sl.h_out[c].p + (t->meta.rgs[rg].first_row - t->meta.rgs[sl.rg0].first_row) *
+                                                  out_bytes_of(t, c)
                             : nullptr;
     out->rowgroup = rg;
     out->nrows = t->meta.rgs[rg].nrows;

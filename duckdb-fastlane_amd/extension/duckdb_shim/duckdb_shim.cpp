@@ -187,6 +187,12 @@ Value Vector::GetValue(idx_t i) const {
 
 DBConfig &DBConfig::GetConfig(DatabaseInstance &db) { return db.config; }
 
+string StringUtil::Upper(const string &s) {
+    string r(s);
+    std::transform(r.begin(), r.end(), r.begin(), [](unsigned char c) { return (char)std::toupper(c); });
+    return r;
+}
+
 string StringUtil::Lower(const string &s) {
     string r(s);
     std::transform(r.begin(), r.end(), r.begin(), [](unsigned char c) { return (char)std::tolower(c); });

@@ -69,6 +69,10 @@ class InternalException : public Exception {
 public:
     explicit InternalException(const string &msg) : Exception(msg) {}
 };
+class CatalogException : public Exception {
+public:
+    explicit CatalogException(const string &msg) : Exception("Catalog Error: " + msg) {}
+};
 class NotImplementedException : public Exception {
 public:
     explicit NotImplementedException(const string &msg) : Exception(msg) {}
@@ -362,6 +366,47 @@ public:
     scalar_function_t function;
 };
 
+// ---- copy functions (COPY ... TO 'x' (FORMAT name, options)) ----------------
+struct GlobalFunctionData {
+    virtual ~GlobalFunctionData() = default;
+    template <class T>
+    T &Cast() { return static_cast<T &>(*this); }
+};
+struct LocalFunctionData {
+    virtual ~LocalFunctionData() = default;
+    template <class T>
+    T &Cast() { return static_cast<T &>(*this); }
+};
+struct CopyInfo {
+    std::map<string, vector<Value>> options;  // option name -> values
+};
+struct CopyFunctionBindInput {
+    const CopyInfo &info;
+};
+using copy_to_bind_t = unique_ptr<FunctionData> (*)(ClientContext &, CopyFunctionBindInput &, const vector<string> &,
+                                                    const vector<LogicalType> &);
+using copy_to_initialize_global_t = unique_ptr<GlobalFunctionData> (*)(ClientContext &, FunctionData &,
+                                                                      const string &);
+using copy_to_initialize_local_t = unique_ptr<LocalFunctionData> (*)(ExecutionContext &, FunctionData &);
+using copy_to_sink_t = void (*)(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &,
+                                DataChunk &);
+using copy_to_combine_t = void (*)(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &);
+using copy_to_finalize_t = void (*)(ClientContext &, FunctionData &, GlobalFunctionData &);
+
+class CopyFunction {
+public:
+    explicit CopyFunction(string name) : name(std::move(name)) {}
+    string name;
+    string extension;
+    copy_to_bind_t copy_to_bind = nullptr;
+    copy_to_initialize_global_t copy_to_initialize_global = nullptr;
+    copy_to_initialize_local_t copy_to_initialize_local = nullptr;
+    copy_to_sink_t copy_to_sink = nullptr;
+    copy_to_combine_t copy_to_combine = nullptr;
+    copy_to_finalize_t copy_to_finalize = nullptr;
+    std::function<TableFunction()> copy_from_function;  // COPY ... FROM
+};
+
 // ---- replacement scans -----------------------------------------------------
 class ParsedExpression {
 public:
@@ -411,6 +456,7 @@ public:
     DBConfig config;
     std::multimap<string, TableFunction> table_functions;
     std::multimap<string, ScalarFunction> scalar_functions;
+    std::map<string, CopyFunction> copy_functions;
 };
 
 class DuckDB {
@@ -435,10 +481,14 @@ struct ExtensionUtil {
     static void RegisterFunction(DatabaseInstance &db, ScalarFunction fn) {
         db.scalar_functions.emplace(fn.name, std::move(fn));
     }
+    static void RegisterFunction(DatabaseInstance &db, CopyFunction fn) {
+        db.copy_functions.emplace(fn.name, std::move(fn));
+    }
 };
 
 struct StringUtil {
     static string Lower(const string &s);
+    static string Upper(const string &s);
     static bool EndsWith(const string &s, const string &suffix) {
         return s.size() >= suffix.size() && s.compare(s.size() - suffix.size(), suffix.size(), suffix) == 0;
     }

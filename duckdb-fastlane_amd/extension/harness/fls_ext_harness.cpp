@@ -266,4 +266,82 @@ int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const in
     }
 }
 
+// COPY (SELECT <proj> FROM fn(src)) TO dst (FORMAT format, key value, ...):
+// bind -> init_global -> init_local -> sink per chunk -> combine -> finalize,
+// the order DuckDB's PhysicalCopyToFile drives a CopyFunction.  Option values
+// are passed as VARCHAR (DuckDB hands the parsed constants; the bind parses).
+int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj, int nproj, const char *format,
+                 const char *dst, const char *const *opt_keys, const char *const *opt_vals, int nopts,
+                 uint64_t *rows) {
+    try {
+        const std::string fmt = StringUtil::Lower(format ? format : "");
+        auto it = d->db.copy_functions.find(fmt);
+        if (it == d->db.copy_functions.end())
+            throw CatalogException("Copy Function with name " + fmt + " does not exist!");
+        CopyFunction &cf = it->second;
+        CopyInfo info;
+        for (int i = 0; i < nopts; ++i) info.options[StringUtil::Lower(opt_keys[i])].push_back(Value(opt_vals[i]));
+        const char *args[1] = {src};
+        Query q = make_query(d, fn, args, 1, 0);
+        std::vector<int> pv(proj, proj + (proj ? nproj : 0));
+        // the source's schema (a bind-only pass, as DuckDB binds the SELECT first)
+        std::vector<std::string> names;
+        std::vector<LogicalType> types;
+        {
+            TableFunction *f = lookup(d, q);
+            named_parameter_map_t named;
+            TableFunctionBindInput bin{q.args, named};
+            vector<LogicalType> rtypes;
+            vector<string> rnames;
+            f->bind(d->ctx, bin, rtypes, rnames);
+            if (pv.empty()) {
+                names.assign(rnames.begin(), rnames.end());
+                types.assign(rtypes.begin(), rtypes.end());
+            } else {
+                for (int p : pv) {
+                    if (p < 0 || (size_t)p >= rtypes.size()) throw BinderException("projection index out of range");
+                    names.push_back(rnames[p]);
+                    types.push_back(rtypes[p]);
+                }
+            }
+        }
+        CopyFunctionBindInput cbin{info};
+        auto bind = cf.copy_to_bind(d->ctx, cbin, vector<string>(names.begin(), names.end()),
+                                    vector<LogicalType>(types.begin(), types.end()));
+        auto gstate = cf.copy_to_initialize_global(d->ctx, *bind, dst ? dst : "");
+        ExecutionContext ectx(d->ctx);
+        auto lstate = cf.copy_to_initialize_local(ectx, *bind);
+        DataChunk out;
+        out.Initialize(vector<LogicalType>(types.begin(), types.end()));
+        uint64_t n = 0;
+        std::vector<std::string> n2;
+        std::vector<LogicalType> t2;
+        execute(d, q, pv, -1, n2, t2, [&](DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+            bool identity = pick.size() == c.ColumnCount() && cnt == c.size();
+            for (size_t k = 0; identity && k < pick.size(); ++k) identity = pick[k] == k;
+            if (identity) {
+                cf.copy_to_sink(ectx, *bind, *gstate, *lstate, c);
+            } else {
+                out.Reset();
+                for (size_t k = 0; k < pick.size(); ++k)
+                    for (idx_t i = 0; i < cnt; ++i) out.data[k].SetValue(i, c.data[pick[k]].GetValue(i));
+                out.SetCardinality(cnt);
+                cf.copy_to_sink(ectx, *bind, *gstate, *lstate, out);
+            }
+            n += cnt;
+        });
+        if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
+        cf.copy_to_finalize(d->ctx, *bind, *gstate);
+        if (rows) *rows = n;
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int fls_ext_has_copy_function(fls_ext_db *d, const char *name) {
+    return d && d->db.copy_functions.count(name) ? 1 : 0;
+}
+
 }  // extern "C"

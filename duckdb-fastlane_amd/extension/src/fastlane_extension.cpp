@@ -1,8 +1,9 @@
 // fastlane_extension.cpp -- extension entry points (reference
 // src/fastlane_extension.cpp:94-124): the same two C symbols and class.
-// Load registers the reference's compiled `scan_fastlanes` plus the typed GPU
-// `read_fastlanes` (VARCHAR and LIST(VARCHAR)) and the .fls/.fastlane
-// replacement scan the reference wrote but never registered (:44-90).
+// Load registers the reference's compiled `scan_fastlanes` plus what the
+// reference wrote but never registered (:44-90): the typed GPU scan (here
+// `read_fastlanes`, VARCHAR and LIST(VARCHAR)), the .fls/.fastlane replacement
+// scan, and the COPY TO (FORMAT fls | fastlane) writer.
 #define DUCKDB_EXTENSION_MAIN
 
 #include "fastlane_extension.hpp"
@@ -10,12 +11,14 @@
 #include "duckdb.hpp"
 #include "scan_fastlanes.hpp"
 #include "table_function/read_fastlanes.hpp"
+#include "writer/copy_fastlanes.hpp"
 
 namespace duckdb {
 
 void FastlaneExtension::Load(DuckDB &db) {
     ScanFastLanes::Register(*db.instance);
     ext_fastlane::RegisterReadFastlanes(*db.instance);
+    ext_fastlane::RegisterFastlaneCopyFunction(*db.instance);
 }
 
 std::string FastlaneExtension::Name() { return "fastlane"; }

@@ -40,7 +40,12 @@ public:
     bool createFile(const std::string &file_path, const std::vector<LogicalType> &types,
                     const std::vector<std::string> &names);
     bool writeChunk(DataChunk &chunk);
-    void finalizeFile();
+    // Not in the reference's header: rows per row group for the COPY option
+    // ROW_GROUP_SIZE (multiple of 1024, <= 65536); call after createFile.
+    bool setRowGroupSize(idx_t rows);
+    // Returns void in the reference's header; bool here so COPY can report
+    // write errors (a void caller ignores it).
+    bool finalizeFile();
 
     bool isValid() const;
 };

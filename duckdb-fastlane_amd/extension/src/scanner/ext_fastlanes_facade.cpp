@@ -35,6 +35,7 @@ public:
     std::vector<std::vector<uint8_t>> wcols;         // fixed-width buffered rows
     std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
     idx_t wrows = 0;
+    idx_t rg_rows = 65536;
 
     void close_read() {
         if (table) fls_table_close(table);
@@ -195,18 +196,26 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                 s.wcols[c].insert(s.wcols[c].end(), b, b + w);
             }
         }
-        if (++s.wrows == 65536 && !s.flush_rowgroup()) return false;
+        if (++s.wrows == s.rg_rows && !s.flush_rowgroup()) return false;
     }
     return true;
 }
 
-void FastLanesFacade::finalizeFile() {
+bool FastLanesFacade::setRowGroupSize(idx_t rows) {
     Impl &s = *pImpl;
-    if (!s.writer) return;
-    s.flush_rowgroup();
-    fls_writer_finish_file(s.writer, s.out_path.c_str());
+    if (!s.writer || s.wrows != 0 || fls_writer_set_rowgroup_size(s.writer, (uint32_t)rows) != 0) return false;
+    s.rg_rows = rows;
+    return true;
+}
+
+bool FastLanesFacade::finalizeFile() {
+    Impl &s = *pImpl;
+    if (!s.writer) return false;
+    bool ok = s.flush_rowgroup();
+    ok = fls_writer_finish_file(s.writer, s.out_path.c_str()) == 0 && ok;
     fls_writer_free(s.writer);
     s.writer = nullptr;
+    return ok;
 }
 
 }  // namespace ext_fastlane

@@ -1,0 +1,121 @@
+// copy_fastlanes.cpp -- the FastLanes COPY TO function.
+//
+// Option handling follows the reference's intended writer
+// (src/writer/write_fastlane_stream.cpp:65-107): ROW_GROUP_SIZE / CHUNK_SIZE
+// (default 65,536, :21-24), ROW_GROUP_SIZE_BYTES (rows = bytes / 1024 bytes per
+// row, :27), the same error texts.  Rows go through
+// ext_fastlane::FastLanesFacade::createFile/writeChunk/finalizeFile into the CPU
+// FastLanes writer (per-chunk encoding choice: FFOR / DELTA / DICT / RLE).
+// ROW_GROUPS_PER_FILE rotation is not supported by this writer (it would need
+// DuckDB's rotate_files hooks) and is rejected at bind time.
+#include "writer/copy_fastlanes.hpp"
+
+#include <mutex>
+
+#include "duckdb/common/string_util.hpp"
+#include "duckdb/main/extension_util.hpp"
+#include "fastlanes_facade.hpp"
+#include "table_function/read_fastlanes.hpp"
+
+namespace duckdb {
+namespace ext_fastlane {
+
+namespace {
+
+struct FastlaneCopyBindData : public TableFunctionData {
+    vector<LogicalType> sql_types;
+    vector<string> column_names;
+    idx_t row_group_size = 65536;
+    static constexpr idx_t BYTES_PER_ROW = 1024;
+};
+
+struct FastlaneCopyGlobalState : public GlobalFunctionData {
+    std::unique_ptr<FastLanesFacade> facade;
+    std::mutex lock;  // sinks may run on several threads; the writer is not thread-safe
+    string file_path;
+};
+
+struct FastlaneCopyLocalState : public LocalFunctionData {};
+
+idx_t ValidRowGroupSize(uint64_t rows) {
+    if (rows == 0 || rows > 65536 || rows % 1024)
+        throw BinderException("ROW_GROUP_SIZE must be a multiple of 1024 between 1024 and 65536 (FastLanes vectors)");
+    return rows;
+}
+
+unique_ptr<FunctionData> CopyBind(ClientContext &, CopyFunctionBindInput &input, const vector<string> &names,
+                                  const vector<LogicalType> &sql_types) {
+    auto bind = make_uniq<FastlaneCopyBindData>();
+    bool size_set = false;
+    for (auto &opt : input.info.options) {
+        const string name = StringUtil::Lower(opt.first);
+        if (opt.second.size() != 1) throw BinderException(StringUtil::Upper(name) + " requires exactly one argument");
+        const Value &v = opt.second[0];
+        if (name == "row_group_size" || name == "chunk_size" || name == "row_group_size_bytes") {
+            if (size_set) throw BinderException("ROW_GROUP_SIZE and ROW_GROUP_SIZE_BYTES are mutually exclusive");
+            size_set = true;
+            const uint64_t x = (uint64_t)std::stoull(v.ToString());
+            bind->row_group_size = name == "row_group_size_bytes"
+                                       ? ValidRowGroupSize(std::max<uint64_t>(1024, x / FastlaneCopyBindData::BYTES_PER_ROW / 1024 * 1024))
+                                       : ValidRowGroupSize(x);
+        } else if (name == "row_groups_per_file") {
+            throw BinderException("ROW_GROUPS_PER_FILE is not supported by the FastLanes writer");
+        } else {
+            throw BinderException("Unknown option for FastLanes: " + StringUtil::Upper(name));
+        }
+    }
+    bind->sql_types = sql_types;
+    bind->column_names = names;
+    return std::move(bind);
+}
+
+unique_ptr<GlobalFunctionData> CopyInitGlobal(ClientContext &, FunctionData &bind_p, const string &path) {
+    auto &bind = bind_p.Cast<FastlaneCopyBindData>();
+    auto state = make_uniq<FastlaneCopyGlobalState>();
+    state->facade = std::make_unique<FastLanesFacade>();
+    if (!state->facade->createFile(path, bind.sql_types, bind.column_names) ||
+        !state->facade->setRowGroupSize(bind.row_group_size)) {
+        throw IOException("Failed to create FastLanes file: " + path);
+    }
+    state->file_path = path;
+    return std::move(state);
+}
+
+unique_ptr<LocalFunctionData> CopyInitLocal(ExecutionContext &, FunctionData &) {
+    return make_uniq<FastlaneCopyLocalState>();
+}
+
+void CopySink(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, LocalFunctionData &, DataChunk &input) {
+    auto &g = gstate.Cast<FastlaneCopyGlobalState>();
+    std::lock_guard<std::mutex> guard(g.lock);
+    if (!g.facade->writeChunk(input)) throw IOException("Failed to write chunk to FastLanes");
+}
+
+void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &) {}
+
+void CopyFinalize(ClientContext &, FunctionData &, GlobalFunctionData &gstate) {
+    auto &g = gstate.Cast<FastlaneCopyGlobalState>();
+    std::lock_guard<std::mutex> guard(g.lock);
+    if (!g.facade->finalizeFile()) throw IOException("Failed to finalize FastLanes file: " + g.file_path);
+}
+
+}  // namespace
+
+void RegisterFastlaneCopyFunction(DatabaseInstance &db) {
+    CopyFunction fn("fls");
+    fn.copy_to_bind = CopyBind;
+    fn.copy_to_initialize_global = CopyInitGlobal;
+    fn.copy_to_initialize_local = CopyInitLocal;
+    fn.copy_to_sink = CopySink;
+    fn.copy_to_combine = CopyCombine;
+    fn.copy_to_finalize = CopyFinalize;
+    fn.copy_from_function = ReadFastlanesFunction;
+    fn.extension = "fls";
+    ExtensionUtil::RegisterFunction(db, fn);
+    fn.name = "fastlane";
+    fn.extension = "fastlane";
+    ExtensionUtil::RegisterFunction(db, fn);
+}
+
+}  // namespace ext_fastlane
+}  // namespace duckdb

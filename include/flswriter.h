@@ -38,7 +38,12 @@ fls_writer *fls_writer_new(uint64_t row_offset);
 void fls_writer_free(fls_writer *w);
 int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t width,
                           uint8_t scale, uint8_t encoding);
-/* Append one row group of nrows (1..65536) rows.  Integer column c:
+/* Rows per row group (multiple of 1024 in [1024, 65536]; default 65536, the
+ * reference's ROW_GROUP_SIZE default, src/writer/write_fastlane_stream.cpp:21-24).
+ * Must be called before the first row group. */
+int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows);
+/* Append one row group of nrows (1..row group size) rows; only the last row
+ * group of a file may be short.  Integer column c:
  * data[c] -> nrows values of the column's width (1/2/4/8 B).  VARCHAR column c:
  * data[c] -> concatenated bytes, str_offsets[c] -> nrows+1 uint32 offsets
  * (str_offsets may be NULL when there is no VARCHAR column). */

@@ -85,3 +85,25 @@ class Ext:
         if self.db:
             self.lib.fls_ext_close(self.db)
             self.db = None
+
+    def has_copy_function(self, name: str) -> bool:
+        self.lib.fls_ext_has_copy_function.argtypes = [C.c_void_p, C.c_char_p]
+        return bool(self.lib.fls_ext_has_copy_function(self.db, name.encode()))
+
+    def copy(self, fn, src, dst, fmt="fls", proj=None, **options):
+        """COPY (SELECT <proj> FROM fn(src)) TO dst (FORMAT fmt, key value ...);
+        returns the number of rows copied."""
+        lib = self.lib
+        lib.fls_ext_copy.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.c_int, C.c_char_p,
+                                     C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int,
+                                     C.POINTER(C.c_uint64)]
+        keys = list(options)
+        k = (C.c_char_p * max(1, len(keys)))(*[x.encode() for x in keys])
+        v = (C.c_char_p * max(1, len(keys)))(*[str(options[x]).encode() for x in keys])
+        p = (C.c_int * len(proj))(*proj) if proj else None
+        rows = C.c_uint64()
+        rc = lib.fls_ext_copy(self.db, fn.encode(), str(src).encode(), p, len(proj) if proj else 0, fmt.encode(),
+                              str(dst).encode(), k, v, len(keys), C.byref(rows))
+        if rc != 0:
+            raise ExtError(lib.fls_ext_last_error().decode())
+        return rows.value

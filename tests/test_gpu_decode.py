@@ -214,3 +214,25 @@ def test_scan_sharded_over_two_device_slots(fl, ref, gpu, monkeypatch):
     # materialize picks the owning device of the row group
     first, cols = t.materialize(rf.nrowgroups - 1, cols=[0])
     assert np.array_equal(cols[0], rf.decode(0, rf.nrowgroups - 1))
+
+
+@pytest.mark.parametrize("rgsz", [1024, 8192])
+def test_small_rowgroups_decode_and_scan(fl, ref, gpu, monkeypatch, rgsz):
+    """Files written with ROW_GROUP_SIZE < 65536 (COPY option): device decode
+    and the batched scan place row group r at first_row = r * rgsz."""
+    monkeypatch.setenv("FLS_SCAN_BATCH", "3")
+    rng = np.random.default_rng(rgsz)
+    n = 7 * rgsz + 333
+    a = rng.integers(-(1 << 40), 1 << 40, n)
+    b = np.cumsum(rng.integers(0, 9, n)).astype(np.int32)
+    s = [["AIR", "MAIL", "TRUCK", "REG AIR LONGER THAN TWELVE"][i] for i in rng.integers(0, 4, n)]
+    img = fl.write_image([("a", fl.INT64, a, fl.ENC_FFOR), ("b", fl.INT32, b, fl.ENC_DELTA),
+                          ("s", fl.VARCHAR, s, fl.ENC_DICT)], rowgroup=rgsz)
+    rf = ref.RefFile(img)
+    t, _ = _check_image(fl, ref, img)
+    got = list(t.scan())
+    assert [r for r, _ in got] == [g * rgsz for g in range(8)]
+    for first, cols in got:
+        g = first // rgsz
+        assert np.array_equal(cols[0], rf.decode(0, g)) and np.array_equal(cols[1], rf.decode(1, g))
+        assert fl.string_t_decode(cols[2]) == rf.strings(rf.decode(2, g))

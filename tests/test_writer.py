@@ -118,3 +118,24 @@ def test_shard_images_concatenate(fl, ref):
     got = np.concatenate([ref.RefFile(p).decode_column(0) for p in parts])
     assert np.array_equal(got, full.decode_column(0))
     assert [ref.RefFile(p).f.row_offset for p in parts] == [0, 3 * 65536, 5 * 65536]
+
+
+@pytest.mark.parametrize("rgsz", [1024, 4096, 20480])
+def test_custom_rowgroup_size(fl, ref, rgsz):
+    # COPY ... (ROW_GROUP_SIZE n) -- src/writer/write_fastlane_stream.cpp:75-90
+    rng = np.random.default_rng(rgsz)
+    n = 3 * rgsz + 555
+    a = rng.integers(-1000, 1000, n).astype(np.int32)
+    s = [f"k{i % 13}" for i in range(n)]
+    img = fl.write_image([("a", fl.INT32, a, fl.ENC_AUTO), ("s", fl.VARCHAR, s, fl.ENC_DICT)], rowgroup=rgsz)
+    rf = ref.RefFile(img)
+    assert rf.f.rowgroup_size == rgsz and rf.nrowgroups == 4
+    assert [rf.rowgroup_rows(g) for g in range(4)] == [rgsz] * 3 + [555]
+    assert np.array_equal(rf.decode_column(0).view(np.int32), a)
+    assert rf.strings(rf.decode_column(1)) == [x.encode() for x in s]
+
+
+@pytest.mark.parametrize("rgsz", [0, 1000, 65537, 131072])
+def test_bad_rowgroup_size_rejected(fl, rgsz):
+    with pytest.raises(fl.FlsError):
+        fl.write_image([("a", fl.INT32, np.arange(10), fl.ENC_FFOR)], rowgroup=rgsz)
