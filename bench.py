@@ -105,6 +105,16 @@ def host_threads(args) -> int:
     return max(1, min(16, os.cpu_count() or 1))
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(fl, args, nthreads: int, nrows_total: int):
     """Oracle (CPU restatement, 'port') on a bounded sample of the same workload."""
     from oracle import flsref
@@ -124,13 +134,24 @@ def cpu_baseline(fl, args, nthreads: int, nrows_total: int):
         for c in range(rf.ncols):
             rf.decode_column(c, nthreads)
     dt = time.perf_counter() - t0
+    # the same restatement on one core (SURVEY.md 8(d) asks for both numbers)
+    t0 = time.perf_counter()
+    reps1 = 0
+    while reps1 == 0 or time.perf_counter() - t0 < args.cpu_seconds / 4:
+        for c in range(rf.ncols):
+            rf.decode_column(c, 1)
+        reps1 += 1
+    dt1 = time.perf_counter() - t0
     return {
         "value": vals_per_pass * reps / dt,
+        "value_1core": vals_per_pass * reps1 / dt1,
+        "cpu_model": cpu_model(),
         "unit": "values/s",
         "cores": nthreads,
         "kind": "port",
         "sample": f"{args.workload} row groups [0,{sample_rg}) = {rf.nrows} rows x {rf.ncols} cols, "
-                  f"oracle/flsref.c (gcc -O3), {nthreads} threads, {reps} passes in {dt:.1f} s",
+                  f"oracle/flsref.c (gcc -O3), {nthreads} threads, {reps} passes in {dt:.1f} s; "
+                  f"1 thread: {reps1} passes in {dt1:.1f} s",
     }
 
 

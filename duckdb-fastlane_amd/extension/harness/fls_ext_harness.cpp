@@ -222,8 +222,10 @@ const char *fls_ext_result_value(const fls_ext_result *r, int64_t row, int col) 
 }
 void fls_ext_result_free(fls_ext_result *r) { delete r; }
 
-// Stream a query without materialising it: rows, an order-dependent checksum
-// over the raw DataChunk bytes (string_t by content) and wall seconds.
+// Stream a query without materialising it: rows, a checksum over the raw
+// DataChunk bytes (string_t by content) and wall seconds.  The checksum is
+// order-dependent within each column and independent of chunk boundaries
+// (per-column FNV-1a over the values, combined at the end).
 int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj, uint64_t *rows,
                        uint64_t *checksum, double *seconds) {
     try {
@@ -232,30 +234,36 @@ int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const in
         std::vector<std::string> names;
         std::vector<LogicalType> types;
         std::vector<int> pv(proj, proj + (proj ? nproj : 0));
-        uint64_t n = 0, h = 1469598103934665603ull;
+        uint64_t n = 0;
+        std::vector<uint64_t> hs;
         auto t0 = std::chrono::steady_clock::now();
         execute(d, q, pv, -1, names, types, [&](DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
-            for (size_t k : pick) {
-                Vector &v = c.data[k];
+            if (hs.empty()) hs.assign(pick.size(), 1469598103934665603ull);
+            for (size_t j = 0; j < pick.size(); ++j) {
+                Vector &v = c.data[pick[j]];
+                uint64_t h = hs[j];
                 if (v.GetType().id() == LogicalTypeId::VARCHAR) {
                     const string_t *s = FlatVector::GetData<string_t>(v);
                     for (idx_t i = 0; i < cnt; ++i) {
                         const char *p = s[i].GetData();
-                        for (uint32_t j = 0; j < s[i].GetSize(); ++j) h = (h ^ (uint8_t)p[j]) * 1099511628211ull;
+                        for (uint32_t k = 0; k < s[i].GetSize(); ++k) h = (h ^ (uint8_t)p[k]) * 1099511628211ull;
                         h = (h ^ 0xFF) * 1099511628211ull;
                     }
                 } else {
                     const idx_t w = v.GetType().PhysicalSize();
                     const uint8_t *p = v.GetData();
-                    for (idx_t i = 0; i < cnt * w; i += 8) {
+                    for (idx_t i = 0; i < cnt; ++i) {
                         uint64_t x = 0;
-                        memcpy(&x, p + i, std::min<idx_t>(8, cnt * w - i));
+                        memcpy(&x, p + i * w, w);
                         h = (h ^ x) * 1099511628211ull;
                     }
                 }
+                hs[j] = h;
             }
             n += cnt;
         });
+        uint64_t h = 1469598103934665603ull;
+        for (uint64_t x : hs) h = (h ^ x) * 1099511628211ull;
         *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         *rows = n;
         *checksum = h;

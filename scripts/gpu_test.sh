@@ -14,4 +14,8 @@ rc2=$?; echo "smoke rc=$rc2"; tail -2 gpurun_out/smoke_$TAG.log
 [ $rc2 -eq 0 ] || exit $rc2
 timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log
 rc3=$?; echo "bench rc=$rc3"; cat gpurun_out/bench_$TAG.json
-exit $((rc + rc3))
+[ $rc3 -eq 0 ] || exit $rc3
+# same bench without the PMC child passes (checks they do not perturb timing)
+timeout -k 10 400 python bench.py --no-traffic --cpu-seconds 0 > gpurun_out/bench_${TAG}_nt.json 2>> gpurun_out/bench_$TAG.log
+rc4=$?; echo "bench(no traffic) rc=$rc4"; cat gpurun_out/bench_${TAG}_nt.json
+exit $((rc + rc4))
