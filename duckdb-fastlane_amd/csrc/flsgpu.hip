@@ -12,7 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <vector>
@@ -155,6 +157,8 @@ struct Slot {                       // one batch of row groups in flight
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
+    uint32_t released = 0;          // row groups of the batch handed back by consumers
+    std::vector<const void *> col_ptrs;  // per (rg - rg0) * ncols + col: pinned host column start
 };
 
 struct ScanDev {
@@ -175,8 +179,12 @@ struct ScanCtx {
     uint32_t rg0 = 0, rg1 = 0, cur = 0;
     uint32_t batch = 8;
     std::vector<ScanDev> devs;
-    int release_dev = -1, release_slot = -1;   // slot to refill at the next call
-    std::vector<const void *> col_ptrs;
+    int64_t held = -1;              // row group fls_scan_next handed out last (released on the next call)
+    // fls_scan_acquire/release may be called from several consumer threads:
+    // claiming a row group, releasing one and refilling a slot happen under mu;
+    // waiting for a batch's decode does not.
+    std::mutex mu;
+    std::condition_variable cv;
 };
 
 }  // namespace
@@ -327,8 +335,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     s.rg0 = rg0;
     s.rg1 = rg1;
     s.cur = rg0;
-    s.release_dev = s.release_slot = -1;
-    s.col_ptrs.assign(ncols, nullptr);
+    s.held = -1;
     const auto &devs = t->conn->devices;
     const uint32_t G = (uint32_t)devs.size(), nrg = rg1 - rg0;
     if (s.devs.size() != G) {
@@ -425,6 +432,14 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                                sl.stream));
     }
     HIP_TRY(hipEventRecord(sl.done, sl.stream));
+    sl.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
+    for (uint32_t r = 0; r < sl.nrg; ++r)
+        for (uint32_t c = 0; c < ncols; ++c)
+            if (col_selected(s.mask, c))
+                sl.col_ptrs[(size_t)r * ncols + c] =
+                    sl.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) *
+                                        out_bytes_of(t, c);
+    sl.released = 0;
     sl.busy = true;
     return 0;
 }
@@ -438,24 +453,35 @@ int scan_start(fls_table *t, ScanCtx &s) {
     return 0;
 }
 
-int scan_next(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
-    if (!s.active) return fail(FLS_ERR_STATE, "scan not started");
-    // refill the slot the consumer has finished with
-    if (s.release_dev >= 0) {
-        ScanDev &d = s.devs[s.release_dev];
-        int rc = enqueue_batch(t, s, d, s.release_slot);
-        s.release_dev = s.release_slot = -1;
-        if (rc) return rc;
-    }
-    if (s.cur >= s.rg1) return 0;
-    const uint32_t rg = s.cur;
-    int g = -1, si = -1;
-    for (size_t i = 0; i < s.devs.size() && g < 0; ++i)
+// the (device, slot) holding row group rg, or false if its batch is not enqueued
+bool find_slot(ScanCtx &s, uint32_t rg, int &g, int &si) {
+    for (size_t i = 0; i < s.devs.size(); ++i)
         for (int j = 0; j < 2; ++j) {
             const Slot &sl = s.devs[i].slots[j];
-            if (sl.busy && rg >= sl.rg0 && rg < sl.rg0 + sl.nrg) { g = (int)i; si = j; break; }
+            if (sl.busy && rg >= sl.rg0 && rg < sl.rg0 + sl.nrg) {
+                g = (int)i;
+                si = j;
+                return true;
+            }
         }
-    if (g < 0) return fail(FLS_ERR_STATE, "internal: row group %u not in flight", rg);
+    return false;
+}
+
+// Claim the next row group in order and wait until its batch is decoded and
+// copied back.  Its buffers stay valid until scan_release(rg).
+int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
+    if (!s.active) return fail(FLS_ERR_STATE, "scan not started");
+    int g = -1, si = -1;
+    uint32_t rg;
+    {
+        std::unique_lock<std::mutex> lk(s.mu);
+        if (s.cur >= s.rg1) return 0;
+        rg = s.cur++;
+        // the batch holding rg is enqueued once every row group of the slot's
+        // previous batch has been released (by this or another consumer)
+        s.cv.wait(lk, [&] { return !s.active || find_slot(s, rg, g, si); });
+        if (!s.active) return fail(FLS_ERR_STATE, "scan ended while waiting for row group %u", rg);
+    }
     ScanDev &d = s.devs[g];
     Slot &sl = d.slots[si];
     HIP_TRY(hipSetDevice(d.dev));
@@ -464,22 +490,39 @@ int scan_next(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
     if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
-    for (uint32_t c = 0; c < ncols; ++c)
-        s.col_ptrs[c] = col_selected(s.mask, c)
-                            ? sl.h_out[c].p + (t->meta.rgs[rg].first_row - t->meta.rgs[sl.rg0].first_row) *
-                                                  out_bytes_of(t, c)
-                            : nullptr;
     out->rowgroup = rg;
     out->nrows = t->meta.rgs[rg].nrows;
     out->first_row = t->meta.row_offset + t->meta.rgs[rg].first_row;
     out->ncols = ncols;
-    out->columns = s.col_ptrs.data();
-    s.cur++;
-    if (rg + 1 == sl.rg0 + sl.nrg) {  // batch fully delivered: refill on next call
-        s.release_dev = g;
-        s.release_slot = si;
-    }
+    out->columns = sl.col_ptrs.data() + (size_t)(rg - sl.rg0) * ncols;
     return 1;
+}
+
+int scan_release(fls_table *t, ScanCtx &s, uint32_t rg) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    int g = -1, si = -1;
+    if (!s.active || !find_slot(s, rg, g, si)) return fail(FLS_ERR_ARG, "row group %u is not held by this scan", rg);
+    ScanDev &d = s.devs[g];
+    Slot &sl = d.slots[si];
+    if (++sl.released < sl.nrg) return 0;
+    // every row group of the batch is back: reuse the slot for the next batch
+    sl.busy = false;
+    int rc = enqueue_batch(t, s, d, si);
+    s.cv.notify_all();
+    return rc;
+}
+
+// single-consumer form: releases the previously delivered row group
+int scan_next(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
+    if (s.held >= 0) {
+        const uint32_t prev = (uint32_t)s.held;
+        s.held = -1;
+        int rc = scan_release(t, s, prev);
+        if (rc) return rc;
+    }
+    int rc = scan_acquire(t, s, out);
+    if (rc == 1) s.held = out->rowgroup;
+    return rc;
 }
 
 int ensure_stream(fls_table *t, int dev) {
@@ -615,6 +658,16 @@ int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uin
 int fls_scan_next(fls_table *t, fls_rowgroup *out) {
     if (!t || !out) return fail(FLS_ERR_ARG, "fls_scan_next: NULL argument");
     return scan_next(t, t->scan, out);
+}
+
+int fls_scan_acquire(fls_table *t, fls_rowgroup *out) {
+    if (!t || !out) return fail(FLS_ERR_ARG, "fls_scan_acquire: NULL argument");
+    return scan_acquire(t, t->scan, out);
+}
+
+int fls_scan_release(fls_table *t, uint32_t rowgroup) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_release: NULL table");
+    return scan_release(t, t->scan, rowgroup);
 }
 
 // ---- device-resident mode -------------------------------------------------

@@ -333,6 +333,24 @@ using table_function_init_local_t = unique_ptr<LocalTableFunctionState> (*)(Exec
                                                                            GlobalTableFunctionState *);
 using table_function_t = void (*)(ClientContext &, TableFunctionInput &, DataChunk &);
 
+// order-preserving parallel scans (DuckDB v1.3 get_partition_data)
+struct OperatorPartitionInfo {
+    bool batch_index = true;
+    bool RequiresBatchIndex() const { return batch_index; }
+};
+struct OperatorPartitionData {
+    explicit OperatorPartitionData(idx_t batch_index) : batch_index(batch_index) {}
+    idx_t batch_index;
+};
+struct TableFunctionGetPartitionInput {
+    optional_ptr<const FunctionData> bind_data;
+    optional_ptr<LocalTableFunctionState> local_state;
+    optional_ptr<GlobalTableFunctionState> global_state;
+    const OperatorPartitionInfo &partition_info;
+};
+using table_function_get_partition_data_t = OperatorPartitionData (*)(ClientContext &,
+                                                                      TableFunctionGetPartitionInput &);
+
 class TableFunction {
 public:
     TableFunction(string name, vector<LogicalType> arguments, table_function_t function,
@@ -347,6 +365,7 @@ public:
     table_function_bind_t bind;
     table_function_init_global_t init_global;
     table_function_init_local_t init_local;
+    table_function_get_partition_data_t get_partition_data = nullptr;
     bool projection_pushdown = false;
     bool filter_pushdown = false;
     bool filter_prune = false;

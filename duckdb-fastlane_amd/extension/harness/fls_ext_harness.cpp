@@ -9,7 +9,10 @@
 // the returned rows.
 #include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "duckdb.hpp"
@@ -81,10 +84,14 @@ TableFunction *lookup(fls_ext_db *d, Query &q) {
     throw BinderException("No function matches the given name and argument types '" + sig + ")'");
 }
 
-// run the query; sink(chunk, column_ids) receives every produced chunk
+// run the query; sink(batch_index, chunk, pick, n) receives every produced
+// chunk.  With nthreads > 1 the scan runs the way DuckDB's pipeline executor
+// runs a parallel source: min(nthreads, MaxThreads()) threads, each with its own
+// local state, all pulling from one global state; the sink is then called
+// concurrently and orders results by batch index itself.
 template <class Sink>
 void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limit, std::vector<std::string> &names,
-             std::vector<LogicalType> &types, Sink sink) {
+             std::vector<LogicalType> &types, Sink sink, int nthreads = 1) {
     TableFunction *f = lookup(d, q);
     named_parameter_map_t named;
     TableFunctionBindInput bin{q.args, named};
@@ -109,8 +116,6 @@ void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limi
     }
     TableFunctionInitInput iin{bind.get(), fn_ids};
     auto gstate = f->init_global ? f->init_global(d->ctx, iin) : nullptr;
-    ExecutionContext ectx(d->ctx);
-    auto lstate = f->init_local ? f->init_local(ectx, iin, gstate.get()) : nullptr;
     vector<LogicalType> chunk_types;
     for (auto id : fn_ids) chunk_types.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? LogicalType::BIGINT : rtypes[id]);
     for (auto id : ids) {
@@ -123,18 +128,48 @@ void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limi
         while (fn_ids[k] != id) ++k;
         pick.push_back(k);
     }
-    DataChunk chunk;
-    chunk.Initialize(chunk_types);
-    int64_t produced = 0;
-    while (limit < 0 || produced < limit) {
-        chunk.Reset();
-        TableFunctionInput tin{bind.get(), lstate.get(), gstate.get()};
-        f->function(d->ctx, tin, chunk);
-        if (chunk.size() == 0) break;
-        const idx_t take = limit < 0 ? chunk.size() : std::min<idx_t>(chunk.size(), (idx_t)(limit - produced));
-        sink(chunk, pick, take);
-        produced += (int64_t)take;
+    int threads = 1;
+    if (nthreads > 1 && limit < 0 && gstate)
+        threads = (int)std::min<idx_t>((idx_t)nthreads, gstate->MaxThreads());
+    OperatorPartitionInfo pinfo;
+    auto worker = [&](int64_t lim) {
+        ExecutionContext ectx(d->ctx);
+        auto lstate = f->init_local ? f->init_local(ectx, iin, gstate.get()) : nullptr;
+        DataChunk chunk;
+        chunk.Initialize(chunk_types);
+        int64_t produced = 0;
+        while (lim < 0 || produced < lim) {
+            chunk.Reset();
+            TableFunctionInput tin{bind.get(), lstate.get(), gstate.get()};
+            f->function(d->ctx, tin, chunk);
+            if (chunk.size() == 0) break;
+            idx_t batch = 0;
+            if (f->get_partition_data) {
+                TableFunctionGetPartitionInput pin{bind.get(), lstate.get(), gstate.get(), pinfo};
+                batch = f->get_partition_data(d->ctx, pin).batch_index;
+            }
+            const idx_t take = lim < 0 ? chunk.size() : std::min<idx_t>(chunk.size(), (idx_t)(lim - produced));
+            sink(batch, chunk, pick, take);
+            produced += (int64_t)take;
+        }
+    };
+    if (threads == 1) {
+        worker(limit);
+        return;
     }
+    std::vector<std::thread> pool;
+    std::vector<std::string> errs(threads);
+    for (int i = 0; i < threads; ++i)
+        pool.emplace_back([&, i] {
+            try {
+                worker(-1);
+            } catch (const std::exception &e) {
+                errs[i] = e.what();
+            }
+        });
+    for (auto &th : pool) th.join();
+    for (auto &e : errs)
+        if (!e.empty()) throw Exception(e);
 }
 
 Query make_query(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list) {
@@ -183,34 +218,55 @@ void fls_ext_close(fls_ext_db *d) { delete d; }
 
 int fls_ext_has_function(fls_ext_db *d, const char *name) { return d && d->db.table_functions.count(name) ? 1 : 0; }
 
-// an argument starting with '\x01' is an INTEGER literal (type errors).
-// as_list: 0 = scalar VARCHAR arguments, 1 = one LIST(VARCHAR) argument,
-// 2 = raw: bypass overload resolution and casts (reaches the bind checks).
-int fls_ext_query(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list, const int *proj,
-                  int nproj, int64_t limit, fls_ext_result **out) {
+int fls_ext_query_mt(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list, const int *proj,
+                     int nproj, int64_t limit, int nthreads, fls_ext_result **out) {
     try {
         Query q = make_query(d, fn, args, nargs, as_list);
         auto *r = new fls_ext_result();
+        std::unique_ptr<fls_ext_result> guard(r);
         std::vector<LogicalType> types;
         std::vector<int> pv(proj, proj + (proj ? nproj : 0));
-        execute(d, q, pv, limit, r->names, types, [r](DataChunk &c, const std::vector<size_t> &pick, idx_t n) {
+        struct Part {
+            std::vector<std::vector<std::string>> cells;
+            std::vector<std::vector<char>> valid;
+        };
+        std::mutex mu;
+        std::map<idx_t, Part> parts;  // batch index -> rows in arrival order (one thread per batch)
+        execute(d, q, pv, limit, r->names, types, [&](idx_t batch, DataChunk &c, const std::vector<size_t> &pick, idx_t n) {
+            Part local;
             for (idx_t i = 0; i < n; ++i) {
-                r->cells.emplace_back();
-                r->valid.emplace_back();
+                local.cells.emplace_back();
+                local.valid.emplace_back();
                 for (size_t k : pick) {
                     Value v = c.data[k].GetValue(i);
-                    r->valid.back().push_back(!v.IsNull());
-                    r->cells.back().push_back(v.IsNull() ? std::string() : v.ToString());
+                    local.valid.back().push_back(!v.IsNull());
+                    local.cells.back().push_back(v.IsNull() ? std::string() : v.ToString());
                 }
             }
-        });
+            std::lock_guard<std::mutex> g(mu);
+            Part &p = parts[batch];
+            for (auto &x : local.cells) p.cells.push_back(std::move(x));
+            for (auto &x : local.valid) p.valid.push_back(std::move(x));
+        }, nthreads);
+        for (auto &b : parts) {
+            for (auto &x : b.second.cells) r->cells.push_back(std::move(x));
+            for (auto &x : b.second.valid) r->valid.push_back(std::move(x));
+        }
         for (auto &t : types) r->types.push_back(t.ToString());
-        *out = r;
+        *out = guard.release();
         return 0;
     } catch (const std::exception &e) {
         g_err = e.what();
         return -1;
     }
+}
+
+// an argument starting with '\x01' is an INTEGER literal (type errors).
+// as_list: 0 = scalar VARCHAR arguments, 1 = one LIST(VARCHAR) argument,
+// 2 = raw: bypass overload resolution and casts (reaches the bind checks).
+int fls_ext_query(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list, const int *proj,
+                  int nproj, int64_t limit, fls_ext_result **out) {
+    return fls_ext_query_mt(d, fn, args, nargs, as_list, proj, nproj, limit, 1, out);
 }
 
 int64_t fls_ext_result_rows(const fls_ext_result *r) { return (int64_t)r->cells.size(); }
@@ -222,56 +278,96 @@ const char *fls_ext_result_value(const fls_ext_result *r, int64_t row, int col) 
 }
 void fls_ext_result_free(fls_ext_result *r) { delete r; }
 
-// Stream a query without materialising it: rows, a checksum over the raw
-// DataChunk bytes (string_t by content) and wall seconds.  The checksum is
-// order-dependent within each column and independent of chunk boundaries
-// (per-column FNV-1a over the values, combined at the end).
-int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj, uint64_t *rows,
-                       uint64_t *checksum, double *seconds) {
+// Stream a query without materialising it: rows, a checksum of the result
+// and wall seconds.  The checksum is a polynomial hash per column over the
+// values in result order (string_t hashed by content), folded across chunks
+// with H(A|B) = H(A) + P^|A| H(B), so it is independent of chunk and batch
+// boundaries and of how many threads scanned: chunks are hashed where they are
+// produced and folded in (batch index, arrival-within-batch) order.
+namespace {
+constexpr uint64_t kPoly = 0x9E3779B97F4A7C15ull | 1;
+uint64_t upow(uint64_t b, uint64_t e) {
+    uint64_t r = 1;
+    for (; e; e >>= 1, b *= b)
+        if (e & 1) r *= b;
+    return r;
+}
+uint64_t mix(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return x;
+}
+struct ChunkHash {
+    uint64_t n = 0;
+    std::vector<uint64_t> col;
+};
+ChunkHash hash_chunk(DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+    ChunkHash r;
+    r.n = cnt;
+    for (size_t k : pick) {
+        Vector &v = c.data[k];
+        uint64_t h = 0, pw = 1;
+        if (v.GetType().id() == LogicalTypeId::VARCHAR) {
+            const string_t *s = FlatVector::GetData<string_t>(v);
+            for (idx_t i = 0; i < cnt; ++i, pw *= kPoly) {
+                uint64_t f = 1469598103934665603ull;
+                const char *p = s[i].GetData();
+                for (uint32_t j = 0; j < s[i].GetSize(); ++j) f = (f ^ (uint8_t)p[j]) * 1099511628211ull;
+                h += pw * mix(f ^ s[i].GetSize());
+            }
+        } else {
+            const idx_t w = v.GetType().PhysicalSize();
+            const uint8_t *p = v.GetData();
+            for (idx_t i = 0; i < cnt; ++i, pw *= kPoly) {
+                uint64_t x = 0;
+                memcpy(&x, p + i * w, w);
+                h += pw * mix(x);
+            }
+        }
+        r.col.push_back(h);
+    }
+    return r;
+}
+}  // namespace
+
+extern "C" int fls_ext_scan_count_mt(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
+                                     int nthreads, uint64_t *rows, uint64_t *checksum, double *seconds) {
     try {
         const char *args[1] = {path};
         Query q = make_query(d, fn, args, 1, 0);
         std::vector<std::string> names;
         std::vector<LogicalType> types;
         std::vector<int> pv(proj, proj + (proj ? nproj : 0));
-        uint64_t n = 0;
-        std::vector<uint64_t> hs;
+        std::mutex mu;
+        std::map<idx_t, std::vector<ChunkHash>> parts;
         auto t0 = std::chrono::steady_clock::now();
-        execute(d, q, pv, -1, names, types, [&](DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
-            if (hs.empty()) hs.assign(pick.size(), 1469598103934665603ull);
-            for (size_t j = 0; j < pick.size(); ++j) {
-                Vector &v = c.data[pick[j]];
-                uint64_t h = hs[j];
-                if (v.GetType().id() == LogicalTypeId::VARCHAR) {
-                    const string_t *s = FlatVector::GetData<string_t>(v);
-                    for (idx_t i = 0; i < cnt; ++i) {
-                        const char *p = s[i].GetData();
-                        for (uint32_t k = 0; k < s[i].GetSize(); ++k) h = (h ^ (uint8_t)p[k]) * 1099511628211ull;
-                        h = (h ^ 0xFF) * 1099511628211ull;
-                    }
-                } else {
-                    const idx_t w = v.GetType().PhysicalSize();
-                    const uint8_t *p = v.GetData();
-                    for (idx_t i = 0; i < cnt; ++i) {
-                        uint64_t x = 0;
-                        memcpy(&x, p + i * w, w);
-                        h = (h ^ x) * 1099511628211ull;
-                    }
-                }
-                hs[j] = h;
-            }
-            n += cnt;
-        });
-        uint64_t h = 1469598103934665603ull;
-        for (uint64_t x : hs) h = (h ^ x) * 1099511628211ull;
+        execute(d, q, pv, -1, names, types, [&](idx_t batch, DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+            ChunkHash h = hash_chunk(c, pick, cnt);
+            std::lock_guard<std::mutex> g(mu);
+            parts[batch].push_back(std::move(h));
+        }, nthreads);
         *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        uint64_t n = 0;
+        std::vector<uint64_t> acc(names.size(), 0);
+        for (auto &b : parts)
+            for (auto &ch : b.second) {
+                const uint64_t pw = upow(kPoly, n);
+                for (size_t j = 0; j < acc.size(); ++j) acc[j] += pw * ch.col[j];
+                n += ch.n;
+            }
+        uint64_t h = 1469598103934665603ull;
+        for (uint64_t x : acc) h = (h ^ x) * 1099511628211ull;
         *rows = n;
-        *checksum = h;
+        *checksum = (h ^ n) * 1099511628211ull;
         return 0;
     } catch (const std::exception &e) {
         g_err = e.what();
         return -1;
     }
+}
+
+extern "C" int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
+                                  uint64_t *rows, uint64_t *checksum, double *seconds) {
+    return fls_ext_scan_count_mt(d, fn, path, proj, nproj, 1, rows, checksum, seconds);
 }
 
 // COPY (SELECT <proj> FROM fn(src)) TO dst (FORMAT format, key value, ...):
@@ -324,7 +420,7 @@ int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj
         uint64_t n = 0;
         std::vector<std::string> n2;
         std::vector<LogicalType> t2;
-        execute(d, q, pv, -1, n2, t2, [&](DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+        execute(d, q, pv, -1, n2, t2, [&](idx_t, DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
             bool identity = pick.size() == c.ColumnCount() && cnt == c.size();
             for (size_t k = 0; identity && k < pick.size(); ++k) identity = pick[k] == k;
             if (identity) {

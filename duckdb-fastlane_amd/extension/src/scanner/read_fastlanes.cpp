@@ -2,12 +2,18 @@
 //
 // Bind reads only footers (no GPU): typed schema via TypeMapping.  InitGlobal
 // turns DuckDB's projected column_ids into the engine's column mask, so only
-// projected columns are uploaded, decoded and copied back.  Scan streams row
-// groups from fls_scan_next (GPU-sharded, decoded ahead into pinned host
-// memory) and fills STANDARD_VECTOR_SIZE-row DataChunks by memcpy of DuckDB's
-// physical layouts; string_t records point into the file image the global
-// state keeps alive.  Error texts follow src/scanner/scan_fastlanes.cpp:62-97.
+// projected columns are uploaded, decoded and copied back.  Scan is parallel
+// (the reference pins MaxThreads to 1, src/scanner/scan_fastlanes.cpp:43-45):
+// each DuckDB thread claims whole row groups from fls_scan_acquire
+// (GPU-sharded, decoded ahead into pinned host memory), fills
+// STANDARD_VECTOR_SIZE-row DataChunks by memcpy of DuckDB's physical layouts
+// and hands the row group back with fls_scan_release.  The batch index is the
+// row group's position over all files, so DuckDB restores file order.
+// string_t records point into the file image, kept alive by every thread that
+// holds one of its row groups.  Error texts follow
+// src/scanner/scan_fastlanes.cpp:62-97.
 #include <cstring>
+#include <mutex>
 
 #include "../../../../include/flsgpu.h"
 #include "../gpu_devices.hpp"
@@ -49,12 +55,23 @@ struct ReadBindData : public TableFunctionData {
 struct ReadGlobalState : public GlobalTableFunctionState {
     vector<column_t> column_ids;
     std::vector<uint8_t> mask;
+    std::vector<idx_t> rg_base;          // batch index of each file's first row group
+    idx_t total_rowgroups = 0;
+    std::mutex lock;                     // file advance and row-group claims
     idx_t file_idx = 0;
-    std::unique_ptr<OpenTable> cur;
+    std::shared_ptr<OpenTable> cur;      // file being scanned (nullptr: open the next)
+    idx_t MaxThreads() const override { return std::max<idx_t>(1, total_rowgroups); }
+};
+
+struct ReadLocalState : public LocalTableFunctionState {
+    std::shared_ptr<OpenTable> table;    // keeps the file (and its string_t targets) alive
     fls_rowgroup rg{};
     bool have_rg = false;
     idx_t rg_pos = 0;
-    idx_t MaxThreads() const override { return 1; }
+    idx_t batch_index = 0;
+    ~ReadLocalState() override {
+        if (have_rg) fls_scan_release(table->table, rg.rowgroup);
+    }
 };
 
 void CollectPaths(const Value &v, vector<string> &files, const char *fn) {
@@ -105,57 +122,78 @@ unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFuncti
             same = ci.type == bind.cols[c].type && ci.width == bind.cols[c].width && ci.scale == bind.cols[c].scale;
         }
         if (!same) throw IOException("FastLanes file " + f + " does not match the schema of " + bind.files[0]);
+        state->rg_base.push_back(state->total_rowgroups);
+        state->total_rowgroups += fls_table_nrowgroups(t.table);
     }
     return std::move(state);
 }
 
-// advance to a row group with rows left; false at the end of all files
-bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &st) {
-    while (true) {
-        if (st.cur && st.have_rg && st.rg_pos < st.rg.nrows) return true;
-        if (st.cur) {
-            const int rc = fls_scan_next(st.cur->table, &st.rg);
-            if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
-            if (rc == 1) {
-                st.have_rg = true;
-                st.rg_pos = 0;
-                continue;
-            }
-            st.cur.reset();
-            st.file_idx++;
-        }
-        if (st.file_idx >= bind.files.size()) return false;
-        st.cur = std::make_unique<OpenTable>();
-        if (!st.cur->open(bind.files[st.file_idx]))
-            throw IOException("Failed to open FastLanes file: " + bind.files[st.file_idx]);
-        if (fls_scan_begin(st.cur->table, st.mask.data(), 0, fls_table_nrowgroups(st.cur->table)) != 0)
+unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &, TableFunctionInitInput &,
+                                                  GlobalTableFunctionState *) {
+    return make_uniq<ReadLocalState>();
+}
+
+// give back the local state's row group and claim the next one (in file and
+// row-group order over all threads); false at the end of all files
+bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &l) {
+    if (l.have_rg) {
+        l.have_rg = false;
+        if (fls_scan_release(l.table->table, l.rg.rowgroup) != 0)
             throw IOException(string("FastLanes scan failed: ") + fls_last_error());
-        st.have_rg = false;
+    }
+    l.table.reset();
+    std::lock_guard<std::mutex> guard(g.lock);
+    while (true) {
+        if (!g.cur) {
+            if (g.file_idx >= bind.files.size()) return false;
+            auto t = std::make_shared<OpenTable>();
+            if (!t->open(bind.files[g.file_idx]))
+                throw IOException("Failed to open FastLanes file: " + bind.files[g.file_idx]);
+            if (fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
+                throw IOException(string("FastLanes scan failed: ") + fls_last_error());
+            g.cur = std::move(t);
+        }
+        const int rc = fls_scan_acquire(g.cur->table, &l.rg);
+        if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
+        if (rc == 1) {
+            l.table = g.cur;
+            l.have_rg = true;
+            l.rg_pos = 0;
+            l.batch_index = g.rg_base[g.file_idx] + l.rg.rowgroup;
+            return true;
+        }
+        g.cur.reset();  // closed once the last thread holding one of its row groups lets go
+        g.file_idx++;
     }
 }
 
 void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
     const auto &bind = data.bind_data->Cast<ReadBindData>();
-    auto &st = data.global_state->Cast<ReadGlobalState>();
+    auto &g = data.global_state->Cast<ReadGlobalState>();
+    auto &l = data.local_state->Cast<ReadLocalState>();
     output.Reset();
-    if (!NextRowGroup(bind, st)) {
+    if (!(l.have_rg && l.rg_pos < l.rg.nrows) && !NextRowGroup(bind, g, l)) {
         output.SetCardinality(0);
         return;
     }
-    const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, st.rg.nrows - st.rg_pos);
+    const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, l.rg.nrows - l.rg_pos);
     for (idx_t j = 0; j < output.ColumnCount(); ++j) {
-        const column_t id = j < st.column_ids.size() ? st.column_ids[j] : j;
+        const column_t id = j < g.column_ids.size() ? g.column_ids[j] : j;
         Vector &vec = output.data[j];
         if (id == COLUMN_IDENTIFIER_ROW_ID) {
             int64_t *rid = FlatVector::GetData<int64_t>(vec);
-            for (idx_t i = 0; i < n; ++i) rid[i] = (int64_t)(st.rg.first_row + st.rg_pos + i);
+            for (idx_t i = 0; i < n; ++i) rid[i] = (int64_t)(l.rg.first_row + l.rg_pos + i);
             continue;
         }
         const idx_t ob = bind.cols[id].out_bytes;
-        memcpy(vec.GetData(), (const uint8_t *)st.rg.columns[id] + st.rg_pos * ob, n * ob);
+        memcpy(vec.GetData(), (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob, n * ob);
     }
-    st.rg_pos += n;
+    l.rg_pos += n;
     output.SetCardinality(n);
+}
+
+OperatorPartitionData ReadPartitionData(ClientContext &, TableFunctionGetPartitionInput &input) {
+    return OperatorPartitionData(input.local_state->Cast<ReadLocalState>().batch_index);
 }
 
 unique_ptr<TableRef> ReadFastlanesReplacementScan(ClientContext &, ReplacementScanInput &input,
@@ -173,7 +211,8 @@ unique_ptr<TableRef> ReadFastlanesReplacementScan(ClientContext &, ReplacementSc
 }  // namespace
 
 TableFunction ReadFastlanesFunction() {
-    TableFunction fn("read_fastlanes", {LogicalType::VARCHAR}, ReadScan, ReadBind, ReadInitGlobal);
+    TableFunction fn("read_fastlanes", {LogicalType::VARCHAR}, ReadScan, ReadBind, ReadInitGlobal, ReadInitLocal);
+    fn.get_partition_data = ReadPartitionData;
     fn.projection_pushdown = true;
     fn.filter_pushdown = false;
     fn.filter_prune = false;

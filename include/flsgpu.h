@@ -16,6 +16,10 @@
  *                          + RowgroupReader::materialize()     src/fastlanes_facade.cpp:41,48
  *   fls_scan_begin/next    the row-group loop the reference never wrote
  *                          (it decodes row group 0 only, :41)
+ *   fls_scan_acquire/release  the same loop for a parallel DuckDB scan
+ *                          (MaxThreads > 1, batch index = row group; the
+ *                          reference pins MaxThreads to 1,
+ *                          src/scanner/scan_fastlanes.cpp:43-45)
  *   fls_table_close/fls_disconnect  FastLanesFacade::closeFile  src/fastlanes_facade.cpp:202-210
  *
  * Conventions: plain pointers and sizes, no exceptions across the ABI; every
@@ -26,8 +30,9 @@
  * u32 length + 12 inline bytes, or u32 length + 4-byte prefix + char* into a
  * pinned host dictionary heap owned by the table).
  * A table handle is used by one host thread at a time (DuckDB's scan thread,
- * src/scanner/scan_fastlanes.cpp:43-45); internally there is one HIP stream
- * set per GPU.
+ * src/scanner/scan_fastlanes.cpp:43-45), except fls_scan_acquire/release,
+ * which any number of threads may call concurrently between fls_scan_begin
+ * and the next begin/close; internally there is one HIP stream set per GPU.
  */
 #ifndef FLSGPU_H
 #define FLSGPU_H
@@ -111,8 +116,16 @@ int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowg
  * sharded contiguously over the connection's GPUs, uploaded once, decoded in
  * batches and copied to pinned host memory ahead of the consumer. */
 int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uint32_t rg_end);
-/* 1 = a row group was delivered into *out, 0 = end of scan, <0 = error. */
+/* 1 = a row group was delivered into *out, 0 = end of scan, <0 = error.
+ * The previous row group's buffers are released by the call. */
 int fls_scan_next(fls_table *t, fls_rowgroup *out);
+/* Thread-safe form for parallel consumers: claims the next row group in order
+ * (1 = delivered, 0 = end, <0 = error); its buffers stay valid until
+ * fls_scan_release(t, out->rowgroup).  A consumer must release what it holds
+ * before acquiring again (a decoded batch is recycled only when all of its
+ * row groups are back).  Do not mix with fls_scan_next on one scan. */
+int fls_scan_acquire(fls_table *t, fls_rowgroup *out);
+int fls_scan_release(fls_table *t, uint32_t rowgroup);
 
 /* ---- device-resident mode (HBM roofline measurement, bench.py) ---------
  * Upload row groups [rg_begin, rg_end) of the table to the connection's first

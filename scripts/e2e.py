@@ -42,11 +42,16 @@ def main():
     img.write(path)
     from ext_harness import Ext
     e = Ext()
-    n, h, sec = e.scan_count("read_fastlanes", path)
-    print(f"read_fastlanes DataChunks (1 scan thread, copy + checksum): {n} rows in {sec:.3f} s = "
-          f"{n / sec / 1e6:.1f} M rows/s", flush=True)
-    n2, h2, sec2 = e.scan_count("read_fastlanes", path, proj=[0, 5, 10])
-    print(f"read_fastlanes projected 3 cols: {n2 / sec2 / 1e6:.1f} M rows/s", flush=True)
+    ref = None
+    for th in (1, 4, 8, 16):
+        n, h, sec = e.scan_count("read_fastlanes", path, threads=th)
+        ref = ref or (n, h)
+        assert (n, h) == ref, "parallel scan changed the result"
+        print(f"read_fastlanes DataChunks ({th} scan threads, copy + checksum): {n} rows in {sec:.3f} s = "
+              f"{n / sec / 1e6:.1f} M rows/s", flush=True)
+    for th in (1, 16):
+        n2, h2, sec2 = e.scan_count("read_fastlanes", path, proj=[0, 5, 10], threads=th)
+        print(f"read_fastlanes projected 3 cols, {th} threads: {n2 / sec2 / 1e6:.1f} M rows/s", flush=True)
     e.close()
 
 

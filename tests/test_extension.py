@@ -158,3 +158,28 @@ def test_read_fastlanes_stream_checksum_matches_oracle_rowcount(fl, ext, gpu, tm
     rows2, h2, _ = ext.scan_count("read_fastlanes", p)
     assert (rows2, h2) == (rows, h1)   # deterministic end-to-end delivery
     print(f"read_fastlanes e2e SF0.1: {rows / sec / 1e6:.1f} M rows/s")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [2, 8])
+def test_read_fastlanes_parallel_scan_keeps_order(fl, ext, gpu, tmpfile, monkeypatch, threads):
+    """MaxThreads > 1 (reference: 1, src/scanner/scan_fastlanes.cpp:43-45):
+    threads claim row groups through fls_scan_acquire/release, the batch index
+    (row group position over all files) restores order."""
+    monkeypatch.setenv("FLS_SCAN_BATCH", "2")
+    img = fl.gen_image("lineitem", 0.1)            # 10 row groups
+    p = tmpfile("li01.fls")
+    img.write(p)
+    one = ext.scan_count("read_fastlanes", p)
+    many = ext.scan_count("read_fastlanes", p, threads=threads)
+    assert many[:2] == one[:2] and one[0] == 600572
+    # rows in order, projected, rowid included
+    _, _, r1 = ext.query("read_fastlanes", p, proj=[-1, 0, 14])
+    _, _, rn = ext.query("read_fastlanes", p, proj=[-1, 0, 14], threads=threads)
+    assert rn == r1 and [int(r[0]) for r in rn[::4099]] == list(range(0, 600572, 4099))
+    # several files, each scanned in parallel, concatenated in list order
+    q = tmpfile("small.fls")
+    fl.gen_image("lineitem", 0.01).write(q)
+    _, _, m1 = ext.query("read_fastlanes", p, q, p, as_list=True, proj=[0, 10])
+    _, _, mn = ext.query("read_fastlanes", p, q, p, as_list=True, proj=[0, 10], threads=threads)
+    assert len(mn) == 2 * 600572 + 60175 and mn == m1
