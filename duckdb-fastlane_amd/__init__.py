@@ -27,15 +27,15 @@ _lib = C.CDLL(str(LIB_PATH))
 
 # --- enums (include/flswriter.h) -------------------------------------------
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64 = 1, 2, 3, 4, 5, 6, 7, 8
-DATE, DECIMAL, VARCHAR = 10, 11, 20
-ENC_AUTO, ENC_FFOR, ENC_DELTA, ENC_DICT, ENC_RLE = 0, 1, 2, 3, 4
+DATE, DECIMAL, FLOAT, DOUBLE, VARCHAR = 10, 11, 12, 13, 20
+ENC_AUTO, ENC_FFOR, ENC_DELTA, ENC_DICT, ENC_RLE, ENC_ALP, ENC_FSST = 0, 1, 2, 3, 4, 5, 7
 
 NP_DTYPE = {INT8: np.int8, INT16: np.int16, INT32: np.int32, INT64: np.int64,
             UINT8: np.uint8, UINT16: np.uint16, UINT32: np.uint32, UINT64: np.uint64,
-            DATE: np.int32, DECIMAL: np.int64}
+            DATE: np.int32, DECIMAL: np.int64, FLOAT: np.float32, DOUBLE: np.float64}
 TYPE_NAMES = {INT8: "TINYINT", INT16: "SMALLINT", INT32: "INTEGER", INT64: "BIGINT",
               UINT8: "UTINYINT", UINT16: "USMALLINT", UINT32: "UINTEGER", UINT64: "UBIGINT",
-              DATE: "DATE", DECIMAL: "DECIMAL", VARCHAR: "VARCHAR"}
+              DATE: "DATE", DECIMAL: "DECIMAL", FLOAT: "FLOAT", DOUBLE: "DOUBLE", VARCHAR: "VARCHAR"}
 ROWGROUP = 65536
 
 
@@ -193,7 +193,8 @@ def gen_dict_string(workload: str, col: int, code: int) -> str | None:
 # --- writer ----------------------------------------------------------------
 def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0) -> Image:
     """columns: list of (name, type, values, encoding[, width, scale]).
-    values: numpy int array for integer types, list of str/bytes for VARCHAR."""
+    values: numpy int array for integer types, float array for FLOAT/DOUBLE
+    (stored bit-exactly), list of str/bytes for VARCHAR."""
     w = _lib.fls_writer_new(row_offset)
     try:
         _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))

@@ -29,7 +29,11 @@
 //     8 segments + lane bases -> 8 x 16 B stores (128 B lines);
 //   * DELTA T<64 and RLE indices scatter into LDS at their transposed position
 //     and scan the 1024/T chains there; DICT codes go through LDS and gather
-//     from the dictionary (staged in LDS when small) with 16 B/lane stores.
+//     from the dictionary (staged in LDS when small) with 16 B/lane stores;
+//   * ALP (FLOAT/DOUBLE): the FFOR stream's integers are converted and scaled
+//     in registers ((F)d * 10^f * 10^-e) and stored like FFOR; vectors with
+//     exceptions go through LDS, where the exception values are patched in.
+// FSST strings have their own kernel (fls_fsst.hip).
 // The path is HBM-bound integer work: no MFMA.
 #include <hip/hip_runtime.h>
 
@@ -37,6 +41,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "fls_alp.hpp"
 #include "fls_decode.hpp"
 #include "fls_format.hpp"
 #include "fls_unpack.hpp"
@@ -63,6 +68,11 @@ template <> struct UInt<32> { using type = uint32_t; };
 template <> struct UInt<64> { using type = uint64_t; };
 
 __device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+
+__constant__ double kF10D[kAlpMaxExpD + 1] = {FLS_ALP_F10_D};
+__constant__ double kIF10D[kAlpMaxExpD + 1] = {FLS_ALP_IF10_D};
+__constant__ float kF10F[kAlpMaxExpF + 1] = {FLS_ALP_F10_F};
+__constant__ float kIF10F[kAlpMaxExpF + 1] = {FLS_ALP_IF10_F};
 // keep unrolled iterations in program order: bounds register pressure to one
 // iteration (the occupancy, not the ILP of one wave, hides latency here)
 // full 16-byte output store (FLS_NT_STORE: non-temporal streaming store)
@@ -495,6 +505,84 @@ struct PathRle {
     }
 };
 
+// ALP: (F)d * 10^f * 10^-e, evaluated left to right in F (as the encoder checks)
+template <int T>
+struct AlpScale;
+template <>
+struct AlpScale<64> {
+    double fm, im;
+    __device__ __forceinline__ AlpScale(uint32_t e, uint32_t f) : fm(kF10D[f]), im(kIF10D[e]) {}
+    __device__ __forceinline__ v4u apply(v4u x) const {
+        const double a = (double)(int64_t)(((uint64_t)x.y << 32) | x.x) * fm * im;
+        const double b = (double)(int64_t)(((uint64_t)x.w << 32) | x.z) * fm * im;
+        const uint64_t ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+        return mk4((uint32_t)ua, (uint32_t)(ua >> 32), (uint32_t)ub, (uint32_t)(ub >> 32));
+    }
+};
+template <>
+struct AlpScale<32> {
+    float fm, im;
+    __device__ __forceinline__ AlpScale(uint32_t e, uint32_t f) : fm(kF10F[f]), im(kIF10F[e]) {}
+    __device__ __forceinline__ uint32_t one(uint32_t d) const {
+        return __float_as_uint((float)(int32_t)d * fm * im);
+    }
+    __device__ __forceinline__ v4u apply(v4u x) const { return mk4(one(x.x), one(x.y), one(x.z), one(x.w)); }
+};
+
+template <int T_>
+struct PathAlp {
+    static constexpr int T = T_;
+    static constexpr uint32_t kMaxE = T_ == 64 ? kAlpMaxExpD : kAlpMaxExpF;
+    using Aux = NoAux;
+    gu8 *aux_base;
+    uint32_t *err;
+    __device__ __forceinline__ PathAlp(const DevChunk &c, const Lds &, uint32_t, uint32_t *e)
+        : aux_base(gptr(c.chunk) + c.aux_off), err(e) {}
+    __device__ __forceinline__ gu8 *aux_ptr(const DevChunk &, const VecInfo &) const { return nullptr; }
+    template <bool FULL>
+    __device__ __forceinline__ void vec(const Lds &s, const VecInfo &x, const Aux &, ou8 *out, uint32_t lane) const {
+        const uint32_t exc = x.acount & 0xFFFF;
+        const uint32_t e = min((x.acount >> 16) & 0xFF, kMaxE), f = min(x.acount >> 24, e);
+        const AlpScale<T> sc(e, f);
+        if (exc == 0) {  // common case: registers straight to HBM, like FFOR
+            const uint32_t limit = x.nvals * (T / 8);
+#pragma unroll
+            for (uint32_t j = 0; j < T / 8; ++j) {
+                const uint32_t ci = lane + 64 * j;
+                const v4u v = sc.apply(add_base<T>(unpack_chunk<T>(s.P, x.W, ci), x.base));
+                if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, v);
+                else store16<T / 8>(out, 16 * ci, limit, v);
+                seq();
+            }
+            return;
+        }
+        // exceptions: decode into LDS, patch, copy out
+#pragma unroll
+        for (uint32_t j = 0; j < T / 8; ++j) {
+            const uint32_t ci = lane + 64 * j;
+            *reinterpret_cast<lv4 *>(s.V + 16 * ci) = sc.apply(add_base<T>(unpack_chunk<T>(s.P, x.W, ci), x.base));
+            seq();
+        }
+        wave_sync();
+        gu8 *ea = aux_base + x.aoff;
+        const FLS_GLOBAL uint16_t *pos = reinterpret_cast<const FLS_GLOBAL uint16_t *>(ea);
+        gu8 *val = ea + ((2 * exc + 15) & ~15u);
+        bool bad = false;
+        for (uint32_t k = lane; k < exc; k += 64) {
+            const uint32_t p = pos[k];
+            if (p >= kVectorSize) { bad = true; continue; }
+            if (T == 64) {
+                *reinterpret_cast<FLS_LDS uint64_t *>(s.V + 8 * p) = reinterpret_cast<const FLS_GLOBAL uint64_t *>(val)[k];
+            } else {
+                *reinterpret_cast<FLS_LDS uint32_t *>(s.V + 4 * p) = reinterpret_cast<const FLS_GLOBAL uint32_t *>(val)[k];
+            }
+        }
+        if (bad) atomicOr(err, KERR_BAD_DESC);
+        wave_sync();
+        copy_out<T / 8, FULL>(s.V, out, x.nvals, lane);
+    }
+};
+
 // One out-of-line function per path: each gets its own register allocation
 // (inlined into one switch, hipcc allocated the union of all paths: 292 VGPRs,
 // one wave per SIMD).  Arguments arrive in VGPRs, which a callee must assume
@@ -620,6 +708,10 @@ __global__ __launch_bounds__(256, 4) void decode_kernel(const DevChunk *__restri
             case 2: call_dict<2>(cg, lp, lv, v_bytes, err, dc); break;
             default: call_dict<1>(cg, lp, lv, v_bytes, err, dc); break;
             }
+            break;
+        case ENC_ALP:
+            if (T == 64) call<PathAlp<64>>(cg, lp, lv, v_bytes, err);
+            else call<PathAlp<32>>(cg, lp, lv, v_bytes, err);
             break;
         case ENC_RLE:
             switch (ob) {

@@ -12,7 +12,8 @@ namespace fls {
 // header load before it can start streaming.
 struct DevChunk {              // 64 B
     const uint8_t *chunk;      // HBM address of the chunk (ChunkHeader)
-    const uint8_t *dict;       // DICT: int dictionary, or string_t table (VARCHAR)
+    const uint8_t *dict;       // DICT: int dictionary, or string_t table (VARCHAR);
+                               // FSST: HBM address of the chunk's string heap (written)
     uint8_t *out;              // HBM address of output row 0 of this chunk
     uint32_t nvec;             // vectors (<= 64)
     uint32_t dict_count;
@@ -20,12 +21,15 @@ struct DevChunk {              // 64 B
     uint32_t packed_off;       // packed area, relative to chunk
     uint32_t aux_off;          // aux area, relative to chunk
     uint8_t enc, T, vbits, ob; // encoding, packing width, value bits, output bytes/value
-    uint32_t pad[4];
+    uint64_t heap_host;        // FSST: address string_t pointers use for heap byte 0
+                               // (the pinned host copy the heap lands in)
+    uint32_t heap_bytes;       // FSST: heap bytes of the chunk (ChunkHeader.reserved1)
+    uint32_t pad;
 };
 static_assert(sizeof(DevChunk) == 64, "DevChunk is 64 B");
 
 // error flags raised by the kernel (corrupt codes / run indices are clamped)
-enum : uint32_t { KERR_DICT_CODE = 1, KERR_RUN_INDEX = 2, KERR_BAD_DESC = 4 };
+enum : uint32_t { KERR_DICT_CODE = 1, KERR_RUN_INDEX = 2, KERR_BAD_DESC = 4, KERR_FSST = 8 };
 
 // Per-launch LDS geometry: per-wave packed staging (>= 128*maxW + 128 bytes)
 // and decoded-vector scratch (path dependent), both multiples of 16; grid = 0
@@ -35,9 +39,11 @@ struct DecodeGeom {
     int grid = 0;
 };
 
-// Launch the fused decode over every vector of nchunks chunks.
+// Launch the fused decode over every vector of nchunks chunks (no FSST).
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream);
+// Launch the FSST string decode over nchunks FSST chunks (fls_fsst.hip).
+hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, hipStream_t stream);
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
 // LDS bytes per wave the v2 kernel needs for one chunk (given its max width)
@@ -47,6 +53,7 @@ inline void chunk_lds_need(uint8_t enc, uint8_t T, uint8_t ob, uint32_t dict_cou
     v_bytes = 0;
     if (enc == 2 /*DELTA*/ && T < 64) v_bytes = 128 * T;
     if (enc == 4 /*RLE*/) v_bytes = 2048;
+    if (enc == 5 /*ALP*/) v_bytes = 128 * T;
     if (enc == 3 /*DICT*/) {
         const uint32_t d = dict_count * ob;
         v_bytes = 4096 + (d <= 4096 ? ((d + 15) & ~15u) : 0);

@@ -30,6 +30,8 @@ enum Encoding : uint8_t {
     ENC_DELTA = 2,  // unified-transposed delta, deltas FFOR-packed, per-lane bases
     ENC_DICT = 3,   // dictionary codes FFOR-packed (T=32), per-row-group dictionary
     ENC_RLE = 4,    // FastLanes-RLE: run values + DELTA(T=16) run-index vector
+    ENC_ALP = 5,    // ALP (FLOAT/DOUBLE): decimal-exponent ints FFOR-packed + exceptions
+    ENC_FSST = 7,   // FSST (VARCHAR): 255-symbol table, byte codes, FFOR-packed lengths
 };
 
 // Logical column types (cf. reference src/type_mapping.cpp:64-109)
@@ -38,18 +40,21 @@ enum TypeId : uint8_t {
     TY_UINT8 = 5, TY_UINT16 = 6, TY_UINT32 = 7, TY_UINT64 = 8,
     TY_DATE = 10,     // int32 days since 1970-01-01 (DuckDB date_t)
     TY_DECIMAL = 11,  // int64 scaled integer (DuckDB DECIMAL(w<=18, s))
-    TY_VARCHAR = 20,  // dictionary strings, decoded to DuckDB string_t (16 B)
+    TY_FLOAT = 12,    // IEEE binary32 (FastLanes flt_col_t)
+    TY_DOUBLE = 13,   // IEEE binary64 (FastLanes dbl_col_t)
+    TY_VARCHAR = 20,  // DICT or FSST strings, decoded to DuckDB string_t (16 B)
 };
 
 inline int type_value_bits(uint8_t t) {
     switch (t) {
     case TY_INT8: case TY_UINT8: return 8;
     case TY_INT16: case TY_UINT16: return 16;
-    case TY_INT32: case TY_UINT32: case TY_DATE: return 32;
-    case TY_INT64: case TY_UINT64: case TY_DECIMAL: return 64;
+    case TY_INT32: case TY_UINT32: case TY_DATE: case TY_FLOAT: return 32;
+    case TY_INT64: case TY_UINT64: case TY_DECIMAL: case TY_DOUBLE: return 64;
     default: return 0;
     }
 }
+inline bool type_is_float(uint8_t t) { return t == TY_FLOAT || t == TY_DOUBLE; }
 // bytes per decoded value in the output column (string_t = 16 B)
 inline int type_out_bytes(uint8_t t) { return t == TY_VARCHAR ? 16 : type_value_bits(t) / 8; }
 inline bool type_valid(uint8_t t) { return type_out_bytes(t) > 0; }
@@ -79,6 +84,34 @@ struct VecMeta {              // 32 B per 1024-value vector
     uint8_t pad;
     uint32_t aux_count;       // RLE: number of runs
 };
+// ALP chunk (FLOAT T=vbits=32 / DOUBLE T=vbits=64): per vector the FFOR
+// stream holds the encoded integers d, value = (float_t)d * kAlpF10[f] *
+// kAlpIF10[e] (fls_alp.hpp); VecMeta.aux_count = exceptions | e << 16 | f << 24;
+// VecMeta.aux_off -> u16 positions[exceptions] (padded to 16 B), then the
+// exception values (T/8 bytes each) that replace the decoded value there.
+inline uint32_t alp_exceptions(uint32_t aux_count) { return aux_count & 0xFFFF; }
+inline uint32_t alp_e(uint32_t aux_count) { return (aux_count >> 16) & 0xFF; }
+inline uint32_t alp_f(uint32_t aux_count) { return aux_count >> 24; }
+inline uint64_t alp_aux_bytes(uint32_t exc, uint32_t vbits) { return ((2ull * exc + 15) & ~15ull) + exc * (vbits / 8ull); }
+
+// FSST chunk (VARCHAR, T=32, vbits=0, is_str=1):
+//   aux[0, 2304): symbol table, u64 symbol[256] (little-endian bytes) then
+//                 u8 length[256] (1..8; code 255 is the escape, unused);
+//   ChunkHeader.dict_count = symbols in use, reserved1 = heap bytes of the
+//   chunk (sum of the vectors' 16-byte-padded decompressed sizes);
+//   per vector: FFOR stream (T=32) of the decompressed string lengths;
+//   VecMeta.aux_count = decompressed bytes of the vector;
+//   VecMeta.aux_off -> FsstVecHeader, then the vector's compressed byte stream
+//   (all its strings' codes concatenated; code 255 = next byte is a literal).
+constexpr uint32_t kFsstTableBytes = 256 * 8 + 256;
+constexpr uint32_t kFsstEscape = 255;
+struct FsstVecHeader {        // 16 B
+    uint32_t heap_off;        // start of this vector's strings in the chunk heap (16-aligned)
+    uint32_t comp_len;        // compressed bytes following the header
+    uint32_t reserved[2];
+};
+static_assert(sizeof(FsstVecHeader) == 16, "FSST vector header is 16 B");
+
 static_assert(sizeof(ChunkHeader) == 64, "chunk header is 64 B");
 static_assert(sizeof(VecMeta) == 32, "vector meta is 32 B");
 static_assert(alignof(VecMeta) == 8 && alignof(ChunkHeader) == 8, "natural alignment, no padding");

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "fls_alp.hpp"
 #include "fls_format.hpp"
 
 namespace fls {
@@ -96,11 +97,15 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
             if (h.magic != kChunkMagic) return "bad chunk magic";
             if (h.nvals != rg.nrows || h.nvec != (rg.nrows + kVectorSize - 1) / kVectorSize) return "chunk row count mismatch";
             if (h.T != 8 && h.T != 16 && h.T != 32 && h.T != 64) return "bad packing width";
-            if (h.enc < ENC_FFOR || h.enc > ENC_RLE) return "bad encoding";
+            if ((h.enc < ENC_FFOR || h.enc > ENC_ALP) && h.enc != ENC_FSST) return "bad encoding";
             const uint8_t ty = m.cols[c].type;
             const bool is_str = ty == TY_VARCHAR;
             if ((bool)h.is_str != is_str) return "chunk/column type mismatch";
-            if (is_str ? h.enc != ENC_DICT : h.vbits != type_value_bits(ty)) return "chunk/column type mismatch";
+            if (is_str ? (h.enc != ENC_DICT && h.enc != ENC_FSST) : h.vbits != type_value_bits(ty))
+                return "chunk/column type mismatch";
+            if (type_is_float(ty) != (h.enc == ENC_ALP)) return "chunk/column type mismatch";
+            if ((h.enc == ENC_ALP) && h.T != h.vbits) return "bad packing width";
+            if (h.enc == ENC_FSST && h.T != 32) return "bad string length width";
             if ((h.enc == ENC_FFOR || h.enc == ENC_DELTA) && h.T != h.vbits) return "bad packing width";
             if (h.enc == ENC_DICT && h.T != 32) return "bad dictionary code width";
             if (h.enc == ENC_RLE && h.T != 16) return "bad run-index width";
@@ -120,6 +125,30 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
                         vm.aux_off + 128 + (uint64_t)vm.aux_count * (h.vbits / 8) > h.aux_len)
                         return "run values out of bounds";
                 }
+                if (h.enc == ENC_ALP) {
+                    const uint32_t exc = alp_exceptions(vm.aux_count), e = alp_e(vm.aux_count), f = alp_f(vm.aux_count);
+                    const uint32_t maxe = h.T == 64 ? kAlpMaxExpD : kAlpMaxExpF;
+                    if (e > maxe || f > e || exc > vm.nvals) return "bad ALP exponent or exception count";
+                    if (exc && (vm.aux_off % 16 || vm.aux_off + alp_aux_bytes(exc, h.vbits) > h.aux_len))
+                        return "ALP exceptions out of bounds";
+                }
+                if (h.enc == ENC_FSST) {
+                    FsstVecHeader fh;
+                    if (vm.aux_off % 16 || vm.aux_off < kFsstTableBytes || vm.aux_off + sizeof(fh) > h.aux_len)
+                        return "FSST vector out of bounds";
+                    memcpy(&fh, img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
+                    if (vm.aux_off + sizeof(fh) + fh.comp_len > h.aux_len || fh.heap_off % 16 ||
+                        fh.heap_off + (uint64_t)vm.aux_count > h.reserved1)
+                        return "FSST vector out of bounds";
+                }
+            }
+            if (h.enc == ENC_FSST) {
+                if (h.aux_len < kFsstTableBytes || h.dict_count > 255) return "bad FSST symbol table";
+                for (uint32_t k = 0; k < h.dict_count; ++k) {
+                    const uint8_t l = img[ch.off + h.aux_off + 8 * 256 + k];
+                    if (l < 1 || l > 8) return "bad FSST symbol length";
+                }
+                if (h.reserved1 > (1ull << 32)) return "FSST heap too large";
             }
             if (h.enc == ENC_DICT) {
                 if (h.dict_count == 0) return "empty dictionary";

@@ -8,6 +8,7 @@
 // and the producer of every benchmark / test input (fls_gen.hpp).
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -19,6 +20,7 @@
 
 #include "../../include/flsgpu.h"
 #include "../../include/flswriter.h"
+#include "fls_alp.hpp"
 #include "fls_common.hpp"
 #include "fls_format.hpp"
 #include "fls_gen.hpp"
@@ -110,7 +112,8 @@ void align_to(std::vector<uint8_t> &b, size_t a) {
 // Assemble one chunk from encoded vectors + chunk-level aux (dictionary).
 std::vector<uint8_t> assemble_chunk(uint8_t enc, uint8_t T, uint8_t vbits, bool is_str,
                                     uint32_t nvals, std::vector<VecOut> &vecs,
-                                    const std::vector<uint8_t> &chunk_aux, uint32_t dict_count) {
+                                    const std::vector<uint8_t> &chunk_aux, uint32_t dict_count,
+                                    uint64_t reserved1 = 0) {
     ChunkHeader h{};
     h.magic = kChunkMagic;
     h.enc = enc;
@@ -143,6 +146,7 @@ std::vector<uint8_t> assemble_chunk(uint8_t enc, uint8_t T, uint8_t vbits, bool 
     }
     h.aux_len = aux.size();
     h.dict_count = dict_count;
+    h.reserved1 = reserved1;
     size_t total = h.aux_off + aux.size();
     total = (total + kChunkAlign - 1) & ~size_t(kChunkAlign - 1);
     std::vector<uint8_t> out(total, 0);
@@ -292,6 +296,183 @@ std::vector<uint8_t> enc_dict_str(const uint32_t *offs, const char *bytes, uint3
     return enc_dict_codes(codes.data(), n, 0, true, str_dict_bytes(entries), (uint32_t)entries.size());
 }
 
+// ---- FSST (VARCHAR) ----------------------------------------------------------
+// Boncz, Neumann, Leis, "FSST: Fast Random Access String Compression", VLDB
+// 2020: a table of up to 255 symbols of 1..8 bytes; a string becomes byte codes
+// (greedy longest match), code 255 escapes one literal byte.  The table is
+// built from a sample in five rounds: compress the sample with the current
+// table, count symbol and adjacent-pair occurrences, keep the 255 candidates
+// (symbols, pair concatenations cut to 8 bytes, single bytes) of highest gain
+// = count x length.  One table per chunk (row group), so chunks stay
+// self-contained; the GPU decodes a vector's code stream code-parallel.
+
+struct FsstTable {
+    uint64_t sym[256] = {};
+    uint8_t len[256] = {};
+    int n = 0;
+    std::vector<uint8_t> by_first[256];  // codes starting with a byte, longest first
+
+    void index() {
+        for (auto &v : by_first) v.clear();
+        for (int c = 0; c < n; ++c) by_first[sym[c] & 0xFF].push_back((uint8_t)c);
+        for (auto &v : by_first)
+            std::stable_sort(v.begin(), v.end(), [this](uint8_t a, uint8_t b) { return len[a] > len[b]; });
+    }
+    // longest symbol matching at p (r bytes left), or -1
+    int match(const uint8_t *p, size_t r) const {
+        for (uint8_t c : by_first[p[0]]) {
+            const uint32_t L = len[c];
+            if (L <= r && memcmp(&sym[c], p, L) == 0) return c;
+        }
+        return -1;
+    }
+    void compress(const uint8_t *p, size_t n_, std::vector<uint8_t> &out) const {
+        for (size_t i = 0; i < n_;) {
+            const int c = match(p + i, n_ - i);
+            if (c >= 0) {
+                out.push_back((uint8_t)c);
+                i += len[c];
+            } else {
+                out.push_back((uint8_t)kFsstEscape);
+                out.push_back(p[i]);
+                ++i;
+            }
+        }
+    }
+};
+
+FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
+    // sample: whole strings at evenly spaced rows, about 16 KiB
+    std::vector<std::pair<uint32_t, uint32_t>> smp;  // (offset, length)
+    const uint64_t total = offs[n] - offs[0];
+    const uint32_t step = (uint32_t)std::max<uint64_t>(1, total / 16384);  // rows between samples
+    uint64_t taken = 0;
+    for (uint32_t i = 0; i < n && taken < 16384; i += step) {
+        smp.emplace_back(offs[i], offs[i + 1] - offs[i]);
+        taken += offs[i + 1] - offs[i];
+    }
+    FsstTable st;
+    struct Key {
+        uint64_t sym;
+        uint32_t len;
+        bool operator==(const Key &o) const { return sym == o.sym && len == o.len; }
+        bool operator<(const Key &o) const { return sym != o.sym ? sym < o.sym : len < o.len; }
+    };
+    struct KeyHash {
+        size_t operator()(const Key &k) const { return (size_t)(k.sym * 0x9E3779B97F4A7C15ull ^ k.len); }
+    };
+    for (int round = 0; round < 5; ++round) {
+        st.index();
+        // ids: 0..n-1 symbols, 256 + b escaped byte b
+        std::vector<uint64_t> c1(512, 0);
+        std::unordered_map<uint32_t, uint64_t> c2;
+        auto sym_of = [&](int id, uint64_t &s, uint32_t &l) {
+            if (id < 256) { s = st.sym[id]; l = st.len[id]; }
+            else { s = (uint64_t)(id - 256); l = 1; }
+        };
+        for (auto &sp : smp) {
+            const uint8_t *p = (const uint8_t *)bytes + sp.first;
+            int prev = -1;
+            for (uint32_t i = 0; i < sp.second;) {
+                const int c = st.match(p + i, sp.second - i);
+                const int id = c >= 0 ? c : 256 + p[i];
+                i += c >= 0 ? st.len[c] : 1;
+                c1[id]++;
+                if (prev >= 0) c2[((uint32_t)prev << 9) | (uint32_t)id]++;
+                prev = id;
+            }
+        }
+        std::unordered_map<Key, uint64_t, KeyHash> gain;  // candidate symbol -> gain
+        auto add = [&](uint64_t sym, uint32_t l, uint64_t g) {
+            uint64_t &x = gain[Key{sym, l}];
+            x = std::max(x, g);
+        };
+        for (int id = 0; id < 512; ++id) {
+            if (!c1[id]) continue;
+            uint64_t sy;
+            uint32_t l;
+            sym_of(id, sy, l);
+            add(sy, l, c1[id] * l);
+        }
+        for (auto &kv : c2) {
+            uint64_t s1, s2;
+            uint32_t l1, l2;
+            sym_of((int)(kv.first >> 9), s1, l1);
+            sym_of((int)(kv.first & 511), s2, l2);
+            if (l1 >= 8) continue;
+            const uint32_t l = std::min<uint32_t>(8, l1 + l2);
+            uint64_t sy = s1 | (s2 << (8 * l1));
+            if (l < 8) sy &= (1ull << (8 * l)) - 1;
+            add(sy, l, kv.second * l);
+        }
+        std::vector<std::pair<Key, uint64_t>> cand(gain.begin(), gain.end());
+        std::sort(cand.begin(), cand.end(), [](const auto &a, const auto &b) {
+            return a.second != b.second ? a.second > b.second : a.first < b.first;
+        });
+        st = FsstTable();
+        for (auto &c : cand) {
+            if (st.n == 255) break;
+            st.sym[st.n] = c.first.sym;
+            st.len[st.n] = (uint8_t)c.first.len;
+            st.n++;
+        }
+    }
+    st.index();
+    return st;
+}
+
+std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n) {
+    const FsstTable st = fsst_build(offs, bytes, n);
+    std::vector<uint8_t> table(kFsstTableBytes, 0);
+    memcpy(table.data(), st.sym, 8 * 256);
+    memcpy(table.data() + 8 * 256, st.len, 256);
+    const uint32_t nvec = (n + 1023) / 1024;
+    std::vector<VecOut> vecs(nvec);
+    uint64_t lens[1024], u[1024];
+    uint64_t heap = 0;
+    std::vector<uint8_t> comp;
+    for (uint32_t k = 0; k < nvec; ++k) {
+        const uint32_t b = k * 1024, vn = std::min<uint32_t>(1024, n - b);
+        comp.clear();
+        for (uint32_t i = 0; i < vn; ++i)
+            st.compress((const uint8_t *)bytes + offs[b + i], offs[b + i + 1] - offs[b + i], comp);
+        for (uint32_t i = 0; i < 1024; ++i) lens[i] = i < vn ? offs[b + i + 1] - offs[b + i] : 0;
+        const uint64_t dbytes = offs[b + vn] - offs[b];
+        int64_t base;
+        const int W = ffor_prepare(32, lens, base, u);
+        VecOut &o = vecs[k];
+        o.meta = VecMeta{};
+        o.meta.for_base = base;
+        o.meta.bw = (uint8_t)W;
+        o.meta.nvals = (uint16_t)vn;
+        o.meta.aux_count = (uint32_t)dbytes;
+        o.packed.assign((size_t)128 * W, 0);
+        pack(32, W, u, o.packed.data());
+        FsstVecHeader vh{};
+        vh.heap_off = (uint32_t)heap;
+        vh.comp_len = (uint32_t)comp.size();
+        o.aux.resize(sizeof(vh) + comp.size());
+        memcpy(o.aux.data(), &vh, sizeof(vh));
+        if (!comp.empty()) memcpy(o.aux.data() + sizeof(vh), comp.data(), comp.size());
+        heap += (dbytes + 15) & ~15ull;
+    }
+    return assemble_chunk(ENC_FSST, 32, 0, true, n, vecs, table, (uint32_t)st.n, heap);
+}
+
+// VARCHAR: DICT when the distinct values are few, else FSST
+std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const char *bytes, uint32_t n) {
+    if (enc == ENC_AUTO) {
+        std::unordered_map<std::string_view, uint32_t> seen;
+        uint64_t dict_bytes = 0;
+        for (uint32_t i = 0; i < n && seen.size() <= n / 8; ++i) {
+            std::string_view sv(bytes + offs[i], offs[i + 1] - offs[i]);
+            if (seen.emplace(sv, 0).second) dict_bytes += sv.size() + 4;
+        }
+        enc = seen.size() <= n / 8 && dict_bytes < (uint64_t)(offs[n] - offs[0]) / 2 ? ENC_DICT : ENC_FSST;
+    }
+    return enc == ENC_FSST ? enc_fsst(offs, bytes, n) : enc_dict_str(offs, bytes, n);
+}
+
 // FastLanes-RLE: per vector run values + run-index vector (u16) DELTA-coded
 std::vector<uint8_t> enc_rle(int T, const uint64_t *vals, uint32_t n) {
     const uint32_t nvec = (n + 1023) / 1024;
@@ -320,6 +501,158 @@ std::vector<uint8_t> enc_rle(int T, const uint64_t *vals, uint32_t n) {
         pack(16, W, u, o.packed.data());
     }
     return assemble_chunk(ENC_RLE, 16, (uint8_t)T, false, n, vecs, {}, 0);
+}
+
+// ---- ALP (FLOAT / DOUBLE) ----------------------------------------------------
+// Afroozeh et al., SIGMOD 2024: per vector an exponent e and factor f (f <= e)
+// such that most values n satisfy n == (F)d * 10^f * 10^-e for the integer
+// d = round(n * 10^e * 10^-f); the d are FFOR-packed, the rest are exceptions
+// (position + original value).  (e, f) selection is ALP's two-level sampling:
+// the chunk's sampled vectors vote for their best combination, each vector
+// then picks the cheapest of the top five on its own sample.
+
+template <class F>
+struct AlpT;
+template <>
+struct AlpT<double> {
+    using I = int64_t;
+    using U = uint64_t;
+    static constexpr int T = 64, kMaxE = kAlpMaxExpD;
+    static constexpr double F10[] = {FLS_ALP_F10_D};
+    static constexpr double IF10[] = {FLS_ALP_IF10_D};
+    static constexpr double kLimit = 9.2233720368547748e18;  // below 2^63
+};
+template <>
+struct AlpT<float> {
+    using I = int32_t;
+    using U = uint32_t;
+    static constexpr int T = 32, kMaxE = kAlpMaxExpF;
+    static constexpr float F10[] = {FLS_ALP_F10_F};
+    static constexpr float IF10[] = {FLS_ALP_IF10_F};
+    static constexpr float kLimit = 2.1474835e9f;  // below 2^31
+};
+
+template <class F>
+inline bool alp_encode_one(F n, int e, int f, typename AlpT<F>::I &d) {
+    using A = AlpT<F>;
+    const F tmp = n * A::F10[e] * A::IF10[f];
+    if (!(std::fabs(tmp) < A::kLimit)) return false;  // also rejects NaN / inf
+    d = (typename A::I)std::nearbyint(tmp);
+    const F back = (F)d * A::F10[f] * A::IF10[e];
+    return memcmp(&back, &n, sizeof(F)) == 0;  // bit-exact (keeps -0.0 as an exception)
+}
+
+// estimated bits of one sample under (e, f)
+template <class F>
+uint64_t alp_cost(const F *x, int n, int e, int f) {
+    using A = AlpT<F>;
+    typename A::I mn = 0, mx = 0, d;
+    bool any = false;
+    int exc = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!alp_encode_one<F>(x[i], e, f, d)) { ++exc; continue; }
+        if (!any) { mn = mx = d; any = true; }
+        mn = std::min(mn, d);
+        mx = std::max(mx, d);
+    }
+    const uint64_t range = any ? (uint64_t)((typename A::U)mx - (typename A::U)mn) : 0;
+    return (uint64_t)bitlen(range) * n + (uint64_t)exc * (16 + A::T);
+}
+
+template <class F>
+void alp_sample(const F *v, uint32_t vn, F *s, int &n) {
+    n = (int)std::min<uint32_t>(32, vn);
+    for (int i = 0; i < n; ++i) s[i] = v[(uint64_t)i * vn / n];
+}
+
+template <class F>
+std::vector<uint8_t> enc_alp(const uint64_t *bits, uint32_t n) {
+    using A = AlpT<F>;
+    constexpr int T = A::T;
+    const uint32_t nvec = (n + 1023) / 1024;
+    std::vector<F> vals(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        typename A::U u = (typename A::U)bits[i];
+        memcpy(&vals[i], &u, sizeof(F));
+    }
+    // level 1: sampled vectors vote for their best (e, f)
+    std::vector<std::pair<int, int>> combos;
+    {
+        std::vector<int> votes((A::kMaxE + 1) * (A::kMaxE + 1), 0);
+        const uint32_t nsv = std::min<uint32_t>(8, nvec);
+        F smp[32];
+        int sn;
+        for (uint32_t k = 0; k < nsv; ++k) {
+            const uint32_t v = (uint32_t)((uint64_t)k * nvec / nsv);
+            const uint32_t b = v * 1024, vn = std::min<uint32_t>(1024, n - b);
+            alp_sample<F>(vals.data() + b, vn, smp, sn);
+            uint64_t best = UINT64_MAX;
+            int be = 0, bf = 0;
+            for (int e = 0; e <= A::kMaxE; ++e)
+                for (int f = 0; f <= e; ++f) {
+                    const uint64_t c = alp_cost<F>(smp, sn, e, f);
+                    if (c < best) { best = c; be = e; bf = f; }
+                }
+            votes[be * (A::kMaxE + 1) + bf]++;
+        }
+        std::vector<int> order(votes.size());
+        for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return votes[a] > votes[b]; });
+        for (int i = 0; i < 5 && votes[order[i]] > 0; ++i)
+            combos.emplace_back(order[i] / (A::kMaxE + 1), order[i] % (A::kMaxE + 1));
+        if (combos.empty()) combos.emplace_back(0, 0);
+    }
+    std::vector<VecOut> vecs(nvec);
+    uint64_t u64v[1024], u[1024];
+    for (uint32_t k = 0; k < nvec; ++k) {
+        const uint32_t b = k * 1024, vn = std::min<uint32_t>(1024, n - b);
+        const F *v = vals.data() + b;
+        // level 2: cheapest of the chunk's combinations on this vector's sample
+        int e = combos[0].first, f = combos[0].second;
+        if (combos.size() > 1) {
+            F smp[32];
+            int sn;
+            alp_sample<F>(v, vn, smp, sn);
+            uint64_t best = UINT64_MAX;
+            for (auto &c : combos) {
+                const uint64_t cost = alp_cost<F>(smp, sn, c.first, c.second);
+                if (cost < best) { best = cost; e = c.first; f = c.second; }
+            }
+        }
+        typename A::I d[1024];
+        std::vector<uint16_t> pos;
+        bool have_fill = false;
+        typename A::I fill = 0;
+        for (uint32_t i = 0; i < vn; ++i) {
+            if (alp_encode_one<F>(v[i], e, f, d[i])) {
+                if (!have_fill) { fill = d[i]; have_fill = true; }
+            } else {
+                pos.push_back((uint16_t)i);
+            }
+        }
+        for (uint16_t p : pos) d[p] = fill;           // keep the FFOR range tight
+        for (uint32_t i = 0; i < 1024; ++i) {
+            const typename A::I x = i < vn ? d[i] : d[vn - 1];
+            u64v[i] = (uint64_t)(typename A::U)x;
+        }
+        int64_t base;
+        const int W = ffor_prepare(T, u64v, base, u);
+        VecOut &o = vecs[k];
+        o.meta = VecMeta{};
+        o.meta.for_base = base;
+        o.meta.bw = (uint8_t)W;
+        o.meta.nvals = (uint16_t)vn;
+        o.meta.aux_count = (uint32_t)pos.size() | ((uint32_t)e << 16) | ((uint32_t)f << 24);
+        o.packed.assign((size_t)128 * W, 0);
+        pack(T, W, u, o.packed.data());
+        if (!pos.empty()) {
+            o.aux.assign(alp_aux_bytes((uint32_t)pos.size(), T), 0);
+            memcpy(o.aux.data(), pos.data(), 2 * pos.size());
+            uint8_t *ev = o.aux.data() + ((2 * pos.size() + 15) & ~size_t(15));
+            for (size_t j = 0; j < pos.size(); ++j) memcpy(ev + j * sizeof(F), &v[pos[j]], sizeof(F));
+        }
+    }
+    return assemble_chunk(ENC_ALP, (uint8_t)T, (uint8_t)T, false, n, vecs, {}, 0);
 }
 
 // estimated encoded bytes for ENC_AUTO
@@ -371,6 +704,8 @@ struct ColSpec {
 
 // Encode one integer chunk with a chosen (or automatic) encoding.
 std::vector<uint8_t> encode_int_chunk(uint8_t type, uint8_t enc, const uint64_t *vals, uint32_t n) {
+    if (type == TY_DOUBLE) return enc_alp<double>(vals, n);
+    if (type == TY_FLOAT) return enc_alp<float>(vals, n);
     const int T = type_value_bits(type);
     if (enc == ENC_AUTO) {
         size_t best = est_ffor(T, vals, n);
@@ -613,9 +948,15 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
                           uint8_t encoding) {
     if (!w || !name) return fail(FLS_ERR_ARG, "fls_writer_add_column: NULL argument");
     if (!type_valid(type)) return fail(FLS_ERR_ARG, "fls_writer_add_column: unsupported type %u", type);
-    if (encoding > ENC_RLE) return fail(FLS_ERR_ARG, "fls_writer_add_column: bad encoding %u", encoding);
-    if (type == TY_VARCHAR && encoding != ENC_AUTO && encoding != ENC_DICT)
-        return fail(FLS_ERR_ARG, "fls_writer_add_column: VARCHAR supports DICT only");
+    if (encoding > ENC_FSST || encoding == 6) return fail(FLS_ERR_ARG, "fls_writer_add_column: bad encoding %u", encoding);
+    if (type == TY_VARCHAR && encoding != ENC_AUTO && encoding != ENC_DICT && encoding != ENC_FSST)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: VARCHAR supports DICT and FSST");
+    if (type_is_float(type) && encoding != ENC_AUTO && encoding != ENC_ALP)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: FLOAT/DOUBLE support ALP");
+    if (!type_is_float(type) && encoding == ENC_ALP)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: ALP needs FLOAT/DOUBLE");
+    if (type != TY_VARCHAR && encoding == ENC_FSST)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: FSST needs VARCHAR");
     if (!w->fb.rgs.empty()) return fail(FLS_ERR_STATE, "fls_writer_add_column: after first row group");
     if (strlen(name) > 65535) return fail(FLS_ERR_ARG, "column name too long");
     w->fb.cols.push_back(ColSpec{name, type, width, scale, encoding});
@@ -640,7 +981,7 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
             const uint32_t *o = str_offsets[c];
             for (uint32_t i = 0; i < nrows; ++i)
                 if (o[i + 1] < o[i]) return fail(FLS_ERR_ARG, "column %zu: offsets not monotone", c);
-            rg.chunks.push_back(enc_dict_str(o, (const char *)data[c], nrows));
+            rg.chunks.push_back(encode_str_chunk(cs.enc, o, (const char *)data[c], nrows));
         } else {
             const int T = type_value_bits(cs.type);
             std::vector<uint64_t> v(nrows);

@@ -144,6 +144,9 @@ struct DeviceShard {
     DevBuf<StrT> strtab;               // string_t tables of VARCHAR chunks
     std::vector<uint64_t> strtab_off;  // per (rg - rg0) * ncols + col: index into strtab
     DevBuf<uint32_t> err;
+    std::vector<DevBuf<uint8_t>> d_heap;   // per FSST column: decoded string bytes
+    std::vector<PinBuf<uint8_t>> h_heap;   // per FSST column: host copy string_t points into
+    std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
 };
 
 struct Slot {                       // one batch of row groups in flight
@@ -151,6 +154,9 @@ struct Slot {                       // one batch of row groups in flight
     bool busy = false;
     std::vector<DevBuf<uint8_t>> d_out;   // per column
     std::vector<PinBuf<uint8_t>> h_out;   // per column (pinned)
+    std::vector<DevBuf<uint8_t>> d_heap;  // per FSST column: decoded string bytes
+    std::vector<PinBuf<uint8_t>> h_heap;  // per FSST column: pinned copy string_t points into
+    std::vector<uint64_t> heap_bytes;     // per column: heap bytes of this batch
     PinBuf<DevChunk> h_chunks;
     DevBuf<DevChunk> d_chunks;
     DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch
@@ -204,6 +210,7 @@ struct fls_table {
     DevBuf<DevChunk> d_chunks;
     std::vector<DevChunk> h_chunks;
     std::vector<uint8_t> dev_mask;     // column mask h_chunks was built for
+    uint32_t dev_nmain = 0;            // h_chunks[0, dev_nmain) main kernel, the rest FSST
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
@@ -232,6 +239,7 @@ int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBu
         for (uint32_t c = 0; c < ncols; ++c) {
             if (t->meta.cols[c].type != TY_VARCHAR) continue;
             const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+            if (ch.hdr.enc != ENC_DICT) continue;  // FSST strings are decoded on the GPU
             const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
             const uint32_t n = ch.hdr.dict_count;
             const char *bytes = (const char *)aux + 4ull * (n + 1);
@@ -251,7 +259,7 @@ int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBu
 
 // Describe chunk (rg, col) located at d_chunk_base (device) for the kernel.
 DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint8_t *d_chunk, const uint8_t *d_dict,
-                       uint8_t *d_out, ByteCount *bc) {
+                       uint8_t *d_out, ByteCount *bc, uint8_t *d_heap = nullptr, const uint8_t *h_heap = nullptr) {
     const ChunkRef &ch = t->meta.rgs[rg].chunks[col];
     const ChunkHeader &h = ch.hdr;
     DevChunk d;
@@ -269,6 +277,23 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
     d.ob = (uint8_t)out_bytes_of(t, col);
     if (h.enc == ENC_DICT) d.dict = h.is_str ? d_dict : d_chunk + h.aux_off;
     bc->values += h.nvals;
+    if (h.enc == ENC_FSST) {
+        d.dict = d_heap;
+        d.heap_host = (uint64_t)(uintptr_t)h_heap;
+        d.heap_bytes = (uint32_t)h.reserved1;
+        bc->out += (uint64_t)h.nvals * 16 + h.reserved1;
+        bc->meta += 32ull * h.nvec + kFsstTableBytes;
+        const uint8_t *meta = t->img + ch.off + h.meta_off;
+        for (uint32_t v = 0; v < h.nvec; ++v) {
+            VecMeta vm;
+            memcpy(&vm, meta + 32ull * v, 32);
+            FsstVecHeader fh;
+            memcpy(&fh, t->img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
+            bc->packed += 128ull * vm.bw + fh.comp_len;
+            bc->meta += sizeof(fh);
+        }
+        return d;  // separate kernel, fixed LDS layout
+    }
     bc->out += (uint64_t)h.nvals * d.ob;
     bc->meta += 32ull * h.nvec;
     const uint8_t *meta = t->img + ch.off + h.meta_off;
@@ -280,6 +305,8 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
         max_w = std::max<uint32_t>(max_w, vm.bw);
         if (h.enc == ENC_DELTA) bc->meta += 128;
         if (h.enc == ENC_RLE) bc->meta += 128 + (uint64_t)vm.aux_count * (h.vbits / 8);
+        if (h.enc == ENC_ALP && alp_exceptions(vm.aux_count))
+            bc->meta += alp_aux_bytes(alp_exceptions(vm.aux_count), h.vbits);
     }
     if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? 16 : h.vbits / 8);
     uint32_t pb, vb;
@@ -290,6 +317,21 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
 }
 
 bool col_selected(const std::vector<uint8_t> &mask, uint32_t c) { return mask.empty() || mask[c]; }
+
+bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[rg].chunks[c].hdr.enc == ENC_FSST; }
+
+// FSST chunks go last (their own kernel); returns how many lead (main kernel)
+uint32_t order_for_launch(std::vector<DevChunk> &v) {
+    auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
+    return (uint32_t)(mid - v.begin());
+}
+
+hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t *d_err, const DecodeGeom &geom,
+                      hipStream_t stream) {
+    hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream);
+    if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, ntotal - nmain, d_err, stream);
+    return e;
+}
 
 }  // namespace
 
@@ -396,19 +438,27 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     HIP_TRY(sl.d_in.alloc(d.dev, hi - lo));
     sl.in_base = lo;
     HIP_TRY(hipMemcpyAsync(sl.d_in.p, t->img + lo, hi - lo, hipMemcpyHostToDevice, sl.stream));
-    // 2. decode into the slot's device columns
+    // 2. decode into the slot's device columns (FSST columns also into a heap)
     const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
-    uint32_t nsel = 0;
+    sl.heap_bytes.assign(ncols, 0);
+    sl.d_heap.resize(ncols);
+    sl.h_heap.resize(ncols);
+    std::vector<uint64_t> hoff((size_t)sl.nrg * ncols, 0);
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
-        ++nsel;
         const uint64_t nb = max_rows * out_bytes_of(t, c);
         HIP_TRY(sl.d_out[c].alloc(d.dev, nb));
         HIP_TRY(sl.h_out[c].alloc(nb));
+        for (uint32_t r = 0; r < sl.nrg; ++r) {
+            hoff[(size_t)r * ncols + c] = sl.heap_bytes[c];
+            if (is_fsst(t, sl.rg0 + r, c)) sl.heap_bytes[c] += t->meta.rgs[sl.rg0 + r].chunks[c].hdr.reserved1;
+        }
+        if (sl.heap_bytes[c]) {
+            HIP_TRY(sl.d_heap[c].alloc(d.dev, sl.heap_bytes[c]));
+            HIP_TRY(sl.h_heap[c].alloc(sl.heap_bytes[c]));
+        }
     }
-    HIP_TRY(sl.h_chunks.alloc((size_t)nsel * sl.nrg));
-    HIP_TRY(sl.d_chunks.alloc(d.dev, (size_t)nsel * sl.nrg));
-    size_t k = 0;
+    std::vector<DevChunk> list;
     ByteCount bc;
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
@@ -418,18 +468,28 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
             uint8_t *out = sl.d_out[c].p +
                            (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * out_bytes_of(t, c);
-            sl.h_chunks.p[k++] = make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc);
+            const uint64_t ho = hoff[(size_t)(r - sl.rg0) * ncols + c];
+            list.push_back(make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc,
+                                         sl.heap_bytes[c] ? sl.d_heap[c].p + ho : nullptr,
+                                         sl.heap_bytes[c] ? sl.h_heap[c].p + ho : nullptr));
         }
     }
+    const uint32_t nmain = order_for_launch(list);
+    const size_t k = list.size();
+    HIP_TRY(sl.h_chunks.alloc(k));
+    HIP_TRY(sl.d_chunks.alloc(d.dev, k));
+    if (k) memcpy(sl.h_chunks.p, list.data(), k * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
-    HIP_TRY(launch_decode(sl.d_chunks.p, (uint32_t)k, d.err.p, bc.geom, sl.stream));
-    // 3. D2H into pinned host columns
+    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, d.err.p, bc.geom, sl.stream));
+    // 3. D2H into pinned host columns (and string heaps)
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
         HIP_TRY(hipMemcpyAsync(sl.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
                                sl.stream));
+        if (sl.heap_bytes[c])
+            HIP_TRY(hipMemcpyAsync(sl.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
     }
     HIP_TRY(hipEventRecord(sl.done, sl.stream));
     sl.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
@@ -697,6 +757,24 @@ int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
     t->res_rows = t->meta.rgs[rg_end - 1].first_row + t->meta.rgs[rg_end - 1].nrows - t->res_first_row;
     t->d_out.resize(ncols);
     for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(t->d_out[c].alloc(dev, t->res_rows * out_bytes_of(t, c)));
+    // FSST heaps: chunk heaps back to back per column, host copy for string_t
+    sh.heap_off.assign((size_t)(rg_end - rg_begin) * ncols, 0);
+    sh.d_heap.resize(ncols);
+    sh.h_heap.resize(ncols);
+    for (uint32_t c = 0; c < ncols; ++c) {
+        uint64_t tot = 0;
+        for (uint32_t r = rg_begin; r < rg_end; ++r) {
+            sh.heap_off[(size_t)(r - rg_begin) * ncols + c] = tot;
+            if (is_fsst(t, r, c)) tot += t->meta.rgs[r].chunks[c].hdr.reserved1;
+        }
+        if (tot) {
+            HIP_TRY(sh.d_heap[c].alloc(dev, tot));
+            HIP_TRY(sh.h_heap[c].alloc(tot));
+        } else {
+            sh.d_heap[c].release();
+            sh.h_heap[c].release();
+        }
+    }
     t->h_chunks.clear();
     t->dev_mask.clear();
     t->launches = 0;
@@ -725,9 +803,13 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
                 const uint64_t so = sh.strtab_off[(size_t)(r - sh.rg0) * ncols + c];
                 const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(sh.strtab.p + so);
                 uint8_t *out = t->d_out[c].p + (t->meta.rgs[r].first_row - t->res_first_row) * out_bytes_of(t, c);
-                chunks.push_back(make_devchunk(t, r, c, sh.img.p + (ch.off - sh.base), dict, out, &bc));
+                const uint64_t ho = sh.heap_off[(size_t)(r - sh.rg0) * ncols + c];
+                chunks.push_back(make_devchunk(t, r, c, sh.img.p + (ch.off - sh.base), dict, out, &bc,
+                                               sh.d_heap[c].p ? sh.d_heap[c].p + ho : nullptr,
+                                               sh.h_heap[c].p ? sh.h_heap[c].p + ho : nullptr));
             }
         }
+        t->dev_nmain = order_for_launch(chunks);
         HIP_TRY(hipStreamSynchronize(t->stream));
         HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
         HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
@@ -746,7 +828,8 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(launch_decode(t->d_chunks.p, (uint32_t)t->h_chunks.size(), sh.err.p, t->last_bytes.geom, t->stream));
+    HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), sh.err.p, t->last_bytes.geom,
+                       t->stream));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;
     t->launched = true;
@@ -796,6 +879,9 @@ int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, vo
     HIP_TRY(hipSetDevice(t->shard.dev));
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(host_dst, t->d_out[col].p + row * ob, n * ob, hipMemcpyDeviceToHost));
+    // FSST: string_t pointers target the host copy of the column's heap
+    if (col < t->shard.d_heap.size() && t->shard.d_heap[col].p)
+        HIP_TRY(hipMemcpy(t->shard.h_heap[col].p, t->shard.d_heap[col].p, t->shard.d_heap[col].n, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -244,6 +244,7 @@ struct FlatVector {
     template <class T>
     static T *GetData(Vector &v) { return reinterpret_cast<T *>(v.GetData()); }
     static void SetNull(Vector &v, idx_t i, bool is_null) { v.SetValid(i, !is_null); }
+    static bool IsNull(const Vector &v, idx_t i) { return !v.RowIsValid(i); }
 };
 struct StringVector {
     static string_t AddString(Vector &v, const string &s) { return v.AddString(s); }
@@ -262,6 +263,7 @@ public:
         count_ = 0;
     }
     void Initialize(const vector<LogicalType> &types) { InitializeEmpty(types); }
+    void Flatten() {}  // shim vectors are always flat
     void Reset() {
         for (auto &v : data) v.Reset();
         count_ = 0;

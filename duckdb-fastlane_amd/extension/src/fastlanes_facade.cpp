@@ -101,6 +101,18 @@ static void RenderCell(Vector &vec, idx_t out_row, const fls_column_info &ci, co
         memcpy(&v, (const uint8_t *)col + 8 * row, 8);
         break;
     }
+    case FLS_FLOAT: {  // flt_col_t -> Value::FLOAT -> VARCHAR (src/fastlanes_facade.cpp:140-147)
+        float x;
+        memcpy(&x, (const uint8_t *)col + 4 * row, 4);
+        FlatVector::GetData<string_t>(vec)[out_row] = StringVector::AddString(vec, Value::FLOAT(x).ToString());
+        return;
+    }
+    case FLS_DOUBLE: {  // dbl_col_t -> Value::DOUBLE -> VARCHAR (:148-155)
+        double x;
+        memcpy(&x, (const uint8_t *)col + 8 * row, 8);
+        FlatVector::GetData<string_t>(vec)[out_row] = StringVector::AddString(vec, Value::DOUBLE(x).ToString());
+        return;
+    }
     case FLS_VARCHAR: {  // str_col_t / FLSStrColumn
         string_t s;
         memcpy(&s, (const uint8_t *)col + 16 * row, 16);

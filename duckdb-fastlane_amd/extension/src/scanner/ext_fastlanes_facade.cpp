@@ -98,6 +98,8 @@ static Value BoxValue(const fls_column_info &ci, const void *col, idx_t row) {
     case FLS_UINT64: return Value::UBIGINT(ld(uint64_t()));
     case FLS_DATE: return Value::DATE(date_t{ld(int32_t())});
     case FLS_DECIMAL: return Value::DECIMAL(ld(int64_t()), ci.width ? ci.width : 18, ci.scale);
+    case FLS_FLOAT: return Value::FLOAT(ld(float()));
+    case FLS_DOUBLE: return Value::DOUBLE(ld(double()));
     case FLS_VARCHAR: {
         string_t s;
         memcpy(&s, p + 16 * row, 16);
@@ -177,22 +179,41 @@ bool FastLanesFacade::Impl::flush_rowgroup() {
     return ok;
 }
 
+// DuckDB's physical width of a fixed-size column (DECIMAL narrows with width)
+static idx_t PhysicalWidth(const LogicalType &t) {
+    if (t.id() == LogicalTypeId::DECIMAL) return t.Width() <= 4 ? 2 : t.Width() <= 9 ? 4 : 8;
+    return TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
+}
+
 bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     Impl &s = *pImpl;
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
+    chunk.Flatten();
     for (idx_t r = 0; r < chunk.size(); ++r) {
         for (size_t c = 0; c < s.wtypes.size(); ++c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
+            const bool null = FlatVector::IsNull(v, r);  // NULLs have no encoding on this path
             if (t.id() == LogicalTypeId::VARCHAR) {
-                const std::string str = v.RowIsValid(r) ? v.GetValue(r).GetValue<string>() : std::string();
-                s.wcols[c].insert(s.wcols[c].end(), str.begin(), str.end());
+                if (!null) {
+                    const string_t str = FlatVector::GetData<string_t>(v)[r];
+                    s.wcols[c].insert(s.wcols[c].end(), str.GetData(), str.GetData() + str.GetSize());
+                }
                 s.woffs[c].push_back((uint32_t)s.wcols[c].size());
             } else {
-                // NULLs have no encoding on this path: written as 0
+                // the physical bytes (FLOAT/DOUBLE bit-exact for ALP); DECIMAL widened to int64
                 const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
-                int64_t x = v.RowIsValid(r) ? v.GetValue(r).GetInt64() : 0;
-                const uint8_t *b = (const uint8_t *)&x;
+                const idx_t pw = PhysicalWidth(t);
+                uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (!null) {
+                    const uint8_t *src = FlatVector::GetData<uint8_t>(v) + r * pw;
+                    if (pw < w) {  // narrow DECIMAL: sign-extend
+                        int64_t x = pw == 2 ? (int64_t)*(const int16_t *)src : (int64_t)*(const int32_t *)src;
+                        memcpy(b, &x, 8);
+                    } else {
+                        memcpy(b, src, w);
+                    }
+                }
                 s.wcols[c].insert(s.wcols[c].end(), b, b + w);
             }
         }

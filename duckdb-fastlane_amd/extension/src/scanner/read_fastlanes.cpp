@@ -12,6 +12,9 @@
 // string_t records point into the file image, kept alive by every thread that
 // holds one of its row groups.  Error texts follow
 // src/scanner/scan_fastlanes.cpp:62-97.
+#include <glob.h>
+
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -81,7 +84,21 @@ void CollectPaths(const Value &v, vector<string> &files, const char *fn) {
         return;
     }
     if (v.type() != LogicalType::VARCHAR) throw BinderException(string(fn) + " file paths must be strings");
-    files.push_back(v.GetValue<string>());
+    const string path = v.GetValue<string>();
+    if (path.find_first_of("*?[") == string::npos) {
+        files.push_back(path);
+        return;
+    }
+    // glob pattern, expanded in sorted order like DuckDB's FileSystem::GlobFiles
+    glob_t g{};
+    const int rc = glob(path.c_str(), 0, nullptr, &g);
+    vector<string> hits;
+    if (rc == 0)
+        for (size_t i = 0; i < g.gl_pathc; ++i) hits.emplace_back(g.gl_pathv[i]);
+    globfree(&g);
+    if (hits.empty()) throw IOException("No files found that match the pattern \"" + path + "\"");
+    std::sort(hits.begin(), hits.end());
+    files.insert(files.end(), hits.begin(), hits.end());
 }
 
 unique_ptr<FunctionData> ReadBind(ClientContext &, TableFunctionBindInput &input, vector<LogicalType> &return_types,

@@ -18,6 +18,8 @@ LogicalType TypeMapping::FastLanesToDuckDB(uint8_t t, uint8_t width, uint8_t sca
     case FLS_UINT64: return LogicalType::UBIGINT;
     case FLS_DATE: return LogicalType::DATE;
     case FLS_DECIMAL: return LogicalType::DECIMAL(width ? width : 18, scale);
+    case FLS_FLOAT: return LogicalType::FLOAT;
+    case FLS_DOUBLE: return LogicalType::DOUBLE;
     case FLS_VARCHAR: return LogicalType::VARCHAR;
     default: return LogicalType::SQLNULL;
     }
@@ -38,7 +40,9 @@ uint8_t TypeMapping::DuckDBToFastLanes(const LogicalType &type) {
     // widths are widened by the writer glue
     case LogicalTypeId::DECIMAL: return type.Width() <= 18 ? FLS_DECIMAL : 0;
     case LogicalTypeId::VARCHAR: return FLS_VARCHAR;
-    default: return 0;  // FLOAT/DOUBLE need ALP, a later row
+    case LogicalTypeId::FLOAT: return FLS_FLOAT;    // ALP
+    case LogicalTypeId::DOUBLE: return FLS_DOUBLE;  // ALP
+    default: return 0;
     }
 }
 
@@ -46,8 +50,8 @@ idx_t TypeMapping::GetFastLanesTypeSize(uint8_t t) {
     switch (t) {
     case FLS_INT8: case FLS_UINT8: return 1;
     case FLS_INT16: case FLS_UINT16: return 2;
-    case FLS_INT32: case FLS_UINT32: case FLS_DATE: return 4;
-    case FLS_INT64: case FLS_UINT64: case FLS_DECIMAL: return 8;
+    case FLS_INT32: case FLS_UINT32: case FLS_DATE: case FLS_FLOAT: return 4;
+    case FLS_INT64: case FLS_UINT64: case FLS_DECIMAL: case FLS_DOUBLE: return 8;
     case FLS_VARCHAR: return 16;
     default: return 0;
     }

@@ -28,10 +28,15 @@ typedef struct fls_writer fls_writer;
 enum fls_type {
     FLS_INT8 = 1, FLS_INT16 = 2, FLS_INT32 = 3, FLS_INT64 = 4,
     FLS_UINT8 = 5, FLS_UINT16 = 6, FLS_UINT32 = 7, FLS_UINT64 = 8,
-    FLS_DATE = 10, FLS_DECIMAL = 11, FLS_VARCHAR = 20
+    FLS_DATE = 10, FLS_DECIMAL = 11, FLS_FLOAT = 12, FLS_DOUBLE = 13, FLS_VARCHAR = 20
 };
-/* Encodings; FLS_ENC_AUTO picks the smallest of the applicable ones per chunk. */
-enum fls_encoding { FLS_ENC_AUTO = 0, FLS_ENC_FFOR = 1, FLS_ENC_DELTA = 2, FLS_ENC_DICT = 3, FLS_ENC_RLE = 4 };
+/* Encodings; FLS_ENC_AUTO picks per chunk: the smallest of FFOR/DELTA/DICT/RLE
+ * for integers, ALP for FLOAT/DOUBLE, DICT or FSST for VARCHAR. */
+enum fls_encoding {
+    FLS_ENC_AUTO = 0, FLS_ENC_FFOR = 1, FLS_ENC_DELTA = 2, FLS_ENC_DICT = 3, FLS_ENC_RLE = 4,
+    FLS_ENC_ALP = 5,  /* FLOAT/DOUBLE */
+    FLS_ENC_FSST = 7  /* VARCHAR */
+};
 
 /* New writer; row_offset = global index of the first row (shards). */
 fls_writer *fls_writer_new(uint64_t row_offset);
@@ -43,7 +48,7 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
  * Must be called before the first row group. */
 int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows);
 /* Append one row group of nrows (1..row group size) rows; only the last row
- * group of a file may be short.  Integer column c:
+ * group of a file may be short.  Integer / FLOAT / DOUBLE column c:
  * data[c] -> nrows values of the column's width (1/2/4/8 B).  VARCHAR column c:
  * data[c] -> concatenated bytes, str_offsets[c] -> nrows+1 uint32 offsets
  * (str_offsets may be NULL when there is no VARCHAR column). */

@@ -17,7 +17,13 @@
  *     16*T tuples; value = lane base + running sum of deltas;
  *   - DICT: value = dict[base + unpacked code];
  *   - RLE (FastLanes-RLE): run index vector decoded as DELTA(T=16), then
- *     value = run_values[index].
+ *     value = run_values[index];
+ *   - ALP (Afroozeh, Kuffo, Boncz, SIGMOD 2024) for FLOAT/DOUBLE: the FFOR
+ *     stream holds integers d, value = (F)d * 10^f * 10^-e, then exceptions
+ *     (position, original value) are patched in;
+ *   - FSST (Boncz, Neumann, Leis, VLDB 2020) for VARCHAR: a string is a run
+ *     of byte codes, code c < 255 expands to symbol[c] (1..8 bytes), code 255
+ *     is followed by one literal byte.
  * It is written as plain scalar loops on purpose: it is the checker, not the
  * thing measured (besides the cpu_baseline leg of bench.py).
  */
@@ -29,12 +35,20 @@
 
 static const uint32_t FL_ORDER[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 
-enum { ENC_FFOR = 1, ENC_DELTA = 2, ENC_DICT = 3, ENC_RLE = 4 };
+enum { ENC_FFOR = 1, ENC_DELTA = 2, ENC_DICT = 3, ENC_RLE = 4, ENC_ALP = 5, ENC_FSST = 7 };
 enum {
     TY_INT8 = 1, TY_INT16 = 2, TY_INT32 = 3, TY_INT64 = 4,
     TY_UINT8 = 5, TY_UINT16 = 6, TY_UINT32 = 7, TY_UINT64 = 8,
-    TY_DATE = 10, TY_DECIMAL = 11, TY_VARCHAR = 20
+    TY_DATE = 10, TY_DECIMAL = 11, TY_FLOAT = 12, TY_DOUBLE = 13, TY_VARCHAR = 20
 };
+
+/* ALP: 10^i and the nearest binary64/binary32 to 10^-i */
+static const double ALP_F10_D[19] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10,
+                                     1e11, 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18};
+static const double ALP_IF10_D[19] = {1e-0, 1e-1, 1e-2, 1e-3, 1e-4, 1e-5, 1e-6, 1e-7, 1e-8, 1e-9, 1e-10,
+                                      1e-11, 1e-12, 1e-13, 1e-14, 1e-15, 1e-16, 1e-17, 1e-18};
+static const float ALP_F10_F[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+static const float ALP_IF10_F[11] = {1e-0f, 1e-1f, 1e-2f, 1e-3f, 1e-4f, 1e-5f, 1e-6f, 1e-7f, 1e-8f, 1e-9f, 1e-10f};
 
 /* little-endian readers; the image is not necessarily aligned for us */
 static uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
@@ -188,8 +202,8 @@ static int value_bytes(int type)
     switch (type) {
     case TY_INT8: case TY_UINT8: return 1;
     case TY_INT16: case TY_UINT16: return 2;
-    case TY_INT32: case TY_UINT32: case TY_DATE: return 4;
-    case TY_INT64: case TY_UINT64: case TY_DECIMAL: return 8;
+    case TY_INT32: case TY_UINT32: case TY_DATE: case TY_FLOAT: return 4;
+    case TY_INT64: case TY_UINT64: case TY_DECIMAL: case TY_DOUBLE: return 8;
     case TY_VARCHAR: return 16;
     default: return 0;
     }
@@ -306,12 +320,113 @@ int64_t flsref_decode(const flsref_file *f, uint32_t col, uint32_t rg, void *out
                 store_val(out, vb, row + i, rd_word(vbits, runs, idx) & vm);
             }
         } break;
+        case ENC_ALP: {
+            const uint32_t exc = acount & 0xFFFF, e = (acount >> 16) & 0xFF, fct = acount >> 24;
+            if (T == 64 ? (e > 18 || fct > e) : (T != 32 || e > 10 || fct > e)) return -1;
+            if (exc > vn) return -1;
+            for (uint32_t i = 0; i < vn; ++i) {
+                const uint64_t d = (for_base + u[i]) & tm;
+                if (T == 64) {
+                    double x = (double)(int64_t)d * ALP_F10_D[fct] * ALP_IF10_D[e];
+                    memcpy(out + 8 * (row + i), &x, 8);
+                } else {
+                    float x = (float)(int32_t)(uint32_t)d * ALP_F10_F[fct] * ALP_IF10_F[e];
+                    memcpy(out + 4 * (row + i), &x, 4);
+                }
+            }
+            const uint8_t *pos = aux + aoff;
+            const uint8_t *val = pos + ((2 * (size_t)exc + 15) & ~(size_t)15);
+            for (uint32_t k = 0; k < exc; ++k) {
+                const uint32_t p = rd16(pos + 2 * k);
+                if (p >= vn) return -1;
+                memcpy(out + (size_t)(T / 8) * (row + p), val + (size_t)(T / 8) * k, T / 8);
+            }
+        } break;
         default:
-            return -1;
+            return -1;  /* FSST strings: flsref_decode_strings */
         }
         row += vn;
     }
     return (int64_t)row;
+}
+
+/* FSST: expand the compressed stream [c, c+clen) into dst (cap bytes).
+ * Returns bytes written, or -1 on a truncated escape / overflow. */
+static int64_t fsst_expand(const uint8_t *table, const uint8_t *c, uint32_t clen, uint8_t *dst, uint64_t cap)
+{
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < clen; ++i) {
+        const uint32_t code = c[i];
+        if (code == 255) {
+            if (++i >= clen || o + 1 > cap) return -1;
+            dst[o++] = c[i];
+        } else {
+            const uint32_t L = table[8 * 256 + code];
+            if (o + L > cap) return -1;
+            memcpy(dst + o, table + 8 * code, L); /* symbol bytes, little-endian order */
+            o += L;
+        }
+    }
+    return (int64_t)o;
+}
+
+int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, uint32_t *offs,
+                              uint8_t *heap, uint64_t cap)
+{
+    if (col >= f->ncols || rg >= f->nrowgroups) return -1;
+    int type, w, s, nl;
+    const char *nm;
+    flsref_column(f, col, &type, &w, &s, &nm, &nl);
+    if (type != TY_VARCHAR) return -1;
+    const uint8_t *rgp = rg_desc(f, rg);
+    const uint32_t rg_rows = rd32(rgp);
+    const uint64_t coff = rd64(rgp + 4 + 16 * (size_t)col);
+    const uint8_t *ch = f->img + coff;
+    const int enc = ch[4];
+    if (enc == ENC_DICT) {
+        uint64_t *pairs = (uint64_t *)malloc(16 * (size_t)rg_rows);
+        if (!pairs) return -1;
+        if (flsref_decode(f, col, rg, pairs) != rg_rows) { free(pairs); return -1; }
+        uint64_t o = 0;
+        offs[0] = 0;
+        for (uint32_t i = 0; i < rg_rows; ++i) {
+            const uint64_t at = pairs[2 * i], len = pairs[2 * i + 1];
+            if (o + len > cap) { free(pairs); return -1; }
+            memcpy(heap + o, f->img + at, len);
+            o += len;
+            offs[i + 1] = (uint32_t)o;
+        }
+        free(pairs);
+        return (int64_t)o;
+    }
+    if (enc != ENC_FSST || ch[5] != 32) return -1;
+    const uint32_t nvec = rd32(ch + 8);
+    const uint8_t *meta = ch + rd64(ch + 16);
+    const uint8_t *packed = ch + rd64(ch + 24);
+    const uint8_t *aux = ch + rd64(ch + 32);
+    uint64_t u[1024];
+    uint64_t o = 0, row = 0;
+    offs[0] = 0;
+    for (uint32_t v = 0; v < nvec; ++v) {
+        const uint8_t *vm_p = meta + 32 * (size_t)v;
+        const uint64_t poff = rd64(vm_p), for_base = rd64(vm_p + 8), aoff = rd64(vm_p + 16);
+        const uint32_t vn = rd16(vm_p + 24), W = vm_p[26], dbytes = rd32(vm_p + 28);
+        if (W > 32 || vn > 1024) return -1;
+        flsref_unpack(32, (int)W, packed + poff, u);
+        const uint8_t *vh = aux + aoff;
+        const uint32_t clen = rd32(vh + 4);
+        if (o + dbytes > cap) return -1;
+        if (fsst_expand(aux, vh + 16, clen, heap + o, dbytes) != (int64_t)dbytes) return -1;
+        uint64_t sum = 0;
+        for (uint32_t i = 0; i < vn; ++i) {
+            sum += (for_base + u[i]) & 0xFFFFFFFFull;
+            offs[row + i + 1] = (uint32_t)(o + sum);
+        }
+        if (sum != dbytes) return -1;
+        o += dbytes;
+        row += vn;
+    }
+    return row == rg_rows ? (int64_t)o : -1;
 }
 
 /* ---- parallel column decode (CPU baseline) ------------------------------ */

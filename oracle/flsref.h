@@ -76,11 +76,18 @@ int64_t flsref_rowgroup_rows(const flsref_file *f, uint32_t rg);
 
 /* Decode column `col` of row group `rg`.
  * Integer columns: out receives nrows values of the column's value width
- *   (1/2/4/8 bytes, little-endian two's complement).
+ *   (1/2/4/8 bytes, little-endian two's complement); FLOAT/DOUBLE (ALP) their
+ *   IEEE bits.  FSST columns are decoded with flsref_decode_strings.
  * VARCHAR columns: out receives nrows pairs {uint64 byte offset into the
  *   image, uint64 length} naming each value's bytes inside the image.
  * Returns number of rows decoded, or -1 on a malformed chunk. */
 int64_t flsref_decode(const flsref_file *f, uint32_t col, uint32_t rg, void *out);
+
+/* Strings of VARCHAR column col, row group rg (DICT or FSST): offs receives
+ * nrows+1 offsets into heap (cap bytes), heap the concatenated bytes.
+ * Returns the byte count, or -1 on error / insufficient cap. */
+int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, uint32_t *offs,
+                              uint8_t *heap, uint64_t cap);
 
 /* Decode every row group of `col` into out (rows concatenated).  Threads:
  * nthreads > 1 decodes row groups in parallel (CPU baseline).  Returns rows. */

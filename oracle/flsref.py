@@ -41,6 +41,8 @@ _lib.flsref_decode.restype = C.c_int64
 _lib.flsref_decode.argtypes = [C.POINTER(_File), C.c_uint32, C.c_uint32, C.c_void_p]
 _lib.flsref_decode_column.restype = C.c_int64
 _lib.flsref_decode_column.argtypes = [C.POINTER(_File), C.c_uint32, C.c_void_p, C.c_int]
+_lib.flsref_decode_strings.restype = C.c_int64
+_lib.flsref_decode_strings.argtypes = [C.POINTER(_File), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64]
 _lib.flsref_out_width.restype = C.c_int
 _lib.flsref_out_width.argtypes = [C.POINTER(_File), C.c_uint32]
 
@@ -118,6 +120,28 @@ class RefFile:
         got = _lib.flsref_decode_column(C.byref(self.f), c, out.ctypes.data, nthreads)
         if got != self.nrows:
             raise ValueError(f"flsref_decode_column failed on col {c}")
+        return out
+
+    def strings_rg(self, c: int, rg: int) -> list[bytes]:
+        """Strings of VARCHAR column c, row group rg (DICT or FSST)."""
+        n = self.rowgroup_rows(rg)
+        offs = np.zeros(n + 1, dtype=np.uint32)
+        cap = 1 << 16
+        while True:
+            heap = np.empty(cap, dtype=np.uint8)
+            got = _lib.flsref_decode_strings(C.byref(self.f), c, rg, offs.ctypes.data, heap.ctypes.data, cap)
+            if got >= 0:
+                break
+            if cap > (1 << 34):
+                raise ValueError(f"flsref_decode_strings failed on col {c} rg {rg}")
+            cap *= 4
+        hb = heap[:got].tobytes()
+        return [hb[offs[i]:offs[i + 1]] for i in range(n)]
+
+    def strings_column(self, c: int) -> list[bytes]:
+        out = []
+        for rg in range(self.nrowgroups):
+            out += self.strings_rg(c, rg)
         return out
 
     def strings(self, raw: np.ndarray) -> list[bytes]:

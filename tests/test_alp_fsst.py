@@ -1,0 +1,214 @@
+"""ALP (FLOAT/DOUBLE) and FSST (VARCHAR) -- SURVEY.md 8(f) row 3, the FP and
+string decoders inside RowgroupReader::materialize() (reference
+src/fastlanes_facade.cpp:48, consumers flt_col_t / dbl_col_t / FLSStrColumn at
+:140-170).
+
+CPU tests: the writer's encodings round-trip bit-exactly through the oracle
+(oracle/flsref.c decodes ALP and FSST independently of the encoder), the
+format invariants hold (exceptions, escapes, heap layout), and corrupt chunks
+are rejected on open.  GPU tests: the HIP ALP path (decode kernel) and the FSST
+kernel produce the oracle's bytes / strings exactly, device-resident and
+through the scan pipeline."""
+import struct
+
+import numpy as np
+import pytest
+
+from helpers import fsst_text, special_doubles
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+@pytest.mark.parametrize("kind", ["price", "ratio", "mixed", "ints", "tiny", "float1", "float_rand"])
+def test_alp_roundtrip_bit_exact(fl, ref, kind):
+    rng = np.random.default_rng(hash(kind) % 2**32)
+    n = 70001
+    if kind == "price":
+        v = np.round(rng.uniform(900, 105000, n), 2)
+    elif kind == "ratio":
+        v = rng.random(n)                                  # mostly exceptions (no decimal form)
+    elif kind == "mixed":
+        v = np.round(rng.normal(0, 1e4, n), 3)
+        v[rng.integers(0, n, 500)] = special_doubles(500, rng)
+    elif kind == "ints":
+        v = rng.integers(-2**40, 2**40, n).astype(np.float64)
+    elif kind == "tiny":
+        v = np.round(rng.uniform(0, 1, n), 5) * 1e-6
+    elif kind == "float1":
+        v = np.round(rng.uniform(-100, 100, n), 1).astype(np.float32)
+    else:
+        v = rng.standard_normal(n).astype(np.float32)
+    ty = fl.FLOAT if v.dtype == np.float32 else fl.DOUBLE
+    img = fl.write_image([("v", ty, v, fl.ENC_ALP)])
+    rf = ref.RefFile(img)
+    got = rf.decode_column(0)
+    assert np.array_equal(got, bits(v))
+
+
+def test_alp_compresses_decimals(fl):
+    rng = np.random.default_rng(5)
+    v = np.round(rng.uniform(900, 105000, 65536), 2)      # l_extendedprice-like
+    img = fl.write_image([("p", fl.DOUBLE, v, fl.ENC_AUTO)])
+    assert len(img.tobytes()) < 0.45 * v.nbytes         # ~24 bits/value vs 64
+
+
+def _chunk_header(raw, col=0, rg=0):
+    """(offset, header fields) of a chunk via the footer."""
+    foot, flen = struct.unpack_from("<QI", raw, len(raw) - 16)
+    ncols = struct.unpack_from("<I", raw, foot + 4)[0]
+    p = foot + 32
+    for _ in range(ncols):
+        p += 6 + struct.unpack_from("<H", raw, p + 4)[0]
+    p += rg * (4 + 16 * ncols)
+    off = struct.unpack_from("<Q", raw, p + 4 + 16 * col)[0]
+    return off
+
+
+def test_alp_exception_layout(fl, ref):
+    v = np.full(1024, 12.25)
+    v[[3, 700]] = [np.nan, -0.0]
+    raw = fl.write_image([("v", fl.DOUBLE, v, fl.ENC_ALP)]).tobytes()
+    off = _chunk_header(raw)
+    enc, T = raw[off + 4], raw[off + 5]
+    meta = struct.unpack_from("<QqQHBBI", raw, off + 64)
+    aux_count = meta[6]
+    assert (enc, T) == (5, 64)
+    assert aux_count & 0xFFFF == 2 and meta[4] == 0      # two exceptions, constant ints -> W=0
+    e, f = (aux_count >> 16) & 0xFF, aux_count >> 24
+    assert f <= e and 12.25 * 10 ** (e - f) == round(12.25 * 10 ** (e - f))
+
+
+@pytest.mark.parametrize("n", [1, 1023, 1025, 65536, 70000])
+def test_fsst_roundtrip_and_escapes(fl, ref, n):
+    rng = np.random.default_rng(n)
+    s = fsst_text(n, rng)
+    # strings the symbol table cannot cover: raw bytes -> escapes (incl. 0xFF)
+    for i in range(0, n, 97):
+        s[i] = bytes(rng.integers(0, 256, rng.integers(0, 30), dtype=np.uint8).tolist())
+    if n > 3:
+        s[1] = b""
+        s[2] = b"\xff" * 20
+    img = fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)])
+    rf = ref.RefFile(img)
+    assert rf.strings_column(0) == [x if isinstance(x, bytes) else x.encode() for x in s]
+
+
+def test_fsst_compresses_text(fl):
+    rng = np.random.default_rng(9)
+    s = fsst_text(65536, rng)
+    img = fl.write_image([("c", fl.VARCHAR, s, fl.ENC_AUTO)])   # AUTO -> FSST (high cardinality)
+    raw = img.tobytes()
+    assert raw[_chunk_header(raw) + 4] == 7
+    assert len(raw) < 0.5 * sum(map(len, s))
+
+
+def test_varchar_auto_picks_dict_for_low_cardinality(fl):
+    s = ["AIR", "MAIL", "SHIP"] * 10000
+    raw = fl.write_image([("c", fl.VARCHAR, s, fl.ENC_AUTO)]).tobytes()
+    assert raw[_chunk_header(raw) + 4] == 3
+
+
+def test_corrupt_alp_and_fsst_rejected(fl, ref):
+    v = np.round(np.arange(5000) * 0.25, 2)
+    raw = bytearray(fl.write_image([("v", fl.DOUBLE, v, fl.ENC_ALP)]).tobytes())
+    off = _chunk_header(raw)
+    struct.pack_into("<I", raw, off + 64 + 28, (30 << 16) | 1)   # exponent 30 > 18
+    with pytest.raises(fl.FlsError, match="ALP exponent"):
+        fl.Connection().read_image(bytes(raw))
+    s = fsst_text(3000, np.random.default_rng(1))
+    raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
+    off = _chunk_header(raw)
+    aux = struct.unpack_from("<Q", raw, off + 32)[0]
+    raw[off + aux + 2048] = 9                                   # symbol length 9
+    with pytest.raises(fl.FlsError, match="FSST symbol length"):
+        fl.Connection().read_image(bytes(raw))
+
+
+# ---- GPU ---------------------------------------------------------------------
+from helpers import assert_column_equal, assert_strings_equal, gpu_decode_all  # noqa: E402
+
+
+def _mixed_table(fl, n, seed):
+    rng = np.random.default_rng(seed)
+    price = np.round(rng.uniform(900, 105000, n), 2)
+    mixed = np.round(rng.normal(0, 1e4, n), 3)
+    mixed[rng.integers(0, n, max(1, n // 100))] = special_doubles(max(1, n // 100), rng)
+    ratio = rng.random(n)
+    f32 = np.round(rng.uniform(-100, 100, n), 1).astype(np.float32)
+    fr = rng.standard_normal(n).astype(np.float32)
+    text = fsst_text(n, rng)
+    for i in range(0, n, 211):
+        text[i] = bytes(rng.integers(0, 256, rng.integers(0, 40), dtype=np.uint8).tolist())
+    cols = [("price", fl.DOUBLE, price, fl.ENC_ALP), ("mixed", fl.DOUBLE, mixed, fl.ENC_ALP),
+            ("ratio", fl.DOUBLE, ratio, fl.ENC_ALP), ("f32", fl.FLOAT, f32, fl.ENC_ALP),
+            ("frand", fl.FLOAT, fr, fl.ENC_ALP), ("comment", fl.VARCHAR, text, fl.ENC_FSST),
+            ("key", fl.INT64, np.arange(n) * 3, fl.ENC_DELTA)]
+    return fl.write_image(cols), cols
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 1000, 1024, 65536, 3 * 65536 + 4321])
+def test_gpu_alp_fsst_device_resident(fl, ref, gpu, n):
+    img, cols = _mixed_table(fl, n, n)
+    t, st, out = gpu_decode_all(fl, img)
+    rf = ref.RefFile(img)
+    for c, (name, ty, vals, _) in enumerate(cols):
+        assert_column_equal(fl, rf, c, out[c], img.ptr)
+        if ty in (fl.FLOAT, fl.DOUBLE):
+            assert np.array_equal(out[c], bits(vals)), name
+
+
+@pytest.mark.gpu
+def test_gpu_fsst_escape_heavy_and_long_strings(fl, ref, gpu):
+    rng = np.random.default_rng(3)
+    n = 20000
+    s = []
+    for i in range(n):
+        k = i % 5
+        if k == 0:
+            s.append(b"")
+        elif k == 1:
+            s.append(b"\xff" * int(rng.integers(1, 50)))                           # escapes only
+        elif k == 2:
+            s.append(bytes(rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8).tolist()))
+        elif k == 3:
+            s.append(("lorem ipsum dolor sit amet " * int(rng.integers(1, 200))).encode())  # up to 5 KB
+        else:
+            s.append(b"x" * 12)
+    img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
+    t, st, out = gpu_decode_all(fl, img)
+    rf = ref.RefFile(img)
+    assert_strings_equal(fl, rf, 0, out[0])
+
+
+@pytest.mark.gpu
+def test_gpu_alp_fsst_scan_pipeline(fl, ref, gpu, monkeypatch):
+    monkeypatch.setenv("FLS_SCAN_BATCH", "3")
+    n = 7 * 65536 + 999
+    img, cols = _mixed_table(fl, n, 77)
+    rf = ref.RefFile(img)
+    conn = fl.Connection([0, 0])
+    t = conn.read_image(img)
+    seen = 0
+    for first, got in t.scan(cols=[0, 4, 5]):
+        rg = first // 65536
+        assert np.array_equal(got[0], rf.decode(0, rg))
+        assert np.array_equal(got[4], rf.decode(4, rg))
+        assert fl.string_t_decode(got[5]) == rf.strings_rg(5, rg)
+        seen += 1
+    assert seen == rf.nrowgroups
+
+
+@pytest.mark.gpu
+def test_gpu_fsst_corrupt_lengths_reported(fl, ref, gpu):
+    s = fsst_text(5000, np.random.default_rng(4))
+    raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
+    off = _chunk_header(raw)
+    struct.pack_into("<I", raw, off + 64 + 28, struct.unpack_from("<I", raw, off + 64 + 28)[0] + 5)
+    t = fl.Connection().read_image(bytes(raw))
+    t.device_upload()
+    t.device_decode()
+    with pytest.raises(fl.FlsError, match="corrupt"):
+        t.device_sync()

@@ -183,3 +183,23 @@ def test_read_fastlanes_parallel_scan_keeps_order(fl, ext, gpu, tmpfile, monkeyp
     _, _, m1 = ext.query("read_fastlanes", p, q, p, as_list=True, proj=[0, 10])
     _, _, mn = ext.query("read_fastlanes", p, q, p, as_list=True, proj=[0, 10], threads=threads)
     assert len(mn) == 2 * 600572 + 60175 and mn == m1
+
+
+def test_read_fastlanes_glob_binds_sorted_files(fl, ext, tmp_path):
+    # src/scanner/scan_fastlanes.cpp:151-185 (multi-file), DuckDB glob semantics
+    with pytest.raises(ExtError, match='^No files found that match the pattern ".*nothing_\\*.fls"$'):
+        ext.query("read_fastlanes", str(tmp_path / "nothing_*.fls"), limit=0)
+    a = np.arange(3000, dtype=np.int32)
+    for i in (2, 0, 1):
+        fl.write_image([("v", fl.INT32, a + i * 10000, fl.ENC_FFOR)]).write(str(tmp_path / f"part_{i}.fls"))
+    names, types, rows = ext.query("read_fastlanes", str(tmp_path / "part_*.fls"), limit=0)
+    assert names == ["v"] and types == ["INTEGER"]
+
+
+@pytest.mark.gpu
+def test_read_fastlanes_glob_scans_in_name_order(fl, ext, gpu, tmp_path):
+    a = np.arange(3000, dtype=np.int32)
+    for i in (2, 0, 1):
+        fl.write_image([("v", fl.INT32, a + i * 10000, fl.ENC_FFOR)]).write(str(tmp_path / f"part_{i}.fls"))
+    _, _, rows = ext.query("read_fastlanes", str(tmp_path / "part_?.fls"), threads=4)
+    assert [int(r[0]) for r in rows] == np.concatenate([a, a + 10000, a + 20000]).tolist()
