@@ -111,6 +111,8 @@ _sig("fls_gen_image", C.c_int, C.c_char_p, C.c_double, C.c_uint64, C.c_uint32, C
      C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_gen_values", C.c_int, C.c_char_p, C.c_double, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, _P)
 _sig("fls_gen_dict_string", C.c_char_p, C.c_char_p, C.c_int, C.c_uint32)
+_sig("fls_gen_strings", C.c_int64, C.c_char_p, C.c_double, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, _P, _P,
+     C.c_uint64)
 
 lib = _lib
 
@@ -183,6 +185,19 @@ def gen_values(workload: str, col: int, row_begin: int, n: int, dtype, scale: fl
     out = np.empty(n, dtype=dtype)
     _check(_lib.fls_gen_values(workload.encode(), scale, nrows, col, row_begin, n, out.ctypes.data))
     return out
+
+
+def gen_strings(workload: str, col: int, row_begin: int, n: int, scale: float = 1.0, nrows: int = 0) -> list[bytes]:
+    """Ground-truth strings of a generated VARCHAR column (dictionary or l_comment)."""
+    offs = np.zeros(n + 1, dtype=np.uint32)
+    cap = max(64, 48 * n)
+    buf = np.empty(cap, dtype=np.uint8)
+    got = _lib.fls_gen_strings(workload.encode(), scale, nrows, col, row_begin, n, offs.ctypes.data, buf.ctypes.data,
+                               cap)
+    if got < 0:
+        _check(int(got))
+    b = buf[:got].tobytes()
+    return [b[offs[i]:offs[i + 1]] for i in range(n)]
 
 
 def gen_dict_string(workload: str, col: int, code: int) -> str | None:

@@ -24,6 +24,7 @@
 #include "fls_common.hpp"
 #include "fls_format.hpp"
 #include "fls_gen.hpp"
+#include "fls_text.hpp"
 
 namespace fls {
 
@@ -820,6 +821,9 @@ struct Workload {
     std::vector<ColSpec> cols;
     uint64_t nrows;
     gen::LineitemParams li;
+    bool lineitem = false;   // lineitem, lineitem_full, lineitem_dbl
+    bool dbl = false;        // quantity / extendedprice / discount / tax as DOUBLE (ALP)
+    int comment_col = -1;    // l_comment (FSST) column
 };
 
 uint64_t lineitem_rows(double sf) {
@@ -846,8 +850,9 @@ bool make_workload(const char *wl, double sf, uint64_t nrows, Workload &w) {
     } else if (w.name == "c4") {
         w.cols = {{"mode", TY_VARCHAR, 0, 0, ENC_DICT}};
         w.nrows = nrows ? nrows : 1000000000ull;
-    } else if (w.name == "lineitem") {
+    } else if (w.name == "lineitem" || w.name == "lineitem_full" || w.name == "lineitem_dbl") {
         if (!(sf > 0)) return false;
+        w.lineitem = true;
         w.cols = {
             {"l_orderkey", TY_INT64, 0, 0, ENC_DELTA},   {"l_partkey", TY_INT32, 0, 0, ENC_FFOR},
             {"l_suppkey", TY_INT32, 0, 0, ENC_FFOR},     {"l_linenumber", TY_INT32, 0, 0, ENC_FFOR},
@@ -858,6 +863,15 @@ bool make_workload(const char *wl, double sf, uint64_t nrows, Workload &w) {
             {"l_receiptdate", TY_DATE, 0, 0, ENC_FFOR},  {"l_shipinstruct", TY_VARCHAR, 0, 0, ENC_DICT},
             {"l_shipmode", TY_VARCHAR, 0, 0, ENC_DICT},
         };
+        if (w.name == "lineitem_dbl") {
+            // the four DECIMAL(15,2) columns as DOUBLE (cents / 100.0), ALP-encoded
+            w.dbl = true;
+            for (int c = 4; c < 8; ++c) w.cols[c] = {w.cols[c].name, TY_DOUBLE, 0, 0, ENC_ALP};
+        }
+        if (w.name == "lineitem_full") {  // all 16 TPC-H columns: l_comment FSST
+            w.comment_col = 15;
+            w.cols.push_back({"l_comment", TY_VARCHAR, 0, 0, ENC_FSST});
+        }
         w.nrows = nrows ? nrows : lineitem_rows(sf);
         w.li.n_part = std::max<int64_t>(1, (int64_t)(200000.0 * sf + 0.5));
         w.li.n_supp = std::max<int64_t>(4, (int64_t)(10000.0 * sf + 0.5));
@@ -873,7 +887,7 @@ bool make_workload(const char *wl, double sf, uint64_t nrows, Workload &w) {
 bool gen_dict(const Workload &w, int col, std::vector<std::string_view> &d) {
     auto fill = [&d](const char *const *t, size_t n) { d.assign(t, t + n); };
     if (w.name == "c4" && col == 0) { fill(kShipMode, 7); return true; }
-    if (w.name == "lineitem") {
+    if (w.lineitem) {
         switch (col) {
         case 8: fill(kReturnFlag, 3); return true;
         case 9: fill(kLineStatus, 2); return true;
@@ -904,13 +918,36 @@ void gen_rows(const Workload &w, uint64_t row0, uint32_t n, std::vector<std::vec
         for (uint32_t i = 0; i < n; ++i, ow.next()) {
             gen::lineitem_row_at(w.li, row0 + i, ow.cur(), r);
             for (int c = 0; c < gen::kLineitemCols; ++c) out[c][i] = (uint64_t)gen::lineitem_col(r, c);
+            if (w.dbl)
+                for (int c = 4; c < 8; ++c) {
+                    const double x = (double)(int64_t)out[c][i] / 100.0;
+                    memcpy(&out[c][i], &x, 8);
+                }
+            if (w.comment_col >= 0) out[w.comment_col][i] = row0 + i;  // strings come from gen::comment
         }
+    }
+}
+
+// l_comment strings of rows [row0, row0+n) as offsets + bytes
+void gen_comments(const Workload &w, uint64_t row0, uint32_t n, std::vector<uint32_t> &offs, std::string &bytes) {
+    offs.assign(n + 1, 0);
+    bytes.clear();
+    for (uint32_t i = 0; i < n; ++i) {
+        const std::string_view c = gen::comment(w.li.seed, row0 + i);
+        bytes.append(c.data(), c.size());
+        offs[i + 1] = (uint32_t)bytes.size();
     }
 }
 
 std::vector<uint8_t> encode_gen_chunk(const Workload &w, int c, const std::vector<uint64_t> &vals) {
     const ColSpec &cs = w.cols[c];
     const uint32_t n = (uint32_t)vals.size();
+    if (c == w.comment_col) {
+        std::vector<uint32_t> offs;
+        std::string bytes;
+        gen_comments(w, vals[0], n, offs, bytes);
+        return enc_fsst(offs.data(), bytes.data(), n);
+    }
     if (cs.type == TY_VARCHAR) {
         std::vector<std::string_view> d;
         gen_dict(w, c, d);
@@ -1079,6 +1116,7 @@ int fls_gen_values(const char *workload, double scale, uint64_t nrows, int col, 
     Workload w;
     if (!make_workload(workload, scale, nrows, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
     if (col < 0 || col >= (int)w.cols.size() || !out) return fail(FLS_ERR_ARG, "bad column %d", col);
+    if (col == w.comment_col) return fail(FLS_ERR_ARG, "column %d holds strings: use fls_gen_strings", col);
     if (row_begin + n > w.nrows) return fail(FLS_ERR_ARG, "rows out of range");
     const int vb = w.cols[col].type == TY_VARCHAR ? 4 : type_value_bits(w.cols[col].type) / 8;
     std::vector<std::vector<uint64_t>> vals;
@@ -1090,6 +1128,33 @@ int fls_gen_values(const char *workload, double scale, uint64_t nrows, int col, 
         r += k;
     }
     return 0;
+}
+
+int64_t fls_gen_strings(const char *workload, double scale, uint64_t nrows, int col, uint64_t row_begin, uint64_t n,
+                        uint32_t *offs, char *bytes, uint64_t cap) {
+    Workload w;
+    if (!make_workload(workload, scale, nrows, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
+    if (col < 0 || col >= (int)w.cols.size() || w.cols[col].type != TY_VARCHAR || !offs)
+        return fail(FLS_ERR_ARG, "column %d is not a VARCHAR column", col);
+    if (row_begin + n > w.nrows) return fail(FLS_ERR_ARG, "rows out of range");
+    uint64_t o = 0;
+    offs[0] = 0;
+    std::vector<std::vector<uint64_t>> vals;
+    std::vector<std::string_view> dict;
+    const bool is_dict = col != w.comment_col && gen_dict(w, col, dict);
+    for (uint64_t r = 0; r < n;) {
+        const uint32_t k = (uint32_t)std::min<uint64_t>(65536, n - r);
+        if (is_dict) gen_rows(w, row_begin + r, k, vals);
+        for (uint32_t i = 0; i < k; ++i) {
+            const std::string_view sv = is_dict ? dict[vals[col][i]] : gen::comment(w.li.seed, row_begin + r + i);
+            if (o + sv.size() > cap || o + sv.size() > UINT32_MAX) return fail(FLS_ERR_ARG, "string buffer too small");
+            if (bytes) memcpy(bytes + o, sv.data(), sv.size());
+            o += sv.size();
+            offs[r + i + 1] = (uint32_t)o;
+        }
+        r += k;
+    }
+    return (int64_t)o;
 }
 
 const char *fls_gen_dict_string(const char *workload, int col, uint32_t code) {

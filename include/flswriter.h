@@ -61,7 +61,9 @@ int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len);
 void fls_image_free(uint8_t *img);
 
 /* ---- seeded synthetic workloads (fls_gen.hpp) -------------------------
- * workload: "c1", "lineitem", "c3", "c4".  scale: lineitem scale factor
+ * workload: "c1", "lineitem", "c3", "c4"; "lineitem_full" (16 columns,
+ * l_comment FSST), "lineitem_dbl" (the DECIMAL columns as DOUBLE, ALP).
+ * scale: lineitem scale factor
  * (ignored otherwise).  nrows: 0 = workload default (c1 1e6, c3/c4 1e9,
  * lineitem dbgen row count for the scale).  Row groups [rg_begin, rg_end) of
  * the full table are encoded into one image (a shard) using nthreads. */
@@ -73,6 +75,11 @@ int fls_gen_image(const char *workload, double scale, uint64_t nrows, uint32_t r
  * in their value width, VARCHAR columns as uint32 dictionary codes. */
 int fls_gen_values(const char *workload, double scale, uint64_t nrows, int col,
                    uint64_t row_begin, uint64_t n, void *out);
+/* Strings of VARCHAR column col (dictionary or l_comment text) for rows
+ * [row_begin, row_begin+n): offs receives n+1 offsets into bytes (cap bytes).
+ * Returns the byte count. */
+int64_t fls_gen_strings(const char *workload, double scale, uint64_t nrows, int col, uint64_t row_begin, uint64_t n,
+                        uint32_t *offs, char *bytes, uint64_t cap);
 /* Dictionary string `code` of VARCHAR column col (NULL if none). */
 const char *fls_gen_dict_string(const char *workload, int col, uint32_t code);
 
