@@ -14,7 +14,7 @@
 //      next byte is a literal) makes a code's meaning depend on its
 //      predecessor; a lane therefore evaluates its bytes for both entry
 //      states and a wave scan composes those 2-state maps (only in rounds that
-//      contain an escape byte at all);
+//      contain an escape byte or start right after one);
 //   3. every string whose first min(len, 12) bytes are decoded gets its 16 B
 //      string_t (inline bytes, or 4-byte prefix + pointer into the heap's host
 //      copy), stored 64 records = 1 KiB at a time;
@@ -208,7 +208,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         bool has_esc = false;
         for (uint32_t k = 0; k < nb; ++k) has_esc |= byte_of(raw, k) == kFsstEscape;
         uint32_t start = 0, lane_out = 0, lane_end = 0;
-        if (__ballot(has_esc) == 0) {
+        if (__ballot(has_esc) == 0 && carry_lit == 0) {  // no escape anywhere: every code is a symbol
             for (uint32_t k = 0; k < nb; ++k) lane_out += min((uint32_t)w.len[byte_of(raw, k)], 8u);
         } else {
             uint32_t o0 = 0, o1 = 0;

@@ -343,6 +343,9 @@ struct FsstTable {
 };
 
 FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
+    // FLS_FSST_MAX_SYMBOLS (tests): a smaller table forces escapes
+    const char *ms = getenv("FLS_FSST_MAX_SYMBOLS");
+    const int max_symbols = ms ? std::max(0, std::min(255, atoi(ms))) : 255;
     // sample: whole strings at evenly spaced rows, about 16 KiB
     std::vector<std::pair<uint32_t, uint32_t>> smp;  // (offset, length)
     const uint64_t total = offs[n] - offs[0];
@@ -412,7 +415,7 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
         });
         st = FsstTable();
         for (auto &c : cand) {
-            if (st.n == 255) break;
+            if (st.n == max_symbols) break;
             st.sym[st.n] = c.first.sym;
             st.len[st.n] = (uint8_t)c.first.len;
             st.n++;

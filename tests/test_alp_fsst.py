@@ -110,6 +110,26 @@ def test_varchar_auto_picks_dict_for_low_cardinality(fl):
     assert raw[_chunk_header(raw) + 4] == 3
 
 
+@pytest.mark.parametrize("wl", ["lineitem_full", "lineitem_dbl"])
+def test_full_fidelity_workloads_match_generator(fl, ref, wl):
+    """lineitem with l_comment (FSST, TPC-H grammar text) and with the DECIMAL
+    columns as DOUBLE (ALP): the oracle decodes the generator's values."""
+    img = fl.gen_image(wl, 0.01)
+    rf = ref.RefFile(img)
+    n = rf.nrows
+    assert n == 60175
+    for c in range(rf.ncols):
+        name, ty, _, _ = rf.column(c)
+        if ty == fl.VARCHAR:
+            assert rf.strings_column(c) == fl.gen_strings(wl, c, 0, n, 0.01), name
+        else:
+            dt = fl.NP_DTYPE[ty]
+            assert np.array_equal(rf.decode_column(c).view(dt), fl.gen_values(wl, c, 0, n, dt, 0.01)), name
+    if wl == "lineitem_full":
+        lens = [len(x) for x in fl.gen_strings(wl, 15, 0, 5000, 0.01)]
+        assert min(lens) == 10 and max(lens) == 43
+
+
 def test_corrupt_alp_and_fsst_rejected(fl, ref):
     v = np.round(np.arange(5000) * 0.25, 2)
     raw = bytearray(fl.write_image([("v", fl.DOUBLE, v, fl.ENC_ALP)]).tobytes())
@@ -202,6 +222,18 @@ def test_gpu_alp_fsst_scan_pipeline(fl, ref, gpu, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wl", ["lineitem_full", "lineitem_dbl"])
+def test_gpu_full_fidelity_lineitem(fl, ref, gpu, wl):
+    img = fl.gen_image(wl, 0.1)
+    t, st, out = gpu_decode_all(fl, img)
+    rf = ref.RefFile(img)
+    for c in range(t.ncols):
+        assert_column_equal(fl, rf, c, out[c], img.ptr)
+    if wl == "lineitem_full":
+        assert fl.string_t_decode(out[15][:16 * 3000]) == fl.gen_strings(wl, 15, 0, 3000, 0.1)
+
+
+@pytest.mark.gpu
 def test_gpu_fsst_corrupt_lengths_reported(fl, ref, gpu):
     s = fsst_text(5000, np.random.default_rng(4))
     raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
@@ -212,3 +244,30 @@ def test_gpu_fsst_corrupt_lengths_reported(fl, ref, gpu):
     t.device_decode()
     with pytest.raises(fl.FlsError, match="corrupt"):
         t.device_sync()
+
+
+def _boundary_strings():
+    """With the table limited to {'a'*8}: string 0 is 1023 codes, string 1 the
+    escape pair (255, 'Z') at compressed bytes 1023/1024 -- the escape is the
+    last byte of decode round 0 and its literal the first of round 1, which has
+    no other escape; then ordinary strings and more escapes across vectors."""
+    s = [b"a" * (8 * 1023), b"Z"] + [b"a" * 8] * 300 + [b"aZa" * 5, b""] * 50
+    s += [b"a" * (8 * 1022) + b"Z", b"QQ", b"a" * 16]      # escape pair straddling a string boundary
+    return s
+
+
+def test_fsst_escape_at_round_boundary_roundtrip(fl, ref, monkeypatch):
+    monkeypatch.setenv("FLS_FSST_MAX_SYMBOLS", "1")
+    s = _boundary_strings()
+    img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
+    assert ref.RefFile(img).strings_column(0) == s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxsym", ["1", "8", "255"])
+def test_gpu_fsst_escape_at_round_boundary(fl, ref, gpu, monkeypatch, maxsym):
+    monkeypatch.setenv("FLS_FSST_MAX_SYMBOLS", maxsym)
+    s = _boundary_strings() * 3
+    img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
+    t, st, out = gpu_decode_all(fl, img)
+    assert fl.string_t_decode(out[0]) == s
