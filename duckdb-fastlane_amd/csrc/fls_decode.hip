@@ -31,8 +31,8 @@
 //     and scan the 1024/T chains there; DICT codes go through LDS and gather
 //     from the dictionary (staged in LDS when small) with 16 B/lane stores;
 //   * ALP (FLOAT/DOUBLE): the FFOR stream's integers are converted and scaled
-//     in registers ((F)d * 10^f * 10^-e) and stored like FFOR; vectors with
-//     exceptions go through LDS, where the exception values are patched in.
+//     in registers ((F)d * 10^f * 10^-e) and stored like FFOR; exception
+//     values are then stored over their positions by the same wave.
 // FSST strings have their own kernel (fls_fsst.hip).
 // The path is HBM-bound integer work: no MFMA.
 #include <hip/hip_runtime.h>
@@ -544,42 +544,36 @@ struct PathAlp {
         const uint32_t exc = x.acount & 0xFFFF;
         const uint32_t e = min((x.acount >> 16) & 0xFF, kMaxE), f = min(x.acount >> 24, e);
         const AlpScale<T> sc(e, f);
-        if (exc == 0) {  // common case: registers straight to HBM, like FFOR
-            const uint32_t limit = x.nvals * (T / 8);
-#pragma unroll
-            for (uint32_t j = 0; j < T / 8; ++j) {
-                const uint32_t ci = lane + 64 * j;
-                const v4u v = sc.apply(add_base<T>(unpack_chunk<T>(s.P, x.W, ci), x.base));
-                if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, v);
-                else store16<T / 8>(out, 16 * ci, limit, v);
-                seq();
-            }
-            return;
-        }
-        // exceptions: decode into LDS, patch, copy out
+        // registers straight to HBM, like FFOR
+        const uint32_t limit = x.nvals * (T / 8);
 #pragma unroll
         for (uint32_t j = 0; j < T / 8; ++j) {
             const uint32_t ci = lane + 64 * j;
-            *reinterpret_cast<lv4 *>(s.V + 16 * ci) = sc.apply(add_base<T>(unpack_chunk<T>(s.P, x.W, ci), x.base));
+            const v4u v = sc.apply(add_base<T>(unpack_chunk<T>(s.P, x.W, ci), x.base));
+            if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, v);
+            else store16<T / 8>(out, 16 * ci, limit, v);
             seq();
         }
-        wave_sync();
+        if (exc == 0) return;
+        // exceptions overwrite their positions (ascending, so lanes write
+        // consecutive slots).  Same-wave stores to one address already land in
+        // issue order; vmcnt(0) makes that explicit at the cost of one wait in
+        // the (rare) vectors that have exceptions.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt/lgkmcnt untouched
         gu8 *ea = aux_base + x.aoff;
         const FLS_GLOBAL uint16_t *pos = reinterpret_cast<const FLS_GLOBAL uint16_t *>(ea);
         gu8 *val = ea + ((2 * exc + 15) & ~15u);
         bool bad = false;
         for (uint32_t k = lane; k < exc; k += 64) {
             const uint32_t p = pos[k];
-            if (p >= kVectorSize) { bad = true; continue; }
+            if (p >= x.nvals) { bad = true; continue; }
             if (T == 64) {
-                *reinterpret_cast<FLS_LDS uint64_t *>(s.V + 8 * p) = reinterpret_cast<const FLS_GLOBAL uint64_t *>(val)[k];
+                reinterpret_cast<FLS_GLOBAL uint64_t *>(out)[p] = reinterpret_cast<const FLS_GLOBAL uint64_t *>(val)[k];
             } else {
-                *reinterpret_cast<FLS_LDS uint32_t *>(s.V + 4 * p) = reinterpret_cast<const FLS_GLOBAL uint32_t *>(val)[k];
+                reinterpret_cast<FLS_GLOBAL uint32_t *>(out)[p] = reinterpret_cast<const FLS_GLOBAL uint32_t *>(val)[k];
             }
         }
         if (bad) atomicOr(err, KERR_BAD_DESC);
-        wave_sync();
-        copy_out<T / 8, FULL>(s.V, out, x.nvals, lane);
     }
 };
 

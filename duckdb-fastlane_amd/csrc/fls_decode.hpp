@@ -24,7 +24,7 @@ struct DevChunk {              // 64 B
     uint64_t heap_host;        // FSST: address string_t pointers use for heap byte 0
                                // (the pinned host copy the heap lands in)
     uint32_t heap_bytes;       // FSST: heap bytes of the chunk (ChunkHeader.reserved1)
-    uint32_t pad;
+    uint32_t vec_base;         // FSST: vectors of the FSST chunks before this one in the launch
 };
 static_assert(sizeof(DevChunk) == 64, "DevChunk is 64 B");
 
@@ -42,8 +42,10 @@ struct DecodeGeom {
 // Launch the fused decode over every vector of nchunks chunks (no FSST).
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream);
-// Launch the FSST string decode over nchunks FSST chunks (fls_fsst.hip).
-hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, hipStream_t stream);
+// Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
+// (DevChunk.vec_base numbers them) (fls_fsst.hip).
+hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                       hipStream_t stream);
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
 // LDS bytes per wave the v2 kernel needs for one chunk (given its max width)
@@ -53,7 +55,6 @@ inline void chunk_lds_need(uint8_t enc, uint8_t T, uint8_t ob, uint32_t dict_cou
     v_bytes = 0;
     if (enc == 2 /*DELTA*/ && T < 64) v_bytes = 128 * T;
     if (enc == 4 /*RLE*/) v_bytes = 2048;
-    if (enc == 5 /*ALP*/) v_bytes = 128 * T;
     if (enc == 3 /*DICT*/) {
         const uint32_t d = dict_count * ob;
         v_bytes = 4096 + (d <= 4096 ? ((d + 15) & ~15u) : 0);

@@ -4,7 +4,9 @@
 // (reference src/fastlanes_facade.cpp:48, the FLSStrColumn consumer at
 // :163-170) for VARCHAR chunks written with ENC_FSST (fls_format.hpp).
 //
-// One 64-lane wave owns a column chunk and walks its vectors.  Per vector:
+// Waves take contiguous ranges of the launch's vectors (so a wave reloads the
+// chunk's symbol table only when its range crosses into the next chunk).
+// Per vector:
 //   1. the FFOR-packed string lengths are unpacked into LDS and scanned into
 //      exclusive offsets (doff[0..1024]) inside the vector's decompressed bytes;
 //   2. the compressed code stream is decoded CODE-PARALLEL in rounds of 1024
@@ -279,22 +281,30 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     if (bad) atomicOr(err, KERR_FSST);
 }
 
-__device__ __attribute__((noinline)) void fsst_chunk(const DevChunk *cg, uint8_t *lds_generic, uint32_t *err_generic) {
-    const uint64_t cp = (uint64_t)cg;
-    const FLS_GLOBAL DevChunk *cptr =
-        (const FLS_GLOBAL DevChunk *)((uint64_t)uni((uint32_t)(cp >> 32)) << 32 | uni((uint32_t)cp));
+__device__ __forceinline__ DevChunk load_chunk(const DevChunk *chunks, uint32_t ci) {
+    const FLS_GLOBAL v4u *q = reinterpret_cast<const FLS_GLOBAL v4u *>(gptr(chunks + ci));
     DevChunk c;
-    {
-        const FLS_GLOBAL v4u *q = reinterpret_cast<const FLS_GLOBAL v4u *>(cptr);
-        v4u *d = reinterpret_cast<v4u *>(&c);
-        d[0] = q[0];
-        d[1] = q[1];
-        d[2] = q[2];
-        d[3] = q[3];
-    }
+    v4u *d = reinterpret_cast<v4u *>(&c);
+    d[0] = q[0];
+    d[1] = q[1];
+    d[2] = q[2];
+    d[3] = q[3];
+    return c;
+}
+
+// Vectors [item0, item1) of the launch (items numbered chunk by chunk through
+// DevChunk.vec_base): the wave loads a chunk's symbol table once and decodes
+// its vectors in order.
+__device__ __attribute__((noinline)) void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t item0,
+                                                     uint32_t item1, uint8_t *lds_generic, uint32_t *err_generic) {
+    const uint64_t cp = (uint64_t)chunks_generic;
+    const DevChunk *chunks = (const DevChunk *)((uint64_t)uni((uint32_t)(cp >> 32)) << 32 | uni((uint32_t)cp));
     const uint64_t ep = (uint64_t)err_generic;
     uint32_t *err = (uint32_t *)((uint64_t)uni((uint32_t)(ep >> 32)) << 32 | uni((uint32_t)ep));
     lu8 *L = (lu8 *)(size_t)uni((uint32_t)(size_t)lds_generic);
+    nchunks = uni(nchunks);
+    item0 = uni(item0);
+    item1 = uni(item1);
     const uint32_t lane = __lane_id();
     Wave w;
     w.P = reinterpret_cast<lv4 *>(L + kOffP);
@@ -302,41 +312,65 @@ __device__ __attribute__((noinline)) void fsst_chunk(const DevChunk *cg, uint8_t
     w.sym = reinterpret_cast<const FLS_LDS uint64_t *>(L + kOffSym);
     w.len = L + kOffLen;
     w.ring = L + kOffRing;
-    gu8 *chunk = gptr(c.chunk);
-    gu8 *aux = chunk + c.aux_off;
-    // symbol table (u64[256] then u8[256]: 144 x 16 B, contiguous in both places)
-    for (uint32_t i = lane; i < kFsstTableBytes / 16; i += 64)
-        reinterpret_cast<lv4 *>(L + kOffSym)[i] = reinterpret_cast<gv4 *>(aux)[i];
-    wave_sync();
-    FLS_GLOBAL uint8_t *heap = (FLS_GLOBAL uint8_t *)(size_t)c.dict;
-    FLS_GLOBAL uint8_t *out = gptr(c.out);
-    const FLS_GLOBAL VecMeta *meta = reinterpret_cast<const FLS_GLOBAL VecMeta *>(chunk + c.meta_off);
-    for (uint32_t v = 0; v < c.nvec; ++v) {
-        const uint32_t poff = uni((uint32_t)meta[v].packed_off);
-        const uint32_t base = uni((uint32_t)meta[v].for_base);
-        const uint32_t aoff = uni((uint32_t)meta[v].aux_off);
-        const uint32_t nvals = uni(meta[v].nvals);
-        const uint32_t W = uni(min((uint32_t)meta[v].bw, 32u));
-        const uint32_t dbytes = uni(meta[v].aux_count);
-        fsst_vector(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff, heap, c.heap_bytes,
-                    c.heap_host, out + 16ull * kVectorSize * v, lane, err);
+    // chunk holding item0: last ci with vec_base <= item0
+    uint32_t lo = 0, hi = nchunks;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (uni(gptr(chunks + mid)->vec_base) <= item0) lo = mid;
+        else hi = mid;
+    }
+    uint32_t ci = lo;
+    DevChunk c = load_chunk(chunks, ci);
+    bool have_table = false;
+    for (uint32_t item = item0; item < item1;) {
+        const uint32_t v = item - uni(c.vec_base);
+        if (v >= uni(c.nvec)) {  // next chunk
+            if (++ci >= nchunks) break;
+            c = load_chunk(chunks, ci);
+            have_table = false;
+            continue;
+        }
+        gu8 *chunk = gptr(c.chunk);
+        gu8 *aux = chunk + c.aux_off;
+        if (!have_table) {
+            // symbol table (u64[256] then u8[256]: 144 x 16 B, contiguous in both places)
+            wave_sync();
+            for (uint32_t i = lane; i < kFsstTableBytes / 16; i += 64)
+                reinterpret_cast<lv4 *>(L + kOffSym)[i] = reinterpret_cast<gv4 *>(aux)[i];
+            wave_sync();
+            have_table = true;
+        }
+        const FLS_GLOBAL VecMeta *meta = reinterpret_cast<const FLS_GLOBAL VecMeta *>(chunk + c.meta_off) + v;
+        const uint32_t poff = uni((uint32_t)meta->packed_off);
+        const uint32_t base = uni((uint32_t)meta->for_base);
+        const uint32_t aoff = uni((uint32_t)meta->aux_off);
+        const uint32_t nvals = uni(meta->nvals);
+        const uint32_t W = uni(min((uint32_t)meta->bw, 32u));
+        const uint32_t dbytes = uni(meta->aux_count);
+        fsst_vector(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
+                    (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
+                    gptr(c.out) + 16ull * kVectorSize * v, lane, err);
         wave_sync();
+        ++item;
     }
 }
 
 __global__ __launch_bounds__(256, 2) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                      uint32_t *__restrict__ err) {
+                                                      uint32_t nitems, uint32_t *__restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     const uint32_t w = uni(threadIdx.x >> 6);
-    uint8_t *mine = lds_raw + w * kWaveLds;
-    const uint32_t stride = gridDim.x * kWaves;
-    for (uint32_t ci = blockIdx.x * kWaves + w; ci < nchunks; ci += stride) fsst_chunk(chunks + ci, mine, err);
+    const uint32_t nwaves = gridDim.x * kWaves, wave = blockIdx.x * kWaves + w;
+    // contiguous vector ranges per wave: a wave mostly stays inside one chunk
+    const uint32_t per = (nitems + nwaves - 1) / nwaves;
+    const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
+    if (i0 < i1) fsst_range(chunks, nchunks, i0, i1, lds_raw + w * kWaveLds, err);
 }
 
 }  // namespace
 
-hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, hipStream_t stream) {
-    if (nchunks == 0) return hipSuccess;
+hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                       hipStream_t stream) {
+    if (nchunks == 0 || nvecs == 0) return hipSuccess;
     const uint32_t shmem = kWaves * kWaveLds;
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
@@ -344,8 +378,8 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_e
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel, 64 * kWaves, shmem) != hipSuccess)
             per_cu = 1;
     }
-    const int grid = std::min<int>(cus * std::max(1, per_cu), (int)((nchunks + kWaves - 1) / kWaves));
-    hipLaunchKernelGGL(fsst_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err);
+    const int grid = std::min<int>(cus * std::max(1, per_cu), (int)((nvecs + kWaves - 1) / kWaves));
+    hipLaunchKernelGGL(fsst_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, nvecs, d_err);
     return hipGetLastError();
 }
 

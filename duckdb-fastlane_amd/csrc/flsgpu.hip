@@ -211,6 +211,7 @@ struct fls_table {
     std::vector<DevChunk> h_chunks;
     std::vector<uint8_t> dev_mask;     // column mask h_chunks was built for
     uint32_t dev_nmain = 0;            // h_chunks[0, dev_nmain) main kernel, the rest FSST
+    uint32_t dev_fsst_vecs = 0;        // vectors of the FSST chunks
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
@@ -320,16 +321,23 @@ bool col_selected(const std::vector<uint8_t> &mask, uint32_t c) { return mask.em
 
 bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[rg].chunks[c].hdr.enc == ENC_FSST; }
 
-// FSST chunks go last (their own kernel); returns how many lead (main kernel)
-uint32_t order_for_launch(std::vector<DevChunk> &v) {
+// FSST chunks go last (their own kernel) and get their vector numbering;
+// returns how many lead (main kernel) and the FSST vector count
+uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
+    uint32_t nv = 0;
+    for (auto it = mid; it != v.end(); ++it) {
+        it->vec_base = nv;
+        nv += it->nvec;
+    }
+    *fsst_vecs = nv;
     return (uint32_t)(mid - v.begin());
 }
 
-hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t *d_err, const DecodeGeom &geom,
-                      hipStream_t stream) {
+hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t fsst_vecs, uint32_t *d_err,
+                      const DecodeGeom &geom, hipStream_t stream) {
     hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream);
-    if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, ntotal - nmain, d_err, stream);
+    if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, ntotal - nmain, fsst_vecs, d_err, stream);
     return e;
 }
 
@@ -474,13 +482,14 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                                          sl.heap_bytes[c] ? sl.h_heap[c].p + ho : nullptr));
         }
     }
-    const uint32_t nmain = order_for_launch(list);
+    uint32_t fsst_vecs = 0;
+    const uint32_t nmain = order_for_launch(list, &fsst_vecs);
     const size_t k = list.size();
     HIP_TRY(sl.h_chunks.alloc(k));
     HIP_TRY(sl.d_chunks.alloc(d.dev, k));
     if (k) memcpy(sl.h_chunks.p, list.data(), k * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
-    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, d.err.p, bc.geom, sl.stream));
+    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream));
     // 3. D2H into pinned host columns (and string heaps)
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
@@ -809,7 +818,7 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
                                                sh.h_heap[c].p ? sh.h_heap[c].p + ho : nullptr));
             }
         }
-        t->dev_nmain = order_for_launch(chunks);
+        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst_vecs);
         HIP_TRY(hipStreamSynchronize(t->stream));
         HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
         HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
@@ -828,8 +837,8 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), sh.err.p, t->last_bytes.geom,
-                       t->stream));
+    HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst_vecs, sh.err.p,
+                       t->last_bytes.geom, t->stream));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;
     t->launched = true;
