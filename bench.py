@@ -191,7 +191,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     traffic, traffic_note = None, "not measured (multi-rank run or --no-traffic)"
-    if world == 1 and not args.no_traffic and not args.pmc_child:
+    under_profiler = "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+    if under_profiler:
+        traffic_note = "not measured (already running under rocprofv3)"
+    if world == 1 and not args.no_traffic and not args.pmc_child and not under_profiler:
         traffic, traffic_note = measure_traffic(args)
         log(f"[traffic] {traffic_note}")
 
