@@ -53,7 +53,19 @@ class ColumnInfo(C.Structure):
 
 class RowGroup(C.Structure):
     _fields_ = [("rowgroup", C.c_uint32), ("nrows", C.c_uint32), ("first_row", C.c_uint64),
-                ("ncols", C.c_uint32), ("columns", C.POINTER(C.c_void_p))]
+                ("ncols", C.c_uint32), ("columns", C.POINTER(C.c_void_p)),
+                ("nrows_scanned", C.c_uint32), ("sel", C.POINTER(C.c_uint32))]
+
+
+class Predicate(C.Structure):
+    _fields_ = [("col", C.c_uint32), ("clause", C.c_uint32), ("op", C.c_uint8), ("pad", C.c_uint8 * 7),
+                ("value", C.c_uint64), ("str", C.c_char_p), ("str_len", C.c_uint64)]
+
+
+# fls_cmp (include/flsgpu.h)
+EQ, NE, LT, LE, GT, GE, IS_NULL, IS_NOT_NULL = range(8)
+OPS = {"=": EQ, "==": EQ, "!=": NE, "<>": NE, "<": LT, "<=": LE, ">": GT, ">=": GE,
+       "is_null": IS_NULL, "is_not_null": IS_NOT_NULL}
 
 
 class DecodeStats(C.Structure):
@@ -91,6 +103,11 @@ _sig("fls_table_column", C.c_int, _P, C.c_uint32, C.POINTER(ColumnInfo))
 _sig("fls_materialize", C.c_int, _P, C.c_uint32, C.POINTER(C.c_uint8), C.POINTER(RowGroup))
 _sig("fls_scan_begin", C.c_int, _P, C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32)
 _sig("fls_scan_next", C.c_int, _P, C.POINTER(RowGroup))
+_sig("fls_scan_filter", C.c_int, _P, C.POINTER(Predicate), C.c_uint32)
+_sig("fls_scan_pruned", C.c_int, _P)
+_sig("fls_table_zonemap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+     C.POINTER(C.c_uint32))
+_sig("fls_rowgroup_may_match", C.c_int, _P, C.c_uint32, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_device_upload", C.c_int, _P, C.c_uint32, C.c_uint32)
 _sig("fls_device_decode", C.c_int, _P, C.POINTER(C.c_uint8))
 _sig("fls_device_sync", C.c_int, _P, C.POINTER(DecodeStats))
@@ -358,6 +375,9 @@ class Table:
                 cols.append(None)
                 continue
             ob = sch[c][4]
+            if rg.nrows == 0:
+                cols.append(np.zeros(0, dtype=np.uint8))
+                continue
             a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(rg.nrows * ob,))
             cols.append(a.copy() if copy else a)
         return cols
@@ -374,6 +394,82 @@ class Table:
         out = RowGroup()
         while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
             yield out.first_row, self._rg_arrays(out)
+
+    # -- pushed-down filters
+    def _preds(self, filt):
+        """filt: list of (col, op, value[, clause]); op a fls_cmp or one of OPS;
+        value int (integers, DATE days, DECIMAL scaled), float (FLOAT/DOUBLE) or
+        str/bytes (VARCHAR).  Terms without a clause get their own clause."""
+        sch = self.schema()
+        arr = (Predicate * max(1, len(filt)))()
+        keep = []
+        for i, term in enumerate(filt):
+            col, op, val = term[:3]
+            p = arr[i]
+            p.col = col
+            p.clause = term[3] if len(term) > 3 else 1000000 + i
+            p.op = OPS[op] if isinstance(op, str) else op
+            ty = sch[col][1] if 0 <= col < len(sch) else None
+            if val is None or ty is None:
+                pass
+            elif ty == VARCHAR:
+                b = val.encode() if isinstance(val, str) else bytes(val)
+                buf = C.create_string_buffer(b, len(b) + 1)
+                keep.append(buf)
+                p.str = C.cast(buf, C.c_char_p)
+                p.str_len = len(b)
+            elif ty == FLOAT:
+                p.value = int(np.array([val], dtype=np.float32).view(np.uint32)[0])
+            elif ty == DOUBLE:
+                p.value = int(np.array([val], dtype=np.float64).view(np.uint64)[0])
+            else:
+                p.value = int(val) & 0xFFFFFFFFFFFFFFFF
+        return arr, len(filt), keep
+
+    def set_filter(self, filt):
+        arr, n, keep = self._preds(filt or [])
+        _check(_lib.fls_scan_filter(self.h, arr, n))
+
+    def may_match(self, rg: int, filt) -> bool:
+        arr, n, keep = self._preds(filt)
+        return _check(_lib.fls_rowgroup_may_match(self.h, rg, arr, n)) == 1
+
+    @property
+    def pruned(self) -> int:
+        return _check(_lib.fls_scan_pruned(self.h))
+
+    def zonemap(self, rg: int, col: int):
+        """(min, max, flags) in the column's comparison domain, or None."""
+        lo, hi, fl = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        if _check(_lib.fls_table_zonemap(self.h, rg, col, C.byref(lo), C.byref(hi), C.byref(fl))) == 0:
+            return None
+        ty = self.column(col).type
+        if ty in (FLOAT, DOUBLE):
+            cv = lambda x: float(np.array([x], dtype=np.uint64).view(np.float64)[0])  # noqa: E731
+        elif ty in (INT8, INT16, INT32, INT64, DATE, DECIMAL):
+            cv = lambda x: int(np.array([x], dtype=np.uint64).view(np.int64)[0])  # noqa: E731
+        else:
+            cv = int
+        return cv(lo.value), cv(hi.value), fl.value
+
+    def scan_filtered(self, filt, cols=None, rg_begin=0, rg_end=None):
+        """Filtered scan: yields (rowgroup, first_row, sel, arrays) with only the
+        qualifying rows (sel = their indices within the row group)."""
+        if rg_end is None:
+            rg_end = self.nrowgroups
+        self.set_filter(filt)
+        try:
+            _check(_lib.fls_scan_begin(self.h, _mask(self, cols), rg_begin, rg_end))
+            out = RowGroup()
+            while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
+                if out.sel:
+                    sel = np.ctypeslib.as_array(out.sel, shape=(out.nrows,)).copy() if out.nrows else \
+                        np.zeros(0, np.uint32)
+                else:
+                    sel = np.arange(out.nrows, dtype=np.uint32)
+                yield out.rowgroup, out.first_row, sel, self._rg_arrays(out)
+        finally:
+            _check(_lib.fls_scan_filter(self.h, None, 0))
 
     # -- device-resident decode (bench)
     def device_upload(self, rg_begin=0, rg_end=None):

@@ -10,6 +10,7 @@
 // 256-byte aligned, every packed vector 16-byte aligned, per-vector metadata is
 // a flat 32-byte record array.  DESIGN.md "Container format" is the spec.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 
 namespace fls {
@@ -121,8 +122,85 @@ static_assert(alignof(VecMeta) == 8 && alignof(ChunkHeader) == 8, "natural align
 //   u64 row_offset,
 //   per column: u8 type, u8 width, u8 scale, u8 pad, u16 name_len, name[name_len]
 //   per row group: u32 nrows, per column {u64 chunk_off, u64 chunk_len}
+//   optional zone-map section (readers that stop after the row-group table,
+//   e.g. oracle/flsref.c, ignore it):
+//   u32 kZoneMagic, u32 entry bytes (24), then per row group per column a
+//   ZoneMap.  Zone maps feed row-group pruning of pushed-down filters
+//   (read_fastlanes filter_pushdown; reference src/scanner/scan_fastlanes.cpp:154
+//   leaves it off).
 // File tail (16 B): u64 footer_off, u32 footer_len, "FLSF".
 constexpr uint32_t kFooterVersion = 1;
 constexpr uint32_t kFooterFixed = 32;
+constexpr uint32_t kZoneMagic = 0x50414D5Au;  // "ZMAP"
+
+// min / max of one column chunk in the column's comparison domain:
+// signed integers (INT*, DATE, DECIMAL) as int64, unsigned as uint64,
+// FLOAT/DOUBLE as the IEEE bits of a double over the non-NaN values (NaN
+// sorts above every number, as in DuckDB).  VARCHAR has none: DICT chunks are
+// pruned on their dictionary instead.
+enum : uint32_t { ZM_VALID = 1, ZM_HAS_NAN = 2, ZM_ALL_NAN = 4 };
+struct ZoneMap {              // 24 B
+    uint64_t min, max;
+    uint32_t flags;
+    uint32_t pad;
+};
+static_assert(sizeof(ZoneMap) == 24, "zone map entry is 24 B");
+
+inline bool type_is_signed(uint8_t t) {
+    return t == TY_INT8 || t == TY_INT16 || t == TY_INT32 || t == TY_INT64 || t == TY_DATE || t == TY_DECIMAL;
+}
+
+// Zone map of n values given as raw T-bit patterns (T = type_value_bits).
+inline ZoneMap zone_of(uint8_t type, const uint64_t *raw, uint32_t n) {
+    ZoneMap z{0, 0, 0, 0};
+    const int T = type_value_bits(type);
+    if (T == 0 || n == 0) return z;
+    z.flags = ZM_VALID;
+    if (type_is_float(type)) {
+        bool any = false;
+        double mn = 0, mx = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            double d;
+            if (T == 32) {
+                float f;
+                const uint32_t b = (uint32_t)raw[i];
+                __builtin_memcpy(&f, &b, 4);
+                d = f;
+            } else {
+                __builtin_memcpy(&d, &raw[i], 8);
+            }
+            if (d != d) { z.flags |= ZM_HAS_NAN; continue; }
+            if (d == 0) d = 0.0;  // -0 == 0: one canonical zero
+            if (!any || d < mn) mn = d;
+            if (!any || d > mx) mx = d;
+            any = true;
+        }
+        if (!any) z.flags |= ZM_ALL_NAN;
+        __builtin_memcpy(&z.min, &mn, 8);
+        __builtin_memcpy(&z.max, &mx, 8);
+        return z;
+    }
+    const uint64_t m = T >= 64 ? ~0ull : ((1ull << T) - 1);
+    if (type_is_signed(type)) {
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+        for (uint32_t i = 0; i < n; ++i) {
+            uint64_t v = raw[i] & m;
+            if (T < 64) { const uint64_t s = 1ull << (T - 1); v = (v ^ s) - s; }
+            mn = std::min(mn, (int64_t)v);
+            mx = std::max(mx, (int64_t)v);
+        }
+        z.min = (uint64_t)mn;
+        z.max = (uint64_t)mx;
+    } else {
+        uint64_t mn = UINT64_MAX, mx = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            mn = std::min(mn, raw[i] & m);
+            mx = std::max(mx, raw[i] & m);
+        }
+        z.min = mn;
+        z.max = mx;
+    }
+    return z;
+}
 
 }  // namespace fls

@@ -26,6 +26,7 @@ struct RowGroupMeta {
     uint32_t nrows;
     uint64_t first_row;            // relative to the file's first row
     std::vector<ChunkRef> chunks;  // one per column
+    std::vector<ZoneMap> zones;    // one per column, empty without a zone-map section
 };
 
 struct FileMeta {
@@ -166,6 +167,19 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
         p += 4 + 16ull * ncols;
     }
     if (rows != m.nrows) return "row count mismatch";
+    // optional zone-map section
+    uint32_t zh[2];
+    if (p + 8 <= fend && rd(p, zh, 8) && zh[0] == kZoneMagic) {
+        if (zh[1] != sizeof(ZoneMap) || p + 8 + (uint64_t)nrg * ncols * sizeof(ZoneMap) > fend)
+            return "truncated zone-map section";
+        for (uint32_t r = 0; r < nrg; ++r) {
+            auto &z = m.rgs[r].zones;
+            z.resize(ncols);
+            rd(p + 8 + (uint64_t)r * ncols * sizeof(ZoneMap), z.data(), ncols * sizeof(ZoneMap));
+            for (uint32_t c = 0; c < ncols; ++c)
+                if (m.cols[c].type == TY_VARCHAR) z[c].flags = 0;
+        }
+    }
     return "";
 }
 

@@ -738,6 +738,7 @@ struct FileBuilder {
     struct RG {
         uint32_t nrows;
         std::vector<std::vector<uint8_t>> chunks;
+        std::vector<ZoneMap> zones;  // per column (VARCHAR: none)
     };
     std::vector<RG> rgs;
 
@@ -764,6 +765,12 @@ struct FileBuilder {
                 put(&len, 8);
             }
         }
+        // zone-map section (fls_format.hpp)
+        uint32_t zm[2] = {kZoneMagic, (uint32_t)sizeof(ZoneMap)};
+        put(zm, 8);
+        const ZoneMap none{0, 0, 0, 0};
+        for (auto &r : rgs)
+            for (size_t c = 0; c < cols.size(); ++c) put(c < r.zones.size() ? &r.zones[c] : &none, sizeof(ZoneMap));
         return f;
     }
 
@@ -942,7 +949,8 @@ void gen_comments(const Workload &w, uint64_t row0, uint32_t n, std::vector<uint
     }
 }
 
-std::vector<uint8_t> encode_gen_chunk(const Workload &w, int c, const std::vector<uint64_t> &vals) {
+std::vector<uint8_t> encode_gen_chunk(const Workload &w, int c, const std::vector<uint64_t> &vals,
+                                      ZoneMap *zone = nullptr) {
     const ColSpec &cs = w.cols[c];
     const uint32_t n = (uint32_t)vals.size();
     if (c == w.comment_col) {
@@ -960,6 +968,7 @@ std::vector<uint8_t> encode_gen_chunk(const Workload &w, int c, const std::vecto
     const int T = type_value_bits(cs.type);
     std::vector<uint64_t> tv(vals);
     for (auto &x : tv) x &= tmask(T);
+    if (zone) *zone = zone_of(cs.type, tv.data(), n);
     return encode_int_chunk(cs.type, cs.enc, tv.data(), n);
 }
 
@@ -1032,6 +1041,8 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
                 v[i] = x;
             }
             rg.chunks.push_back(encode_int_chunk(cs.type, cs.enc, v.data(), nrows));
+            rg.zones.resize(c + 1, ZoneMap{0, 0, 0, 0});
+            rg.zones[c] = zone_of(cs.type, v.data(), nrows);
         }
     }
     w->fb.rgs.push_back(std::move(rg));
@@ -1104,7 +1115,9 @@ int fls_gen_image(const char *workload, double scale, uint64_t nrows, uint32_t r
             auto &out = fb.rgs[rg - rg_begin];
             out.nrows = n;
             out.chunks.resize(w.cols.size());
-            for (size_t c = 0; c < w.cols.size(); ++c) out.chunks[c] = encode_gen_chunk(w, (int)c, vals[c]);
+            out.zones.assign(w.cols.size(), ZoneMap{0, 0, 0, 0});
+            for (size_t c = 0; c < w.cols.size(); ++c)
+                out.chunks[c] = encode_gen_chunk(w, (int)c, vals[c], &out.zones[c]);
         }
     };
     std::vector<std::thread> th;

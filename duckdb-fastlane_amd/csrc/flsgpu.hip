@@ -22,6 +22,7 @@
 #include "../../include/flsgpu.h"
 #include "fls_common.hpp"
 #include "fls_decode.hpp"
+#include "fls_filter.hpp"
 #include "fls_format.hpp"
 #include "fls_reader.hpp"
 
@@ -150,10 +151,10 @@ struct DeviceShard {
 };
 
 struct Slot {                       // one batch of row groups in flight
-    uint32_t rg0 = 0, nrg = 0;      // absolute row groups
+    uint32_t rg0 = 0, nrg = 0;      // absolute row groups (consecutive, all surviving pruning)
     bool busy = false;
-    std::vector<DevBuf<uint8_t>> d_out;   // per column
-    std::vector<PinBuf<uint8_t>> h_out;   // per column (pinned)
+    std::vector<DevBuf<uint8_t>> d_out;   // per decoded column
+    std::vector<PinBuf<uint8_t>> h_out;   // per delivered column (pinned)
     std::vector<DevBuf<uint8_t>> d_heap;  // per FSST column: decoded string bytes
     std::vector<PinBuf<uint8_t>> h_heap;  // per FSST column: pinned copy string_t points into
     std::vector<uint64_t> heap_bytes;     // per column: heap bytes of this batch
@@ -165,13 +166,24 @@ struct Slot {                       // one batch of row groups in flight
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
     uint32_t released = 0;          // row groups of the batch handed back by consumers
     std::vector<const void *> col_ptrs;  // per (rg - rg0) * ncols + col: pinned host column start
+    // filtered batches (fls_scan_filter)
+    DevBuf<uint64_t> d_mask;        // selection bits, 16 words per 1024-row vector
+    DevBuf<uint32_t> d_counts;      // selected rows per vector
+    PinBuf<uint32_t> h_counts;
+    PinBuf<uint32_t> h_sel;         // selected row indices within their row group
+    PinBuf<uint8_t> h_fdesc;        // DevTerm[] + DevOut[] + constant strings
+    DevBuf<uint8_t> d_fdesc;
+    uint32_t nvec = 0;              // vectors of the batch
+    bool sel_ready = false;         // sel_off computed from h_counts
+    std::vector<uint32_t> sel_off;  // per row group of the batch (+1): first selected row
 };
 
 struct ScanDev {
     int dev = -1;
     hipStream_t stream = nullptr;
-    uint32_t rg0 = 0, rg1 = 0;      // row groups this GPU owns within the scan
-    uint32_t next_batch_rg = 0;     // next row group to enqueue
+    uint32_t rg0 = 0, rg1 = 0;      // span of row groups this GPU owns within the scan
+    uint32_t p0 = 0, p1 = 0;        // ... as positions in ScanCtx::rgs
+    uint32_t next_p = 0;            // next position to enqueue
     Slot slots[2];
     DevBuf<StrT> strtab;
     std::vector<uint64_t> strtab_off;
@@ -179,10 +191,22 @@ struct ScanDev {
     int grid = 0;
 };
 
+// One term of a pushed-down filter (fls_scan_filter), host side.
+struct HostTerm {
+    uint32_t col = 0, clause = 0;
+    uint8_t op = 0, kind = 0;
+    uint64_t value = 0;             // comparison domain: int64 / uint64 / double bits
+    std::string str;
+};
+
 struct ScanCtx {
     bool active = false;
-    std::vector<uint8_t> mask;
-    uint32_t rg0 = 0, rg1 = 0, cur = 0;
+    std::vector<uint8_t> mask;      // delivered columns
+    std::vector<uint8_t> dmask;     // decoded columns (delivered + filter columns)
+    std::vector<HostTerm> terms;    // filter of this scan, sorted by clause (empty: none)
+    std::vector<uint32_t> rgs;      // row groups to scan, in order (pruned ones left out)
+    uint32_t cur = 0;               // next position in rgs to hand out
+    uint32_t pruned = 0;
     uint32_t batch = 8;
     std::vector<ScanDev> devs;
     int64_t held = -1;              // row group fls_scan_next handed out last (released on the next call)
@@ -223,6 +247,7 @@ struct fls_table {
     bool launched = false;
 
     ScanCtx scan, mat;
+    std::vector<HostTerm> filter;   // fls_scan_filter: applies to the next fls_scan_begin
     ~fls_table();
 };
 
@@ -367,7 +392,65 @@ fls_table::~fls_table() {
 
 namespace {
 
-int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, uint32_t rg1) {
+// May any row of row group rg satisfy term h?  (zone maps / dictionary)
+bool term_may_match(const fls_table *t, uint32_t rg, const HostTerm &h) {
+    if (h.op == OP_IS_NULL) return false;  // the format has no NULLs
+    if (h.op == OP_IS_NOT_NULL) return true;
+    const RowGroupMeta &r = t->meta.rgs[rg];
+    const ChunkRef &ch = r.chunks[h.col];
+    if (h.kind == FK_STR) {
+        if (ch.hdr.enc != ENC_DICT) return true;  // FSST: no statistics
+        const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
+        const uint8_t *bytes = aux + 4ull * (ch.hdr.dict_count + 1);
+        for (uint32_t i = 0; i < ch.hdr.dict_count; ++i) {
+            uint32_t b0, b1;
+            memcpy(&b0, aux + 4ull * i, 4);
+            memcpy(&b1, aux + 4ull * (i + 1), 4);
+            if (op_holds(h.op, cmp_bytes(bytes + b0, b1 - b0, (const uint8_t *)h.str.data(), (uint32_t)h.str.size())))
+                return true;
+        }
+        return false;
+    }
+    if (r.zones.empty() || !(r.zones[h.col].flags & ZM_VALID)) return true;
+    const ZoneMap &z = r.zones[h.col];
+    int cmin, cmax;  // min vs constant, max vs constant
+    if (h.kind == FK_INT) {
+        cmin = cmp_int((int64_t)z.min, (int64_t)h.value);
+        cmax = cmp_int((int64_t)z.max, (int64_t)h.value);
+    } else if (h.kind == FK_UINT) {
+        cmin = cmp_uint(z.min, h.value);
+        cmax = cmp_uint(z.max, h.value);
+    } else {
+        const double nan = __builtin_nan("");
+        const double lo = (z.flags & ZM_ALL_NAN) ? nan : as_double(z.min);
+        const double hi = (z.flags & ZM_HAS_NAN) ? nan : as_double(z.max);
+        cmin = cmp_float(lo, as_double(h.value));
+        cmax = cmp_float(hi, as_double(h.value));
+    }
+    switch (h.op) {
+    case OP_EQ: return cmin <= 0 && cmax >= 0;
+    case OP_NE: return !(cmin == 0 && cmax == 0);
+    case OP_LT: return cmin < 0;
+    case OP_LE: return cmin <= 0;
+    case OP_GT: return cmax > 0;
+    default: return cmax >= 0;  // OP_GE
+    }
+}
+
+// Every clause has a term that may match (terms sorted by clause).
+bool rowgroup_may_match(const fls_table *t, uint32_t rg, const std::vector<HostTerm> &terms) {
+    size_t i = 0;
+    while (i < terms.size()) {
+        bool any = false;
+        const uint32_t cl = terms[i].clause;
+        for (; i < terms.size() && terms[i].clause == cl; ++i) any = any || term_may_match(t, rg, terms[i]);
+        if (!any) return false;
+    }
+    return true;
+}
+
+int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, uint32_t rg1,
+               const std::vector<HostTerm> *filter) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     if (rg1 > t->meta.rgs.size() || rg0 > rg1) return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg0, rg1);
     // tear down a previous scan on this context
@@ -382,12 +465,22 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     s.mask.assign(ncols, 1);
     if (col_mask)
         for (uint32_t c = 0; c < ncols; ++c) s.mask[c] = col_mask[c] ? 1 : 0;
-    s.rg0 = rg0;
-    s.rg1 = rg1;
-    s.cur = rg0;
+    s.terms.clear();
+    if (filter) s.terms = *filter;
+    s.dmask = s.mask;
+    for (auto &h : s.terms)
+        if (h.op < OP_IS_NULL) s.dmask[h.col] = 1;
+    // row-group pruning on zone maps / dictionaries
+    s.rgs.clear();
+    s.pruned = 0;
+    for (uint32_t r = rg0; r < rg1; ++r) {
+        if (s.terms.empty() || rowgroup_may_match(t, r, s.terms)) s.rgs.push_back(r);
+        else s.pruned++;
+    }
+    s.cur = 0;
     s.held = -1;
     const auto &devs = t->conn->devices;
-    const uint32_t G = (uint32_t)devs.size(), nrg = rg1 - rg0;
+    const uint32_t G = (uint32_t)devs.size(), n = (uint32_t)s.rgs.size();
     if (s.devs.size() != G) {
         for (auto &d : s.devs) {
             hipSetDevice(d.dev);
@@ -413,9 +506,12 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
             sl.d_out.resize(ncols);
             sl.h_out.resize(ncols);
         }
-        d.rg0 = rg0 + (uint32_t)((uint64_t)nrg * g / G);
-        d.rg1 = rg0 + (uint32_t)((uint64_t)nrg * (g + 1) / G);
-        d.next_batch_rg = d.rg0;
+        // contiguous shard of the surviving row groups
+        d.p0 = (uint32_t)((uint64_t)n * g / G);
+        d.p1 = (uint32_t)((uint64_t)n * (g + 1) / G);
+        d.next_p = d.p0;
+        d.rg0 = d.p0 < d.p1 ? s.rgs[d.p0] : 0;
+        d.rg1 = d.p0 < d.p1 ? s.rgs[d.p1 - 1] + 1 : 0;
         int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off);
         if (rc) return rc;
         HIP_TRY(d.err.alloc(d.dev, 1));
@@ -431,14 +527,83 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     return 0;
 }
 
-// enqueue the next batch of device d into slot si
+// Filter descriptors of a batch: the terms over the slot's decoded columns,
+// the delivered columns' compaction targets, then the constant strings.
+int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows, uint64_t in_lo, uint64_t in_len) {
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    std::vector<DevOut> outs;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        if (!col_selected(s.mask, c)) continue;
+        DevOut o;
+        memset(&o, 0, sizeof(o));
+        o.src = sl.d_out[c].p;
+        o.dst = sl.h_out[c].p;
+        o.ob = (uint32_t)out_bytes_of(t, c);
+        outs.push_back(o);
+    }
+    const size_t nt = s.terms.size(), no = outs.size();
+    size_t str_bytes = 0;
+    for (auto &h : s.terms) str_bytes += (h.str.size() + 15) & ~size_t(15);
+    const size_t bytes = nt * sizeof(DevTerm) + no * sizeof(DevOut) + str_bytes;
+    HIP_TRY(sl.h_fdesc.alloc(bytes));
+    HIP_TRY(sl.d_fdesc.alloc(d.dev, bytes));
+    uint8_t *hb = sl.h_fdesc.p;
+    DevTerm *terms = (DevTerm *)hb;
+    size_t so = nt * sizeof(DevTerm) + no * sizeof(DevOut);
+    for (size_t i = 0; i < nt; ++i) {
+        const HostTerm &h = s.terms[i];
+        DevTerm &dt = terms[i];
+        memset(&dt, 0, sizeof(dt));
+        dt.col = sl.d_out[h.col].p;
+        dt.value = h.value;
+        dt.kind = h.kind;
+        dt.op = h.op;
+        dt.ob = (uint8_t)out_bytes_of(t, h.col);
+        dt.end_clause = (i + 1 == nt || s.terms[i + 1].clause != h.clause) ? 1 : 0;
+        if (h.kind == FK_STR) {
+            memcpy(hb + so, h.str.data(), h.str.size());
+            dt.str = sl.d_fdesc.p + so;
+            dt.str_len = (uint32_t)h.str.size();
+            so += (h.str.size() + 15) & ~size_t(15);
+            if (sl.heap_bytes[h.col]) {  // FSST: long strings live in the batch heap
+                dt.host_lo = (uint64_t)(uintptr_t)sl.h_heap[h.col].p;
+                dt.host_hi = dt.host_lo + sl.heap_bytes[h.col];
+                dt.dev_delta = (int64_t)((uintptr_t)sl.d_heap[h.col].p - (uintptr_t)sl.h_heap[h.col].p);
+            } else {  // DICT: long strings point into the file image, uploaded as d_in
+                dt.host_lo = (uint64_t)(uintptr_t)(t->img + in_lo);
+                dt.host_hi = dt.host_lo + in_len;
+                dt.dev_delta = (int64_t)((uintptr_t)sl.d_in.p - (uintptr_t)(t->img + in_lo));
+            }
+        }
+    }
+    memcpy(hb + nt * sizeof(DevTerm), outs.data(), no * sizeof(DevOut));
+    HIP_TRY(hipMemcpyAsync(sl.d_fdesc.p, hb, bytes, hipMemcpyHostToDevice, sl.stream));
+    sl.nvec = (uint32_t)((rows + 1023) / 1024);
+    HIP_TRY(sl.d_mask.alloc(d.dev, (size_t)sl.nvec * 16));
+    HIP_TRY(sl.d_counts.alloc(d.dev, sl.nvec));
+    HIP_TRY(sl.h_counts.alloc(sl.nvec));
+    HIP_TRY(sl.h_sel.alloc(std::max<uint64_t>(rows, 1)));
+    HIP_TRY(launch_filter((const DevTerm *)sl.d_fdesc.p, (uint32_t)nt, (uint32_t)rows, sl.d_mask.p, sl.d_counts.p,
+                          d.err.p, sl.stream));
+    HIP_TRY(launch_compact((const DevOut *)(sl.d_fdesc.p + nt * sizeof(DevTerm)), (uint32_t)no, sl.d_mask.p,
+                           sl.d_counts.p, (uint32_t)rows, t->meta.rowgroup_size, sl.h_sel.p, sl.stream));
+    HIP_TRY(hipMemcpyAsync(sl.h_counts.p, sl.d_counts.p, sl.nvec * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           sl.stream));
+    sl.sel_ready = false;
+    return 0;
+}
+
+// enqueue the next batch of device d into slot si: up to s.batch consecutive
+// surviving row groups
 int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     Slot &sl = d.slots[si];
-    if (d.next_batch_rg >= d.rg1) { sl.busy = false; return 0; }
+    if (d.next_p >= d.p1) { sl.busy = false; return 0; }
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
-    sl.rg0 = d.next_batch_rg;
-    sl.nrg = std::min(s.batch, d.rg1 - sl.rg0);
-    d.next_batch_rg += sl.nrg;
+    const bool filtered = !s.terms.empty();
+    sl.rg0 = s.rgs[d.next_p];
+    sl.nrg = 1;
+    while (sl.nrg < s.batch && d.next_p + sl.nrg < d.p1 && s.rgs[d.next_p + sl.nrg] == sl.rg0 + sl.nrg) sl.nrg++;
+    d.next_p += sl.nrg;
     HIP_TRY(hipSetDevice(d.dev));
     // 1. H2D of the batch's compressed bytes
     uint64_t lo, hi;
@@ -453,10 +618,10 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     sl.h_heap.resize(ncols);
     std::vector<uint64_t> hoff((size_t)sl.nrg * ncols, 0);
     for (uint32_t c = 0; c < ncols; ++c) {
-        if (!col_selected(s.mask, c)) continue;
+        if (!col_selected(s.dmask, c)) continue;
         const uint64_t nb = max_rows * out_bytes_of(t, c);
         HIP_TRY(sl.d_out[c].alloc(d.dev, nb));
-        HIP_TRY(sl.h_out[c].alloc(nb));
+        if (col_selected(s.mask, c)) HIP_TRY(sl.h_out[c].alloc(nb));
         for (uint32_t r = 0; r < sl.nrg; ++r) {
             hoff[(size_t)r * ncols + c] = sl.heap_bytes[c];
             if (is_fsst(t, sl.rg0 + r, c)) sl.heap_bytes[c] += t->meta.rgs[sl.rg0 + r].chunks[c].hdr.reserved1;
@@ -469,7 +634,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     std::vector<DevChunk> list;
     ByteCount bc;
     for (uint32_t c = 0; c < ncols; ++c) {
-        if (!col_selected(s.mask, c)) continue;
+        if (!col_selected(s.dmask, c)) continue;
         for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) {
             const ChunkRef &ch = t->meta.rgs[r].chunks[c];
             const uint64_t so = d.strtab_off[(size_t)(r - d.rg0) * ncols + c];
@@ -490,24 +655,31 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     if (k) memcpy(sl.h_chunks.p, list.data(), k * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream));
-    // 3. D2H into pinned host columns (and string heaps)
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
+    if (filtered) {
+        // 3a. select + compact the qualifying rows straight into pinned host memory
+        int rc = enqueue_filter(t, s, d, sl, rows, lo, hi - lo);
+        if (rc) return rc;
+    }
+    // 3. D2H into pinned host columns (and string heaps)
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
-        HIP_TRY(hipMemcpyAsync(sl.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
-                               sl.stream));
+        if (!filtered)
+            HIP_TRY(hipMemcpyAsync(sl.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
+                                   sl.stream));
         if (sl.heap_bytes[c])
             HIP_TRY(hipMemcpyAsync(sl.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
     }
     HIP_TRY(hipEventRecord(sl.done, sl.stream));
     sl.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
-    for (uint32_t r = 0; r < sl.nrg; ++r)
-        for (uint32_t c = 0; c < ncols; ++c)
-            if (col_selected(s.mask, c))
-                sl.col_ptrs[(size_t)r * ncols + c] =
-                    sl.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) *
-                                        out_bytes_of(t, c);
+    if (!filtered)
+        for (uint32_t r = 0; r < sl.nrg; ++r)
+            for (uint32_t c = 0; c < ncols; ++c)
+                if (col_selected(s.mask, c))
+                    sl.col_ptrs[(size_t)r * ncols + c] =
+                        sl.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) *
+                                            out_bytes_of(t, c);
     sl.released = 0;
     sl.busy = true;
     return 0;
@@ -536,6 +708,27 @@ bool find_slot(ScanCtx &s, uint32_t rg, int &g, int &si) {
     return false;
 }
 
+// filtered batch: selected-row offsets of its row groups from the per-vector
+// counts (every row group of a batch but the table's last is whole vectors)
+void batch_selection(fls_table *t, ScanCtx &s, Slot &sl) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (sl.sel_ready) return;
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    sl.sel_off.assign(sl.nrg + 1, 0);
+    uint32_t v = 0, acc = 0;
+    for (uint32_t r = 0; r < sl.nrg; ++r) {
+        sl.sel_off[r] = acc;
+        const uint32_t nv = (t->meta.rgs[sl.rg0 + r].nrows + 1023) / 1024;
+        for (uint32_t k = 0; k < nv && v < sl.nvec; ++k) acc += sl.h_counts.p[v++];
+    }
+    sl.sel_off[sl.nrg] = acc;
+    for (uint32_t r = 0; r < sl.nrg; ++r)
+        for (uint32_t c = 0; c < ncols; ++c)
+            if (col_selected(s.mask, c))
+                sl.col_ptrs[(size_t)r * ncols + c] = sl.h_out[c].p + (uint64_t)sl.sel_off[r] * out_bytes_of(t, c);
+    sl.sel_ready = true;
+}
+
 // Claim the next row group in order and wait until its batch is decoded and
 // copied back.  Its buffers stay valid until scan_release(rg).
 int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
@@ -544,8 +737,8 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     uint32_t rg;
     {
         std::unique_lock<std::mutex> lk(s.mu);
-        if (s.cur >= s.rg1) return 0;
-        rg = s.cur++;
+        if (s.cur >= s.rgs.size()) return 0;
+        rg = s.rgs[s.cur++];
         // the batch holding rg is enqueued once every row group of the slot's
         // previous batch has been released (by this or another consumer)
         s.cv.wait(lk, [&] { return !s.active || find_slot(s, rg, g, si); });
@@ -557,12 +750,21 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     HIP_TRY(hipEventSynchronize(sl.done));
     uint32_t err = 0;
     HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
+    if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
     if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     out->rowgroup = rg;
     out->nrows = t->meta.rgs[rg].nrows;
     out->first_row = t->meta.row_offset + t->meta.rgs[rg].first_row;
     out->ncols = ncols;
+    out->nrows_scanned = out->nrows;
+    out->sel = nullptr;
+    if (!s.terms.empty()) {
+        batch_selection(t, s, sl);
+        const uint32_t i = rg - sl.rg0;
+        out->nrows = sl.sel_off[i + 1] - sl.sel_off[i];
+        out->sel = sl.h_sel.p + sl.sel_off[i];
+    }
     out->columns = sl.col_ptrs.data() + (size_t)(rg - sl.rg0) * ncols;
     return 1;
 }
@@ -592,6 +794,45 @@ int scan_next(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     int rc = scan_acquire(t, s, out);
     if (rc == 1) s.held = out->rowgroup;
     return rc;
+}
+
+// fls_predicate[] -> host terms in the comparison domain, sorted by clause
+int to_terms(const fls_table *t, const fls_predicate *p, uint32_t n, std::vector<HostTerm> &out) {
+    out.clear();
+    if (n && !p) return fail(FLS_ERR_ARG, "fls_scan_filter: NULL predicates");
+    for (uint32_t i = 0; i < n; ++i) {
+        if (p[i].col >= t->meta.cols.size()) return fail(FLS_ERR_ARG, "filter column %u out of range", p[i].col);
+        if (p[i].op > FLS_CMP_IS_NOT_NULL) return fail(FLS_ERR_ARG, "filter operator %u unknown", p[i].op);
+        HostTerm h;
+        h.col = p[i].col;
+        h.clause = p[i].clause;
+        h.op = p[i].op;
+        const uint8_t ty = t->meta.cols[h.col].type;
+        if (ty == TY_VARCHAR) {
+            h.kind = FK_STR;
+            if (p[i].str_len && !p[i].str) return fail(FLS_ERR_ARG, "filter on column %u: NULL string", h.col);
+            if (p[i].str_len > 0xFFFFFFFFull) return fail(FLS_ERR_ARG, "filter string too long");
+            if (p[i].str_len) h.str.assign(p[i].str, p[i].str_len);
+        } else if (type_is_float(ty)) {
+            h.kind = FK_FLOAT;
+            double d;
+            if (ty == TY_FLOAT) {
+                float f;
+                const uint32_t b = (uint32_t)p[i].value;
+                memcpy(&f, &b, 4);
+                d = f;
+            } else {
+                memcpy(&d, &p[i].value, 8);
+            }
+            memcpy(&h.value, &d, 8);
+        } else {
+            h.kind = type_is_signed(ty) ? FK_INT : FK_UINT;
+            h.value = p[i].value;
+        }
+        out.push_back(std::move(h));
+    }
+    std::stable_sort(out.begin(), out.end(), [](const HostTerm &a, const HostTerm &b) { return a.clause < b.clause; });
+    return 0;
 }
 
 int ensure_stream(fls_table *t, int dev) {
@@ -709,7 +950,7 @@ int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowg
     one.devices = {t->conn->devices[g]};
     fls_connection *saved = t->conn;
     t->conn = &one;
-    int rc = scan_setup(t, t->mat, col_mask, rg, rg + 1);
+    int rc = scan_setup(t, t->mat, col_mask, rg, rg + 1, nullptr);
     if (!rc) rc = scan_start(t, t->mat);
     t->conn = saved;
     if (rc) return rc;
@@ -719,9 +960,42 @@ int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowg
 
 int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uint32_t rg_end) {
     if (!t) return fail(FLS_ERR_ARG, "fls_scan_begin: NULL table");
-    int rc = scan_setup(t, t->scan, col_mask, rg_begin, rg_end);
+    int rc = scan_setup(t, t->scan, col_mask, rg_begin, rg_end, &t->filter);
     if (rc) return rc;
     return scan_start(t, t->scan);
+}
+
+int fls_scan_filter(fls_table *t, const fls_predicate *preds, uint32_t n) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_filter: NULL table");
+    std::vector<HostTerm> terms;
+    int rc = to_terms(t, preds, n, terms);
+    if (rc) return rc;
+    t->filter.swap(terms);
+    return 0;
+}
+
+int fls_scan_pruned(const fls_table *t) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_pruned: NULL table");
+    return (int)t->scan.pruned;
+}
+
+int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *min, uint64_t *max, uint32_t *flags) {
+    if (!t || rg >= t->meta.rgs.size() || col >= t->meta.cols.size())
+        return fail(FLS_ERR_ARG, "zone map (%u, %u) out of range", rg, col);
+    const auto &z = t->meta.rgs[rg].zones;
+    if (z.empty() || !(z[col].flags & ZM_VALID)) return 0;
+    if (min) *min = z[col].min;
+    if (max) *max = z[col].max;
+    if (flags) *flags = z[col].flags;
+    return 1;
+}
+
+int fls_rowgroup_may_match(const fls_table *t, uint32_t rg, const fls_predicate *preds, uint32_t n) {
+    if (!t || rg >= t->meta.rgs.size()) return fail(FLS_ERR_ARG, "row group %u out of range", rg);
+    std::vector<HostTerm> terms;
+    int rc = to_terms(t, preds, n, terms);
+    if (rc) return rc;
+    return rowgroup_may_match(t, rg, terms) ? 1 : 0;
 }
 
 int fls_scan_next(fls_table *t, fls_rowgroup *out) {

@@ -186,6 +186,8 @@ public:
     template <class T>
     T GetValue() const;
     int64_t GetInt64() const { return int_; }
+    template <class T>
+    T GetValueUnsafe() const { return (T)int_; }
     double GetDouble() const { return dbl_; }
     const vector<Value> &ListChildren() const { return list_; }
     // DuckDB's VARCHAR rendering of the value (the cast Vector::SetValue applies)
@@ -208,6 +210,15 @@ template <>
 inline int32_t Value::GetValue<int32_t>() const { return (int32_t)int_; }
 template <>
 inline bool Value::GetValue<bool>() const { return int_ != 0; }
+template <>
+inline uint64_t Value::GetValue<uint64_t>() const { return (uint64_t)int_; }
+template <>
+inline double Value::GetValue<double>() const { return dbl_; }
+template <>
+inline float Value::GetValue<float>() const { return (float)dbl_; }
+template <>
+inline date_t Value::GetValue<date_t>() const { return date_t{(int32_t)int_}; }
+
 
 // ---- vectors ---------------------------------------------------------------
 enum class VectorType : uint8_t { FLAT_VECTOR, CONSTANT_VECTOR };
@@ -312,6 +323,91 @@ struct LocalTableFunctionState {
 using named_parameter_map_t = std::unordered_map<string, Value>;
 using named_parameter_type_map_t = std::unordered_map<string, LogicalType>;
 
+// ---- pushed-down table filters (duckdb/planner/table_filter.hpp and
+// duckdb/planner/filter/*.hpp).  TableFilterSet::filters is keyed by the
+// position in TableFunctionInitInput::column_ids.
+enum class ExpressionType : uint8_t {
+    COMPARE_EQUAL = 25, COMPARE_NOTEQUAL = 26, COMPARE_LESSTHAN = 27, COMPARE_GREATERTHAN = 28,
+    COMPARE_LESSTHANOREQUALTO = 29, COMPARE_GREATERTHANOREQUALTO = 30
+};
+enum class TableFilterType : uint8_t {
+    CONSTANT_COMPARISON = 0, IS_NULL = 1, IS_NOT_NULL = 2, CONJUNCTION_OR = 3, CONJUNCTION_AND = 4,
+    STRUCT_EXTRACT = 5, OPTIONAL_FILTER = 6, IN_FILTER = 7, DYNAMIC_FILTER = 8, EXPRESSION_FILTER = 9
+};
+class TableFilter {
+public:
+    explicit TableFilter(TableFilterType t) : filter_type(t) {}
+    virtual ~TableFilter() = default;
+    TableFilterType filter_type;
+    template <class T>
+    T &Cast() { return static_cast<T &>(*this); }
+    template <class T>
+    const T &Cast() const { return static_cast<const T &>(*this); }
+};
+class ConstantFilter : public TableFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::CONSTANT_COMPARISON;
+    ConstantFilter(ExpressionType comparison_type, Value constant)
+        : TableFilter(TYPE), comparison_type(comparison_type), constant(std::move(constant)) {}
+    ExpressionType comparison_type;
+    Value constant;
+};
+class IsNullFilter : public TableFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::IS_NULL;
+    IsNullFilter() : TableFilter(TYPE) {}
+};
+class IsNotNullFilter : public TableFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::IS_NOT_NULL;
+    IsNotNullFilter() : TableFilter(TYPE) {}
+};
+class ConjunctionFilter : public TableFilter {
+public:
+    explicit ConjunctionFilter(TableFilterType t) : TableFilter(t) {}
+    vector<unique_ptr<TableFilter>> child_filters;
+};
+class ConjunctionOrFilter : public ConjunctionFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::CONJUNCTION_OR;
+    ConjunctionOrFilter() : ConjunctionFilter(TYPE) {}
+};
+class ConjunctionAndFilter : public ConjunctionFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::CONJUNCTION_AND;
+    ConjunctionAndFilter() : ConjunctionFilter(TYPE) {}
+};
+class InFilter : public TableFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::IN_FILTER;
+    explicit InFilter(vector<Value> values) : TableFilter(TYPE), values(std::move(values)) {}
+    vector<Value> values;
+};
+class OptionalFilter : public TableFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::OPTIONAL_FILTER;
+    explicit OptionalFilter(unique_ptr<TableFilter> child = nullptr) : TableFilter(TYPE), child_filter(std::move(child)) {}
+    unique_ptr<TableFilter> child_filter;
+};
+class TableFilterSet {
+public:
+    std::map<idx_t, unique_ptr<TableFilter>> filters;
+    // a second filter on one column AND-s with the first (TableFilterSet::PushFilter)
+    void PushFilter(idx_t column_index, unique_ptr<TableFilter> filter) {
+        auto it = filters.find(column_index);
+        if (it == filters.end()) {
+            filters[column_index] = std::move(filter);
+            return;
+        }
+        if (it->second->filter_type != TableFilterType::CONJUNCTION_AND) {
+            auto conj = make_uniq<ConjunctionAndFilter>();
+            conj->child_filters.push_back(std::move(it->second));
+            it->second = std::move(conj);
+        }
+        it->second->Cast<ConjunctionAndFilter>().child_filters.push_back(std::move(filter));
+    }
+};
+
 struct TableFunctionBindInput {
     vector<Value> &inputs;
     named_parameter_map_t &named_parameters;
@@ -319,6 +415,9 @@ struct TableFunctionBindInput {
 struct TableFunctionInitInput {
     optional_ptr<const FunctionData> bind_data;
     const vector<column_t> &column_ids;
+    // filter_prune: positions in column_ids the output chunk holds (empty = all)
+    vector<idx_t> projection_ids = {};
+    optional_ptr<TableFilterSet> filters = nullptr;
 };
 struct TableFunctionInput {
     optional_ptr<const FunctionData> bind_data;

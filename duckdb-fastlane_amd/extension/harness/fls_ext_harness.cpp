@@ -8,6 +8,8 @@
 // reference test uses (COUNT, LIMIT, LIKE, LENGTH) are applied by the tests on
 // the returned rows.
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -84,6 +86,106 @@ TableFunction *lookup(fls_ext_db *d, Query &q) {
     throw BinderException("No function matches the given name and argument types '" + sig + ")'");
 }
 
+// ---- WHERE clauses handed to the scan as DuckDB TableFilters --------------
+// A filter is (table column, expression text) with the expression one of
+//   "<op> v"  (op = <> < <= > >=)     -> ConstantFilter
+//   "IN v1|v2|..."                     -> InFilter
+//   "OR <op> v|<op> v|..."             -> ConjunctionOrFilter of ConstantFilters
+//   "ISNULL" / "ISNOTNULL"             -> IsNullFilter / IsNotNullFilter
+//   "OPT <expr>"                       -> OptionalFilter(<expr>)
+// Several filters on one column AND together (TableFilterSet::PushFilter).
+// Constants are cast to the column type, as DuckDB's binder does before
+// pushing a comparison down: DATE 'YYYY-MM-DD', DECIMAL '12.34', 'nan'.
+struct FilterSpec {
+    int col;
+    std::string expr;
+};
+
+int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const unsigned yoe = (unsigned)(y - era * 400);
+    const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + (int64_t)doe - 719468;
+}
+
+Value parse_constant(const std::string &t, const LogicalType &type) {
+    switch (type.id()) {
+    case LogicalTypeId::TINYINT: return Value::TINYINT((int8_t)std::stoll(t));
+    case LogicalTypeId::SMALLINT: return Value::SMALLINT((int16_t)std::stoll(t));
+    case LogicalTypeId::INTEGER: return Value::INTEGER((int32_t)std::stoll(t));
+    case LogicalTypeId::BIGINT: return Value::BIGINT(std::stoll(t));
+    case LogicalTypeId::UTINYINT: return Value::UTINYINT((uint8_t)std::stoull(t));
+    case LogicalTypeId::USMALLINT: return Value::USMALLINT((uint16_t)std::stoull(t));
+    case LogicalTypeId::UINTEGER: return Value::UINTEGER((uint32_t)std::stoull(t));
+    case LogicalTypeId::UBIGINT: return Value::UBIGINT(std::stoull(t));
+    case LogicalTypeId::DATE: {
+        int y, m, d;
+        if (sscanf(t.c_str(), "%d-%d-%d", &y, &m, &d) == 3) return Value::DATE(date_t{(int32_t)days_from_civil(y, m, d)});
+        return Value::DATE(date_t{(int32_t)std::stoll(t)});
+    }
+    case LogicalTypeId::DECIMAL: {
+        // exact decimal text -> scaled integer (rounded half away from zero)
+        const bool neg = !t.empty() && t[0] == '-';
+        std::string digits = neg ? t.substr(1) : t;
+        const size_t dot = digits.find('.');
+        std::string ip = dot == std::string::npos ? digits : digits.substr(0, dot);
+        std::string fp = dot == std::string::npos ? "" : digits.substr(dot + 1);
+        const unsigned sc = type.Scale();
+        bool up = fp.size() > sc && fp[sc] >= '5';
+        fp.resize(sc, '0');
+        int64_t v = std::stoll((ip.empty() ? "0" : ip) + fp) + (up ? 1 : 0);
+        return Value::DECIMAL(neg ? -v : v, type.Width(), type.Scale());
+    }
+    case LogicalTypeId::FLOAT: return Value::FLOAT(std::strtof(t.c_str(), nullptr));
+    case LogicalTypeId::DOUBLE: return Value::DOUBLE(std::strtod(t.c_str(), nullptr));
+    case LogicalTypeId::VARCHAR: return Value(t);
+    default: throw NotImplementedException("harness: no constant for " + type.ToString());
+    }
+}
+
+ExpressionType parse_op(const std::string &op) {
+    if (op == "=") return ExpressionType::COMPARE_EQUAL;
+    if (op == "<>" || op == "!=") return ExpressionType::COMPARE_NOTEQUAL;
+    if (op == "<") return ExpressionType::COMPARE_LESSTHAN;
+    if (op == "<=") return ExpressionType::COMPARE_LESSTHANOREQUALTO;
+    if (op == ">") return ExpressionType::COMPARE_GREATERTHAN;
+    if (op == ">=") return ExpressionType::COMPARE_GREATERTHANOREQUALTO;
+    throw BinderException("harness: unknown comparison " + op);
+}
+
+std::vector<std::string> split(const std::string &s, char sep) {
+    std::vector<std::string> out;
+    size_t a = 0;
+    while (true) {
+        const size_t b = s.find(sep, a);
+        out.push_back(s.substr(a, b == std::string::npos ? std::string::npos : b - a));
+        if (b == std::string::npos) return out;
+        a = b + 1;
+    }
+}
+
+unique_ptr<TableFilter> parse_filter(const std::string &e, const LogicalType &type) {
+    auto head = [&](const char *kw) { return e.rfind(kw, 0) == 0; };
+    if (e == "ISNULL") return make_uniq<IsNullFilter>();
+    if (e == "ISNOTNULL") return make_uniq<IsNotNullFilter>();
+    if (head("OPT ")) return make_uniq<OptionalFilter>(parse_filter(e.substr(4), type));
+    if (head("IN ")) {
+        vector<Value> vals;
+        for (auto &v : split(e.substr(3), '|')) vals.push_back(parse_constant(v, type));
+        return make_uniq<InFilter>(std::move(vals));
+    }
+    if (head("OR ")) {
+        auto f = make_uniq<ConjunctionOrFilter>();
+        for (auto &part : split(e.substr(3), '|')) f->child_filters.push_back(parse_filter(part, type));
+        return std::move(f);
+    }
+    const size_t sp = e.find(' ');
+    if (sp == std::string::npos) throw BinderException("harness: bad filter '" + e + "'");
+    return make_uniq<ConstantFilter>(parse_op(e.substr(0, sp)), parse_constant(e.substr(sp + 1), type));
+}
+
 // run the query; sink(batch_index, chunk, pick, n) receives every produced
 // chunk.  With nthreads > 1 the scan runs the way DuckDB's pipeline executor
 // runs a parallel source: min(nthreads, MaxThreads()) threads, each with its own
@@ -91,7 +193,8 @@ TableFunction *lookup(fls_ext_db *d, Query &q) {
 // concurrently and orders results by batch index itself.
 template <class Sink>
 void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limit, std::vector<std::string> &names,
-             std::vector<LogicalType> &types, Sink sink, int nthreads = 1) {
+             std::vector<LogicalType> &types, Sink sink, int nthreads = 1,
+             const std::vector<FilterSpec> &where = {}) {
     TableFunction *f = lookup(d, q);
     named_parameter_map_t named;
     TableFunctionBindInput bin{q.args, named};
@@ -114,10 +217,30 @@ void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limi
         fn_ids.clear();
         for (column_t c = 0; c < rtypes.size(); ++c) fn_ids.push_back(c);
     }
-    TableFunctionInitInput iin{bind.get(), fn_ids};
+    // WHERE: filter columns join column_ids (after the projected ones); with
+    // filter_prune the chunk holds only the projected positions
+    TableFilterSet filter_set;
+    vector<idx_t> projection_ids;
+    if (!where.empty()) {
+        if (!f->filter_pushdown) throw NotImplementedException("harness: " + q.fn + " takes no filters");
+        const size_t nproj_ids = fn_ids.size();
+        for (auto &w : where) {
+            if (w.col < 0 || (size_t)w.col >= rtypes.size()) throw BinderException("filter column out of range");
+            size_t pos = 0;
+            while (pos < fn_ids.size() && fn_ids[pos] != (column_t)w.col) ++pos;
+            if (pos == fn_ids.size()) fn_ids.push_back((column_t)w.col);
+            filter_set.PushFilter(pos, parse_filter(w.expr, rtypes[w.col]));
+        }
+        if (f->filter_prune && fn_ids.size() > nproj_ids)
+            for (idx_t i = 0; i < nproj_ids; ++i) projection_ids.push_back(i);
+    }
+    TableFunctionInitInput iin{bind.get(), fn_ids, projection_ids, where.empty() ? nullptr : &filter_set};
     auto gstate = f->init_global ? f->init_global(d->ctx, iin) : nullptr;
     vector<LogicalType> chunk_types;
-    for (auto id : fn_ids) chunk_types.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? LogicalType::BIGINT : rtypes[id]);
+    for (size_t i = 0; i < (projection_ids.empty() ? fn_ids.size() : projection_ids.size()); ++i) {
+        const column_t id = fn_ids[projection_ids.empty() ? i : projection_ids[i]];
+        chunk_types.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? LogicalType::BIGINT : rtypes[id]);
+    }
     for (auto id : ids) {
         names.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? "rowid" : rnames[id]);
         types.push_back(id == COLUMN_IDENTIFIER_ROW_ID ? LogicalType::BIGINT : rtypes[id]);
@@ -218,9 +341,26 @@ void fls_ext_close(fls_ext_db *d) { delete d; }
 
 int fls_ext_has_function(fls_ext_db *d, const char *name) { return d && d->db.table_functions.count(name) ? 1 : 0; }
 
+static std::vector<FilterSpec> make_where(const int *fcols, const char *const *fexprs, int nfilters) {
+    std::vector<FilterSpec> w;
+    for (int i = 0; i < nfilters; ++i) w.push_back(FilterSpec{fcols[i], fexprs[i] ? fexprs[i] : ""});
+    return w;
+}
+
+int fls_ext_query_where(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list,
+                        const int *proj, int nproj, const int *fcols, const char *const *fexprs, int nfilters,
+                        int64_t limit, int nthreads, fls_ext_result **out);
+
 int fls_ext_query_mt(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list, const int *proj,
                      int nproj, int64_t limit, int nthreads, fls_ext_result **out) {
+    return fls_ext_query_where(d, fn, args, nargs, as_list, proj, nproj, nullptr, nullptr, 0, limit, nthreads, out);
+}
+
+int fls_ext_query_where(fls_ext_db *d, const char *fn, const char *const *args, int nargs, int as_list,
+                        const int *proj, int nproj, const int *fcols, const char *const *fexprs, int nfilters,
+                        int64_t limit, int nthreads, fls_ext_result **out) {
     try {
+        const std::vector<FilterSpec> where = make_where(fcols, fexprs, nfilters);
         Query q = make_query(d, fn, args, nargs, as_list);
         auto *r = new fls_ext_result();
         std::unique_ptr<fls_ext_result> guard(r);
@@ -247,7 +387,7 @@ int fls_ext_query_mt(fls_ext_db *d, const char *fn, const char *const *args, int
             Part &p = parts[batch];
             for (auto &x : local.cells) p.cells.push_back(std::move(x));
             for (auto &x : local.valid) p.valid.push_back(std::move(x));
-        }, nthreads);
+        }, nthreads, where);
         for (auto &b : parts) {
             for (auto &x : b.second.cells) r->cells.push_back(std::move(x));
             for (auto &x : b.second.valid) r->valid.push_back(std::move(x));
@@ -329,9 +469,20 @@ ChunkHash hash_chunk(DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
 }
 }  // namespace
 
+extern "C" int fls_ext_scan_count_where(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
+                                        const int *fcols, const char *const *fexprs, int nfilters, int nthreads,
+                                        uint64_t *rows, uint64_t *checksum, double *seconds);
+
 extern "C" int fls_ext_scan_count_mt(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
                                      int nthreads, uint64_t *rows, uint64_t *checksum, double *seconds) {
+    return fls_ext_scan_count_where(d, fn, path, proj, nproj, nullptr, nullptr, 0, nthreads, rows, checksum, seconds);
+}
+
+extern "C" int fls_ext_scan_count_where(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
+                                        const int *fcols, const char *const *fexprs, int nfilters, int nthreads,
+                                        uint64_t *rows, uint64_t *checksum, double *seconds) {
     try {
+        const std::vector<FilterSpec> where = make_where(fcols, fexprs, nfilters);
         const char *args[1] = {path};
         Query q = make_query(d, fn, args, 1, 0);
         std::vector<std::string> names;
@@ -344,7 +495,7 @@ extern "C" int fls_ext_scan_count_mt(fls_ext_db *d, const char *fn, const char *
             ChunkHash h = hash_chunk(c, pick, cnt);
             std::lock_guard<std::mutex> g(mu);
             parts[batch].push_back(std::move(h));
-        }, nthreads);
+        }, nthreads, where);
         *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         uint64_t n = 0;
         std::vector<uint64_t> acc(names.size(), 0);

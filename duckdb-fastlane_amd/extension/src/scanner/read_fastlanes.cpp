@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <mutex>
 
 #include "../../../../include/flsgpu.h"
@@ -26,6 +27,12 @@
 #include "duckdb/parser/expression/constant_expression.hpp"
 #include "duckdb/parser/expression/function_expression.hpp"
 #include "duckdb/parser/tableref/table_function_ref.hpp"
+#include "duckdb/planner/filter/conjunction_filter.hpp"
+#include "duckdb/planner/filter/constant_filter.hpp"
+#include "duckdb/planner/filter/in_filter.hpp"
+#include "duckdb/planner/filter/null_filter.hpp"
+#include "duckdb/planner/filter/optional_filter.hpp"
+#include "duckdb/planner/table_filter.hpp"
 #include "table_function/read_fastlanes.hpp"
 #include "type_mapping.hpp"
 
@@ -57,7 +64,10 @@ struct ReadBindData : public TableFunctionData {
 
 struct ReadGlobalState : public GlobalTableFunctionState {
     vector<column_t> column_ids;
-    std::vector<uint8_t> mask;
+    vector<idx_t> out_ids;               // output column -> position in column_ids
+    std::vector<uint8_t> mask;           // delivered table columns
+    std::vector<fls_predicate> preds;    // pushed-down filter (empty: none)
+    std::deque<string> pred_strs;        // VARCHAR constants the predicates point at
     std::vector<idx_t> rg_base;          // batch index of each file's first row group
     idx_t total_rowgroups = 0;
     std::mutex lock;                     // file advance and row-group claims
@@ -121,13 +131,138 @@ unique_ptr<FunctionData> ReadBind(ClientContext &, TableFunctionBindInput &input
     return std::move(bind);
 }
 
+uint8_t CompareOp(ExpressionType t) {
+    switch (t) {
+    case ExpressionType::COMPARE_EQUAL: return FLS_CMP_EQ;
+    case ExpressionType::COMPARE_NOTEQUAL: return FLS_CMP_NE;
+    case ExpressionType::COMPARE_LESSTHAN: return FLS_CMP_LT;
+    case ExpressionType::COMPARE_LESSTHANOREQUALTO: return FLS_CMP_LE;
+    case ExpressionType::COMPARE_GREATERTHAN: return FLS_CMP_GT;
+    case ExpressionType::COMPARE_GREATERTHANOREQUALTO: return FLS_CMP_GE;
+    default: throw NotImplementedException("read_fastlanes: unsupported comparison in pushed-down filter");
+    }
+}
+
+// `col <op> constant` with the constant in the column's physical type
+fls_predicate MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v, const LogicalType &type,
+                       std::deque<string> &strs) {
+    fls_predicate p;
+    memset(&p, 0, sizeof(p));
+    p.col = col;
+    p.clause = clause;
+    p.op = op;
+    if (v.IsNull()) {  // a comparison with NULL is never true
+        p.op = FLS_CMP_IS_NULL;
+        return p;
+    }
+    switch (type.id()) {
+    case LogicalTypeId::TINYINT: case LogicalTypeId::SMALLINT: case LogicalTypeId::INTEGER:
+    case LogicalTypeId::BIGINT:
+        p.value = (uint64_t)v.GetValue<int64_t>();
+        break;
+    case LogicalTypeId::UTINYINT: case LogicalTypeId::USMALLINT: case LogicalTypeId::UINTEGER:
+    case LogicalTypeId::UBIGINT:
+        p.value = v.GetValue<uint64_t>();
+        break;
+    case LogicalTypeId::DATE:
+        p.value = (uint64_t)(int64_t)v.GetValue<date_t>().days;
+        break;
+    case LogicalTypeId::DECIMAL:  // DuckDB casts the constant to the column's DECIMAL type
+        p.value = (uint64_t)(type.Width() <= 4   ? (int64_t)v.GetValueUnsafe<int16_t>()
+                             : type.Width() <= 9 ? (int64_t)v.GetValueUnsafe<int32_t>()
+                                                 : v.GetValueUnsafe<int64_t>());
+        break;
+    case LogicalTypeId::FLOAT: {
+        const float f = v.GetValue<float>();
+        uint32_t b;
+        memcpy(&b, &f, 4);
+        p.value = b;
+        break;
+    }
+    case LogicalTypeId::DOUBLE: {
+        const double d = v.GetValue<double>();
+        memcpy(&p.value, &d, 8);
+        break;
+    }
+    case LogicalTypeId::VARCHAR:
+        strs.push_back(v.GetValue<string>());
+        p.str = strs.back().data();
+        p.str_len = strs.back().size();
+        break;
+    default: throw NotImplementedException("read_fastlanes: unsupported filter type " + type.ToString());
+    }
+    return p;
+}
+
+// one clause of OR-ed terms (constants, IN lists, IS [NOT] NULL)
+void AddOrTerms(const TableFilter &f, uint32_t col, uint32_t clause, const LogicalType &type,
+                std::vector<fls_predicate> &out, std::deque<string> &strs) {
+    switch (f.filter_type) {
+    case TableFilterType::CONSTANT_COMPARISON: {
+        auto &c = f.Cast<ConstantFilter>();
+        out.push_back(MakeTerm(col, clause, CompareOp(c.comparison_type), c.constant, type, strs));
+        break;
+    }
+    case TableFilterType::IN_FILTER:
+        for (auto &v : f.Cast<InFilter>().values) out.push_back(MakeTerm(col, clause, FLS_CMP_EQ, v, type, strs));
+        break;
+    case TableFilterType::IS_NULL:
+    case TableFilterType::IS_NOT_NULL: {
+        fls_predicate p;
+        memset(&p, 0, sizeof(p));
+        p.col = col;
+        p.clause = clause;
+        p.op = f.filter_type == TableFilterType::IS_NULL ? FLS_CMP_IS_NULL : FLS_CMP_IS_NOT_NULL;
+        out.push_back(p);
+        break;
+    }
+    case TableFilterType::CONJUNCTION_OR:
+        for (auto &ch : f.Cast<ConjunctionOrFilter>().child_filters) AddOrTerms(*ch, col, clause, type, out, strs);
+        break;
+    default: throw NotImplementedException("read_fastlanes: unsupported filter inside OR");
+    }
+}
+
+// TableFilter on one column -> clauses (AND of ORs)
+void AddFilter(const TableFilter &f, uint32_t col, const LogicalType &type, uint32_t &clause,
+               std::vector<fls_predicate> &out, std::deque<string> &strs) {
+    switch (f.filter_type) {
+    case TableFilterType::CONJUNCTION_AND:
+        for (auto &ch : f.Cast<ConjunctionAndFilter>().child_filters) AddFilter(*ch, col, type, clause, out, strs);
+        break;
+    case TableFilterType::OPTIONAL_FILTER:  // optional by definition: DuckDB re-checks it above the scan
+        break;
+    case TableFilterType::CONSTANT_COMPARISON: case TableFilterType::IN_FILTER: case TableFilterType::IS_NULL:
+    case TableFilterType::IS_NOT_NULL: case TableFilterType::CONJUNCTION_OR:
+        AddOrTerms(f, col, clause++, type, out, strs);
+        break;
+    default: throw NotImplementedException("read_fastlanes: unsupported pushed-down filter type");
+    }
+}
+
 unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFunctionInitInput &input) {
     const auto &bind = input.bind_data->Cast<ReadBindData>();
     auto state = make_uniq<ReadGlobalState>();
     state->column_ids = input.column_ids;
+    if (input.projection_ids.empty()) {
+        for (idx_t i = 0; i < input.column_ids.size(); ++i) state->out_ids.push_back(i);
+    } else {
+        state->out_ids = input.projection_ids;
+    }
     state->mask.assign(bind.cols.size(), 0);
-    for (auto id : state->column_ids)
+    for (auto pos : state->out_ids) {
+        const column_t id = state->column_ids[pos];
         if (id != COLUMN_IDENTIFIER_ROW_ID && id < bind.cols.size()) state->mask[id] = 1;
+    }
+    if (input.filters) {
+        uint32_t clause = 0;
+        for (auto &entry : input.filters->filters) {
+            const column_t id = state->column_ids[entry.first];
+            if (id == COLUMN_IDENTIFIER_ROW_ID || id >= bind.cols.size())
+                throw NotImplementedException("read_fastlanes: filter on a non-table column");
+            AddFilter(*entry.second, (uint32_t)id, bind.types[id], clause, state->preds, state->pred_strs);
+        }
+    }
     // fail early on unreadable or schema-incompatible files
     for (auto &f : bind.files) {
         OpenTable t;
@@ -166,6 +301,8 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
             auto t = std::make_shared<OpenTable>();
             if (!t->open(bind.files[g.file_idx]))
                 throw IOException("Failed to open FastLanes file: " + bind.files[g.file_idx]);
+            if (fls_scan_filter(t->table, g.preds.data(), (uint32_t)g.preds.size()) != 0)
+                throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             if (fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             g.cur = std::move(t);
@@ -189,21 +326,38 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
     auto &g = data.global_state->Cast<ReadGlobalState>();
     auto &l = data.local_state->Cast<ReadLocalState>();
     output.Reset();
-    if (!(l.have_rg && l.rg_pos < l.rg.nrows) && !NextRowGroup(bind, g, l)) {
-        output.SetCardinality(0);
-        return;
+    // (a filtered row group can deliver no rows)
+    while (!(l.have_rg && l.rg_pos < l.rg.nrows)) {
+        if (!NextRowGroup(bind, g, l)) {
+            output.SetCardinality(0);
+            return;
+        }
     }
     const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, l.rg.nrows - l.rg_pos);
     for (idx_t j = 0; j < output.ColumnCount(); ++j) {
-        const column_t id = j < g.column_ids.size() ? g.column_ids[j] : j;
+        const column_t id = j < g.out_ids.size() ? g.column_ids[g.out_ids[j]] : j;
         Vector &vec = output.data[j];
         if (id == COLUMN_IDENTIFIER_ROW_ID) {
             int64_t *rid = FlatVector::GetData<int64_t>(vec);
-            for (idx_t i = 0; i < n; ++i) rid[i] = (int64_t)(l.rg.first_row + l.rg_pos + i);
+            for (idx_t i = 0; i < n; ++i)
+                rid[i] = (int64_t)(l.rg.first_row + (l.rg.sel ? l.rg.sel[l.rg_pos + i] : l.rg_pos + i));
             continue;
         }
         const idx_t ob = bind.cols[id].out_bytes;
-        memcpy(vec.GetData(), (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob, n * ob);
+        const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
+        const idx_t phys = vec.GetType().PhysicalSize();
+        if (phys == ob) {
+            memcpy(vec.GetData(), src, n * ob);
+        } else {  // DECIMAL(w<=9): the int64 scaled value narrowed to DuckDB's physical width
+            const int64_t *v = (const int64_t *)src;
+            if (phys == 4) {
+                int32_t *d = FlatVector::GetData<int32_t>(vec);
+                for (idx_t i = 0; i < n; ++i) d[i] = (int32_t)v[i];
+            } else {
+                int16_t *d = FlatVector::GetData<int16_t>(vec);
+                for (idx_t i = 0; i < n; ++i) d[i] = (int16_t)v[i];
+            }
+        }
     }
     l.rg_pos += n;
     output.SetCardinality(n);
@@ -231,8 +385,8 @@ TableFunction ReadFastlanesFunction() {
     TableFunction fn("read_fastlanes", {LogicalType::VARCHAR}, ReadScan, ReadBind, ReadInitGlobal, ReadInitLocal);
     fn.get_partition_data = ReadPartitionData;
     fn.projection_pushdown = true;
-    fn.filter_pushdown = false;
-    fn.filter_prune = false;
+    fn.filter_pushdown = true;
+    fn.filter_prune = true;
     return fn;
 }
 

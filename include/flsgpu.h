@@ -65,12 +65,37 @@ typedef struct fls_column_info {
 
 typedef struct fls_rowgroup {
     uint32_t rowgroup;            /* row-group index within the table */
-    uint32_t nrows;
-    uint64_t first_row;           /* global row index of the first row */
+    uint32_t nrows;               /* rows delivered (after a pushed-down filter) */
+    uint64_t first_row;           /* global row index of the row group's first row */
     uint32_t ncols;
     const void *const *columns;   /* ncols pointers into pinned host memory;
                                      NULL for columns not selected */
+    uint32_t nrows_scanned;       /* rows of the row group */
+    const uint32_t *sel;          /* filtered scan: the delivered rows' indices
+                                     within the row group (ascending); NULL
+                                     when every row is delivered */
 } fls_rowgroup;
+
+/* Pushed-down filter term: `column <op> constant` (DuckDB TableFilterSet:
+ * ConstantFilter / IsNullFilter / IsNotNullFilter; ConjunctionOr and InFilter
+ * become several terms of one clause, ConjunctionAnd several clauses).
+ * Terms with equal `clause` are OR-ed, clauses are AND-ed. */
+typedef enum fls_cmp {
+    FLS_CMP_EQ = 0, FLS_CMP_NE = 1, FLS_CMP_LT = 2, FLS_CMP_LE = 3, FLS_CMP_GT = 4, FLS_CMP_GE = 5,
+    FLS_CMP_IS_NULL = 6, FLS_CMP_IS_NOT_NULL = 7
+} fls_cmp;
+typedef struct fls_predicate {
+    uint32_t col;                 /* table column */
+    uint32_t clause;
+    uint8_t op;                   /* fls_cmp */
+    uint8_t pad[7];
+    uint64_t value;               /* constant in the column's physical type:
+                                     signed ints / DATE days / DECIMAL scaled as
+                                     int64, unsigned as uint64, FLOAT as IEEE
+                                     binary32 bits (low 32), DOUBLE binary64 bits */
+    const char *str;              /* VARCHAR constant (copied) */
+    uint64_t str_len;
+} fls_predicate;
 
 typedef struct fls_decode_stats {
     double kernel_ms;             /* duration of the last decode launch (HIP events) */
@@ -119,6 +144,21 @@ int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uin
 /* 1 = a row group was delivered into *out, 0 = end of scan, <0 = error.
  * The previous row group's buffers are released by the call. */
 int fls_scan_next(fls_table *t, fls_rowgroup *out);
+/* Filter for the following fls_scan_begin calls on this table (n = 0
+ * clears).  The scan then skips row groups whose zone maps / dictionaries
+ * rule every row out, evaluates the filter per row on the GPU and delivers
+ * only qualifying rows (fls_rowgroup.nrows / sel), in row order.  The
+ * filter's columns are decoded whether or not col_mask delivers them. */
+int fls_scan_filter(fls_table *t, const fls_predicate *preds, uint32_t n);
+/* Row groups the current scan skipped by zone maps / dictionaries. */
+int fls_scan_pruned(const fls_table *t);
+/* Zone map of column col in row group rg: 1 and *min / *max (int64, uint64
+ * or double bits by column type, see fls_predicate.value; FLOAT widened to
+ * double) when present, 0 when the file has none for it. */
+int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *min, uint64_t *max, uint32_t *flags);
+/* May a row of row group rg satisfy the filter?  (1 yes / 0 no; host only) */
+int fls_rowgroup_may_match(const fls_table *t, uint32_t rg, const fls_predicate *preds, uint32_t n);
+
 /* Thread-safe form for parallel consumers: claims the next row group in order
  * (1 = delivered, 0 = end, <0 = error); its buffers stay valid until
  * fls_scan_release(t, out->rowgroup).  A consumer must release what it holds

@@ -43,20 +43,32 @@ class Ext:
     def has_function(self, name: str) -> bool:
         return bool(self.lib.fls_ext_has_function(self.db, name.encode()))
 
-    def query(self, fn, *args, as_list=False, raw=False, proj=None, limit=-1, threads=1):
+    @staticmethod
+    def _where(where):
+        """where: [(table column, expr)], expr per fls_ext_harness.cpp (e.g.
+        ">= 1994-01-01", "IN AIR|MAIL", "OR < 3|> 40", "ISNULL", "OPT = 5")."""
+        where = where or []
+        cols = (C.c_int * max(1, len(where)))(*[c for c, _ in where])
+        exprs = (C.c_char_p * max(1, len(where)))(*[e.encode() for _, e in where])
+        return cols, exprs, len(where)
+
+    def query(self, fn, *args, as_list=False, raw=False, proj=None, limit=-1, threads=1, where=None):
         """Returns (names, types, rows) with rows as lists of str/None.
         fn=None resolves args[0] through the replacement scans.
-        An int argument is passed as an INTEGER value (type errors)."""
+        An int argument is passed as an INTEGER value (type errors).
+        where: WHERE clauses the executor pushes into the scan as TableFilters."""
         a = (C.c_char_p * max(1, len(args)))(*[(b"\x01%d" % x) if isinstance(x, int) else str(x).encode()
                                                for x in args])
         p = (C.c_int * len(proj))(*proj) if proj else None
         out = C.c_void_p()
         mode = 2 if raw else int(as_list)
-        self.lib.fls_ext_query_mt.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_int, C.c_int,
-                                              C.POINTER(C.c_int), C.c_int, C.c_int64, C.c_int,
-                                              C.POINTER(C.c_void_p)]
-        rc = self.lib.fls_ext_query_mt(self.db, fn.encode() if fn else None, a, len(args), mode, p,
-                                       len(proj) if proj else 0, limit, threads, C.byref(out))
+        wc, we, wn = self._where(where)
+        self.lib.fls_ext_query_where.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                                 C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int),
+                                                 C.POINTER(C.c_char_p), C.c_int, C.c_int64, C.c_int,
+                                                 C.POINTER(C.c_void_p)]
+        rc = self.lib.fls_ext_query_where(self.db, fn.encode() if fn else None, a, len(args), mode, p,
+                                          len(proj) if proj else 0, wc, we, wn, limit, threads, C.byref(out))
         if rc != 0:
             raise ExtError(self.lib.fls_ext_last_error().decode())
         r = out.value
@@ -75,16 +87,18 @@ class Ext:
         finally:
             self.lib.fls_ext_result_free(r)
 
-    def scan_count(self, fn, path, proj=None, threads=1):
+    def scan_count(self, fn, path, proj=None, threads=1, where=None):
         """(rows, checksum, seconds); the checksum depends only on the result
         rows in order (not on chunking or the number of scan threads)."""
         p = (C.c_int * len(proj))(*proj) if proj else None
         rows, h, sec = C.c_uint64(), C.c_uint64(), C.c_double()
-        self.lib.fls_ext_scan_count_mt.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.c_int,
-                                                   C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
-                                                   C.POINTER(C.c_double)]
-        rc = self.lib.fls_ext_scan_count_mt(self.db, fn.encode(), str(path).encode(), p, len(proj) if proj else 0,
-                                            threads, C.byref(rows), C.byref(h), C.byref(sec))
+        wc, we, wn = self._where(where)
+        self.lib.fls_ext_scan_count_where.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int),
+                                                      C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_char_p), C.c_int,
+                                                      C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                                      C.POINTER(C.c_double)]
+        rc = self.lib.fls_ext_scan_count_where(self.db, fn.encode(), str(path).encode(), p, len(proj) if proj else 0,
+                                               wc, we, wn, threads, C.byref(rows), C.byref(h), C.byref(sec))
         if rc != 0:
             raise ExtError(self.lib.fls_ext_last_error().decode())
         return rows.value, h.value, sec.value

@@ -119,3 +119,48 @@ def special_doubles(n, rng):
     pool = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 1.7976931348623157e308,
                      2.2250738585072014e-308, 1e300, 0.1, 1 / 3])
     return pool[rng.integers(0, len(pool), n)]
+
+
+# ---- pushed-down filters: numpy restatement of DuckDB comparison semantics ----
+def _cmp(a, v):
+    """-1/0/1 of a (numpy column or list of bytes) against constant v, with
+    DuckDB's float order (NaN == NaN, NaN above every number, -0 == 0)."""
+    if isinstance(a, list):
+        return np.array([(x > v) - (x < v) for x in a], dtype=np.int8)
+    if a.dtype.kind == "f":
+        v = np.float64(v)
+        an = np.isnan(a)
+        if np.isnan(v):
+            return np.where(an, 0, -1).astype(np.int8)
+        a64 = a.astype(np.float64)
+        c = (a64 > v).astype(np.int8) - (a64 < v).astype(np.int8)
+        return np.where(an, 1, c).astype(np.int8)
+    # integers: exact (object arithmetic for 64-bit unsigned / mixed signs)
+    a = a.astype(np.int64) if a.dtype.kind == "i" else a.astype(np.uint64)
+    if a.dtype == np.uint64 and v < 0:
+        return np.ones(len(a), np.int8)
+    vv = a.dtype.type(v)
+    return (a > vv).astype(np.int8) - (a < vv).astype(np.int8)
+
+
+def filter_mask(cols: dict, terms, n: int) -> np.ndarray:
+    """Rows satisfying the conjunction of clauses; terms = (col, op, value[, clause])
+    as in Table.scan_filtered.  cols[c] = numpy values or list of bytes."""
+    ops = {"=": lambda c: c == 0, "!=": lambda c: c != 0, "<": lambda c: c < 0, "<=": lambda c: c <= 0,
+           ">": lambda c: c > 0, ">=": lambda c: c >= 0}
+    clauses = {}
+    for i, t in enumerate(terms):
+        clauses.setdefault(t[3] if len(t) > 3 else 1000000 + i, []).append(t)
+    out = np.ones(n, dtype=bool)
+    for cl in clauses.values():
+        acc = np.zeros(n, dtype=bool)
+        for col, op, val, *_ in cl:
+            if op == "is_null":
+                continue
+            if op == "is_not_null":
+                acc[:] = True
+                continue
+            v = val.encode() if isinstance(val, str) else val
+            acc |= ops[op](_cmp(cols[col], v))
+        out &= acc
+    return out
