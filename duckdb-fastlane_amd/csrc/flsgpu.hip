@@ -9,7 +9,11 @@
 //     GPUs (no collectives: row groups are independent); per
 //     GPU a two-slot pipeline H2D(compressed batch) -> decode -> D2H(pinned)
 //     runs ahead of the consumer (DuckDB's scan thread).
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -161,6 +165,7 @@ struct Slot {                       // one batch of row groups in flight
     PinBuf<DevChunk> h_chunks;
     DevBuf<DevChunk> d_chunks;
     DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch
+    PinBuf<uint8_t> h_stage;        // pinned bounce buffer when the image cannot be pinned
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
@@ -227,6 +232,9 @@ struct fls_table {
     FileMeta meta;
     std::vector<std::string> names;
     bool registered = false;        // img pinned with hipHostRegister
+    bool pin_tried = false;
+    void *map = nullptr;            // fls_read_fls: the file, mapped read-only
+    size_t map_len = 0;
 
     // device-resident mode
     DeviceShard shard;
@@ -385,6 +393,7 @@ fls_table::~fls_table() {
             if (d.stream) hipStreamDestroy(d.stream);
         }
     if (registered) hipHostUnregister((void *)img);
+    if (map) munmap(map, map_len);
 }
 
 // ------------------------------------------------------------------------------
@@ -518,10 +527,13 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         HIP_TRY(hipMemsetAsync(d.err.p, 0, sizeof(uint32_t), d.stream));
         HIP_TRY(hipStreamSynchronize(d.stream));
     }
-    // pin the file image once so batch uploads are true async DMA
-    if (!t->registered && t->len > 0) {
+    // pin the file image once so batch uploads are true async DMA; where that
+    // is refused (e.g. a read-only file mapping) batches are staged through a
+    // pinned buffer per slot
+    if (!t->pin_tried && t->len > 0) {
+        t->pin_tried = true;
         if (hipHostRegister((void *)t->img, t->len, hipHostRegisterDefault) == hipSuccess) t->registered = true;
-        else (void)hipGetLastError();  // fall back to staged (pageable) copies
+        else (void)hipGetLastError();
     }
     s.active = true;
     return 0;
@@ -610,7 +622,13 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     rg_byte_range(t->meta, sl.rg0, sl.rg0 + sl.nrg, lo, hi);
     HIP_TRY(sl.d_in.alloc(d.dev, hi - lo));
     sl.in_base = lo;
-    HIP_TRY(hipMemcpyAsync(sl.d_in.p, t->img + lo, hi - lo, hipMemcpyHostToDevice, sl.stream));
+    const uint8_t *src = t->img + lo;
+    if (!t->registered) {
+        HIP_TRY(sl.h_stage.alloc(hi - lo));
+        memcpy(sl.h_stage.p, src, hi - lo);
+        src = sl.h_stage.p;
+    }
+    HIP_TRY(hipMemcpyAsync(sl.d_in.p, src, hi - lo, hipMemcpyHostToDevice, sl.stream));
     // 2. decode into the slot's device columns (FSST columns also into a heap)
     const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
     sl.heap_bytes.assign(ncols, 0);
@@ -888,18 +906,37 @@ void fls_disconnect(fls_connection *conn) { delete conn; }
 
 int fls_read_fls(fls_connection *conn, const char *path, fls_table **out) {
     if (!conn || !path || !out) return fail(FLS_ERR_ARG, "fls_read_fls: NULL argument");
-    FILE *f = fopen(path, "rb");
-    if (!f) return fail(FLS_ERR_IO, "Failed to open FastLanes file: %s", path);
+    // map the file: opening reads only the footer and the chunk headers it
+    // validates (DuckDB opens a file at bind and at init), the scan streams
+    // the row groups it keeps
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return fail(FLS_ERR_IO, "Failed to open FastLanes file: %s", path);
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+        close(fd);
+        return fail(FLS_ERR_IO, "Failed to open FastLanes file: %s", path);
+    }
     auto *t = new fls_table();
-    fseek(f, 0, SEEK_END);
-    long n = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    if (n < 0) { fclose(f); delete t; return fail(FLS_ERR_IO, "Failed to open FastLanes file: %s", path); }
-    t->owned.resize((size_t)n);
-    size_t rd = n ? fread(t->owned.data(), 1, (size_t)n, f) : 0;
-    fclose(f);
-    if (rd != (size_t)n) { delete t; return fail(FLS_ERR_IO, "short read of %s", path); }
-    t->img = t->owned.data();
+    const size_t n = (size_t)st.st_size;
+    if (n > 0) {
+        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) {  // e.g. a pipe-backed or special file system: read it
+            t->owned.resize(n);
+            size_t got = 0;
+            while (got < n) {
+                const ssize_t r = pread(fd, t->owned.data() + got, n - got, (off_t)got);
+                if (r <= 0) break;
+                got += (size_t)r;
+            }
+            if (got != n) { close(fd); delete t; return fail(FLS_ERR_IO, "short read of %s", path); }
+            t->img = t->owned.data();
+        } else {
+            t->map = m;
+            t->map_len = n;
+            t->img = (const uint8_t *)m;
+        }
+    }
+    close(fd);
     t->len = (uint64_t)n;
     return open_common(conn, t, out);
 }

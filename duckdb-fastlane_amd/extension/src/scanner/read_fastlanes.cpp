@@ -69,6 +69,7 @@ struct ReadGlobalState : public GlobalTableFunctionState {
     std::vector<fls_predicate> preds;    // pushed-down filter (empty: none)
     std::deque<string> pred_strs;        // VARCHAR constants the predicates point at
     std::vector<idx_t> rg_base;          // batch index of each file's first row group
+    std::vector<std::shared_ptr<OpenTable>> tables;  // opened (mapped) at init, scanned in order
     idx_t total_rowgroups = 0;
     std::mutex lock;                     // file advance and row-group claims
     idx_t file_idx = 0;
@@ -265,17 +266,18 @@ unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFuncti
     }
     // fail early on unreadable or schema-incompatible files
     for (auto &f : bind.files) {
-        OpenTable t;
-        if (!t.open(f)) throw IOException("Failed to open FastLanes file: " + f);
-        bool same = fls_table_ncols(t.table) == bind.cols.size();
+        auto t = std::make_shared<OpenTable>();
+        if (!t->open(f)) throw IOException("Failed to open FastLanes file: " + f);
+        bool same = fls_table_ncols(t->table) == bind.cols.size();
         for (uint32_t c = 0; same && c < bind.cols.size(); ++c) {
             fls_column_info ci;
-            fls_table_column(t.table, c, &ci);
+            fls_table_column(t->table, c, &ci);
             same = ci.type == bind.cols[c].type && ci.width == bind.cols[c].width && ci.scale == bind.cols[c].scale;
         }
         if (!same) throw IOException("FastLanes file " + f + " does not match the schema of " + bind.files[0]);
         state->rg_base.push_back(state->total_rowgroups);
-        state->total_rowgroups += fls_table_nrowgroups(t.table);
+        state->total_rowgroups += fls_table_nrowgroups(t->table);
+        state->tables.push_back(std::move(t));
     }
     return std::move(state);
 }
@@ -298,9 +300,7 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
     while (true) {
         if (!g.cur) {
             if (g.file_idx >= bind.files.size()) return false;
-            auto t = std::make_shared<OpenTable>();
-            if (!t->open(bind.files[g.file_idx]))
-                throw IOException("Failed to open FastLanes file: " + bind.files[g.file_idx]);
+            auto t = std::move(g.tables[g.file_idx]);  // opened by InitGlobal
             if (fls_scan_filter(t->table, g.preds.data(), (uint32_t)g.preds.size()) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             if (fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
