@@ -663,15 +663,32 @@ __device__ __forceinline__ void call_dict(const DevChunk *c, uint32_t lp, uint32
     else call<PathDict<OB, false>>(c, lp, lv, vb, err);
 }
 
-__global__ __launch_bounds__(256, 4) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+#ifndef FLS_WAVES_PER_SIMD
+#define FLS_WAVES_PER_SIMD 4
+#endif
+// Next chunk of this wave: from the launch's work queue (one atomic per chunk,
+// lane 0, broadcast) when there is one -- chunks are then taken in the host's
+// largest-first order, so the launch ends on small chunks -- else grid-stride.
+// The first chunk of every wave is static (no burst of same-address atomics
+// at launch); the queue hands out the chunks after the grid's first round.
+__device__ __forceinline__ uint32_t next_chunk(uint32_t *queue, uint32_t prev, uint32_t first, uint32_t stride) {
+    if (prev == UINT32_MAX) return first;
+    if (!queue) return prev + stride;
+    uint32_t ci = 0;
+    if (__lane_id() == 0) ci = atomicAdd(queue, 1u);
+    return stride + uni(ci);
+}
+
+__global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                         uint32_t *__restrict__ err, uint32_t p_bytes,
-                                                        uint32_t v_bytes) {
+                                                        uint32_t v_bytes, uint32_t *__restrict__ queue) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     const uint32_t w = uni(threadIdx.x >> 6);
     const uint32_t lp = (uint32_t)(size_t)((lu8 *)lds_raw + w * (p_bytes + v_bytes));
     const uint32_t lv = lp + p_bytes;
-    const uint32_t stride = gridDim.x * kWaves;
-    for (uint32_t ci = blockIdx.x * kWaves + w; ci < nchunks; ci += stride) {
+    const uint32_t stride = gridDim.x * kWaves, first = blockIdx.x * kWaves + w;
+    for (uint32_t ci = next_chunk(queue, UINT32_MAX, first, stride); ci < nchunks;
+         ci = next_chunk(queue, ci, first, stride)) {
         const DevChunk *cg = chunks + ci;
         const FLS_GLOBAL DevChunk *c = gptr(cg);
         const uint32_t nvec = c->nvec, dc = c->dict_count;
@@ -736,12 +753,16 @@ int decode_grid_size(uint32_t shmem_per_block) {
 }
 
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
-                         hipStream_t stream) {
+                         hipStream_t stream, uint32_t *d_queue) {
     if (nchunks == 0) return hipSuccess;
     const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
     const int grid = std::min<int>(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), (nchunks + kWaves - 1) / kWaves);
+    if (d_queue) {
+        const hipError_t e = hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
-                       geom.p_bytes, geom.v_bytes);
+                       geom.p_bytes, geom.v_bytes, d_queue);
     return hipGetLastError();
 }
 

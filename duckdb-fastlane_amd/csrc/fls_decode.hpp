@@ -40,8 +40,10 @@ struct DecodeGeom {
 };
 
 // Launch the fused decode over every vector of nchunks chunks (no FSST).
+// d_queue (one zeroed word, may be NULL): waves take chunks from this work
+// queue in list order instead of a static grid-stride split.
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
-                         hipStream_t stream);
+                         hipStream_t stream, uint32_t *d_queue = nullptr);
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,

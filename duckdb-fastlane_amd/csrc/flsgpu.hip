@@ -149,6 +149,7 @@ struct DeviceShard {
     DevBuf<StrT> strtab;               // string_t tables of VARCHAR chunks
     std::vector<uint64_t> strtab_off;  // per (rg - rg0) * ncols + col: index into strtab
     DevBuf<uint32_t> err;
+    DevBuf<uint32_t> queue;                // decode work-queue counter
     std::vector<DevBuf<uint8_t>> d_heap;   // per FSST column: decoded string bytes
     std::vector<PinBuf<uint8_t>> h_heap;   // per FSST column: host copy string_t points into
     std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
@@ -166,6 +167,7 @@ struct Slot {                       // one batch of row groups in flight
     DevBuf<DevChunk> d_chunks;
     DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch
     PinBuf<uint8_t> h_stage;        // pinned bounce buffer when the image cannot be pinned
+    DevBuf<uint32_t> queue;         // decode work-queue counter
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
@@ -243,6 +245,7 @@ struct fls_table {
     std::vector<DevChunk> h_chunks;
     std::vector<uint8_t> dev_mask;     // column mask h_chunks was built for
     uint32_t dev_nmain = 0;            // h_chunks[0, dev_nmain) main kernel, the rest FSST
+    int dev_policy = -1;               // decode_policy() h_chunks was ordered for
     uint32_t dev_fsst_vecs = 0;        // vectors of the FSST chunks
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -354,10 +357,25 @@ bool col_selected(const std::vector<uint8_t> &mask, uint32_t c) { return mask.em
 
 bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[rg].chunks[c].hdr.enc == ENC_FSST; }
 
+// Decode work distribution (A/B knob FLS_DECODE_POLICY, read per call so both
+// arms run on the same buffers): 0 = work queue, largest chunks first
+// (default); bit 0 = static grid-stride split; bit 1 = keep column order.
+enum : int { POLICY_STATIC = 1, POLICY_NO_LPT = 2 };
+int decode_policy() {
+    const char *e = getenv("FLS_DECODE_POLICY");
+    return e ? atoi(e) : 0;
+}
+
 // FSST chunks go last (their own kernel) and get their vector numbering;
 // returns how many lead (main kernel) and the FSST vector count
-uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs) {
+uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int policy) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
+    if (!(policy & (POLICY_STATIC | POLICY_NO_LPT))) {
+        // largest output first: the work queue then ends the launch on small chunks
+        std::stable_sort(v.begin(), mid, [](const DevChunk &a, const DevChunk &b) {
+            return (uint64_t)a.nvec * a.ob > (uint64_t)b.nvec * b.ob;
+        });
+    }
     uint32_t nv = 0;
     for (auto it = mid; it != v.end(); ++it) {
         it->vec_base = nv;
@@ -368,8 +386,8 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs) {
 }
 
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t fsst_vecs, uint32_t *d_err,
-                      const DecodeGeom &geom, hipStream_t stream) {
-    hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream);
+                      const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy) {
+    hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue);
     if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, ntotal - nmain, fsst_vecs, d_err, stream);
     return e;
 }
@@ -666,13 +684,15 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         }
     }
     uint32_t fsst_vecs = 0;
-    const uint32_t nmain = order_for_launch(list, &fsst_vecs);
+    const int policy = decode_policy();
+    const uint32_t nmain = order_for_launch(list, &fsst_vecs, policy);
     const size_t k = list.size();
     HIP_TRY(sl.h_chunks.alloc(k));
     HIP_TRY(sl.d_chunks.alloc(d.dev, k));
     if (k) memcpy(sl.h_chunks.p, list.data(), k * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
-    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream));
+    HIP_TRY(sl.queue.alloc(d.dev, 1));
+    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream, sl.queue.p, policy));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
     if (filtered) {
@@ -1111,7 +1131,8 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     if (col_mask)
         for (uint32_t c = 0; c < ncols; ++c) mask[c] = col_mask[c] ? 1 : 0;
     HIP_TRY(hipSetDevice(sh.dev));
-    if (mask != t->dev_mask || t->h_chunks.empty()) {
+    const int policy = decode_policy();
+    if (mask != t->dev_mask || t->h_chunks.empty() || policy != t->dev_policy) {
         // (re)build the launch descriptor list: column-major task order, so
         // concurrent waves stream one column's consecutive row groups
         std::vector<DevChunk> chunks;
@@ -1129,7 +1150,8 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
                                                sh.h_heap[c].p ? sh.h_heap[c].p + ho : nullptr));
             }
         }
-        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst_vecs);
+        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst_vecs, policy);
+        t->dev_policy = policy;
         HIP_TRY(hipStreamSynchronize(t->stream));
         HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
         HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
@@ -1148,8 +1170,9 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
+    HIP_TRY(sh.queue.alloc(sh.dev, 1));
     HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst_vecs, sh.err.p,
-                       t->last_bytes.geom, t->stream));
+                       t->last_bytes.geom, t->stream, sh.queue.p, policy));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;
     t->launched = true;
