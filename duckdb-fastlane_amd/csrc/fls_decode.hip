@@ -92,11 +92,12 @@ __device__ __forceinline__ v4u ld16(const FLS_GLOBAL v4u *p) {
 #endif
 }
 
-#ifdef FLS_NO_SEQ
-__device__ __forceinline__ void seq() {}
-#else
+// Scheduling fence between unrolled 16-byte-chunk steps: one step's registers
+// live at a time (occupancy, not one wave's ILP, hides latency here).
+// Measured: fencing every second step instead (LDS reads of two steps in
+// flight) was neutral to 2 % slower (profiles/r1/abenv_prefetch_width_*.txt,
+// arm p8).
 __device__ __forceinline__ void seq() { __builtin_amdgcn_sched_barrier(0); }
-#endif
 __device__ __forceinline__ uint32_t bitrev3(uint32_t g) { return ((g & 1) << 2) | (g & 2) | ((g >> 2) & 1); }
 
 // per-lane copy of the chunk's VecMeta[lane]
@@ -581,7 +582,9 @@ struct PathAlp {
 // (inlined into one switch, hipcc allocated the union of all paths: 292 VGPRs,
 // one wave per SIMD).  Arguments arrive in VGPRs, which a callee must assume
 // divergent, so everything uniform is re-established with readfirstlane.
-template <class Path>
+// L = 16-byte prefetch loads per lane the chunk's widest vector needs
+// (8 W / 64 rounded up): the register prefetch holds only that many.
+template <class Path, int L>
 __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generic, uint32_t lds_p, uint32_t lds_v,
                                                     uint32_t v_bytes, uint32_t *err_generic) {
     const uint64_t cp = (uint64_t)chunk_generic;
@@ -604,7 +607,6 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
     uint32_t *err = (uint32_t *)((uint64_t)uni((uint32_t)(ep >> 32)) << 32 | uni((uint32_t)ep));
     const uint32_t lane = __lane_id();
     const Path path(c, s, lane, err);
-    constexpr int L = Path::T / 8;
     using Aux = typename Path::Aux;
     const uint32_t nvec = c.nvec;
     const uint32_t ob = c.ob;
@@ -617,16 +619,19 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
 
     v4u r[L];
     Aux aux, aux_next;
+    // aux (DELTA / RLE bases) is loaded before the packed bits of the same
+    // vector: waiting for the packed bits (stage) then covers it, so no wait
+    // on the aux load ever depends on the W-dependent number of packed loads
     VecInfo cur = vec_info(m, 0);
-    prefetch<L>(packed + cur.poff16, 8 * cur.W, dummy, lane, r);
     aux.load(path.aux_ptr(c, cur), lane);
+    prefetch<L>(packed + cur.poff16, 8 * cur.W, dummy, lane, r);
     uint32_t v = 0;
     if (nfull > 0) {
         // peeled first iteration: the loop header then only sees the steady state
         stage<L>(s.P, r, 8 * cur.W, lane);
         VecInfo nxt = vec_info(m, nvec > 1 ? 1 : 0);
-        prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
         aux_next.load(path.aux_ptr(c, nxt), lane);
+        prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
         wave_sync();
         path.template vec<true>(s, cur, aux, out, lane);
         cur = nxt;
@@ -635,8 +640,8 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
             wave_sync();
             stage<L>(s.P, r, 8 * cur.W, lane);
             nxt = vec_info(m, v + 1 < nvec ? v + 1 : v);
-            prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
             aux_next.load(path.aux_ptr(c, nxt), lane);
+            prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
             wave_sync();
             path.template vec<true>(s, cur, aux, out + (size_t)v * kVectorSize * ob, lane);
             cur = nxt;
@@ -651,21 +656,35 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
     }
 }
 
+// The register prefetch holds L = 8 W / 64 (rounded up to a power of two)
+// 16-byte loads per lane for the chunk's widest vector W, not T / 8: fewer
+// live VGPRs, no spills of in-flight prefetch data (measured: halving L for
+// W <= T/2 took c3's DELTA64 keys from 2.01 to 1.88 ms,
+// profiles/r1/abenv_prefetch_width_c3.txt).
+template <class Path, int L>
+__device__ __forceinline__ void call_l(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
+                                       uint32_t max_w) {
+    if constexpr (L > 1) {
+        if (max_w <= 4 * L) {  // W <= 8 (L / 2): half as many loads suffice
+            call_l<Path, L / 2>(c, lp, lv, vb, err, max_w);
+            return;
+        }
+    }
+    run_chunk<Path, L>(c, lp, lv, vb, err);
+}
 template <class Path>
-__device__ __forceinline__ void call(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err) {
-    run_chunk<Path>(c, lp, lv, vb, err);
+__device__ __forceinline__ void call(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
+                                     uint32_t max_w) {
+    call_l<Path, Path::T / 8>(c, lp, lv, vb, err, max_w);
 }
 
 template <int OB>
 __device__ __forceinline__ void call_dict(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
-                                          uint32_t dict_count) {
-    if (dict_count * OB + 4096 <= vb) call<PathDict<OB, true>>(c, lp, lv, vb, err);
-    else call<PathDict<OB, false>>(c, lp, lv, vb, err);
+                                          uint32_t dict_count, uint32_t max_w) {
+    if (dict_count * OB + 4096 <= vb) call<PathDict<OB, true>>(c, lp, lv, vb, err, max_w);
+    else call<PathDict<OB, false>>(c, lp, lv, vb, err, max_w);
 }
 
-#ifndef FLS_WAVES_PER_SIMD
-#define FLS_WAVES_PER_SIMD 4
-#endif
 // Next chunk of this wave: from the launch's work queue (one atomic per chunk,
 // lane 0, broadcast) when there is one -- chunks are then taken in the host's
 // largest-first order, so the launch ends on small chunks -- else grid-stride.
@@ -679,6 +698,9 @@ __device__ __forceinline__ uint32_t next_chunk(uint32_t *queue, uint32_t prev, u
     return stride + uni(ci);
 }
 
+#ifndef FLS_WAVES_PER_SIMD
+#define FLS_WAVES_PER_SIMD 4
+#endif
 __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                         uint32_t *__restrict__ err, uint32_t p_bytes,
                                                         uint32_t v_bytes, uint32_t *__restrict__ queue) {
@@ -691,45 +713,45 @@ __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const D
          ci = next_chunk(queue, ci, first, stride)) {
         const DevChunk *cg = chunks + ci;
         const FLS_GLOBAL DevChunk *c = gptr(cg);
-        const uint32_t nvec = c->nvec, dc = c->dict_count;
+        const uint32_t nvec = c->nvec, dc = c->dict_count, mw = c->max_w;
         const uint32_t enc = c->enc, T = c->T, ob = c->ob;
         if (nvec == 0) continue;
         switch (enc) {
         case ENC_FFOR:
             switch (T) {
-            case 64: call<PathFfor<64>>(cg, lp, lv, v_bytes, err); break;
-            case 32: call<PathFfor<32>>(cg, lp, lv, v_bytes, err); break;
-            case 16: call<PathFfor<16>>(cg, lp, lv, v_bytes, err); break;
-            default: call<PathFfor<8>>(cg, lp, lv, v_bytes, err); break;
+            case 64: call<PathFfor<64>>(cg, lp, lv, v_bytes, err, mw); break;
+            case 32: call<PathFfor<32>>(cg, lp, lv, v_bytes, err, mw); break;
+            case 16: call<PathFfor<16>>(cg, lp, lv, v_bytes, err, mw); break;
+            default: call<PathFfor<8>>(cg, lp, lv, v_bytes, err, mw); break;
             }
             break;
         case ENC_DELTA:
             switch (T) {
-            case 64: call<PathDelta64>(cg, lp, lv, v_bytes, err); break;
-            case 32: call<PathDeltaSmall<32>>(cg, lp, lv, v_bytes, err); break;
-            case 16: call<PathDeltaSmall<16>>(cg, lp, lv, v_bytes, err); break;
-            default: call<PathDeltaSmall<8>>(cg, lp, lv, v_bytes, err); break;
+            case 64: call<PathDelta64>(cg, lp, lv, v_bytes, err, mw); break;
+            case 32: call<PathDeltaSmall<32>>(cg, lp, lv, v_bytes, err, mw); break;
+            case 16: call<PathDeltaSmall<16>>(cg, lp, lv, v_bytes, err, mw); break;
+            default: call<PathDeltaSmall<8>>(cg, lp, lv, v_bytes, err, mw); break;
             }
             break;
         case ENC_DICT:
             switch (ob) {
-            case 16: call_dict<16>(cg, lp, lv, v_bytes, err, dc); break;
-            case 8: call_dict<8>(cg, lp, lv, v_bytes, err, dc); break;
-            case 4: call_dict<4>(cg, lp, lv, v_bytes, err, dc); break;
-            case 2: call_dict<2>(cg, lp, lv, v_bytes, err, dc); break;
-            default: call_dict<1>(cg, lp, lv, v_bytes, err, dc); break;
+            case 16: call_dict<16>(cg, lp, lv, v_bytes, err, dc, mw); break;
+            case 8: call_dict<8>(cg, lp, lv, v_bytes, err, dc, mw); break;
+            case 4: call_dict<4>(cg, lp, lv, v_bytes, err, dc, mw); break;
+            case 2: call_dict<2>(cg, lp, lv, v_bytes, err, dc, mw); break;
+            default: call_dict<1>(cg, lp, lv, v_bytes, err, dc, mw); break;
             }
             break;
         case ENC_ALP:
-            if (T == 64) call<PathAlp<64>>(cg, lp, lv, v_bytes, err);
-            else call<PathAlp<32>>(cg, lp, lv, v_bytes, err);
+            if (T == 64) call<PathAlp<64>>(cg, lp, lv, v_bytes, err, mw);
+            else call<PathAlp<32>>(cg, lp, lv, v_bytes, err, mw);
             break;
         case ENC_RLE:
             switch (ob) {
-            case 8: call<PathRle<8>>(cg, lp, lv, v_bytes, err); break;
-            case 4: call<PathRle<4>>(cg, lp, lv, v_bytes, err); break;
-            case 2: call<PathRle<2>>(cg, lp, lv, v_bytes, err); break;
-            default: call<PathRle<1>>(cg, lp, lv, v_bytes, err); break;
+            case 8: call<PathRle<8>>(cg, lp, lv, v_bytes, err, mw); break;
+            case 4: call<PathRle<4>>(cg, lp, lv, v_bytes, err, mw); break;
+            case 2: call<PathRle<2>>(cg, lp, lv, v_bytes, err, mw); break;
+            default: call<PathRle<1>>(cg, lp, lv, v_bytes, err, mw); break;
             }
             break;
         default:

@@ -24,7 +24,11 @@ struct DevChunk {              // 64 B
     uint64_t heap_host;        // FSST: address string_t pointers use for heap byte 0
                                // (the pinned host copy the heap lands in)
     uint32_t heap_bytes;       // FSST: heap bytes of the chunk (ChunkHeader.reserved1)
-    uint32_t vec_base;         // FSST: vectors of the FSST chunks before this one in the launch
+    union {
+        uint32_t vec_base;     // FSST: vectors of the FSST chunks before this one in the launch
+        uint32_t max_w;        // other encodings: widest vector of the chunk (bits) -- sizes the
+                               // register prefetch, so narrow chunks hold fewer VGPRs in flight
+    };
 };
 static_assert(sizeof(DevChunk) == 64, "DevChunk is 64 B");
 

@@ -346,6 +346,7 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
             bc->meta += alp_aux_bytes(alp_exceptions(vm.aux_count), h.vbits);
     }
     if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? 16 : h.vbits / 8);
+    d.max_w = max_w;
     uint32_t pb, vb;
     chunk_lds_need(h.enc, h.T, d.ob, h.dict_count, max_w, pb, vb);
     bc->geom.p_bytes = std::max(bc->geom.p_bytes, pb);
@@ -360,7 +361,9 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // Decode work distribution (A/B knob FLS_DECODE_POLICY, read per call so both
 // arms run on the same buffers): 0 = work queue, largest chunks first
 // (default); bit 0 = static grid-stride split; bit 1 = keep column order.
-enum : int { POLICY_STATIC = 1, POLICY_NO_LPT = 2 };
+// bit 2 = full-width register prefetch for every chunk (descriptor max_w = T).
+// bit 3 = unpack two 16-byte steps per scheduling fence (decode_kernel<2>).
+enum : int { POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_GROUP2 = 8 };
 int decode_policy() {
     const char *e = getenv("FLS_DECODE_POLICY");
     return e ? atoi(e) : 0;
@@ -370,6 +373,8 @@ int decode_policy() {
 // returns how many lead (main kernel) and the FSST vector count
 uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int policy) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
+    if (policy & POLICY_FULL_PREFETCH)
+        for (auto it = v.begin(); it != mid; ++it) it->max_w = it->T;
     if (!(policy & (POLICY_STATIC | POLICY_NO_LPT))) {
         // largest output first: the work queue then ends the launch on small chunks
         std::stable_sort(v.begin(), mid, [](const DevChunk &a, const DevChunk &b) {

@@ -68,6 +68,25 @@ __global__ __launch_bounds__(256) void k_copy(const v4u *__restrict__ in, v4u *_
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) out[i] = in[i];
 }
 
+// one wave writes 8 KB blocks with 8 store instructions, either each
+// instruction 1 KB contiguous (SEG=0) or 8 x 128-B segments 1 KB apart (SEG=1,
+// the DELTA64 register layout)
+template <int SEG>
+__global__ __launch_bounds__(256) void k_block(v4u *__restrict__ out, size_t nblk) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (size_t)gridDim.x * 4;
+    const uint32_t g = lane >> 3, q = lane & 7;
+    for (size_t b = wave; b < nblk; b += nw) {
+        v4u *o = out + b * 512;  // 8 KB = 512 x 16 B
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const v4u v = {lane, j, (uint32_t)b, 1u};
+            if (SEG) o[8 * (8 * g + j) + q] = v;
+            else o[64 * j + lane] = v;
+        }
+    }
+}
+
 template <class F>
 double time_ms(F f, int reps = 10) {
     hipEvent_t a, b;
@@ -94,7 +113,7 @@ int main() {
     CK(hipMemset(in, 1, bytes));
     int cus = 256;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    for (int per_cu : {2, 4, 8}) {
+    for (int per_cu : {4, 16}) {
         const int grid = cus * per_cu;
         double ms;
         ms = time_ms([&] { k_write<0, 4><<<grid, 256>>>(out, n16); });
@@ -111,6 +130,10 @@ int main() {
         printf("mix 1:7      grid %5d: %7.1f GB/s (read+write)\n", grid, (bytes + bytes / 7) / ms / 1e6);
         ms = time_ms([&] { k_mix<3><<<grid, 256>>>(in, out, n16); });
         printf("mix 1:3      grid %5d: %7.1f GB/s (read+write)\n", grid, (bytes + bytes / 3) / ms / 1e6);
+        ms = time_ms([&] { k_block<0><<<grid, 256>>>(out, bytes / 8192); });
+        printf("8K blk 1KB   grid %5d: %7.1f GB/s\n", grid, bytes / ms / 1e6);
+        ms = time_ms([&] { k_block<1><<<grid, 256>>>(out, bytes / 8192); });
+        printf("8K blk 8x128 grid %5d: %7.1f GB/s\n", grid, bytes / ms / 1e6);
     }
     return 0;
 }
