@@ -37,7 +37,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="lineitem", choices=["lineitem", "c1", "c3", "c4"])
+    p.add_argument("--workload", default="lineitem",
+                   choices=["lineitem", "c1", "c3", "c4", "lineitem_full", "lineitem_dbl"])
     p.add_argument("--scale", type=float, default=100.0, help="lineitem scale factor")
     p.add_argument("--rows", type=int, default=0, help="row override (c1/c3/c4; 0 = config default)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
@@ -78,15 +79,16 @@ def measure_traffic(args):
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
         except Exception as e:  # noqa: BLE001 - report, never fail the bench on profiling
             return None, f"rocprofv3 {ctr} pass failed: {e}"
-        per = []
+        per = {}  # kernel -> samples (a step is decode_kernel, plus fsst_kernel for FSST columns)
         for path in Path(d).rglob("*counter_collection.csv"):
             for r in csv.DictReader(open(path)):
-                if "decode_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
-                    per.append(float(r["Counter_Value"]))
+                k = r.get("Kernel_Name", "")
+                if ("decode_kernel" in k or "fsst_kernel" in k) and r.get("Counter_Name") == ctr:
+                    per.setdefault("fsst" if "fsst_kernel" in k else "decode", []).append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
-        if not per:
+        if "decode" not in per:
             return None, f"no {ctr} samples"
-        vals[ctr] = sum(per) / len(per) * 1024.0  # KiB -> bytes, per launch
+        vals[ctr] = sum(sum(v) / len(v) for v in per.values()) * 1024.0  # KiB -> bytes, per step
     return 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"], \
         f"rocprofv3 --pmc per launch: FETCH_SIZE x2 {2 * vals['FETCH_SIZE'] / 1e9:.3f} GB + " \
         f"WRITE_SIZE {vals['WRITE_SIZE'] / 1e9:.3f} GB"
@@ -165,7 +167,6 @@ def verify(fl, t, args, rg_list):
         for c, (name, ty, _, _, ob) in enumerate(sch):
             got = t.device_copy_out(c, r0, n)
             if ty == fl.VARCHAR:
-                codes = fl.gen_values(args.workload, c, first + r0, n, np.uint32, args.scale, args.rows)
                 dic = {}
                 k = 0
                 while True:
@@ -174,8 +175,12 @@ def verify(fl, t, args, rg_list):
                         break
                     dic[k] = s.encode()
                     k += 1
-                strs = fl.string_t_decode(got)
-                if strs != [dic[int(x)] for x in codes]:
+                if dic:
+                    codes = fl.gen_values(args.workload, c, first + r0, n, np.uint32, args.scale, args.rows)
+                    exp = [dic[int(x)] for x in codes]
+                else:  # free text (l_comment, FSST)
+                    exp = fl.gen_strings(args.workload, c, first + r0, n, args.scale, args.rows)
+                if fl.string_t_decode(got) != exp:
                     return f"{name} rg {rg}"
             else:
                 exp = fl.gen_values(args.workload, c, first + r0, n, fl.NP_DTYPE[ty], args.scale, args.rows)
@@ -292,15 +297,20 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",  # fixed SF100 total, row groups split over ranks
             "vs_baseline": None,
-            "dtype": "int64/int32/string_t (integer unpack)",
-            "data": "synthetic (seeded TPC-H-like generator, l_comment excluded)",
+            "dtype": "int64/int32/string_t (integer unpack)" if args.workload != "lineitem_dbl"
+            else "int64/int32/string_t + f64 (ALP)",
+            "data": {"lineitem": "synthetic (seeded TPC-H-like generator, l_comment excluded)",
+                     "lineitem_full": "synthetic (seeded TPC-H-like generator, l_comment FSST text)",
+                     "lineitem_dbl": "synthetic (seeded TPC-H-like generator, DECIMAL columns as DOUBLE/ALP)"}.get(
+                args.workload, "synthetic (seeded generator)"),
             "config": cfg,
             "hbm_gbs": achieved * world,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic / 1e9 if traffic else None,
                          "traffic_unit": "GB per launch (HBM, PMC)", "traffic_note": traffic_note,
-                         "kernel": "fls::decode_kernel", "kernel_ms": avg_ms,
+                         "kernel": "fls::decode_kernel" + (" + fls::fsst_kernel" if args.workload == "lineitem_full" else ""),
+                         "kernel_ms": avg_ms,
                          "algo_bytes_per_launch": algo,
                          "algo_bytes_split": {"packed": int(st.packed_bytes), "meta": int(st.meta_bytes),
                                               "out": int(st.out_bytes)}},

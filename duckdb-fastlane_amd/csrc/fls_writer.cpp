@@ -255,15 +255,46 @@ std::vector<uint8_t> enc_dict_codes(const uint32_t *codes, uint32_t n, uint8_t v
     return assemble_chunk(ENC_DICT, 32, vbits, is_str, n, vecs, dict, dict_count);
 }
 
+// Open-addressing set / map of 64-bit values (row-group sized: n <= 65,536),
+// the distinct-value pass of ENC_AUTO's dictionary estimate and of DICT.
+struct U64Table {
+    std::vector<uint64_t> key;
+    std::vector<uint32_t> val;  // UINT32_MAX = empty slot
+    uint64_t mask;
+    size_t count = 0;
+    explicit U64Table(uint32_t n) {
+        size_t cap = 16;
+        while (cap < 2ull * n) cap <<= 1;
+        key.resize(cap);
+        val.assign(cap, UINT32_MAX);
+        mask = cap - 1;
+    }
+    static uint64_t h(uint64_t x) {
+        x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33;
+        return x;
+    }
+    size_t slot(uint64_t x) const {
+        size_t i = h(x) & mask;
+        while (val[i] != UINT32_MAX && key[i] != x) i = (i + 1) & mask;
+        return i;
+    }
+    void insert(uint64_t x) {
+        const size_t i = slot(x);
+        if (val[i] == UINT32_MAX) { key[i] = x; val[i] = 0; ++count; }
+    }
+};
+
 std::vector<uint8_t> enc_dict_int(int T, const uint64_t *vals, uint32_t n) {
-    std::vector<uint64_t> uniq(vals, vals + n);
+    U64Table tab(n);
+    for (uint32_t i = 0; i < n; ++i) tab.insert(vals[i]);
+    std::vector<uint64_t> uniq;
+    uniq.reserve(tab.count);
+    for (size_t i = 0; i <= tab.mask; ++i)
+        if (tab.val[i] != UINT32_MAX) uniq.push_back(tab.key[i]);
     std::sort(uniq.begin(), uniq.end(), [T](uint64_t a, uint64_t b) { return sext(a, T) < sext(b, T); });
-    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    for (uint32_t i = 0; i < uniq.size(); ++i) tab.val[tab.slot(uniq[i])] = i;
     std::vector<uint32_t> codes(n);
-    std::unordered_map<uint64_t, uint32_t> idx;
-    idx.reserve(uniq.size() * 2);
-    for (uint32_t i = 0; i < uniq.size(); ++i) idx[uniq[i]] = i;
-    for (uint32_t i = 0; i < n; ++i) codes[i] = idx[vals[i]];
+    for (uint32_t i = 0; i < n; ++i) codes[i] = tab.val[tab.slot(vals[i])];
     std::vector<uint8_t> dict((size_t)uniq.size() * (T / 8));
     for (size_t i = 0; i < uniq.size(); ++i) put_word(dict.data(), T, i, uniq[i]);
     return enc_dict_codes(codes.data(), n, (uint8_t)T, false, dict, (uint32_t)uniq.size());
@@ -692,9 +723,17 @@ size_t est_rle(int T, const uint64_t *vals, uint32_t n) {
     return runs * (T / 8) + ((n + 1023) / 1024) * (32 + 128 + 128 * 5);
 }
 size_t est_dict(int T, const uint64_t *vals, uint32_t n) {
-    std::vector<uint64_t> s(vals, vals + n);
-    std::sort(s.begin(), s.end());
-    size_t d = std::unique(s.begin(), s.end()) - s.begin();
+    // a 1,024-value sample first: high-cardinality columns (keys, prices)
+    // skip the full distinct count, which dominated ENC_AUTO's cost
+    if (n > 4096) {
+        uint64_t smp[1024];
+        for (uint32_t i = 0; i < 1024; ++i) smp[i] = vals[(uint64_t)i * n / 1024];
+        std::sort(smp, smp + 1024);
+        if (std::unique(smp, smp + 1024) - smp > 512) return SIZE_MAX;
+    }
+    U64Table tab(n);
+    for (uint32_t i = 0; i < n; ++i) tab.insert(vals[i]);
+    const size_t d = tab.count;
     if (d > 65536) return SIZE_MAX;
     return d * (T / 8) + ((n + 1023) / 1024) * (32 + 128 * (size_t)bitlen(d - 1 ? d - 1 : 0));
 }
@@ -979,8 +1018,16 @@ using namespace fls;
 
 // ---- C-ABI ----------------------------------------------------------------
 
+namespace {
+int default_writer_threads() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::min(16u, std::max(1u, hw));
+}
+}  // namespace
+
 struct fls_writer {
     FileBuilder fb;
+    int threads = default_writer_threads();  // column-parallel encode per row group
 };
 
 extern "C" {
@@ -1020,9 +1067,8 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (!w->fb.rgs.empty() && w->fb.rgs.back().nrows != w->fb.rowgroup_size)
         return fail(FLS_ERR_STATE, "only the last row group may be short");
-    FileBuilder::RG rg;
-    rg.nrows = nrows;
-    for (size_t c = 0; c < w->fb.cols.size(); ++c) {
+    const size_t ncols = w->fb.cols.size();
+    for (size_t c = 0; c < ncols; ++c) {
         const ColSpec &cs = w->fb.cols[c];
         if (!data[c]) return fail(FLS_ERR_ARG, "column %zu: NULL data", c);
         if (cs.type == TY_VARCHAR) {
@@ -1030,22 +1076,50 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
             const uint32_t *o = str_offsets[c];
             for (uint32_t i = 0; i < nrows; ++i)
                 if (o[i + 1] < o[i]) return fail(FLS_ERR_ARG, "column %zu: offsets not monotone", c);
-            rg.chunks.push_back(encode_str_chunk(cs.enc, o, (const char *)data[c], nrows));
-        } else {
-            const int T = type_value_bits(cs.type);
-            std::vector<uint64_t> v(nrows);
-            const uint8_t *p = (const uint8_t *)data[c];
-            for (uint32_t i = 0; i < nrows; ++i) {
-                uint64_t x = 0;
-                memcpy(&x, p + (size_t)i * (T / 8), T / 8);
-                v[i] = x;
-            }
-            rg.chunks.push_back(encode_int_chunk(cs.type, cs.enc, v.data(), nrows));
-            rg.zones.resize(c + 1, ZoneMap{0, 0, 0, 0});
-            rg.zones[c] = zone_of(cs.type, v.data(), nrows);
         }
     }
+    FileBuilder::RG rg;
+    rg.nrows = nrows;
+    rg.chunks.resize(ncols);
+    rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
+    // columns are independent: encode them on up to w->threads threads
+    auto encode_col = [&](size_t c) {
+        const ColSpec &cs = w->fb.cols[c];
+        if (cs.type == TY_VARCHAR) {
+            rg.chunks[c] = encode_str_chunk(cs.enc, str_offsets[c], (const char *)data[c], nrows);
+            return;
+        }
+        const int T = type_value_bits(cs.type);
+        std::vector<uint64_t> v(nrows);
+        const uint8_t *p = (const uint8_t *)data[c];
+        for (uint32_t i = 0; i < nrows; ++i) {
+            uint64_t x = 0;
+            memcpy(&x, p + (size_t)i * (T / 8), T / 8);
+            v[i] = x;
+        }
+        rg.chunks[c] = encode_int_chunk(cs.type, cs.enc, v.data(), nrows);
+        rg.zones[c] = zone_of(cs.type, v.data(), nrows);
+    };
+    const size_t nth = std::min<size_t>(ncols, (size_t)std::max(1, w->threads));
+    if (nth <= 1) {
+        for (size_t c = 0; c < ncols; ++c) encode_col(c);
+    } else {
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            for (size_t c; (c = next.fetch_add(1)) < ncols;) encode_col(c);
+        };
+        std::vector<std::thread> th;
+        for (size_t i = 1; i < nth; ++i) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+    }
     w->fb.rgs.push_back(std::move(rg));
+    return 0;
+}
+
+int fls_writer_set_threads(fls_writer *w, int nthreads) {
+    if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_threads: NULL writer");
+    w->threads = nthreads > 0 ? nthreads : default_writer_threads();
     return 0;
 }
 

@@ -47,6 +47,9 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
  * reference's ROW_GROUP_SIZE default, src/writer/write_fastlane_stream.cpp:21-24).
  * Must be called before the first row group. */
 int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows);
+/* Threads encoding the columns of a row group in parallel (0 = default:
+ * min(16, hardware threads)).  Output bytes do not depend on it. */
+int fls_writer_set_threads(fls_writer *w, int nthreads);
 /* Append one row group of nrows (1..row group size) rows; only the last row
  * group of a file may be short.  Integer / FLOAT / DOUBLE column c:
  * data[c] -> nrows values of the column's width (1/2/4/8 B).  VARCHAR column c:

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Write-path rates: the CPU FastLanes encoder behind
+COPY ... TO (FORMAT fls) and fls_writer_*.
+
+  1. C-ABI writer (ENC_AUTO), 1 and N column-parallel threads: lineitem
+     columns handed over as arrays (what COPY's sink does per row group),
+     encoded and assembled;
+  2. the seeded workload encoder (fls_gen_image: generate + encode) on N threads;
+  3. COPY (SELECT * FROM read_fastlanes(src)) TO dst (FORMAT fls) through the
+     executor harness: GPU scan of the source + encode + write (needs a GPU).
+
+    python scripts/writer_bench.py [--scale 1] [--threads 16] [--copy]
+"""
+import argparse
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--copy", action="store_true")
+    a = ap.parse_args()
+    import pkgload
+    fl = pkgload.load()
+    wl = "lineitem"
+    n = fl.gen_nrows(wl, a.scale)
+    img = fl.gen_image(wl, a.scale, nthreads=a.threads)
+    t = fl.Connection([0]).read_image(img)
+    sch = t.schema()
+    cols = []
+    raw = 0
+    for c, (name, ty, w, s, ob) in enumerate(sch):
+        if ty == fl.VARCHAR:
+            codes = fl.gen_values(wl, c, 0, n, np.uint32, a.scale)
+            words = []
+            while (x := fl.gen_dict_string(wl, c, len(words))) is not None:
+                words.append(x)
+            vals = [words[k] for k in codes]
+            raw += int(np.array([len(x) for x in words])[codes].sum())
+            cols.append((name, ty, vals, fl.ENC_AUTO, w, s))
+        else:
+            v = fl.gen_values(wl, c, 0, n, fl.NP_DTYPE[ty], a.scale)
+            raw += v.nbytes
+            cols.append((name, ty, v, fl.ENC_AUTO, w, s))
+    # marshal every row group's buffers first (what a COPY sink already holds),
+    # then time only the C-ABI encode + assemble
+    import ctypes as C
+    lib = fl.lib
+    parts = []
+    for r0 in range(0, n, fl.ROWGROUP):
+        r1 = min(n, r0 + fl.ROWGROUP)
+        keep, data, offs = [], (C.c_void_p * len(cols))(), (C.c_void_p * len(cols))()
+        for c, (name, ty, vals, *_rest) in enumerate(cols):
+            if ty == fl.VARCHAR:
+                sl = [x.encode() for x in vals[r0:r1]]
+                o = np.zeros(len(sl) + 1, dtype=np.uint32)
+                o[1:] = np.cumsum([len(x) for x in sl])
+                buf = np.frombuffer(b"".join(sl), dtype=np.uint8).copy()
+                keep += [o, buf]
+                data[c], offs[c] = buf.ctypes.data, o.ctypes.data
+            else:
+                part = np.ascontiguousarray(vals[r0:r1])
+                keep.append(part)
+                data[c] = part.ctypes.data
+        parts.append((r1 - r0, data, offs, keep))
+    for th in sorted({1, a.threads}):
+        w = lib.fls_writer_new(0)
+        lib.fls_writer_set_threads.argtypes = [C.c_void_p, C.c_int]
+        lib.fls_writer_set_threads(w, th)
+        for name, ty, vals, enc, wd, sc in cols:
+            fl._check(lib.fls_writer_add_column(w, name.encode(), ty, wd, sc, enc))
+        t0 = time.perf_counter()
+        for m, data, offs, _ in parts:
+            fl._check(lib.fls_writer_add_rowgroup(w, m, data, offs))
+        p, ln = C.c_void_p(), C.c_uint64()
+        fl._check(lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)))
+        dt = time.perf_counter() - t0
+        lib.fls_image_free(p)
+        lib.fls_writer_free(w)
+        print(f"C-ABI writer (ENC_AUTO, {th} threads), lineitem SF{a.scale:g}: {n} rows x {len(cols)} cols in "
+              f"{dt:.2f} s = {n / dt / 1e6:.2f} M rows/s, {raw / dt / 1e6:.0f} MB/s of input -> "
+              f"{ln.value / 1e6:.0f} MB (ratio {raw / ln.value:.2f})", flush=True)
+    for th in sorted({1, a.threads}):
+        t0 = time.perf_counter()
+        g = fl.gen_image(wl, a.scale, nthreads=th)
+        dt = time.perf_counter() - t0
+        print(f"generate + encode (fls_gen_image), {th} threads: {n / dt / 1e6:.1f} M rows/s "
+              f"({g.len / 1e6:.0f} MB in {dt:.2f} s)", flush=True)
+    if a.copy:
+        from ext_harness import Ext
+        e = Ext()
+        with tempfile.TemporaryDirectory() as d:
+            src, dst = os.path.join(d, "src.fls"), os.path.join(d, "dst.fls")
+            img.write(src)
+            t0 = time.perf_counter()
+            rows = e.copy("read_fastlanes", src, dst, fmt="fls")
+            dt = time.perf_counter() - t0
+            print(f"COPY (SELECT * FROM read_fastlanes) TO (FORMAT fls): {rows} rows in {dt:.2f} s = "
+                  f"{rows / dt / 1e6:.2f} M rows/s", flush=True)
+        e.close()
+
+
+if __name__ == "__main__":
+    main()
