@@ -138,6 +138,26 @@ class RefFile:
         hb = heap[:got].tobytes()
         return [hb[offs[i]:offs[i + 1]] for i in range(n)]
 
+    def decode_strings_column(self, c: int, nthreads: int = 1) -> int:
+        """Decode every row group of VARCHAR column c (DICT or FSST) into
+        offsets + bytes, row groups spread over nthreads (ctypes releases the
+        GIL); returns the string bytes produced.  CPU-baseline timing only."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        def one(rg):
+            n = self.rowgroup_rows(rg)
+            offs = np.zeros(n + 1, dtype=np.uint32)
+            cap = 64 * n + 4096
+            while True:
+                heap = np.empty(cap, dtype=np.uint8)
+                got = _lib.flsref_decode_strings(C.byref(self.f), c, rg, offs.ctypes.data, heap.ctypes.data, cap)
+                if got >= 0:
+                    return got
+                cap *= 4
+
+        with ThreadPoolExecutor(max(1, nthreads)) as ex:
+            return sum(ex.map(one, range(self.nrowgroups)))
+
     def strings_column(self, c: int) -> list[bytes]:
         out = []
         for rg in range(self.nrowgroups):
