@@ -50,8 +50,9 @@ hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d
                          hipStream_t stream, uint32_t *d_queue = nullptr);
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
+// bytes_per_lane: compressed bytes a lane decodes per round (8 or 16).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                       hipStream_t stream);
+                       hipStream_t stream, int bytes_per_lane = 8);
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
 // LDS bytes per wave the v2 kernel needs for one chunk (given its max width)

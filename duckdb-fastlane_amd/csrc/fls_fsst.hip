@@ -4,19 +4,22 @@
 // (reference src/fastlanes_facade.cpp:48, the FLSStrColumn consumer at
 // :163-170) for VARCHAR chunks written with ENC_FSST (fls_format.hpp).
 //
-// Waves take contiguous ranges of the launch's vectors (so a wave reloads the
-// chunk's symbol table only when its range crosses into the next chunk).
-// Per vector:
+// One wave per 64-thread block; a CU holds as many waves as its LDS fits
+// (10.6 KB each at 8 B per lane per round).  Waves take contiguous ranges of
+// the launch's vectors (so a wave reloads the chunk's symbol table only when
+// its range crosses into the next chunk).  Per vector:
 //   1. the FFOR-packed string lengths are unpacked into LDS and scanned into
 //      exclusive offsets (doff[0..1024]) inside the vector's decompressed bytes;
-//   2. the compressed code stream is decoded CODE-PARALLEL in rounds of 1024
-//      bytes (16 per lane, one coalesced 16 B load each): a lane sums its
-//      codes' symbol lengths, a wave scan turns them into output positions and
-//      the lane writes its symbols into an LDS ring.  The escape code (255:
-//      next byte is a literal) makes a code's meaning depend on its
-//      predecessor; a lane therefore evaluates its bytes for both entry
-//      states and a wave scan composes those 2-state maps (only in rounds that
-//      contain an escape byte or start right after one);
+//   2. the compressed code stream is decoded CODE-PARALLEL in rounds of
+//      64 x BPL bytes (BPL = 8 per lane, one coalesced load each, the next
+//      round's load in flight while this one decodes): a lane looks up its
+//      codes' symbol lengths (all LDS reads issued together), a DPP wave scan
+//      turns them into output positions and the lane ORs its symbols into the
+//      zeroed LDS ring as aligned dwords.  The escape code (255: next byte is
+//      a literal) makes a code's meaning depend on its predecessor; a lane then
+//      evaluates its bytes for both entry states and a wave scan composes those
+//      2-state maps (only in rounds that contain an escape byte or start right
+//      after one; escape-free rounds take a branch-free path);
 //   3. every string whose first min(len, 12) bytes are decoded gets its 16 B
 //      string_t (inline bytes, or 4-byte prefix + pointer into the heap's host
 //      copy), stored 64 records = 1 KiB at a time;
@@ -29,6 +32,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "fls_decode.hpp"
 #include "fls_format.hpp"
@@ -45,28 +50,40 @@ using lv4 = FLS_LDS v4u;
 using lu8 = FLS_LDS uint8_t;
 using lu32 = FLS_LDS uint32_t;
 
-constexpr int kWaves = 4;
-// per-wave LDS layout (bytes, all 16-aligned)
-constexpr uint32_t kOffP = 0;                      // packed lengths: 128*32 + 128
-constexpr uint32_t kOffD = kOffP + 128 * 32 + 128;  // doff[1025] (u32)
-constexpr uint32_t kOffSym = kOffD + 4112;         // u64 symbol[256]
-constexpr uint32_t kOffLen = kOffSym + 2048;       // u8 length[256]
-constexpr uint32_t kOffRing = kOffLen + 256;       // decoded bytes
-constexpr uint32_t kRing = 8192 + 64;              // one round (<= 1024 codes x 8 B) + carry
-constexpr uint32_t kWaveLds = kOffRing + kRing;
-static_assert(kOffSym % 16 == 0 && kOffRing % 16 == 0 && kWaveLds % 16 == 0, "LDS layout alignment");
+// One wave per 64-thread block (LDS is allocated per wave, so a CU holds as
+// many waves as its LDS fits).  BPL = compressed bytes per lane per round
+// (a round decodes 64 * BPL codes); the LDS ring must hold one round's output
+// (<= 8 B per code) plus a carried tail.  Per-wave LDS layout (bytes, all
+// 16-aligned); the packed string lengths of step 1 are staged in the ring,
+// which is free until the rounds start.
+constexpr uint32_t kOffD = 0;                   // doff[1025] (u32)
+constexpr uint32_t kOffSym = 4112;              // u64 symbol[256]
+constexpr uint32_t kOffLen = kOffSym + 2048;    // u8 length[256]
+constexpr uint32_t kOffRing = kOffLen + 256;    // decoded bytes (and step 1's packed lengths)
+constexpr uint32_t kPackedMax = 128 * 32 + 128; // lengths FFOR-packed at W <= 32, plus a zero row
+template <int BPL>
+struct Lds {
+    static constexpr uint32_t kRound = 64 * BPL;
+    static constexpr uint32_t kRing = (kRound * 8 + 64) > kPackedMax ? kRound * 8 + 64 : kPackedMax;
+    static constexpr uint32_t kWave = kOffRing + kRing;
+};
+static_assert(kOffSym % 16 == 0 && kOffRing % 16 == 0 && Lds<16>::kWave % 16 == 0 && Lds<8>::kWave % 16 == 0,
+              "LDS layout alignment");
 
 __device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
 __device__ __forceinline__ uint32_t byte_of(const v4u &r, uint32_t k) {
     const uint32_t w = k < 4 ? r.x : k < 8 ? r.y : k < 12 ? r.z : r.w;
     return (w >> (8 * (k & 3))) & 0xFF;
 }
-__device__ __forceinline__ uint32_t scan_incl(uint32_t x, uint32_t lane) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
+// Inclusive wave-64 prefix sum on DPP (row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast 15/31 across rows): six VALU steps, no LDS round trip.
+__device__ __forceinline__ uint32_t scan_incl(uint32_t x, uint32_t /*lane*/) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return x;
 }
 
@@ -78,23 +95,60 @@ struct Wave {
     lu8 *ring;
 };
 
-// 2-state escape automaton over a lane's bytes from entry state s:
-// returns the exit state, adds the produced bytes to out
-__device__ __forceinline__ uint32_t simulate(const Wave &w, const v4u &raw, uint32_t nb, uint32_t s, uint32_t &out) {
-    for (uint32_t k = 0; k < 16; ++k) {
-        if (k >= nb) break;
-        const uint32_t b = byte_of(raw, k);
-        if (s) {
-            out += 1;
-            s = 0;
-        } else if (b == kFsstEscape) {
-            s = 1;
-        } else {
-            out += min((uint32_t)w.len[b], 8u);
+// 2-state escape automaton over a lane's codes from entry state s: returns the
+// exit state, adds the produced bytes to out (sl[k] = symbol length of code k)
+template <int BPL>
+__device__ __forceinline__ uint32_t simulate(const uint32_t (&code)[BPL], const uint32_t (&sl)[BPL], uint32_t nb,
+                                             uint32_t s, uint32_t &out) {
+#pragma unroll
+    for (uint32_t k = 0; k < BPL; ++k) {
+        if (k < nb) {
+            if (s) {
+                out += 1;
+                s = 0;
+            } else if (code[k] == kFsstEscape) {
+                s = 1;
+            } else {
+                out += sl[k];
+            }
         }
     }
     return s;
 }
+
+// Appends a lane's decoded bytes to the ring as aligned dwords.  A lane's
+// output is one contiguous byte range whose edge dwords may be shared with the
+// neighbouring lanes' output, so every dword is OR-ed (ds_or_b32) into the
+// ring region zeroed for the round: one instruction shape, no per-lane branch
+// on which dword is an edge.
+struct RingWriter {
+    FLS_LDS uint32_t *ring32;
+    uint64_t acc;   // pending bytes, low first
+    uint32_t bits;  // valid bits in acc (< 32 between appends)
+    uint32_t d;     // dword index of acc's first byte
+    __device__ __forceinline__ RingWriter(lu8 *ring, uint32_t wp)
+        : ring32(reinterpret_cast<FLS_LDS uint32_t *>(ring)), acc(0), bits(8 * (wp & 3)), d(wp >> 2) {}
+    __device__ __forceinline__ void emit() {
+        __hip_atomic_fetch_or(ring32 + d, (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        ++d;
+        acc >>= 32;
+        bits -= 32;
+    }
+    // append n <= 4 bytes (low bytes of x); n = 0 appends nothing
+    __device__ __forceinline__ void put4(uint32_t x, uint32_t n) {
+        x &= n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u;
+        acc |= (uint64_t)x << bits;
+        bits += 8 * n;
+        if (bits >= 32) emit();
+    }
+    __device__ __forceinline__ void put(uint64_t sym, uint32_t n) {  // n <= 8
+        put4((uint32_t)sym, min(n, 4u));
+        put4((uint32_t)(sym >> 32), n > 4 ? n - 4 : 0u);
+    }
+    __device__ __forceinline__ void finish() {
+        if (bits > 0) emit();
+    }
+};
 
 // string_t of string i (doff d0, length n) from the ring (ring_base = global
 // position of ring byte 0)
@@ -119,6 +173,7 @@ __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t 
     return mk4(n, keep(b0, 0), keep(b1, 4), keep(b2, 8));
 }
 
+template <int BPL, bool PF>
 __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t base, uint32_t nvals,
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
                             uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err) {
@@ -203,18 +258,50 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     };
 
     // ---- 2-4. code-parallel rounds -----------------------------------------
-    for (uint32_t r0 = 0; r0 < comp_len; r0 += 1024) {
-        const uint32_t idx0 = r0 + 16 * lane;
-        const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, 16u) : 0u;
-        const v4u raw = nb ? comp[(r0 >> 4) + lane] : mk4(0, 0, 0, 0);
+    constexpr uint32_t kRound = Lds<BPL>::kRound;
+    // a lane's compressed bytes of the round starting at r0 (zeros past the end)
+    auto load_raw = [&](uint32_t r0) -> v4u {
+        const uint32_t idx0 = r0 + BPL * lane;
+        v4u x = mk4(0, 0, 0, 0);
+        if (idx0 < comp_len) {
+            if constexpr (BPL == 16) {
+                x = comp[(r0 >> 4) + lane];
+            } else {  // 8 B per lane: one dwordx2 load (the stream is 16 B aligned)
+                const v2u h = reinterpret_cast<const FLS_GLOBAL v2u *>(comp)[(r0 >> 3) + lane];
+                x = mk4(h.x, h.y, 0, 0);
+            }
+        }
+        return x;
+    };
+    // PF: the next round's bytes are loaded while this round decodes
+    v4u raw_next = load_raw(0);
+    for (uint32_t r0 = 0; r0 < comp_len; r0 += kRound) {
+        const uint32_t idx0 = r0 + BPL * lane;
+        const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, (uint32_t)BPL) : 0u;
+        v4u raw;
+        if constexpr (PF) {
+            raw = raw_next;
+            if (r0 + kRound < comp_len) raw_next = load_raw(r0 + kRound);
+        } else {
+            raw = load_raw(r0);
+        }
+        // codes and their symbol lengths / symbols, all table reads issued at once
+        uint32_t code[BPL], sl[BPL];
         bool has_esc = false;
-        for (uint32_t k = 0; k < nb; ++k) has_esc |= byte_of(raw, k) == kFsstEscape;
+#pragma unroll
+        for (uint32_t k = 0; k < BPL; ++k) {
+            code[k] = byte_of(raw, k);
+            sl[k] = k < nb ? min((uint32_t)w.len[code[k]], 8u) : 0u;
+            has_esc |= k < nb && code[k] == kFsstEscape;
+        }
         uint32_t start = 0, lane_out = 0, lane_end = 0;
-        if (__ballot(has_esc) == 0 && carry_lit == 0) {  // no escape anywhere: every code is a symbol
-            for (uint32_t k = 0; k < nb; ++k) lane_out += min((uint32_t)w.len[byte_of(raw, k)], 8u);
+        const bool plain = __ballot(has_esc) == 0 && carry_lit == 0;  // wave-uniform
+        if (plain) {  // no escape anywhere: every code is a symbol
+#pragma unroll
+            for (uint32_t k = 0; k < BPL; ++k) lane_out += sl[k];
         } else {
             uint32_t o0 = 0, o1 = 0;
-            const uint32_t e0 = simulate(w, raw, nb, 0, o0), e1 = simulate(w, raw, nb, 1, o1);
+            const uint32_t e0 = simulate<BPL>(code, sl, nb, 0, o0), e1 = simulate<BPL>(code, sl, nb, 1, o1);
             // inclusive scan of the lanes' state maps f (bit s = f(s)); apply earlier first
             uint32_t f = e0 | (e1 << 1);
 #pragma unroll
@@ -230,24 +317,39 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         }
         const uint32_t incl = scan_incl(lane_out, lane);
         const uint32_t round_total = rl(incl, 63);
+        // zero the ring dwords this round writes (OR targets), keeping the
+        // already decoded bytes below out_pos in the first one
+        const uint32_t p0 = out_pos - ring_base;
+        {
+            FLS_LDS uint32_t *r32 = reinterpret_cast<FLS_LDS uint32_t *>(w.ring);
+            const uint32_t z0 = (p0 + 3) >> 2, z1 = (p0 + round_total + 3) >> 2;
+            for (uint32_t q = z0 + lane; q < z1; q += 64) r32[q] = 0;
+            if (lane == 0 && (p0 & 3)) r32[p0 >> 2] &= (1u << (8 * (p0 & 3))) - 1u;
+        }
+        wave_sync();
         // write this lane's symbols into the ring
-        uint32_t wp = out_pos - ring_base + (incl - lane_out);
-        uint32_t st = start;
-        for (uint32_t k = 0; k < nb; ++k) {
-            const uint32_t b = byte_of(raw, k);
-            if (st) {
-                w.ring[wp++] = (uint8_t)b;
-                st = 0;
-            } else if (b == kFsstEscape) {
-                st = 1;
-            } else {
-                const uint32_t L = min((uint32_t)w.len[b], 8u);
-                const uint64_t sy = w.sym[b];
+        {
+            RingWriter rw(w.ring, p0 + (incl - lane_out));
+            if (plain) {  // sl[k] = 0 past the stream end
 #pragma unroll
-                for (uint32_t q = 0; q < 8; ++q)
-                    if (q < L) w.ring[wp + q] = (uint8_t)(sy >> (8 * q));
-                wp += L;
+                for (uint32_t k = 0; k < BPL; ++k) rw.put(w.sym[code[k]], sl[k]);
+            } else {
+                uint32_t st = start;
+#pragma unroll
+                for (uint32_t k = 0; k < BPL; ++k) {
+                    if (k < nb) {
+                        if (st) {
+                            rw.put4(code[k], 1);
+                            st = 0;
+                        } else if (code[k] == kFsstEscape) {
+                            st = 1;
+                        } else {
+                            rw.put(w.sym[code[k]], sl[k]);
+                        }
+                    }
+                }
             }
+            rw.finish();
         }
         carry_lit = rl(lane_end, 63);
         wave_sync();
@@ -295,7 +397,8 @@ __device__ __forceinline__ DevChunk load_chunk(const DevChunk *chunks, uint32_t 
 // Vectors [item0, item1) of the launch (items numbered chunk by chunk through
 // DevChunk.vec_base): the wave loads a chunk's symbol table once and decodes
 // its vectors in order.
-__device__ __attribute__((noinline)) void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t item0,
+template <int BPL, bool PF>
+__device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t item0,
                                                      uint32_t item1, uint8_t *lds_generic, uint32_t *err_generic) {
     const uint64_t cp = (uint64_t)chunks_generic;
     const DevChunk *chunks = (const DevChunk *)((uint64_t)uni((uint32_t)(cp >> 32)) << 32 | uni((uint32_t)cp));
@@ -307,7 +410,7 @@ __device__ __attribute__((noinline)) void fsst_range(const DevChunk *chunks_gene
     item1 = uni(item1);
     const uint32_t lane = __lane_id();
     Wave w;
-    w.P = reinterpret_cast<lv4 *>(L + kOffP);
+    w.P = reinterpret_cast<lv4 *>(L + kOffRing);
     w.D = reinterpret_cast<lu32 *>(L + kOffD);
     w.sym = reinterpret_cast<const FLS_LDS uint64_t *>(L + kOffSym);
     w.len = L + kOffLen;
@@ -347,7 +450,7 @@ __device__ __attribute__((noinline)) void fsst_range(const DevChunk *chunks_gene
         const uint32_t nvals = uni(meta->nvals);
         const uint32_t W = uni(min((uint32_t)meta->bw, 32u));
         const uint32_t dbytes = uni(meta->aux_count);
-        fsst_vector(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
+        fsst_vector<BPL, PF>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
                     (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
                     gptr(c.out) + 16ull * kVectorSize * v, lane, err);
         wave_sync();
@@ -355,32 +458,46 @@ __device__ __attribute__((noinline)) void fsst_range(const DevChunk *chunks_gene
     }
 }
 
-__global__ __launch_bounds__(256, 2) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                      uint32_t nitems, uint32_t *__restrict__ err) {
+template <int BPL, bool PF>
+__global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                     uint32_t nitems, uint32_t *__restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
-    const uint32_t w = uni(threadIdx.x >> 6);
-    const uint32_t nwaves = gridDim.x * kWaves, wave = blockIdx.x * kWaves + w;
+    const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
     // contiguous vector ranges per wave: a wave mostly stays inside one chunk
     const uint32_t per = (nitems + nwaves - 1) / nwaves;
     const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
-    if (i0 < i1) fsst_range(chunks, nchunks, i0, i1, lds_raw + w * kWaveLds, err);
+    if (i0 < i1) fsst_range<BPL, PF>(chunks, nchunks, i0, i1, lds_raw, err);
+}
+
+template <int BPL, bool PF>
+hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                         hipStream_t stream) {
+    const uint32_t shmem = Lds<BPL>::kWave;
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, PF>, 64, shmem) != hipSuccess)
+            per_cu = 1;
+    }
+    const int grid = std::min<int>(cus * std::max(1, per_cu), (int)nvecs);
+    if (getenv("FLS_DEBUG"))
+        fprintf(stderr, "DEBUG: fsst_kernel<%d,%d>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors\n", BPL,
+                (int)PF, grid, per_cu, shmem, nvecs);
+    hipLaunchKernelGGL((fsst_kernel<BPL, PF>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err);
+    return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                       hipStream_t stream) {
+                       hipStream_t stream, int bytes_per_lane) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
-    const uint32_t shmem = kWaves * kWaveLds;
-    int dev = 0, cus = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel, 64 * kWaves, shmem) != hipSuccess)
-            per_cu = 1;
-    }
-    const int grid = std::min<int>(cus * std::max(1, per_cu), (int)((nvecs + kWaves - 1) / kWaves));
-    hipLaunchKernelGGL(fsst_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, nvecs, d_err);
-    return hipGetLastError();
+    const bool pf = !getenv("FLS_FSST_NO_PREFETCH");  // A/B knob
+    if (bytes_per_lane == 8)
+        return pf ? launch_fsst_t<8, true>(d_chunks, nchunks, nvecs, d_err, stream)
+                  : launch_fsst_t<8, false>(d_chunks, nchunks, nvecs, d_err, stream);
+    return pf ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream)
+              : launch_fsst_t<16, false>(d_chunks, nchunks, nvecs, d_err, stream);
 }
 
 }  // namespace fls

@@ -362,8 +362,8 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // arms run on the same buffers): 0 = work queue, largest chunks first
 // (default); bit 0 = static grid-stride split; bit 1 = keep column order.
 // bit 2 = full-width register prefetch for every chunk (descriptor max_w = T).
-// bit 3 = unpack two 16-byte steps per scheduling fence (decode_kernel<2>).
-enum : int { POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_GROUP2 = 8 };
+// bit 4 = FSST rounds of 16 compressed bytes per lane instead of 8.
+enum : int { POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST16 = 16 };
 int decode_policy() {
     const char *e = getenv("FLS_DECODE_POLICY");
     return e ? atoi(e) : 0;
@@ -393,7 +393,8 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int pol
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t fsst_vecs, uint32_t *d_err,
                       const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy) {
     hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue);
-    if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, ntotal - nmain, fsst_vecs, d_err, stream);
+    if (e == hipSuccess)
+        e = launch_fsst(d_chunks + nmain, ntotal - nmain, fsst_vecs, d_err, stream, (policy & POLICY_FSST16) ? 16 : 8);
     return e;
 }
 
