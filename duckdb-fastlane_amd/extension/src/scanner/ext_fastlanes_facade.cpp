@@ -9,6 +9,7 @@
 #include <cstring>
 #include <vector>
 
+#include <algorithm>
 #include "../../../../include/flsgpu.h"
 #include "../../../../include/flswriter.h"
 #include "../gpu_devices.hpp"
@@ -189,35 +190,45 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     Impl &s = *pImpl;
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
     chunk.Flatten();
-    for (idx_t r = 0; r < chunk.size(); ++r) {
+    // column-major: append each column's slice up to the row-group boundary
+    // in bulk, then let the writer encode the full row group (column-parallel)
+    idx_t r0 = 0;
+    while (r0 < chunk.size()) {
+        const idx_t n = std::min<idx_t>(chunk.size() - r0, s.rg_rows - s.wrows);
         for (size_t c = 0; c < s.wtypes.size(); ++c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
-            const bool null = FlatVector::IsNull(v, r);  // NULLs have no encoding on this path
+            std::vector<uint8_t> &col = s.wcols[c];
             if (t.id() == LogicalTypeId::VARCHAR) {
-                if (!null) {
-                    const string_t str = FlatVector::GetData<string_t>(v)[r];
-                    s.wcols[c].insert(s.wcols[c].end(), str.GetData(), str.GetData() + str.GetSize());
+                const string_t *str = FlatVector::GetData<string_t>(v);
+                for (idx_t r = r0; r < r0 + n; ++r) {
+                    if (!FlatVector::IsNull(v, r))  // NULLs have no encoding on this path: empty string
+                        col.insert(col.end(), str[r].GetData(), str[r].GetData() + str[r].GetSize());
+                    s.woffs[c].push_back((uint32_t)col.size());
                 }
-                s.woffs[c].push_back((uint32_t)s.wcols[c].size());
-            } else {
-                // the physical bytes (FLOAT/DOUBLE bit-exact for ALP); DECIMAL widened to int64
-                const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
-                const idx_t pw = PhysicalWidth(t);
-                uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (!null) {
-                    const uint8_t *src = FlatVector::GetData<uint8_t>(v) + r * pw;
-                    if (pw < w) {  // narrow DECIMAL: sign-extend
-                        int64_t x = pw == 2 ? (int64_t)*(const int16_t *)src : (int64_t)*(const int32_t *)src;
-                        memcpy(b, &x, 8);
-                    } else {
-                        memcpy(b, src, w);
-                    }
-                }
-                s.wcols[c].insert(s.wcols[c].end(), b, b + w);
+                continue;
             }
+            // the physical bytes (FLOAT/DOUBLE bit-exact for ALP); DECIMAL widened to int64
+            const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
+            const idx_t pw = PhysicalWidth(t);
+            const uint8_t *src = FlatVector::GetData<uint8_t>(v) + r0 * pw;
+            const size_t at = col.size();
+            col.resize(at + n * w);
+            uint8_t *dst = col.data() + at;
+            if (pw == w) {
+                memcpy(dst, src, n * w);
+            } else {  // narrow DECIMAL: sign-extend
+                for (idx_t i = 0; i < n; ++i) {
+                    const int64_t x = pw == 2 ? (int64_t)((const int16_t *)src)[i] : (int64_t)((const int32_t *)src)[i];
+                    memcpy(dst + 8 * i, &x, 8);
+                }
+            }
+            for (idx_t i = 0; i < n; ++i)  // NULLs: zero bytes
+                if (FlatVector::IsNull(v, r0 + i)) memset(dst + i * w, 0, w);
         }
-        if (++s.wrows == s.rg_rows && !s.flush_rowgroup()) return false;
+        s.wrows += n;
+        r0 += n;
+        if (s.wrows == s.rg_rows && !s.flush_rowgroup()) return false;
     }
     return true;
 }
