@@ -76,6 +76,7 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
         c.name.assign((const char *)img + p + 6, nl);
         p += 6 + nl;
     }
+    if ((uint64_t)nrg * (4 + 16ull * ncols) > fend - p) return "truncated row-group descriptor";
     m.rgs.resize(nrg);
     uint64_t rows = 0;
     for (uint32_t r = 0; r < nrg; ++r) {
@@ -159,6 +160,14 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
                     uint32_t last;
                     memcpy(&last, img + ch.off + h.aux_off + 4ull * h.dict_count, 4);
                     if (need + last > h.aux_len) return "dictionary out of bounds";
+                    // entry i is bytes [off[i], off[i+1]): offsets start at 0 and never decrease
+                    uint32_t prev = 0;
+                    for (uint32_t k = 0; k <= h.dict_count; ++k) {
+                        uint32_t o;
+                        memcpy(&o, img + ch.off + h.aux_off + 4ull * k, 4);
+                        if ((k == 0 && o != 0) || o < prev) return "dictionary offsets not monotone";
+                        prev = o;
+                    }
                 } else if ((uint64_t)h.dict_count * (h.vbits / 8) > h.aux_len) {
                     return "dictionary out of bounds";
                 }
@@ -181,6 +190,16 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
         }
     }
     return "";
+}
+
+// String i of a validated VARCHAR DICT chunk (aux area: u32 offsets[n + 1],
+// then the bytes).  The offsets were checked monotone and inside the chunk.
+inline void dict_string(const uint8_t *aux, uint32_t n, uint32_t i, const uint8_t *&p, uint32_t &len) {
+    uint32_t b0, b1;
+    memcpy(&b0, aux + 4ull * i, 4);
+    memcpy(&b1, aux + 4ull * (i + 1), 4);
+    p = aux + 4ull * (n + 1) + b0;
+    len = b1 - b0;
 }
 
 }  // namespace fls

@@ -279,13 +279,12 @@ int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBu
             if (ch.hdr.enc != ENC_DICT) continue;  // FSST strings are decoded on the GPU
             const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
             const uint32_t n = ch.hdr.dict_count;
-            const char *bytes = (const char *)aux + 4ull * (n + 1);
             offs[(size_t)(r - rg0) * ncols + c] = host.size();
             for (uint32_t i = 0; i < n; ++i) {
-                uint32_t b0, b1;
-                memcpy(&b0, aux + 4ull * i, 4);
-                memcpy(&b1, aux + 4ull * (i + 1), 4);
-                host.push_back(make_string_t(bytes + b0, b1 - b0));
+                const uint8_t *p;
+                uint32_t len;
+                dict_string(aux, n, i, p, len);
+                host.push_back(make_string_t((const char *)p, len));
             }
         }
     HIP_TRY(hipSetDevice(dev));
@@ -434,12 +433,11 @@ bool term_may_match(const fls_table *t, uint32_t rg, const HostTerm &h) {
     if (h.kind == FK_STR) {
         if (ch.hdr.enc != ENC_DICT) return true;  // FSST: no statistics
         const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
-        const uint8_t *bytes = aux + 4ull * (ch.hdr.dict_count + 1);
         for (uint32_t i = 0; i < ch.hdr.dict_count; ++i) {
-            uint32_t b0, b1;
-            memcpy(&b0, aux + 4ull * i, 4);
-            memcpy(&b1, aux + 4ull * (i + 1), 4);
-            if (op_holds(h.op, cmp_bytes(bytes + b0, b1 - b0, (const uint8_t *)h.str.data(), (uint32_t)h.str.size())))
+            const uint8_t *p;
+            uint32_t len;
+            dict_string(aux, ch.hdr.dict_count, i, p, len);
+            if (op_holds(h.op, cmp_bytes(p, len, (const uint8_t *)h.str.data(), (uint32_t)h.str.size())))
                 return true;
         }
         return false;
