@@ -586,7 +586,7 @@ struct PathAlp {
 // (8 W / 64 rounded up): the register prefetch holds only that many.
 template <class Path, int L>
 __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generic, uint32_t lds_p, uint32_t lds_v,
-                                                    uint32_t v_bytes, uint32_t *err_generic) {
+                                                    uint32_t v_bytes, uint32_t *err_generic, uint32_t vrange) {
     const uint64_t cp = (uint64_t)chunk_generic;
     const FLS_GLOBAL DevChunk *cptr =
         (const FLS_GLOBAL DevChunk *)((uint64_t)uni((uint32_t)(cp >> 32)) << 32 | uni((uint32_t)cp));
@@ -614,32 +614,35 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
     gv4 *packed = reinterpret_cast<gv4 *>(gptr(c.chunk) + c.packed_off);
     gv4 *dummy = reinterpret_cast<gv4 *>(gptr(c.chunk));
     ou8 *out = gptr(c.out);
+    // this call decodes vectors [vb, ve) of the chunk (vrange = vb | ve << 8;
+    // a balanced split may cut a chunk between waves)
+    const uint32_t vb = uni(vrange) & 0xFF, ve = min(uni(vrange) >> 8, nvec);
     const uint32_t last_nvals = rl(m.nvbw, nvec - 1) & 0xFFFF;
-    const uint32_t nfull = last_nvals == kVectorSize ? nvec : nvec - 1;
+    const uint32_t nfull = (ve == nvec && last_nvals != kVectorSize) ? ve - 1 : ve;
 
     v4u r[L];
     Aux aux, aux_next;
     // aux (DELTA / RLE bases) is loaded before the packed bits of the same
     // vector: waiting for the packed bits (stage) then covers it, so no wait
     // on the aux load ever depends on the W-dependent number of packed loads
-    VecInfo cur = vec_info(m, 0);
+    VecInfo cur = vec_info(m, vb);
     aux.load(path.aux_ptr(c, cur), lane);
     prefetch<L>(packed + cur.poff16, 8 * cur.W, dummy, lane, r);
-    uint32_t v = 0;
-    if (nfull > 0) {
+    uint32_t v = vb;
+    if (vb < nfull) {
         // peeled first iteration: the loop header then only sees the steady state
         stage<L>(s.P, r, 8 * cur.W, lane);
-        VecInfo nxt = vec_info(m, nvec > 1 ? 1 : 0);
+        VecInfo nxt = vec_info(m, vb + 1 < ve ? vb + 1 : vb);
         aux_next.load(path.aux_ptr(c, nxt), lane);
         prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
         wave_sync();
-        path.template vec<true>(s, cur, aux, out, lane);
+        path.template vec<true>(s, cur, aux, out + (size_t)vb * kVectorSize * ob, lane);
         cur = nxt;
         aux = aux_next;
-        for (v = 1; v < nfull; ++v) {
+        for (v = vb + 1; v < nfull; ++v) {
             wave_sync();
             stage<L>(s.P, r, 8 * cur.W, lane);
-            nxt = vec_info(m, v + 1 < nvec ? v + 1 : v);
+            nxt = vec_info(m, v + 1 < ve ? v + 1 : v);
             aux_next.load(path.aux_ptr(c, nxt), lane);
             prefetch<L>(packed + nxt.poff16, 8 * nxt.W, dummy, lane, r);
             wave_sync();
@@ -648,7 +651,7 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
             aux = aux_next;
         }
     }
-    if (nfull < nvec) {  // partial tail vector (only the last row group of a table)
+    if (nfull < ve) {  // partial tail vector (only the last row group of a table)
         wave_sync();
         stage<L>(s.P, r, 8 * cur.W, lane);
         wave_sync();
@@ -663,26 +666,26 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
 // profiles/r1/abenv_prefetch_width_c3.txt).
 template <class Path, int L>
 __device__ __forceinline__ void call_l(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
-                                       uint32_t max_w) {
+                                       uint32_t max_w, uint32_t vr) {
     if constexpr (L > 1) {
         if (max_w <= 4 * L) {  // W <= 8 (L / 2): half as many loads suffice
-            call_l<Path, L / 2>(c, lp, lv, vb, err, max_w);
+            call_l<Path, L / 2>(c, lp, lv, vb, err, max_w, vr);
             return;
         }
     }
-    run_chunk<Path, L>(c, lp, lv, vb, err);
+    run_chunk<Path, L>(c, lp, lv, vb, err, vr);
 }
 template <class Path>
 __device__ __forceinline__ void call(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
-                                     uint32_t max_w) {
-    call_l<Path, Path::T / 8>(c, lp, lv, vb, err, max_w);
+                                     uint32_t max_w, uint32_t vr) {
+    call_l<Path, Path::T / 8>(c, lp, lv, vb, err, max_w, vr);
 }
 
 template <int OB>
 __device__ __forceinline__ void call_dict(const DevChunk *c, uint32_t lp, uint32_t lv, uint32_t vb, uint32_t *err,
-                                          uint32_t dict_count, uint32_t max_w) {
-    if (dict_count * OB + 4096 <= vb) call<PathDict<OB, true>>(c, lp, lv, vb, err, max_w);
-    else call<PathDict<OB, false>>(c, lp, lv, vb, err, max_w);
+                                          uint32_t dict_count, uint32_t max_w, uint32_t vr) {
+    if (dict_count * OB + 4096 <= vb) call<PathDict<OB, true>>(c, lp, lv, vb, err, max_w, vr);
+    else call<PathDict<OB, false>>(c, lp, lv, vb, err, max_w, vr);
 }
 
 // Next chunk of this wave: from the launch's work queue (one atomic per chunk,
@@ -698,66 +701,107 @@ __device__ __forceinline__ uint32_t next_chunk(uint32_t *queue, uint32_t prev, u
     return stride + uni(ci);
 }
 
+// Decode vectors [vr & 0xFF, vr >> 8) of one chunk: the chunk's (encoding, T,
+// output width) picks the path instantiation.
+__device__ __forceinline__ void decode_chunk(const DevChunk *cg, uint32_t lp, uint32_t lv, uint32_t v_bytes,
+                                             uint32_t *err, uint32_t vr) {
+    const FLS_GLOBAL DevChunk *c = gptr(cg);
+    const uint32_t dc = c->dict_count, mw = c->max_w;
+    const uint32_t enc = c->enc, T = c->T, ob = c->ob;
+    switch (enc) {
+    case ENC_FFOR:
+        switch (T) {
+        case 64: call<PathFfor<64>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        case 32: call<PathFfor<32>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        case 16: call<PathFfor<16>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        default: call<PathFfor<8>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        }
+        break;
+    case ENC_DELTA:
+        switch (T) {
+        case 64: call<PathDelta64>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        case 32: call<PathDeltaSmall<32>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        case 16: call<PathDeltaSmall<16>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        default: call<PathDeltaSmall<8>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        }
+        break;
+    case ENC_DICT:
+        switch (ob) {
+        case 16: call_dict<16>(cg, lp, lv, v_bytes, err, dc, mw, vr); break;
+        case 8: call_dict<8>(cg, lp, lv, v_bytes, err, dc, mw, vr); break;
+        case 4: call_dict<4>(cg, lp, lv, v_bytes, err, dc, mw, vr); break;
+        case 2: call_dict<2>(cg, lp, lv, v_bytes, err, dc, mw, vr); break;
+        default: call_dict<1>(cg, lp, lv, v_bytes, err, dc, mw, vr); break;
+        }
+        break;
+    case ENC_ALP:
+        if (T == 64) call<PathAlp<64>>(cg, lp, lv, v_bytes, err, mw, vr);
+        else call<PathAlp<32>>(cg, lp, lv, v_bytes, err, mw, vr);
+        break;
+    case ENC_RLE:
+        switch (ob) {
+        case 8: call<PathRle<8>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        case 4: call<PathRle<4>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        case 2: call<PathRle<2>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        default: call<PathRle<1>>(cg, lp, lv, v_bytes, err, mw, vr); break;
+        }
+        break;
+    default:
+        if ((threadIdx.x & 63) == 0) atomicOr(err, KERR_BAD_DESC);
+        break;
+    }
+}
+
+// vectors from position s0 to s1 (position = chunk << 7 | vector)
+__device__ __forceinline__ void decode_range(const DevChunk *chunks, uint32_t nchunks, uint32_t s0, uint32_t s1,
+                                             uint32_t lp, uint32_t lv, uint32_t v_bytes, uint32_t *err) {
+    const uint32_t ce = min(s1 >> 7, nchunks), vend = s1 & 127;
+    uint32_t vb = s0 & 127;
+    for (uint32_t ci = s0 >> 7; ci < ce || (ci == ce && ci < nchunks && vb < vend); ++ci, vb = 0) {
+        const uint32_t nvec = gptr(chunks)[ci].nvec;
+        const uint32_t ve = min(ci == ce ? vend : nvec, nvec);
+        if (vb < ve) decode_chunk(chunks + ci, lp, lv, v_bytes, err, vb | ve << 8);
+    }
+}
+
 #ifndef FLS_WAVES_PER_SIMD
 #define FLS_WAVES_PER_SIMD 4
 #endif
+// Work distribution, one of:
+//   split != NULL: balanced split (balanced_split) -- wave gw first decodes
+//     its static range [split[gw], split[gw + 1]), then pulls tail pieces p
+//     = [split[nw + 1 + p], split[nw + 2 + p]) from the queue; a chunk may be
+//     shared by several waves;
+//   queue != NULL: whole chunks, the first static, then from the work queue;
+//   neither: whole chunks, grid-stride.
 __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                         uint32_t *__restrict__ err, uint32_t p_bytes,
-                                                        uint32_t v_bytes, uint32_t *__restrict__ queue) {
+                                                        uint32_t v_bytes, uint32_t *__restrict__ queue,
+                                                        const uint32_t *__restrict__ split, uint32_t npieces) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     const uint32_t w = uni(threadIdx.x >> 6);
     const uint32_t lp = (uint32_t)(size_t)((lu8 *)lds_raw + w * (p_bytes + v_bytes));
     const uint32_t lv = lp + p_bytes;
     const uint32_t stride = gridDim.x * kWaves, first = blockIdx.x * kWaves + w;
+    if (split) {
+        const FLS_GLOBAL uint32_t *sp = gptr(split);
+        decode_range(chunks, nchunks, uni(sp[first]), uni(sp[first + 1]), lp, lv, v_bytes, err);
+        if (!queue) return;
+        const FLS_GLOBAL uint32_t *pp = sp + stride + 1;
+        for (;;) {
+            uint32_t p = 0;
+            if (__lane_id() == 0) p = atomicAdd(queue, 1u);
+            p = uni(p);
+            if (p >= npieces) break;
+            decode_range(chunks, nchunks, uni(pp[p]), uni(pp[p + 1]), lp, lv, v_bytes, err);
+        }
+        return;
+    }
     for (uint32_t ci = next_chunk(queue, UINT32_MAX, first, stride); ci < nchunks;
          ci = next_chunk(queue, ci, first, stride)) {
-        const DevChunk *cg = chunks + ci;
-        const FLS_GLOBAL DevChunk *c = gptr(cg);
-        const uint32_t nvec = c->nvec, dc = c->dict_count, mw = c->max_w;
-        const uint32_t enc = c->enc, T = c->T, ob = c->ob;
+        const uint32_t nvec = gptr(chunks)[ci].nvec;
         if (nvec == 0) continue;
-        switch (enc) {
-        case ENC_FFOR:
-            switch (T) {
-            case 64: call<PathFfor<64>>(cg, lp, lv, v_bytes, err, mw); break;
-            case 32: call<PathFfor<32>>(cg, lp, lv, v_bytes, err, mw); break;
-            case 16: call<PathFfor<16>>(cg, lp, lv, v_bytes, err, mw); break;
-            default: call<PathFfor<8>>(cg, lp, lv, v_bytes, err, mw); break;
-            }
-            break;
-        case ENC_DELTA:
-            switch (T) {
-            case 64: call<PathDelta64>(cg, lp, lv, v_bytes, err, mw); break;
-            case 32: call<PathDeltaSmall<32>>(cg, lp, lv, v_bytes, err, mw); break;
-            case 16: call<PathDeltaSmall<16>>(cg, lp, lv, v_bytes, err, mw); break;
-            default: call<PathDeltaSmall<8>>(cg, lp, lv, v_bytes, err, mw); break;
-            }
-            break;
-        case ENC_DICT:
-            switch (ob) {
-            case 16: call_dict<16>(cg, lp, lv, v_bytes, err, dc, mw); break;
-            case 8: call_dict<8>(cg, lp, lv, v_bytes, err, dc, mw); break;
-            case 4: call_dict<4>(cg, lp, lv, v_bytes, err, dc, mw); break;
-            case 2: call_dict<2>(cg, lp, lv, v_bytes, err, dc, mw); break;
-            default: call_dict<1>(cg, lp, lv, v_bytes, err, dc, mw); break;
-            }
-            break;
-        case ENC_ALP:
-            if (T == 64) call<PathAlp<64>>(cg, lp, lv, v_bytes, err, mw);
-            else call<PathAlp<32>>(cg, lp, lv, v_bytes, err, mw);
-            break;
-        case ENC_RLE:
-            switch (ob) {
-            case 8: call<PathRle<8>>(cg, lp, lv, v_bytes, err, mw); break;
-            case 4: call<PathRle<4>>(cg, lp, lv, v_bytes, err, mw); break;
-            case 2: call<PathRle<2>>(cg, lp, lv, v_bytes, err, mw); break;
-            default: call<PathRle<1>>(cg, lp, lv, v_bytes, err, mw); break;
-            }
-            break;
-        default:
-            if ((threadIdx.x & 63) == 0) atomicOr(err, KERR_BAD_DESC);
-            break;
-        }
+        decode_chunk(chunks + ci, lp, lv, v_bytes, err, nvec << 8);
     }
 }
 
@@ -770,21 +814,74 @@ int decode_grid_size(uint32_t shmem_per_block) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel, 64 * kWaves, shmem_per_block) !=
             hipSuccess)
             per_cu = 1;
+        // A/B knob: blocks per CU below what the occupancy query reports
+        if (const char *e = getenv("FLS_BLOCKS_PER_CU")) per_cu = std::min(per_cu, std::max(1, atoi(e)));
     }
     return cus * std::max(1, per_cu);
 }
 
+uint32_t decode_waves(const DecodeGeom &geom) {
+    const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
+    return (uint32_t)(geom.grid > 0 ? geom.grid : decode_grid_size(shmem)) * kWaves;
+}
+
+// Cost of one vector of chunk d in the balanced split: the bytes it moves
+// (output + packed estimate at the chunk's widest W) plus a fixed per-vector
+// term for the work that does not scale with bytes (metadata, LDS staging).
+static inline uint64_t vec_cost(const DevChunk &d) { return 1024ull * d.ob + 128ull * d.max_w + 512; }
+
+SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t static_pct, uint32_t pieces_per_wave,
+                         std::vector<uint32_t> &pos) {
+    uint64_t total = 0, nvecs = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        total += h[i].nvec * vec_cost(h[i]);
+        nvecs += h[i].nvec;
+    }
+    SplitPlan plan;
+    // no more waves than vectors (rounded to whole blocks)
+    plan.waves = (uint32_t)std::min<uint64_t>(nw, (nvecs + kWaves - 1) / kWaves * kWaves);
+    if (plan.waves == 0) plan.waves = kWaves;
+    static_pct = std::min(static_pct, 100u);
+    plan.pieces = static_pct < 100 ? plan.waves * std::max(1u, pieces_per_wave) : 0;
+    const uint64_t stat = (uint64_t)((unsigned __int128)total * static_pct / 100);
+    pos.clear();
+    pos.reserve(plan.positions());
+    // one monotone walk over the targets: static boundaries, then tail pieces
+    uint64_t acc = 0;
+    uint32_t i = 0;
+    auto at = [&](uint64_t tgt) {
+        while (i < n && acc + h[i].nvec * vec_cost(h[i]) <= tgt) {
+            acc += h[i].nvec * vec_cost(h[i]);
+            ++i;
+        }
+        pos.push_back(i < n ? (i << 7 | (uint32_t)((tgt - acc) / vec_cost(h[i]))) : n << 7);
+    };
+    // static boundaries 0..waves (the last one = where the tail starts)
+    for (uint32_t w = 0; w <= plan.waves; ++w) at((uint64_t)((unsigned __int128)stat * w / plan.waves));
+    // tail piece boundaries 0..pieces (pieces == 0: one unused entry)
+    at(stat);
+    for (uint32_t p = 1; p < plan.pieces; ++p) at(stat + (uint64_t)((unsigned __int128)(total - stat) * p / plan.pieces));
+    if (plan.pieces) pos.push_back(n << 7);
+    return plan;
+}
+
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
-                         hipStream_t stream, uint32_t *d_queue) {
+                         hipStream_t stream, uint32_t *d_queue, const uint32_t *d_split, SplitPlan plan) {
     if (nchunks == 0) return hipSuccess;
     const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
-    const int grid = std::min<int>(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), (nchunks + kWaves - 1) / kWaves);
+    int grid;
+    if (d_split) {
+        grid = (int)(plan.waves / kWaves);
+        if (!plan.pieces) d_queue = nullptr;
+    } else {
+        grid = std::min<int>(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), (nchunks + kWaves - 1) / kWaves);
+    }
     if (d_queue) {
         const hipError_t e = hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
-                       geom.p_bytes, geom.v_bytes, d_queue);
+                       geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces);
     return hipGetLastError();
 }
 

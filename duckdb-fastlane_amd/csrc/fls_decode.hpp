@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace fls {
 
@@ -43,11 +44,31 @@ struct DecodeGeom {
     int grid = 0;
 };
 
+// Balanced split of a launch's vectors (positions = chunk << 7 | vector):
+// waves + 1 static boundaries (wave w decodes [pos[w], pos[w + 1])), then
+// pieces + 1 boundaries of the tail pieces the waves pull from the work queue
+// when their static range is done.  waves == 0: no split.
+struct SplitPlan {
+    uint32_t waves = 0, pieces = 0;
+    size_t positions() const { return waves ? (size_t)waves + pieces + 2 : 0; }
+};
+
 // Launch the fused decode over every vector of nchunks chunks (no FSST).
-// d_queue (one zeroed word, may be NULL): waves take chunks from this work
-// queue in list order instead of a static grid-stride split.
+// d_split (plan.positions() positions from balanced_split, may be NULL): each
+// wave decodes its own balanced range of vectors, then tail pieces from
+// d_queue; else d_queue (one zeroed word, may be NULL): waves take whole
+// chunks from this work queue in list order; else a static grid-stride split
+// of whole chunks.
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
-                         hipStream_t stream, uint32_t *d_queue = nullptr);
+                         hipStream_t stream, uint32_t *d_queue = nullptr, const uint32_t *d_split = nullptr,
+                         SplitPlan plan = SplitPlan());
+// Waves of a resident decode launch with this LDS geometry.
+uint32_t decode_waves(const DecodeGeom &geom);
+// Split the vectors of h[0, n) over at most nw waves: static_pct % of the
+// estimated bytes as equal static ranges, the rest as pieces_per_wave * waves
+// equal tail pieces (dynamic: the waves that finish first take them).
+SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t static_pct, uint32_t pieces_per_wave,
+                         std::vector<uint32_t> &pos);
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
 // bytes_per_lane: compressed bytes a lane decodes per round (8 or 16).

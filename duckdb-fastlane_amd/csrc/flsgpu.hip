@@ -246,7 +246,9 @@ struct fls_table {
     std::vector<uint8_t> dev_mask;     // column mask h_chunks was built for
     uint32_t dev_nmain = 0;            // h_chunks[0, dev_nmain) main kernel, the rest FSST
     int dev_policy = -1;               // decode_policy() h_chunks was ordered for
+    int dev_lpolicy = 0;               // ... and the launch policy it resolved to (launch_policy)
     uint32_t dev_fsst_vecs = 0;        // vectors of the FSST chunks
+    SplitPlan dev_split;               // balanced split after h_chunks on the device (waves 0: none)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
@@ -362,10 +364,38 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // (default); bit 0 = static grid-stride split; bit 1 = keep column order.
 // bit 2 = full-width register prefetch for every chunk (descriptor max_w = T).
 // bit 4 = FSST rounds of 16 compressed bytes per lane instead of 8.
-enum : int { POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST16 = 16 };
+// bit 5 = balanced static split of vectors over the resident waves, chunks in
+// file (row-group-major) order (balanced_split).  bit 6 = work queue even for
+// small launches (launch_policy).
+enum : int {
+    POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST16 = 16, POLICY_BALANCED = 32,
+    POLICY_QUEUE = 64
+};
+// Balanced-split knobs, folded into the policy word (so a change rebuilds the
+// cached launch list): FLS_STATIC_PCT = % of the bytes split statically
+// (bits 8-15, default 100), FLS_TAIL_PIECES = tail pieces per wave for the
+// rest (bits 16-23, default 2).
 int decode_policy() {
     const char *e = getenv("FLS_DECODE_POLICY");
-    return e ? atoi(e) : 0;
+    const char *sp = getenv("FLS_STATIC_PCT");
+    const char *tp = getenv("FLS_TAIL_PIECES");
+    const int pct = sp ? std::min(100, std::max(0, atoi(sp))) : 100;
+    const int pieces = tp ? std::min(255, std::max(1, atoi(tp))) : 2;
+    return (e ? (atoi(e) & 0xFF) : 0) | pct << 8 | pieces << 16;
+}
+
+// Policy for one launch: the default (no distribution bits) switches to the
+// balanced split when the launch has fewer main-kernel chunks than resident
+// waves (the scan pipeline's 8-row-group batches: ~120 chunks for ~4,096
+// waves), where whole-chunk work items would leave most waves idle.  Large
+// launches keep the work queue: same-buffer A/B on SF100 lineitem, c3 and c4
+// found the split no faster than the queue (profiles/r1/abenv_bal_*.txt).
+int launch_policy(int policy, const std::vector<DevChunk> &v, DecodeGeom &geom) {
+    if (policy & (POLICY_STATIC | POLICY_BALANCED | POLICY_QUEUE)) return policy;
+    size_t nmain = 0;
+    for (const DevChunk &d : v) nmain += d.enc != ENC_FSST;
+    if (geom.grid <= 0) geom.grid = decode_grid_size(4 * (geom.p_bytes + geom.v_bytes));
+    return nmain < decode_waves(geom) ? (policy | POLICY_BALANCED) : policy;
 }
 
 // FSST chunks go last (their own kernel) and get their vector numbering;
@@ -374,7 +404,11 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int pol
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
     if (policy & POLICY_FULL_PREFETCH)
         for (auto it = v.begin(); it != mid; ++it) it->max_w = it->T;
-    if (!(policy & (POLICY_STATIC | POLICY_NO_LPT))) {
+    if (policy & POLICY_BALANCED) {
+        // file order = row-group-major: every wave's range mixes all columns
+        // (paths that run slower per byte are spread over the waves)
+        std::stable_sort(v.begin(), mid, [](const DevChunk &a, const DevChunk &b) { return a.chunk < b.chunk; });
+    } else if (!(policy & (POLICY_STATIC | POLICY_NO_LPT))) {
         // largest output first: the work queue then ends the launch on small chunks
         std::stable_sort(v.begin(), mid, [](const DevChunk &a, const DevChunk &b) {
             return (uint64_t)a.nvec * a.ob > (uint64_t)b.nvec * b.ob;
@@ -389,9 +423,25 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int pol
     return (uint32_t)(mid - v.begin());
 }
 
+// Append the balanced split of the main chunks to the descriptor list (as
+// extra DevChunk slots, so it uploads with it); plan.waves == 0 when the
+// policy does not split.
+SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const DecodeGeom &geom, int policy) {
+    if (!(policy & POLICY_BALANCED) || nmain == 0) return SplitPlan();
+    std::vector<uint32_t> pos;
+    const SplitPlan plan = balanced_split(list.data(), nmain, decode_waves(geom), (policy >> 8) & 0xFF,
+                                          (policy >> 16) & 0xFF, pos);
+    const size_t k = list.size();
+    list.resize(k + (pos.size() * 4 + sizeof(DevChunk) - 1) / sizeof(DevChunk));
+    memcpy(list.data() + k, pos.data(), pos.size() * 4);
+    return plan;
+}
+
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t fsst_vecs, uint32_t *d_err,
-                      const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy) {
-    hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue);
+                      const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy, SplitPlan plan) {
+    const uint32_t *d_split = plan.waves ? reinterpret_cast<const uint32_t *>(d_chunks + ntotal) : nullptr;
+    hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue,
+                                 d_split, plan);
     if (e == hipSuccess)
         e = launch_fsst(d_chunks + nmain, ntotal - nmain, fsst_vecs, d_err, stream, (policy & POLICY_FSST16) ? 16 : 8);
     return e;
@@ -688,15 +738,18 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         }
     }
     uint32_t fsst_vecs = 0;
-    const int policy = decode_policy();
+    const int policy = launch_policy(decode_policy(), list, bc.geom);
     const uint32_t nmain = order_for_launch(list, &fsst_vecs, policy);
     const size_t k = list.size();
-    HIP_TRY(sl.h_chunks.alloc(k));
-    HIP_TRY(sl.d_chunks.alloc(d.dev, k));
-    if (k) memcpy(sl.h_chunks.p, list.data(), k * sizeof(DevChunk));
-    HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, k * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
+    const SplitPlan plan = append_split(list, nmain, bc.geom, policy);
+    const size_t kk = list.size();
+    HIP_TRY(sl.h_chunks.alloc(kk));
+    HIP_TRY(sl.d_chunks.alloc(d.dev, kk));
+    if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
+    HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(sl.queue.alloc(d.dev, 1));
-    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream, sl.queue.p, policy));
+    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
+                       plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
     if (filtered) {
@@ -1154,14 +1207,18 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
                                                sh.h_heap[c].p ? sh.h_heap[c].p + ho : nullptr));
             }
         }
-        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst_vecs, policy);
+        const int lpol = launch_policy(policy, chunks, bc.geom);
+        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst_vecs, lpol);
         t->dev_policy = policy;
+        t->dev_lpolicy = lpol;
+        const size_t k = chunks.size();
+        t->dev_split = append_split(chunks, t->dev_nmain, bc.geom, lpol);
         HIP_TRY(hipStreamSynchronize(t->stream));
         HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
         HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
+        chunks.resize(k);
         t->h_chunks.swap(chunks);
         t->dev_mask = mask;
-        bc.geom.grid = decode_grid_size(4 * (bc.geom.p_bytes + bc.geom.v_bytes));
         t->last_bytes = bc;
     }
     if (t->ev_used + 2 > t->ev_pool.size()) {
@@ -1176,7 +1233,7 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     HIP_TRY(hipEventRecord(e0, t->stream));
     HIP_TRY(sh.queue.alloc(sh.dev, 1));
     HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst_vecs, sh.err.p,
-                       t->last_bytes.geom, t->stream, sh.queue.p, policy));
+                       t->last_bytes.geom, t->stream, sh.queue.p, t->dev_lpolicy, t->dev_split));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;
     t->launched = true;

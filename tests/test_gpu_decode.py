@@ -236,3 +236,34 @@ def test_small_rowgroups_decode_and_scan(fl, ref, gpu, monkeypatch, rgsz):
         g = first // rgsz
         assert np.array_equal(cols[0], rf.decode(0, g)) and np.array_equal(cols[1], rf.decode(1, g))
         assert fl.string_t_decode(cols[2]) == rf.strings(rf.decode(2, g))
+
+
+# Work distribution policies (FLS_DECODE_POLICY, read per decode call): the
+# default (0: small launches like this one take the balanced split), the work
+# queue of whole chunks (64), static grid-stride (1), the balanced split of
+# vector ranges (32: a chunk may be cut between waves, including inside the
+# ragged last row group) with and without dynamic tail pieces.  Every policy
+# must decode identically.
+@pytest.mark.parametrize("env", [
+    {"FLS_DECODE_POLICY": "0"},
+    {"FLS_DECODE_POLICY": "64"},
+    {"FLS_DECODE_POLICY": "1"},
+    {"FLS_DECODE_POLICY": "32"},
+    {"FLS_DECODE_POLICY": "32", "FLS_STATIC_PCT": "70", "FLS_TAIL_PIECES": "3"},
+    {"FLS_DECODE_POLICY": "32", "FLS_STATIC_PCT": "0", "FLS_TAIL_PIECES": "1"},
+    {"FLS_DECODE_POLICY": "32", "FLS_BLOCKS_PER_CU": "1"},
+], ids=["default", "queue", "static", "balanced", "balanced_tail70", "tail_only", "balanced_1blk"])
+def test_work_distribution_policies(fl, ref, gpu, monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(77)
+    n = 5 * 65536 + 1234
+    a = rng.integers(-50, 50, n).astype(np.int32)
+    b = np.cumsum(rng.integers(0, 4, n)).astype(np.int64)
+    s = [["N", "O", "DELIVER IN PERSON"][i] for i in rng.integers(0, 3, n)]
+    r = (b // 100).astype(np.int16)
+    img = fl.write_image([("a", fl.INT32, a, fl.ENC_FFOR), ("b", fl.INT64, b, fl.ENC_DELTA),
+                          ("s", fl.VARCHAR, s, fl.ENC_DICT), ("r", fl.INT16, r, fl.ENC_RLE),
+                          ("d", fl.INT32, (a % 7).astype(np.int32), fl.ENC_DICT)])
+    _check_image(fl, ref, img)
+    _check_image(fl, ref, img, [1, 2])
