@@ -74,6 +74,11 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 // bytes_per_lane: compressed bytes a lane decodes per round (8 or 16).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, int bytes_per_lane = 8);
+// Launch the string-parallel FSST decode over nchunks FSST chunks whose
+// strings are all <= 255 bytes (DevChunk.vbits = 1), nvecs vectors numbered
+// through DevChunk.vec_base (fls_fsst.hip).
+hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                          hipStream_t stream);
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
 // LDS bytes per wave the v2 kernel needs for one chunk (given its max width)

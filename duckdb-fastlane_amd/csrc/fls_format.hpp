@@ -102,15 +102,22 @@ inline uint64_t alp_aux_bytes(uint32_t exc, uint32_t vbits) { return ((2ull * ex
 //   chunk (sum of the vectors' 16-byte-padded decompressed sizes);
 //   per vector: FFOR stream (T=32) of the decompressed string lengths;
 //   VecMeta.aux_count = decompressed bytes of the vector;
-//   VecMeta.aux_off -> FsstVecHeader, then the vector's compressed byte stream
-//   (all its strings' codes concatenated; code 255 = next byte is a literal).
+//   VecMeta.aux_off -> FsstVecHeader, then the FFOR stream (T=32, clen_w bits,
+//   base clen_base: 128 * clen_w bytes) of the strings' COMPRESSED lengths,
+//   then the vector's compressed byte stream (every string compressed on its
+//   own, codes concatenated; code 255 = next byte is a literal, never the
+//   last code of a string).  The compressed lengths let a decoder start every
+//   string independently (fls_fsst.hip's string-parallel path).
 constexpr uint32_t kFsstTableBytes = 256 * 8 + 256;
 constexpr uint32_t kFsstEscape = 255;
 struct FsstVecHeader {        // 16 B
     uint32_t heap_off;        // start of this vector's strings in the chunk heap (16-aligned)
-    uint32_t comp_len;        // compressed bytes following the header
-    uint32_t reserved[2];
+    uint32_t comp_len;        // compressed bytes (after the compressed-length stream)
+    uint32_t clen_base;       // FOR base of the compressed string lengths
+    uint32_t clen_w;          // their bit width (<= 32)
 };
+// compressed stream of a vector, relative to its FsstVecHeader
+inline uint64_t fsst_stream_off(const FsstVecHeader &h) { return sizeof(FsstVecHeader) + 128ull * h.clen_w; }
 static_assert(sizeof(FsstVecHeader) == 16, "FSST vector header is 16 B");
 
 static_assert(sizeof(ChunkHeader) == 64, "chunk header is 64 B");

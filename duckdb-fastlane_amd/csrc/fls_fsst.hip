@@ -150,19 +150,13 @@ struct RingWriter {
     }
 };
 
-// string_t of string i (doff d0, length n) from the ring (ring_base = global
-// position of ring byte 0)
-__device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t n, uint32_t ring_base,
-                                           uint64_t ptr_base) {
-    const uint32_t x = d0 - ring_base;
-    const lu32 *r32 = reinterpret_cast<const lu32 *>(w.ring) + (x >> 2);
+// string_t of a string of n bytes at ring byte x, host pointer p
+__device__ __forceinline__ v4u make_record_at(const lu8 *ring, uint32_t x, uint32_t n, uint64_t p) {
+    const lu32 *r32 = reinterpret_cast<const lu32 *>(ring) + (x >> 2);
     const uint32_t sh = x & 3;
     const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2], w3 = r32[3];
     const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-    if (n > 12) {
-        const uint64_t p = ptr_base + d0;
-        return mk4(n, b0, (uint32_t)p, (uint32_t)(p >> 32));
-    }
+    if (n > 12) return mk4(n, b0, (uint32_t)p, (uint32_t)(p >> 32));
     const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
     const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
     auto keep = [n](uint32_t word, uint32_t first) -> uint32_t {  // zero bytes at index >= n
@@ -171,6 +165,13 @@ __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t 
         return word & ((1u << (8 * (n - first))) - 1u);
     };
     return mk4(n, keep(b0, 0), keep(b1, 4), keep(b2, 8));
+}
+
+// string_t of string i (doff d0, length n) from the ring (ring_base = global
+// position of ring byte 0)
+__device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t n, uint32_t ring_base,
+                                           uint64_t ptr_base) {
+    return make_record_at(w.ring, d0 - ring_base, n, ptr_base + d0);
 }
 
 template <int BPL, bool PF>
@@ -221,11 +222,11 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     const uint32_t total = uni(w.D[1024]);
     if (total != dbytes) bad = true;
     const FLS_GLOBAL FsstVecHeader *hp = reinterpret_cast<const FLS_GLOBAL FsstVecHeader *>(vh);
-    const uint32_t heap_off = uni(hp->heap_off), comp_len = uni(hp->comp_len);
+    const uint32_t heap_off = uni(hp->heap_off), comp_len = uni(hp->comp_len), clen_w = uni(min(hp->clen_w, 32u));
     const uint32_t hlim = min((dbytes + 15) & ~15u, heap_bytes > heap_off ? heap_bytes - heap_off : 0u);
     FLS_GLOBAL uint8_t *vheap = heap + heap_off;
     const uint64_t ptr_base = heap_host + heap_off;
-    gv4 *comp = reinterpret_cast<gv4 *>(vh + sizeof(FsstVecHeader));
+    gv4 *comp = reinterpret_cast<gv4 *>(vh + sizeof(FsstVecHeader) + 128 * clen_w);
 
     uint32_t out_pos = 0, ring_base = 0, carry_lit = 0, next_str = 0;
     // strings whose leading bytes are all decoded get their string_t
@@ -487,7 +488,299 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
     return hipGetLastError();
 }
 
+// ============================================================================
+// String-parallel path (chunks whose strings are all <= 255 bytes, both
+// decompressed and compressed: the host marks them, DevChunk.vbits = 1).
+// Every string is compressed on its own and the vector stores the strings'
+// compressed lengths, so lane j decodes string s + j of a round by itself: no
+// escape-state composition, no per-code wave scans.  Per vector:
+//   1. both length streams (FFOR, W <= 8) are unpacked into u8 arrays;
+//   2. rounds of up to 64 strings (as many as fit the LDS rings: inclusive
+//      wave scans of the lengths + ballot): the round's compressed bytes are
+//      staged into the IN ring with 16 B coalesced loads, the OUT ring's
+//      dwords for the round are zeroed, then every lane walks its string 4
+//      codes at a time (one unaligned dword of codes, the 4 symbol / length
+//      lookups issued together) and ORs the symbols into OUT as aligned
+//      dwords (a string's edge dwords are shared with its neighbours);
+//   3. the round's string_t records (64 x 16 B) and the complete 16 B blocks
+//      of OUT go to HBM; the unfinished tail (< 16 B) moves to the ring start.
+// Corrupt lengths (a string that expands to more or fewer bytes than its
+// length, a truncated escape, streams that do not add up) are clamped to the
+// string's own bytes and reported through KERR_FSST.
+constexpr uint32_t kSpIncap = 1536;   // IN ring: compressed bytes of a round (+16 B slack)
+constexpr uint32_t kSpOutcap = 2560;  // OUT ring: decoded bytes of a round incl. the carried tail
+constexpr uint32_t kSpSym = 0, kSpLen = 2048, kSpDL = 2304, kSpCL = kSpDL + 1024, kSpIn = kSpCL + 1024;
+constexpr uint32_t kSpOut = kSpIn + kSpIncap + 16;
+constexpr uint32_t kSpWave = kSpOut + kSpOutcap + 16;
+static_assert(kSpIncap >= 128 * 8 + 128 && kSpIncap >= 255 + 16 && kSpOutcap >= 255 + 16, "SP ring sizes");
+static_assert(kSpIn % 16 == 0 && kSpOut % 16 == 0 && kSpWave % 16 == 0, "SP LDS layout alignment");
+
+struct SpWave {
+    const FLS_LDS uint64_t *sym;
+    const lu8 *len;
+    lu8 *DL, *CL, *IN, *OUT;
+};
+
+// u8 lengths of the vector (base + FFOR(T=32, W <= 8), zero past nvals); the
+// packed bits are staged in the IN ring
+__device__ __forceinline__ void unpack_u8(const SpWave &w, gu8 *packed, uint32_t W, uint32_t base, uint32_t nvals,
+                                          lu8 *dst, uint32_t lane) {
+    lv4 *P = reinterpret_cast<lv4 *>(w.IN);
+    const uint32_t n16 = 8 * W;
+    gv4 *pk = reinterpret_cast<gv4 *>(packed);
+    for (uint32_t i = lane; i < n16; i += 64) P[i] = pk[i];
+    if (lane < 8) P[n16 + lane] = mk4(0, 0, 0, 0);
+    wave_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t ci = lane + 64 * j;
+        const v4u v = add_base<32>(unpack_chunk<32>(P, W, ci), base);
+        const uint32_t b0 = 4 * ci < nvals ? v.x & 255 : 0, b1 = 4 * ci + 1 < nvals ? v.y & 255 : 0;
+        const uint32_t b2 = 4 * ci + 2 < nvals ? v.z & 255 : 0, b3 = 4 * ci + 3 < nvals ? v.w & 255 : 0;
+        reinterpret_cast<lu32 *>(dst)[ci] = b0 | b1 << 8 | b2 << 16 | b3 << 24;
+    }
+    wave_sync();
+}
+
+// Wave-64 maximum (DPP, like scan_incl), valid in every lane after readlane
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return rl(x, 63);
+}
+
+// The round's strings, one per lane: codes IN[cb, cb + cl) -> OUT[wp, wp + dl).
+// Branch-free: the wave walks the round's longest compressed string (maxcl,
+// uniform) 4 codes per step and every lane predicates its codes with
+// selects, not branches (divergent control flow cost more scalar exec-mask
+// instructions than the decode itself).  A lane assembles its bytes in a
+// 64-bit accumulator and ORs them into the zeroed OUT ring as aligned qwords
+// (a string's edge qwords are shared with its neighbours); a qword is OR-ed
+// every step, zero when the accumulator is not yet full.  The symbol table is
+// sanitised (symbols masked to their length, the escape code = {0, 0}).
+// Returns false on corrupt input (wrong byte count, truncated escape).
+__device__ __forceinline__ bool sp_decode(const SpWave &w, uint32_t cb, uint32_t cl, uint32_t wp, uint32_t dl,
+                                          uint32_t maxcl) {
+    const lu32 *in32 = reinterpret_cast<const lu32 *>(w.IN);
+    FLS_LDS uint64_t *o64 = reinterpret_cast<FLS_LDS uint64_t *>(w.OUT);
+    constexpr uint32_t kLastQ = (kSpOutcap + 16) / 8 - 1;
+    const uint32_t ce = cb + cl;
+    uint32_t q = wp >> 3, bits = 8 * (wp & 7), pos = 0;
+    uint64_t acc = 0;
+    bool lit = false;
+    for (uint32_t it = 0; it < maxcl; it += 4) {
+        const uint32_t c = cb + it;
+        const uint32_t x = __builtin_amdgcn_alignbyte(in32[(c >> 2) + 1], in32[c >> 2], c & 3);
+        const uint32_t nk = c < ce ? min(ce - c, 4u) : 0u;
+        uint32_t b[4], sl[4];
+        uint64_t sy[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            b[k] = (x >> (8 * k)) & 255;
+            sy[k] = w.sym[b[k]];
+            sl[k] = w.len[b[k]];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const bool valid = k < nk, l = lit;
+            lit = valid && !l && b[k] == kFsstEscape;
+            uint64_t v = l ? (uint64_t)b[k] : sy[k];
+            uint32_t n = l ? 1u : sl[k];
+            v = valid ? v : 0ull;
+            n = valid ? n : 0u;
+            pos += n;
+            const uint64_t lo = v << bits;
+            const uint64_t hi = bits ? v >> (64 - bits) : 0ull;
+            acc |= lo;
+            const uint32_t nb = bits + 8 * n;
+            const bool e = nb >= 64;
+            __hip_atomic_fetch_or(o64 + min(q, kLastQ), e ? acc : 0ull, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+            q += e ? 1u : 0u;
+            acc = e ? hi : acc;
+            bits = nb & 63;
+        }
+    }
+    __hip_atomic_fetch_or(o64 + min(q, kLastQ), acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return !lit && pos == dl;
+}
+
+__device__ void fsst_vector_sp(const SpWave &w, gu8 *packed_vec, uint32_t W, uint32_t base, uint32_t nvals,
+                               uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
+                               uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err) {
+    const FLS_GLOBAL FsstVecHeader *hp = reinterpret_cast<const FLS_GLOBAL FsstVecHeader *>(vh);
+    const uint32_t heap_off = uni(hp->heap_off), comp_len = uni(hp->comp_len);
+    const uint32_t cbase = uni(hp->clen_base), cw = uni(min(hp->clen_w, 8u));
+    bool bad = false;
+    // ---- 1. both length streams -> u8 arrays --------------------------------
+    unpack_u8(w, packed_vec, min(W, 8u), base, nvals, w.DL, lane);
+    unpack_u8(w, vh + sizeof(FsstVecHeader), cw, cbase, nvals, w.CL, lane);
+    const uint32_t hlim = min((dbytes + 15) & ~15u, heap_bytes > heap_off ? heap_bytes - heap_off : 0u);
+    FLS_GLOBAL uint8_t *vheap = heap + heap_off;
+    const uint64_t ptr_base = heap_host + heap_off;
+    gv4 *cs = reinterpret_cast<gv4 *>(vh + sizeof(FsstVecHeader) + 128 * cw);
+    const uint32_t lim16 = (comp_len + 15) >> 4;
+    lu32 *o32 = reinterpret_cast<lu32 *>(w.OUT);
+    lv4 *in16 = reinterpret_cast<lv4 *>(w.IN);
+    const lv4 *out16 = reinterpret_cast<const lv4 *>(w.OUT);
+    // stream complete 16 B blocks [ring_base, upto) of OUT to the heap
+    auto flush = [&](uint32_t ring_base, uint32_t upto) {
+        const uint32_t nblk = (upto - ring_base) >> 4;
+        for (uint32_t q = lane; q < nblk; q += 64) {
+            const uint32_t g = ring_base + 16 * q;
+            if (g + 16 <= hlim) *reinterpret_cast<ov4 *>(vheap + g) = out16[q];
+            else bad = true;
+        }
+    };
+    // ---- 2-3. rounds of up to 64 strings, one per lane ----------------------
+    uint32_t s = 0, dpos = 0, cpos = 0, ring_base = 0;
+    while (s < nvals) {
+        const uint32_t i = s + lane;
+        const uint32_t dl = i < nvals ? (uint32_t)w.DL[i] : 0u, cl = i < nvals ? (uint32_t)w.CL[i] : 0u;
+        const uint32_t dinc = scan_incl(dl, lane), cinc = scan_incl(cl, lane);
+        const uint32_t tail = dpos - ring_base, cskew = cpos & 15;
+        const bool fits = i < nvals && tail + dinc <= kSpOutcap && cskew + cinc <= kSpIncap;
+        const uint64_t m = __ballot(fits);
+        const uint32_t nr = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);  // >= 1: one string always fits
+        const uint32_t rd = rl(dinc, nr - 1), rc = rl(cinc, nr - 1);
+        // stage the round's compressed bytes (from the 16 B block holding cpos)
+        const uint32_t g16 = cpos >> 4, n16 = (cskew + rc + 15) >> 4;
+        for (uint32_t q = lane; q < n16; q += 64) in16[q] = g16 + q < lim16 ? cs[g16 + q] : mk4(0, 0, 0, 0);
+        if (lane == 0) in16[n16] = mk4(0, 0, 0, 0);  // a lane's dword read may pass the end by one dword
+        // zero the OUT dwords the round ORs into, keeping the carried tail bytes
+        {
+            const uint32_t z0 = (tail + 3) >> 2, z1 = (tail + rd + 3) >> 2;
+            for (uint32_t q = z0 + lane; q < z1; q += 64) o32[q] = 0;
+            if (lane == 0 && (tail & 3)) o32[tail >> 2] &= (1u << (8 * (tail & 3))) - 1u;
+        }
+        wave_sync();
+        const uint32_t wp = tail + dinc - dl;
+        {
+            const bool act = lane < nr;
+            const uint32_t acl = act ? cl : 0u;
+            const uint32_t maxcl = wave_max(acl);
+            if (!sp_decode(w, act ? cskew + cinc - cl : 0u, acl, act ? wp : 0u, act ? dl : 0u, maxcl)) bad = true;
+        }
+        wave_sync();
+        // string_t records of the round's strings (64 x 16 B = one 1 KiB store)
+        if (lane < nr)
+            *reinterpret_cast<ov4 *>(out + 16ull * i) = make_record_at(w.OUT, wp, dl, ptr_base + (dpos + dinc - dl));
+        const uint32_t new_base = (dpos + rd) & ~15u;
+        flush(ring_base, new_base);
+        wave_sync();
+        // move the unfinished tail (< 16 B) to the ring start
+        const uint32_t src = (new_base - ring_base) >> 2;
+        uint32_t t = 0;
+        if (lane < 4) t = o32[src + lane];
+        wave_sync();
+        if (lane < 4) o32[lane] = t;
+        wave_sync();
+        dpos += rd;
+        cpos += rc;
+        s += nr;
+        ring_base = new_base;
+    }
+    if (dpos != dbytes || cpos != comp_len) bad = true;
+    // zero the padding of the last block, then flush it
+    const uint32_t end = (dpos + 15) & ~15u;
+    if (lane < 16 && dpos + lane < end) w.OUT[dpos - ring_base + lane] = 0;
+    wave_sync();
+    flush(ring_base, end);
+    if (bad) atomicOr(err, KERR_FSST);
+}
+
+// Vectors [item0, item1) of the launch's string-parallel chunks (numbered
+// through DevChunk.vec_base); a chunk's symbol table is staged once, each
+// symbol masked to its length (so OR-ing whole symbols is exact) and the
+// escape code's entry emptied.
+__device__ __forceinline__ void fsst_sp_range(const DevChunk *chunks, uint32_t nchunks, uint32_t item0, uint32_t item1,
+                                              lu8 *L, uint32_t *err) {
+    const uint32_t lane = __lane_id();
+    SpWave w;
+    w.sym = reinterpret_cast<const FLS_LDS uint64_t *>(L + kSpSym);
+    w.len = L + kSpLen;
+    w.DL = L + kSpDL;
+    w.CL = L + kSpCL;
+    w.IN = L + kSpIn;
+    w.OUT = L + kSpOut;
+    uint32_t lo = 0, hi = nchunks;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (uni(gptr(chunks + mid)->vec_base) <= item0) lo = mid;
+        else hi = mid;
+    }
+    uint32_t ci = lo;
+    DevChunk c = load_chunk(chunks, ci);
+    bool have_table = false;
+    for (uint32_t item = item0; item < item1;) {
+        const uint32_t v = item - uni(c.vec_base);
+        if (v >= uni(c.nvec)) {
+            if (++ci >= nchunks) break;
+            c = load_chunk(chunks, ci);
+            have_table = false;
+            continue;
+        }
+        gu8 *chunk = gptr(c.chunk);
+        gu8 *aux = chunk + c.aux_off;
+        if (!have_table) {
+            wave_sync();
+            const FLS_GLOBAL uint64_t *gs = reinterpret_cast<const FLS_GLOBAL uint64_t *>(aux);
+            FLS_LDS uint64_t *ls = reinterpret_cast<FLS_LDS uint64_t *>(L + kSpSym);
+            for (uint32_t k = lane; k < 256; k += 64) {
+                const uint32_t n = k == kFsstEscape ? 0u : min((uint32_t)aux[8 * 256 + k], 8u);
+                const uint64_t sy = gs[k];
+                ls[k] = n >= 8 ? sy : sy & ((1ull << (8 * n)) - 1);
+                L[kSpLen + k] = (uint8_t)n;
+            }
+            wave_sync();
+            have_table = true;
+        }
+        const FLS_GLOBAL VecMeta *meta = reinterpret_cast<const FLS_GLOBAL VecMeta *>(chunk + c.meta_off) + v;
+        const uint32_t poff = uni((uint32_t)meta->packed_off);
+        const uint32_t base = uni((uint32_t)meta->for_base);
+        const uint32_t aoff = uni((uint32_t)meta->aux_off);
+        const uint32_t nvals = uni(meta->nvals);
+        const uint32_t W = uni((uint32_t)meta->bw);
+        const uint32_t dbytes = uni(meta->aux_count);
+        fsst_vector_sp(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
+                       (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
+                       gptr(c.out) + 16ull * kVectorSize * v, lane, err);
+        wave_sync();
+        ++item;
+    }
+}
+
+__global__ __launch_bounds__(64) void fsst_sp_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+                                                      uint32_t nitems, uint32_t *__restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
+    const uint32_t per = (nitems + nwaves - 1) / nwaves;
+    const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
+    if (i0 < i1) fsst_sp_range(chunks, uni(nchunks), uni(i0), uni(i1), (lu8 *)(size_t)(uint32_t)(size_t)lds_raw, err);
+}
+
 }  // namespace
+
+hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                          hipStream_t stream) {
+    if (nchunks == 0 || nvecs == 0) return hipSuccess;
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_sp_kernel, 64, kSpWave) != hipSuccess)
+            per_cu = 1;
+    }
+    const int grid = std::min<int>(cus * std::max(1, per_cu), (int)nvecs);
+    if (getenv("FLS_DEBUG"))
+        fprintf(stderr, "DEBUG: fsst_sp_kernel: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors\n", grid, per_cu,
+                kSpWave, nvecs);
+    hipLaunchKernelGGL(fsst_sp_kernel, dim3(grid), dim3(64), kSpWave, stream, d_chunks, nchunks, nvecs, d_err);
+    return hipGetLastError();
+}
 
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, int bytes_per_lane) {

@@ -139,8 +139,8 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
                     if (vm.aux_off % 16 || vm.aux_off < kFsstTableBytes || vm.aux_off + sizeof(fh) > h.aux_len)
                         return "FSST vector out of bounds";
                     memcpy(&fh, img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
-                    if (vm.aux_off + sizeof(fh) + fh.comp_len > h.aux_len || fh.heap_off % 16 ||
-                        fh.heap_off + (uint64_t)vm.aux_count > h.reserved1)
+                    if (fh.clen_w > 32 || vm.aux_off + fsst_stream_off(fh) + fh.comp_len > h.aux_len ||
+                        fh.heap_off % 16 || fh.heap_off + (uint64_t)vm.aux_count > h.reserved1)
                         return "FSST vector out of bounds";
                 }
             }

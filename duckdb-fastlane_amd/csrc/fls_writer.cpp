@@ -463,14 +463,17 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
     memcpy(table.data() + 8 * 256, st.len, 256);
     const uint32_t nvec = (n + 1023) / 1024;
     std::vector<VecOut> vecs(nvec);
-    uint64_t lens[1024], u[1024];
+    uint64_t lens[1024], clens[1024], u[1024];
     uint64_t heap = 0;
     std::vector<uint8_t> comp;
     for (uint32_t k = 0; k < nvec; ++k) {
         const uint32_t b = k * 1024, vn = std::min<uint32_t>(1024, n - b);
         comp.clear();
-        for (uint32_t i = 0; i < vn; ++i)
-            st.compress((const uint8_t *)bytes + offs[b + i], offs[b + i + 1] - offs[b + i], comp);
+        for (uint32_t i = 0; i < 1024; ++i) {
+            const size_t c0 = comp.size();
+            if (i < vn) st.compress((const uint8_t *)bytes + offs[b + i], offs[b + i + 1] - offs[b + i], comp);
+            clens[i] = comp.size() - c0;
+        }
         for (uint32_t i = 0; i < 1024; ++i) lens[i] = i < vn ? offs[b + i + 1] - offs[b + i] : 0;
         const uint64_t dbytes = offs[b + vn] - offs[b];
         int64_t base;
@@ -486,9 +489,14 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
         FsstVecHeader vh{};
         vh.heap_off = (uint32_t)heap;
         vh.comp_len = (uint32_t)comp.size();
-        o.aux.resize(sizeof(vh) + comp.size());
+        int64_t cbase;
+        const int Wc = ffor_prepare(32, clens, cbase, u);
+        vh.clen_base = (uint32_t)cbase;
+        vh.clen_w = (uint32_t)Wc;
+        o.aux.assign(fsst_stream_off(vh) + comp.size(), 0);
         memcpy(o.aux.data(), &vh, sizeof(vh));
-        if (!comp.empty()) memcpy(o.aux.data() + sizeof(vh), comp.data(), comp.size());
+        pack(32, Wc, u, o.aux.data() + sizeof(vh));
+        if (!comp.empty()) memcpy(o.aux.data() + fsst_stream_off(vh), comp.data(), comp.size());
         heap += (dbytes + 15) & ~15ull;
     }
     return assemble_chunk(ENC_FSST, 32, 0, true, n, vecs, table, (uint32_t)st.n, heap);

@@ -122,6 +122,16 @@ struct fls_connection {
 
 namespace {
 
+// Device images are allocated this much past their last chunk: kernels read
+// whole 16 B blocks of a stream whose last block may end inside it.
+constexpr uint64_t kImagePad = 256;
+
+// FSST chunks of a launch: string-parallel (nsp chunks, sp_vecs vectors), then
+// code-parallel (cp_vecs vectors)
+struct FsstCounts {
+    uint32_t nsp = 0, sp_vecs = 0, cp_vecs = 0;
+};
+
 // Per-chunk algorithmic byte accounting (roofline numerator).
 struct ByteCount {
     uint64_t values = 0, packed = 0, meta = 0, out = 0;
@@ -247,7 +257,7 @@ struct fls_table {
     uint32_t dev_nmain = 0;            // h_chunks[0, dev_nmain) main kernel, the rest FSST
     int dev_policy = -1;               // decode_policy() h_chunks was ordered for
     int dev_lpolicy = 0;               // ... and the launch policy it resolved to (launch_policy)
-    uint32_t dev_fsst_vecs = 0;        // vectors of the FSST chunks
+    FsstCounts dev_fsst;               // FSST chunks of h_chunks
     SplitPlan dev_split;               // balanced split after h_chunks on the device (waves 0: none)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -322,15 +332,22 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
         bc->out += (uint64_t)h.nvals * 16 + h.reserved1;
         bc->meta += 32ull * h.nvec + kFsstTableBytes;
         const uint8_t *meta = t->img + ch.off + h.meta_off;
+        bool sp = true;
         for (uint32_t v = 0; v < h.nvec; ++v) {
             VecMeta vm;
             memcpy(&vm, meta + 32ull * v, 32);
             FsstVecHeader fh;
             memcpy(&fh, t->img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
-            bc->packed += 128ull * vm.bw + fh.comp_len;
+            bc->packed += 128ull * vm.bw + 128ull * fh.clen_w + fh.comp_len;
             bc->meta += sizeof(fh);
+            // string-parallel kernel iff every string of the chunk is <= 255
+            // bytes, decompressed and compressed (bounds from the two FFOR streams)
+            const uint64_t dmax = (uint64_t)vm.for_base + (vm.bw >= 32 ? 0xFFFFFFFFull : (1ull << vm.bw) - 1);
+            const uint64_t cmax = (uint64_t)fh.clen_base + (fh.clen_w >= 32 ? 0xFFFFFFFFull : (1ull << fh.clen_w) - 1);
+            if (vm.for_base < 0 || dmax > 255 || cmax > 255) sp = false;
         }
-        return d;  // separate kernel, fixed LDS layout
+        d.vbits = sp ? 1 : 0;
+        return d;  // separate kernels, fixed LDS layouts
     }
     bc->out += (uint64_t)h.nvals * d.ob;
     bc->meta += 32ull * h.nvec;
@@ -366,10 +383,11 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // bit 4 = FSST rounds of 16 compressed bytes per lane instead of 8.
 // bit 5 = balanced static split of vectors over the resident waves, chunks in
 // file (row-group-major) order (balanced_split).  bit 6 = work queue even for
-// small launches (launch_policy).
+// small launches (launch_policy).  bit 7 = every FSST chunk on the
+// code-parallel kernel.
 enum : int {
     POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST16 = 16, POLICY_BALANCED = 32,
-    POLICY_QUEUE = 64
+    POLICY_QUEUE = 64, POLICY_FSST_CP = 128
 };
 // Balanced-split knobs, folded into the policy word (so a change rebuilds the
 // cached launch list): FLS_STATIC_PCT = % of the bytes split statically
@@ -398,10 +416,14 @@ int launch_policy(int policy, const std::vector<DevChunk> &v, DecodeGeom &geom) 
     return nmain < decode_waves(geom) ? (policy | POLICY_BALANCED) : policy;
 }
 
-// FSST chunks go last (their own kernel) and get their vector numbering;
-// returns how many lead (main kernel) and the FSST vector count
-uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int policy) {
+// FSST chunks go last (their own kernels: string-parallel ones first, then
+// code-parallel ones, each group numbering its vectors through vec_base);
+// returns how many lead (main kernel) and the FSST counts
+uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int policy) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
+    if (policy & POLICY_FSST_CP)
+        for (auto it = mid; it != v.end(); ++it) it->vbits = 0;
+    auto sp_end = std::stable_partition(mid, v.end(), [](const DevChunk &d) { return d.vbits == 1; });
     if (policy & POLICY_FULL_PREFETCH)
         for (auto it = v.begin(); it != mid; ++it) it->max_w = it->T;
     if (policy & POLICY_BALANCED) {
@@ -414,12 +436,16 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, uint32_t *fsst_vecs, int pol
             return (uint64_t)a.nvec * a.ob > (uint64_t)b.nvec * b.ob;
         });
     }
-    uint32_t nv = 0;
-    for (auto it = mid; it != v.end(); ++it) {
-        it->vec_base = nv;
-        nv += it->nvec;
+    *fc = FsstCounts();
+    fc->nsp = (uint32_t)(sp_end - mid);
+    for (auto it = mid; it != sp_end; ++it) {
+        it->vec_base = fc->sp_vecs;
+        fc->sp_vecs += it->nvec;
     }
-    *fsst_vecs = nv;
+    for (auto it = sp_end; it != v.end(); ++it) {
+        it->vec_base = fc->cp_vecs;
+        fc->cp_vecs += it->nvec;
+    }
     return (uint32_t)(mid - v.begin());
 }
 
@@ -437,13 +463,16 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
     return plan;
 }
 
-hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, uint32_t fsst_vecs, uint32_t *d_err,
-                      const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy, SplitPlan plan) {
+hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
+                      uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
+                      SplitPlan plan) {
     const uint32_t *d_split = plan.waves ? reinterpret_cast<const uint32_t *>(d_chunks + ntotal) : nullptr;
     hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue,
                                  d_split, plan);
+    if (e == hipSuccess) e = launch_fsst_sp(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream);
     if (e == hipSuccess)
-        e = launch_fsst(d_chunks + nmain, ntotal - nmain, fsst_vecs, d_err, stream, (policy & POLICY_FSST16) ? 16 : 8);
+        e = launch_fsst(d_chunks + nmain + fc.nsp, ntotal - nmain - fc.nsp, fc.cp_vecs, d_err, stream,
+                        (policy & POLICY_FSST16) ? 16 : 8);
     return e;
 }
 
@@ -692,7 +721,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     // 1. H2D of the batch's compressed bytes
     uint64_t lo, hi;
     rg_byte_range(t->meta, sl.rg0, sl.rg0 + sl.nrg, lo, hi);
-    HIP_TRY(sl.d_in.alloc(d.dev, hi - lo));
+    HIP_TRY(sl.d_in.alloc(d.dev, hi - lo + kImagePad));
     sl.in_base = lo;
     const uint8_t *src = t->img + lo;
     if (!t->registered) {
@@ -737,9 +766,9 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                                          sl.heap_bytes[c] ? sl.h_heap[c].p + ho : nullptr));
         }
     }
-    uint32_t fsst_vecs = 0;
+    FsstCounts fsst;
     const int policy = launch_policy(decode_policy(), list, bc.geom);
-    const uint32_t nmain = order_for_launch(list, &fsst_vecs, policy);
+    const uint32_t nmain = order_for_launch(list, &fsst, policy);
     const size_t k = list.size();
     const SplitPlan plan = append_split(list, nmain, bc.geom, policy);
     const size_t kk = list.size();
@@ -748,7 +777,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(sl.queue.alloc(d.dev, 1));
-    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst_vecs, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
+    HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
                        plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
@@ -1143,7 +1172,7 @@ int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
     uint64_t lo, hi;
     rg_byte_range(t->meta, rg_begin, rg_end, lo, hi);
     sh.base = lo;
-    HIP_TRY(sh.img.alloc(dev, hi - lo));
+    HIP_TRY(sh.img.alloc(dev, hi - lo + kImagePad));
     HIP_TRY(hipMemcpy(sh.img.p, t->img + lo, hi - lo, hipMemcpyHostToDevice));
     rc = build_strtabs(t, dev, rg_begin, rg_end, sh.strtab, sh.strtab_off);
     if (rc) return rc;
@@ -1208,7 +1237,7 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
             }
         }
         const int lpol = launch_policy(policy, chunks, bc.geom);
-        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst_vecs, lpol);
+        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst, lpol);
         t->dev_policy = policy;
         t->dev_lpolicy = lpol;
         const size_t k = chunks.size();
@@ -1232,7 +1261,7 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
     HIP_TRY(sh.queue.alloc(sh.dev, 1));
-    HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst_vecs, sh.err.p,
+    HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst, sh.err.p,
                        t->last_bytes.geom, t->stream, sh.queue.p, t->dev_lpolicy, t->dev_split));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;

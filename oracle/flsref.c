@@ -23,7 +23,9 @@
  *     (position, original value) are patched in;
  *   - FSST (Boncz, Neumann, Leis, VLDB 2020) for VARCHAR: a string is a run
  *     of byte codes, code c < 255 expands to symbol[c] (1..8 bytes), code 255
- *     is followed by one literal byte.
+ *     is followed by one literal byte; every string is compressed on its
+ *     own and a vector stores its strings' compressed lengths (FFOR), so the
+ *     checker expands and bounds-checks string by string.
  * It is written as plain scalar loops on purpose: it is the checker, not the
  * thing measured (besides the cpu_baseline leg of bench.py).
  */
@@ -413,16 +415,26 @@ int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, u
         const uint32_t vn = rd16(vm_p + 24), W = vm_p[26], dbytes = rd32(vm_p + 28);
         if (W > 32 || vn > 1024) return -1;
         flsref_unpack(32, (int)W, packed + poff, u);
+        /* FsstVecHeader: heap_off, comp_len, clen_base, clen_w; then the FFOR
+         * stream of the compressed string lengths; then the code stream */
         const uint8_t *vh = aux + aoff;
-        const uint32_t clen = rd32(vh + 4);
-        if (o + dbytes > cap) return -1;
-        if (fsst_expand(aux, vh + 16, clen, heap + o, dbytes) != (int64_t)dbytes) return -1;
-        uint64_t sum = 0;
+        const uint32_t clen = rd32(vh + 4), cbase = rd32(vh + 8), cw = rd32(vh + 12);
+        if (cw > 32 || o + dbytes > cap) return -1;
+        uint64_t cu[1024];
+        flsref_unpack(32, (int)cw, vh + 16, cu);
+        const uint8_t *cs = vh + 16 + 128 * (size_t)cw;
+        /* every string is compressed on its own: expand string by string */
+        uint64_t sum = 0, cpos = 0;
         for (uint32_t i = 0; i < vn; ++i) {
-            sum += (for_base + u[i]) & 0xFFFFFFFFull;
+            const uint32_t dl = (uint32_t)((for_base + u[i]) & 0xFFFFFFFFull);
+            const uint32_t cl = (uint32_t)((cbase + cu[i]) & 0xFFFFFFFFull);
+            if (cpos + cl > clen || sum + dl > dbytes) return -1;
+            if (fsst_expand(aux, cs + cpos, cl, heap + o + sum, dl) != (int64_t)dl) return -1;
+            cpos += cl;
+            sum += dl;
             offs[row + i + 1] = (uint32_t)(o + sum);
         }
-        if (sum != dbytes) return -1;
+        if (sum != dbytes || cpos != clen) return -1;
         o += dbytes;
         row += vn;
     }

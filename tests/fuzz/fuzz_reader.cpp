@@ -47,7 +47,7 @@ static void walk(const std::vector<uint8_t> &img, const FileMeta &m) {
                 if (h.enc == ENC_FSST) {
                     FsstVecHeader fh;
                     memcpy(&fh, aux + vm.aux_off, sizeof(fh));
-                    touch(aux + vm.aux_off + sizeof(fh), fh.comp_len);
+                    touch(aux + vm.aux_off + sizeof(fh), fsst_stream_off(fh) - sizeof(fh) + fh.comp_len);
                 }
             }
             if (h.enc == ENC_DICT) {

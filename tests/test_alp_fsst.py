@@ -271,3 +271,67 @@ def test_gpu_fsst_escape_at_round_boundary(fl, ref, gpu, monkeypatch, maxsym):
     img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
     t, st, out = gpu_decode_all(fl, img)
     assert fl.string_t_decode(out[0]) == s
+
+
+# ---- FSST string-parallel kernel (chunks whose strings are <= 255 bytes) ----
+def _sp_tables(fl, rng):
+    """(name, strings) cases around the string-parallel kernel's eligibility:
+    every string <= 255 bytes decompressed AND compressed, per chunk."""
+    n = 70000
+    text = fsst_text(n, rng)
+    esc = [b"\xff" * int(k) for k in rng.integers(0, 128, 3000)]              # 2 compressed bytes per byte
+    bin127 = [bytes(rng.integers(0, 256, int(k), dtype=np.uint8).tolist()) for k in rng.integers(0, 128, 3000)]
+    edge = [b"", b"q", b"a" * 255, b"", b"lorem ipsum " * 21] * 300          # 255-byte strings, empties
+    # row group 0 gets one 300-byte string (code-parallel), row group 1 stays short (string-parallel)
+    mixed = fsst_text(65536, rng)
+    mixed[777] = "long " * 60
+    mixed += fsst_text(9000, rng)
+    return [("text", text), ("escapes", esc), ("binary127", bin127), ("edge255", edge), ("mixed_rg", mixed)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["0", "128"], ids=["string_parallel", "code_parallel"])
+def test_gpu_fsst_string_and_code_parallel_agree(fl, ref, gpu, monkeypatch, capfd, policy):
+    monkeypatch.setenv("FLS_DECODE_POLICY", policy)
+    monkeypatch.setenv("FLS_DEBUG", "1")
+    for name, s in _sp_tables(fl, np.random.default_rng(21)):
+        img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
+        t, st, out = gpu_decode_all(fl, img)
+        rf = ref.RefFile(img)
+        assert_strings_equal(fl, rf, 0, out[0])
+        err = capfd.readouterr().err
+        # which kernels ran: every case but binary-heavy long strings is string-parallel by default
+        assert ("fsst_sp_kernel" in err) == (policy == "0"), name
+        assert ("fsst_kernel<" in err) == (policy == "128" or name == "mixed_rg"), name
+
+
+@pytest.mark.gpu
+def test_gpu_fsst_string_parallel_scan_pipeline(fl, ref, gpu, monkeypatch):
+    """Scan batches (balanced main kernel + string-parallel FSST) deliver the
+    oracle's strings row group by row group."""
+    monkeypatch.setenv("FLS_SCAN_BATCH", "2")
+    img = fl.gen_image("lineitem_full", 0.05)
+    rf = ref.RefFile(img)
+    t = fl.Connection([0]).read_image(img)
+    for first, got in t.scan(cols=[15]):
+        assert fl.string_t_decode(got[15]) == rf.strings_rg(15, first // 65536)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field", ["clen_base", "comp_len"])
+def test_gpu_fsst_corrupt_compressed_lengths_reported(fl, ref, gpu, field):
+    """A compressed-length stream that disagrees with the code stream (the
+    string-parallel kernel's string starts) is clamped and reported."""
+    s = fsst_text(5000, np.random.default_rng(6))
+    raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
+    off = _chunk_header(raw)
+    aux_off = struct.unpack_from("<Q", raw, off + 32)[0]
+    meta = off + struct.unpack_from("<Q", raw, off + 16)[0]
+    vh = off + aux_off + struct.unpack_from("<Q", raw, meta + 16)[0]
+    at = vh + (8 if field == "clen_base" else 4)
+    struct.pack_into("<I", raw, at, struct.unpack_from("<I", raw, at)[0] - 1)
+    t = fl.Connection().read_image(bytes(raw))
+    t.device_upload()
+    t.device_decode()
+    with pytest.raises(fl.FlsError, match="corrupt"):
+        t.device_sync()
