@@ -559,8 +559,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 // selects, not branches (divergent control flow cost more scalar exec-mask
 // instructions than the decode itself).  A lane assembles its bytes in a
 // 64-bit accumulator and ORs them into the zeroed OUT ring as aligned qwords
-// (a string's edge qwords are shared with its neighbours); a qword is OR-ed
-// every step, zero when the accumulator is not yet full.  The symbol table is
+// (a string's edge qwords are shared with its neighbours); the accumulator is
+// OR-ed into its qword every step, full or not.  The symbol table is
 // sanitised (symbols masked to their length, the escape code = {0, 0}).
 // Returns false on corrupt input (wrong byte count, truncated escape).
 __device__ __forceinline__ bool sp_decode(const SpWave &w, uint32_t cb, uint32_t cl, uint32_t wp, uint32_t dl,
@@ -576,30 +576,32 @@ __device__ __forceinline__ bool sp_decode(const SpWave &w, uint32_t cb, uint32_t
         const uint32_t c = cb + it;
         const uint32_t x = __builtin_amdgcn_alignbyte(in32[(c >> 2) + 1], in32[c >> 2], c & 3);
         const uint32_t nk = c < ce ? min(ce - c, 4u) : 0u;
+        // codes past the string's end read as the escape code, whose table
+        // entry is {0, 0} (and which then starts no literal)
         uint32_t b[4], sl[4];
         uint64_t sy[4];
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-            b[k] = (x >> (8 * k)) & 255;
+            b[k] = k < nk ? (x >> (8 * k)) & 255 : kFsstEscape;
             sy[k] = w.sym[b[k]];
             sl[k] = w.len[b[k]];
         }
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-            const bool valid = k < nk, l = lit;
-            lit = valid && !l && b[k] == kFsstEscape;
-            uint64_t v = l ? (uint64_t)b[k] : sy[k];
-            uint32_t n = l ? 1u : sl[k];
-            v = valid ? v : 0ull;
-            n = valid ? n : 0u;
+            const bool l = lit;
+            lit = k < nk && !l && b[k] == kFsstEscape;
+            const uint64_t v = l ? (uint64_t)b[k] : sy[k];
+            const uint32_t n = l ? 1u : sl[k];
             pos += n;
-            const uint64_t lo = v << bits;
-            const uint64_t hi = bits ? v >> (64 - bits) : 0ull;
+            // v << bits spans qwords q (lo) and q + 1 (hi); (v >> 1) >> (63 - bits)
+            // is v >> (64 - bits) without the bits == 0 case
+            const uint64_t lo = v << bits, hi = (v >> 1) >> (63 - bits);
             acc |= lo;
+            // OR the accumulator every step (OR is idempotent): no select on
+            // whether qword q is complete
+            __hip_atomic_fetch_or(o64 + min(q, kLastQ), acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             const uint32_t nb = bits + 8 * n;
             const bool e = nb >= 64;
-            __hip_atomic_fetch_or(o64 + min(q, kLastQ), e ? acc : 0ull, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
             q += e ? 1u : 0u;
             acc = e ? hi : acc;
             bits = nb & 63;
@@ -616,9 +618,6 @@ __device__ void fsst_vector_sp(const SpWave &w, gu8 *packed_vec, uint32_t W, uin
     const uint32_t heap_off = uni(hp->heap_off), comp_len = uni(hp->comp_len);
     const uint32_t cbase = uni(hp->clen_base), cw = uni(min(hp->clen_w, 8u));
     bool bad = false;
-    // ---- 1. both length streams -> u8 arrays --------------------------------
-    unpack_u8(w, packed_vec, min(W, 8u), base, nvals, w.DL, lane);
-    unpack_u8(w, vh + sizeof(FsstVecHeader), cw, cbase, nvals, w.CL, lane);
     const uint32_t hlim = min((dbytes + 15) & ~15u, heap_bytes > heap_off ? heap_bytes - heap_off : 0u);
     FLS_GLOBAL uint8_t *vheap = heap + heap_off;
     const uint64_t ptr_base = heap_host + heap_off;
@@ -637,6 +636,21 @@ __device__ void fsst_vector_sp(const SpWave &w, gu8 *packed_vec, uint32_t W, uin
         }
     };
     // ---- 2-3. rounds of up to 64 strings, one per lane ----------------------
+    // The IN window of a round (kSpIncap bytes from the 16 B block holding its
+    // first code) is loaded into registers one round ahead, so the round only
+    // waits for loads issued before the previous round's decode.
+    constexpr uint32_t kInBlocks = kSpIncap / 16;
+    static_assert(kInBlocks > 64 && kInBlocks <= 128, "two 16 B prefetch loads per lane");
+    v4u pf0 = mk4(0, 0, 0, 0), pf1 = mk4(0, 0, 0, 0);
+    auto prefetch_in = [&](uint32_t from) {
+        const uint32_t g = from >> 4;
+        pf0 = g + lane < lim16 ? cs[g + lane] : mk4(0, 0, 0, 0);
+        pf1 = lane + 64 < kInBlocks && g + lane + 64 < lim16 ? cs[g + lane + 64] : mk4(0, 0, 0, 0);
+    };
+    prefetch_in(0);
+    // ---- 1. both length streams -> u8 arrays (the first window in flight) ---
+    unpack_u8(w, packed_vec, min(W, 8u), base, nvals, w.DL, lane);
+    unpack_u8(w, vh + sizeof(FsstVecHeader), cw, cbase, nvals, w.CL, lane);
     uint32_t s = 0, dpos = 0, cpos = 0, ring_base = 0;
     while (s < nvals) {
         const uint32_t i = s + lane;
@@ -647,10 +661,11 @@ __device__ void fsst_vector_sp(const SpWave &w, gu8 *packed_vec, uint32_t W, uin
         const uint64_t m = __ballot(fits);
         const uint32_t nr = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);  // >= 1: one string always fits
         const uint32_t rd = rl(dinc, nr - 1), rc = rl(cinc, nr - 1);
-        // stage the round's compressed bytes (from the 16 B block holding cpos)
-        const uint32_t g16 = cpos >> 4, n16 = (cskew + rc + 15) >> 4;
-        for (uint32_t q = lane; q < n16; q += 64) in16[q] = g16 + q < lim16 ? cs[g16 + q] : mk4(0, 0, 0, 0);
-        if (lane == 0) in16[n16] = mk4(0, 0, 0, 0);  // a lane's dword read may pass the end by one dword
+        // stage the round's compressed bytes (prefetched window), then start
+        // loading the next round's window
+        in16[lane] = pf0;
+        if (lane + 64 < kInBlocks) in16[lane + 64] = pf1;
+        prefetch_in(cpos + rc);
         // zero the OUT dwords the round ORs into, keeping the carried tail bytes
         {
             const uint32_t z0 = (tail + 3) >> 2, z1 = (tail + rd + 3) >> 2;
