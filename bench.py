@@ -79,12 +79,14 @@ def measure_traffic(args):
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
         except Exception as e:  # noqa: BLE001 - report, never fail the bench on profiling
             return None, f"rocprofv3 {ctr} pass failed: {e}"
-        per = {}  # kernel -> samples (a step is decode_kernel, plus fsst_kernel for FSST columns)
+        per = {}  # kernel -> samples (a step is decode_kernel, plus the FSST kernels for FSST columns)
         for path in Path(d).rglob("*counter_collection.csv"):
             for r in csv.DictReader(open(path)):
                 k = r.get("Kernel_Name", "")
-                if ("decode_kernel" in k or "fsst_kernel" in k) and r.get("Counter_Name") == ctr:
-                    per.setdefault("fsst" if "fsst_kernel" in k else "decode", []).append(float(r["Counter_Value"]))
+                kind = ("fsst_sp" if "fsst_sp_kernel" in k else "fsst_cp" if "fsst_kernel" in k
+                        else "decode" if "decode_kernel" in k else None)
+                if kind and r.get("Counter_Name") == ctr:
+                    per.setdefault(kind, []).append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if "decode" not in per:
             return None, f"no {ctr} samples"

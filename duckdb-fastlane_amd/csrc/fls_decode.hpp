@@ -71,9 +71,10 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
                          std::vector<uint32_t> &pos);
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
-// bytes_per_lane: compressed bytes a lane decodes per round (8 or 16).
+// bytes_per_lane: compressed bytes a lane decodes per round (8 or 16);
+// small: every string of these chunks is <= 255 bytes (DevChunk.vbits = 1).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                       hipStream_t stream, int bytes_per_lane = 8);
+                       hipStream_t stream, int bytes_per_lane = 8, bool small = false);
 // Launch the string-parallel FSST decode over nchunks FSST chunks whose
 // strings are all <= 255 bytes (DevChunk.vbits = 1), nvecs vectors numbered
 // through DevChunk.vec_base (fls_fsst.hip).

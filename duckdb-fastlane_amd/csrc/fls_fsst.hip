@@ -54,21 +54,25 @@ using lu32 = FLS_LDS uint32_t;
 // many waves as its LDS fits).  BPL = compressed bytes per lane per round
 // (a round decodes 64 * BPL codes); the LDS ring must hold one round's output
 // (<= 8 B per code) plus a carried tail.  Per-wave LDS layout (bytes, all
-// 16-aligned); the packed string lengths of step 1 are staged in the ring,
-// which is free until the rounds start.
-constexpr uint32_t kOffD = 0;                   // doff[1025] (u32)
-constexpr uint32_t kOffSym = 4112;              // u64 symbol[256]
-constexpr uint32_t kOffLen = kOffSym + 2048;    // u8 length[256]
-constexpr uint32_t kOffRing = kOffLen + 256;    // decoded bytes (and step 1's packed lengths)
-constexpr uint32_t kPackedMax = 128 * 32 + 128; // lengths FFOR-packed at W <= 32, plus a zero row
-template <int BPL>
+// 16-aligned): the vector's string lengths -- SMALL chunks (every string
+// <= 255 bytes, DevChunk.vbits = 1) keep them as u8[1024], others as exclusive
+// u32 offsets doff[1025] -- then u64 symbol[256], u8 length[256] and the ring.
+// The packed string lengths of step 1 are staged in the ring, which is free
+// until the rounds start.
+template <int BPL, bool SMALL>
 struct Lds {
+    static constexpr uint32_t kOffD = 0;
+    static constexpr uint32_t kOffSym = SMALL ? 1024 : 4112;
+    static constexpr uint32_t kOffLen = kOffSym + 2048;
+    static constexpr uint32_t kOffRing = kOffLen + 256;
+    static constexpr uint32_t kPackedMax = SMALL ? 128 * 8 + 128 : 128 * 32 + 128;  // W <= 8 | 32, + zero row
     static constexpr uint32_t kRound = 64 * BPL;
-    static constexpr uint32_t kRing = (kRound * 8 + 64) > kPackedMax ? kRound * 8 + 64 : kPackedMax;
+    // 2 KiB holds a round's output at up to ~4 bytes per code; a round that
+    // decodes to more is written in parts (lanes [l0, l1) at a time)
+    static constexpr uint32_t kRing = kPackedMax > 2048 + 64 ? kPackedMax : 2048 + 64;
     static constexpr uint32_t kWave = kOffRing + kRing;
+    static_assert(kOffSym % 16 == 0 && kOffRing % 16 == 0 && kWave % 16 == 0, "LDS layout alignment");
 };
-static_assert(kOffSym % 16 == 0 && kOffRing % 16 == 0 && Lds<16>::kWave % 16 == 0 && Lds<8>::kWave % 16 == 0,
-              "LDS layout alignment");
 
 __device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
 __device__ __forceinline__ uint32_t byte_of(const v4u &r, uint32_t k) {
@@ -95,60 +99,91 @@ struct Wave {
     lu8 *ring;
 };
 
-// 2-state escape automaton over a lane's codes from entry state s: returns the
-// exit state, adds the produced bytes to out (sl[k] = symbol length of code k)
-template <int BPL>
-__device__ __forceinline__ uint32_t simulate(const uint32_t (&code)[BPL], const uint32_t (&sl)[BPL], uint32_t nb,
-                                             uint32_t s, uint32_t &out) {
-#pragma unroll
-    for (uint32_t k = 0; k < BPL; ++k) {
-        if (k < nb) {
-            if (s) {
-                out += 1;
-                s = 0;
-            } else if (code[k] == kFsstEscape) {
-                s = 1;
-            } else {
-                out += sl[k];
-            }
-        }
-    }
-    return s;
+// Escape state entering a lane's first code (the parity rule).  Code 255 is
+// the escape (the next byte is a literal).  After any byte other than 0xFF
+// the decoder is in the normal state (that byte was a symbol code, or the
+// literal of an escape), so the state entering byte p is the parity of the
+// run of 0xFF bytes that ends at p - 1.  A lane holding some non-0xFF byte
+// therefore leaves its segment in state (length of its trailing 0xFF run) & 1
+// whatever its entry state; a lane of BPL (even) 0xFF bytes leaves it in its
+// entry state.  So a lane's entry state is the exit state of the nearest
+// earlier lane holding a non-0xFF byte (one ballot + one ds_bpermute), or the
+// state the previous round ended in.  No 2-state maps, no per-round wave
+// composition, no special path for rounds that contain escapes.
+__device__ __forceinline__ uint32_t entry_state(bool has_plain, uint32_t exit_if_plain, uint32_t carry,
+                                                uint32_t lane) {
+    const uint64_t m = __ballot(has_plain) & ((1ull << lane) - 1ull);  // lane 0: 0
+    const uint32_t src = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
+    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)exit_if_plain);
+    return m ? v : carry;
 }
 
-// Appends a lane's decoded bytes to the ring as aligned dwords.  A lane's
-// output is one contiguous byte range whose edge dwords may be shared with the
-// neighbouring lanes' output, so every dword is OR-ed (ds_or_b32) into the
-// ring region zeroed for the round: one instruction shape, no per-lane branch
-// on which dword is an edge.
-struct RingWriter {
-    FLS_LDS uint32_t *ring32;
-    uint64_t acc;   // pending bytes, low first
-    uint32_t bits;  // valid bits in acc (< 32 between appends)
-    uint32_t d;     // dword index of acc's first byte
-    __device__ __forceinline__ RingWriter(lu8 *ring, uint32_t wp)
-        : ring32(reinterpret_cast<FLS_LDS uint32_t *>(ring)), acc(0), bits(8 * (wp & 3)), d(wp >> 2) {}
-    __device__ __forceinline__ void emit() {
-        __hip_atomic_fetch_or(ring32 + d, (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        ++d;
-        acc >>= 32;
-        bits -= 32;
-    }
-    // append n <= 4 bytes (low bytes of x); n = 0 appends nothing
-    __device__ __forceinline__ void put4(uint32_t x, uint32_t n) {
-        x &= n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u;
-        acc |= (uint64_t)x << bits;
-        bits += 8 * n;
-        if (bits >= 32) emit();
-    }
-    __device__ __forceinline__ void put(uint64_t sym, uint32_t n) {  // n <= 8
-        put4((uint32_t)sym, min(n, 4u));
-        put4((uint32_t)(sym >> 32), n > 4 ? n - 4 : 0u);
+// Appends symbols to the zeroed ring at byte wp through a 64-bit accumulator
+// that is OR-ed (ds_or_b64) into its aligned qword after every symbol: OR is
+// idempotent, so no select on whether the qword is complete; a lane's edge
+// qwords are shared with its neighbours' output and OR-ing merges them.
+// Symbols must be masked to their length (the staged table is).  Measured
+// against OR-ing every symbol into both qwords it spans (no accumulator,
+// fewer VALU, twice the ds_or_b64): 1-2 % faster on l_comment.
+struct QwordWriter {
+    FLS_LDS uint64_t *o64;
+    uint64_t acc;
+    uint32_t q, bits;
+    __device__ __forceinline__ QwordWriter(lu8 *ring, uint32_t wp)
+        : o64(reinterpret_cast<FLS_LDS uint64_t *>(ring)), acc(0), q(wp >> 3), bits(8 * (wp & 7)) {}
+    __device__ __forceinline__ void put(uint64_t v, uint32_t n) {  // n <= 8 bytes
+        // v << bits spans qwords q (lo) and q + 1 (hi); (v >> 1) >> (63 - bits)
+        // is v >> (64 - bits) without the bits == 0 case
+        const uint64_t lo = v << bits, hi = (v >> 1) >> (63 - bits);
+        acc |= lo;
+        __hip_atomic_fetch_or(o64 + q, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t nb = bits + 8 * n;
+        const bool e = nb >= 64;
+        q += e ? 1u : 0u;
+        acc = e ? hi : acc;
+        bits = nb & 63;
     }
     __device__ __forceinline__ void finish() {
-        if (bits > 0) emit();
+        __hip_atomic_fetch_or(o64 + q, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 };
+
+// One round's codes of this lane (nb valid bytes of raw) from the escape
+// state the previous round ended in (carry): the symbols v[k] and their byte
+// counts n[k] (a literal is one byte, the escape code none -- its staged table
+// entry is {0, 0} -- and a symbol its length; nothing past the stream end,
+// FULL = no lane of the round reaches it).  Returns the lane's byte count;
+// st_out = the state after its last valid byte (held across an empty tail).
+template <int BPL, bool FULL>
+__device__ __forceinline__ uint32_t lane_codes(const Wave &w, const v4u &raw, uint32_t nb, uint32_t carry,
+                                               uint32_t lane, uint64_t (&v)[BPL], uint32_t (&n)[BPL],
+                                               uint32_t &st_out) {
+    uint32_t code[BPL], sl[BPL];
+    uint64_t sy[BPL];
+    int32_t last = -1;  // last non-0xFF byte of the lane's segment
+#pragma unroll
+    for (uint32_t k = 0; k < BPL; ++k) {  // all table reads issued together
+        code[k] = byte_of(raw, k);
+        sy[k] = w.sym[code[k]];
+        sl[k] = w.len[code[k]];
+        if ((FULL || k < nb) && code[k] != kFsstEscape) last = (int32_t)k;
+    }
+    const uint32_t end = FULL ? (uint32_t)BPL : nb;
+    uint32_t st = entry_state(last >= 0, ((int32_t)end - 1 - last) & 1, carry, lane);
+    uint32_t out = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BPL; ++k) {
+        const bool lit = st != 0, in = FULL || k < nb;
+        const uint64_t vk = lit ? (uint64_t)code[k] : sy[k];
+        const uint32_t nk = lit ? 1u : sl[k];
+        v[k] = in ? vk : 0ull;
+        n[k] = in ? nk : 0u;
+        st = in ? (uint32_t)(!lit && code[k] == kFsstEscape) : st;
+        out += n[k];
+    }
+    st_out = st;
+    return out;
+}
 
 // string_t of a string of n bytes at ring byte x, host pointer p
 __device__ __forceinline__ v4u make_record_at(const lu8 *ring, uint32_t x, uint32_t n, uint64_t p) {
@@ -174,29 +209,44 @@ __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t 
     return make_record_at(w.ring, d0 - ring_base, n, ptr_base + d0);
 }
 
-template <int BPL, bool PF>
+template <int BPL, bool SMALL>
 __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t base, uint32_t nvals,
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
                             uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err) {
     bool bad = false;
-    // ---- 1. lengths -> offsets --------------------------------------------
+    // ---- 1. string lengths: u8 lengths (SMALL) or exclusive u32 offsets -----
+    W = SMALL ? min(W, 8u) : W;
     const uint32_t n16 = 8 * W;
     gv4 *pk = reinterpret_cast<gv4 *>(packed_vec);
     for (uint32_t i = lane; i < n16; i += 64) w.P[i] = pk[i];
     if (lane < 8) w.P[n16 + lane] = mk4(0, 0, 0, 0);
     wave_sync();
+    uint32_t total = 0;
+    if constexpr (SMALL) {
+        uint32_t run = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t ci = lane + 64 * j;
-        v4u v = add_base<32>(unpack_chunk<32>(w.P, W, ci), base);
-        if (4 * ci + 0 >= nvals) v.x = 0;
-        if (4 * ci + 1 >= nvals) v.y = 0;
-        if (4 * ci + 2 >= nvals) v.z = 0;
-        if (4 * ci + 3 >= nvals) v.w = 0;
-        reinterpret_cast<lv4 *>(w.D)[ci] = v;
-    }
-    wave_sync();
-    {
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t ci = lane + 64 * j;
+            const v4u v = add_base<32>(unpack_chunk<32>(w.P, W, ci), base);
+            const uint32_t b0 = 4 * ci < nvals ? v.x & 255 : 0, b1 = 4 * ci + 1 < nvals ? v.y & 255 : 0;
+            const uint32_t b2 = 4 * ci + 2 < nvals ? v.z & 255 : 0, b3 = 4 * ci + 3 < nvals ? v.w & 255 : 0;
+            reinterpret_cast<lu32 *>(w.D)[ci] = b0 | b1 << 8 | b2 << 16 | b3 << 24;
+            run += b0 + b1 + b2 + b3;
+        }
+        total = rl(scan_incl(run, lane), 63);
+        wave_sync();
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t ci = lane + 64 * j;
+            v4u v = add_base<32>(unpack_chunk<32>(w.P, W, ci), base);
+            if (4 * ci + 0 >= nvals) v.x = 0;
+            if (4 * ci + 1 >= nvals) v.y = 0;
+            if (4 * ci + 2 >= nvals) v.z = 0;
+            if (4 * ci + 3 >= nvals) v.w = 0;
+            reinterpret_cast<lv4 *>(w.D)[ci] = v;
+        }
+        wave_sync();
         uint32_t a[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -217,9 +267,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             reinterpret_cast<lv4 *>(w.D)[4 * lane + q] =
                 mk4(excl + a[4 * q], excl + a[4 * q + 1], excl + a[4 * q + 2], excl + a[4 * q + 3]);
         if (lane == 63) w.D[1024] = incl;
+        total = rl(incl, 63);
+        wave_sync();
     }
-    wave_sync();
-    const uint32_t total = uni(w.D[1024]);
     if (total != dbytes) bad = true;
     const FLS_GLOBAL FsstVecHeader *hp = reinterpret_cast<const FLS_GLOBAL FsstVecHeader *>(vh);
     const uint32_t heap_off = uni(hp->heap_off), comp_len = uni(hp->comp_len), clen_w = uni(min(hp->clen_w, 32u));
@@ -228,25 +278,33 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     const uint64_t ptr_base = heap_host + heap_off;
     gv4 *comp = reinterpret_cast<gv4 *>(vh + sizeof(FsstVecHeader) + 128 * clen_w);
 
-    uint32_t out_pos = 0, ring_base = 0, carry_lit = 0, next_str = 0;
+    // next_str = first string without its string_t yet, str_base = its offset
+    uint32_t out_pos = 0, ring_base = 0, carry_lit = 0, next_str = 0, str_base = 0;
     // strings whose leading bytes are all decoded get their string_t
     auto finalize = [&]() {
         while (next_str < nvals) {
             const uint32_t i = next_str + lane;
-            bool ok = false;
-            uint32_t d0 = 0, n = 0;
-            if (i < nvals) {
+            uint32_t d0 = 0, n = 0, incl = 0;
+            if constexpr (SMALL) {
+                n = i < nvals ? (uint32_t)reinterpret_cast<const lu8 *>(w.D)[i] : 0u;
+                incl = scan_incl(n, lane);
+                d0 = str_base + incl - n;
+            } else if (i < nvals) {
                 d0 = w.D[i];
                 n = w.D[i + 1] - d0;
-                ok = d0 + min(n, 12u) <= out_pos;
             }
+            const bool ok = i < nvals && d0 + min(n, 12u) <= out_pos;
             const uint64_t m = __ballot(ok);
             const uint32_t n_ok = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);
             if (lane < n_ok)
                 *reinterpret_cast<ov4 *>(out + 16ull * i) = make_record(w, d0, n, ring_base, ptr_base);
+            if constexpr (SMALL) {
+                if (n_ok > 0) str_base += rl(incl, n_ok - 1);
+            }
             next_str += n_ok;
             if (n_ok < 64) break;
         }
+        if constexpr (!SMALL) str_base = next_str < nvals ? uni(w.D[next_str]) : out_pos;
     };
     // stream complete 16 B blocks below `upto` (16-aligned) to the heap
     auto flush = [&](uint32_t upto) {
@@ -259,7 +317,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     };
 
     // ---- 2-4. code-parallel rounds -----------------------------------------
-    constexpr uint32_t kRound = Lds<BPL>::kRound;
+    constexpr uint32_t kRound = Lds<BPL, SMALL>::kRound;
     // a lane's compressed bytes of the round starting at r0 (zeros past the end)
     auto load_raw = [&](uint32_t r0) -> v4u {
         const uint32_t idx0 = r0 + BPL * lane;
@@ -274,93 +332,14 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         }
         return x;
     };
-    // PF: the next round's bytes are loaded while this round decodes
-    v4u raw_next = load_raw(0);
-    for (uint32_t r0 = 0; r0 < comp_len; r0 += kRound) {
-        const uint32_t idx0 = r0 + BPL * lane;
-        const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, (uint32_t)BPL) : 0u;
-        v4u raw;
-        if constexpr (PF) {
-            raw = raw_next;
-            if (r0 + kRound < comp_len) raw_next = load_raw(r0 + kRound);
-        } else {
-            raw = load_raw(r0);
-        }
-        // codes and their symbol lengths / symbols, all table reads issued at once
-        uint32_t code[BPL], sl[BPL];
-        bool has_esc = false;
-#pragma unroll
-        for (uint32_t k = 0; k < BPL; ++k) {
-            code[k] = byte_of(raw, k);
-            sl[k] = k < nb ? min((uint32_t)w.len[code[k]], 8u) : 0u;
-            has_esc |= k < nb && code[k] == kFsstEscape;
-        }
-        uint32_t start = 0, lane_out = 0, lane_end = 0;
-        const bool plain = __ballot(has_esc) == 0 && carry_lit == 0;  // wave-uniform
-        if (plain) {  // no escape anywhere: every code is a symbol
-#pragma unroll
-            for (uint32_t k = 0; k < BPL; ++k) lane_out += sl[k];
-        } else {
-            uint32_t o0 = 0, o1 = 0;
-            const uint32_t e0 = simulate<BPL>(code, sl, nb, 0, o0), e1 = simulate<BPL>(code, sl, nb, 1, o1);
-            // inclusive scan of the lanes' state maps f (bit s = f(s)); apply earlier first
-            uint32_t f = e0 | (e1 << 1);
-#pragma unroll
-            for (uint32_t d = 1; d < 64; d <<= 1) {
-                const uint32_t g = __shfl_up(f, d, 64);
-                if (lane >= d) f = (((f >> (g & 1)) & 1)) | (((f >> ((g >> 1) & 1)) & 1) << 1);
-            }
-            uint32_t pre = __shfl_up(f, 1, 64);
-            if (lane == 0) pre = 2;  // identity map
-            start = (pre >> carry_lit) & 1;
-            lane_out = start ? o1 : o0;
-            lane_end = start ? e1 : e0;
-        }
-        const uint32_t incl = scan_incl(lane_out, lane);
-        const uint32_t round_total = rl(incl, 63);
-        // zero the ring dwords this round writes (OR targets), keeping the
-        // already decoded bytes below out_pos in the first one
-        const uint32_t p0 = out_pos - ring_base;
-        {
-            FLS_LDS uint32_t *r32 = reinterpret_cast<FLS_LDS uint32_t *>(w.ring);
-            const uint32_t z0 = (p0 + 3) >> 2, z1 = (p0 + round_total + 3) >> 2;
-            for (uint32_t q = z0 + lane; q < z1; q += 64) r32[q] = 0;
-            if (lane == 0 && (p0 & 3)) r32[p0 >> 2] &= (1u << (8 * (p0 & 3))) - 1u;
-        }
-        wave_sync();
-        // write this lane's symbols into the ring
-        {
-            RingWriter rw(w.ring, p0 + (incl - lane_out));
-            if (plain) {  // sl[k] = 0 past the stream end
-#pragma unroll
-                for (uint32_t k = 0; k < BPL; ++k) rw.put(w.sym[code[k]], sl[k]);
-            } else {
-                uint32_t st = start;
-#pragma unroll
-                for (uint32_t k = 0; k < BPL; ++k) {
-                    if (k < nb) {
-                        if (st) {
-                            rw.put4(code[k], 1);
-                            st = 0;
-                        } else if (code[k] == kFsstEscape) {
-                            st = 1;
-                        } else {
-                            rw.put(w.sym[code[k]], sl[k]);
-                        }
-                    }
-                }
-            }
-            rw.finish();
-        }
-        carry_lit = rl(lane_end, 63);
-        wave_sync();
-        out_pos += round_total;
+    // string_t records of the strings decoded so far, complete 16 B blocks of
+    // the ring to the heap, the unfinished tail (< 32 B) to the ring start
+    auto retire = [&]() {
         finalize();
-        const uint32_t keep_from = next_str < nvals ? min(uni(w.D[next_str]), out_pos) : out_pos;
+        const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
         const uint32_t new_base = keep_from & ~15u;
         flush(new_base);
         wave_sync();
-        // move the unfinished tail (< 32 B) to the ring start
         const uint32_t src = (new_base - ring_base) >> 2;
         uint32_t t = 0;
         if (lane < 8) t = reinterpret_cast<const lu32 *>(w.ring)[src + lane];
@@ -368,9 +347,63 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         if (lane < 8) reinterpret_cast<lu32 *>(w.ring)[lane] = t;
         ring_base = new_base;
         wave_sync();
+    };
+    v4u raw_next = load_raw(0);
+    for (uint32_t r0 = 0; r0 < comp_len; r0 += kRound) {
+        const uint32_t idx0 = r0 + BPL * lane;
+        const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, (uint32_t)BPL) : 0u;
+        const v4u raw = raw_next;  // the next round's bytes load while this one decodes
+        if (r0 + kRound < comp_len) raw_next = load_raw(r0 + kRound);
+        // the previous round's stores go out now, after this round's load was
+        // issued and a whole decode before the next wait (vmcnt counts loads
+        // and stores in issue order, and the variable store count makes that
+        // wait a vmcnt(0): issued at the end of their own round, the stores'
+        // latency was exposed every round)
+        if (r0 > 0) retire();
+        uint32_t n[BPL], lane_end;
+        uint64_t v[BPL];
+        const uint32_t lane_out = r0 + kRound <= comp_len
+                                      ? lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end)
+                                      : lane_codes<BPL, false>(w, raw, nb, carry_lit, lane, v, n, lane_end);
+        const uint32_t incl = scan_incl(lane_out, lane);
+        // write the round into the ring: normally all 64 lanes at once; when
+        // their output would overrun the ring, the lanes that fit first, then
+        // retire() to empty the ring and continue (a lane writes <= 8 BPL bytes)
+        constexpr uint32_t kCap = Lds<BPL, SMALL>::kRing - 48;  // slack: qword ORs, retire()'s 32 B tail read
+        uint32_t l0 = 0, done = 0;
+        for (;;) {
+            const uint32_t p0 = out_pos - ring_base;
+            const bool fits = lane < l0 || p0 + (incl - done) <= kCap;
+            const uint64_t fm = __ballot(fits);
+            const uint32_t l1 = ~fm == 0 ? 64u : (uint32_t)__builtin_ctzll(~fm);
+            const uint32_t part = rl(incl, l1 - 1) - done;
+            // zero the ring dwords these lanes OR into, keeping the already
+            // decoded bytes below out_pos in the first one
+            {
+                FLS_LDS uint32_t *r32 = reinterpret_cast<FLS_LDS uint32_t *>(w.ring);
+                const uint32_t z0 = (p0 + 3) >> 2, z1 = ((p0 + part + 7) & ~7u) >> 2;
+                for (uint32_t q = z0 + lane; q < z1; q += 64) r32[q] = 0;
+                if (lane == 0 && (p0 & 3)) r32[p0 >> 2] &= (1u << (8 * (p0 & 3))) - 1u;
+            }
+            wave_sync();
+            if (lane >= l0 && lane < l1) {
+                QwordWriter qw(w.ring, p0 + (incl - lane_out - done));
+#pragma unroll
+                for (uint32_t k = 0; k < BPL; ++k) qw.put(v[k], n[k]);
+                qw.finish();
+            }
+            wave_sync();
+            out_pos += part;
+            done += part;
+            if (l1 == 64) break;
+            retire();
+            l0 = l1;
+        }
+        // state after the round's last valid byte (lane 63 unless the stream ends here)
+        carry_lit = rl(lane_end, min(63u, (comp_len - 1 - r0) / BPL));
     }
     if (carry_lit) bad = true;  // stream ends inside an escape
-    finalize();
+    retire();
     if (next_str < nvals) {     // lengths claim more bytes than the stream holds
         bad = true;
         for (uint32_t i = next_str + lane; i < nvals; i += 64)
@@ -398,7 +431,7 @@ __device__ __forceinline__ DevChunk load_chunk(const DevChunk *chunks, uint32_t 
 // Vectors [item0, item1) of the launch (items numbered chunk by chunk through
 // DevChunk.vec_base): the wave loads a chunk's symbol table once and decodes
 // its vectors in order.
-template <int BPL, bool PF>
+template <int BPL, bool SMALL>
 __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t item0,
                                                      uint32_t item1, uint8_t *lds_generic, uint32_t *err_generic) {
     const uint64_t cp = (uint64_t)chunks_generic;
@@ -410,12 +443,13 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     item0 = uni(item0);
     item1 = uni(item1);
     const uint32_t lane = __lane_id();
+    using Layout = Lds<BPL, SMALL>;
     Wave w;
-    w.P = reinterpret_cast<lv4 *>(L + kOffRing);
-    w.D = reinterpret_cast<lu32 *>(L + kOffD);
-    w.sym = reinterpret_cast<const FLS_LDS uint64_t *>(L + kOffSym);
-    w.len = L + kOffLen;
-    w.ring = L + kOffRing;
+    w.P = reinterpret_cast<lv4 *>(L + Layout::kOffRing);
+    w.D = reinterpret_cast<lu32 *>(L + Layout::kOffD);
+    w.sym = reinterpret_cast<const FLS_LDS uint64_t *>(L + Layout::kOffSym);
+    w.len = L + Layout::kOffLen;
+    w.ring = L + Layout::kOffRing;
     // chunk holding item0: last ci with vec_base <= item0
     uint32_t lo = 0, hi = nchunks;
     while (hi - lo > 1) {
@@ -437,10 +471,17 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
         gu8 *chunk = gptr(c.chunk);
         gu8 *aux = chunk + c.aux_off;
         if (!have_table) {
-            // symbol table (u64[256] then u8[256]: 144 x 16 B, contiguous in both places)
+            // symbol table, sanitised: each symbol masked to its length (so
+            // OR-ing whole symbols is exact), the escape code's entry {0, 0}
             wave_sync();
-            for (uint32_t i = lane; i < kFsstTableBytes / 16; i += 64)
-                reinterpret_cast<lv4 *>(L + kOffSym)[i] = reinterpret_cast<gv4 *>(aux)[i];
+            const FLS_GLOBAL uint64_t *gs = reinterpret_cast<const FLS_GLOBAL uint64_t *>(aux);
+            FLS_LDS uint64_t *ls = reinterpret_cast<FLS_LDS uint64_t *>(L + Layout::kOffSym);
+            for (uint32_t k = lane; k < 256; k += 64) {
+                const uint32_t n = k == kFsstEscape ? 0u : min((uint32_t)aux[8 * 256 + k], 8u);
+                const uint64_t sy = gs[k];
+                ls[k] = n >= 8 ? sy : sy & ((1ull << (8 * n)) - 1);
+                L[Layout::kOffLen + k] = (uint8_t)n;
+            }
             wave_sync();
             have_table = true;
         }
@@ -451,7 +492,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
         const uint32_t nvals = uni(meta->nvals);
         const uint32_t W = uni(min((uint32_t)meta->bw, 32u));
         const uint32_t dbytes = uni(meta->aux_count);
-        fsst_vector<BPL, PF>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
+        fsst_vector<BPL, SMALL>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
                     (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
                     gptr(c.out) + 16ull * kVectorSize * v, lane, err);
         wave_sync();
@@ -459,7 +500,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     }
 }
 
-template <int BPL, bool PF>
+template <int BPL, bool SMALL>
 __global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                      uint32_t nitems, uint32_t *__restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
@@ -467,24 +508,24 @@ __global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict_
     // contiguous vector ranges per wave: a wave mostly stays inside one chunk
     const uint32_t per = (nitems + nwaves - 1) / nwaves;
     const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
-    if (i0 < i1) fsst_range<BPL, PF>(chunks, nchunks, i0, i1, lds_raw, err);
+    if (i0 < i1) fsst_range<BPL, SMALL>(chunks, nchunks, i0, i1, lds_raw, err);
 }
 
-template <int BPL, bool PF>
+template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream) {
-    const uint32_t shmem = Lds<BPL>::kWave;
+    const uint32_t shmem = Lds<BPL, SMALL>::kWave;
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, PF>, 64, shmem) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL>, 64, shmem) != hipSuccess)
             per_cu = 1;
     }
     const int grid = std::min<int>(cus * std::max(1, per_cu), (int)nvecs);
     if (getenv("FLS_DEBUG"))
-        fprintf(stderr, "DEBUG: fsst_kernel<%d,%d>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors\n", BPL,
-                (int)PF, grid, per_cu, shmem, nvecs);
-    hipLaunchKernelGGL((fsst_kernel<BPL, PF>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err);
+        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors\n", BPL,
+                SMALL ? "small" : "any", grid, per_cu, shmem, nvecs);
+    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err);
     return hipGetLastError();
 }
 
@@ -798,14 +839,13 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
 }
 
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                       hipStream_t stream, int bytes_per_lane) {
+                       hipStream_t stream, int bytes_per_lane, bool small) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
-    const bool pf = !getenv("FLS_FSST_NO_PREFETCH");  // A/B knob
     if (bytes_per_lane == 8)
-        return pf ? launch_fsst_t<8, true>(d_chunks, nchunks, nvecs, d_err, stream)
-                  : launch_fsst_t<8, false>(d_chunks, nchunks, nvecs, d_err, stream);
-    return pf ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream)
-              : launch_fsst_t<16, false>(d_chunks, nchunks, nvecs, d_err, stream);
+        return small ? launch_fsst_t<8, true>(d_chunks, nchunks, nvecs, d_err, stream)
+                     : launch_fsst_t<8, false>(d_chunks, nchunks, nvecs, d_err, stream);
+    return small ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream)
+                 : launch_fsst_t<16, false>(d_chunks, nchunks, nvecs, d_err, stream);
 }
 
 }  // namespace fls

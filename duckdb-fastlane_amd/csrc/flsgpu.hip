@@ -383,11 +383,12 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // bit 4 = FSST rounds of 16 compressed bytes per lane instead of 8.
 // bit 5 = balanced static split of vectors over the resident waves, chunks in
 // file (row-group-major) order (balanced_split).  bit 6 = work queue even for
-// small launches (launch_policy).  bit 7 = every FSST chunk on the
-// code-parallel kernel.
+// small launches (launch_policy).  bit 7 = FSST chunks whose strings are all
+// <= 255 bytes on the string-parallel kernel (default: every FSST chunk on the
+// code-parallel kernel; same-buffer A/B profiles/r1/abenv_fsst_cp.txt).
 enum : int {
     POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST16 = 16, POLICY_BALANCED = 32,
-    POLICY_QUEUE = 64, POLICY_FSST_CP = 128
+    POLICY_QUEUE = 64, POLICY_FSST_SP = 128
 };
 // Balanced-split knobs, folded into the policy word (so a change rebuilds the
 // cached launch list): FLS_STATIC_PCT = % of the bytes split statically
@@ -421,8 +422,6 @@ int launch_policy(int policy, const std::vector<DevChunk> &v, DecodeGeom &geom) 
 // returns how many lead (main kernel) and the FSST counts
 uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int policy) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
-    if (policy & POLICY_FSST_CP)
-        for (auto it = mid; it != v.end(); ++it) it->vbits = 0;
     auto sp_end = std::stable_partition(mid, v.end(), [](const DevChunk &d) { return d.vbits == 1; });
     if (policy & POLICY_FULL_PREFETCH)
         for (auto it = v.begin(); it != mid; ++it) it->max_w = it->T;
@@ -469,10 +468,14 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     const uint32_t *d_split = plan.waves ? reinterpret_cast<const uint32_t *>(d_chunks + ntotal) : nullptr;
     hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue,
                                  d_split, plan);
-    if (e == hipSuccess) e = launch_fsst_sp(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream);
+    // FSST chunks whose strings are all <= 255 bytes (first group): the
+    // code-parallel kernel with u8 string lengths, or the string-parallel one
+    const int bpl = (policy & POLICY_FSST16) ? 16 : 8;
     if (e == hipSuccess)
-        e = launch_fsst(d_chunks + nmain + fc.nsp, ntotal - nmain - fc.nsp, fc.cp_vecs, d_err, stream,
-                        (policy & POLICY_FSST16) ? 16 : 8);
+        e = (policy & POLICY_FSST_SP) ? launch_fsst_sp(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream)
+                                      : launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, bpl, true);
+    if (e == hipSuccess)
+        e = launch_fsst(d_chunks + nmain + fc.nsp, ntotal - nmain - fc.nsp, fc.cp_vecs, d_err, stream, bpl, false);
     return e;
 }
 

@@ -286,11 +286,16 @@ def _sp_tables(fl, rng):
     mixed = fsst_text(65536, rng)
     mixed[777] = "long " * 60
     mixed += fsst_text(9000, rng)
-    return [("text", text), ("escapes", esc), ("binary127", bin127), ("edge255", edge), ("mixed_rg", mixed)]
+    # ~8 decoded bytes per code: a round's output overruns the code-parallel
+    # kernel's 2 KiB ring and is written in parts
+    # (lengths in [192, 255] so the chunk's FFOR length bound stays <= 255)
+    rep = [(b"abcdefgh" * 32)[: int(k)] for k in rng.integers(192, 249, 5000)]
+    return [("text", text), ("escapes", esc), ("binary127", bin127), ("edge255", edge), ("repeat8", rep),
+            ("mixed_rg", mixed)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("policy", ["0", "128"], ids=["string_parallel", "code_parallel"])
+@pytest.mark.parametrize("policy", ["128", "0"], ids=["string_parallel", "code_parallel"])
 def test_gpu_fsst_string_and_code_parallel_agree(fl, ref, gpu, monkeypatch, capfd, policy):
     monkeypatch.setenv("FLS_DECODE_POLICY", policy)
     monkeypatch.setenv("FLS_DEBUG", "1")
@@ -300,9 +305,12 @@ def test_gpu_fsst_string_and_code_parallel_agree(fl, ref, gpu, monkeypatch, capf
         rf = ref.RefFile(img)
         assert_strings_equal(fl, rf, 0, out[0])
         err = capfd.readouterr().err
-        # which kernels ran: every case but binary-heavy long strings is string-parallel by default
-        assert ("fsst_sp_kernel" in err) == (policy == "0"), name
-        assert ("fsst_kernel<" in err) == (policy == "128" or name == "mixed_rg"), name
+        # which kernels ran: every chunk is code-parallel by default (u8 string
+        # lengths when all strings are <= 255 bytes); policy 128 sends those
+        # chunks to the string-parallel kernel
+        assert ("fsst_sp_kernel" in err) == (policy == "128"), name
+        assert ("fsst_kernel<8,small>" in err) == (policy == "0"), name
+        assert ("fsst_kernel<8,any>" in err) == (name == "mixed_rg"), name
 
 
 @pytest.mark.gpu
@@ -319,11 +327,17 @@ def test_gpu_fsst_string_parallel_scan_pipeline(fl, ref, gpu, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("field", ["clen_base", "comp_len"])
-def test_gpu_fsst_corrupt_compressed_lengths_reported(fl, ref, gpu, field):
+@pytest.mark.parametrize("policy", ["128", "0"], ids=["string_parallel", "code_parallel"])
+def test_gpu_fsst_corrupt_compressed_lengths_reported(fl, ref, gpu, monkeypatch, field, policy):
     """A compressed-length stream that disagrees with the code stream (the
-    string-parallel kernel's string starts) is clamped and reported."""
+    string-parallel kernel's string starts) is clamped and reported by the
+    string-parallel kernel.  The code-parallel kernel never reads the
+    per-string compressed lengths: it decodes such a vector exactly, and
+    reports a code stream shortened under the strings' lengths."""
+    monkeypatch.setenv("FLS_DECODE_POLICY", policy)
     s = fsst_text(5000, np.random.default_rng(6))
-    raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
+    img = fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)])
+    raw = bytearray(img.tobytes())
     off = _chunk_header(raw)
     aux_off = struct.unpack_from("<Q", raw, off + 32)[0]
     meta = off + struct.unpack_from("<Q", raw, off + 16)[0]
@@ -333,5 +347,9 @@ def test_gpu_fsst_corrupt_compressed_lengths_reported(fl, ref, gpu, field):
     t = fl.Connection().read_image(bytes(raw))
     t.device_upload()
     t.device_decode()
+    if field == "clen_base" and policy == "0":
+        t.device_sync()
+        assert_strings_equal(fl, ref.RefFile(img), 0, t.device_copy_out(0))
+        return
     with pytest.raises(fl.FlsError, match="corrupt"):
         t.device_sync()
