@@ -462,6 +462,14 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
     return plan;
 }
 
+// The FSST kernels follow the main one on the same stream.  Measured
+// alternatives (lineitem_full SF100): overlapping them on a second stream (a
+// narrow FSST grid beside a main grid of 3 blocks per CU, a full FSST grid
+// after it, all draining one piece queue) ran 25.97 vs 26.15 ms: the FSST
+// waves ran at full speed but slowed the main kernel by as much (17.9 vs
+// 15.6 ms in the kernel trace), so they compete for the CUs' LDS and issue
+// slots, not only for HBM.  A piece queue instead of contiguous vector ranges
+// per wave was 2-4 % slower on l_comment (symbol table reloads).
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
                       uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
                       SplitPlan plan) {
