@@ -90,7 +90,10 @@ def measure_traffic(args):
         shutil.rmtree(d, ignore_errors=True)
         if "decode" not in per:
             return None, f"no {ctr} samples"
-        vals[ctr] = sum(sum(v) / len(v) for v in per.values()) * 1024.0  # KiB -> bytes, per step
+        # per step: every dispatch of the step's kernels (a table decode with
+        # FSST columns runs several grids of each kind), over the child's
+        # warmup + steps decode calls
+        vals[ctr] = sum(sum(v) for v in per.values()) / 3.0 * 1024.0  # KiB -> bytes, per step
     return 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"], \
         f"rocprofv3 --pmc per launch: FETCH_SIZE x2 {2 * vals['FETCH_SIZE'] / 1e9:.3f} GB + " \
         f"WRITE_SIZE {vals['WRITE_SIZE'] / 1e9:.3f} GB"

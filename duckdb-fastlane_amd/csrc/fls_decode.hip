@@ -693,8 +693,9 @@ __device__ __forceinline__ void call_dict(const DevChunk *c, uint32_t lp, uint32
 // largest-first order, so the launch ends on small chunks -- else grid-stride.
 // The first chunk of every wave is static (no burst of same-address atomics
 // at launch); the queue hands out the chunks after the grid's first round.
+// stride == 0: every chunk from the queue (several grids share it).
 __device__ __forceinline__ uint32_t next_chunk(uint32_t *queue, uint32_t prev, uint32_t first, uint32_t stride) {
-    if (prev == UINT32_MAX) return first;
+    if (prev == UINT32_MAX && stride) return first;
     if (!queue) return prev + stride;
     uint32_t ci = 0;
     if (__lane_id() == 0) ci = atomicAdd(queue, 1u);
@@ -777,12 +778,13 @@ __device__ __forceinline__ void decode_range(const DevChunk *chunks, uint32_t nc
 __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                         uint32_t *__restrict__ err, uint32_t p_bytes,
                                                         uint32_t v_bytes, uint32_t *__restrict__ queue,
-                                                        const uint32_t *__restrict__ split, uint32_t npieces) {
+                                                        const uint32_t *__restrict__ split, uint32_t npieces,
+                                                        uint32_t shared_queue) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     const uint32_t w = uni(threadIdx.x >> 6);
     const uint32_t lp = (uint32_t)(size_t)((lu8 *)lds_raw + w * (p_bytes + v_bytes));
     const uint32_t lv = lp + p_bytes;
-    const uint32_t stride = gridDim.x * kWaves, first = blockIdx.x * kWaves + w;
+    const uint32_t stride = shared_queue ? 0u : gridDim.x * kWaves, first = blockIdx.x * kWaves + w;
     if (split) {
         const FLS_GLOBAL uint32_t *sp = gptr(split);
         decode_range(chunks, nchunks, uni(sp[first]), uni(sp[first + 1]), lp, lv, v_bytes, err);
@@ -866,7 +868,8 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 }
 
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
-                         hipStream_t stream, uint32_t *d_queue, const uint32_t *d_split, SplitPlan plan) {
+                         hipStream_t stream, uint32_t *d_queue, const uint32_t *d_split, SplitPlan plan,
+                         bool shared_queue) {
     if (nchunks == 0) return hipSuccess;
     const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
     int grid;
@@ -876,12 +879,12 @@ hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d
     } else {
         grid = std::min<int>(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), (nchunks + kWaves - 1) / kWaves);
     }
-    if (d_queue) {
+    if (d_queue && !shared_queue) {
         const hipError_t e = hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
-                       geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces);
+                       geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces, (uint32_t)(shared_queue && d_queue));
     return hipGetLastError();
 }
 

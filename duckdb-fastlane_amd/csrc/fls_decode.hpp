@@ -58,10 +58,11 @@ struct SplitPlan {
 // wave decodes its own balanced range of vectors, then tail pieces from
 // d_queue; else d_queue (one zeroed word, may be NULL): waves take whole
 // chunks from this work queue in list order; else a static grid-stride split
-// of whole chunks.
+// of whole chunks.  shared_queue: the caller zeroed d_queue and several grids
+// drain it (every chunk from the queue, none static).
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream, uint32_t *d_queue = nullptr, const uint32_t *d_split = nullptr,
-                         SplitPlan plan = SplitPlan());
+                         SplitPlan plan = SplitPlan(), bool shared_queue = false);
 // Waves of a resident decode launch with this LDS geometry.
 uint32_t decode_waves(const DecodeGeom &geom);
 // Split the vectors of h[0, n) over at most nw waves: static_pct % of the
@@ -69,12 +70,18 @@ uint32_t decode_waves(const DecodeGeom &geom);
 // equal tail pieces (dynamic: the waves that finish first take them).
 SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t static_pct, uint32_t pieces_per_wave,
                          std::vector<uint32_t> &pos);
+// How one FSST launch runs (launch_fsst).
+struct FsstLaunch {
+    int bytes_per_lane = 8;       // compressed bytes a lane decodes per round (8 or 16)
+    bool small = false;           // every string of these chunks is <= 255 bytes (DevChunk.vbits = 1)
+    uint32_t *queue = nullptr;    // piece counter (overlapped launches); nullptr: contiguous ranges
+    bool reset_queue = true;      // zero it first (false: drain a queue another launch started)
+    int waves_per_cu = 0;         // grid: 0 = as many as fit, else at most this many per CU
+};
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
-// bytes_per_lane: compressed bytes a lane decodes per round (8 or 16);
-// small: every string of these chunks is <= 255 bytes (DevChunk.vbits = 1).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                       hipStream_t stream, int bytes_per_lane = 8, bool small = false);
+                       hipStream_t stream, const FsstLaunch &how);
 // Launch the string-parallel FSST decode over nchunks FSST chunks whose
 // strings are all <= 255 bytes (DevChunk.vbits = 1), nvecs vectors numbered
 // through DevChunk.vec_base (fls_fsst.hip).

@@ -500,20 +500,39 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     }
 }
 
+// Work distribution.  Standalone launches: contiguous vector ranges per wave
+// (a wave mostly stays inside one chunk and stages its symbol table once).
+// Overlapped launches (queue != nullptr, FsstLaunch::overlap): pieces of
+// `piece` consecutive vectors from a counter shared by the narrow grid that
+// runs beside the main decode kernel and the full grid that follows it, one
+// atomic per piece, so no vector is decoded twice and late waves find work.
+// (A piece queue for standalone launches measured 2-4 % slower on l_comment
+// at SF10: more symbol-table reloads.)
 template <int BPL, bool SMALL>
 __global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
-                                                     uint32_t nitems, uint32_t *__restrict__ err) {
+                                                     uint32_t nitems, uint32_t *__restrict__ err,
+                                                     uint32_t *__restrict__ queue, uint32_t piece) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
-    const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
-    // contiguous vector ranges per wave: a wave mostly stays inside one chunk
-    const uint32_t per = (nitems + nwaves - 1) / nwaves;
-    const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
-    if (i0 < i1) fsst_range<BPL, SMALL>(chunks, nchunks, i0, i1, lds_raw, err);
+    if (!queue) {
+        const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
+        const uint32_t per = (nitems + nwaves - 1) / nwaves;
+        const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
+        if (i0 < i1) fsst_range<BPL, SMALL>(chunks, nchunks, i0, i1, lds_raw, err);
+        return;
+    }
+    for (;;) {
+        uint32_t p = 0;
+        if (__lane_id() == 0) p = atomicAdd(queue, 1u);
+        p = rl(p, 0);
+        if (p >= (nitems + piece - 1) / piece) break;  // every wave reaches this exit
+        const uint32_t i0 = p * piece;
+        fsst_range<BPL, SMALL>(chunks, nchunks, i0, min(i0 + piece, nitems), lds_raw, err);
+    }
 }
 
 template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                         hipStream_t stream) {
+                         hipStream_t stream, const FsstLaunch &how) {
     const uint32_t shmem = Lds<BPL, SMALL>::kWave;
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
@@ -521,11 +540,19 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL>, 64, shmem) != hipSuccess)
             per_cu = 1;
     }
-    const int grid = std::min<int>(cus * std::max(1, per_cu), (int)nvecs);
+    const int full = cus * std::max(1, per_cu);
+    const int grid = std::min<int>(how.waves_per_cu > 0 ? cus * std::min(how.waves_per_cu, per_cu) : full, (int)nvecs);
+    // overlapped: pieces of ~1/4 of a wave's share of a full grid, <= 16 vectors
+    const uint32_t piece = std::max<uint32_t>(1, std::min<uint32_t>(16, nvecs / (4u * (uint32_t)full)));
+    if (how.queue && how.reset_queue) {
+        const hipError_t e = hipMemsetAsync(how.queue, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+    }
     if (getenv("FLS_DEBUG"))
-        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors\n", BPL,
-                SMALL ? "small" : "any", grid, per_cu, shmem, nvecs);
-    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err);
+        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors%s\n", BPL,
+                SMALL ? "small" : "any", grid, per_cu, shmem, nvecs, how.queue ? " (piece queue)" : "");
+    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err,
+                       how.queue, piece);
     return hipGetLastError();
 }
 
@@ -839,13 +866,13 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
 }
 
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
-                       hipStream_t stream, int bytes_per_lane, bool small) {
+                       hipStream_t stream, const FsstLaunch &how) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
-    if (bytes_per_lane == 8)
-        return small ? launch_fsst_t<8, true>(d_chunks, nchunks, nvecs, d_err, stream)
-                     : launch_fsst_t<8, false>(d_chunks, nchunks, nvecs, d_err, stream);
-    return small ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream)
-                 : launch_fsst_t<16, false>(d_chunks, nchunks, nvecs, d_err, stream);
+    if (how.bytes_per_lane == 16)
+        return how.small ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                         : launch_fsst_t<16, false>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    return how.small ? launch_fsst_t<8, true>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                     : launch_fsst_t<8, false>(d_chunks, nchunks, nvecs, d_err, stream, how);
 }
 
 }  // namespace fls

@@ -236,6 +236,12 @@ struct ScanCtx {
 
 }  // namespace
 
+// Second stream a table decode overlaps its FSST kernels on (launch_all).
+struct SideStream {
+    hipStream_t stream = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+
 struct fls_table {
     fls_connection *conn = nullptr;
     std::vector<uint8_t> owned;
@@ -260,6 +266,7 @@ struct fls_table {
     FsstCounts dev_fsst;               // FSST chunks of h_chunks
     SplitPlan dev_split;               // balanced split after h_chunks on the device (waves 0: none)
     hipStream_t stream = nullptr;
+    SideStream side;                   // FSST kernels overlapping the main decode kernel
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
     uint32_t ev_used = 0;
@@ -462,35 +469,97 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
     return plan;
 }
 
-// The FSST kernels follow the main one on the same stream.  Measured
-// alternatives (lineitem_full SF100): overlapping them on a second stream (a
-// narrow FSST grid beside a main grid of 3 blocks per CU, a full FSST grid
-// after it, all draining one piece queue) ran 25.97 vs 26.15 ms: the FSST
-// waves ran at full speed but slowed the main kernel by as much (17.9 vs
-// 15.6 ms in the kernel trace), so they compete for the CUs' LDS and issue
-// slots, not only for HBM.  A piece queue instead of contiguous vector ranges
-// per wave was 2-4 % slower on l_comment (symbol table reloads).
+// Overlap split (launch_all): blocks per CU of the narrow main decode grid
+// and FSST waves per CU of the narrow FSST grid; knobs FLS_OVERLAP_DECODE_BPC /
+// FLS_OVERLAP_FSST_WPC (0 FSST waves = no overlap).
+struct OverlapSplit {
+    int decode_bpc = 1, fsst_wpc = 16;
+};
+OverlapSplit overlap_split() {
+    OverlapSplit o;
+    if (const char *e = getenv("FLS_OVERLAP_DECODE_BPC")) o.decode_bpc = std::max(1, atoi(e));
+    if (const char *e = getenv("FLS_OVERLAP_FSST_WPC")) o.fsst_wpc = std::max(0, atoi(e));
+    return o;
+}
+
+// d_queue[0] = main decode work queue, [1] / [2] = FSST piece counters of the
+// small-string and the other FSST chunks.
+//
+// Without a side stream (scan batches) the FSST kernels follow the main one
+// on its stream.  With one (a table decode), the FSST kernels (VALU-bound)
+// overlap the main decode kernel (HBM-bound):
+//   main stream: narrow decode grid (decode_bpc blocks per CU), then a full
+//                FSST grid;
+//   side stream: narrow FSST grid (fsst_wpc waves per CU), then a full decode
+//                grid.
+// Every grid of a kind drains one shared queue (decode chunks / FSST pieces),
+// so no work is done twice, and whichever kind runs out first, its stream
+// follows with a full grid of the other kind onto the freed wave slots.  The
+// split holds whichever kernel the hardware dispatches first.
+// Measured on lineitem_full SF100 (same-buffer A/B, profiles/r1/abenv_overlap.txt):
+// 26.7 ms serial -> 24.3 ms at 1 decode block + 12..20 FSST waves per CU
+// (2 blocks + 8..12 waves: 24.7 ms).  The kernel trace shows the overlap phase
+// moving ~4.9 TB/s together, below the 5.6 TB/s of the main kernel alone: the
+// two compete for the CUs' LDS and issue slots as well as for HBM.
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
                       uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
-                      SplitPlan plan) {
+                      SplitPlan plan, const SideStream *side = nullptr) {
     const uint32_t *d_split = plan.waves ? reinterpret_cast<const uint32_t *>(d_chunks + ntotal) : nullptr;
-    hipError_t e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue,
-                                 d_split, plan);
+    const uint32_t ncp = ntotal - nmain - fc.nsp;
+    const bool sp = (policy & POLICY_FSST_SP) != 0;
+    const OverlapSplit ov = overlap_split();
+    FsstLaunch small, any;
+    small.bytes_per_lane = any.bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
+    small.small = true;
+    const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && (fc.sp_vecs + fc.cp_vecs) > 0 &&
+                         !d_split && !sp && !(policy & POLICY_STATIC);
+    hipError_t e = hipSuccess;
+    if (overlap) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        DecodeGeom narrow = geom;
+        const uint32_t shmem = 4 * (geom.p_bytes + geom.v_bytes);
+        narrow.grid = std::min(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), cus * ov.decode_bpc);
+        e = hipMemsetAsync(d_queue, 0, 3 * sizeof(uint32_t), stream);
+        if (e == hipSuccess) e = hipEventRecord(side->fork, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(side->stream, side->fork, 0);
+        small.queue = d_queue + 1;
+        any.queue = d_queue + 2;
+        small.reset_queue = any.reset_queue = false;
+        FsstLaunch ns = small, na = any;
+        ns.waves_per_cu = na.waves_per_cu = ov.fsst_wpc;
+        // main stream: narrow decode, then full FSST
+        if (e == hipSuccess) e = launch_decode(d_chunks, nmain, d_err, narrow, stream, d_queue, nullptr, SplitPlan(), true);
+        // side stream: narrow FSST, then full decode
+        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, side->stream, ns);
+        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, side->stream, na);
+        if (e == hipSuccess) e = launch_decode(d_chunks, nmain, d_err, geom, side->stream, d_queue, nullptr, SplitPlan(), true);
+        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, small);
+        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, stream, any);
+        if (e == hipSuccess) e = hipEventRecord(side->join, side->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join, 0);
+        return e;
+    }
+    e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue, d_split, plan);
     // FSST chunks whose strings are all <= 255 bytes (first group): the
     // code-parallel kernel with u8 string lengths, or the string-parallel one
-    const int bpl = (policy & POLICY_FSST16) ? 16 : 8;
     if (e == hipSuccess)
-        e = (policy & POLICY_FSST_SP) ? launch_fsst_sp(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream)
-                                      : launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, bpl, true);
-    if (e == hipSuccess)
-        e = launch_fsst(d_chunks + nmain + fc.nsp, ntotal - nmain - fc.nsp, fc.cp_vecs, d_err, stream, bpl, false);
+        e = sp ? launch_fsst_sp(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream)
+               : launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, small);
+    if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, stream, any);
     return e;
 }
 
 }  // namespace
 
 fls_table::~fls_table() {
+    if (side.stream) hipStreamSynchronize(side.stream);
     if (stream) hipStreamDestroy(stream);
+    if (side.stream) hipStreamDestroy(side.stream);
+    if (side.fork) hipEventDestroy(side.fork);
+    if (side.join) hipEventDestroy(side.join);
     for (auto e : ev_pool) hipEventDestroy(e);
     if (ev0) hipEventDestroy(ev0);
     if (ev1) hipEventDestroy(ev1);
@@ -787,7 +856,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     HIP_TRY(sl.d_chunks.alloc(d.dev, kk));
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
-    HIP_TRY(sl.queue.alloc(d.dev, 1));
+    HIP_TRY(sl.queue.alloc(d.dev, 3));
     HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
                        plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
@@ -1268,12 +1337,18 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
             t->ev_pool.push_back(e);
         }
     }
+    // queue counters and the side stream exist before the timed region
+    HIP_TRY(sh.queue.alloc(sh.dev, 3));
+    if (!t->side.stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&t->side.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&t->side.fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&t->side.join, hipEventDisableTiming));
+    }
     hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
     t->ev_used += 2;
     HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(sh.queue.alloc(sh.dev, 1));
     HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst, sh.err.p,
-                       t->last_bytes.geom, t->stream, sh.queue.p, t->dev_lpolicy, t->dev_split));
+                       t->last_bytes.geom, t->stream, sh.queue.p, t->dev_lpolicy, t->dev_split, &t->side));
     HIP_TRY(hipEventRecord(e1, t->stream));
     t->launches++;
     t->launched = true;

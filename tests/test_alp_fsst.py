@@ -222,8 +222,19 @@ def test_gpu_alp_fsst_scan_pipeline(fl, ref, gpu, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wl", ["lineitem_full", "lineitem_dbl"])
-def test_gpu_full_fidelity_lineitem(fl, ref, gpu, wl):
+@pytest.mark.parametrize("wl,split", [("lineitem_full", None), ("lineitem_full", "0"), ("lineitem_full", "1,28"),
+                                      ("lineitem_full", "4,1"), ("lineitem_dbl", None)],
+                         ids=["full-overlap", "full-serial", "full-fsst-wide", "full-fsst-narrow", "dbl"])
+def test_gpu_full_fidelity_lineitem(fl, ref, gpu, monkeypatch, wl, split):
+    """Full-fidelity lineitem; with FSST columns the table decode overlaps the
+    FSST kernels with the main one (launch_all): default split, serial
+    (FLS_OVERLAP_FSST_WPC=0) and extreme splits must all decode exactly."""
+    if split == "0":
+        monkeypatch.setenv("FLS_OVERLAP_FSST_WPC", "0")
+    elif split:
+        bpc, wpc = split.split(",")
+        monkeypatch.setenv("FLS_OVERLAP_DECODE_BPC", bpc)
+        monkeypatch.setenv("FLS_OVERLAP_FSST_WPC", wpc)
     img = fl.gen_image(wl, 0.1)
     t, st, out = gpu_decode_all(fl, img)
     rf = ref.RefFile(img)
