@@ -400,14 +400,18 @@ enum : int {
 // Balanced-split knobs, folded into the policy word (so a change rebuilds the
 // cached launch list): FLS_STATIC_PCT = % of the bytes split statically
 // (bits 8-15, default 100), FLS_TAIL_PIECES = tail pieces per wave for the
-// rest (bits 16-23, default 2).
+// rest (bits 16-23, default 2), FLS_BLOCKS_PER_CU (bits 24-30, 0 = unset).
 int decode_policy() {
     const char *e = getenv("FLS_DECODE_POLICY");
     const char *sp = getenv("FLS_STATIC_PCT");
     const char *tp = getenv("FLS_TAIL_PIECES");
     const int pct = sp ? std::min(100, std::max(0, atoi(sp))) : 100;
     const int pieces = tp ? std::min(255, std::max(1, atoi(tp))) : 2;
-    return (e ? (atoi(e) & 0xFF) : 0) | pct << 8 | pieces << 16;
+    // FLS_BLOCKS_PER_CU (decode_grid_size) only enters the grid when the
+    // launch list is rebuilt: fold it in so a change rebuilds it
+    const char *bp = getenv("FLS_BLOCKS_PER_CU");
+    const int bpc = bp ? std::min(127, std::max(0, atoi(bp))) : 0;
+    return (e ? (atoi(e) & 0xFF) : 0) | pct << 8 | pieces << 16 | bpc << 24;
 }
 
 // Policy for one launch: the default (no distribution bits) switches to the
