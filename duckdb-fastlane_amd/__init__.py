@@ -119,6 +119,13 @@ _sig("fls_writer_free", None, _P)
 _sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8)
 _sig("fls_writer_add_rowgroup", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P))
 _sig("fls_writer_set_rowgroup_size", C.c_int, _P, C.c_uint32)
+_sig("fls_writer_set_device", C.c_int, _P, C.c_int)
+_sig("fls_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(_P))
+_sig("fls_device_free", C.c_int, C.c_int, _P)
+_sig("fls_device_memcpy", C.c_int, C.c_int, _P, _P, C.c_uint64, C.c_int)
+_sig("fls_encode_slot_bytes", C.c_uint64, C.c_uint8, C.c_uint8, C.c_uint32)
+_sig("fls_encode_device", C.c_int, C.c_int, C.c_uint8, C.c_uint8, _P, C.c_uint64, C.c_uint32, _P,
+     C.POINTER(C.c_uint64), C.POINTER(C.c_float))
 _sig("fls_writer_finish_file", C.c_int, _P, C.c_char_p)
 _sig("fls_writer_finish_image", C.c_int, _P, C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_image_free", None, _P)
@@ -223,13 +230,16 @@ def gen_dict_string(workload: str, col: int, code: int) -> str | None:
 
 
 # --- writer ----------------------------------------------------------------
-def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0) -> Image:
+def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: int = -1) -> Image:
     """columns: list of (name, type, values, encoding[, width, scale]).
     values: numpy int array for integer types, float array for FLOAT/DOUBLE
-    (stored bit-exactly), list of str/bytes for VARCHAR."""
+    (stored bit-exactly), list of str/bytes for VARCHAR.  device >= 0: the
+    FFOR / DELTA integer columns are encoded on that GPU (same bytes)."""
     w = _lib.fls_writer_new(row_offset)
     try:
         _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))
+        if device >= 0:
+            _check(_lib.fls_writer_set_device(w, device))
         n = None
         prepped = []
         for spec in columns:
@@ -272,6 +282,56 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0) -> Image
         return _take_image(rc, p, ln)
     finally:
         _lib.fls_writer_free(w)
+
+
+def encode_device(device: int, ty: int, enc: int, d_values: int, nrows: int, d_out: int,
+                  rowgroup: int = ROWGROUP):
+    """GPU chunk encoder over a device-resident column (fls_encode_device):
+    d_values / d_out are device addresses (e.g. torch tensor data_ptr()).
+    Returns (chunk lengths, kernel ms); chunk i starts at
+    d_out + i * encode_slot_bytes(ty, enc, rowgroup)."""
+    nrg = (nrows + rowgroup - 1) // rowgroup
+    lens = (C.c_uint64 * nrg)()
+    ms = C.c_float()
+    _check(_lib.fls_encode_device(device, ty, enc, d_values, nrows, rowgroup, d_out, lens, C.byref(ms)))
+    return [int(x) for x in lens], float(ms.value)
+
+
+def encode_slot_bytes(ty: int, enc: int, rowgroup: int = ROWGROUP) -> int:
+    return int(_lib.fls_encode_slot_bytes(ty, enc, rowgroup))
+
+
+class DeviceBuffer:
+    """A raw device allocation through the engine's own HIP runtime
+    (fls_device_alloc): no second runtime (e.g. torch's) in the process."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device, self.nbytes = device, int(nbytes)
+        p = _P()
+        _check(_lib.fls_device_alloc(device, self.nbytes, C.byref(p)))
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, arr: np.ndarray, device: int = 0) -> "DeviceBuffer":
+        arr = np.ascontiguousarray(arr)
+        b = cls(arr.nbytes, device)
+        _check(_lib.fls_device_memcpy(device, b.ptr, arr.ctypes.data, arr.nbytes, 0))
+        return b
+
+    def read(self, offset: int = 0, nbytes: int | None = None) -> bytes:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            _check(_lib.fls_device_memcpy(self.device, out.ctypes.data, self.ptr + offset, n, 1))
+        return out.tobytes()
+
+    def free(self):
+        if self.ptr:
+            _lib.fls_device_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
 
 
 # --- engine ----------------------------------------------------------------

@@ -1,0 +1,420 @@
+// fls_encode.hip -- MI355X (gfx950) FastLanes chunk encoder: FFOR and
+// unified-transposed DELTA for integer columns, byte-identical to the CPU
+// writer's chunks (fls_writer.cpp enc_ffor / enc_delta / assemble_chunk).
+//
+// The write side of the scan path (COPY ... TO (FORMAT
+// FLS); the reference's writer is a stub, src/writer/write_fastlane_stream.cpp
+// :65-314).  The arithmetic is the decode kernel's run backwards:
+//   * one 256-thread block (4 waves) per column chunk (<= 64 vectors);
+//   * one pass per vector (one wave): the 1024 values (tail padded with the
+//     last value, as the CPU writer does) are staged in LDS; DELTA turns them
+//     into per-chain deltas in transposed position order (chain c = tuples
+//     blk*16T + l + 16k, FL_ORDER = {0,4,2,6,1,5,3,7}) and writes the chain
+//     bases; the wave reduces the signed minimum (FOR base) and the OR of
+//     value - base (bit width W), puts value - base in LDS in position order
+//     and every lane assembles 16-byte rows of the interleaved packing (word k
+//     of FastLanes lane L = bits [kT, kT + T) of lane L's stream of T values of
+//     W bits -- the inverse of fls_unpack.hpp) into the chunk's scratch area
+//     at the vector's widest position (v * 128 T);
+//   * wave 0 scans the vectors' 128 W packed bytes into offsets and writes the
+//     chunk header and the VecMeta records;
+//   * the waves copy each vector's packed rows from scratch (just written,
+//     cache-resident) to their place in the chunk, then the DELTA bases and
+//     the zero padding.  A vector's place depends on the widths of the vectors
+//     before it, so without the scratch area the input would be read twice
+//     (v1 did: 3.16 ms for 1e9 INT64 keys, 2.78 TB/s of algorithmic traffic,
+//     16.8 GB actually read; profiles/r1/encode_bench_v1_twopass.txt).
+// Integer work, HBM-bound: per value it reads T/8 bytes and writes W/8 bytes
+// (plus W/8 through the cached scratch).  No MFMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "../../include/flsgpu.h"
+#include "../../include/flswriter.h"
+#include "fls_common.hpp"
+#include "fls_decode.hpp"
+#include "fls_encode.hpp"
+#include "fls_format.hpp"
+#include "fls_unpack.hpp"
+
+namespace fls {
+namespace {
+using namespace dev;
+
+constexpr int kEncWaves = 4;
+
+__device__ __forceinline__ uint64_t tmask_d(uint32_t T) { return T >= 64 ? ~0ull : ((1ull << T) - 1ull); }
+__device__ __forceinline__ int64_t sext_d(uint64_t v, uint32_t T) {
+    if (T >= 64) return (int64_t)v;
+    const uint64_t sign = 1ull << (T - 1);
+    v &= tmask_d(T);
+    return (int64_t)((v ^ sign) - sign);
+}
+// transposed position p -> tuple index (FL_ORDER is the 3-bit bit reversal)
+__device__ __forceinline__ uint32_t tau_d(uint32_t p) {
+    const uint32_t b = (p >> 4) & 7;
+    const uint32_t rb = ((b & 1) << 2) | (b & 2) | ((b >> 2) & 1);
+    return (rb << 7) | (((p >> 7) & 7) << 4) | (p & 15);
+}
+__device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+// wave reductions (64-bit) through LDS-free cross-lane shuffles
+__device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int64_t y = (int64_t)__shfl_xor((unsigned long long)x, d, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
+    for (int d = 32; d >= 1; d >>= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, d, 64);
+    return x;
+}
+
+// 1024 values of vector v of the chunk into V (u64, zero-extended T-bit),
+// the tail past vn padded with the last value
+template <int T>
+__device__ __forceinline__ void stage_values(const uint8_t *in, uint32_t v, uint32_t vn, FLS_LDS uint64_t *V,
+                                             uint32_t lane) {
+    using U = typename std::conditional<T == 8, uint8_t,
+              typename std::conditional<T == 16, uint16_t,
+              typename std::conditional<T == 32, uint32_t, uint64_t>::type>::type>::type;
+    const FLS_GLOBAL U *src = (const FLS_GLOBAL U *)in + (size_t)v * kVectorSize;
+    if (vn == kVectorSize) {
+        // 16-byte loads: 16 / (T/8) values each
+        constexpr uint32_t per = 16 / (T / 8);
+        const FLS_GLOBAL v4u *s16 = reinterpret_cast<const FLS_GLOBAL v4u *>(src);
+        for (uint32_t q = lane; q < kVectorSize / per; q += 64) {
+            const v4u x = s16[q];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (uint32_t i = 0; i < per; ++i) {
+                uint64_t val;
+                if (T == 64) val = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+                else val = (w[(i * T) / 32] >> ((i * T) % 32)) & (uint32_t)tmask_d(T);
+                V[q * per + i] = val;
+            }
+        }
+    } else {
+        for (uint32_t j = lane; j < kVectorSize; j += 64) V[j] = (uint64_t)src[j < vn ? j : vn - 1];
+    }
+}
+
+// position-ordered value p of the vector staged in V: FFOR the value itself,
+// DELTA the delta of tuple tau(p) on its chain (0 at a chain start)
+template <int T, bool DELTA>
+__device__ __forceinline__ uint64_t pos_value(const FLS_LDS uint64_t *V, uint32_t p) {
+    if (!DELTA) return V[p];
+    const uint32_t i = tau_d(p);
+    return ((i >> 4) % T == 0) ? 0ull : (V[i] - V[i - 16]) & tmask_d(T);
+}
+
+struct VecStat {
+    int64_t base;
+    uint32_t W;
+};
+
+template <int T, bool DELTA>
+__device__ VecStat analyze(const FLS_LDS uint64_t *V, uint32_t lane) {
+    int64_t mn = INT64_MAX;
+#pragma unroll 4
+    for (uint32_t k = 0; k < 16; ++k) {
+        const int64_t x = sext_d(pos_value<T, DELTA>(V, lane + 64 * k), T);
+        mn = x < mn ? x : mn;
+    }
+    mn = wave_min_i64(mn);
+    uint64_t o = 0;
+#pragma unroll 4
+    for (uint32_t k = 0; k < 16; ++k) o |= (pos_value<T, DELTA>(V, lane + 64 * k) - (uint64_t)mn) & tmask_d(T);
+    o = wave_or_u64(o);
+    VecStat s;
+    s.base = mn;
+    s.W = o ? 64u - (uint32_t)__builtin_clzll(o) : 0u;
+    return s;
+}
+
+// Interleaved packing of the position-ordered u = value - base staged in U:
+// 16-byte row chunk ci = (word row k = ci / 8, byte column 16 (ci % 8)) holds
+// word k of FastLanes lanes L = (ci % 8) * 128/T + j, j < 128/T; word k of lane
+// L = OR over rows r of u[r * 1024/T + L] << (r W - k T) (bits [kT, kT + T) of
+// the lane's stream).
+template <int T>
+__device__ void pack_vector(const FLS_LDS uint64_t *U, uint32_t W, FLS_GLOBAL uint8_t *dst, uint32_t lane) {
+    constexpr uint32_t nl = kVectorSize / T, wpc = 128 / T;  // lanes, words per 16 B
+    const uint64_t tm = tmask_d(T);
+    for (uint32_t ci = lane; ci < 8 * W; ci += 64) {
+        const uint32_t k = ci >> 3, L0 = (ci & 7) * wpc;
+        const uint32_t r0 = (k * T) / W, r1 = min((uint32_t)T - 1, ((k + 1) * T - 1) / W);
+        uint32_t out[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t j = 0; j < wpc; ++j) {
+            uint64_t word = 0;
+            for (uint32_t r = r0; r <= r1; ++r) {
+                const uint64_t u = U[r * nl + L0 + j];
+                const int32_t sh = (int32_t)(r * W) - (int32_t)(k * T);
+                word |= sh >= 0 ? (sh < 64 ? u << sh : 0ull) : u >> (uint32_t)(-sh);
+            }
+            word &= tm;
+            // place word j (T bits) into the 16-byte chunk
+            if (T == 64) {
+                out[2 * j] = (uint32_t)word;
+                out[2 * j + 1] = (uint32_t)(word >> 32);
+            } else {
+                out[(j * T) / 32] |= (uint32_t)word << ((j * T) % 32);
+            }
+        }
+        *reinterpret_cast<FLS_GLOBAL v4u *>(dst + 16ull * ci) = mk4(out[0], out[1], out[2], out[3]);
+    }
+}
+
+template <int T, bool DELTA>
+__device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS uint32_t *Wv,
+                             FLS_LDS int64_t *Bv, FLS_LDS uint64_t *Ov) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    FLS_LDS uint64_t *V = Vall + w * kVectorSize;
+    const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
+    const uint8_t *in = (const uint8_t *)c.in;
+    FLS_GLOBAL uint8_t *out = (FLS_GLOBAL uint8_t *)c.out;
+    FLS_GLOBAL uint8_t *scratch = (FLS_GLOBAL uint8_t *)c.scratch;
+    // ---- one pass per vector: base, width, DELTA bases, packing into scratch
+    // (bases go to scratch too, after the packed vectors: their place in the
+    // chunk also depends on every width)
+    FLS_GLOBAL uint8_t *sbases = scratch + 128ull * T * kVectorsPerRowGroup;
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
+        stage_values<T>(in, v, vn, V, lane);
+        wave_sync();
+        const VecStat s = analyze<T, DELTA>(V, lane);
+        if (lane == 0) {
+            Wv[v] = s.W;
+            Bv[v] = s.base;
+        }
+        if (DELTA) {
+            // chain c's base = its first tuple blk*16T + l (put_word layout, T/8 bytes)
+            if (lane < kVectorSize / T) {
+                const uint64_t b = V[(lane / 16) * 16 * T + (lane % 16)];
+                FLS_GLOBAL uint8_t *bp = sbases + 128ull * v + lane * (T / 8);
+                if (T == 64) *(FLS_GLOBAL uint64_t *)bp = b;
+                else if (T == 32) *(FLS_GLOBAL uint32_t *)bp = (uint32_t)b;
+                else if (T == 16) *(FLS_GLOBAL uint16_t *)bp = (uint16_t)b;
+                else *bp = (uint8_t)b;
+            }
+            if (T == 8 && lane < 64) {  // 128 chains of T = 8: lanes 0..63 take chains 64..127 too
+                const uint32_t c2 = lane + 64;
+                sbases[128ull * v + c2] = (uint8_t)V[(c2 / 16) * 16 * T + (c2 % 16)];
+            }
+        }
+        uint64_t u[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k)
+            u[k] = (pos_value<T, DELTA>(V, lane + 64 * k) - (uint64_t)s.base) & tmask_d(T);
+        wave_sync();
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = u[k];
+        wave_sync();
+        pack_vector<T>(V, s.W, scratch + 128ull * T * v, lane);
+        wave_sync();
+    }
+    __syncthreads();
+    // ---- chunk layout (assemble_chunk) --------------------------------------
+    const uint64_t meta_off = sizeof(ChunkHeader);
+    const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
+    if (w == 0) {
+        const uint32_t pw = lane < nvec ? 128u * Wv[lane] : 0u;
+        uint32_t incl = pw;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        const uint64_t packed_total = rl(incl, 63);
+        const uint64_t aux_off = (packed_off + packed_total + 15) & ~15ull;
+        const uint64_t aux_len = DELTA ? 128ull * nvec : 0ull;
+        const uint64_t total = (aux_off + aux_len + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
+        if (lane < nvec) {
+            VecMeta m;
+            m.packed_off = incl - pw;
+            m.for_base = Bv[lane];
+            m.aux_off = DELTA ? 128ull * lane : 0ull;
+            m.nvals = (uint16_t)min(kVectorSize, n - lane * kVectorSize);
+            m.bw = (uint8_t)Wv[lane];
+            m.pad = 0;
+            m.aux_count = 0;
+            const uint32_t *mw = reinterpret_cast<const uint32_t *>(&m);
+            FLS_GLOBAL uint32_t *dm = reinterpret_cast<FLS_GLOBAL uint32_t *>(out + meta_off + sizeof(VecMeta) * lane);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dm[i] = mw[i];
+            Ov[lane] = incl - pw;
+        }
+        if (lane == 0) {
+            ChunkHeader h;
+            h.magic = kChunkMagic;
+            h.enc = DELTA ? ENC_DELTA : ENC_FFOR;
+            h.T = (uint8_t)T;
+            h.vbits = (uint8_t)T;
+            h.is_str = 0;
+            h.nvec = nvec;
+            h.nvals = n;
+            h.meta_off = meta_off;
+            h.packed_off = packed_off;
+            h.aux_off = aux_off;
+            h.aux_len = aux_len;
+            h.dict_count = 0;
+            h.reserved0 = 0;
+            h.reserved1 = 0;
+            const uint32_t *hw = reinterpret_cast<const uint32_t *>(&h);
+            FLS_GLOBAL uint32_t *dh = reinterpret_cast<FLS_GLOBAL uint32_t *>(out);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dh[i] = hw[i];
+            Ov[64] = packed_total;
+            Ov[65] = aux_off;
+            Ov[66] = total;
+            *(FLS_GLOBAL uint64_t *)c.len_out = total;
+        }
+    }
+    __syncthreads();
+    const uint64_t packed_total = Ov[64], aux_off = Ov[65], total = Ov[66];
+    // ---- packed rows from scratch to their place; DELTA bases; padding -----
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(scratch + 128ull * T * v);
+        FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + packed_off + Ov[v]);
+        for (uint32_t i = lane; i < 8 * Wv[v]; i += 64) dst[i] = src[i];
+    }
+    if (DELTA) {
+        const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(sbases);
+        FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + aux_off);
+        for (uint32_t i = threadIdx.x; i < 8 * nvec; i += blockDim.x) dst[i] = src[i];
+    }
+    {
+        const uint64_t gaps[3][2] = {{meta_off + sizeof(VecMeta) * nvec, packed_off},
+                                     {packed_off + packed_total, aux_off},
+                                     {aux_off + (DELTA ? 128ull * nvec : 0ull), total}};
+        for (int g = 0; g < 3; ++g)
+            for (uint64_t b = gaps[g][0] + threadIdx.x; b < gaps[g][1]; b += blockDim.x) out[b] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void encode_kernel(const EncChunk *__restrict__ chunks, uint32_t nchunks) {
+    __shared__ uint64_t Vall[kEncWaves * kVectorSize];
+    __shared__ uint32_t Wv[64];
+    __shared__ int64_t Bv[64];
+    __shared__ uint64_t Ov[67];
+    const EncChunk c = chunks[blockIdx.x];
+    FLS_LDS uint64_t *V = (FLS_LDS uint64_t *)Vall;
+    FLS_LDS uint32_t *W = (FLS_LDS uint32_t *)Wv;
+    FLS_LDS int64_t *B = (FLS_LDS int64_t *)Bv;
+    FLS_LDS uint64_t *O = (FLS_LDS uint64_t *)Ov;
+    const bool delta = c.enc == ENC_DELTA;
+    switch (c.T) {
+    case 8: delta ? encode_chunk<8, true>(c, V, W, B, O) : encode_chunk<8, false>(c, V, W, B, O); break;
+    case 16: delta ? encode_chunk<16, true>(c, V, W, B, O) : encode_chunk<16, false>(c, V, W, B, O); break;
+    case 32: delta ? encode_chunk<32, true>(c, V, W, B, O) : encode_chunk<32, false>(c, V, W, B, O); break;
+    default: delta ? encode_chunk<64, true>(c, V, W, B, O) : encode_chunk<64, false>(c, V, W, B, O); break;
+    }
+}
+
+}  // namespace
+
+uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
+    const uint64_t nvec = (nrows + kVectorSize - 1) / kVectorSize;
+    const uint64_t packed_off = (sizeof(ChunkHeader) + sizeof(VecMeta) * nvec + 15) & ~15ull;
+    const uint64_t aux = enc == ENC_DELTA ? 128ull * nvec : 0ull;
+    return (packed_off + 128ull * T * nvec + aux + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
+}
+
+hipError_t launch_encode(const EncChunk *d_chunks, uint32_t nchunks, hipStream_t stream) {
+    if (nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(encode_kernel, dim3(nchunks), dim3(64 * kEncWaves), 0, stream, d_chunks, nchunks);
+    return hipGetLastError();
+}
+
+}  // namespace fls
+
+using namespace fls;
+
+#define ENC_HIP(expr)                                                                           \
+    do {                                                                                        \
+        const hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" {
+
+uint64_t fls_encode_slot_bytes(uint8_t type, uint8_t encoding, uint32_t rowgroup_rows) {
+    const int T = type_value_bits(type);
+    if (T == 0 || type_is_float(type)) return 0;
+    return enc_slot_bytes((uint32_t)T, rowgroup_rows, encoding);
+}
+
+int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_values, uint64_t nrows,
+                      uint32_t rowgroup_rows, void *d_out, uint64_t *chunk_lens, float *kernel_ms) {
+    const int T = type_value_bits(type);
+    if (T == 0 || type_is_float(type) || type == TY_VARCHAR)
+        return fail(FLS_ERR_ARG, "fls_encode_device: integer types only (type %u)", type);
+    if (encoding != ENC_FFOR && encoding != ENC_DELTA)
+        return fail(FLS_ERR_ARG, "fls_encode_device: FFOR or DELTA only (encoding %u)", encoding);
+    if (!d_values || !d_out || !chunk_lens || nrows == 0) return fail(FLS_ERR_ARG, "fls_encode_device: bad argument");
+    if (rowgroup_rows == 0 || rowgroup_rows > kRowGroupSize || rowgroup_rows % kVectorSize)
+        return fail(FLS_ERR_ARG, "fls_encode_device: row group size %u", rowgroup_rows);
+    if (((uintptr_t)d_values & 15) || ((uintptr_t)d_out & 15))
+        return fail(FLS_ERR_ARG, "fls_encode_device: buffers must be 16-byte aligned");
+    const uint64_t nrg = (nrows + rowgroup_rows - 1) / rowgroup_rows;
+    const uint64_t slot = enc_slot_bytes((uint32_t)T, rowgroup_rows, encoding);
+    ENC_HIP(hipSetDevice(device));
+    // scratch: one area per chunk, kept per device across calls (grown as needed)
+    static std::mutex mu;
+    static std::vector<std::pair<uint8_t *, uint64_t>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((size_t)device >= cache.size()) cache.resize(device + 1, {nullptr, 0});
+    const uint64_t need = nrg * enc_scratch_bytes((uint32_t)T);
+    if (cache[device].second < need) {
+        hipFree(cache[device].first);
+        cache[device] = {nullptr, 0};
+        ENC_HIP(hipMalloc((void **)&cache[device].first, need));
+        cache[device].second = need;
+    }
+    uint8_t *scratch = cache[device].first;
+    std::vector<EncChunk> desc(nrg);
+    EncChunk *d_desc = nullptr;
+    uint64_t *d_lens = nullptr;
+    ENC_HIP(hipMalloc((void **)&d_desc, nrg * sizeof(EncChunk)));
+    const hipError_t ea = hipMalloc((void **)&d_lens, nrg * sizeof(uint64_t));
+    if (ea != hipSuccess) {
+        hipFree(d_desc);
+        return fail(FLS_ERR_DEVICE, "hipMalloc: %s", hipGetErrorString(ea));
+    }
+    for (uint64_t i = 0; i < nrg; ++i) {
+        EncChunk &c = desc[i];
+        c.in = (uint64_t)(uintptr_t)d_values + i * rowgroup_rows * (uint64_t)(T / 8);
+        c.out = (uint64_t)(uintptr_t)d_out + i * slot;
+        c.len_out = (uint64_t)(uintptr_t)(d_lens + i);
+        c.scratch = (uint64_t)(uintptr_t)(scratch + i * enc_scratch_bytes((uint32_t)T));
+        c.nrows = (uint32_t)std::min<uint64_t>(rowgroup_rows, nrows - i * rowgroup_rows);
+        c.T = (uint8_t)T;
+        c.enc = encoding;
+        c.pad[0] = c.pad[1] = 0;
+        c.pad2 = 0;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipMemcpy(d_desc, desc.data(), nrg * sizeof(EncChunk), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipEventRecord(e0, nullptr);
+    if (e == hipSuccess) e = launch_encode(d_desc, (uint32_t)nrg, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) e = hipMemcpy(chunk_lens, d_lens, nrg * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    hipFree(d_desc);
+    hipFree(d_lens);
+    if (e != hipSuccess) return fail(FLS_ERR_DEVICE, "fls_encode_device: %s", hipGetErrorString(e));
+    if (kernel_ms) *kernel_ms = ms;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,31 @@
+// fls_encode.hpp -- GPU chunk encoder (fls_encode.hip): launch descriptors.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace fls {
+
+// One column chunk to encode (one block of encode_kernel).
+struct EncChunk {
+    uint64_t in;       // device address of the chunk's first value (T/8 bytes each)
+    uint64_t out;      // device address of the chunk's output slot (enc_slot_bytes)
+    uint64_t len_out;  // device address of a uint64: the chunk's byte length (written)
+    uint64_t scratch;  // device address of enc_scratch_bytes(T) bytes for the packed vectors
+    uint32_t nrows;    // rows of the chunk (1..65536)
+    uint8_t T, enc;    // packing width 8/16/32/64; ENC_FFOR or ENC_DELTA
+    uint8_t pad[2];
+    uint64_t pad2;
+};
+static_assert(sizeof(EncChunk) == 48, "EncChunk is 48 B");
+
+// Scratch bytes per chunk: every vector packed at its widest (64 x 128 T),
+// then 64 x 128 B of DELTA chain bases.
+inline uint64_t enc_scratch_bytes(uint32_t T) { return 64ull * 128ull * T + 64ull * 128ull; }
+
+// Bytes an output slot needs for a chunk of nrows values (the chunk at W = T).
+uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
+// Encode nchunks chunks (d_chunks in device memory), one block each.
+hipError_t launch_encode(const EncChunk *d_chunks, uint32_t nchunks, hipStream_t stream);
+
+}  // namespace fls

@@ -22,6 +22,7 @@
 #include "../../include/flswriter.h"
 #include "fls_alp.hpp"
 #include "fls_common.hpp"
+#include "fls_encode.hpp"
 #include "fls_format.hpp"
 #include "fls_gen.hpp"
 #include "fls_text.hpp"
@@ -1033,9 +1034,151 @@ int default_writer_threads() {
 }
 }  // namespace
 
+// GPU chunk encoding of a row group's FFOR / DELTA integer columns
+// (fls_writer_set_device): the columns' values go through one pinned staging
+// buffer and one H2D copy, one encode_kernel launch (a block per chunk), then
+// the lengths and one D2H copy per chunk.  Buffers are kept across row groups.
+struct GpuEncoder {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *h_stage = nullptr, *d_in = nullptr, *d_out = nullptr, *d_scratch = nullptr;
+    uint64_t *h_lens = nullptr, *d_lens = nullptr;
+    EncChunk *d_desc = nullptr;
+    size_t in_cap = 0, out_cap = 0, desc_cap = 0;
+
+    void release() {
+        if (dev < 0) return;
+        hipSetDevice(dev);
+        if (stream) hipStreamSynchronize(stream);
+        hipHostFree(h_stage);
+        hipHostFree(h_lens);
+        hipFree(d_in);
+        hipFree(d_out);
+        hipFree(d_lens);
+        hipFree(d_desc);
+        hipFree(d_scratch);
+        if (stream) hipStreamDestroy(stream);
+        h_stage = d_in = d_out = d_scratch = nullptr;
+        h_lens = d_lens = nullptr;
+        d_desc = nullptr;
+        stream = nullptr;
+        in_cap = out_cap = desc_cap = 0;
+    }
+    ~GpuEncoder() { release(); }
+
+    std::vector<size_t> pending_cols, pending_out_off;  // submitted, not yet collected
+
+    // Submit columns cols of one row group (nrows rows): staging, H2D, one
+    // encode_kernel launch, the lengths back; collect() finishes it.
+    int submit(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, uint32_t nrows,
+               const void *const *data, int nthreads) {
+#define WHIP(expr)                                                                                  \
+    do {                                                                                            \
+        const hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+        WHIP(hipSetDevice(dev));
+        if (!stream) WHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        std::vector<size_t> in_off(cols.size()), out_off(cols.size());
+        size_t in_total = 0, out_total = 0;
+        for (size_t i = 0; i < cols.size(); ++i) {
+            const ColSpec &cs = specs[cols[i]];
+            const int T = type_value_bits(cs.type);
+            in_off[i] = in_total;
+            in_total += ((size_t)nrows * (T / 8) + 15) & ~size_t(15);
+            out_off[i] = out_total;
+            out_total += enc_slot_bytes((uint32_t)T, nrows, cs.enc);
+        }
+        if (in_total > in_cap) {
+            hipHostFree(h_stage);
+            hipFree(d_in);
+            h_stage = d_in = nullptr;
+            in_cap = 0;
+            WHIP(hipHostMalloc((void **)&h_stage, in_total, 0));
+            WHIP(hipMalloc((void **)&d_in, in_total));
+            in_cap = in_total;
+        }
+        if (out_total > out_cap) {
+            hipFree(d_out);
+            d_out = nullptr;
+            out_cap = 0;
+            WHIP(hipMalloc((void **)&d_out, out_total));
+            out_cap = out_total;
+        }
+        if (cols.size() > desc_cap) {
+            hipFree(d_desc);
+            hipFree(d_lens);
+            hipHostFree(h_lens);
+            hipFree(d_scratch);
+            d_desc = nullptr;
+            d_lens = h_lens = nullptr;
+            d_scratch = nullptr;
+            desc_cap = 0;
+            WHIP(hipMalloc((void **)&d_desc, cols.size() * sizeof(EncChunk)));
+            WHIP(hipMalloc((void **)&d_lens, cols.size() * sizeof(uint64_t)));
+            WHIP(hipHostMalloc((void **)&h_lens, cols.size() * sizeof(uint64_t), 0));
+            WHIP(hipMalloc((void **)&d_scratch, cols.size() * enc_scratch_bytes(64)));
+            desc_cap = cols.size();
+        }
+        // stage the columns into pinned memory, column-parallel (one memcpy
+        // thread would cap the path at a few GB/s)
+        {
+            std::atomic<size_t> next{0};
+            auto work = [&]() {
+                for (size_t i; (i = next.fetch_add(1)) < cols.size();)
+                    memcpy(h_stage + in_off[i], data[cols[i]],
+                           (size_t)nrows * (type_value_bits(specs[cols[i]].type) / 8));
+            };
+            std::vector<std::thread> th;
+            const size_t nth = std::min<size_t>(cols.size(), (size_t)std::max(1, nthreads));
+            for (size_t t = 1; t < nth; ++t) th.emplace_back(work);
+            work();
+            for (auto &t : th) t.join();
+        }
+        std::vector<EncChunk> desc(cols.size());
+        for (size_t i = 0; i < cols.size(); ++i) {
+            const ColSpec &cs = specs[cols[i]];
+            const int T = type_value_bits(cs.type);
+            EncChunk &c = desc[i];
+            c.in = (uint64_t)(uintptr_t)(d_in + in_off[i]);
+            c.out = (uint64_t)(uintptr_t)(d_out + out_off[i]);
+            c.len_out = (uint64_t)(uintptr_t)(d_lens + i);
+            c.scratch = (uint64_t)(uintptr_t)(d_scratch + i * enc_scratch_bytes(64));
+            c.nrows = nrows;
+            c.T = (uint8_t)T;
+            c.enc = cs.enc;
+            c.pad[0] = c.pad[1] = 0;
+            c.pad2 = 0;
+        }
+        WHIP(hipMemcpyAsync(d_in, h_stage, in_total, hipMemcpyHostToDevice, stream));
+        WHIP(hipMemcpyAsync(d_desc, desc.data(), cols.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
+        WHIP(launch_encode(d_desc, (uint32_t)cols.size(), stream));
+        WHIP(hipMemcpyAsync(h_lens, d_lens, cols.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        pending_cols = cols;
+        pending_out_off = out_off;
+        return 0;
+    }
+
+    // Wait for the row group submitted last and copy its chunks into chunks[c].
+    int collect(std::vector<std::vector<uint8_t>> &chunks) {
+        const std::vector<size_t> &cols = pending_cols;
+        const std::vector<size_t> &out_off = pending_out_off;
+        WHIP(hipSetDevice(dev));
+        WHIP(hipStreamSynchronize(stream));
+        for (size_t i = 0; i < cols.size(); ++i) {
+            chunks[cols[i]].resize(h_lens[i]);
+            WHIP(hipMemcpyAsync(chunks[cols[i]].data(), d_out + out_off[i], h_lens[i], hipMemcpyDeviceToHost, stream));
+        }
+        WHIP(hipStreamSynchronize(stream));
+#undef WHIP
+        return 0;
+    }
+};
+
 struct fls_writer {
     FileBuilder fb;
     int threads = default_writer_threads();  // column-parallel encode per row group
+    GpuEncoder gpu;                          // fls_writer_set_device
 };
 
 extern "C" {
@@ -1090,6 +1233,24 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
     rg.nrows = nrows;
     rg.chunks.resize(ncols);
     rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
+    // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA
+    std::vector<uint8_t> on_gpu(ncols, 0);
+    if (w->gpu.dev >= 0) {
+        std::vector<size_t> gcols;
+        for (size_t c = 0; c < ncols; ++c) {
+            const ColSpec &cs = w->fb.cols[c];
+            if (cs.type != TY_VARCHAR && !type_is_float(cs.type) && (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA)) {
+                gcols.push_back(c);
+                on_gpu[c] = 1;
+            }
+        }
+        if (!gcols.empty()) {
+            const int rc = w->gpu.submit(w->fb.cols, gcols, nrows, data, w->threads);
+            if (rc) return rc;
+        }
+    }
+    // (the GPU encodes while the CPU threads below build the zone maps and
+    // encode the other columns)
     // columns are independent: encode them on up to w->threads threads
     auto encode_col = [&](size_t c) {
         const ColSpec &cs = w->fb.cols[c];
@@ -1105,7 +1266,7 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
             memcpy(&x, p + (size_t)i * (T / 8), T / 8);
             v[i] = x;
         }
-        rg.chunks[c] = encode_int_chunk(cs.type, cs.enc, v.data(), nrows);
+        if (!on_gpu[c]) rg.chunks[c] = encode_int_chunk(cs.type, cs.enc, v.data(), nrows);
         rg.zones[c] = zone_of(cs.type, v.data(), nrows);
     };
     const size_t nth = std::min<size_t>(ncols, (size_t)std::max(1, w->threads));
@@ -1121,6 +1282,11 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
         work();
         for (auto &t : th) t.join();
     }
+    if (w->gpu.dev >= 0 && !w->gpu.pending_cols.empty()) {
+        const int rc = w->gpu.collect(rg.chunks);
+        w->gpu.pending_cols.clear();
+        if (rc) return rc;
+    }
     w->fb.rgs.push_back(std::move(rg));
     return 0;
 }
@@ -1128,6 +1294,18 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
 int fls_writer_set_threads(fls_writer *w, int nthreads) {
     if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_threads: NULL writer");
     w->threads = nthreads > 0 ? nthreads : default_writer_threads();
+    return 0;
+}
+
+int fls_writer_set_device(fls_writer *w, int device) {
+    if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_device: NULL writer");
+    w->gpu.release();
+    w->gpu.dev = -1;
+    if (device < 0) return 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device >= n)
+        return fail(FLS_ERR_DEVICE, "fls_writer_set_device: no GPU %d (%d visible)", device, n);
+    w->gpu.dev = device;
     return 0;
 }
 

@@ -1083,6 +1083,31 @@ int fls_device_count(void) {
     return n;
 }
 
+int fls_device_alloc(int device, uint64_t bytes, void **ptr) {
+    if (!ptr) return fail(FLS_ERR_ARG, "fls_device_alloc: NULL out");
+    *ptr = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMalloc(ptr, std::max<uint64_t>(bytes, 1)));
+    return 0;
+}
+
+int fls_device_free(int device, void *ptr) {
+    if (!ptr) return 0;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipFree(ptr));
+    return 0;
+}
+
+int fls_device_memcpy(int device, void *dst, const void *src, uint64_t bytes, int kind) {
+    if (!dst || !src) return fail(FLS_ERR_ARG, "fls_device_memcpy: NULL pointer");
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                           : hipMemcpyDeviceToDevice;
+    if (kind < 0 || kind > 2) return fail(FLS_ERR_ARG, "fls_device_memcpy: kind %d", kind);
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMemcpy(dst, src, bytes, k));
+    return 0;
+}
+
 int fls_connect(const int *devices, int ndevices, fls_connection **out) {
     if (!out) return fail(FLS_ERR_ARG, "fls_connect: NULL out");
     auto *c = new fls_connection();

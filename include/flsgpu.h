@@ -113,6 +113,12 @@ const char *fls_last_error(void);
 const char *fls_version(void);
 /* Number of HIP devices visible (0 when there is no GPU). */
 int fls_device_count(void);
+/* Raw device buffers and copies on GPU `device`, for callers that hold no HIP
+ * runtime of their own (bindings, tests, the encoder bench): kind 0 = host to
+ * device, 1 = device to host, 2 = device to device. */
+int fls_device_alloc(int device, uint64_t bytes, void **ptr);
+int fls_device_free(int device, void *ptr);
+int fls_device_memcpy(int device, void *dst, const void *src, uint64_t bytes, int kind);
 
 /* fastlanes::connect(): devices = HIP ordinals to shard row groups over
  * (NULL/0 = device 0). */

@@ -50,6 +50,21 @@ int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows);
 /* Threads encoding the columns of a row group in parallel (0 = default:
  * min(16, hardware threads)).  Output bytes do not depend on it. */
 int fls_writer_set_threads(fls_writer *w, int nthreads);
+/* Encode the FFOR and DELTA integer columns of every later row group on GPU
+ * `device` (fls_encode.hip: one block per column chunk); -1 = CPU (default).
+ * The chunks are byte-identical to the CPU writer's.  Other columns (AUTO,
+ * DICT, RLE, ALP, VARCHAR) stay on the CPU threads. */
+int fls_writer_set_device(fls_writer *w, int device);
+
+/* GPU chunk encoder over a device-resident integer column (the write side of
+ * the scan path).  nrows values of `type` (1/2/4/8 B,
+ * 16-byte aligned) at d_values become ceil(nrows / rowgroup_rows) FFOR or
+ * DELTA chunks, chunk i at d_out + i * fls_encode_slot_bytes(type, encoding,
+ * rowgroup_rows), byte-identical to the CPU writer's; chunk_lens (host, one per
+ * chunk) receive their lengths, kernel_ms (may be NULL) the kernel time. */
+uint64_t fls_encode_slot_bytes(uint8_t type, uint8_t encoding, uint32_t rowgroup_rows);
+int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_values, uint64_t nrows,
+                      uint32_t rowgroup_rows, void *d_out, uint64_t *chunk_lens, float *kernel_ms);
 /* Append one row group of nrows (1..row group size) rows; only the last row
  * group of a file may be short.  Integer / FLOAT / DOUBLE column c:
  * data[c] -> nrows values of the column's width (1/2/4/8 B).  VARCHAR column c:

@@ -1,0 +1,116 @@
+"""GPU chunk encoder (csrc/fls_encode.hip): FFOR / DELTA chunks byte-identical
+to the CPU writer's (csrc/fls_writer.cpp enc_ffor / enc_delta), which the
+oracle tests pin against the restated FastLanes layout.  The write side of the
+scan path: SURVEY.md 8(f) row 1 (COPY ... TO (FORMAT FLS); the reference's
+writer is a stub, src/writer/write_fastlane_stream.cpp:65-314)."""
+import numpy as np
+import pytest
+
+INT_TYPES = ["INT8", "INT16", "INT32", "INT64", "UINT8", "UINT16", "UINT32", "UINT64", "DATE", "DECIMAL"]
+
+
+def _columns(fl, n, rng):
+    """Every integer type under FFOR and DELTA, with value shapes that hit
+    W = 0 (constant), W = T (full range), negative bases, sorted keys."""
+    cols = []
+    for tn in INT_TYPES:
+        ty = getattr(fl, tn)
+        dt = np.dtype(fl.NP_DTYPE[ty])
+        info = np.iinfo(dt)
+        full = rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+        small = (rng.integers(-50, 50, n) + (int(info.min) + int(info.max)) // 2).astype(dt)
+        const = np.full(n, info.max // 3, dtype=dt)
+        keys = np.sort(rng.integers(info.min // 2, info.max // 2, n, dtype=dt))
+        for enc in (fl.ENC_FFOR, fl.ENC_DELTA):
+            e = "ffor" if enc == fl.ENC_FFOR else "delta"
+            cols += [(f"{tn}_{e}_full", ty, full, enc), (f"{tn}_{e}_small", ty, small, enc),
+                     (f"{tn}_{e}_const", ty, const, enc), (f"{tn}_{e}_keys", ty, keys, enc)]
+    return cols
+
+
+def test_encode_slot_bytes(fl):
+    # header + VecMeta[64] + 128 T bytes per vector (W <= T), DELTA + 128 B
+    # bases per vector, rounded up to the 256-byte chunk alignment
+    def r256(x):
+        return (x + 255) // 256 * 256
+    assert fl.encode_slot_bytes(fl.INT64, fl.ENC_FFOR) == r256(64 + 64 * 32 + 64 * 128 * 64)
+    assert fl.encode_slot_bytes(fl.INT64, fl.ENC_DELTA) == r256(64 + 64 * 32 + 64 * 128 * 64 + 64 * 128)
+    assert fl.encode_slot_bytes(fl.INT8, fl.ENC_FFOR, 1024) % 256 == 0
+    assert fl.encode_slot_bytes(fl.FLOAT, fl.ENC_ALP) == 0
+
+
+def test_set_device_rejects_missing_gpu(fl):
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_set_device(w, 1 << 20) < 0
+        assert fl.lib.fls_writer_set_device(w, -1) == 0
+    finally:
+        fl.lib.fls_writer_free(w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (1024, 1024), (1, 65536),
+                                        (65536 * 3, 65536)])
+def test_gpu_writer_bytes_identical(fl, gpu, n, rowgroup):
+    cols = _columns(fl, n, np.random.default_rng(n))
+    cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+
+
+@pytest.mark.gpu
+def test_gpu_writer_mixed_columns_and_decode(fl, ref, gpu):
+    """GPU-encoded FFOR / DELTA columns next to CPU-encoded AUTO / DICT /
+    VARCHAR ones in one file; the file decodes exactly on the GPU."""
+    from helpers import assert_column_equal, gpu_decode_all
+    rng = np.random.default_rng(5)
+    n = 150000
+    keys = np.cumsum(rng.integers(0, 4, n)).astype(np.int64)
+    cols = [("k", fl.INT64, keys, fl.ENC_DELTA), ("q", fl.INT32, rng.integers(-9, 9, n), fl.ENC_FFOR),
+            ("a", fl.INT32, rng.integers(0, 3, n), fl.ENC_AUTO), ("d", fl.INT16, rng.integers(0, 5, n), fl.ENC_DICT),
+            ("s", fl.VARCHAR, [f"v{i % 7}" for i in range(n)], fl.ENC_AUTO)]
+    img = fl.write_image(cols, device=0)
+    assert img.tobytes() == fl.write_image(cols).tobytes()
+    t, st, out = gpu_decode_all(fl, img)
+    rf = ref.RefFile(img)
+    for c in range(t.ncols):
+        assert_column_equal(fl, rf, c, out[c], img.ptr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("enc", ["FFOR", "DELTA"])
+def test_gpu_encode_device_resident(fl, gpu, enc):
+    """fls_encode_device over a column already in HBM: the chunks, laid end to
+    end, are the CPU writer's file body for the same single-column table."""
+    rng = np.random.default_rng(11)
+    n = 65536 * 5 + 3000
+    vals = np.cumsum(rng.integers(0, 26, n)).astype(np.int64) + 1_000_000
+    e = getattr(fl, "ENC_" + enc)
+    cpu = fl.write_image([("k", fl.INT64, vals, e)]).tobytes()
+    d_in = fl.DeviceBuffer.from_array(vals)
+    slot = fl.encode_slot_bytes(fl.INT64, e)
+    nrg = (n + 65535) // 65536
+    d_out = fl.DeviceBuffer(slot * nrg)
+    lens, ms = fl.encode_device(0, fl.INT64, e, d_in.ptr, n, d_out.ptr)
+    assert ms > 0
+    body = b"".join(d_out.read(i * slot, lens[i]) for i in range(nrg))
+    assert body == cpu[256:256 + len(body)]
+    assert sum(lens) == len(body)
+
+
+@pytest.mark.gpu
+def test_gpu_encode_device_1e8_keys(fl, gpu):
+    """At 1e8 rows: GPU-encoded DELTA chunks of config 3's sorted keys equal the
+    CPU writer's chunk for the same row group (sampled row groups)."""
+    n = 100_000_000
+    vals = fl.gen_values("c3", 0, 0, n, np.int64, 1.0, n)
+    d_in = fl.DeviceBuffer.from_array(vals)
+    slot = fl.encode_slot_bytes(fl.INT64, fl.ENC_DELTA)
+    nrg = (n + 65535) // 65536
+    d_out = fl.DeviceBuffer(slot * nrg)
+    lens, ms = fl.encode_device(0, fl.INT64, fl.ENC_DELTA, d_in.ptr, n, d_out.ptr)
+    for rg in sorted({0, 1, nrg // 2, nrg - 1}):
+        part = vals[rg * 65536:(rg + 1) * 65536]
+        cpu = fl.write_image([("k", fl.INT64, part, fl.ENC_DELTA)]).tobytes()
+        assert d_out.read(rg * slot, lens[rg]) == cpu[256:256 + lens[rg]], rg
