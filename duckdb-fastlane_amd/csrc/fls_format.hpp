@@ -210,4 +210,35 @@ inline ZoneMap zone_of(uint8_t type, const uint64_t *raw, uint32_t n) {
     return z;
 }
 
+// Zone map of n integer values stored in the column's own width (1/2/4/8 B):
+// the same result as zone_of over their raw patterns, one vectorisable pass
+// without widening (the writer's GPU-encoded columns never widen their data).
+template <class I>
+inline ZoneMap zone_of_ints(const I *v, uint32_t n) {
+    ZoneMap z{0, 0, ZM_VALID, 0};
+    I mn = v[0], mx = v[0];
+    for (uint32_t i = 1; i < n; ++i) {
+        mn = v[i] < mn ? v[i] : mn;
+        mx = v[i] > mx ? v[i] : mx;
+    }
+    if (I(-1) < I(0)) {  // signed: sign-extended int64 patterns
+        z.min = (uint64_t)(int64_t)mn;
+        z.max = (uint64_t)(int64_t)mx;
+    } else {
+        z.min = (uint64_t)mn;
+        z.max = (uint64_t)mx;
+    }
+    return z;
+}
+inline ZoneMap zone_of_typed(uint8_t type, const void *data, uint32_t n) {
+    if (n == 0 || type_is_float(type) || type_value_bits(type) == 0) return ZoneMap{0, 0, 0, 0};
+    const bool sg = type_is_signed(type);
+    switch (type_value_bits(type)) {
+    case 8: return sg ? zone_of_ints((const int8_t *)data, n) : zone_of_ints((const uint8_t *)data, n);
+    case 16: return sg ? zone_of_ints((const int16_t *)data, n) : zone_of_ints((const uint16_t *)data, n);
+    case 32: return sg ? zone_of_ints((const int32_t *)data, n) : zone_of_ints((const uint32_t *)data, n);
+    default: return sg ? zone_of_ints((const int64_t *)data, n) : zone_of_ints((const uint64_t *)data, n);
+    }
+}
+
 }  // namespace fls
