@@ -508,12 +508,14 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
 // atomic per piece, so no vector is decoded twice and late waves find work.
 // (A piece queue for standalone launches measured 2-4 % slower on l_comment
 // at SF10: more symbol-table reloads.)
-template <int BPL, bool SMALL>
+// (QUEUE is a template parameter: one kernel holding both loops needed 98
+// VGPRs instead of 82 for <8, small>, one wave per SIMD less.)
+template <int BPL, bool SMALL, bool QUEUE>
 __global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                      uint32_t nitems, uint32_t *__restrict__ err,
                                                      uint32_t *__restrict__ queue, uint32_t piece) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
-    if (!queue) {
+    if (!QUEUE) {
         const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
         const uint32_t per = (nitems + nwaves - 1) / nwaves;
         const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
@@ -530,14 +532,15 @@ __global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict_
     }
 }
 
-template <int BPL, bool SMALL>
-hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+template <int BPL, bool SMALL, bool QUEUE>
+hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     const uint32_t shmem = Lds<BPL, SMALL>::kWave;
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL>, 64, shmem) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL, QUEUE>, 64, shmem) !=
+            hipSuccess)
             per_cu = 1;
     }
     const int full = cus * std::max(1, per_cu);
@@ -551,9 +554,15 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
     if (getenv("FLS_DEBUG"))
         fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors%s\n", BPL,
                 SMALL ? "small" : "any", grid, per_cu, shmem, nvecs, how.queue ? " (piece queue)" : "");
-    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err,
-                       how.queue, piece);
+    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL, QUEUE>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs,
+                       d_err, how.queue, piece);
     return hipGetLastError();
+}
+template <int BPL, bool SMALL>
+hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                         hipStream_t stream, const FsstLaunch &how) {
+    return how.queue ? launch_fsst_q<BPL, SMALL, true>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                     : launch_fsst_q<BPL, SMALL, false>(d_chunks, nchunks, nvecs, d_err, stream, how);
 }
 
 // ============================================================================
