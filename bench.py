@@ -218,9 +218,12 @@ def main():
     import torch.distributed as dist
 
     dist_on = world > 1
+    # this rank's GPU: its local rank, unless the launcher already narrowed the
+    # visible devices to one per process
+    dev = local_rank if torch.cuda.device_count() > local_rank else 0
     if dist_on:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
 
     import pkgload
     fl = pkgload.load()
@@ -236,7 +239,7 @@ def main():
     t_gen = time.perf_counter() - t_gen
     log(f"[rank {rank}] encoded row groups [{rg0},{rg1}) of {nrg}: {img.len / 1e9:.2f} GB in {t_gen:.1f} s")
 
-    conn = fl.Connection([local_rank])
+    conn = fl.Connection([dev])
     t = conn.read_image(img)
     t_up = time.perf_counter()
     t.device_upload()
