@@ -673,6 +673,10 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     }
     s.cur = 0;
     s.held = -1;
+    if (s.rgs.empty()) {  // an empty table or range, or every row group pruned: no device work
+        s.active = true;
+        return 0;
+    }
     const auto &devs = t->conn->devices;
     const uint32_t G = (uint32_t)devs.size(), n = (uint32_t)s.rgs.size();
     if (s.devs.size() != G) {
@@ -894,6 +898,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
 }
 
 int scan_start(fls_table *t, ScanCtx &s) {
+    if (s.rgs.empty()) return 0;
     for (auto &d : s.devs)
         for (int si = 0; si < 2; ++si) {
             int rc = enqueue_batch(t, s, d, si);

@@ -203,3 +203,17 @@ def test_read_fastlanes_glob_scans_in_name_order(fl, ext, gpu, tmp_path):
         fl.write_image([("v", fl.INT32, a + i * 10000, fl.ENC_FFOR)]).write(str(tmp_path / f"part_{i}.fls"))
     _, _, rows = ext.query("read_fastlanes", str(tmp_path / "part_?.fls"), threads=4)
     assert [int(r[0]) for r in rows] == np.concatenate([a, a + 10000, a + 20000]).tolist()
+
+
+def test_read_fastlanes_empty_file(fl, ext, tmpfile):
+    """A file with a schema and zero row groups binds and scans to no rows
+    (the scan ends before any device work, so this needs no GPU)."""
+    img = fl.write_image([("a", fl.INT32, np.zeros(0, np.int32), fl.ENC_FFOR),
+                          ("s", fl.VARCHAR, [], fl.ENC_AUTO)])
+    p = tmpfile("empty.fls")
+    img.write(p)
+    names, types, rows = ext.query("read_fastlanes", p)
+    assert names == ["a", "s"] and types == ["INTEGER", "VARCHAR"] and rows == []
+    assert ext.scan_count("read_fastlanes", p)[0] == 0
+    _, _, rows = ext.query("read_fastlanes", p, p, as_list=True)
+    assert rows == []

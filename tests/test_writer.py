@@ -145,3 +145,39 @@ def test_custom_rowgroup_size(fl, ref, rgsz):
 def test_bad_rowgroup_size_rejected(fl, rgsz):
     with pytest.raises(fl.FlsError):
         fl.write_image([("a", fl.INT32, np.arange(10), fl.ENC_FFOR)], rowgroup=rgsz)
+
+
+def _empty_image(fl):
+    return fl.write_image([("a", fl.INT32, np.zeros(0, np.int32), fl.ENC_FFOR),
+                           ("s", fl.VARCHAR, [], fl.ENC_AUTO)])
+
+
+def test_empty_table_scans_nothing_without_a_gpu(fl, ref):
+    """A table with columns but no rows: schema, no row groups, and a scan
+    that ends at once (no device work, so this runs without a GPU)."""
+    img = _empty_image(fl)
+    rf = ref.RefFile(img)
+    assert rf.nrows == 0 and rf.nrowgroups == 0
+    t = fl.Connection().read_image(img)
+    assert (t.nrows, t.nrowgroups, t.ncols) == (0, 0, 2)
+    assert [c[0] for c in t.schema()] == ["a", "s"]
+    assert list(t.scan()) == []
+    # an empty row-group range of a non-empty table is empty too
+    t2 = fl.Connection().read_image(fl.write_image([("a", fl.INT32, np.arange(10, dtype=np.int32), fl.ENC_FFOR)]))
+    assert list(t2.scan(rg_begin=1, rg_end=1)) == []
+
+
+def test_filter_pruning_everything_scans_nothing(fl):
+    """Zone maps prune every row group: the scan ends without device work."""
+    img = fl.write_image([("k", fl.INT64, np.arange(200000, dtype=np.int64), fl.ENC_DELTA)])
+    t = fl.Connection().read_image(img)
+    assert list(t.scan_filtered([(0, ">", 10 ** 9)])) == []
+    assert t.pruned == t.nrowgroups
+
+
+@pytest.mark.gpu
+def test_gpu_empty_table_device_paths(fl, gpu):
+    t = fl.Connection().read_image(_empty_image(fl))
+    assert list(t.scan()) == []
+    with pytest.raises(fl.FlsError, match="out of bounds"):
+        t.device_upload()
