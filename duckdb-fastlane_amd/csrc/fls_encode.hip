@@ -6,26 +6,33 @@
 // FLS); the reference's writer is a stub, src/writer/write_fastlane_stream.cpp
 // :65-314).  The arithmetic is the decode kernel's run backwards:
 //   * one 256-thread block (4 waves) per column chunk (<= 64 vectors);
-//   * one pass per vector (one wave): the 1024 values (tail padded with the
-//     last value, as the CPU writer does) are staged in LDS; DELTA turns them
-//     into per-chain deltas in transposed position order (chain c = tuples
-//     blk*16T + l + 16k, FL_ORDER = {0,4,2,6,1,5,3,7}) and writes the chain
-//     bases; the wave reduces the signed minimum (FOR base) and the OR of
-//     value - base (bit width W), puts value - base in LDS in position order
-//     and every lane assembles 16-byte rows of the interleaved packing (word k
-//     of FastLanes lane L = bits [kT, kT + T) of lane L's stream of T values of
-//     W bits -- the inverse of fls_unpack.hpp) into the chunk's scratch area
-//     at the vector's widest position (v * 128 T);
+//   * the waves take the vectors in rounds of four, one vector per wave, one
+//     pass each: the 1024 values (tail padded with the last value, as the CPU
+//     writer does) are staged in LDS; DELTA turns them into per-chain deltas
+//     in transposed position order (chain c = tuples blk*16T + l + 16k,
+//     FL_ORDER = {0,4,2,6,1,5,3,7}) and writes the chain bases to scratch;
+//     the 16 position-ordered values of each lane are read once into
+//     registers, and the wave reduces their signed minimum (FOR base) and
+//     maximum together (W = bit width of max - min, which equals the width of
+//     OR(value - base) that the CPU writer computes); value - base goes back
+//     to LDS in position order;
+//   * one block barrier per round makes the round's widths visible; a vector's
+//     packed rows start where those of the vectors before it end, so every
+//     lane then assembles 16-byte rows of the interleaved packing (word k of
+//     FastLanes lane L = bits [kT, kT + T) of lane L's stream of T values of
+//     W bits -- the inverse of fls_unpack.hpp) straight at their place;
 //   * wave 0 scans the vectors' 128 W packed bytes into offsets and writes the
-//     chunk header and the VecMeta records;
-//   * the waves copy each vector's packed rows from scratch (just written,
-//     cache-resident) to their place in the chunk, then the DELTA bases and
-//     the zero padding.  A vector's place depends on the widths of the vectors
-//     before it, so without the scratch area the input would be read twice
-//     (v1 did: 3.16 ms for 1e9 INT64 keys, 2.78 TB/s of algorithmic traffic,
-//     16.8 GB actually read; profiles/r1/encode_bench_v1_twopass.txt).
-// Integer work, HBM-bound: per value it reads T/8 bytes and writes W/8 bytes
-// (plus W/8 through the cached scratch).  No MFMA.
+//     chunk header and the VecMeta records; the waves then move the DELTA
+//     bases after the packed area and write the zero padding.
+//   History (profiles/r1/encode_*): v1 read the input twice (analyse, then
+//   pack): 3.16 ms for 1e9 INT64 keys.  v2 packed into a scratch area at the
+//   vector's widest position and moved the rows once every width was known:
+//   2.09-2.23 ms.  Reading the values into registers once (one min/max
+//   reduction instead of a min pass and an OR pass over LDS) took INT64 DELTA
+//   2.11 -> 1.96 ms and INT32 FFOR 1.87 -> 1.78 ms (FLS_ENC_LDS_ANALYZE keeps
+//   the two-pass analysis for A/B; FLS_ENC_SCRATCH_PACK the scratch packing).
+// Integer work, HBM-bound: per value it reads T/8 bytes and writes W/8 bytes.
+// No MFMA.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,6 +80,15 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
     for (int d = 32; d >= 1; d >>= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, d, 64);
     return x;
 }
+// min and max together: two independent shuffle chains, one latency
+__device__ __forceinline__ void wave_minmax_i64(int64_t &mn, int64_t &mx) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int64_t a = (int64_t)__shfl_xor((unsigned long long)mn, d, 64);
+        const int64_t b = (int64_t)__shfl_xor((unsigned long long)mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+}
 
 // 1024 values of vector v of the chunk into V (u64, zero-extended T-bit),
 // the tail past vn padded with the last value
@@ -117,6 +133,29 @@ struct VecStat {
     uint32_t W;
 };
 
+#ifndef FLS_ENC_LDS_ANALYZE
+// FOR base and bit width of the vector's 16 position-ordered values per lane,
+// held in registers (read from LDS once): base = signed minimum; W = bit
+// width of max - min, which is the width of OR(x - min) that the CPU writer
+// computes (the highest set bit of an OR is that of its largest operand).
+template <int T>
+__device__ __forceinline__ VecStat analyze_regs(const uint64_t (&x)[16]) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+        const int64_t y = sext_d(x[k], T);
+        mn = y < mn ? y : mn;
+        mx = y > mx ? y : mx;
+    }
+    wave_minmax_i64(mn, mx);
+    const uint64_t range = ((uint64_t)mx - (uint64_t)mn) & tmask_d(T);
+    VecStat s;
+    s.base = mn;
+    s.W = range ? 64u - (uint32_t)__builtin_clzll(range) : 0u;
+    return s;
+}
+#else
+// A/B reference: two LDS passes (min, then OR of value - min)
 template <int T, bool DELTA>
 __device__ VecStat analyze(const FLS_LDS uint64_t *V, uint32_t lane) {
     int64_t mn = INT64_MAX;
@@ -135,6 +174,7 @@ __device__ VecStat analyze(const FLS_LDS uint64_t *V, uint32_t lane) {
     s.W = o ? 64u - (uint32_t)__builtin_clzll(o) : 0u;
     return s;
 }
+#endif
 
 // Interleaved packing of the position-ordered u = value - base staged in U:
 // 16-byte row chunk ci = (word row k = ci / 8, byte column 16 (ci % 8)) holds
@@ -179,49 +219,83 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
     const uint8_t *in = (const uint8_t *)c.in;
     FLS_GLOBAL uint8_t *out = (FLS_GLOBAL uint8_t *)c.out;
     FLS_GLOBAL uint8_t *scratch = (FLS_GLOBAL uint8_t *)c.scratch;
-    // ---- one pass per vector: base, width, DELTA bases, packing into scratch
-    // (bases go to scratch too, after the packed vectors: their place in the
-    // chunk also depends on every width)
+    // ---- one pass per vector: base, width, DELTA bases, packing.  The waves
+    // take the vectors in rounds of kEncWaves; a vector's packed rows start
+    // where the packed rows of the vectors before it end, so once a round's
+    // widths are in LDS (one block barrier) every wave packs straight to its
+    // vector's place in the chunk.  (FLS_ENC_SCRATCH_PACK: pack into scratch
+    // and move the rows once every width is known -- the A/B reference.)
+    // The DELTA bases go to scratch: their place follows the packed area.
+#ifndef FLS_ENC_SCRATCH_PACK
+    constexpr bool kDirect = true;
+#else
+    constexpr bool kDirect = false;
+#endif
+    const uint64_t meta_off = sizeof(ChunkHeader);
+    const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
     FLS_GLOBAL uint8_t *sbases = scratch + 128ull * T * kVectorsPerRowGroup;
-    for (uint32_t v = w; v < nvec; v += kEncWaves) {
-        const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
-        stage_values<T>(in, v, vn, V, lane);
-        wave_sync();
-        const VecStat s = analyze<T, DELTA>(V, lane);
-        if (lane == 0) {
-            Wv[v] = s.W;
-            Bv[v] = s.base;
-        }
-        if (DELTA) {
-            // chain c's base = its first tuple blk*16T + l (put_word layout, T/8 bytes)
-            if (lane < kVectorSize / T) {
-                const uint64_t b = V[(lane / 16) * 16 * T + (lane % 16)];
-                FLS_GLOBAL uint8_t *bp = sbases + 128ull * v + lane * (T / 8);
-                if (T == 64) *(FLS_GLOBAL uint64_t *)bp = b;
-                else if (T == 32) *(FLS_GLOBAL uint32_t *)bp = (uint32_t)b;
-                else if (T == 16) *(FLS_GLOBAL uint16_t *)bp = (uint16_t)b;
-                else *bp = (uint8_t)b;
-            }
-            if (T == 8 && lane < 64) {  // 128 chains of T = 8: lanes 0..63 take chains 64..127 too
-                const uint32_t c2 = lane + 64;
-                sbases[128ull * v + c2] = (uint8_t)V[(c2 / 16) * 16 * T + (c2 % 16)];
-            }
-        }
-        uint64_t u[16];
+    uint32_t done = 0;  // packed bytes of the earlier rounds' vectors
+    for (uint32_t r = 0; r < nvec; r += kEncWaves) {
+        const uint32_t v = r + w;
+        const bool act = v < nvec;  // wave-uniform
+        VecStat s{0, 0};
+        if (act) {
+            const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
+            stage_values<T>(in, v, vn, V, lane);
+            wave_sync();
+#ifndef FLS_ENC_LDS_ANALYZE
+            uint64_t x[16];
 #pragma unroll
-        for (uint32_t k = 0; k < 16; ++k)
-            u[k] = (pos_value<T, DELTA>(V, lane + 64 * k) - (uint64_t)s.base) & tmask_d(T);
-        wave_sync();
+            for (uint32_t k = 0; k < 16; ++k) x[k] = pos_value<T, DELTA>(V, lane + 64 * k);
+            s = analyze_regs<T>(x);
+#else
+            s = analyze<T, DELTA>(V, lane);
+#endif
+            if (lane == 0) {
+                Wv[v] = s.W;
+                Bv[v] = s.base;
+            }
+            if (DELTA) {
+                // chain c's base = its first tuple blk*16T + l (put_word layout, T/8 bytes)
+                if (lane < kVectorSize / T) {
+                    const uint64_t b = V[(lane / 16) * 16 * T + (lane % 16)];
+                    FLS_GLOBAL uint8_t *bp = sbases + 128ull * v + lane * (T / 8);
+                    if (T == 64) *(FLS_GLOBAL uint64_t *)bp = b;
+                    else if (T == 32) *(FLS_GLOBAL uint32_t *)bp = (uint32_t)b;
+                    else if (T == 16) *(FLS_GLOBAL uint16_t *)bp = (uint16_t)b;
+                    else *bp = (uint8_t)b;
+                }
+                if (T == 8 && lane < 64) {  // 128 chains of T = 8: lanes 0..63 take chains 64..127 too
+                    const uint32_t c2 = lane + 64;
+                    sbases[128ull * v + c2] = (uint8_t)V[(c2 / 16) * 16 * T + (c2 % 16)];
+                }
+            }
+            uint64_t u[16];
 #pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = u[k];
-        wave_sync();
-        pack_vector<T>(V, s.W, scratch + 128ull * T * v, lane);
+            for (uint32_t k = 0; k < 16; ++k)
+#ifndef FLS_ENC_LDS_ANALYZE
+                u[k] = (x[k] - (uint64_t)s.base) & tmask_d(T);
+#else
+                u[k] = (pos_value<T, DELTA>(V, lane + 64 * k) - (uint64_t)s.base) & tmask_d(T);
+#endif
+            wave_sync();
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = u[k];
+            wave_sync();
+        }
+        if (kDirect) __syncthreads();  // this round's widths are in Wv
+        if (act) {
+            uint32_t off = done;
+            if (kDirect)
+                for (uint32_t i = r; i < v; ++i) off += 128u * Wv[i];
+            pack_vector<T>(V, s.W, kDirect ? out + packed_off + off : scratch + 128ull * T * v, lane);
+        }
+        if (kDirect)
+            for (uint32_t i = r; i < min(r + (uint32_t)kEncWaves, nvec); ++i) done += 128u * Wv[i];
         wave_sync();
     }
     __syncthreads();
     // ---- chunk layout (assemble_chunk) --------------------------------------
-    const uint64_t meta_off = sizeof(ChunkHeader);
-    const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
     if (w == 0) {
         const uint32_t pw = lane < nvec ? 128u * Wv[lane] : 0u;
         uint32_t incl = pw;
@@ -276,11 +350,13 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
     }
     __syncthreads();
     const uint64_t packed_total = Ov[64], aux_off = Ov[65], total = Ov[66];
-    // ---- packed rows from scratch to their place; DELTA bases; padding -----
-    for (uint32_t v = w; v < nvec; v += kEncWaves) {
-        const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(scratch + 128ull * T * v);
-        FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + packed_off + Ov[v]);
-        for (uint32_t i = lane; i < 8 * Wv[v]; i += 64) dst[i] = src[i];
+    // ---- (scratch packing: packed rows to their place); DELTA bases; padding
+    if (!kDirect) {
+        for (uint32_t v = w; v < nvec; v += kEncWaves) {
+            const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(scratch + 128ull * T * v);
+            FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + packed_off + Ov[v]);
+            for (uint32_t i = lane; i < 8 * Wv[v]; i += 64) dst[i] = src[i];
+        }
     }
     if (DELTA) {
         const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(sbases);

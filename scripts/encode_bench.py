@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--scale", type=float, default=10.0)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--no-writer", action="store_true", help="device-resident cases only")
     a = ap.parse_args()
     import pkgload
     fl = pkgload.load()
@@ -110,7 +111,8 @@ def main():
         vals = gen()
         print(json.dumps(device_case(fl, name, ty, enc, vals, a.reps)), flush=True)
         del vals
-    print(json.dumps(writer_case(fl, a.scale, a.threads)), flush=True)
+    if not a.no_writer:
+        print(json.dumps(writer_case(fl, a.scale, a.threads)), flush=True)
 
 
 if __name__ == "__main__":
