@@ -119,6 +119,28 @@ __device__ __forceinline__ void stage_values(const uint8_t *in, uint32_t v, uint
     }
 }
 
+// Register prefetch of a full vector (T <= 32: T/8 16-byte loads per lane,
+// at most 16 VGPRs) and its staging, the full-vector case of stage_values
+template <int T>
+__device__ __forceinline__ void load_vec(const uint8_t *in, uint32_t v, uint32_t lane, v4u (&r)[T / 8]) {
+    const FLS_GLOBAL v4u *s16 = (const FLS_GLOBAL v4u *)(in + (size_t)v * kVectorSize * (T / 8));
+#pragma unroll
+    for (uint32_t i = 0; i < T / 8; ++i) r[i] = s16[lane + 64 * i];
+}
+template <int T>
+__device__ __forceinline__ void stage_regs(const v4u (&r)[T / 8], FLS_LDS uint64_t *V, uint32_t lane) {
+    constexpr uint32_t per = 16 / (T / 8);
+#pragma unroll
+    for (uint32_t i = 0; i < T / 8; ++i) {
+        const uint32_t q = lane + 64 * i;
+        const uint32_t w[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
+#pragma unroll
+        for (uint32_t j = 0; j < per; ++j)
+            V[q * per + j] = T == 64 ? ((uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32))
+                                     : (w[(j * T) / 32] >> ((j * T) % 32)) & (uint32_t)tmask_d(T);
+    }
+}
+
 // position-ordered value p of the vector staged in V: FFOR the value itself,
 // DELTA the delta of tuple tau(p) on its chain (0 at a chain start)
 template <int T, bool DELTA>
@@ -235,13 +257,28 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
     const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
     FLS_GLOBAL uint8_t *sbases = scratch + 128ull * T * kVectorsPerRowGroup;
     uint32_t done = 0;  // packed bytes of the earlier rounds' vectors
+    // T <= 32: the wave's next full vector (v + kEncWaves) is loaded into
+    // registers while this one is analysed and packed (INT32 FFOR 1.70 ->
+    // see DESIGN.md section 10; T = 64 would hold 32 more VGPRs and measured slower)
+#ifndef FLS_ENC_PF_MAX_T
+#define FLS_ENC_PF_MAX_T 32
+#endif
+    constexpr bool kPf = T <= FLS_ENC_PF_MAX_T;
+    constexpr int TP = kPf ? T : 8;  // prefetch instantiation (unused when !kPf)
+    constexpr uint32_t kPfN = TP / 8;
+    v4u pf[kPfN];
+    auto full = [&](uint32_t x) { return (x + 1) * kVectorSize <= n; };
+    if (kPf && w < nvec && full(w)) load_vec<TP>(in, w, lane, pf);
     for (uint32_t r = 0; r < nvec; r += kEncWaves) {
         const uint32_t v = r + w;
         const bool act = v < nvec;  // wave-uniform
         VecStat s{0, 0};
         if (act) {
             const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
-            stage_values<T>(in, v, vn, V, lane);
+            if (kPf && vn == kVectorSize) stage_regs<TP>(pf, V, lane);
+            else stage_values<T>(in, v, vn, V, lane);
+            if (kPf && v + kEncWaves < nvec && full(v + kEncWaves))
+                load_vec<TP>(in, v + kEncWaves, lane, pf);
             wave_sync();
 #ifndef FLS_ENC_LDS_ANALYZE
             uint64_t x[16];

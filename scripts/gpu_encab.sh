@@ -8,6 +8,10 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_encode.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pt_encab_$TAG.log 2>&1
 rc=$?; echo "encode parity: $(tail -1 gpurun_out/pt_encab_$TAG.log)"; [ $rc -eq 0 ] || exit $rc
+for v in "$@"; do
+  FLS_LIB=libflsgpu_$v.so timeout -k 10 300 python -u -m pytest tests/test_encode.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pt_encab_${TAG}_$v.log 2>&1
+  rc=$?; echo "encode parity $v: $(tail -1 gpurun_out/pt_encab_${TAG}_$v.log)"; [ $rc -eq 0 ] || exit $rc
+done
 for round in 1 2; do
   for v in base "$@"; do
     lib=libflsgpu.so; [ $v = base ] || lib=libflsgpu_$v.so
