@@ -29,8 +29,9 @@
 //   vector's widest position and moved the rows once every width was known:
 //   2.09-2.23 ms.  Reading the values into registers once (one min/max
 //   reduction instead of a min pass and an OR pass over LDS) took INT64 DELTA
-//   2.11 -> 1.96 ms and INT32 FFOR 1.87 -> 1.78 ms (FLS_ENC_LDS_ANALYZE keeps
-//   the two-pass analysis for A/B; FLS_ENC_SCRATCH_PACK the scratch packing).
+//   2.11 -> 1.96 ms and INT32 FFOR 1.87 -> 1.78 ms; packing straight to the
+//   final place, INT64 FFOR 2.29 -> 1.78 ms; the T <= 32 register prefetch,
+//   INT32 FFOR 1.71 -> 1.39 ms.
 // Integer work, HBM-bound: per value it reads T/8 bytes and writes W/8 bytes.
 // No MFMA.
 #include <hip/hip_runtime.h>
@@ -68,18 +69,6 @@ __device__ __forceinline__ uint32_t tau_d(uint32_t p) {
     return (rb << 7) | (((p >> 7) & 7) << 4) | (p & 15);
 }
 __device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
-// wave reductions (64-bit) through LDS-free cross-lane shuffles
-__device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
-    for (int d = 32; d >= 1; d >>= 1) {
-        const int64_t y = (int64_t)__shfl_xor((unsigned long long)x, d, 64);
-        x = y < x ? y : x;
-    }
-    return x;
-}
-__device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
-    for (int d = 32; d >= 1; d >>= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, d, 64);
-    return x;
-}
 // min and max together: two independent shuffle chains, one latency
 __device__ __forceinline__ void wave_minmax_i64(int64_t &mn, int64_t &mx) {
     for (int d = 32; d >= 1; d >>= 1) {
@@ -90,10 +79,15 @@ __device__ __forceinline__ void wave_minmax_i64(int64_t &mn, int64_t &mx) {
     }
 }
 
-// 1024 values of vector v of the chunk into V (u64, zero-extended T-bit),
-// the tail past vn padded with the last value
+// LDS / register storage of a T-bit value: u32 for T <= 32 (half the LDS
+// and VGPRs of u64), u64 for T = 64
 template <int T>
-__device__ __forceinline__ void stage_values(const uint8_t *in, uint32_t v, uint32_t vn, FLS_LDS uint64_t *V,
+using Sto = typename std::conditional<T == 64, uint64_t, uint32_t>::type;
+
+// 1024 values of vector v of the chunk into V (zero-extended T-bit), the
+// tail past vn padded with the last value
+template <int T, typename S>
+__device__ __forceinline__ void stage_values(const uint8_t *in, uint32_t v, uint32_t vn, FLS_LDS S *V,
                                              uint32_t lane) {
     using U = typename std::conditional<T == 8, uint8_t,
               typename std::conditional<T == 16, uint16_t,
@@ -111,11 +105,11 @@ __device__ __forceinline__ void stage_values(const uint8_t *in, uint32_t v, uint
                 uint64_t val;
                 if (T == 64) val = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
                 else val = (w[(i * T) / 32] >> ((i * T) % 32)) & (uint32_t)tmask_d(T);
-                V[q * per + i] = val;
+                V[q * per + i] = (S)val;
             }
         }
     } else {
-        for (uint32_t j = lane; j < kVectorSize; j += 64) V[j] = (uint64_t)src[j < vn ? j : vn - 1];
+        for (uint32_t j = lane; j < kVectorSize; j += 64) V[j] = (S)src[j < vn ? j : vn - 1];
     }
 }
 
@@ -127,8 +121,8 @@ __device__ __forceinline__ void load_vec(const uint8_t *in, uint32_t v, uint32_t
 #pragma unroll
     for (uint32_t i = 0; i < T / 8; ++i) r[i] = s16[lane + 64 * i];
 }
-template <int T>
-__device__ __forceinline__ void stage_regs(const v4u (&r)[T / 8], FLS_LDS uint64_t *V, uint32_t lane) {
+template <int T, typename S>
+__device__ __forceinline__ void stage_regs(const v4u (&r)[T / 8], FLS_LDS S *V, uint32_t lane) {
     constexpr uint32_t per = 16 / (T / 8);
 #pragma unroll
     for (uint32_t i = 0; i < T / 8; ++i) {
@@ -136,18 +130,18 @@ __device__ __forceinline__ void stage_regs(const v4u (&r)[T / 8], FLS_LDS uint64
         const uint32_t w[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
 #pragma unroll
         for (uint32_t j = 0; j < per; ++j)
-            V[q * per + j] = T == 64 ? ((uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32))
-                                     : (w[(j * T) / 32] >> ((j * T) % 32)) & (uint32_t)tmask_d(T);
+            V[q * per + j] = (S)(T == 64 ? ((uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32))
+                                         : (w[(j * T) / 32] >> ((j * T) % 32)) & (uint32_t)tmask_d(T));
     }
 }
 
 // position-ordered value p of the vector staged in V: FFOR the value itself,
 // DELTA the delta of tuple tau(p) on its chain (0 at a chain start)
-template <int T, bool DELTA>
-__device__ __forceinline__ uint64_t pos_value(const FLS_LDS uint64_t *V, uint32_t p) {
+template <int T, bool DELTA, typename S>
+__device__ __forceinline__ S pos_value(const FLS_LDS S *V, uint32_t p) {
     if (!DELTA) return V[p];
     const uint32_t i = tau_d(p);
-    return ((i >> 4) % T == 0) ? 0ull : (V[i] - V[i - 16]) & tmask_d(T);
+    return ((i >> 4) % T == 0) ? (S)0 : (S)((V[i] - V[i - 16]) & (S)tmask_d(T));
 }
 
 struct VecStat {
@@ -155,7 +149,6 @@ struct VecStat {
     uint32_t W;
 };
 
-#ifndef FLS_ENC_LDS_ANALYZE
 // FOR base and bit width of the vector's 16 position-ordered values per lane,
 // held in registers (read from LDS once): base = signed minimum; W = bit
 // width of max - min, which is the width of OR(x - min) that the CPU writer
@@ -176,35 +169,37 @@ __device__ __forceinline__ VecStat analyze_regs(const uint64_t (&x)[16]) {
     s.W = range ? 64u - (uint32_t)__builtin_clzll(range) : 0u;
     return s;
 }
-#else
-// A/B reference: two LDS passes (min, then OR of value - min)
-template <int T, bool DELTA>
-__device__ VecStat analyze(const FLS_LDS uint64_t *V, uint32_t lane) {
-    int64_t mn = INT64_MAX;
-#pragma unroll 4
+// T <= 32: the same in 32-bit registers and shuffles
+template <int T>
+__device__ __forceinline__ VecStat analyze_regs(const uint32_t (&x)[16]) {
+    int32_t mn = INT32_MAX, mx = INT32_MIN;
+#pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
-        const int64_t x = sext_d(pos_value<T, DELTA>(V, lane + 64 * k), T);
-        mn = x < mn ? x : mn;
+        const uint32_t sign = 1u << (T - 1);
+        const int32_t y = T == 32 ? (int32_t)x[k] : (int32_t)(((x[k] & (uint32_t)tmask_d(T)) ^ sign) - sign);
+        mn = y < mn ? y : mn;
+        mx = y > mx ? y : mx;
     }
-    mn = wave_min_i64(mn);
-    uint64_t o = 0;
-#pragma unroll 4
-    for (uint32_t k = 0; k < 16; ++k) o |= (pos_value<T, DELTA>(V, lane + 64 * k) - (uint64_t)mn) & tmask_d(T);
-    o = wave_or_u64(o);
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int32_t a = __shfl_xor(mn, d, 64);
+        const int32_t b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    const uint32_t range = ((uint32_t)mx - (uint32_t)mn) & (uint32_t)tmask_d(T);
     VecStat s;
     s.base = mn;
-    s.W = o ? 64u - (uint32_t)__builtin_clzll(o) : 0u;
+    s.W = range ? 32u - (uint32_t)__builtin_clz(range) : 0u;
     return s;
 }
-#endif
 
 // Interleaved packing of the position-ordered u = value - base staged in U:
 // 16-byte row chunk ci = (word row k = ci / 8, byte column 16 (ci % 8)) holds
 // word k of FastLanes lanes L = (ci % 8) * 128/T + j, j < 128/T; word k of lane
 // L = OR over rows r of u[r * 1024/T + L] << (r W - k T) (bits [kT, kT + T) of
 // the lane's stream).
-template <int T>
-__device__ void pack_vector(const FLS_LDS uint64_t *U, uint32_t W, FLS_GLOBAL uint8_t *dst, uint32_t lane) {
+template <int T, typename S>
+__device__ void pack_vector(const FLS_LDS S *U, uint32_t W, FLS_GLOBAL uint8_t *dst, uint32_t lane) {
     constexpr uint32_t nl = kVectorSize / T, wpc = 128 / T;  // lanes, words per 16 B
     const uint64_t tm = tmask_d(T);
     for (uint32_t ci = lane; ci < 8 * W; ci += 64) {
@@ -233,10 +228,11 @@ __device__ void pack_vector(const FLS_LDS uint64_t *U, uint32_t W, FLS_GLOBAL ui
 }
 
 template <int T, bool DELTA>
-__device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS uint32_t *Wv,
+__device__ void encode_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS uint32_t *Wv,
                              FLS_LDS int64_t *Bv, FLS_LDS uint64_t *Ov) {
+    using S = Sto<T>;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    FLS_LDS uint64_t *V = Vall + w * kVectorSize;
+    FLS_LDS S *V = Vall + w * kVectorSize;
     const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
     const uint8_t *in = (const uint8_t *)c.in;
     FLS_GLOBAL uint8_t *out = (FLS_GLOBAL uint8_t *)c.out;
@@ -245,17 +241,11 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
     // take the vectors in rounds of kEncWaves; a vector's packed rows start
     // where the packed rows of the vectors before it end, so once a round's
     // widths are in LDS (one block barrier) every wave packs straight to its
-    // vector's place in the chunk.  (FLS_ENC_SCRATCH_PACK: pack into scratch
-    // and move the rows once every width is known -- the A/B reference.)
-    // The DELTA bases go to scratch: their place follows the packed area.
-#ifndef FLS_ENC_SCRATCH_PACK
-    constexpr bool kDirect = true;
-#else
-    constexpr bool kDirect = false;
-#endif
+    // vector's place in the chunk.  The DELTA bases go to scratch: their place
+    // follows the packed area.
     const uint64_t meta_off = sizeof(ChunkHeader);
     const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
-    FLS_GLOBAL uint8_t *sbases = scratch + 128ull * T * kVectorsPerRowGroup;
+    FLS_GLOBAL uint8_t *sbases = scratch;
     uint32_t done = 0;  // packed bytes of the earlier rounds' vectors
     // T <= 32: the wave's next full vector (v + kEncWaves) is loaded into
     // registers while this one is analysed and packed (INT32 FFOR 1.70 ->
@@ -280,14 +270,10 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
             if (kPf && v + kEncWaves < nvec && full(v + kEncWaves))
                 load_vec<TP>(in, v + kEncWaves, lane, pf);
             wave_sync();
-#ifndef FLS_ENC_LDS_ANALYZE
-            uint64_t x[16];
+            S x[16];
 #pragma unroll
             for (uint32_t k = 0; k < 16; ++k) x[k] = pos_value<T, DELTA>(V, lane + 64 * k);
             s = analyze_regs<T>(x);
-#else
-            s = analyze<T, DELTA>(V, lane);
-#endif
             if (lane == 0) {
                 Wv[v] = s.W;
                 Bv[v] = s.base;
@@ -307,28 +293,21 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
                     sbases[128ull * v + c2] = (uint8_t)V[(c2 / 16) * 16 * T + (c2 % 16)];
                 }
             }
-            uint64_t u[16];
+            S u[16];
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k)
-#ifndef FLS_ENC_LDS_ANALYZE
-                u[k] = (x[k] - (uint64_t)s.base) & tmask_d(T);
-#else
-                u[k] = (pos_value<T, DELTA>(V, lane + 64 * k) - (uint64_t)s.base) & tmask_d(T);
-#endif
+            for (uint32_t k = 0; k < 16; ++k) u[k] = (S)((x[k] - (S)s.base) & (S)tmask_d(T));
             wave_sync();
 #pragma unroll
             for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = u[k];
             wave_sync();
         }
-        if (kDirect) __syncthreads();  // this round's widths are in Wv
+        __syncthreads();  // this round's widths are in Wv
         if (act) {
             uint32_t off = done;
-            if (kDirect)
-                for (uint32_t i = r; i < v; ++i) off += 128u * Wv[i];
-            pack_vector<T>(V, s.W, kDirect ? out + packed_off + off : scratch + 128ull * T * v, lane);
+            for (uint32_t i = r; i < v; ++i) off += 128u * Wv[i];
+            pack_vector<T>(V, s.W, out + packed_off + off, lane);
         }
-        if (kDirect)
-            for (uint32_t i = r; i < min(r + (uint32_t)kEncWaves, nvec); ++i) done += 128u * Wv[i];
+        for (uint32_t i = r; i < min(r + (uint32_t)kEncWaves, nvec); ++i) done += 128u * Wv[i];
         wave_sync();
     }
     __syncthreads();
@@ -387,14 +366,7 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
     }
     __syncthreads();
     const uint64_t packed_total = Ov[64], aux_off = Ov[65], total = Ov[66];
-    // ---- (scratch packing: packed rows to their place); DELTA bases; padding
-    if (!kDirect) {
-        for (uint32_t v = w; v < nvec; v += kEncWaves) {
-            const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(scratch + 128ull * T * v);
-            FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + packed_off + Ov[v]);
-            for (uint32_t i = lane; i < 8 * Wv[v]; i += 64) dst[i] = src[i];
-        }
-    }
+    // ---- DELTA bases after the packed area; padding
     if (DELTA) {
         const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(sbases);
         FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + aux_off);
@@ -409,22 +381,35 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS uint64_t *Vall, FLS_LDS 
     }
 }
 
-__global__ __launch_bounds__(256) void encode_kernel(const EncChunk *__restrict__ chunks, uint32_t nchunks) {
-    __shared__ uint64_t Vall[kEncWaves * kVectorSize];
+// One kernel per storage width: S = uint64_t for T = 64 chunks, uint32_t for
+// T <= 32 (half the LDS and VGPRs: more waves per SIMD for the narrow types).
+// The narrow kernel runs at 5 waves per SIMD (93 VGPRs, no spills): INT32
+// FFOR 1.38 ms with u64 storage -> 1.08 ms (u32, 4 waves) -> 1.03 ms.  Forcing
+// 6 waves (80 VGPRs, 6 spilled to scratch) gave byte mismatches in mixed
+// launches, intermittently, so it is not used.
+#ifndef FLS_ENC_NARROW_WAVES
+#define FLS_ENC_NARROW_WAVES 5
+#endif
+template <typename S>
+__global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) void encode_kernel(const EncChunk *__restrict__ chunks, uint32_t nchunks) {
+    __shared__ S Vall[kEncWaves * kVectorSize];
     __shared__ uint32_t Wv[64];
     __shared__ int64_t Bv[64];
     __shared__ uint64_t Ov[67];
     const EncChunk c = chunks[blockIdx.x];
-    FLS_LDS uint64_t *V = (FLS_LDS uint64_t *)Vall;
+    FLS_LDS S *V = (FLS_LDS S *)Vall;
     FLS_LDS uint32_t *W = (FLS_LDS uint32_t *)Wv;
     FLS_LDS int64_t *B = (FLS_LDS int64_t *)Bv;
     FLS_LDS uint64_t *O = (FLS_LDS uint64_t *)Ov;
     const bool delta = c.enc == ENC_DELTA;
-    switch (c.T) {
-    case 8: delta ? encode_chunk<8, true>(c, V, W, B, O) : encode_chunk<8, false>(c, V, W, B, O); break;
-    case 16: delta ? encode_chunk<16, true>(c, V, W, B, O) : encode_chunk<16, false>(c, V, W, B, O); break;
-    case 32: delta ? encode_chunk<32, true>(c, V, W, B, O) : encode_chunk<32, false>(c, V, W, B, O); break;
-    default: delta ? encode_chunk<64, true>(c, V, W, B, O) : encode_chunk<64, false>(c, V, W, B, O); break;
+    if constexpr (sizeof(S) == 8) {
+        delta ? encode_chunk<64, true>(c, V, W, B, O) : encode_chunk<64, false>(c, V, W, B, O);
+    } else {
+        switch (c.T) {
+        case 8: delta ? encode_chunk<8, true>(c, V, W, B, O) : encode_chunk<8, false>(c, V, W, B, O); break;
+        case 16: delta ? encode_chunk<16, true>(c, V, W, B, O) : encode_chunk<16, false>(c, V, W, B, O); break;
+        default: delta ? encode_chunk<32, true>(c, V, W, B, O) : encode_chunk<32, false>(c, V, W, B, O); break;
+        }
     }
 }
 
@@ -437,10 +422,17 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
     return (packed_off + 128ull * T * nvec + aux + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
 }
 
-hipError_t launch_encode(const EncChunk *d_chunks, uint32_t nchunks, hipStream_t stream) {
-    if (nchunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(encode_kernel, dim3(nchunks), dim3(64 * kEncWaves), 0, stream, d_chunks, nchunks);
+hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream) {
+    if (n_wide) hipLaunchKernelGGL(encode_kernel<uint64_t>, dim3(n_wide), dim3(64 * kEncWaves), 0, stream, d_chunks, n_wide);
+    if (n_narrow)
+        hipLaunchKernelGGL(encode_kernel<uint32_t>, dim3(n_narrow), dim3(64 * kEncWaves), 0, stream, d_chunks + n_wide,
+                           n_narrow);
     return hipGetLastError();
+}
+
+uint32_t order_for_launch(std::vector<EncChunk> &desc) {
+    const auto mid = std::stable_partition(desc.begin(), desc.end(), [](const EncChunk &c) { return c.T == 64; });
+    return (uint32_t)(mid - desc.begin());
 }
 
 }  // namespace fls
@@ -481,7 +473,7 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
     static std::vector<std::pair<uint8_t *, uint64_t>> cache;
     std::lock_guard<std::mutex> lock(mu);
     if ((size_t)device >= cache.size()) cache.resize(device + 1, {nullptr, 0});
-    const uint64_t need = nrg * enc_scratch_bytes((uint32_t)T);
+    const uint64_t need = nrg * enc_scratch_bytes();
     if (cache[device].second < need) {
         hipFree(cache[device].first);
         cache[device] = {nullptr, 0};
@@ -503,7 +495,7 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
         c.in = (uint64_t)(uintptr_t)d_values + i * rowgroup_rows * (uint64_t)(T / 8);
         c.out = (uint64_t)(uintptr_t)d_out + i * slot;
         c.len_out = (uint64_t)(uintptr_t)(d_lens + i);
-        c.scratch = (uint64_t)(uintptr_t)(scratch + i * enc_scratch_bytes((uint32_t)T));
+        c.scratch = (uint64_t)(uintptr_t)(scratch + i * enc_scratch_bytes());
         c.nrows = (uint32_t)std::min<uint64_t>(rowgroup_rows, nrows - i * rowgroup_rows);
         c.T = (uint8_t)T;
         c.enc = encoding;
@@ -515,7 +507,7 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
     if (e == hipSuccess) e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
     if (e == hipSuccess) e = hipEventRecord(e0, nullptr);
-    if (e == hipSuccess) e = launch_encode(d_desc, (uint32_t)nrg, nullptr);
+    if (e == hipSuccess) e = launch_encode(d_desc, T == 64 ? (uint32_t)nrg : 0u, T == 64 ? 0u : (uint32_t)nrg, nullptr);
     if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0;

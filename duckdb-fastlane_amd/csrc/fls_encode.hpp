@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace fls {
 
@@ -11,7 +12,7 @@ struct EncChunk {
     uint64_t in;       // device address of the chunk's first value (T/8 bytes each)
     uint64_t out;      // device address of the chunk's output slot (enc_slot_bytes)
     uint64_t len_out;  // device address of a uint64: the chunk's byte length (written)
-    uint64_t scratch;  // device address of enc_scratch_bytes(T) bytes for the packed vectors
+    uint64_t scratch;  // device address of enc_scratch_bytes() bytes (the DELTA chain bases)
     uint32_t nrows;    // rows of the chunk (1..65536)
     uint8_t T, enc;    // packing width 8/16/32/64; ENC_FFOR or ENC_DELTA
     uint8_t pad[2];
@@ -19,13 +20,19 @@ struct EncChunk {
 };
 static_assert(sizeof(EncChunk) == 48, "EncChunk is 48 B");
 
-// Scratch bytes per chunk: every vector packed at its widest (64 x 128 T),
-// then 64 x 128 B of DELTA chain bases.
-inline uint64_t enc_scratch_bytes(uint32_t T) { return 64ull * 128ull * T + 64ull * 128ull; }
+// Scratch bytes per chunk: 64 x 128 B of DELTA chain bases (their place in
+// the chunk follows the packed area, known only once every width is).
+inline uint64_t enc_scratch_bytes() { return 64ull * 128ull; }
 
 // Bytes an output slot needs for a chunk of nrows values (the chunk at W = T).
 uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // Encode nchunks chunks (d_chunks in device memory), one block each.
-hipError_t launch_encode(const EncChunk *d_chunks, uint32_t nchunks, hipStream_t stream);
+// Launch over chunks [0, n_wide) of T = 64 and then [n_wide, n_wide + n_narrow)
+// of T <= 32 (one kernel each: u64 or u32 registers and LDS).
+hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream);
+// Order a launch's descriptors for launch_encode (T = 64 first, stable);
+// returns n_wide.  Each descriptor carries its own output and length
+// addresses, so the order is free.
+uint32_t order_for_launch(std::vector<EncChunk> &desc);
 
 }  // namespace fls

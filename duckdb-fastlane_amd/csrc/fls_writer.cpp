@@ -1139,7 +1139,7 @@ struct GpuEncoder {
                 WHIP(hipMalloc((void **)&d_desc, nj * sizeof(EncChunk)));
                 WHIP(hipMalloc((void **)&d_lens, nj * sizeof(uint64_t)));
                 WHIP(hipHostMalloc((void **)&h_lens, nj * sizeof(uint64_t), 0));
-                WHIP(hipMalloc((void **)&d_scratch, nj * enc_scratch_bytes(64)));
+                WHIP(hipMalloc((void **)&d_scratch, nj * enc_scratch_bytes()));
                 job_cap = nj;
             }
         }
@@ -1178,16 +1178,17 @@ struct GpuEncoder {
             c.in = (uint64_t)(uintptr_t)(d_in + jb.in_off);
             c.out = (uint64_t)(uintptr_t)(d_out + jb.out_off);
             c.len_out = (uint64_t)(uintptr_t)(d_lens + i);
-            c.scratch = (uint64_t)(uintptr_t)(d_scratch + i * enc_scratch_bytes(64));
+            c.scratch = (uint64_t)(uintptr_t)(d_scratch + i * enc_scratch_bytes());
             c.nrows = jb.nrows;
             c.T = jb.T;
             c.enc = jb.enc;
             c.pad[0] = c.pad[1] = 0;
             c.pad2 = 0;
         }
+        const uint32_t n_wide = order_for_launch(desc);
         WHIP(hipMemcpyAsync(d_in, h_stage, in_used, hipMemcpyHostToDevice, stream));
         WHIP(hipMemcpyAsync(d_desc, desc.data(), jobs.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
-        WHIP(launch_encode(d_desc, (uint32_t)jobs.size(), stream));
+        WHIP(launch_encode(d_desc, n_wide, (uint32_t)jobs.size() - n_wide, stream));
         WHIP(hipMemcpyAsync(h_lens, d_lens, jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         // the slots come back in one pinned copy (slots are sized for W = T,
         // so this moves more than the chunks hold, but one large copy beats
