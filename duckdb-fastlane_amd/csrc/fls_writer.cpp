@@ -8,6 +8,9 @@
 // and the producer of every benchmark / test input (fls_gen.hpp).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -1042,6 +1045,25 @@ int default_writer_threads() {
 // back, then one D2H copy per chunk into its row group.  (Per-row-group
 // launches of ~11 blocks left the GPU idle: 46 M rows/s against 65 M on 16
 // CPU threads for lineitem SF10.)  Buffers are kept across batches.
+// FLS_WRITER_PROFILE=1: wall time of the writer's phases, summed over the
+// writer's calls and printed to stderr when the image is finished
+struct WriterProfile {
+    bool on = getenv("FLS_WRITER_PROFILE") != nullptr;
+    double cpu = 0, submit = 0, gpu_wait = 0, copy_out = 0, finish = 0;
+    uint64_t flushes = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void print() const {
+        if (on)
+            fprintf(stderr,
+                    "fls_writer profile: CPU columns, GPU staging and zone maps %.3f s, submit %.3f s, gpu wait %.3f s, "
+                    "copy out %.3f s (%llu flushes), finish %.3f s\n",
+                    cpu, submit, gpu_wait, copy_out, (unsigned long long)flushes, finish);
+    }
+};
+static WriterProfile g_prof;
+
 struct GpuEncoder {
     static constexpr uint32_t kBatch = 32;  // row groups per launch
     int dev = -1;
@@ -1090,9 +1112,11 @@ struct GpuEncoder {
         if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-    // Stage columns cols of row group rg (nrows rows) into the batch.
+    // Reserve the batch's room for columns cols of row group rg (nrows rows);
+    // stage[c] = where column c's values go in the pinned staging buffer (the
+    // caller copies them there, together with the column's zone map pass).
     int add(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, size_t rg, uint32_t nrows,
-            const void *const *data, int nthreads, std::vector<FileBuilder::RG> &rgs) {
+            int nthreads, std::vector<FileBuilder::RG> &rgs, std::vector<uint8_t *> &stage) {
         WHIP(hipSetDevice(dev));
         if (!stream) WHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         // capacity for a full batch of row groups like this one (the first
@@ -1105,7 +1129,7 @@ struct GpuEncoder {
         }
         if (in_used + in_rg > in_cap || out_used + out_rg > out_cap || jobs.size() + cols.size() > job_cap) {
             if (!jobs.empty()) {
-                const int rc = flush(rgs);
+                const int rc = flush(rgs, nthreads);
                 if (rc) return rc;
             }
             if (kBatch * in_rg > in_cap) {
@@ -1143,33 +1167,22 @@ struct GpuEncoder {
                 job_cap = nj;
             }
         }
-        const size_t j0 = jobs.size();
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
             jobs.push_back(Job{rg, c, in_used, out_used, nrows, (uint8_t)T, specs[c].enc});
+            stage[c] = h_stage + in_used;
             in_used += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
             out_used += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
         }
-        // stage the columns, column-parallel (one memcpy thread caps at a few GB/s)
-        std::atomic<size_t> next{0};
-        auto work = [&]() {
-            for (size_t i; (i = next.fetch_add(1)) < cols.size();) {
-                const Job &jb = jobs[j0 + i];
-                memcpy(h_stage + jb.in_off, data[jb.col], (size_t)nrows * (jb.T / 8));
-            }
-        };
-        std::vector<std::thread> th;
-        const size_t nth = std::min<size_t>(cols.size(), (size_t)std::max(1, nthreads));
-        for (size_t t = 1; t < nth; ++t) th.emplace_back(work);
-        work();
-        for (auto &t : th) t.join();
         ++batched;  // the caller flushes a full batch once this row group is in rgs
         return 0;
     }
 
-    // Encode the batch and move its chunks into their row groups.
-    int flush(std::vector<FileBuilder::RG> &rgs) {
+    // Encode the batch and move its chunks into their row groups (on up to
+    // nthreads threads).
+    int flush(std::vector<FileBuilder::RG> &rgs, int nthreads) {
         if (jobs.empty()) return 0;
+        const double t0 = g_prof.on ? WriterProfile::now() : 0;
         WHIP(hipSetDevice(dev));
         std::vector<EncChunk> desc(jobs.size());
         for (size_t i = 0; i < jobs.size(); ++i) {
@@ -1194,10 +1207,27 @@ struct GpuEncoder {
         // so this moves more than the chunks hold, but one large copy beats
         // a small pageable copy per chunk), then each chunk's bytes move out
         WHIP(hipMemcpyAsync(h_out, d_out, out_used, hipMemcpyDeviceToHost, stream));
+        const double t1 = g_prof.on ? WriterProfile::now() : 0;
         WHIP(hipStreamSynchronize(stream));
-        for (size_t i = 0; i < jobs.size(); ++i) {
-            std::vector<uint8_t> &dst = rgs[jobs[i].rg].chunks[jobs[i].col];
-            dst.assign(h_out + jobs[i].out_off, h_out + jobs[i].out_off + h_lens[i]);
+        const double t2 = g_prof.on ? WriterProfile::now() : 0;
+        std::atomic<size_t> next{0};
+        auto move_out = [&]() {
+            for (size_t i; (i = next.fetch_add(1)) < jobs.size();) {
+                std::vector<uint8_t> &dst = rgs[jobs[i].rg].chunks[jobs[i].col];
+                dst.assign(h_out + jobs[i].out_off, h_out + jobs[i].out_off + h_lens[i]);
+            }
+        };
+        std::vector<std::thread> th;
+        const size_t nth = std::min<size_t>(jobs.size(), (size_t)std::max(1, nthreads));
+        for (size_t t = 1; t < nth; ++t) th.emplace_back(move_out);
+        move_out();
+        for (auto &t : th) t.join();
+        if (g_prof.on) {
+            const double t3 = WriterProfile::now();
+            g_prof.submit += t1 - t0;
+            g_prof.gpu_wait += t2 - t1;
+            g_prof.copy_out += t3 - t2;
+            ++g_prof.flushes;
         }
         jobs.clear();
         in_used = out_used = 0;
@@ -1267,6 +1297,7 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
     rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
     // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA
     std::vector<uint8_t> on_gpu(ncols, 0);
+    std::vector<uint8_t *> stage(ncols, nullptr);
     if (w->gpu.dev >= 0) {
         std::vector<size_t> gcols;
         for (size_t c = 0; c < ncols; ++c) {
@@ -1277,21 +1308,24 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
             }
         }
         if (!gcols.empty()) {
-            // staged now (the caller's buffers are only valid during this
-            // call), encoded with the batch (GpuEncoder::flush)
-            const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size(), nrows, data, w->threads, w->fb.rgs);
+            // room in the batch now; the values are staged below, with the
+            // zone maps (the caller's buffers are only valid during this
+            // call), and encoded with the batch (GpuEncoder::flush)
+            const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size(), nrows, w->threads, w->fb.rgs, stage);
             if (rc) return rc;
         }
     }
     // columns are independent: encode them on up to w->threads threads
+    const double tc = g_prof.on ? WriterProfile::now() : 0;
     auto encode_col = [&](size_t c) {
         const ColSpec &cs = w->fb.cols[c];
         if (cs.type == TY_VARCHAR) {
             rg.chunks[c] = encode_str_chunk(cs.enc, str_offsets[c], (const char *)data[c], nrows);
             return;
         }
-        if (on_gpu[c]) {  // encoded by the GPU batch: only the zone map here
-            rg.zones[c] = zone_of_typed(cs.type, data[c], nrows);
+        if (on_gpu[c]) {  // encoded by the GPU batch: staging copy and zone map here
+            memcpy(stage[c], data[c], (size_t)nrows * (type_value_bits(cs.type) / 8));
+            rg.zones[c] = zone_of_typed(cs.type, stage[c], nrows);
             return;
         }
         const int T = type_value_bits(cs.type);
@@ -1318,9 +1352,10 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
         work();
         for (auto &t : th) t.join();
     }
+    if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
     w->fb.rgs.push_back(std::move(rg));
     // a full batch is encoded once its last row group is in place
-    if (w->gpu.dev >= 0 && w->gpu.batched >= GpuEncoder::kBatch) return w->gpu.flush(w->fb.rgs);
+    if (w->gpu.dev >= 0 && w->gpu.batched >= GpuEncoder::kBatch) return w->gpu.flush(w->fb.rgs, w->threads);
     return 0;
 }
 
@@ -1356,10 +1391,17 @@ int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
     if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (w->gpu.dev >= 0) {
-        const int rc = w->gpu.flush(w->fb.rgs);
+        const int rc = w->gpu.flush(w->fb.rgs, w->threads);
         if (rc) return rc;
     }
-    return w->fb.finish(img, len, 1);
+    const double tf = g_prof.on ? WriterProfile::now() : 0;
+    const int rc = w->fb.finish(img, len, 1);
+    if (g_prof.on) {
+        g_prof.finish += WriterProfile::now() - tf;
+        g_prof.print();
+        g_prof = WriterProfile();
+    }
+    return rc;
 }
 
 int fls_writer_finish_file(fls_writer *w, const char *path) {
