@@ -430,10 +430,6 @@ hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_n
     return hipGetLastError();
 }
 
-uint32_t order_for_launch(std::vector<EncChunk> &desc) {
-    const auto mid = std::stable_partition(desc.begin(), desc.end(), [](const EncChunk &c) { return c.T == 64; });
-    return (uint32_t)(mid - desc.begin());
-}
 
 }  // namespace fls
 

@@ -3,7 +3,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <vector>
 
 namespace fls {
 
@@ -30,9 +29,5 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // Launch over chunks [0, n_wide) of T = 64 and then [n_wide, n_wide + n_narrow)
 // of T <= 32 (one kernel each: u64 or u32 registers and LDS).
 hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream);
-// Order a launch's descriptors for launch_encode (T = 64 first, stable);
-// returns n_wide.  Each descriptor carries its own output and length
-// addresses, so the order is free.
-uint32_t order_for_launch(std::vector<EncChunk> &desc);
 
 }  // namespace fls

@@ -1037,14 +1037,6 @@ int default_writer_threads() {
 }
 }  // namespace
 
-// GPU chunk encoding of the FFOR / DELTA integer columns (fls_writer_set_device).
-// Row groups are batched: add() stages a row group's columns into pinned memory
-// (column-parallel memcpy) and records one job per chunk; every kBatch row
-// groups, and before the file is assembled, flush() sends the batch to the GPU
-// in one H2D copy, one encode_kernel launch (a block per chunk), the lengths
-// back, then one D2H copy per chunk into its row group.  (Per-row-group
-// launches of ~11 blocks left the GPU idle: 46 M rows/s against 65 M on 16
-// CPU threads for lineitem SF10.)  Buffers are kept across batches.
 // FLS_WRITER_PROFILE=1: wall time of the writer's phases, summed over the
 // writer's calls and printed to stderr when the image is finished
 struct WriterProfile {
@@ -1064,47 +1056,67 @@ struct WriterProfile {
 };
 static WriterProfile g_prof;
 
+// GPU chunk encoding of the FFOR / DELTA integer columns (fls_writer_set_device).
+// Row groups are batched, kBatch per launch, in two buffer sets used in turn.
+// add() reserves a row group's room in the current set (the caller stages the
+// values into pinned memory in the same worker pass as the zone maps) and
+// records one job per chunk.  A full set is submitted -- one H2D copy, the
+// encode launches (a block per chunk), the lengths and the slots back in two
+// D2H copies, all async on the encoder's stream -- and staging continues in
+// the other set.  A set's chunks move into their row groups when the set is
+// needed again or at finish(); by then its GPU work has run under the staging
+// of the next batch.  (Per-row-group launches of ~11 blocks left the GPU
+// idle: 46 M rows/s against 65 M on 16 CPU threads for lineitem SF10; one
+// synchronous flush per batch with a separate staging pass: 54 M rows/s.)
 struct GpuEncoder {
     static constexpr uint32_t kBatch = 32;  // row groups per launch
-    int dev = -1;
-    hipStream_t stream = nullptr;
-    uint8_t *h_stage = nullptr, *d_in = nullptr, *d_out = nullptr, *d_scratch = nullptr, *h_out = nullptr;
-    uint64_t *h_lens = nullptr, *d_lens = nullptr;
-    EncChunk *d_desc = nullptr;
-    size_t in_cap = 0, out_cap = 0, job_cap = 0;
     struct Job {
         size_t rg, col;
         uint64_t in_off, out_off;
         uint32_t nrows;
         uint8_t T, enc;
     };
-    std::vector<Job> jobs;
-    uint64_t in_used = 0, out_used = 0;
-    uint32_t batched = 0;  // row groups in the batch
+    struct Set {
+        uint8_t *h_stage = nullptr, *d_in = nullptr, *d_out = nullptr, *d_scratch = nullptr, *h_out = nullptr;
+        uint64_t *h_lens = nullptr, *d_lens = nullptr;
+        EncChunk *h_desc = nullptr, *d_desc = nullptr;
+        size_t in_cap = 0, out_cap = 0, job_cap = 0;
+        std::vector<Job> jobs;
+        uint64_t in_used = 0, out_used = 0;
+        uint32_t batched = 0;  // row groups in the set
+        bool in_flight = false;
+        hipEvent_t done = nullptr;
+    };
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    Set sets[2];
+    int cur = 0;
 
+    static void free_set(Set &b) {
+        hipHostFree(b.h_stage);
+        hipHostFree(b.h_lens);
+        hipHostFree(b.h_out);
+        hipHostFree(b.h_desc);
+        hipFree(b.d_in);
+        hipFree(b.d_out);
+        hipFree(b.d_lens);
+        hipFree(b.d_desc);
+        hipFree(b.d_scratch);
+        if (b.done) hipEventDestroy(b.done);
+        b = Set();
+    }
     void release() {
         if (dev < 0) return;
         hipSetDevice(dev);
         if (stream) hipStreamSynchronize(stream);
-        hipHostFree(h_stage);
-        hipHostFree(h_lens);
-        hipHostFree(h_out);
-        hipFree(d_in);
-        hipFree(d_out);
-        hipFree(d_lens);
-        hipFree(d_desc);
-        hipFree(d_scratch);
+        free_set(sets[0]);
+        free_set(sets[1]);
         if (stream) hipStreamDestroy(stream);
-        h_stage = d_in = d_out = d_scratch = h_out = nullptr;
-        h_lens = d_lens = nullptr;
-        d_desc = nullptr;
         stream = nullptr;
-        in_cap = out_cap = job_cap = 0;
-        jobs.clear();
-        in_used = out_used = 0;
-        batched = 0;
+        cur = 0;
     }
     ~GpuEncoder() { release(); }
+    bool full() const { return sets[cur].batched >= kBatch; }
 
 #define WHIP(expr)                                                                                  \
     do {                                                                                            \
@@ -1112,8 +1124,51 @@ struct GpuEncoder {
         if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-    // Reserve the batch's room for columns cols of row group rg (nrows rows);
-    // stage[c] = where column c's values go in the pinned staging buffer (the
+    // Room for a full batch of row groups needing in_rg / out_rg / nj each
+    // (the set is empty and idle here).
+    int ensure(Set &b, uint64_t in_rg, uint64_t out_rg, size_t nj) {
+        if (!b.done) WHIP(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+        if (kBatch * in_rg > b.in_cap) {
+            hipHostFree(b.h_stage);
+            hipFree(b.d_in);
+            b.h_stage = b.d_in = nullptr;
+            b.in_cap = 0;
+            WHIP(hipHostMalloc((void **)&b.h_stage, kBatch * in_rg, 0));
+            WHIP(hipMalloc((void **)&b.d_in, kBatch * in_rg));
+            b.in_cap = kBatch * in_rg;
+        }
+        if (kBatch * out_rg > b.out_cap) {
+            hipFree(b.d_out);
+            hipHostFree(b.h_out);
+            b.d_out = b.h_out = nullptr;
+            b.out_cap = 0;
+            WHIP(hipMalloc((void **)&b.d_out, kBatch * out_rg));
+            WHIP(hipHostMalloc((void **)&b.h_out, kBatch * out_rg, 0));
+            b.out_cap = kBatch * out_rg;
+        }
+        if (kBatch * nj > b.job_cap) {
+            hipFree(b.d_desc);
+            hipFree(b.d_lens);
+            hipHostFree(b.h_lens);
+            hipHostFree(b.h_desc);
+            hipFree(b.d_scratch);
+            b.d_desc = b.h_desc = nullptr;
+            b.d_lens = b.h_lens = nullptr;
+            b.d_scratch = nullptr;
+            b.job_cap = 0;
+            const size_t n = kBatch * nj;
+            WHIP(hipMalloc((void **)&b.d_desc, n * sizeof(EncChunk)));
+            WHIP(hipHostMalloc((void **)&b.h_desc, n * sizeof(EncChunk), 0));
+            WHIP(hipMalloc((void **)&b.d_lens, n * sizeof(uint64_t)));
+            WHIP(hipHostMalloc((void **)&b.h_lens, n * sizeof(uint64_t), 0));
+            WHIP(hipMalloc((void **)&b.d_scratch, n * enc_scratch_bytes()));
+            b.job_cap = n;
+        }
+        return 0;
+    }
+
+    // Reserve the current set's room for columns cols of row group rg (nrows
+    // rows); stage[c] = where column c's values go in pinned memory (the
     // caller copies them there, together with the column's zone map pass).
     int add(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, size_t rg, uint32_t nrows,
             int nthreads, std::vector<FileBuilder::RG> &rgs, std::vector<uint8_t *> &stage) {
@@ -1127,112 +1182,107 @@ struct GpuEncoder {
             in_rg += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
             out_rg += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
         }
-        if (in_used + in_rg > in_cap || out_used + out_rg > out_cap || jobs.size() + cols.size() > job_cap) {
-            if (!jobs.empty()) {
-                const int rc = flush(rgs, nthreads);
+        if (sets[cur].in_flight) {
+            const int rc = complete(sets[cur], rgs, nthreads);
+            if (rc) return rc;
+        }
+        Set *b = &sets[cur];
+        if (b->in_used + in_rg > b->in_cap || b->out_used + out_rg > b->out_cap || b->jobs.size() + cols.size() > b->job_cap) {
+            if (!b->jobs.empty()) {
+                int rc = submit();
                 if (rc) return rc;
+                b = &sets[cur];
+                if (b->in_flight && (rc = complete(*b, rgs, nthreads))) return rc;
             }
-            if (kBatch * in_rg > in_cap) {
-                hipHostFree(h_stage);
-                hipFree(d_in);
-                h_stage = d_in = nullptr;
-                in_cap = 0;
-                WHIP(hipHostMalloc((void **)&h_stage, kBatch * in_rg, 0));
-                WHIP(hipMalloc((void **)&d_in, kBatch * in_rg));
-                in_cap = kBatch * in_rg;
-            }
-            if (kBatch * out_rg > out_cap) {
-                hipFree(d_out);
-                hipHostFree(h_out);
-                d_out = h_out = nullptr;
-                out_cap = 0;
-                WHIP(hipMalloc((void **)&d_out, kBatch * out_rg));
-                WHIP(hipHostMalloc((void **)&h_out, kBatch * out_rg, 0));
-                out_cap = kBatch * out_rg;
-            }
-            if (kBatch * cols.size() > job_cap) {
-                hipFree(d_desc);
-                hipFree(d_lens);
-                hipHostFree(h_lens);
-                hipFree(d_scratch);
-                d_desc = nullptr;
-                d_lens = h_lens = nullptr;
-                d_scratch = nullptr;
-                job_cap = 0;
-                const size_t nj = kBatch * cols.size();
-                WHIP(hipMalloc((void **)&d_desc, nj * sizeof(EncChunk)));
-                WHIP(hipMalloc((void **)&d_lens, nj * sizeof(uint64_t)));
-                WHIP(hipHostMalloc((void **)&h_lens, nj * sizeof(uint64_t), 0));
-                WHIP(hipMalloc((void **)&d_scratch, nj * enc_scratch_bytes()));
-                job_cap = nj;
-            }
+            const int rc = ensure(*b, in_rg, out_rg, cols.size());
+            if (rc) return rc;
         }
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
-            jobs.push_back(Job{rg, c, in_used, out_used, nrows, (uint8_t)T, specs[c].enc});
-            stage[c] = h_stage + in_used;
-            in_used += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
-            out_used += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
+            b->jobs.push_back(Job{rg, c, b->in_used, b->out_used, nrows, (uint8_t)T, specs[c].enc});
+            stage[c] = b->h_stage + b->in_used;
+            b->in_used += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
+            b->out_used += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
         }
-        ++batched;  // the caller flushes a full batch once this row group is in rgs
+        ++b->batched;  // the caller submits a full set once this row group is in rgs
         return 0;
     }
 
-    // Encode the batch and move its chunks into their row groups (on up to
-    // nthreads threads).
-    int flush(std::vector<FileBuilder::RG> &rgs, int nthreads) {
-        if (jobs.empty()) return 0;
+    // Send the current set to the GPU (async) and switch to the other set.
+    int submit() {
+        Set &b = sets[cur];
+        if (b.jobs.empty()) return 0;
         const double t0 = g_prof.on ? WriterProfile::now() : 0;
         WHIP(hipSetDevice(dev));
-        std::vector<EncChunk> desc(jobs.size());
-        for (size_t i = 0; i < jobs.size(); ++i) {
-            const Job &jb = jobs[i];
-            EncChunk &c = desc[i];
-            c.in = (uint64_t)(uintptr_t)(d_in + jb.in_off);
-            c.out = (uint64_t)(uintptr_t)(d_out + jb.out_off);
-            c.len_out = (uint64_t)(uintptr_t)(d_lens + i);
-            c.scratch = (uint64_t)(uintptr_t)(d_scratch + i * enc_scratch_bytes());
+        for (size_t i = 0; i < b.jobs.size(); ++i) {
+            const Job &jb = b.jobs[i];
+            EncChunk &c = b.h_desc[i];
+            c.in = (uint64_t)(uintptr_t)(b.d_in + jb.in_off);
+            c.out = (uint64_t)(uintptr_t)(b.d_out + jb.out_off);
+            c.len_out = (uint64_t)(uintptr_t)(b.d_lens + i);
+            c.scratch = (uint64_t)(uintptr_t)(b.d_scratch + i * enc_scratch_bytes());
             c.nrows = jb.nrows;
             c.T = jb.T;
             c.enc = jb.enc;
             c.pad[0] = c.pad[1] = 0;
             c.pad2 = 0;
         }
-        const uint32_t n_wide = order_for_launch(desc);
-        WHIP(hipMemcpyAsync(d_in, h_stage, in_used, hipMemcpyHostToDevice, stream));
-        WHIP(hipMemcpyAsync(d_desc, desc.data(), jobs.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
-        WHIP(launch_encode(d_desc, n_wide, (uint32_t)jobs.size() - n_wide, stream));
-        WHIP(hipMemcpyAsync(h_lens, d_lens, jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        // T = 64 chunks first (launch_encode); each carries its own addresses
+        EncChunk *first = b.h_desc, *last = b.h_desc + b.jobs.size();
+        const uint32_t n_wide =
+            (uint32_t)(std::stable_partition(first, last, [](const EncChunk &c) { return c.T == 64; }) - first);
+        WHIP(hipMemcpyAsync(b.d_in, b.h_stage, b.in_used, hipMemcpyHostToDevice, stream));
+        WHIP(hipMemcpyAsync(b.d_desc, b.h_desc, b.jobs.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
+        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream));
+        WHIP(hipMemcpyAsync(b.h_lens, b.d_lens, b.jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         // the slots come back in one pinned copy (slots are sized for W = T,
         // so this moves more than the chunks hold, but one large copy beats
-        // a small pageable copy per chunk), then each chunk's bytes move out
-        WHIP(hipMemcpyAsync(h_out, d_out, out_used, hipMemcpyDeviceToHost, stream));
+        // a small copy per chunk); complete() moves each chunk's bytes out
+        WHIP(hipMemcpyAsync(b.h_out, b.d_out, b.out_used, hipMemcpyDeviceToHost, stream));
+        WHIP(hipEventRecord(b.done, stream));
+        b.in_flight = true;
+        cur ^= 1;
+        if (g_prof.on) g_prof.submit += WriterProfile::now() - t0;
+        return 0;
+    }
+
+    // Wait for a submitted set and move its chunks into their row groups (on
+    // up to nthreads threads); the set is then empty.
+    int complete(Set &b, std::vector<FileBuilder::RG> &rgs, int nthreads) {
+        const double t0 = g_prof.on ? WriterProfile::now() : 0;
+        WHIP(hipEventSynchronize(b.done));
         const double t1 = g_prof.on ? WriterProfile::now() : 0;
-        WHIP(hipStreamSynchronize(stream));
-        const double t2 = g_prof.on ? WriterProfile::now() : 0;
         std::atomic<size_t> next{0};
         auto move_out = [&]() {
-            for (size_t i; (i = next.fetch_add(1)) < jobs.size();) {
-                std::vector<uint8_t> &dst = rgs[jobs[i].rg].chunks[jobs[i].col];
-                dst.assign(h_out + jobs[i].out_off, h_out + jobs[i].out_off + h_lens[i]);
+            for (size_t i; (i = next.fetch_add(1)) < b.jobs.size();) {
+                const Job &jb = b.jobs[i];
+                std::vector<uint8_t> &dst = rgs[jb.rg].chunks[jb.col];
+                dst.assign(b.h_out + jb.out_off, b.h_out + jb.out_off + b.h_lens[i]);
             }
         };
         std::vector<std::thread> th;
-        const size_t nth = std::min<size_t>(jobs.size(), (size_t)std::max(1, nthreads));
+        const size_t nth = std::min<size_t>(b.jobs.size(), (size_t)std::max(1, nthreads));
         for (size_t t = 1; t < nth; ++t) th.emplace_back(move_out);
         move_out();
         for (auto &t : th) t.join();
+        b.jobs.clear();
+        b.in_used = b.out_used = 0;
+        b.batched = 0;
+        b.in_flight = false;
         if (g_prof.on) {
-            const double t3 = WriterProfile::now();
-            g_prof.submit += t1 - t0;
-            g_prof.gpu_wait += t2 - t1;
-            g_prof.copy_out += t3 - t2;
+            g_prof.gpu_wait += t1 - t0;
+            g_prof.copy_out += WriterProfile::now() - t1;
             ++g_prof.flushes;
         }
-        jobs.clear();
-        in_used = out_used = 0;
-        batched = 0;
         return 0;
+    }
+
+    // Every staged row group encoded and in place (before the file is assembled).
+    int finish(std::vector<FileBuilder::RG> &rgs, int nthreads) {
+        int rc = submit();
+        for (int k = 0; k < 2 && !rc; ++k)
+            if (sets[k].in_flight) rc = complete(sets[k], rgs, nthreads);
+        return rc;
     }
 #undef WHIP
 };
@@ -1355,7 +1405,7 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
     if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
     w->fb.rgs.push_back(std::move(rg));
     // a full batch is encoded once its last row group is in place
-    if (w->gpu.dev >= 0 && w->gpu.batched >= GpuEncoder::kBatch) return w->gpu.flush(w->fb.rgs, w->threads);
+    if (w->gpu.dev >= 0 && w->gpu.full()) return w->gpu.submit();
     return 0;
 }
 
@@ -1391,11 +1441,11 @@ int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
     if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (w->gpu.dev >= 0) {
-        const int rc = w->gpu.flush(w->fb.rgs, w->threads);
+        const int rc = w->gpu.finish(w->fb.rgs, w->threads);
         if (rc) return rc;
     }
     const double tf = g_prof.on ? WriterProfile::now() : 0;
-    const int rc = w->fb.finish(img, len, 1);
+    const int rc = w->fb.finish(img, len, w->threads);
     if (g_prof.on) {
         g_prof.finish += WriterProfile::now() - tf;
         g_prof.print();
