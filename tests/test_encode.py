@@ -50,7 +50,10 @@ def test_set_device_rejects_missing_gpu(fl):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (1024, 1024), (1, 65536),
-                                        (65536 * 3, 65536)])
+                                        (65536 * 3, 65536),
+                                        # > 32 row groups: the writer's two buffer sets take turns
+                                        # (async submit of batch k while batch k+1 is staged)
+                                        (1024 * 70 + 3, 1024), (200000, 1024)])
 def test_gpu_writer_bytes_identical(fl, gpu, n, rowgroup):
     cols = _columns(fl, n, np.random.default_rng(n))
     cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
