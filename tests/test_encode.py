@@ -83,23 +83,35 @@ def test_gpu_writer_mixed_columns_and_decode(fl, ref, gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("enc", ["FFOR", "DELTA"])
-def test_gpu_encode_device_resident(fl, gpu, enc):
+@pytest.mark.parametrize("tn", ["INT64", "INT32", "INT16", "UINT8"])
+def test_gpu_encode_device_resident(fl, gpu, enc, tn):
     """fls_encode_device over a column already in HBM: the chunks, laid end to
-    end, are the CPU writer's file body for the same single-column table."""
+    end, are the CPU writer's file body for the same single-column table
+    (INT64 runs the u64 kernel, the narrower types the u32 one)."""
     rng = np.random.default_rng(11)
     n = 65536 * 5 + 3000
-    vals = np.cumsum(rng.integers(0, 26, n)).astype(np.int64) + 1_000_000
+    ty = getattr(fl, tn)
+    dt = np.dtype(fl.NP_DTYPE[ty])
+    info = np.iinfo(dt)
+    if tn == "INT64":
+        vals = np.cumsum(rng.integers(0, 26, n)).astype(np.int64) + 1_000_000
+    else:
+        vals = rng.integers(int(info.min) // 2, int(info.max) // 2, n).astype(dt)
+        if enc == "DELTA":
+            vals = np.sort(vals)
     e = getattr(fl, "ENC_" + enc)
-    cpu = fl.write_image([("k", fl.INT64, vals, e)]).tobytes()
+    cpu = fl.write_image([("k", ty, vals, e)]).tobytes()
     d_in = fl.DeviceBuffer.from_array(vals)
-    slot = fl.encode_slot_bytes(fl.INT64, e)
+    slot = fl.encode_slot_bytes(ty, e)
     nrg = (n + 65535) // 65536
     d_out = fl.DeviceBuffer(slot * nrg)
-    lens, ms = fl.encode_device(0, fl.INT64, e, d_in.ptr, n, d_out.ptr)
+    lens, ms = fl.encode_device(0, ty, e, d_in.ptr, n, d_out.ptr)
     assert ms > 0
     body = b"".join(d_out.read(i * slot, lens[i]) for i in range(nrg))
     assert body == cpu[256:256 + len(body)]
     assert sum(lens) == len(body)
+    d_in.free()
+    d_out.free()
 
 
 @pytest.mark.gpu
