@@ -103,6 +103,8 @@ _sig("fls_table_column", C.c_int, _P, C.c_uint32, C.POINTER(ColumnInfo))
 _sig("fls_materialize", C.c_int, _P, C.c_uint32, C.POINTER(C.c_uint8), C.POINTER(RowGroup))
 _sig("fls_scan_begin", C.c_int, _P, C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32)
 _sig("fls_scan_next", C.c_int, _P, C.POINTER(RowGroup))
+_sig("fls_scan_acquire", C.c_int, _P, C.POINTER(RowGroup))
+_sig("fls_scan_release", C.c_int, _P, C.c_uint32)
 _sig("fls_scan_filter", C.c_int, _P, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_scan_pruned", C.c_int, _P)
 _sig("fls_table_zonemap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
@@ -114,6 +116,7 @@ _sig("fls_device_sync", C.c_int, _P, C.POINTER(DecodeStats))
 _sig("fls_device_column", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_device_copy_out", C.c_int, _P, C.c_uint32, C.c_uint64, C.c_uint64, _P)
 _sig("fls_device_rows", C.c_uint64, _P)
+_sig("fls_device_heap", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_writer_new", _P, C.c_uint64)
 _sig("fls_writer_free", None, _P)
 _sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8)
@@ -597,7 +600,7 @@ def _checklib():
         lib_.fls_check_workload.restype = C.c_int
         lib_.fls_check_workload.argtypes = [C.c_char_p, C.c_double, C.c_uint64, C.c_uint64, C.c_uint64,
                                             C.POINTER(_P), C.POINTER(C.c_uint8), C.c_int, C.POINTER(_P),
-                                            C.POINTER(C.c_uint64)]
+                                            C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
         lib_.fls_check_last_error.restype = C.c_char_p
         _check_lib = lib_
     return _check_lib
@@ -613,10 +616,15 @@ def check_device_table(t: "Table", workload: str, scale: float = 1.0, nrows: int
     obs = (C.c_uint8 * nc)()
     dicts = (_P * nc)()
     keep = []
+    deltas = (C.c_int64 * nc)()
     for c in range(nc):
         ptr, _ = t.device_column(c)
         cols[c] = ptr
         obs[c] = t.column(c).out_bytes
+        dp, hp, hn = _P(), _P(), C.c_uint64()
+        if obs[c] == 16 and _lib.fls_device_heap(t.h, c, C.byref(dp), C.byref(hp), C.byref(hn)) == 1:
+            deltas[c] = (dp.value or 0) - (hp.value or 0)   # free text (FSST): no dictionary
+            continue
         if obs[c] == 16:
             words = []
             k = 0
@@ -628,7 +636,7 @@ def check_device_table(t: "Table", workload: str, scale: float = 1.0, nrows: int
             dicts[c] = C.cast(b, _P)
     mism = (C.c_uint64 * nc)()
     rc = lib_.fls_check_workload(workload.encode(), scale, total, t.row_offset, t.device_rows, cols, obs, nc,
-                                 dicts, mism)
+                                 dicts, deltas, mism)
     if rc != 0:
         raise FlsError(rc, lib_.fls_check_last_error().decode())
     return list(mism)

@@ -8,6 +8,11 @@
 // rows per column.  Integer codecs are lossless: any mismatch is a decode bug.
 // VARCHAR string_t records are compared in full when inlined (<= 12 bytes) and
 // on length + 4-byte prefix when they point into the host dictionary heap.
+// Free text (l_comment, FSST, workload lineitem_full) is compared in full:
+// length, inline bytes or prefix, and every byte of a long string read from
+// the column's device heap (string_t pointer + heap_delta) against the text
+// pool uploaded next to it.  lineitem_dbl's ALP columns are compared as the
+// IEEE bits of cents / 100.0.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -16,6 +21,7 @@
 
 #include "../../include/flscheck.h"
 #include "fls_gen.hpp"
+#include "fls_text.hpp"
 
 namespace {
 
@@ -28,8 +34,13 @@ struct CheckArgs {
     uint32_t ob[kMaxCols];          // output bytes per value
     uint32_t str_cmp[kMaxCols];     // VARCHAR: per code bytes to compare (16 or 8), packed 4 bits x 8
     uint4 dict[kMaxCols][kMaxDict]; // expected string_t per code (pointer bytes zero)
+    int64_t heap_delta[kMaxCols];   // free-text column: device heap address - string_t pointer base
+    uint32_t text_col;              // free-text column (l_comment) or kMaxCols
+    uint32_t dbl_mask;              // columns decoded as DOUBLE = cents / 100.0 (lineitem_dbl)
+    const uint8_t *pool;            // text pool (device), pool_size bytes
+    uint64_t pool_size;
     int ncols;
-    int workload;                   // 0 c1, 1 lineitem, 2 c3, 3 c4
+    int workload;                   // 0 c1, 1 lineitem (+ _full, _dbl), 2 c3, 3 c4
     fls::gen::LineitemParams li;
     uint64_t row_begin;             // global row of decoded row 0
     uint64_t n;
@@ -54,6 +65,34 @@ __device__ __forceinline__ bool eq_col(const CheckArgs &a, int c, uint64_t i, in
     }
 }
 
+// l_comment of global row `row` against its decoded string_t record
+__device__ __forceinline__ bool eq_text(const CheckArgs &a, int c, uint64_t i, uint64_t row) {
+    uint64_t off;
+    uint32_t len;
+    fls::gen::comment_span(a.li.seed, row, a.pool_size, off, len);
+    const uint4 got = *(const uint4 *)(a.col[c] + 16 * i);
+    if (got.x != len) return false;
+    const uint8_t *want = a.pool + off;
+    if (len <= 12) {
+        const uint8_t *b = (const uint8_t *)&got + 4;
+        for (uint32_t k = 0; k < 12; ++k)
+            if (b[k] != (k < len ? want[k] : 0)) return false;
+        return true;
+    }
+    const uint8_t *pre = (const uint8_t *)&got + 4;
+    for (uint32_t k = 0; k < 4; ++k)
+        if (pre[k] != want[k]) return false;
+    const uint8_t *str = (const uint8_t *)(((uint64_t)got.w << 32 | got.z) + (uint64_t)a.heap_delta[c]);
+    for (uint32_t k = 0; k < len; ++k)
+        if (str[k] != want[k]) return false;
+    return true;
+}
+
+__device__ __forceinline__ int64_t dbl_bits(int64_t cents) {
+    const double d = (double)cents / 100.0;
+    return __double_as_longlong(d);
+}
+
 __global__ void check_kernel(CheckArgs a, unsigned long long *mism) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t i0 = t * kRowsPerThread;
@@ -68,8 +107,15 @@ __global__ void check_kernel(CheckArgs a, unsigned long long *mism) {
         fls::gen::LineitemRow r;
         for (uint64_t i = i0; i < i1; ++i, ow.next()) {
             fls::gen::lineitem_row_at(a.li, a.row_begin + i, ow.cur(), r);
-            for (int c = 0; c < a.ncols; ++c)
-                if (a.col[c] && !eq_col(a, c, i, fls::gen::lineitem_col(r, c))) bad[c]++;
+            for (int c = 0; c < a.ncols; ++c) {
+                if (!a.col[c]) continue;
+                if ((uint32_t)c == a.text_col) {
+                    if (!eq_text(a, c, i, a.row_begin + i)) bad[c]++;
+                    continue;
+                }
+                const int64_t v = fls::gen::lineitem_col(r, c);
+                if (!eq_col(a, c, i, (a.dbl_mask >> c) & 1 ? dbl_bits(v) : v)) bad[c]++;
+            }
         }
     } else if (a.workload == 2) {
         fls::gen::OrderWalker ow;
@@ -102,14 +148,31 @@ const char *fls_check_last_error(void) { return g_err.c_str(); }
 
 int fls_check_workload(const char *workload, double scale, uint64_t nrows_total, uint64_t row_begin, uint64_t n,
                        const void *const *d_cols, const uint8_t *out_bytes, int ncols, const void *const *dicts,
-                       uint64_t *mismatches) {
+                       const int64_t *heap_delta, uint64_t *mismatches) {
     if (!workload || !d_cols || !out_bytes || !mismatches || ncols < 1 || ncols > kMaxCols)
         return err("fls_check_workload: bad arguments");
     CheckArgs a;
     memset(&a, 0, sizeof(a));
     std::string w = workload;
-    a.workload = w == "c1" ? 0 : w == "lineitem" ? 1 : w == "c3" ? 2 : w == "c4" ? 3 : -1;
+    const bool li = w == "lineitem" || w == "lineitem_full" || w == "lineitem_dbl";
+    a.workload = w == "c1" ? 0 : li ? 1 : w == "c3" ? 2 : w == "c4" ? 3 : -1;
     if (a.workload < 0) return err("unknown workload " + w);
+    a.text_col = kMaxCols;
+    if (w == "lineitem_dbl") a.dbl_mask = 0xF0u;  // quantity, extendedprice, discount, tax
+    uint8_t *d_pool = nullptr;
+    if (w == "lineitem_full" && ncols > 15 && d_cols[15]) {
+        if (!heap_delta) return err("lineitem_full: l_comment needs its heap_delta");
+        const std::string &pool = fls::gen::text_pool();
+        if (hipMalloc(&d_pool, pool.size()) != hipSuccess) return err("hipMalloc failed");
+        if (hipMemcpy(d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d_pool);
+            return err("hipMemcpy failed");
+        }
+        a.text_col = 15;
+        a.pool = d_pool;
+        a.pool_size = pool.size();
+        a.heap_delta[15] = heap_delta[15];
+    }
     a.ncols = ncols;
     a.li.seed = fls::gen::kSeed;
     a.li.nrows = nrows_total;
@@ -120,7 +183,7 @@ int fls_check_workload(const char *workload, double scale, uint64_t nrows_total,
     for (int c = 0; c < ncols; ++c) {
         a.col[c] = (const uint8_t *)d_cols[c];
         a.ob[c] = out_bytes[c];
-        if (out_bytes[c] == 16) {
+        if (out_bytes[c] == 16 && (uint32_t)c != a.text_col) {
             // dicts[c]: NUL-separated list of the column's dictionary strings (<= 8)
             const char *s = dicts ? (const char *)dicts[c] : nullptr;
             if (!s) return err("VARCHAR column needs its dictionary");
@@ -137,12 +200,16 @@ int fls_check_workload(const char *workload, double scale, uint64_t nrows_total,
         }
     }
     unsigned long long *d_m = nullptr;
-    if (hipMalloc(&d_m, sizeof(unsigned long long) * kMaxCols) != hipSuccess) return err("hipMalloc failed");
+    if (hipMalloc(&d_m, sizeof(unsigned long long) * kMaxCols) != hipSuccess) {
+        if (d_pool) (void)hipFree(d_pool);
+        return err("hipMalloc failed");
+    }
     if (hipMemset(d_m, 0, sizeof(unsigned long long) * kMaxCols) != hipSuccess) return err("hipMemset failed");
     const uint64_t threads = (n + kRowsPerThread - 1) / kRowsPerThread;
     const uint32_t blocks = (uint32_t)((threads + 255) / 256);
     if (blocks) hipLaunchKernelGGL(check_kernel, dim3(blocks), dim3(256), 0, 0, a, d_m);
     hipError_t e = hipDeviceSynchronize();
+    if (d_pool) (void)hipFree(d_pool);
     if (e != hipSuccess) {
         (void)hipFree(d_m);
         return err(std::string("check kernel failed: ") + hipGetErrorString(e));

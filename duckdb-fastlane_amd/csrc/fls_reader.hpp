@@ -36,6 +36,10 @@ struct FileMeta {
     std::vector<RowGroupMeta> rgs;
 };
 
+// Is [off, off + n) inside [0, lim)?  Each term is compared on its own, so a
+// u64 field near 2^64 taken from the file cannot wrap the sum past the check.
+inline bool fits(uint64_t off, uint64_t n, uint64_t lim) { return off <= lim && n <= lim - off; }
+
 // Parse and validate; returns empty string on success, else the reason.
 inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
     auto rd = [&](uint64_t off, void *dst, size_t n) -> bool {
@@ -111,8 +115,8 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
             if ((h.enc == ENC_FFOR || h.enc == ENC_DELTA) && h.T != h.vbits) return "bad packing width";
             if (h.enc == ENC_DICT && h.T != 32) return "bad dictionary code width";
             if (h.enc == ENC_RLE && h.T != 16) return "bad run-index width";
-            if (h.meta_off + 32ull * h.nvec > ch.len || h.packed_off > ch.len || h.aux_off > ch.len ||
-                h.aux_len > ch.len - h.aux_off || h.packed_off % 16 || h.meta_off % 16 || h.aux_off % 16)
+            if (!fits(h.meta_off, 32ull * h.nvec, ch.len) || h.packed_off > h.aux_off || !fits(h.aux_off, h.aux_len, ch.len) ||
+                h.packed_off % 16 || h.meta_off % 16 || h.aux_off % 16)
                 return "chunk layout out of bounds";
             // per-vector validation: packed extents, widths, aux extents
             for (uint32_t v = 0; v < h.nvec; ++v) {
@@ -120,26 +124,27 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
                 memcpy(&vm, img + ch.off + h.meta_off + 32ull * v, 32);
                 if (vm.bw > h.T || vm.nvals == 0 || vm.nvals > kVectorSize) return "bad vector meta";
                 if (v + 1 < h.nvec && vm.nvals != kVectorSize) return "short vector before the last";
-                if (vm.packed_off % 16 || h.packed_off + vm.packed_off + 128ull * vm.bw > h.aux_off) return "packed vector out of bounds";
-                if (h.enc == ENC_DELTA && (vm.aux_off % 16 || vm.aux_off + 128 > h.aux_len)) return "delta bases out of bounds";
+                if (vm.packed_off % 16 || !fits(vm.packed_off, 128ull * vm.bw, h.aux_off - h.packed_off))
+                    return "packed vector out of bounds";
+                if (h.enc == ENC_DELTA && (vm.aux_off % 16 || !fits(vm.aux_off, 128, h.aux_len))) return "delta bases out of bounds";
                 if (h.enc == ENC_RLE) {
                     if (vm.aux_off % 16 || vm.aux_count == 0 || vm.aux_count > kVectorSize ||
-                        vm.aux_off + 128 + (uint64_t)vm.aux_count * (h.vbits / 8) > h.aux_len)
+                        !fits(vm.aux_off, 128 + (uint64_t)vm.aux_count * (h.vbits / 8), h.aux_len))
                         return "run values out of bounds";
                 }
                 if (h.enc == ENC_ALP) {
                     const uint32_t exc = alp_exceptions(vm.aux_count), e = alp_e(vm.aux_count), f = alp_f(vm.aux_count);
                     const uint32_t maxe = h.T == 64 ? kAlpMaxExpD : kAlpMaxExpF;
                     if (e > maxe || f > e || exc > vm.nvals) return "bad ALP exponent or exception count";
-                    if (exc && (vm.aux_off % 16 || vm.aux_off + alp_aux_bytes(exc, h.vbits) > h.aux_len))
+                    if (exc && (vm.aux_off % 16 || !fits(vm.aux_off, alp_aux_bytes(exc, h.vbits), h.aux_len)))
                         return "ALP exceptions out of bounds";
                 }
                 if (h.enc == ENC_FSST) {
                     FsstVecHeader fh;
-                    if (vm.aux_off % 16 || vm.aux_off < kFsstTableBytes || vm.aux_off + sizeof(fh) > h.aux_len)
+                    if (vm.aux_off % 16 || vm.aux_off < kFsstTableBytes || !fits(vm.aux_off, sizeof(fh), h.aux_len))
                         return "FSST vector out of bounds";
                     memcpy(&fh, img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
-                    if (fh.clen_w > 32 || vm.aux_off + fsst_stream_off(fh) + fh.comp_len > h.aux_len ||
+                    if (fh.clen_w > 32 || !fits(vm.aux_off, fsst_stream_off(fh) + fh.comp_len, h.aux_len) ||
                         fh.heap_off % 16 || fh.heap_off + (uint64_t)vm.aux_count > h.reserved1)
                         return "FSST vector out of bounds";
                 }

@@ -1,4 +1,4 @@
-// fls_text.hpp -- seeded TPC-H-like comment text (host only).
+// fls_text.hpp -- seeded TPC-H-like comment text (pool built on the host).
 //
 // TPC-H (spec 4.2.2.10) draws comment columns as random substrings of a text
 // pool produced by a small sentence grammar; l_comment is 10..43 characters.
@@ -94,12 +94,18 @@ inline const std::string &text_pool() {
     return pool;
 }
 
-// l_comment of a row: 10..43 characters cut from the pool
+// l_comment of a row: 10..43 characters cut from the pool at [off, off + len)
+// (host and device: the GPU check regenerates it next to the decoded column)
+FLS_HD void comment_span(uint64_t seed, uint64_t row, uint64_t pool_size, uint64_t &off, uint32_t &len) {
+    const uint64_t r = rnd(seed, S_COMMENT, row);
+    len = 10 + (uint32_t)(r % 34);
+    off = (r >> 8) % (pool_size - len);
+}
 inline std::string_view comment(uint64_t seed, uint64_t row) {
     const std::string &p = text_pool();
-    const uint64_t r = rnd(seed, S_COMMENT, row);
-    const uint32_t len = 10 + (uint32_t)(r % 34);
-    const uint64_t off = (r >> 8) % (p.size() - len);
+    uint64_t off;
+    uint32_t len;
+    comment_span(seed, row, p.size(), off, len);
     return std::string_view(p.data() + off, len);
 }
 

@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -165,13 +166,33 @@ struct DeviceShard {
     std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
 };
 
+// Pinned host side of one decoded batch: what consumers read.  It belongs to
+// the batch's row groups, not to the device slot that produced it: once every
+// row group of the batch has been handed out (fls_scan_acquire) the slot is
+// refilled with a fresh HostBatch from the pool, and this one goes back to the
+// pool when the last of its row groups is released.  So a consumer that keeps
+// a row group (DuckDB vectors that reference the pinned columns) never holds
+// up the GPU pipeline, and no consumer waits for another one's release.
+struct HostBatch {
+    uint32_t rg0 = 0, nrg = 0;
+    uint32_t handed = 0, released = 0;    // row groups handed out / handed back
+    std::vector<PinBuf<uint8_t>> h_out;   // per delivered column (pinned)
+    std::vector<PinBuf<uint8_t>> h_heap;  // per FSST column: pinned copy string_t points into
+    std::vector<const void *> col_ptrs;   // per (rg - rg0) * ncols + col: pinned host column start
+    PinBuf<uint32_t> h_counts;            // filtered: selected rows per vector
+    PinBuf<uint32_t> h_sel;               // filtered: selected row indices within their row group
+    uint32_t nvec = 0;                    // vectors of the batch
+    bool sel_ready = false;               // sel_off computed from h_counts
+    std::vector<uint32_t> sel_off;        // per row group of the batch (+1): first selected row
+};
+
 struct Slot {                       // one batch of row groups in flight
     uint32_t rg0 = 0, nrg = 0;      // absolute row groups (consecutive, all surviving pruning)
-    bool busy = false;
+    bool busy = false;              // a batch is enqueued and not yet fully handed out
+    bool starved = false;           // refill deferred: the host-batch pool is at its cap
+    HostBatch *hb = nullptr;        // host side of the batch in flight
     std::vector<DevBuf<uint8_t>> d_out;   // per decoded column
-    std::vector<PinBuf<uint8_t>> h_out;   // per delivered column (pinned)
     std::vector<DevBuf<uint8_t>> d_heap;  // per FSST column: decoded string bytes
-    std::vector<PinBuf<uint8_t>> h_heap;  // per FSST column: pinned copy string_t points into
     std::vector<uint64_t> heap_bytes;     // per column: heap bytes of this batch
     PinBuf<DevChunk> h_chunks;
     DevBuf<DevChunk> d_chunks;
@@ -181,18 +202,11 @@ struct Slot {                       // one batch of row groups in flight
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
-    uint32_t released = 0;          // row groups of the batch handed back by consumers
-    std::vector<const void *> col_ptrs;  // per (rg - rg0) * ncols + col: pinned host column start
     // filtered batches (fls_scan_filter)
     DevBuf<uint64_t> d_mask;        // selection bits, 16 words per 1024-row vector
     DevBuf<uint32_t> d_counts;      // selected rows per vector
-    PinBuf<uint32_t> h_counts;
-    PinBuf<uint32_t> h_sel;         // selected row indices within their row group
     PinBuf<uint8_t> h_fdesc;        // DevTerm[] + DevOut[] + constant strings
     DevBuf<uint8_t> d_fdesc;
-    uint32_t nvec = 0;              // vectors of the batch
-    bool sel_ready = false;         // sel_off computed from h_counts
-    std::vector<uint32_t> sel_off;  // per row group of the batch (+1): first selected row
 };
 
 struct ScanDev {
@@ -202,6 +216,8 @@ struct ScanDev {
     uint32_t p0 = 0, p1 = 0;        // ... as positions in ScanCtx::rgs
     uint32_t next_p = 0;            // next position to enqueue
     Slot slots[2];
+    std::vector<std::unique_ptr<HostBatch>> batches;  // host-batch pool of this GPU
+    std::vector<HostBatch *> free_batches;
     DevBuf<StrT> strtab;
     std::vector<uint64_t> strtab_off;
     DevBuf<uint32_t> err;
@@ -227,6 +243,13 @@ struct ScanCtx {
     uint32_t batch = 8;
     std::vector<ScanDev> devs;
     int64_t held = -1;              // row group fls_scan_next handed out last (released on the next call)
+    std::vector<std::pair<uint32_t, HostBatch *>> out;  // row groups handed out and not yet released
+    uint32_t max_batches = 64;      // host-batch pool cap per GPU (FLS_SCAN_HOST_BATCHES)
+    // sticky error of a failed batch refill (scan_release): consumers waiting
+    // for a row group of that batch, and every later acquire, return it
+    // instead of waiting for a batch that will never be enqueued
+    int err_rc = 0;
+    std::string err_msg;
     // fls_scan_acquire/release may be called from several consumer threads:
     // claiming a row group, releasing one and refilling a slot happen under mu;
     // waiting for a batch's decode does not.
@@ -654,8 +677,15 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         for (auto &sl : d.slots) {
             if (sl.stream) hipStreamSynchronize(sl.stream);
             sl.busy = false;
+            sl.starved = false;
+            sl.hb = nullptr;
         }
+        // every host batch back to the pool (a row group still held from the
+        // previous scan is invalid from here on, as documented in flsgpu.h)
+        d.free_batches.clear();
+        for (auto &b : d.batches) d.free_batches.push_back(b.get());
     }
+    s.out.clear();
     s.mask.assign(ncols, 1);
     if (col_mask)
         for (uint32_t c = 0; c < ncols; ++c) s.mask[c] = col_mask[c] ? 1 : 0;
@@ -673,6 +703,8 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     }
     s.cur = 0;
     s.held = -1;
+    s.err_rc = 0;
+    s.err_msg.clear();
     if (s.rgs.empty()) {  // an empty table or range, or every row group pruned: no device work
         s.active = true;
         return 0;
@@ -693,6 +725,8 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
     }
     const char *b = getenv("FLS_SCAN_BATCH");
     s.batch = b ? (uint32_t)std::max(1, atoi(b)) : 8u;
+    const char *mb = getenv("FLS_SCAN_HOST_BATCHES");
+    s.max_batches = mb ? (uint32_t)std::max(2, atoi(mb)) : 64u;
     for (uint32_t g = 0; g < G; ++g) {
         ScanDev &d = s.devs[g];
         d.dev = devs[g];
@@ -702,7 +736,6 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
             if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
             if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
             sl.d_out.resize(ncols);
-            sl.h_out.resize(ncols);
         }
         // contiguous shard of the surviving row groups
         d.p0 = (uint32_t)((uint64_t)n * g / G);
@@ -738,7 +771,7 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
         DevOut o;
         memset(&o, 0, sizeof(o));
         o.src = sl.d_out[c].p;
-        o.dst = sl.h_out[c].p;
+        o.dst = sl.hb->h_out[c].p;
         o.ob = (uint32_t)out_bytes_of(t, c);
         outs.push_back(o);
     }
@@ -748,8 +781,8 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
     const size_t bytes = nt * sizeof(DevTerm) + no * sizeof(DevOut) + str_bytes;
     HIP_TRY(sl.h_fdesc.alloc(bytes));
     HIP_TRY(sl.d_fdesc.alloc(d.dev, bytes));
-    uint8_t *hb = sl.h_fdesc.p;
-    DevTerm *terms = (DevTerm *)hb;
+    uint8_t *fd = sl.h_fdesc.p;
+    DevTerm *terms = (DevTerm *)fd;
     size_t so = nt * sizeof(DevTerm) + no * sizeof(DevOut);
     for (size_t i = 0; i < nt; ++i) {
         const HostTerm &h = s.terms[i];
@@ -762,14 +795,14 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
         dt.ob = (uint8_t)out_bytes_of(t, h.col);
         dt.end_clause = (i + 1 == nt || s.terms[i + 1].clause != h.clause) ? 1 : 0;
         if (h.kind == FK_STR) {
-            memcpy(hb + so, h.str.data(), h.str.size());
+            memcpy(fd + so, h.str.data(), h.str.size());
             dt.str = sl.d_fdesc.p + so;
             dt.str_len = (uint32_t)h.str.size();
             so += (h.str.size() + 15) & ~size_t(15);
             if (sl.heap_bytes[h.col]) {  // FSST: long strings live in the batch heap
-                dt.host_lo = (uint64_t)(uintptr_t)sl.h_heap[h.col].p;
+                dt.host_lo = (uint64_t)(uintptr_t)sl.hb->h_heap[h.col].p;
                 dt.host_hi = dt.host_lo + sl.heap_bytes[h.col];
-                dt.dev_delta = (int64_t)((uintptr_t)sl.d_heap[h.col].p - (uintptr_t)sl.h_heap[h.col].p);
+                dt.dev_delta = (int64_t)((uintptr_t)sl.d_heap[h.col].p - (uintptr_t)sl.hb->h_heap[h.col].p);
             } else {  // DICT: long strings point into the file image, uploaded as d_in
                 dt.host_lo = (uint64_t)(uintptr_t)(t->img + in_lo);
                 dt.host_hi = dt.host_lo + in_len;
@@ -777,20 +810,21 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
             }
         }
     }
-    memcpy(hb + nt * sizeof(DevTerm), outs.data(), no * sizeof(DevOut));
-    HIP_TRY(hipMemcpyAsync(sl.d_fdesc.p, hb, bytes, hipMemcpyHostToDevice, sl.stream));
-    sl.nvec = (uint32_t)((rows + 1023) / 1024);
-    HIP_TRY(sl.d_mask.alloc(d.dev, (size_t)sl.nvec * 16));
-    HIP_TRY(sl.d_counts.alloc(d.dev, sl.nvec));
-    HIP_TRY(sl.h_counts.alloc(sl.nvec));
-    HIP_TRY(sl.h_sel.alloc(std::max<uint64_t>(rows, 1)));
+    memcpy(fd + nt * sizeof(DevTerm), outs.data(), no * sizeof(DevOut));
+    HIP_TRY(hipMemcpyAsync(sl.d_fdesc.p, fd, bytes, hipMemcpyHostToDevice, sl.stream));
+    HostBatch &hb = *sl.hb;
+    hb.nvec = (uint32_t)((rows + 1023) / 1024);
+    HIP_TRY(sl.d_mask.alloc(d.dev, (size_t)hb.nvec * 16));
+    HIP_TRY(sl.d_counts.alloc(d.dev, hb.nvec));
+    HIP_TRY(hb.h_counts.alloc(hb.nvec));
+    HIP_TRY(hb.h_sel.alloc(std::max<uint64_t>(rows, 1)));
     HIP_TRY(launch_filter((const DevTerm *)sl.d_fdesc.p, (uint32_t)nt, (uint32_t)rows, sl.d_mask.p, sl.d_counts.p,
                           d.err.p, sl.stream));
     HIP_TRY(launch_compact((const DevOut *)(sl.d_fdesc.p + nt * sizeof(DevTerm)), (uint32_t)no, sl.d_mask.p,
-                           sl.d_counts.p, (uint32_t)rows, t->meta.rowgroup_size, sl.h_sel.p, sl.stream));
-    HIP_TRY(hipMemcpyAsync(sl.h_counts.p, sl.d_counts.p, sl.nvec * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           sl.d_counts.p, (uint32_t)rows, t->meta.rowgroup_size, hb.h_sel.p, sl.stream));
+    HIP_TRY(hipMemcpyAsync(hb.h_counts.p, sl.d_counts.p, hb.nvec * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            sl.stream));
-    sl.sel_ready = false;
+    hb.sel_ready = false;
     return 0;
 }
 
@@ -798,13 +832,38 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
 // surviving row groups
 int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     Slot &sl = d.slots[si];
-    if (d.next_p >= d.p1) { sl.busy = false; return 0; }
+    sl.busy = false;
+    sl.starved = false;
+    sl.hb = nullptr;
+    if (d.next_p >= d.p1) return 0;
+    // host side from the pool; at the cap the refill waits for a release
+    if (d.free_batches.empty()) {
+        if (d.batches.size() >= s.max_batches) {
+            sl.starved = true;
+            return 0;
+        }
+        d.batches.push_back(std::make_unique<HostBatch>());
+        d.free_batches.push_back(d.batches.back().get());
+    }
+    {   // test hook: FLS_TEST_FAIL_ENQUEUE=k fails the k-th batch enqueue of the
+        // process (1-based) as an allocation failure would (tests/test_scan_errors.py)
+        static std::atomic<long> n_enqueue{0};
+        const char *f = getenv("FLS_TEST_FAIL_ENQUEUE");
+        if (f && ++n_enqueue == atol(f)) return fail(FLS_ERR_NOMEM, "injected batch enqueue failure (FLS_TEST_FAIL_ENQUEUE)");
+    }
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     const bool filtered = !s.terms.empty();
     sl.rg0 = s.rgs[d.next_p];
     sl.nrg = 1;
     while (sl.nrg < s.batch && d.next_p + sl.nrg < d.p1 && s.rgs[d.next_p + sl.nrg] == sl.rg0 + sl.nrg) sl.nrg++;
     d.next_p += sl.nrg;
+    sl.hb = d.free_batches.back();
+    d.free_batches.pop_back();
+    HostBatch &hb = *sl.hb;
+    hb.rg0 = sl.rg0;
+    hb.nrg = sl.nrg;
+    hb.handed = hb.released = 0;
+    hb.h_out.resize(ncols);
     HIP_TRY(hipSetDevice(d.dev));
     // 1. H2D of the batch's compressed bytes
     uint64_t lo, hi;
@@ -822,20 +881,20 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
     sl.heap_bytes.assign(ncols, 0);
     sl.d_heap.resize(ncols);
-    sl.h_heap.resize(ncols);
+    hb.h_heap.resize(ncols);
     std::vector<uint64_t> hoff((size_t)sl.nrg * ncols, 0);
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.dmask, c)) continue;
         const uint64_t nb = max_rows * out_bytes_of(t, c);
         HIP_TRY(sl.d_out[c].alloc(d.dev, nb));
-        if (col_selected(s.mask, c)) HIP_TRY(sl.h_out[c].alloc(nb));
+        if (col_selected(s.mask, c)) HIP_TRY(hb.h_out[c].alloc(nb));
         for (uint32_t r = 0; r < sl.nrg; ++r) {
             hoff[(size_t)r * ncols + c] = sl.heap_bytes[c];
             if (is_fsst(t, sl.rg0 + r, c)) sl.heap_bytes[c] += t->meta.rgs[sl.rg0 + r].chunks[c].hdr.reserved1;
         }
         if (sl.heap_bytes[c]) {
             HIP_TRY(sl.d_heap[c].alloc(d.dev, sl.heap_bytes[c]));
-            HIP_TRY(sl.h_heap[c].alloc(sl.heap_bytes[c]));
+            HIP_TRY(hb.h_heap[c].alloc(sl.heap_bytes[c]));
         }
     }
     std::vector<DevChunk> list;
@@ -851,7 +910,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const uint64_t ho = hoff[(size_t)(r - sl.rg0) * ncols + c];
             list.push_back(make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc,
                                          sl.heap_bytes[c] ? sl.d_heap[c].p + ho : nullptr,
-                                         sl.heap_bytes[c] ? sl.h_heap[c].p + ho : nullptr));
+                                         sl.heap_bytes[c] ? hb.h_heap[c].p + ho : nullptr));
         }
     }
     FsstCounts fsst;
@@ -878,21 +937,20 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
         if (!filtered)
-            HIP_TRY(hipMemcpyAsync(sl.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
+            HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
                                    sl.stream));
         if (sl.heap_bytes[c])
-            HIP_TRY(hipMemcpyAsync(sl.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
+            HIP_TRY(hipMemcpyAsync(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
     }
     HIP_TRY(hipEventRecord(sl.done, sl.stream));
-    sl.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
+    hb.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
     if (!filtered)
         for (uint32_t r = 0; r < sl.nrg; ++r)
             for (uint32_t c = 0; c < ncols; ++c)
                 if (col_selected(s.mask, c))
-                    sl.col_ptrs[(size_t)r * ncols + c] =
-                        sl.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) *
+                    hb.col_ptrs[(size_t)r * ncols + c] =
+                        hb.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) *
                                             out_bytes_of(t, c);
-    sl.released = 0;
     sl.busy = true;
     return 0;
 }
@@ -923,48 +981,74 @@ bool find_slot(ScanCtx &s, uint32_t rg, int &g, int &si) {
 
 // filtered batch: selected-row offsets of its row groups from the per-vector
 // counts (every row group of a batch but the table's last is whole vectors)
-void batch_selection(fls_table *t, ScanCtx &s, Slot &sl) {
+void batch_selection(fls_table *t, ScanCtx &s, HostBatch &hb) {
     std::lock_guard<std::mutex> lk(s.mu);
-    if (sl.sel_ready) return;
+    if (hb.sel_ready) return;
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
-    sl.sel_off.assign(sl.nrg + 1, 0);
+    hb.sel_off.assign(hb.nrg + 1, 0);
     uint32_t v = 0, acc = 0;
-    for (uint32_t r = 0; r < sl.nrg; ++r) {
-        sl.sel_off[r] = acc;
-        const uint32_t nv = (t->meta.rgs[sl.rg0 + r].nrows + 1023) / 1024;
-        for (uint32_t k = 0; k < nv && v < sl.nvec; ++k) acc += sl.h_counts.p[v++];
+    for (uint32_t r = 0; r < hb.nrg; ++r) {
+        hb.sel_off[r] = acc;
+        const uint32_t nv = (t->meta.rgs[hb.rg0 + r].nrows + 1023) / 1024;
+        for (uint32_t k = 0; k < nv && v < hb.nvec; ++k) acc += hb.h_counts.p[v++];
     }
-    sl.sel_off[sl.nrg] = acc;
-    for (uint32_t r = 0; r < sl.nrg; ++r)
+    hb.sel_off[hb.nrg] = acc;
+    for (uint32_t r = 0; r < hb.nrg; ++r)
         for (uint32_t c = 0; c < ncols; ++c)
             if (col_selected(s.mask, c))
-                sl.col_ptrs[(size_t)r * ncols + c] = sl.h_out[c].p + (uint64_t)sl.sel_off[r] * out_bytes_of(t, c);
-    sl.sel_ready = true;
+                hb.col_ptrs[(size_t)r * ncols + c] = hb.h_out[c].p + (uint64_t)hb.sel_off[r] * out_bytes_of(t, c);
+    hb.sel_ready = true;
+}
+
+// sticky scan error (call with s.mu held): every waiting and later acquire
+// returns it instead of waiting for a batch that will never arrive
+void set_scan_error(ScanCtx &s, int rc) {
+    if (rc && !s.err_rc) {
+        s.err_rc = rc;
+        s.err_msg = fls_last_error();
+    }
 }
 
 // Claim the next row group in order and wait until its batch is decoded and
-// copied back.  Its buffers stay valid until scan_release(rg).
+// copied back.  Its buffers stay valid until scan_release(rg).  Handing out a
+// batch's last row group refills its slot (the device side is idle once the
+// batch's D2H completed), so no consumer waits on another one's release.
 int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     if (!s.active) return fail(FLS_ERR_STATE, "scan not started");
     int g = -1, si = -1;
     uint32_t rg;
+    HostBatch *hb = nullptr;
     {
         std::unique_lock<std::mutex> lk(s.mu);
+        if (s.err_rc) return fail(s.err_rc, "%s", s.err_msg.c_str());
         if (s.cur >= s.rgs.size()) return 0;
         rg = s.rgs[s.cur++];
-        // the batch holding rg is enqueued once every row group of the slot's
-        // previous batch has been released (by this or another consumer)
-        s.cv.wait(lk, [&] { return !s.active || find_slot(s, rg, g, si); });
-        if (!s.active) return fail(FLS_ERR_STATE, "scan ended while waiting for row group %u", rg);
+        // the batch holding rg is enqueued once the slot's previous batch has
+        // been handed out (or, at the host-batch cap, once one is released)
+        s.cv.wait(lk, [&] { return find_slot(s, rg, g, si) || !s.active || s.err_rc != 0; });
+        if (g < 0) {
+            if (!s.active) return fail(FLS_ERR_STATE, "scan ended while waiting for row group %u", rg);
+            return fail(s.err_rc, "%s", s.err_msg.c_str());
+        }
+        hb = s.devs[g].slots[si].hb;
     }
     ScanDev &d = s.devs[g];
     Slot &sl = d.slots[si];
-    HIP_TRY(hipSetDevice(d.dev));
-    HIP_TRY(hipEventSynchronize(sl.done));
-    uint32_t err = 0;
-    HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
-    if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
-    if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
+    auto wait_batch = [&]() -> int {
+        HIP_TRY(hipSetDevice(d.dev));
+        HIP_TRY(hipEventSynchronize(sl.done));
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
+        if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
+        if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
+        return 0;
+    };
+    if (int rc = wait_batch()) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        set_scan_error(s, rc);
+        s.cv.notify_all();
+        return rc;
+    }
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     out->rowgroup = rg;
     out->nrows = t->meta.rgs[rg].nrows;
@@ -973,25 +1057,45 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     out->nrows_scanned = out->nrows;
     out->sel = nullptr;
     if (!s.terms.empty()) {
-        batch_selection(t, s, sl);
-        const uint32_t i = rg - sl.rg0;
-        out->nrows = sl.sel_off[i + 1] - sl.sel_off[i];
-        out->sel = sl.h_sel.p + sl.sel_off[i];
+        batch_selection(t, s, *hb);
+        const uint32_t i = rg - hb->rg0;
+        out->nrows = hb->sel_off[i + 1] - hb->sel_off[i];
+        out->sel = hb->h_sel.p + hb->sel_off[i];
     }
-    out->columns = sl.col_ptrs.data() + (size_t)(rg - sl.rg0) * ncols;
+    out->columns = hb->col_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
+    std::lock_guard<std::mutex> lk(s.mu);
+    s.out.emplace_back(rg, hb);
+    if (++hb->handed == hb->nrg) {
+        // a failed refill does not take this row group back: it is delivered,
+        // and the error surfaces at the next acquire
+        set_scan_error(s, enqueue_batch(t, s, d, si));
+    }
+    s.cv.notify_all();
     return 1;
 }
 
 int scan_release(fls_table *t, ScanCtx &s, uint32_t rg) {
     std::lock_guard<std::mutex> lk(s.mu);
-    int g = -1, si = -1;
-    if (!s.active || !find_slot(s, rg, g, si)) return fail(FLS_ERR_ARG, "row group %u is not held by this scan", rg);
-    ScanDev &d = s.devs[g];
-    Slot &sl = d.slots[si];
-    if (++sl.released < sl.nrg) return 0;
-    // every row group of the batch is back: reuse the slot for the next batch
-    sl.busy = false;
-    int rc = enqueue_batch(t, s, d, si);
+    auto it = std::find_if(s.out.begin(), s.out.end(), [&](const auto &o) { return o.first == rg; });
+    if (!s.active || it == s.out.end()) return fail(FLS_ERR_ARG, "row group %u is not held by this scan", rg);
+    HostBatch *hb = it->second;
+    s.out.erase(it);
+    if (++hb->released < hb->nrg) return 0;
+    // every row group of the batch is back: its host side returns to the pool,
+    // and a slot whose refill waited for one goes now
+    int rc = 0;
+    for (auto &d : s.devs) {
+        bool mine = false;
+        for (auto &b : d.batches) mine = mine || b.get() == hb;
+        if (!mine) continue;
+        d.free_batches.push_back(hb);
+        for (int si = 0; si < 2 && !rc; ++si)
+            if (d.slots[si].starved) {
+                rc = enqueue_batch(t, s, d, si);
+                set_scan_error(s, rc);
+            }
+        break;
+    }
     s.cv.notify_all();
     return rc;
 }
@@ -1423,6 +1527,15 @@ int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbyt
     if (dev_ptr) *dev_ptr = t->d_out[col].p;
     if (nbytes) *nbytes = t->res_rows * out_bytes_of(t, col);
     return 0;
+}
+
+int fls_device_heap(fls_table *t, uint32_t col, void **dev_ptr, const void **host_ptr, uint64_t *nbytes) {
+    if (!t || col >= t->d_out.size() || !t->d_out[col].p) return fail(FLS_ERR_ARG, "column %u not resident", col);
+    const bool has = col < t->shard.d_heap.size() && t->shard.d_heap[col].p;
+    if (dev_ptr) *dev_ptr = has ? t->shard.d_heap[col].p : nullptr;
+    if (host_ptr) *host_ptr = has ? t->shard.h_heap[col].p : nullptr;
+    if (nbytes) *nbytes = has ? t->shard.d_heap[col].n : 0;
+    return has ? 1 : 0;
 }
 
 int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, void *host_dst) {

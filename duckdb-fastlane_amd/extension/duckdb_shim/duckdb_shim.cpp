@@ -120,13 +120,47 @@ string Value::ToString() const {
 }
 
 Vector::Vector(LogicalType type, idx_t capacity)
-    : type_(std::move(type)), capacity_(capacity), data_(capacity * type_.PhysicalSize(), 0), valid_(capacity, true) {}
+    : type_(std::move(type)), capacity_(capacity), data_(capacity * type_.PhysicalSize(), 0),
+      data_ptr_(data_.data()), valid_(capacity, true) {}
 
+Vector::Vector(Vector &&o) noexcept
+    : type_(std::move(o.type_)), capacity_(o.capacity_), data_(std::move(o.data_)), auxiliary_(std::move(o.auxiliary_)),
+      valid_(std::move(o.valid_)), heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
+    // a moved std::vector keeps its storage, so an owned data pointer stays valid
+    data_ptr_ = o.data_ptr_;
+    o.data_ptr_ = nullptr;
+}
+
+// DataChunk::Reset -> Vector::ResetFromCache in DuckDB: back to the vector's
+// own buffer, dropping any foreign data pointer and its auxiliary holder
 void Vector::Reset() {
+    data_ptr_ = data_.data();
+    auxiliary_.reset();
     std::fill(valid_.begin(), valid_.end(), true);
     heap_.clear();
     keep_.clear();
     vtype_ = VectorType::FLAT_VECTOR;
+}
+
+void Vector::Reference(const Vector &o) {
+    type_ = o.type_;
+    valid_ = o.valid_;
+    vtype_ = o.vtype_;
+    if (o.auxiliary_) {  // foreign data kept alive by its holder: share it
+        data_ptr_ = o.data_ptr_;
+        auxiliary_ = o.auxiliary_;
+        return;
+    }
+    const size_t w = type_.PhysicalSize();
+    data_.assign(o.data_ptr_, o.data_ptr_ + o.capacity_ * w);
+    capacity_ = o.capacity_;
+    data_ptr_ = data_.data();
+    keep_ = o.keep_;
+    if (type_.id() == LogicalTypeId::VARCHAR) {  // strings of o's heap into this one's
+        string_t *sv = reinterpret_cast<string_t *>(data_ptr_);
+        for (idx_t i = 0; i < capacity_; ++i)
+            if (valid_[i] && sv[i].GetSize() > string_t::INLINE_LENGTH) sv[i] = AddString(sv[i].GetString());
+    }
 }
 
 string_t Vector::AddString(const string &s) {
@@ -142,7 +176,7 @@ void Vector::SetValue(idx_t i, const Value &v) {
         return;
     }
     valid_[i] = true;
-    uint8_t *p = data_.data() + i * type_.PhysicalSize();
+    uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     switch (type_.id()) {
     case LogicalTypeId::VARCHAR: {
         // implicit cast to VARCHAR, as DuckDB's Vector::SetValue does
@@ -161,7 +195,7 @@ void Vector::SetValue(idx_t i, const Value &v) {
 
 Value Vector::GetValue(idx_t i) const {
     if (!valid_[i]) return Value();
-    const uint8_t *p = data_.data() + i * type_.PhysicalSize();
+    const uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     auto ld = [p](auto x) { memcpy(&x, p, sizeof(x)); return x; };
     switch (type_.id()) {
     case LogicalTypeId::VARCHAR: return Value(ld(string_t()).GetString());

@@ -223,14 +223,46 @@ inline date_t Value::GetValue<date_t>() const { return date_t{(int32_t)int_}; }
 // ---- vectors ---------------------------------------------------------------
 enum class VectorType : uint8_t { FLAT_VECTOR, CONSTANT_VECTOR };
 
+// DuckDB v1.3.2 common/types/vector_buffer.hpp: a buffer a Vector can hold
+// on to.  OPAQUE_BUFFER subclasses keep foreign memory alive while a vector
+// points into it (FlatVector::SetData + Vector::SetAuxiliary, as the Arrow
+// scan does for zero-copy columns).
+enum class VectorBufferType : uint8_t { STANDARD_BUFFER, STRING_BUFFER, OPAQUE_BUFFER };
+class VectorBuffer {
+public:
+    explicit VectorBuffer(VectorBufferType type = VectorBufferType::STANDARD_BUFFER) : type_(type) {}
+    virtual ~VectorBuffer() = default;
+    VectorBufferType GetBufferType() const { return type_; }
+
+private:
+    VectorBufferType type_;
+};
+template <class T>
+using buffer_ptr = shared_ptr<T>;
+template <class T, class... Args>
+buffer_ptr<T> make_buffer(Args &&...args) {
+    return std::make_shared<T>(std::forward<Args>(args)...);
+}
+
 class Vector {
 public:
     explicit Vector(LogicalType type, idx_t capacity = STANDARD_VECTOR_SIZE);
+    Vector(Vector &&o) noexcept;
+    Vector(const Vector &) = delete;
+    Vector &operator=(const Vector &) = delete;
     const LogicalType &GetType() const { return type_; }
     void SetValue(idx_t index, const Value &val);
     Value GetValue(idx_t index) const;
-    data_ptr_t GetData() { return data_.data(); }
-    const uint8_t *GetData() const { return data_.data(); }
+    data_ptr_t GetData() { return data_ptr_; }
+    const uint8_t *GetData() const { return data_ptr_; }
+    // FlatVector::SetData: point the vector at memory it does not own (valid
+    // while the auxiliary buffer, or the caller, keeps it alive)
+    void SetDataPtr(data_ptr_t p) { data_ptr_ = p; }
+    void SetAuxiliary(buffer_ptr<VectorBuffer> b) { auxiliary_ = std::move(b); }
+    // Vector::Reference: share other's data (and the buffer keeping it alive);
+    // the shim's own storage is not shareable, so owned data is copied
+    void Reference(const Vector &other);
+    buffer_ptr<VectorBuffer> GetAuxiliary() const { return auxiliary_; }
     bool RowIsValid(idx_t i) const { return valid_[i]; }
     void SetValid(idx_t i, bool v) { valid_[i] = v; }
     void SetVectorType(VectorType t) { vtype_ = t; }
@@ -245,6 +277,8 @@ private:
     LogicalType type_;
     idx_t capacity_;
     vector<uint8_t> data_;
+    data_ptr_t data_ptr_;                 // data_.data(), or foreign memory (SetData)
+    buffer_ptr<VectorBuffer> auxiliary_;  // keeps foreign memory alive
     vector<bool> valid_;
     std::deque<string> heap_;
     vector<shared_ptr<void>> keep_;
@@ -254,6 +288,7 @@ private:
 struct FlatVector {
     template <class T>
     static T *GetData(Vector &v) { return reinterpret_cast<T *>(v.GetData()); }
+    static void SetData(Vector &v, data_ptr_t data) { v.SetDataPtr(data); }
     static void SetNull(Vector &v, idx_t i, bool is_null) { v.SetValid(i, !is_null); }
     static bool IsNull(const Vector &v, idx_t i) { return !v.RowIsValid(i); }
 };
@@ -278,6 +313,15 @@ public:
     void Reset() {
         for (auto &v : data) v.Reset();
         count_ = 0;
+    }
+    // DataChunk::Reference: this chunk's vectors reference other's
+    void Reference(const DataChunk &other) {
+        data.clear();
+        for (auto &v : other.data) {
+            data.emplace_back(v.GetType());
+            data.back().Reference(v);
+        }
+        count_ = other.count_;
     }
     vector<LogicalType> GetTypes() const {
         vector<LogicalType> t;

@@ -7,6 +7,7 @@
 // duckdb/ submodule is empty, .gitmodules:1-4).  SQL-level operators the
 // reference test uses (COUNT, LIMIT, LIKE, LENGTH) are applied by the tests on
 // the returned rows.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -516,6 +517,76 @@ extern "C" int fls_ext_scan_count_where(fls_ext_db *d, const char *fn, const cha
     }
 }
 
+// DataChunk delivery rate: the scan through the executor with a sink that
+// only counts rows (no checksum, no copy), i.e. what the table function itself
+// costs a DuckDB pipeline.
+extern "C" int fls_ext_scan_rows(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
+                                 int nthreads, uint64_t *rows, double *seconds) {
+    try {
+        const char *args[1] = {path};
+        Query q = make_query(d, fn, args, 1, 0);
+        std::vector<std::string> names;
+        std::vector<LogicalType> types;
+        std::vector<int> pv(proj, proj + (proj ? nproj : 0));
+        std::atomic<uint64_t> n{0};
+        auto t0 = std::chrono::steady_clock::now();
+        execute(d, q, pv, -1, names, types, [&](idx_t, DataChunk &, const std::vector<size_t> &, idx_t cnt) {
+            n += cnt;
+        }, nthreads);
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        *rows = n;
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+// The scan with a sink that KEEPS a reference to every chunk it receives
+// (DataChunk::Reference, as an operator that buffers its input would) and
+// hashes them all only after the scan has ended: zero-copy vectors must stay
+// valid while referenced, whatever the engine recycled meanwhile (ADVICE r1:
+// FSST strings pointing into a recycled batch heap).  Same checksum as
+// fls_ext_scan_count.
+extern "C" int fls_ext_scan_hold(fls_ext_db *d, const char *fn, const char *path, int nthreads, uint64_t *rows,
+                                 uint64_t *checksum, double *seconds) {
+    try {
+        const char *args[1] = {path};
+        Query q = make_query(d, fn, args, 1, 0);
+        std::vector<std::string> names;
+        std::vector<LogicalType> types;
+        std::mutex mu;
+        std::map<idx_t, std::vector<std::pair<std::unique_ptr<DataChunk>, idx_t>>> held;
+        std::vector<size_t> pick0;
+        auto t0 = std::chrono::steady_clock::now();
+        execute(d, q, {}, -1, names, types, [&](idx_t batch, DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+            auto h = std::make_unique<DataChunk>();
+            h->Reference(c);
+            std::lock_guard<std::mutex> g(mu);
+            pick0 = pick;
+            held[batch].emplace_back(std::move(h), cnt);
+        }, nthreads);
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        uint64_t n = 0;
+        std::vector<uint64_t> acc(names.size(), 0);
+        for (auto &b : held)
+            for (auto &ch : b.second) {
+                ChunkHash hc = hash_chunk(*ch.first, pick0, ch.second);
+                const uint64_t pw = upow(kPoly, n);
+                for (size_t j = 0; j < acc.size(); ++j) acc[j] += pw * hc.col[j];
+                n += hc.n;
+            }
+        uint64_t h = 1469598103934665603ull;
+        for (uint64_t x : acc) h = (h ^ x) * 1099511628211ull;
+        *rows = n;
+        *checksum = (h ^ n) * 1099511628211ull;
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 extern "C" int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *path, const int *proj, int nproj,
                                   uint64_t *rows, uint64_t *checksum, double *seconds) {
     return fls_ext_scan_count_mt(d, fn, path, proj, nproj, 1, rows, checksum, seconds);
@@ -588,6 +659,63 @@ int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj
         if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
         cf.copy_to_finalize(d->ctx, *bind, *gstate);
         if (rows) *rows = n;
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+// COPY (SELECT * FROM (VALUES ...) t(names)) TO dst (FORMAT format): literal
+// rows, cells[row * ncols + col] as text or NULL for SQL NULL, in one chunk per
+// STANDARD_VECTOR_SIZE rows.  Types: INTEGER, BIGINT, DOUBLE, VARCHAR.
+int fls_ext_copy_values(fls_ext_db *d, const char *format, const char *dst, int ncols, const char *const *names,
+                        const char *const *type_names, int64_t nrows, const char *const *cells, uint64_t *rows) {
+    try {
+        const std::string fmt = StringUtil::Lower(format ? format : "");
+        auto it = d->db.copy_functions.find(fmt);
+        if (it == d->db.copy_functions.end())
+            throw CatalogException("Copy Function with name " + fmt + " does not exist!");
+        CopyFunction &cf = it->second;
+        vector<string> cn;
+        vector<LogicalType> ct;
+        for (int c = 0; c < ncols; ++c) {
+            const std::string tn = StringUtil::Upper(type_names[c]);
+            cn.emplace_back(names[c]);
+            if (tn == "INTEGER") ct.push_back(LogicalType::INTEGER);
+            else if (tn == "BIGINT") ct.push_back(LogicalType::BIGINT);
+            else if (tn == "DOUBLE") ct.push_back(LogicalType::DOUBLE);
+            else if (tn == "VARCHAR") ct.push_back(LogicalType::VARCHAR);
+            else throw BinderException("harness: unsupported VALUES type " + tn);
+        }
+        CopyInfo info;
+        CopyFunctionBindInput cbin{info};
+        auto bind = cf.copy_to_bind(d->ctx, cbin, cn, ct);
+        auto gstate = cf.copy_to_initialize_global(d->ctx, *bind, dst ? dst : "");
+        ExecutionContext ectx(d->ctx);
+        auto lstate = cf.copy_to_initialize_local(ectx, *bind);
+        DataChunk chunk;
+        chunk.Initialize(ct);
+        for (int64_t r0 = 0; r0 < nrows; r0 += STANDARD_VECTOR_SIZE) {
+            const idx_t n = (idx_t)std::min<int64_t>(STANDARD_VECTOR_SIZE, nrows - r0);
+            chunk.Reset();
+            for (int c = 0; c < ncols; ++c)
+                for (idx_t i = 0; i < n; ++i) {
+                    const char *x = cells[(r0 + (int64_t)i) * ncols + c];
+                    Value v;
+                    if (!x) v = Value();
+                    else if (ct[c].id() == LogicalTypeId::INTEGER) v = Value::INTEGER(std::atoi(x));
+                    else if (ct[c].id() == LogicalTypeId::BIGINT) v = Value::BIGINT(std::atoll(x));
+                    else if (ct[c].id() == LogicalTypeId::DOUBLE) v = Value::DOUBLE(std::atof(x));
+                    else v = Value(std::string(x));
+                    chunk.data[c].SetValue(i, v);
+                }
+            chunk.SetCardinality(n);
+            cf.copy_to_sink(ectx, *bind, *gstate, *lstate, chunk);
+        }
+        if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
+        cf.copy_to_finalize(d->ctx, *bind, *gstate);
+        if (rows) *rows = (uint64_t)nrows;
         return 0;
     } catch (const std::exception &e) {
         g_err = e.what();

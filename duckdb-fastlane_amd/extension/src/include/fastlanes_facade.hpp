@@ -48,6 +48,9 @@ public:
     bool finalizeFile();
 
     bool isValid() const;
+    // Not in the reference's header: why the last writeChunk returned false
+    // (empty when no reason was recorded), for COPY's error message.
+    const std::string &lastError() const;
 };
 
 }  // namespace ext_fastlane

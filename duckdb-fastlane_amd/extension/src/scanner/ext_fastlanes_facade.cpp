@@ -32,7 +32,9 @@ public:
     // write side
     fls_writer *writer = nullptr;
     std::string out_path;
+    std::string error;                               // why the last call returned false (lastError)
     std::vector<LogicalType> wtypes;
+    std::vector<std::string> wnames;
     std::vector<std::vector<uint8_t>> wcols;         // fixed-width buffered rows
     std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
     idx_t wrows = 0;
@@ -136,6 +138,8 @@ bool FastLanesFacade::readNextChunk(std::vector<Value> &values, idx_t &rows_read
 
 void FastLanesFacade::closeFile() { pImpl->close_read(); }
 
+const std::string &FastLanesFacade::lastError() const { return pImpl->error; }
+
 bool FastLanesFacade::isValid() const { return pImpl->table != nullptr || pImpl->writer != nullptr; }
 
 // ---- write path ------------------------------------------------------------
@@ -157,6 +161,7 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     }
     s.out_path = file_path;
     s.wtypes = types;
+    s.wnames = names;
     s.wcols.assign(types.size(), {});
     s.woffs.assign(types.size(), {0});
     s.wrows = 0;
@@ -190,6 +195,15 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     Impl &s = *pImpl;
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
     chunk.Flatten();
+    // The container has no validity bitmap yet: a NULL would come back as 0 or
+    // '' and a pushed-down IS NULL would match nothing, so refuse it instead of
+    // writing a value (nothing of this chunk is appended).
+    for (size_t c = 0; c < s.wtypes.size(); ++c)
+        for (idx_t r = 0; r < chunk.size(); ++r)
+            if (FlatVector::IsNull(chunk.data[c], r)) {
+                s.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
+                return false;
+            }
     // column-major: append each column's slice up to the row-group boundary
     // in bulk, then let the writer encode the full row group (column-parallel)
     idx_t r0 = 0;
@@ -202,8 +216,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             if (t.id() == LogicalTypeId::VARCHAR) {
                 const string_t *str = FlatVector::GetData<string_t>(v);
                 for (idx_t r = r0; r < r0 + n; ++r) {
-                    if (!FlatVector::IsNull(v, r))  // NULLs have no encoding on this path: empty string
-                        col.insert(col.end(), str[r].GetData(), str[r].GetData() + str[r].GetSize());
+                    col.insert(col.end(), str[r].GetData(), str[r].GetData() + str[r].GetSize());
                     s.woffs[c].push_back((uint32_t)col.size());
                 }
                 continue;
@@ -223,8 +236,6 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                     memcpy(dst + 8 * i, &x, 8);
                 }
             }
-            for (idx_t i = 0; i < n; ++i)  // NULLs: zero bytes
-                if (FlatVector::IsNull(v, r0 + i)) memset(dst + i * w, 0, w);
         }
         s.wrows += n;
         r0 += n;

@@ -5,13 +5,17 @@
 // projected columns are uploaded, decoded and copied back.  Scan is parallel
 // (the reference pins MaxThreads to 1, src/scanner/scan_fastlanes.cpp:43-45):
 // each DuckDB thread claims whole row groups from fls_scan_acquire
-// (GPU-sharded, decoded ahead into pinned host memory), fills
-// STANDARD_VECTOR_SIZE-row DataChunks by memcpy of DuckDB's physical layouts
-// and hands the row group back with fls_scan_release.  The batch index is the
-// row group's position over all files, so DuckDB restores file order.
-// string_t records point into the file image, kept alive by every thread that
-// holds one of its row groups.  Error texts follow
-// src/scanner/scan_fastlanes.cpp:62-97.
+// (GPU-sharded, decoded ahead into pinned host memory) and emits
+// STANDARD_VECTOR_SIZE-row DataChunks that REFERENCE the pinned row-group
+// buffers (FlatVector::SetData, zero-copy: the decoded columns are already in
+// DuckDB's physical layouts).  Each vector carries a RowGroupPin as its
+// auxiliary buffer; the row group goes back to the engine (fls_scan_release)
+// when the last vector referencing it is reset, so a chunk DuckDB keeps past
+// the Scan call stays valid.  string_t records point into the file image
+// (DICT) or the batch's pinned FSST heap, both kept alive by the same pin.
+// DECIMAL(w<=9) columns are narrowed from the engine's int64 by a copy.  The
+// batch index is the row group's position over all files, so DuckDB restores
+// file order.  Error texts follow src/scanner/scan_fastlanes.cpp:62-97.
 #include <glob.h>
 
 #include <algorithm>
@@ -77,15 +81,24 @@ struct ReadGlobalState : public GlobalTableFunctionState {
     idx_t MaxThreads() const override { return std::max<idx_t>(1, total_rowgroups); }
 };
 
+// A delivered row group's pinned buffers, held by the local state while it
+// emits chunks and by every vector that references them.  The last holder
+// hands the row group back to the engine, which then recycles its batch slot.
+// A failed release (a batch refill that could not be enqueued) is sticky in
+// the engine: the next fls_scan_acquire reports it as an IOException.
+struct RowGroupPin : public VectorBuffer {
+    std::shared_ptr<OpenTable> table;    // keeps the file (DICT string_t targets) open
+    uint32_t rowgroup;
+    RowGroupPin(std::shared_ptr<OpenTable> t, uint32_t rg)
+        : VectorBuffer(VectorBufferType::OPAQUE_BUFFER), table(std::move(t)), rowgroup(rg) {}
+    ~RowGroupPin() override { fls_scan_release(table->table, rowgroup); }
+};
+
 struct ReadLocalState : public LocalTableFunctionState {
-    std::shared_ptr<OpenTable> table;    // keeps the file (and its string_t targets) alive
+    buffer_ptr<RowGroupPin> pin;         // the row group being emitted (nullptr: none)
     fls_rowgroup rg{};
-    bool have_rg = false;
     idx_t rg_pos = 0;
     idx_t batch_index = 0;
-    ~ReadLocalState() override {
-        if (have_rg) fls_scan_release(table->table, rg.rowgroup);
-    }
 };
 
 void CollectPaths(const Value &v, vector<string> &files, const char *fn) {
@@ -290,12 +303,7 @@ unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &, TableFunct
 // give back the local state's row group and claim the next one (in file and
 // row-group order over all threads); false at the end of all files
 bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &l) {
-    if (l.have_rg) {
-        l.have_rg = false;
-        if (fls_scan_release(l.table->table, l.rg.rowgroup) != 0)
-            throw IOException(string("FastLanes scan failed: ") + fls_last_error());
-    }
-    l.table.reset();
+    l.pin.reset();  // released now unless a chunk DuckDB still holds references it
     std::lock_guard<std::mutex> guard(g.lock);
     while (true) {
         if (!g.cur) {
@@ -310,8 +318,7 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
         const int rc = fls_scan_acquire(g.cur->table, &l.rg);
         if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
         if (rc == 1) {
-            l.table = g.cur;
-            l.have_rg = true;
+            l.pin = make_buffer<RowGroupPin>(g.cur, l.rg.rowgroup);
             l.rg_pos = 0;
             l.batch_index = g.rg_base[g.file_idx] + l.rg.rowgroup;
             return true;
@@ -327,7 +334,7 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
     auto &l = data.local_state->Cast<ReadLocalState>();
     output.Reset();
     // (a filtered row group can deliver no rows)
-    while (!(l.have_rg && l.rg_pos < l.rg.nrows)) {
+    while (!(l.pin && l.rg_pos < l.rg.nrows)) {
         if (!NextRowGroup(bind, g, l)) {
             output.SetCardinality(0);
             return;
@@ -346,8 +353,9 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
         const idx_t ob = bind.cols[id].out_bytes;
         const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
         const idx_t phys = vec.GetType().PhysicalSize();
-        if (phys == ob) {
-            memcpy(vec.GetData(), src, n * ob);
+        if (phys == ob) {  // zero-copy: reference the pinned row group
+            FlatVector::SetData(vec, (data_ptr_t)src);
+            vec.SetAuxiliary(l.pin);
         } else {  // DECIMAL(w<=9): the int64 scaled value narrowed to DuckDB's physical width
             const int64_t *v = (const int64_t *)src;
             if (phys == 4) {

@@ -88,7 +88,10 @@ unique_ptr<LocalFunctionData> CopyInitLocal(ExecutionContext &, FunctionData &) 
 void CopySink(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, LocalFunctionData &, DataChunk &input) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
     std::lock_guard<std::mutex> guard(g.lock);
-    if (!g.facade->writeChunk(input)) throw IOException("Failed to write chunk to FastLanes");
+    if (!g.facade->writeChunk(input)) {
+        const std::string &why = g.facade->lastError();
+        throw IOException("Failed to write chunk to FastLanes" + (why.empty() ? std::string() : ": " + why));
+    }
 }
 
 void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &) {}

@@ -167,9 +167,13 @@ int fls_rowgroup_may_match(const fls_table *t, uint32_t rg, const fls_predicate 
 
 /* Thread-safe form for parallel consumers: claims the next row group in order
  * (1 = delivered, 0 = end, <0 = error); its buffers stay valid until
- * fls_scan_release(t, out->rowgroup).  A consumer must release what it holds
- * before acquiring again (a decoded batch is recycled only when all of its
- * row groups are back).  Do not mix with fls_scan_next on one scan. */
+ * fls_scan_release(t, out->rowgroup), so a consumer may keep several row
+ * groups (DuckDB vectors referencing the pinned columns, zero-copy).  A GPU's
+ * batch slot is refilled as soon as every row group of its batch has been
+ * handed out; the pinned host side of a batch goes back to a per-GPU pool when
+ * its last row group is released (pool cap FLS_SCAN_HOST_BATCHES, default 64;
+ * at the cap a refill waits for a release).  A failed refill is sticky: every
+ * later acquire returns its error.  Do not mix with fls_scan_next on one scan. */
 int fls_scan_acquire(fls_table *t, fls_rowgroup *out);
 int fls_scan_release(fls_table *t, uint32_t rowgroup);
 
@@ -185,6 +189,11 @@ int fls_device_decode(fls_table *t, const uint8_t *col_mask);
 int fls_device_sync(fls_table *t, fls_decode_stats *stats);
 /* HBM address and byte size of a resident output column. */
 int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbytes);
+/* String heap of a resident FSST (free-text) VARCHAR column: its HBM address,
+ * the host address the column's string_t pointers are based on (the heap's
+ * host copy, filled by fls_device_copy_out) and its size.  Returns 1, or 0
+ * (pointers NULL) for a column without one. */
+int fls_device_heap(fls_table *t, uint32_t col, void **dev_ptr, const void **host_ptr, uint64_t *nbytes);
 /* Copy rows [row, row+n) (relative to the first resident row) of a decoded
  * column into host memory. */
 int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, void *host_dst);

@@ -129,3 +129,52 @@ class Ext:
         if rc != 0:
             raise ExtError(lib.fls_ext_last_error().decode())
         return rows.value
+
+    def copy_values(self, columns, dst, fmt="fls"):
+        """COPY (SELECT * FROM (VALUES ...)) TO dst (FORMAT fmt): columns =
+        [(name, "INTEGER" | "BIGINT" | "DOUBLE" | "VARCHAR", [values, None = NULL])]."""
+        lib = self.lib
+        lib.fls_ext_copy_values.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p),
+                                            C.POINTER(C.c_char_p), C.c_int64, C.POINTER(C.c_char_p),
+                                            C.POINTER(C.c_uint64)]
+        nc = len(columns)
+        nr = len(columns[0][2]) if columns else 0
+        names = (C.c_char_p * nc)(*[c[0].encode() for c in columns])
+        types = (C.c_char_p * nc)(*[c[1].encode() for c in columns])
+        cells = (C.c_char_p * max(1, nc * nr))()
+        for r in range(nr):
+            for j, c in enumerate(columns):
+                v = c[2][r]
+                cells[r * nc + j] = None if v is None else str(v).encode()
+        rows = C.c_uint64()
+        rc = lib.fls_ext_copy_values(self.db, fmt.encode(), str(dst).encode(), nc, names, types, nr, cells,
+                                     C.byref(rows))
+        if rc != 0:
+            raise ExtError(lib.fls_ext_last_error().decode())
+        return rows.value
+
+    def scan_rows(self, fn, path, proj=None, threads=1):
+        """DataChunk delivery only (a sink that counts rows): (rows, seconds)."""
+        lib = self.lib
+        lib.fls_ext_scan_rows.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.c_int, C.c_int,
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        p = (C.c_int * len(proj))(*proj) if proj else None
+        rows, sec = C.c_uint64(), C.c_double()
+        rc = lib.fls_ext_scan_rows(self.db, fn.encode(), str(path).encode(), p, len(proj) if proj else 0, threads,
+                                   C.byref(rows), C.byref(sec))
+        if rc != 0:
+            raise ExtError(lib.fls_ext_last_error().decode())
+        return rows.value, sec.value
+
+    def scan_hold(self, fn, path, threads=1):
+        """Scan keeping a reference to every chunk until the end, then hash
+        them (same checksum as scan_count): (rows, checksum, seconds)."""
+        lib = self.lib
+        lib.fls_ext_scan_hold.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        rows, h, sec = C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = lib.fls_ext_scan_hold(self.db, fn.encode(), str(path).encode(), threads, C.byref(rows), C.byref(h),
+                                   C.byref(sec))
+        if rc != 0:
+            raise ExtError(lib.fls_ext_last_error().decode())
+        return rows.value, h.value, sec.value

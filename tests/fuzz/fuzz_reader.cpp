@@ -11,6 +11,7 @@
 // Any out-of-bounds read aborts the process (-fno-sanitize-recover).
 //
 //   fuzz_reader <image.fls> <iterations> <seed>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -96,6 +97,39 @@ int main(int argc, char **argv) {
             hot.push_back(c.off + c.hdr.meta_off);
             hot.push_back(c.off + c.hdr.aux_off);
         }
+    // targeted u64 wrap-around cases: offsets chosen so that
+    // `a + b > lim` checks would wrap and accept an image whose streams start
+    // before the chunk; every one must be rejected
+    long wrap_cases = 0;
+    for (auto &rg : base.rgs)
+        for (auto &c : rg.chunks) {
+            const ChunkHeader &h = c.hdr;
+            auto reject = [&](uint64_t at, uint64_t val, const char *what) {
+                std::vector<uint8_t> img = orig;
+                memcpy(img.data() + at, &val, 8);
+                FileMeta m;
+                ++wrap_cases;
+                if (parse_file(img.data(), img.size(), m).empty()) {
+                    fprintf(stderr, "wrap case accepted: %s = 0x%llx at %llu\n", what, (unsigned long long)val,
+                            (unsigned long long)at);
+                    exit(3);
+                }
+            };
+            const uint64_t hm = c.off + offsetof(ChunkHeader, meta_off);
+            reject(hm, ~0ull - 31, "meta_off");
+            reject(c.off + offsetof(ChunkHeader, aux_off), ~0ull - 15, "aux_off");
+            reject(c.off + offsetof(ChunkHeader, aux_len), ~0ull - 15, "aux_len");
+            for (uint32_t v = 0; v < h.nvec; ++v) {
+                const uint64_t vo = c.off + h.meta_off + 32ull * v;
+                VecMeta vm;
+                memcpy(&vm, orig.data() + vo, 32);
+                reject(vo + offsetof(VecMeta, packed_off), (uint64_t)0 - (h.packed_off + 128ull * vm.bw), "vm.packed_off");
+                reject(vo + offsetof(VecMeta, packed_off), ~0ull - 15, "vm.packed_off");
+                if (h.enc == ENC_DELTA || h.enc == ENC_RLE || h.enc == ENC_FSST ||
+                    (h.enc == ENC_ALP && alp_exceptions(vm.aux_count)))
+                    reject(vo + offsetof(VecMeta, aux_off), (uint64_t)0 - 128, "vm.aux_off");
+            }
+        }
     uint64_t foot;
     memcpy(&foot, orig.data() + orig.size() - 16, 8);
     long accepted = 0;
@@ -135,6 +169,7 @@ int main(int argc, char **argv) {
             walk(img, m);
         }
     }
-    printf("iterations %ld accepted %ld sink %llu\n", iters, accepted, (unsigned long long)(g_sink & 0xFF));
+    printf("iterations %ld accepted %ld wrap_cases %ld sink %llu\n", iters, accepted, wrap_cases,
+           (unsigned long long)(g_sink & 0xFF));
     return 0;
 }

@@ -82,3 +82,29 @@ def test_copy_projected_to_fls(fl, ext, gpu, li_file, tmpfile):
     assert [int(r[1]) for r in rows[::101]] == okey[::101].tolist()
     # replacement scan on the new file, FROM 'proj.fls'
     assert ext.query(None, dst, limit=3)[2] == rows[:3]
+
+
+def test_copy_refuses_null_values(ext, tmpfile):
+    """COPY (SELECT NULL::INT ...) TO 'x.fls': the container has no validity
+    bitmap, so a NULL must fail the COPY with a clear message rather than be
+    written as 0 / '' (ADVICE r1).  CPU only: the writer runs on the host."""
+    for cols in ([("a", "INTEGER", [1, None, 3])],
+                 [("a", "BIGINT", [1, 2, 3]), ("s", "VARCHAR", ["x", "y", None])],
+                 [("d", "DOUBLE", [None])]):
+        with pytest.raises(ExtError, match='^Failed to write chunk to FastLanes: column "[ads]" holds NULL values'):
+            ext.copy_values(cols, tmpfile("nulls.fls"))
+
+
+def test_copy_values_roundtrip_cpu(ext, ref, tmpfile):
+    """The same VALUES source without NULLs writes a file whose oracle decode
+    (oracle/flsref.c) returns the values: 5000 rows over two chunks-worth of
+    STANDARD_VECTOR_SIZE and a partial vector."""
+    n = 5000
+    a = [(i * 7919) % 100003 - 50000 for i in range(n)]
+    s = [f"s{i % 13}" * (i % 5) for i in range(n)]
+    dst = tmpfile("vals.fls")
+    assert ext.copy_values([("a", "INTEGER", a), ("s", "VARCHAR", s)], dst) == n
+    rf = ref.RefFile(open(dst, "rb").read())
+    assert rf.nrows == n
+    assert rf.decode(0, 0).view(np.int32).tolist() == a
+    assert rf.strings_column(1) == [x.encode() for x in s]

@@ -217,3 +217,36 @@ def test_read_fastlanes_empty_file(fl, ext, tmpfile):
     assert ext.scan_count("read_fastlanes", p)[0] == 0
     _, _, rows = ext.query("read_fastlanes", p, p, as_list=True)
     assert rows == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 4])
+def test_read_fastlanes_zero_copy_chunks_stay_valid_when_held(fl, ext, gpu, tmpfile, monkeypatch, threads):
+    """read_fastlanes hands DuckDB vectors that reference the engine's pinned
+    row-group buffers (FlatVector::SetData + a RowGroupPin auxiliary).  A sink
+    that keeps a reference to EVERY chunk and hashes them only after the scan
+    has recycled every batch slot must see the same bytes as one that hashes
+    them on arrival -- including l_comment (FSST), whose string_t records point
+    into the batch's pinned heap (strings overwritten by a reused
+    slot).  One row group per batch maximises slot reuse."""
+    monkeypatch.setenv("FLS_SCAN_BATCH", "1")
+    p = tmpfile("lif.fls")
+    fl.gen_image("lineitem_full", 0.1).write(p)    # 10 row groups, 16 columns
+    rows, h_live, _ = ext.scan_count("read_fastlanes", p, threads=threads)
+    rows2, h_held, _ = ext.scan_hold("read_fastlanes", p, threads=threads)
+    assert rows == rows2 == 600572 and h_held == h_live
+    # the held bytes are the generator's (l_comment sample)
+    _, _, got = ext.query("read_fastlanes", p, proj=[15], limit=5000)
+    assert [r[0].encode() for r in got] == fl.gen_strings("lineitem_full", 15, 0, 5000, 0.1)
+
+
+@pytest.mark.gpu
+def test_read_fastlanes_delivery_rate_zero_copy(fl, ext, gpu, tmpfile):
+    """DataChunk delivery without a checksum sink: reports rows/s at 1 and 8
+    threads (the engine scan into pinned memory bounds it)."""
+    p = tmpfile("li1.fls")
+    fl.gen_image("lineitem", 1.0).write(p)
+    for th in (1, 8):
+        n, sec = ext.scan_rows("read_fastlanes", p, threads=th)
+        assert n == 6001215
+        print(f"read_fastlanes zero-copy DataChunks SF1, {th} threads: {n / sec / 1e6:.1f} M rows/s")

@@ -48,3 +48,30 @@ def test_lineitem_sf10_bit_exact_and_idempotent(fl, gpu):
     st2 = t.device_sync()
     assert st2.timed_launches == 3
     assert fl.check_device_table(t, "lineitem", 10.0) == [0] * 15
+
+
+@pytest.mark.parametrize("wl", ["lineitem_full", "lineitem_dbl"])
+def test_lineitem_variants_sf1_bit_exact(fl, gpu, wl):
+    """All 16 columns (l_comment FSST: length, inline bytes / prefix and every
+    heap byte vs the text pool) and the ALP-encoded DOUBLE variant (IEEE bits
+    of cents / 100.0), checked on the GPU over every row; the l_comment check
+    must catch a single flipped heap byte."""
+    img = fl.gen_image(wl, 1.0)
+    t, st = _decode(fl, img)
+    assert t.nrows == 6001215
+    mism = fl.check_device_table(t, wl, 1.0)
+    assert mism == [0] * t.ncols
+    if wl == "lineitem_full":
+        import ctypes
+        dp, hp, hn = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        assert fl.lib.fls_device_heap(t.h, 15, ctypes.byref(dp), ctypes.byref(hp), ctypes.byref(hn)) == 1
+        rec = t.device_copy_out(15, 0, 64).reshape(-1, 16)
+        i = next(k for k in range(64) if int(rec[k, :4].view(np.uint32)[0]) > 12)
+        ptr = int(rec[i, 8:16].copy().view(np.uint64)[0])
+        at = ctypes.c_void_p(ptr + 5 + dp.value - hp.value)     # a byte past the 4-byte prefix
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        b = (ctypes.c_uint8 * 1)()
+        assert hip.hipMemcpy(b, at, 1, 2) == 0
+        b[0] ^= 0x20
+        assert hip.hipMemcpy(at, b, 1, 1) == 0
+        assert fl.check_device_table(t, wl, 1.0)[15] == 1
