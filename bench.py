@@ -2,24 +2,35 @@
 """bench.py -- decoded values/s + achieved HBM GB/s of the MI355X FastLanes scan.
 
 Metric (BASELINE.json): "decoded values/sec + achieved HBM GB/s, TPC-H SF100
-lineitem scan at 1/2/4/8 GPU".  A step is ONE fused decode launch over every
+lineitem scan at 1/2/4/8 GPU".  A step is ONE decode launch over every
 resident vector of every column of this rank's row-group shard (compressed
-input resident in HBM, decoded columns written to HBM).  Row groups are sharded
-contiguously over ranks with no data-path collective; the
-torch.distributed barrier / MAX reduction only brackets the timing.
+input resident in HBM, decoded columns written to HBM): the fused
+decode_kernel plus, for l_comment, the FSST kernel overlapped with it.  The
+default workload is the full 16-column lineitem (l_comment FSST-compressed).
+Row groups are sharded contiguously over ranks with no data-path collective
+(SURVEY.md 8(e)); torch.distributed only brackets the timing (barrier, MAX of
+times, SUM of values) and reduces the per-rank verification.
 
-N=1 workload = the metric's own configuration (SF100 fits one GPU: ~11 GB
-compressed + ~77 GB decoded).  Inputs are synthetic (seeded TPC-H-like
-generator, fls_gen.hpp) and encoded by this repo's CPU writer before timing.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lineitem_full]
+                    [--scale 100] [--cpu-seconds 10] [--e2e-scale 10]
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lineitem]
-                    [--scale 100] [--cpu-seconds 10]
+--gpus N without a torch.distributed launcher starts N ranks itself (one
+process per GPU, before this process touches a GPU); under torchrun the
+launcher's RANK / LOCAL_RANK / WORLD_SIZE are used.  Every rank checks every
+decoded value of its shard on its GPU against the seeded generator
+(libflscheck.so) after the timed region.  Rank 0 of a 1-GPU run also times
+the CPU baseline (a FastLanes-shaped CPU decoder, oracle/flsfast.cpp, on the
+host's cores) and the end-to-end rates into pinned host memory / DuckDB
+DataChunks, which are never `value`.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -29,25 +40,35 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+PCIE_GBS = 63.0         # PCIe Gen5 x16 per GPU, spec (MI355X_MICROARCH.md)
+WORKLOADS = ["lineitem_full", "lineitem", "lineitem_dbl", "c1", "c3", "c4"]
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="lineitem",
-                   choices=["lineitem", "c1", "c3", "c4", "lineitem_full", "lineitem_dbl"])
+    p.add_argument("--workload", default="lineitem_full", choices=WORKLOADS)
     p.add_argument("--scale", type=float, default=100.0, help="lineitem scale factor")
     p.add_argument("--rows", type=int, default=0, help="row override (c1/c3/c4; 0 = config default)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
-    p.add_argument("--threads", type=int, default=0, help="host threads for encode / CPU baseline")
-    p.add_argument("--verify-rowgroups", type=int, default=3)
+    p.add_argument("--e2e-scale", type=float, default=10.0,
+                   help="scale of the end-to-end (pinned host / DataChunk) measurement (0 = skip)")
+    p.add_argument("--threads", type=int, default=0, help="host threads for encode / CPU baseline (0 = host cores)")
+    p.add_argument("--no-verify", action="store_true", help="skip the full-shard GPU check")
     p.add_argument("--no-traffic", action="store_true",
                    help="skip the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return p.parse_args()
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher rehearsal on CPU: ranks, shards and the cross-rank reduction over gloo; "
+                        "no GPU, no decode (tests/test_bench_launcher.py)")
+    return p.parse_args(argv)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
 
 
 def shard_range(nrg: int, rank: int, world: int):
@@ -56,6 +77,81 @@ def shard_range(nrg: int, rank: int, world: int):
     return nrg * rank // world, nrg * (rank + 1) // world
 
 
+# ---- host CPU facts ---------------------------------------------------------
+def cgroup_cpu_quota() -> float | None:
+    """CPUs the cgroup may use (cpu.max quota / period), None if unlimited."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    try:  # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cores() -> dict:
+    """The CPUs this process may run on: its affinity mask, capped by the
+    cgroup CPU quota (the GPU box gives each GPU a quota of host cores)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    usable = aff if quota is None else max(1, min(aff, math.floor(quota + 1e-9)))
+    return {"usable": usable, "affinity": aff, "cgroup_quota": quota, "model": cpu_model()}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads(args, world_local: int = 1) -> int:
+    if args.threads:
+        return args.threads
+    return max(1, host_cores()["usable"] // max(1, world_local))
+
+
+# ---- launcher ---------------------------------------------------------------
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base_env: dict) -> list[dict]:
+    """Environment of each of n ranks started by this script (one per GPU)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        envs.append(e)
+    return envs
+
+
+def launch(args, argv) -> int:
+    """--gpus N with no launcher: start N fresh ranks of this script before any
+    GPU call here, wait for all of them, exit with the worst status.  Rank 0
+    prints the JSON line."""
+    envs = rank_envs(args.gpus, free_port(), os.environ)
+    procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + list(argv), env=e) for e in envs]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return max(bad, key=abs) if bad else 0
+
+
+# ---- measurement pieces -----------------------------------------------------
 def measure_traffic(args):
     """HBM bytes per decode launch from rocprofv3 PMC counters, each counter in
     its own pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950).
@@ -64,7 +160,6 @@ def measure_traffic(args):
     reports half the bytes of 16 B/lane streaming reads -> x2."""
     import csv
     import shutil
-    import subprocess
     import tempfile
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
@@ -74,7 +169,7 @@ def measure_traffic(args):
         cmd = ["rocprofv3", "--pmc", ctr, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
                sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--steps", "2", "--warmup", "1",
                "--workload", args.workload, "--scale", str(args.scale), "--rows", str(args.rows),
-               "--cpu-seconds", "0", "--verify-rowgroups", "0", "--no-traffic"]
+               "--cpu-seconds", "0", "--e2e-scale", "0", "--no-verify", "--no-traffic"]
         try:
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
         except Exception as e:  # noqa: BLE001 - report, never fail the bench on profiling
@@ -99,112 +194,179 @@ def measure_traffic(args):
         f"WRITE_SIZE {vals['WRITE_SIZE'] / 1e9:.3f} GB"
 
 
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
-
-
-def host_threads(args) -> int:
-    if args.threads:
-        return args.threads
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit():
-        return max(1, int(env))
-    return max(1, min(16, os.cpu_count() or 1))
-
-
-def cpu_model() -> str:
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
-
-
-def cpu_baseline(fl, args, nthreads: int, nrows_total: int):
-    """Oracle (CPU restatement, 'port') on a bounded sample of the same workload."""
-    from oracle import flsref
+def cpu_baseline(fl, args, nthreads: int, nrows_total: int, cores: dict):
+    """FastLanes-shaped CPU decoder (oracle/flsfast.cpp: width-specialised
+    lane loops, FFOR / DELTA / DICT / RLE / ALP fused per vector, FSST's
+    classic decoder) on a bounded sample of the same workload, all usable host
+    cores, output buffers the size of the sample (several GB, well beyond the
+    host's L3) reused across passes, as the GPU reuses its HBM columns."""
+    from oracle import flsfast, flsref
     nrg_total = (nrows_total + 65535) // 65536
-    sample_rg = min(nrg_total, 128)
+    sample_rg = min(nrg_total, 512)
     img = fl.gen_image(args.workload, args.scale, args.rows, 0, sample_rg, nthreads)
     rf = flsref.RefFile(img)
-    vals_per_pass = rf.nrows * rf.ncols
-    fsst = {c for c in range(rf.ncols) if rf.column(c)[1] == fl.VARCHAR and fl.gen_dict_string(args.workload, c, 0) is None}
-
-    def one_pass(nth):
-        for c in range(rf.ncols):
-            if c in fsst:  # free text: the oracle's FSST decoder into offsets + bytes
-                rf.decode_strings_column(c, nth)
-            else:
-                rf.decode_column(c, nth)
-
-    # one pass to size the run, then repeat within the budget
-    t0 = time.perf_counter()
-    one_pass(nthreads)
-    one = time.perf_counter() - t0
-    reps = max(1, int(args.cpu_seconds / max(one, 1e-6)))
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        one_pass(nthreads)
-    dt = time.perf_counter() - t0
-    # the same restatement on one core (SURVEY.md 8(d) asks for both numbers)
-    t0 = time.perf_counter()
-    reps1 = 0
-    while reps1 == 0 or time.perf_counter() - t0 < args.cpu_seconds / 4:
-        one_pass(1)
-        reps1 += 1
-    dt1 = time.perf_counter() - t0
+    obs = [rf.out_width(c) for c in range(rf.ncols)]
+    res = {}
+    for build in flsfast.available():
+        d = flsfast.Decoder(img, img.ptr, img.len, obs, rf.nrows, 0, rf.nrowgroups, build)
+        d.decode(nthreads)  # first touch of the output pages
+        t0 = time.perf_counter()
+        n = d.decode(nthreads)
+        one = time.perf_counter() - t0
+        reps = max(1, int(args.cpu_seconds / 3 / max(one, 1e-6)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            n = d.decode(nthreads)
+        dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        reps1 = 0
+        while reps1 == 0 or time.perf_counter() - t0 < args.cpu_seconds / 6:
+            d.decode(1)
+            reps1 += 1
+        dt1 = time.perf_counter() - t0
+        res[build] = {"value": n * reps / dt, "value_1core": n * reps1 / dt1, "passes": reps, "seconds": dt}
+        del d
+    best = max(res, key=lambda b: res[b]["value"])
+    out_gb = rf.nrows * sum(obs) / 1e9
     return {
-        "value": vals_per_pass * reps / dt,
-        "value_1core": vals_per_pass * reps1 / dt1,
-        "cpu_model": cpu_model(),
+        "value": res[best]["value"],
         "unit": "values/s",
         "cores": nthreads,
         "kind": "port",
-        "sample": f"{args.workload} row groups [0,{sample_rg}) = {rf.nrows} rows x {rf.ncols} cols, "
-                  f"oracle/flsref.c (gcc -O3), {nthreads} threads, {reps} passes in {dt:.1f} s; "
-                  f"1 thread: {reps1} passes in {dt1:.1f} s",
+        "build": best,
+        "value_1core": res[best]["value_1core"],
+        "builds": res,
+        "host": cores,
+        "sample": f"{args.workload} row groups [0,{sample_rg}) = {rf.nrows} rows x {rf.ncols} cols "
+                  f"({out_gb:.1f} GB decoded per pass, beyond L3), oracle/flsfast.cpp FastLanes-shaped decoder, "
+                  f"{nthreads} threads ({cores['usable']} usable CPUs: affinity {cores['affinity']}, "
+                  f"cgroup quota {cores['cgroup_quota']}), best of builds {list(res)}",
     }
 
 
-def verify(fl, t, args, rg_list):
-    """Bit-exact check of sampled row groups against the generator ground truth."""
-    first = t.row_offset
-    sch = t.schema()
-    for rg in rg_list:
-        r0 = rg * 65536
-        n = t.rowgroup_rows(rg)
-        for c, (name, ty, _, _, ob) in enumerate(sch):
-            got = t.device_copy_out(c, r0, n)
-            if ty == fl.VARCHAR:
-                dic = {}
-                k = 0
-                while True:
-                    s = fl.gen_dict_string(args.workload, c, k)
-                    if s is None:
-                        break
-                    dic[k] = s.encode()
-                    k += 1
-                if dic:
-                    codes = fl.gen_values(args.workload, c, first + r0, n, np.uint32, args.scale, args.rows)
-                    exp = [dic[int(x)] for x in codes]
-                else:  # free text (l_comment, FSST)
-                    exp = fl.gen_strings(args.workload, c, first + r0, n, args.scale, args.rows)
-                if fl.string_t_decode(got) != exp:
-                    return f"{name} rg {rg}"
-            else:
-                exp = fl.gen_values(args.workload, c, first + r0, n, fl.NP_DTYPE[ty], args.scale, args.rows)
-                if not np.array_equal(got.view(fl.NP_DTYPE[ty]), exp):
-                    return f"{name} rg {rg}"
-    return None
+def e2e_rates(fl, args, nthreads: int):
+    """PCIe-inclusive rates (never `value`): the engine scan (compressed batch
+    H2D -> decode -> D2H into pinned host memory, fls_scan_*) and read_fastlanes
+    delivering zero-copy DataChunks through the executor harness (count-only
+    sink), on an SF(--e2e-scale) file of the same workload."""
+    import ctypes as C
+    import tempfile
+    wl = args.workload if args.workload.startswith("lineitem") else "lineitem"
+    img = fl.gen_image(wl, args.e2e_scale, 0, 0, None, nthreads)
+    t = fl.Connection([0]).read_image(img)
+    ob = sum(t.column(c).out_bytes for c in range(t.ncols))
+    for _ in t.scan():  # warm: pins the image, allocates the slots
+        break
+    passes = []
+    for _ in range(3):
+        rows = 0
+        out = fl.RowGroup()
+        t0 = time.perf_counter()
+        fl._check(fl.lib.fls_scan_begin(t.h, None, 0, t.nrowgroups))
+        while fl._check(fl.lib.fls_scan_next(t.h, C.byref(out))) == 1:
+            rows += out.nrows
+        passes.append((time.perf_counter() - t0, rows))
+    dt, rows = min(passes)
+    res = {"file": f"{wl} SF{args.e2e_scale:g}: {t.nrows} rows x {t.ncols} cols",
+           "engine_scan_rows_s": rows / dt,
+           "engine_scan_gbs": rows * ob / dt / 1e9,
+           "engine_scan_frac_pcie": rows * ob / dt / 1e9 / PCIE_GBS,
+           "engine_scan_note": "decoded column bytes delivered into pinned host memory (string_t 16 B; "
+                               "FSST heap bytes not counted), best of 3 passes"}
+    t.close()
+    sys.path.insert(0, str(ROOT / "tests"))
+    from ext_harness import Ext
+    fd, path = tempfile.mkstemp(suffix=".fls", dir=os.environ.get("TMPDIR", "/tmp"))
+    os.close(fd)
+    try:
+        img.write(path)
+        e = Ext()
+        for th in sorted({1, nthreads}):
+            best = None
+            for _ in range(2):
+                n, sec = e.scan_rows("read_fastlanes", path, threads=th)
+                best = sec if best is None else min(best, sec)
+            res[f"datachunk_rows_s_{th}t"] = n / best
+        e.close()
+    finally:
+        os.unlink(path)
+    res["datachunk_note"] = ("read_fastlanes -> DuckDB DataChunks (vectors reference the pinned row groups), "
+                             "count-only sink, best of 2, includes bind/open")
+    return res
 
 
-def main():
-    args = parse()
+def verify_full(fl, t, args) -> tuple[int, int]:
+    """Every decoded value of the resident shard vs the generator, on the GPU.
+    Returns (mismatching values, values checked)."""
+    mism = fl.check_device_table(t, args.workload, args.scale, args.rows)
+    return int(sum(mism)), int(t.device_rows) * t.ncols
+
+
+# ---- cross-rank reduction -----------------------------------------------------
+# per-rank record: [seconds, values, achieved GB/s, kernel ms, algorithmic
+# bytes per launch, mismatching values, values checked, row groups]
+def gather_ranks(local: list[float], dist_on: bool, device: str) -> list[list[float]]:
+    if not dist_on:
+        return [list(local)]
+    import torch
+    import torch.distributed as dist
+    x = torch.tensor(local, dtype=torch.float64, device=device)
+    allx = [torch.zeros_like(x) for _ in range(dist.get_world_size())]
+    dist.all_gather(allx, x)
+    return [a.tolist() for a in allx]
+
+
+def reduce_ranks(per_rank: list[list[float]]) -> dict:
+    """Aggregate over ranks: the job's time is the slowest rank's, its values
+    the sum (total values / max-over-GPUs wall time)."""
+    return {"dt": max(r[0] for r in per_rank),
+            "values": sum(r[1] for r in per_rank),
+            "mean_achieved": sum(r[2] for r in per_rank) / len(per_rank),
+            "hbm_gbs": sum(r[2] for r in per_rank),
+            "mismatches": int(sum(r[5] for r in per_rank)),
+            "checked": int(sum(r[6] for r in per_rank)),
+            "rowgroups": [int(r[7]) for r in per_rank]}
+
+
+def dry_run(args) -> None:
+    """Launcher rehearsal (no GPU): every rank takes its shard of the
+    workload's row groups, makes a synthetic per-rank record from it and the
+    records go through the same gloo all_gather + reduction as a GPU run."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    import pkgload
+    fl = pkgload.load()
+    nrows = fl.gen_nrows(args.workload, args.scale, args.rows)
+    nrg = (nrows + 65535) // 65536
+    rg0, rg1 = shard_range(nrg, rank, world)
+    rows = min(nrows, rg1 * 65536) - rg0 * 65536
+    local = [1.0 + 0.25 * rank, float(rows), 100.0 * (rank + 1), 1.0, 0.0, 0.0, float(rows), float(rg1 - rg0)]
+    per_rank = gather_ranks(local, world > 1, "cpu")
+    if rank == 0:
+        red = reduce_ranks(per_rank)
+        print(json.dumps({"dry_run": True, "n_gpus": world, "rowgroups": nrg, "rows": nrows,
+                          "shards": [list(shard_range(nrg, r, world)) for r in range(world)],
+                          "reduced": red, "value": red["values"] / red["dt"]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---- main -------------------------------------------------------------------
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args, argv))
+    if args.dry_run:
+        dry_run(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
 
     traffic, traffic_note = None, "not measured (multi-rank run or --no-traffic)"
     under_profiler = "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
@@ -227,9 +389,8 @@ def main():
 
     import pkgload
     fl = pkgload.load()
-    nthreads = host_threads(args)
-    if dist_on:
-        nthreads = max(1, nthreads // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world))))
+    cores = host_cores()
+    nthreads = host_threads(args, local_world if dist_on else 1)
 
     nrows = fl.gen_nrows(args.workload, args.scale, args.rows)
     nrg = (nrows + 65535) // 65536
@@ -237,7 +398,8 @@ def main():
     t_gen = time.perf_counter()
     img = fl.gen_image(args.workload, args.scale, args.rows, rg0, rg1, nthreads)
     t_gen = time.perf_counter() - t_gen
-    log(f"[rank {rank}] encoded row groups [{rg0},{rg1}) of {nrg}: {img.len / 1e9:.2f} GB in {t_gen:.1f} s")
+    log(f"[rank {rank}] encoded row groups [{rg0},{rg1}) of {nrg}: {img.len / 1e9:.2f} GB in {t_gen:.1f} s "
+        f"({nthreads} threads)")
 
     conn = fl.Connection([dev])
     t = conn.read_image(img)
@@ -264,44 +426,47 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
 
-    local_vals = st.values * args.steps
-    if dist_on:
-        x = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        dt = float(x.item())
-        v = torch.tensor([local_vals], dtype=torch.float64, device="cuda")
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        total_vals = float(v.item())
-    else:
-        total_vals = float(local_vals)
-
-    # roofline of the (single, fused) decode kernel on this rank
+    # roofline of this rank's decode launch (HIP events on the decode stream)
     avg_ms = st.kernel_ms_total / max(1, st.timed_launches)
     algo = st.algo_bytes
     achieved = algo / (avg_ms * 1e-3) / 1e9
 
-    bad = None
-    if args.verify_rowgroups > 0:
-        n_local = rg1 - rg0
-        picks = sorted({0, n_local // 2, n_local - 1})[: args.verify_rowgroups]
-        bad = verify(fl, t, args, picks)
+    bad, checked = 0, 0
+    if not args.no_verify:
+        bad, checked = verify_full(fl, t, args)
         if bad:
-            log(f"[rank {rank}] VERIFY FAILED: {bad}")
+            log(f"[rank {rank}] VERIFY FAILED: {bad} of {checked} values differ from the generator")
 
+    local = [dt, float(st.values * args.steps), achieved, avg_ms, float(algo), float(bad), float(checked),
+             float(rg1 - rg0)]
+    per_rank = gather_ranks(local, dist_on, "cuda")
+    red = reduce_ranks(per_rank)
+    dt, total_vals, bad_total, checked_total = red["dt"], red["values"], red["mismatches"], red["checked"]
+    mean_achieved = red["mean_achieved"]
+
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_scale > 0 and not args.pmc_child:
+        try:
+            e2e = e2e_rates(fl, args, nthreads)
+        except Exception as e:  # noqa: BLE001 - the e2e numbers are reported beside the metric
+            e2e = {"error": repr(e)}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(fl, args, nthreads, nrows)
+        cpu = cpu_baseline(fl, args, nthreads, nrows, cores)
 
     if rank == 0:
-        cfg = {"workload": f"{args.workload}" + (f" SF{args.scale:g}" if args.workload == "lineitem" else ""),
+        big = args.workload.startswith("lineitem")
+        cfg = {"workload": args.workload + (f" SF{args.scale:g}" if big else ""),
                "rows": nrows, "columns": t.ncols, "rowgroups": nrg,
-               "rowgroups_per_gpu": rg1 - rg0, "parallelism": f"rowgroup-shard x{world}",
-               "step": "one fused decode launch over all resident vectors (HBM -> HBM)",
-               "compressed_bytes_per_gpu": img.len, "decoded_bytes_per_gpu": int(st.out_bytes),
-               "verified_rowgroups_bit_exact": bad is None and args.verify_rowgroups > 0}
+               "rowgroups_per_gpu": red["rowgroups"], "parallelism": f"rowgroup-shard x{world}",
+               "step": "one decode launch over all resident vectors of the shard (HBM -> HBM)",
+               "compressed_bytes_rank0": img.len, "decoded_bytes_rank0": int(st.out_bytes),
+               "verified_values_bit_exact": checked_total if (bad_total == 0 and checked_total > 0) else 0,
+               "verified_mismatches": bad_total,
+               "verification": "every decoded value of every rank's shard vs the seeded generator, on the GPU "
+                               "(libflscheck.so)" if not args.no_verify else "skipped (--no-verify)"}
         line = {
-            "metric": "decoded values/sec (TPC-H lineitem full scan)" if args.workload == "lineitem"
-            else f"decoded values/sec ({args.workload})",
+            "metric": f"decoded values/sec ({args.workload}" + (f" SF{args.scale:g} full scan)" if big else ")"),
             "value": total_vals / dt,
             "unit": "values/s",
             "n_gpus": world,
@@ -311,29 +476,33 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",  # fixed SF100 total, row groups split over ranks
             "vs_baseline": None,
-            "dtype": "int64/int32/string_t (integer unpack)" if args.workload != "lineitem_dbl"
-            else "int64/int32/string_t + f64 (ALP)",
-            "data": {"lineitem": "synthetic (seeded TPC-H-like generator, l_comment excluded)",
-                     "lineitem_full": "synthetic (seeded TPC-H-like generator, l_comment FSST text)",
+            "dtype": "u8..u64 integer unpack -> int32/int64/string_t" + (" + f64 (ALP)" if "dbl" in args.workload
+                                                                          else ""),
+            "data": {"lineitem_full": "synthetic (seeded TPC-H-like generator, all 16 columns, l_comment FSST)",
+                     "lineitem": "synthetic (seeded TPC-H-like generator, l_comment excluded)",
                      "lineitem_dbl": "synthetic (seeded TPC-H-like generator, DECIMAL columns as DOUBLE/ALP)"}.get(
                 args.workload, "synthetic (seeded generator)"),
             "config": cfg,
-            "hbm_gbs": achieved * world,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
+            "hbm_gbs": red["hbm_gbs"],
+            "roofline": {"bound": "hbm", "achieved": mean_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": mean_achieved / HBM_PEAK_GBS,
                          "traffic": traffic / 1e9 if traffic else None,
                          "traffic_unit": "GB per launch (HBM, PMC)", "traffic_note": traffic_note,
-                         "kernel": "fls::decode_kernel" + (" + fls::fsst_kernel" if args.workload == "lineitem_full" else ""),
+                         "kernel": "fls::decode_kernel" + (" + fls::fsst_kernel" if args.workload == "lineitem_full"
+                                                           else ""),
                          "kernel_ms": avg_ms,
                          "algo_bytes_per_launch": algo,
                          "algo_bytes_split": {"packed": int(st.packed_bytes), "meta": int(st.meta_bytes),
-                                              "out": int(st.out_bytes)}},
+                                              "out": int(st.out_bytes)},
+                         "per_rank": [{"achieved_gbs": r[2], "kernel_ms": r[3], "algo_bytes": r[4]}
+                                      for r in per_rank] if world > 1 else None},
+            "e2e": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist_on:
         dist.destroy_process_group()
-    if bad:
+    if bad_total:
         sys.exit(3)
 
 

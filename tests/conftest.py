@@ -16,7 +16,7 @@ def pytest_configure(config):
 
 
 def _make(d: Path):
-    subprocess.run(["make", "-s", "-C", str(d)], check=True)
+    subprocess.run(["make", "-s", "-j3", "-C", str(d)], check=True)
 
 
 @pytest.fixture(scope="session", autouse=True)

@@ -1,0 +1,56 @@
+"""bench.py's multi-GPU entry point, rehearsed on CPU:
+`bench.py --gpus N` without a torch.distributed launcher starts N ranks
+itself; each rank takes its contiguous row-group shard and the per-rank
+records go through the same all_gather + reduction a GPU run uses (gloo here,
+RCCL on the GPUs): job time = slowest rank, values = sum over ranks."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+import bench
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_rank_envs_one_process_per_gpu():
+    envs = bench.rank_envs(4, 29511, {"PATH": "/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["LOCAL_WORLD_SIZE"] == "4" for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29511" and e["PATH"] == "/bin"
+               for e in envs)
+
+
+def test_reduce_ranks_max_time_sum_values():
+    recs = [[2.0, 100.0, 5000.0, 1.0, 0, 0, 100.0, 3], [2.5, 120.0, 4000.0, 1.1, 0, 2, 120.0, 4]]
+    r = bench.reduce_ranks(recs)
+    assert r["dt"] == 2.5 and r["values"] == 220.0 and r["mismatches"] == 2 and r["checked"] == 220
+    assert r["mean_achieved"] == 4500.0 and r["hbm_gbs"] == 9000.0 and r["rowgroups"] == [3, 4]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_spawns_ranks_and_reduces(_built, n):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--dry-run",
+                        "--workload", "lineitem", "--scale", "100"],
+                       capture_output=True, text=True, env=env, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["rowgroups"] == 9156 and out["rows"] == 600037902
+    shards = out["shards"]
+    assert shards[0][0] == 0 and shards[-1][1] == 9156
+    assert all(a[1] == b[0] for a, b in zip(shards, shards[1:]))          # contiguous, in rank order
+    assert max(b - a for a, b in shards) - min(b - a for a, b in shards) <= 1
+    red = out["reduced"]
+    assert red["values"] == 600037902 and red["checked"] == 600037902
+    assert red["dt"] == 1.0 + 0.25 * (n - 1)                               # the slowest rank's time
+    assert red["rowgroups"] == [b - a for a, b in shards]
+    assert out["value"] == pytest.approx(600037902 / red["dt"])
