@@ -22,6 +22,7 @@
 #include <mutex>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/flsgpu.h"
@@ -115,11 +116,90 @@ struct PinBuf {
     ~PinBuf() { release(); }
 };
 
-}  // namespace
+// Host threads that split a large memcpy: a scan stages each batch's
+// compressed bytes from the mapped file into pinned memory for its H2D
+// (instead of pinning the whole file up front, which cost ~0.12 s per GB
+// before the first row group could move).  The copy must keep pace with
+// compressed/decoded x the D2H rate (lineitem: ~9 GB/s at 50 GB/s D2H), more
+// than one thread's page-cache copy rate.  Threads start on first use;
+// FLS_COPY_THREADS (default 4) sets how many besides the caller.
+class CopyPool {
+  public:
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void copy(void *dst, const void *src, size_t n) {
+        constexpr size_t kMinPart = 2u << 20;
+        start();
+        const size_t parts = std::min<size_t>(th_.size() + 1, std::max<size_t>(1, n / kMinPart));
+        if (parts <= 1) {
+            memcpy(dst, src, n);
+            return;
+        }
+        Call call;
+        call.left = (int)parts - 1;
+        const size_t per = (n / parts + 63) & ~size_t(63);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (size_t p = 1; p < parts; ++p) {
+                const size_t o = std::min(n, p * per), e = std::min(n, o + per);
+                jobs_.push_back({(uint8_t *)dst + o, (const uint8_t *)src + o, p + 1 == parts ? n - o : e - o, &call});
+            }
+        }
+        cv_.notify_all();
+        memcpy(dst, src, std::min(n, per));
+        std::unique_lock<std::mutex> lk(call.m);
+        call.cv.wait(lk, [&] { return call.left == 0; });
+    }
 
-struct fls_connection {
-    std::vector<int> devices;
+  private:
+    struct Call {
+        std::mutex m;
+        std::condition_variable cv;
+        int left = 0;
+    };
+    struct Job {
+        uint8_t *d;
+        const uint8_t *s;
+        size_t n;
+        Call *call;
+    };
+    void start() {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (started_) return;
+        started_ = true;
+        int n = 4;
+        if (const char *e = getenv("FLS_COPY_THREADS")) n = std::max(0, std::min(64, atoi(e)));
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+    }
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+                if (jobs_.empty()) return;
+                j = jobs_.back();
+                jobs_.pop_back();
+            }
+            memcpy(j.d, j.s, j.n);
+            std::lock_guard<std::mutex> lk(j.call->m);
+            if (--j.call->left == 0) j.call->cv.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<Job> jobs_;
+    std::vector<std::thread> th_;
+    bool started_ = false, stop_ = false;
 };
+
+}  // namespace
 
 namespace {
 
@@ -209,6 +289,11 @@ struct Slot {                       // one batch of row groups in flight
     DevBuf<uint8_t> d_fdesc;
 };
 
+// One GPU's scan pipeline: streams, the two device slots and the pinned
+// host-batch pool.  A scan borrows one per GPU from its connection
+// (ConnRes::take) and the table gives it back when it closes, so the next
+// table -- a new DuckDB query -- starts without stream creation, hipMalloc or
+// hipHostMalloc.
 struct ScanDev {
     int dev = -1;
     hipStream_t stream = nullptr;
@@ -222,6 +307,24 @@ struct ScanDev {
     std::vector<uint64_t> strtab_off;
     DevBuf<uint32_t> err;
     int grid = 0;
+    ScanDev() = default;
+    ScanDev(const ScanDev &) = delete;
+    ScanDev &operator=(const ScanDev &) = delete;
+    void sync() {
+        if (dev < 0) return;
+        hipSetDevice(dev);
+        if (stream) hipStreamSynchronize(stream);
+        for (auto &sl : slots)
+            if (sl.stream) hipStreamSynchronize(sl.stream);
+    }
+    ~ScanDev() {
+        sync();
+        for (auto &sl : slots) {
+            if (sl.done) hipEventDestroy(sl.done);
+            if (sl.stream) hipStreamDestroy(sl.stream);
+        }
+        if (stream) hipStreamDestroy(stream);
+    }
 };
 
 // One term of a pushed-down filter (fls_scan_filter), host side.
@@ -241,7 +344,7 @@ struct ScanCtx {
     uint32_t cur = 0;               // next position in rgs to hand out
     uint32_t pruned = 0;
     uint32_t batch = 8;
-    std::vector<ScanDev> devs;
+    std::vector<std::unique_ptr<ScanDev>> devs;  // borrowed from the connection (ConnRes)
     int64_t held = -1;              // row group fls_scan_next handed out last (released on the next call)
     std::vector<std::pair<uint32_t, HostBatch *>> out;  // row groups handed out and not yet released
     uint32_t max_batches = 64;      // host-batch pool cap per GPU (FLS_SCAN_HOST_BATCHES)
@@ -257,7 +360,55 @@ struct ScanCtx {
     std::condition_variable cv;
 };
 
+// What a connection keeps between scans: idle per-GPU pipelines (at most
+// kIdlePerDev per GPU, each with at most kKeepBatches pinned host batches)
+// and the staging copy threads.  Tables share it by reference, so it lives
+// until the connection and every table opened on it are closed.
+struct ConnRes {
+    static constexpr size_t kIdlePerDev = 2, kKeepBatches = 8;
+    std::mutex mu;
+    std::vector<std::unique_ptr<ScanDev>> idle;
+    CopyPool copy;
+    std::unique_ptr<ScanDev> take(int dev) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (size_t i = 0; i < idle.size(); ++i)
+                if (idle[i]->dev == dev) {
+                    auto d = std::move(idle[i]);
+                    idle.erase(idle.begin() + (long)i);
+                    return d;
+                }
+        }
+        auto d = std::make_unique<ScanDev>();
+        d->dev = dev;
+        return d;
+    }
+    // back from a closing table; a pipeline with a host batch still out (a
+    // row group never released) is freed rather than reused
+    void give(std::unique_ptr<ScanDev> d) {
+        if (!d) return;
+        d->sync();
+        if (d->free_batches.size() != d->batches.size()) return;
+        for (auto &sl : d->slots) {
+            sl.busy = sl.starved = false;
+            sl.hb = nullptr;
+        }
+        while (d->batches.size() > kKeepBatches) d->batches.pop_back();
+        d->free_batches.clear();
+        for (auto &b : d->batches) d->free_batches.push_back(b.get());
+        std::lock_guard<std::mutex> lk(mu);
+        size_t same = 0;
+        for (auto &x : idle) same += x->dev == d->dev;
+        if (same < kIdlePerDev) idle.push_back(std::move(d));
+    }
+};
+
 }  // namespace
+
+struct fls_connection {
+    std::vector<int> devices;
+    std::shared_ptr<ConnRes> res = std::make_shared<ConnRes>();
+};
 
 // Second stream a table decode overlaps its FSST kernels on (launch_all).
 struct SideStream {
@@ -266,13 +417,14 @@ struct SideStream {
 };
 
 struct fls_table {
-    fls_connection *conn = nullptr;
+    std::vector<int> devices;          // the connection's GPUs (row groups shard over them)
+    std::shared_ptr<ConnRes> res;      // the connection's scan resources (outlive a disconnect)
     std::vector<uint8_t> owned;
     const uint8_t *img = nullptr;
     uint64_t len = 0;
     FileMeta meta;
     std::vector<std::string> names;
-    bool registered = false;        // img pinned with hipHostRegister
+    bool registered = false;        // img pinned with hipHostRegister (FLS_SCAN_PIN=1)
     bool pin_tried = false;
     void *map = nullptr;            // fls_read_fls: the file, mapped read-only
     size_t map_len = 0;
@@ -590,16 +742,12 @@ fls_table::~fls_table() {
     for (auto e : ev_pool) hipEventDestroy(e);
     if (ev0) hipEventDestroy(ev0);
     if (ev1) hipEventDestroy(ev1);
+    // the scan pipelines go back to the connection (synchronised first: their
+    // copies may read the image or the pinned stage)
     for (ScanCtx *s : {&scan, &mat})
         for (auto &d : s->devs) {
-            hipSetDevice(d.dev);
-            if (d.stream) hipStreamSynchronize(d.stream);
-            for (auto &sl : d.slots) {
-                if (sl.stream) hipStreamSynchronize(sl.stream);
-                if (sl.done) hipEventDestroy(sl.done);
-                if (sl.stream) hipStreamDestroy(sl.stream);
-            }
-            if (d.stream) hipStreamDestroy(d.stream);
+            if (res) res->give(std::move(d));
+            d.reset();
         }
     if (registered) hipHostUnregister((void *)img);
     if (map) munmap(map, map_len);
@@ -666,16 +814,15 @@ bool rowgroup_may_match(const fls_table *t, uint32_t rg, const std::vector<HostT
     return true;
 }
 
-int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, uint32_t rg1,
-               const std::vector<HostTerm> *filter) {
+int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uint8_t *col_mask, uint32_t rg0,
+               uint32_t rg1, const std::vector<HostTerm> *filter) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     if (rg1 > t->meta.rgs.size() || rg0 > rg1) return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg0, rg1);
     // tear down a previous scan on this context
-    for (auto &d : s.devs) {
-        hipSetDevice(d.dev);
-        if (d.stream) hipStreamSynchronize(d.stream);
+    for (auto &dp : s.devs) {
+        ScanDev &d = *dp;
+        d.sync();
         for (auto &sl : d.slots) {
-            if (sl.stream) hipStreamSynchronize(sl.stream);
             sl.busy = false;
             sl.starved = false;
             sl.hb = nullptr;
@@ -709,27 +856,22 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         s.active = true;
         return 0;
     }
-    const auto &devs = t->conn->devices;
     const uint32_t G = (uint32_t)devs.size(), n = (uint32_t)s.rgs.size();
-    if (s.devs.size() != G) {
-        for (auto &d : s.devs) {
-            hipSetDevice(d.dev);
-            for (auto &sl : d.slots) {
-                if (sl.done) hipEventDestroy(sl.done);
-                if (sl.stream) hipStreamDestroy(sl.stream);
-            }
-            if (d.stream) hipStreamDestroy(d.stream);
-        }
+    // one pipeline per GPU of this scan, borrowed from the connection (kept
+    // from the previous scan of this context when it targets the same GPUs)
+    bool same = s.devs.size() == G;
+    for (uint32_t g = 0; same && g < G; ++g) same = s.devs[g] && s.devs[g]->dev == devs[g];
+    if (!same) {
+        for (auto &d : s.devs) t->res->give(std::move(d));
         s.devs.clear();
-        s.devs.resize(G);
+        for (uint32_t g = 0; g < G; ++g) s.devs.push_back(t->res->take(devs[g]));
     }
     const char *b = getenv("FLS_SCAN_BATCH");
     s.batch = b ? (uint32_t)std::max(1, atoi(b)) : 8u;
     const char *mb = getenv("FLS_SCAN_HOST_BATCHES");
     s.max_batches = mb ? (uint32_t)std::max(2, atoi(mb)) : 64u;
     for (uint32_t g = 0; g < G; ++g) {
-        ScanDev &d = s.devs[g];
-        d.dev = devs[g];
+        ScanDev &d = *s.devs[g];
         HIP_TRY(hipSetDevice(d.dev));
         if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         for (auto &sl : d.slots) {
@@ -749,10 +891,12 @@ int scan_setup(fls_table *t, ScanCtx &s, const uint8_t *col_mask, uint32_t rg0, 
         HIP_TRY(hipMemsetAsync(d.err.p, 0, sizeof(uint32_t), d.stream));
         HIP_TRY(hipStreamSynchronize(d.stream));
     }
-    // pin the file image once so batch uploads are true async DMA; where that
-    // is refused (e.g. a read-only file mapping) batches are staged through a
-    // pinned buffer per slot
-    if (!t->pin_tried && t->len > 0) {
+    // batches are staged from the image into a pinned buffer per slot by the
+    // connection's copy threads (enqueue_batch); FLS_SCAN_PIN=1 instead pins
+    // the whole image once (hipHostRegister: no host copies afterwards, but
+    // ~0.12 s per GB before the first batch can move)
+    static const bool pin = getenv("FLS_SCAN_PIN") && atoi(getenv("FLS_SCAN_PIN")) != 0;
+    if (pin && !t->pin_tried && t->len > 0) {
         t->pin_tried = true;
         if (hipHostRegister((void *)t->img, t->len, hipHostRegisterDefault) == hipSuccess) t->registered = true;
         else (void)hipGetLastError();
@@ -873,7 +1017,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     const uint8_t *src = t->img + lo;
     if (!t->registered) {
         HIP_TRY(sl.h_stage.alloc(hi - lo));
-        memcpy(sl.h_stage.p, src, hi - lo);
+        t->res->copy.copy(sl.h_stage.p, src, hi - lo);
         src = sl.h_stage.p;
     }
     HIP_TRY(hipMemcpyAsync(sl.d_in.p, src, hi - lo, hipMemcpyHostToDevice, sl.stream));
@@ -959,7 +1103,7 @@ int scan_start(fls_table *t, ScanCtx &s) {
     if (s.rgs.empty()) return 0;
     for (auto &d : s.devs)
         for (int si = 0; si < 2; ++si) {
-            int rc = enqueue_batch(t, s, d, si);
+            int rc = enqueue_batch(t, s, *d, si);
             if (rc) return rc;
         }
     return 0;
@@ -969,7 +1113,7 @@ int scan_start(fls_table *t, ScanCtx &s) {
 bool find_slot(ScanCtx &s, uint32_t rg, int &g, int &si) {
     for (size_t i = 0; i < s.devs.size(); ++i)
         for (int j = 0; j < 2; ++j) {
-            const Slot &sl = s.devs[i].slots[j];
+            const Slot &sl = s.devs[i]->slots[j];
             if (sl.busy && rg >= sl.rg0 && rg < sl.rg0 + sl.nrg) {
                 g = (int)i;
                 si = j;
@@ -1030,9 +1174,9 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
             if (!s.active) return fail(FLS_ERR_STATE, "scan ended while waiting for row group %u", rg);
             return fail(s.err_rc, "%s", s.err_msg.c_str());
         }
-        hb = s.devs[g].slots[si].hb;
+        hb = s.devs[g]->slots[si].hb;
     }
-    ScanDev &d = s.devs[g];
+    ScanDev &d = *s.devs[g];
     Slot &sl = d.slots[si];
     auto wait_batch = [&]() -> int {
         HIP_TRY(hipSetDevice(d.dev));
@@ -1084,7 +1228,8 @@ int scan_release(fls_table *t, ScanCtx &s, uint32_t rg) {
     // every row group of the batch is back: its host side returns to the pool,
     // and a slot whose refill waited for one goes now
     int rc = 0;
-    for (auto &d : s.devs) {
+    for (auto &dp : s.devs) {
+        ScanDev &d = *dp;
         bool mine = false;
         for (auto &b : d.batches) mine = mine || b.get() == hb;
         if (!mine) continue;
@@ -1166,7 +1311,8 @@ int open_common(fls_connection *conn, fls_table *t, fls_table **out) {
         delete t;
         return fail(FLS_ERR_FORMAT, "not a valid FastLanes file: %s", why.c_str());
     }
-    t->conn = conn;
+    t->devices = conn->devices;
+    t->res = conn->res;
     for (auto &c : t->meta.cols) t->names.push_back(c.name);
     *out = t;
     if (debug_enabled())
@@ -1304,16 +1450,11 @@ int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowg
     if (!t || !out) return fail(FLS_ERR_ARG, "fls_materialize: NULL argument");
     if (rg >= t->meta.rgs.size()) return fail(FLS_ERR_ARG, "row group %u out of range", rg);
     // a one-row-group scan on the GPU that owns rg in a full-table sharding
-    const uint32_t G = (uint32_t)t->conn->devices.size(), N = (uint32_t)t->meta.rgs.size();
+    const uint32_t G = (uint32_t)t->devices.size(), N = (uint32_t)t->meta.rgs.size();
     uint32_t g = 0;
     while (g + 1 < G && rg >= (uint64_t)N * (g + 1) / G) ++g;
-    fls_connection one;
-    one.devices = {t->conn->devices[g]};
-    fls_connection *saved = t->conn;
-    t->conn = &one;
-    int rc = scan_setup(t, t->mat, col_mask, rg, rg + 1, nullptr);
+    int rc = scan_setup(t, t->mat, {t->devices[g]}, col_mask, rg, rg + 1, nullptr);
     if (!rc) rc = scan_start(t, t->mat);
-    t->conn = saved;
     if (rc) return rc;
     rc = scan_next(t, t->mat, out);
     return rc == 1 ? 0 : (rc == 0 ? fail(FLS_ERR_STATE, "internal: empty materialize") : rc);
@@ -1321,7 +1462,7 @@ int fls_materialize(fls_table *t, uint32_t rg, const uint8_t *col_mask, fls_rowg
 
 int fls_scan_begin(fls_table *t, const uint8_t *col_mask, uint32_t rg_begin, uint32_t rg_end) {
     if (!t) return fail(FLS_ERR_ARG, "fls_scan_begin: NULL table");
-    int rc = scan_setup(t, t->scan, col_mask, rg_begin, rg_end, &t->filter);
+    int rc = scan_setup(t, t->scan, t->devices, col_mask, rg_begin, rg_end, &t->filter);
     if (rc) return rc;
     return scan_start(t, t->scan);
 }
@@ -1380,7 +1521,7 @@ int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
     if (!t) return fail(FLS_ERR_ARG, "fls_device_upload: NULL table");
     if (rg_end > t->meta.rgs.size() || rg_begin >= rg_end)
         return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg_begin, rg_end);
-    const int dev = t->conn->devices[0];
+    const int dev = t->devices[0];
     int rc = ensure_stream(t, dev);
     if (rc) return rc;
     DeviceShard &sh = t->shard;

@@ -38,9 +38,8 @@ struct FastLanesFacade::Impl {
 
     void release() {
         if (table) fls_table_close(table);
-        if (conn) fls_disconnect(conn);
         table = nullptr;
-        conn = nullptr;
+        conn = nullptr;  // the process-wide connection (SharedConnection) stays open
         initialized = false;
         current_row = total_rows = 0;
     }
@@ -56,9 +55,8 @@ bool FastLanesFacade::openFile(const std::string &filename) {
     Impl &s = *pImpl;
     s.release();
     if (Debug()) std::cerr << "DEBUG: Opening FastLanes file: " << filename << std::endl;
-    std::vector<int> devs = ext_fastlane::GpuDevices();
-    if (fls_connect(devs.data(), (int)devs.size(), &s.conn) != 0 ||
-        fls_read_fls(s.conn, filename.c_str(), &s.table) != 0) {
+    s.conn = ext_fastlane::SharedConnection();
+    if (!s.conn || fls_read_fls(s.conn, filename.c_str(), &s.table) != 0) {
         if (Debug()) std::cerr << "DEBUG: Error opening file: " << fls_last_error() << std::endl;
         s.release();
         return false;

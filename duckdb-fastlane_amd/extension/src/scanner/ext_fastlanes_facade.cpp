@@ -42,9 +42,8 @@ public:
 
     void close_read() {
         if (table) fls_table_close(table);
-        if (conn) fls_disconnect(conn);
         table = nullptr;
-        conn = nullptr;
+        conn = nullptr;  // the process-wide connection (SharedConnection) stays open
         have_rg = eof = false;
         rg_pos = 0;
     }
@@ -61,9 +60,8 @@ FastLanesFacade::~FastLanesFacade() = default;
 bool FastLanesFacade::openFile(const std::string &file_path) {
     Impl &s = *pImpl;
     s.close_read();
-    std::vector<int> devs = GpuDevices();
-    if (fls_connect(devs.data(), (int)devs.size(), &s.conn) != 0 ||
-        fls_read_fls(s.conn, file_path.c_str(), &s.table) != 0) {
+    s.conn = SharedConnection();
+    if (!s.conn || fls_read_fls(s.conn, file_path.c_str(), &s.table) != 0) {
         s.close_read();
         return false;
     }

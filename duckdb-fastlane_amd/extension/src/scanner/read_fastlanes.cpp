@@ -45,17 +45,16 @@ namespace ext_fastlane {
 
 namespace {
 
+// An open file on the process-wide engine connection (SharedConnection: its
+// scan pipelines and pinned buffers carry over between queries).
 struct OpenTable {
-    fls_connection *conn = nullptr;
     fls_table *table = nullptr;
     ~OpenTable() {
         if (table) fls_table_close(table);
-        if (conn) fls_disconnect(conn);
     }
     bool open(const std::string &path) {
-        std::vector<int> devs = GpuDevices();
-        return fls_connect(devs.data(), (int)devs.size(), &conn) == 0 &&
-               fls_read_fls(conn, path.c_str(), &table) == 0;
+        fls_connection *conn = SharedConnection();
+        return conn && fls_read_fls(conn, path.c_str(), &table) == 0;
     }
 };
 
