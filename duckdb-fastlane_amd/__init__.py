@@ -78,6 +78,11 @@ class DecodeStats(C.Structure):
         return int(self.packed_bytes + self.meta_bytes + self.out_bytes)
 
 
+class PartInfo(C.Structure):
+    _fields_ = [("device", C.c_int), ("rg_begin", C.c_uint32), ("rg_end", C.c_uint32), ("first_row", C.c_uint64),
+                ("nrows", C.c_uint64)]
+
+
 def _sig(name, res, *args):
     f = getattr(_lib, name)
     f.restype = res
@@ -117,6 +122,10 @@ _sig("fls_device_column", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_
 _sig("fls_device_copy_out", C.c_int, _P, C.c_uint32, C.c_uint64, C.c_uint64, _P)
 _sig("fls_device_rows", C.c_uint64, _P)
 _sig("fls_device_heap", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_uint64))
+_sig("fls_device_parts", C.c_int, _P)
+_sig("fls_device_part", C.c_int, _P, C.c_uint32, C.POINTER(PartInfo))
+_sig("fls_device_part_column", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64))
+_sig("fls_device_part_heap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_writer_new", _P, C.c_uint64)
 _sig("fls_writer_free", None, _P)
 _sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8)
@@ -553,6 +562,21 @@ class Table:
         _check(_lib.fls_device_column(self.h, c, C.byref(p), C.byref(n)))
         return p.value, n.value
 
+    def device_parts(self) -> list[PartInfo]:
+        """The resident parts: one per GPU holding row groups (device_upload
+        splits the range over the connection's GPUs)."""
+        out = []
+        for i in range(_lib.fls_device_parts(self.h)):
+            pi = PartInfo()
+            _check(_lib.fls_device_part(self.h, i, C.byref(pi)))
+            out.append(pi)
+        return out
+
+    def device_part_column(self, part: int, c: int):
+        p, n = _P(), C.c_uint64()
+        _check(_lib.fls_device_part_column(self.h, part, c, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
     @property
     def device_rows(self) -> int:
         return _lib.fls_device_rows(self.h)
@@ -601,6 +625,8 @@ def _checklib():
         lib_.fls_check_workload.argtypes = [C.c_char_p, C.c_double, C.c_uint64, C.c_uint64, C.c_uint64,
                                             C.POINTER(_P), C.POINTER(C.c_uint8), C.c_int, C.POINTER(_P),
                                             C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
+        lib_.fls_check_workload_on.restype = C.c_int
+        lib_.fls_check_workload_on.argtypes = [C.c_int] + lib_.fls_check_workload.argtypes
         lib_.fls_check_last_error.restype = C.c_char_p
         _check_lib = lib_
     return _check_lib
@@ -608,35 +634,38 @@ def _checklib():
 
 def check_device_table(t: "Table", workload: str, scale: float = 1.0, nrows: int = 0) -> list[int]:
     """Mismatching rows per column of t's resident decoded columns vs the
-    workload generator (computed on the GPU).  Call after device_sync()."""
+    workload generator (computed on the GPU holding each resident part).
+    Call after device_sync()."""
     lib_ = _checklib()
     nc = t.ncols
     total = gen_nrows(workload, scale, nrows)
-    cols = (_P * nc)()
-    obs = (C.c_uint8 * nc)()
+    obs = (C.c_uint8 * nc)(*[t.column(c).out_bytes for c in range(nc)])
     dicts = (_P * nc)()
     keep = []
-    deltas = (C.c_int64 * nc)()
     for c in range(nc):
-        ptr, _ = t.device_column(c)
-        cols[c] = ptr
-        obs[c] = t.column(c).out_bytes
-        dp, hp, hn = _P(), _P(), C.c_uint64()
-        if obs[c] == 16 and _lib.fls_device_heap(t.h, c, C.byref(dp), C.byref(hp), C.byref(hn)) == 1:
-            deltas[c] = (dp.value or 0) - (hp.value or 0)   # free text (FSST): no dictionary
-            continue
         if obs[c] == 16:
             words = []
             k = 0
             while (s := gen_dict_string(workload, c, k)) is not None:
                 words.append(s.encode())
                 k += 1
-            b = C.create_string_buffer(b"\0".join(words) + b"\0\0")
-            keep.append(b)
-            dicts[c] = C.cast(b, _P)
-    mism = (C.c_uint64 * nc)()
-    rc = lib_.fls_check_workload(workload.encode(), scale, total, t.row_offset, t.device_rows, cols, obs, nc,
-                                 dicts, deltas, mism)
-    if rc != 0:
-        raise FlsError(rc, lib_.fls_check_last_error().decode())
-    return list(mism)
+            if words:
+                b = C.create_string_buffer(b"\0".join(words) + b"\0\0")
+                keep.append(b)
+                dicts[c] = C.cast(b, _P)
+    mism_total = [0] * nc
+    for i, part in enumerate(t.device_parts()):
+        cols = (_P * nc)()
+        deltas = (C.c_int64 * nc)()
+        for c in range(nc):
+            cols[c] = t.device_part_column(i, c)[0]
+            dp, hp, hn = _P(), _P(), C.c_uint64()
+            if obs[c] == 16 and _lib.fls_device_part_heap(t.h, i, c, C.byref(dp), C.byref(hp), C.byref(hn)) == 1:
+                deltas[c] = (dp.value or 0) - (hp.value or 0)   # free text (FSST): no dictionary
+        mism = (C.c_uint64 * nc)()
+        rc = lib_.fls_check_workload_on(part.device, workload.encode(), scale, total, t.row_offset + part.first_row,
+                                        part.nrows, cols, obs, nc, dicts, deltas, mism)
+        if rc != 0:
+            raise FlsError(rc, lib_.fls_check_last_error().decode())
+        mism_total = [a + b for a, b in zip(mism_total, mism)]
+    return mism_total

@@ -221,4 +221,12 @@ int fls_check_workload(const char *workload, double scale, uint64_t nrows_total,
     return 0;
 }
 
+int fls_check_workload_on(int device, const char *workload, double scale, uint64_t nrows_total, uint64_t row_begin,
+                          uint64_t n, const void *const *d_cols, const uint8_t *out_bytes, int ncols,
+                          const void *const *dicts, const int64_t *heap_delta, uint64_t *mismatches) {
+    if (hipSetDevice(device) != hipSuccess) return err("hipSetDevice failed");
+    return fls_check_workload(workload, scale, nrows_total, row_begin, n, d_cols, out_bytes, ncols, dicts, heap_delta,
+                              mismatches);
+}
+
 }  // extern "C"

@@ -231,21 +231,6 @@ void rg_byte_range(const FileMeta &m, uint32_t rg0, uint32_t rg1, uint64_t &lo, 
     lo &= ~uint64_t(255);
 }
 
-// A shard of row groups uploaded to one GPU, with its VARCHAR string_t tables.
-struct DeviceShard {
-    int dev = -1;
-    uint32_t rg0 = 0, rg1 = 0;
-    uint64_t base = 0;                 // file offset of d_img[0]
-    DevBuf<uint8_t> img;               // compressed bytes of [rg0, rg1)
-    DevBuf<StrT> strtab;               // string_t tables of VARCHAR chunks
-    std::vector<uint64_t> strtab_off;  // per (rg - rg0) * ncols + col: index into strtab
-    DevBuf<uint32_t> err;
-    DevBuf<uint32_t> queue;                // decode work-queue counter
-    std::vector<DevBuf<uint8_t>> d_heap;   // per FSST column: decoded string bytes
-    std::vector<PinBuf<uint8_t>> h_heap;   // per FSST column: host copy string_t points into
-    std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
-};
-
 // Pinned host side of one decoded batch: what consumers read.  It belongs to
 // the batch's row groups, not to the device slot that produced it: once every
 // row group of the batch has been handed out (fls_scan_acquire) the slot is
@@ -416,6 +401,58 @@ struct SideStream {
     hipEvent_t fork = nullptr, join = nullptr;
 };
 
+namespace {
+
+// One GPU's part of a device-resident table (fls_device_*): a contiguous
+// range of row groups uploaded verbatim to its HBM with their string_t
+// tables, the decoded columns, the launch descriptor list and the streams and
+// events of its decode launches.  A table is split over the connection's GPUs
+// like a scan (no data crosses GPUs: row groups are independent).
+struct Resident {
+    int dev = -1;
+    uint32_t rg0 = 0, rg1 = 0;
+    uint64_t base = 0;                 // file offset of img[0]
+    uint64_t first_row = 0, rows = 0;  // resident rows, relative to the file's first row
+    DevBuf<uint8_t> img;               // compressed bytes of [rg0, rg1)
+    DevBuf<StrT> strtab;               // string_t tables of VARCHAR chunks
+    std::vector<uint64_t> strtab_off;  // per (rg - rg0) * ncols + col: index into strtab
+    DevBuf<uint32_t> err;
+    DevBuf<uint32_t> queue;                // decode work-queue counters
+    std::vector<DevBuf<uint8_t>> d_heap;   // per FSST column: decoded string bytes
+    std::vector<PinBuf<uint8_t>> h_heap;   // per FSST column: host copy string_t points into
+    std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
+    std::vector<DevBuf<uint8_t>> d_out;    // per column, rows of [rg0, rg1)
+    DevBuf<DevChunk> d_chunks;
+    std::vector<DevChunk> h_chunks;
+    std::vector<uint8_t> mask;         // column mask h_chunks was built for
+    uint32_t nmain = 0;                // h_chunks[0, nmain) main kernel, the rest FSST
+    int policy = -1;                   // decode_policy() h_chunks was ordered for
+    int lpolicy = 0;                   // ... and the launch policy it resolved to (launch_policy)
+    FsstCounts fsst;                   // FSST chunks of h_chunks
+    SplitPlan split;                   // balanced split after h_chunks on the device (waves 0: none)
+    ByteCount bytes;                   // algorithmic bytes of one launch
+    hipStream_t stream = nullptr;
+    SideStream side;                   // FSST kernels overlapping the main decode kernel
+    std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
+    uint32_t ev_used = 0;
+    Resident() = default;
+    Resident(const Resident &) = delete;
+    Resident &operator=(const Resident &) = delete;
+    ~Resident() {
+        if (dev < 0) return;
+        hipSetDevice(dev);
+        if (stream) hipStreamSynchronize(stream);
+        if (side.stream) hipStreamSynchronize(side.stream);
+        if (stream) hipStreamDestroy(stream);
+        if (side.stream) hipStreamDestroy(side.stream);
+        if (side.fork) hipEventDestroy(side.fork);
+        if (side.join) hipEventDestroy(side.join);
+        for (auto e : ev_pool) hipEventDestroy(e);
+    }
+};
+
+}  // namespace
+
 struct fls_table {
     std::vector<int> devices;          // the connection's GPUs (row groups shard over them)
     std::shared_ptr<ConnRes> res;      // the connection's scan resources (outlive a disconnect)
@@ -429,27 +466,9 @@ struct fls_table {
     void *map = nullptr;            // fls_read_fls: the file, mapped read-only
     size_t map_len = 0;
 
-    // device-resident mode
-    DeviceShard shard;
-    std::vector<DevBuf<uint8_t>> d_out;  // per column, rows of [rg0, rg1)
-    DevBuf<DevChunk> d_chunks;
-    std::vector<DevChunk> h_chunks;
-    std::vector<uint8_t> dev_mask;     // column mask h_chunks was built for
-    uint32_t dev_nmain = 0;            // h_chunks[0, dev_nmain) main kernel, the rest FSST
-    int dev_policy = -1;               // decode_policy() h_chunks was ordered for
-    int dev_lpolicy = 0;               // ... and the launch policy it resolved to (launch_policy)
-    FsstCounts dev_fsst;               // FSST chunks of h_chunks
-    SplitPlan dev_split;               // balanced split after h_chunks on the device (waves 0: none)
-    hipStream_t stream = nullptr;
-    SideStream side;                   // FSST kernels overlapping the main decode kernel
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::vector<hipEvent_t> ev_pool;   // per-launch (start, stop) pairs since last sync
-    uint32_t ev_used = 0;
-    int grid = 0;
-    uint64_t res_rows = 0, res_first_row = 0;
-    ByteCount last_bytes;
+    // device-resident mode: one part per GPU (fls_device_upload)
+    std::vector<std::unique_ptr<Resident>> resident;
     uint32_t launches = 0;
-    bool launched = false;
 
     ScanCtx scan, mat;
     std::vector<HostTerm> filter;   // fls_scan_filter: applies to the next fls_scan_begin
@@ -734,14 +753,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
 }  // namespace
 
 fls_table::~fls_table() {
-    if (side.stream) hipStreamSynchronize(side.stream);
-    if (stream) hipStreamDestroy(stream);
-    if (side.stream) hipStreamDestroy(side.stream);
-    if (side.fork) hipEventDestroy(side.fork);
-    if (side.join) hipEventDestroy(side.join);
-    for (auto e : ev_pool) hipEventDestroy(e);
-    if (ev0) hipEventDestroy(ev0);
-    if (ev1) hipEventDestroy(ev1);
+    resident.clear();
     // the scan pipelines go back to the connection (synchronised first: their
     // copies may read the image or the pinned stage)
     for (ScanCtx *s : {&scan, &mat})
@@ -1297,14 +1309,6 @@ int to_terms(const fls_table *t, const fls_predicate *p, uint32_t n, std::vector
     return 0;
 }
 
-int ensure_stream(fls_table *t, int dev) {
-    HIP_TRY(hipSetDevice(dev));
-    if (!t->stream) HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
-    if (!t->ev0) HIP_TRY(hipEventCreate(&t->ev0));
-    if (!t->ev1) HIP_TRY(hipEventCreate(&t->ev1));
-    return 0;
-}
-
 int open_common(fls_connection *conn, fls_table *t, fls_table **out) {
     std::string why = parse_file(t->img, t->len, t->meta);
     if (!why.empty()) {
@@ -1517,181 +1521,282 @@ int fls_scan_release(fls_table *t, uint32_t rowgroup) {
 
 // ---- device-resident mode -------------------------------------------------
 
-int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
-    if (!t) return fail(FLS_ERR_ARG, "fls_device_upload: NULL table");
-    if (rg_end > t->meta.rgs.size() || rg_begin >= rg_end)
-        return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg_begin, rg_end);
-    const int dev = t->devices[0];
-    int rc = ensure_stream(t, dev);
-    if (rc) return rc;
-    DeviceShard &sh = t->shard;
-    sh.dev = dev;
-    sh.rg0 = rg_begin;
-    sh.rg1 = rg_end;
+}  // extern "C"
+
+namespace {
+
+// Upload one GPU's part: row groups [rg0, rg1) verbatim, their string_t
+// tables, HBM output columns and FSST heaps.
+int upload_part(fls_table *t, Resident &r) {
+    HIP_TRY(hipSetDevice(r.dev));
+    if (!r.stream) HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     uint64_t lo, hi;
-    rg_byte_range(t->meta, rg_begin, rg_end, lo, hi);
-    sh.base = lo;
-    HIP_TRY(sh.img.alloc(dev, hi - lo + kImagePad));
-    HIP_TRY(hipMemcpy(sh.img.p, t->img + lo, hi - lo, hipMemcpyHostToDevice));
-    rc = build_strtabs(t, dev, rg_begin, rg_end, sh.strtab, sh.strtab_off);
+    rg_byte_range(t->meta, r.rg0, r.rg1, lo, hi);
+    r.base = lo;
+    HIP_TRY(r.img.alloc(r.dev, hi - lo + kImagePad));
+    HIP_TRY(hipMemcpy(r.img.p, t->img + lo, hi - lo, hipMemcpyHostToDevice));
+    int rc = build_strtabs(t, r.dev, r.rg0, r.rg1, r.strtab, r.strtab_off);
     if (rc) return rc;
-    HIP_TRY(sh.err.alloc(dev, 1));
-    HIP_TRY(hipMemset(sh.err.p, 0, sizeof(uint32_t)));
+    HIP_TRY(r.err.alloc(r.dev, 1));
+    HIP_TRY(hipMemset(r.err.p, 0, sizeof(uint32_t)));
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
-    t->res_first_row = t->meta.rgs[rg_begin].first_row;
-    t->res_rows = t->meta.rgs[rg_end - 1].first_row + t->meta.rgs[rg_end - 1].nrows - t->res_first_row;
-    t->d_out.resize(ncols);
-    for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(t->d_out[c].alloc(dev, t->res_rows * out_bytes_of(t, c)));
+    r.first_row = t->meta.rgs[r.rg0].first_row;
+    r.rows = t->meta.rgs[r.rg1 - 1].first_row + t->meta.rgs[r.rg1 - 1].nrows - r.first_row;
+    r.d_out.resize(ncols);
+    for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(r.d_out[c].alloc(r.dev, r.rows * out_bytes_of(t, c)));
     // FSST heaps: chunk heaps back to back per column, host copy for string_t
-    sh.heap_off.assign((size_t)(rg_end - rg_begin) * ncols, 0);
-    sh.d_heap.resize(ncols);
-    sh.h_heap.resize(ncols);
+    r.heap_off.assign((size_t)(r.rg1 - r.rg0) * ncols, 0);
+    r.d_heap.resize(ncols);
+    r.h_heap.resize(ncols);
     for (uint32_t c = 0; c < ncols; ++c) {
         uint64_t tot = 0;
-        for (uint32_t r = rg_begin; r < rg_end; ++r) {
-            sh.heap_off[(size_t)(r - rg_begin) * ncols + c] = tot;
-            if (is_fsst(t, r, c)) tot += t->meta.rgs[r].chunks[c].hdr.reserved1;
+        for (uint32_t g = r.rg0; g < r.rg1; ++g) {
+            r.heap_off[(size_t)(g - r.rg0) * ncols + c] = tot;
+            if (is_fsst(t, g, c)) tot += t->meta.rgs[g].chunks[c].hdr.reserved1;
         }
         if (tot) {
-            HIP_TRY(sh.d_heap[c].alloc(dev, tot));
-            HIP_TRY(sh.h_heap[c].alloc(tot));
+            HIP_TRY(r.d_heap[c].alloc(r.dev, tot));
+            HIP_TRY(r.h_heap[c].alloc(tot));
         } else {
-            sh.d_heap[c].release();
-            sh.h_heap[c].release();
+            r.d_heap[c].release();
+            r.h_heap[c].release();
         }
     }
-    t->h_chunks.clear();
-    t->dev_mask.clear();
-    t->launches = 0;
-    t->launched = false;
+    r.h_chunks.clear();
+    r.mask.clear();
     return 0;
 }
 
-int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
-    if (!t) return fail(FLS_ERR_ARG, "fls_device_decode: NULL table");
-    DeviceShard &sh = t->shard;
-    if (sh.dev < 0 || !sh.img.p) return fail(FLS_ERR_STATE, "fls_device_decode before fls_device_upload");
+// Enqueue one decode launch of the selected columns on part r (asynchronous).
+int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
-    std::vector<uint8_t> mask(ncols, 1);
-    if (col_mask)
-        for (uint32_t c = 0; c < ncols; ++c) mask[c] = col_mask[c] ? 1 : 0;
-    HIP_TRY(hipSetDevice(sh.dev));
+    HIP_TRY(hipSetDevice(r.dev));
     const int policy = decode_policy();
-    if (mask != t->dev_mask || t->h_chunks.empty() || policy != t->dev_policy) {
+    if (mask != r.mask || r.h_chunks.empty() || policy != r.policy) {
         // (re)build the launch descriptor list: column-major task order, so
         // concurrent waves stream one column's consecutive row groups
         std::vector<DevChunk> chunks;
         ByteCount bc;
         for (uint32_t c = 0; c < ncols; ++c) {
             if (!mask[c]) continue;
-            for (uint32_t r = sh.rg0; r < sh.rg1; ++r) {
-                const ChunkRef &ch = t->meta.rgs[r].chunks[c];
-                const uint64_t so = sh.strtab_off[(size_t)(r - sh.rg0) * ncols + c];
-                const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(sh.strtab.p + so);
-                uint8_t *out = t->d_out[c].p + (t->meta.rgs[r].first_row - t->res_first_row) * out_bytes_of(t, c);
-                const uint64_t ho = sh.heap_off[(size_t)(r - sh.rg0) * ncols + c];
-                chunks.push_back(make_devchunk(t, r, c, sh.img.p + (ch.off - sh.base), dict, out, &bc,
-                                               sh.d_heap[c].p ? sh.d_heap[c].p + ho : nullptr,
-                                               sh.h_heap[c].p ? sh.h_heap[c].p + ho : nullptr));
+            for (uint32_t g = r.rg0; g < r.rg1; ++g) {
+                const ChunkRef &ch = t->meta.rgs[g].chunks[c];
+                const uint64_t so = r.strtab_off[(size_t)(g - r.rg0) * ncols + c];
+                const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(r.strtab.p + so);
+                uint8_t *out = r.d_out[c].p + (t->meta.rgs[g].first_row - r.first_row) * out_bytes_of(t, c);
+                const uint64_t ho = r.heap_off[(size_t)(g - r.rg0) * ncols + c];
+                chunks.push_back(make_devchunk(t, g, c, r.img.p + (ch.off - r.base), dict, out, &bc,
+                                               r.d_heap[c].p ? r.d_heap[c].p + ho : nullptr,
+                                               r.h_heap[c].p ? r.h_heap[c].p + ho : nullptr));
             }
         }
         const int lpol = launch_policy(policy, chunks, bc.geom);
-        t->dev_nmain = order_for_launch(chunks, &t->dev_fsst, lpol);
-        t->dev_policy = policy;
-        t->dev_lpolicy = lpol;
+        r.nmain = order_for_launch(chunks, &r.fsst, lpol);
+        r.policy = policy;
+        r.lpolicy = lpol;
         const size_t k = chunks.size();
-        t->dev_split = append_split(chunks, t->dev_nmain, bc.geom, lpol);
-        HIP_TRY(hipStreamSynchronize(t->stream));
-        HIP_TRY(t->d_chunks.alloc(sh.dev, chunks.size()));
-        HIP_TRY(hipMemcpy(t->d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
+        r.split = append_split(chunks, r.nmain, bc.geom, lpol);
+        HIP_TRY(hipStreamSynchronize(r.stream));
+        HIP_TRY(r.d_chunks.alloc(r.dev, chunks.size()));
+        HIP_TRY(hipMemcpy(r.d_chunks.p, chunks.data(), chunks.size() * sizeof(DevChunk), hipMemcpyHostToDevice));
         chunks.resize(k);
-        t->h_chunks.swap(chunks);
-        t->dev_mask = mask;
-        t->last_bytes = bc;
+        r.h_chunks.swap(chunks);
+        r.mask = mask;
+        r.bytes = bc;
     }
-    if (t->ev_used + 2 > t->ev_pool.size()) {
+    if (r.ev_used + 2 > r.ev_pool.size()) {
         for (int i = 0; i < 2; ++i) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
-            t->ev_pool.push_back(e);
+            r.ev_pool.push_back(e);
         }
     }
     // queue counters and the side stream exist before the timed region
-    HIP_TRY(sh.queue.alloc(sh.dev, 3));
-    if (!t->side.stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&t->side.stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&t->side.fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&t->side.join, hipEventDisableTiming));
+    HIP_TRY(r.queue.alloc(r.dev, 3));
+    if (!r.side.stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&r.side.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&r.side.fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&r.side.join, hipEventDisableTiming));
     }
-    hipEvent_t e0 = t->ev_pool[t->ev_used], e1 = t->ev_pool[t->ev_used + 1];
-    t->ev_used += 2;
-    HIP_TRY(hipEventRecord(e0, t->stream));
-    HIP_TRY(launch_all(t->d_chunks.p, t->dev_nmain, (uint32_t)t->h_chunks.size(), t->dev_fsst, sh.err.p,
-                       t->last_bytes.geom, t->stream, sh.queue.p, t->dev_lpolicy, t->dev_split, &t->side));
-    HIP_TRY(hipEventRecord(e1, t->stream));
+    hipEvent_t e0 = r.ev_pool[r.ev_used], e1 = r.ev_pool[r.ev_used + 1];
+    r.ev_used += 2;
+    HIP_TRY(hipEventRecord(e0, r.stream));
+    HIP_TRY(launch_all(r.d_chunks.p, r.nmain, (uint32_t)r.h_chunks.size(), r.fsst, r.err.p, r.bytes.geom, r.stream,
+                       r.queue.p, r.lpolicy, r.split, &r.side));
+    HIP_TRY(hipEventRecord(e1, r.stream));
+    return 0;
+}
+
+uint64_t resident_rows(const fls_table *t) {
+    uint64_t n = 0;
+    for (auto &r : t->resident) n += r->rows;
+    return n;
+}
+
+const Resident *part_of(const fls_table *t, uint32_t part) {
+    return t && part < t->resident.size() ? t->resident[part].get() : nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_device_upload: NULL table");
+    if (rg_end > t->meta.rgs.size() || rg_begin >= rg_end)
+        return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg_begin, rg_end);
+    // contiguous shards over the connection's GPUs, as a scan splits them
+    const uint32_t G = (uint32_t)t->devices.size(), n = rg_end - rg_begin;
+    t->resident.clear();
+    t->launches = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t a = rg_begin + (uint32_t)((uint64_t)n * g / G), b = rg_begin + (uint32_t)((uint64_t)n * (g + 1) / G);
+        if (a == b) continue;
+        auto r = std::make_unique<Resident>();
+        r->dev = t->devices[g];
+        r->rg0 = a;
+        r->rg1 = b;
+        int rc = upload_part(t, *r);
+        t->resident.push_back(std::move(r));
+        if (rc) {
+            t->resident.clear();
+            return rc;
+        }
+    }
+    return 0;
+}
+
+int fls_device_decode(fls_table *t, const uint8_t *col_mask) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_device_decode: NULL table");
+    if (t->resident.empty()) return fail(FLS_ERR_STATE, "fls_device_decode before fls_device_upload");
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    std::vector<uint8_t> mask(ncols, 1);
+    if (col_mask)
+        for (uint32_t c = 0; c < ncols; ++c) mask[c] = col_mask[c] ? 1 : 0;
+    for (auto &r : t->resident) {  // every GPU's launch is queued before any waits
+        int rc = decode_part(t, *r, mask);
+        if (rc) return rc;
+    }
     t->launches++;
-    t->launched = true;
     return 0;
 }
 
 int fls_device_sync(fls_table *t, fls_decode_stats *stats) {
     if (!t) return fail(FLS_ERR_ARG, "fls_device_sync: NULL table");
-    if (!t->stream) return fail(FLS_ERR_STATE, "nothing uploaded");
-    HIP_TRY(hipSetDevice(t->shard.dev));
-    HIP_TRY(hipStreamSynchronize(t->stream));
+    if (t->resident.empty()) return fail(FLS_ERR_STATE, "nothing uploaded");
     uint32_t err = 0;
-    HIP_TRY(hipMemcpy(&err, t->shard.err.p, sizeof(err), hipMemcpyDeviceToHost));
+    for (auto &r : t->resident) {
+        HIP_TRY(hipSetDevice(r->dev));
+        HIP_TRY(hipStreamSynchronize(r->stream));
+        uint32_t e = 0;
+        HIP_TRY(hipMemcpy(&e, r->err.p, sizeof(e), hipMemcpyDeviceToHost));
+        err |= e;
+    }
     if (stats) {
+        // per launch the slowest GPU's time (the parts run concurrently)
         memset(stats, 0, sizeof(*stats));
-        double total = 0;
-        float ms = 0;
-        for (uint32_t i = 0; i < t->ev_used; i += 2) {
-            HIP_TRY(hipEventElapsedTime(&ms, t->ev_pool[i], t->ev_pool[i + 1]));
-            total += ms;
+        const uint32_t nl = t->resident[0]->ev_used / 2;
+        double total = 0, last = 0;
+        for (uint32_t i = 0; i < nl; ++i) {
+            double span = 0;
+            for (auto &r : t->resident) {
+                if (2 * i + 1 >= r->ev_used) continue;
+                float ms = 0;
+                HIP_TRY(hipSetDevice(r->dev));
+                HIP_TRY(hipEventElapsedTime(&ms, r->ev_pool[2 * i], r->ev_pool[2 * i + 1]));
+                span = std::max(span, (double)ms);
+            }
+            total += span;
+            last = span;
         }
-        stats->kernel_ms = ms;
+        stats->kernel_ms = last;
         stats->kernel_ms_total = total;
-        stats->timed_launches = t->ev_used / 2;
-        stats->values = t->last_bytes.values;
-        stats->packed_bytes = t->last_bytes.packed;
-        stats->meta_bytes = t->last_bytes.meta;
-        stats->out_bytes = t->last_bytes.out;
+        stats->timed_launches = nl;
+        for (auto &r : t->resident) {
+            stats->values += r->bytes.values;
+            stats->packed_bytes += r->bytes.packed;
+            stats->meta_bytes += r->bytes.meta;
+            stats->out_bytes += r->bytes.out;
+        }
         stats->launches = t->launches;
     }
-    t->ev_used = 0;
+    for (auto &r : t->resident) r->ev_used = 0;
     if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
     return 0;
 }
 
-int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbytes) {
-    if (!t || col >= t->d_out.size() || !t->d_out[col].p) return fail(FLS_ERR_ARG, "column %u not resident", col);
-    if (dev_ptr) *dev_ptr = t->d_out[col].p;
-    if (nbytes) *nbytes = t->res_rows * out_bytes_of(t, col);
+int fls_device_parts(const fls_table *t) { return t ? (int)t->resident.size() : 0; }
+
+int fls_device_part(const fls_table *t, uint32_t part, fls_device_part_info *out) {
+    const Resident *r = part_of(t, part);
+    if (!r || !out) return fail(FLS_ERR_ARG, "resident part %u out of range", part);
+    out->device = r->dev;
+    out->rg_begin = r->rg0;
+    out->rg_end = r->rg1;
+    out->first_row = r->first_row;
+    out->nrows = r->rows;
     return 0;
 }
 
-int fls_device_heap(fls_table *t, uint32_t col, void **dev_ptr, const void **host_ptr, uint64_t *nbytes) {
-    if (!t || col >= t->d_out.size() || !t->d_out[col].p) return fail(FLS_ERR_ARG, "column %u not resident", col);
-    const bool has = col < t->shard.d_heap.size() && t->shard.d_heap[col].p;
-    if (dev_ptr) *dev_ptr = has ? t->shard.d_heap[col].p : nullptr;
-    if (host_ptr) *host_ptr = has ? t->shard.h_heap[col].p : nullptr;
-    if (nbytes) *nbytes = has ? t->shard.d_heap[col].n : 0;
+int fls_device_part_column(fls_table *t, uint32_t part, uint32_t col, void **dev_ptr, uint64_t *nbytes) {
+    const Resident *r = part_of(t, part);
+    if (!r || col >= r->d_out.size() || !r->d_out[col].p)
+        return fail(FLS_ERR_ARG, "column %u of part %u not resident", col, part);
+    if (dev_ptr) *dev_ptr = r->d_out[col].p;
+    if (nbytes) *nbytes = r->rows * out_bytes_of(t, col);
+    return 0;
+}
+
+int fls_device_part_heap(fls_table *t, uint32_t part, uint32_t col, void **dev_ptr, const void **host_ptr,
+                         uint64_t *nbytes) {
+    const Resident *r = part_of(t, part);
+    if (!r || col >= r->d_out.size() || !r->d_out[col].p)
+        return fail(FLS_ERR_ARG, "column %u of part %u not resident", col, part);
+    const bool has = col < r->d_heap.size() && r->d_heap[col].p;
+    if (dev_ptr) *dev_ptr = has ? r->d_heap[col].p : nullptr;
+    if (host_ptr) *host_ptr = has ? r->h_heap[col].p : nullptr;
+    if (nbytes) *nbytes = has ? r->d_heap[col].n : 0;
     return has ? 1 : 0;
 }
 
+// single-GPU accessors: the table's only part (a table split over several
+// GPUs is addressed per part)
+int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbytes) {
+    if (t && t->resident.size() > 1)
+        return fail(FLS_ERR_STATE, "table is resident on %zu GPUs: use fls_device_part_column", t->resident.size());
+    return fls_device_part_column(t, 0, col, dev_ptr, nbytes);
+}
+
+int fls_device_heap(fls_table *t, uint32_t col, void **dev_ptr, const void **host_ptr, uint64_t *nbytes) {
+    if (t && t->resident.size() > 1)
+        return fail(FLS_ERR_STATE, "table is resident on %zu GPUs: use fls_device_part_heap", t->resident.size());
+    return fls_device_part_heap(t, 0, col, dev_ptr, host_ptr, nbytes);
+}
+
 int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, void *host_dst) {
-    if (!t || col >= t->d_out.size() || !t->d_out[col].p || !host_dst) return fail(FLS_ERR_ARG, "column %u not resident", col);
-    if (row > t->res_rows || n > t->res_rows - row) return fail(FLS_ERR_ARG, "rows out of range");
+    if (!t || t->resident.empty() || col >= t->meta.cols.size() || !host_dst)
+        return fail(FLS_ERR_ARG, "column %u not resident", col);
+    const uint64_t total = resident_rows(t);
+    if (row > total || n > total - row) return fail(FLS_ERR_ARG, "rows out of range");
     const int ob = out_bytes_of(t, col);
-    HIP_TRY(hipSetDevice(t->shard.dev));
-    HIP_TRY(hipStreamSynchronize(t->stream));
-    HIP_TRY(hipMemcpy(host_dst, t->d_out[col].p + row * ob, n * ob, hipMemcpyDeviceToHost));
-    // FSST: string_t pointers target the host copy of the column's heap
-    if (col < t->shard.d_heap.size() && t->shard.d_heap[col].p)
-        HIP_TRY(hipMemcpy(t->shard.h_heap[col].p, t->shard.d_heap[col].p, t->shard.d_heap[col].n, hipMemcpyDeviceToHost));
+    uint64_t at = 0;  // first resident row of the part, counted over the parts
+    for (auto &rp : t->resident) {
+        Resident &r = *rp;
+        const uint64_t a = std::max(row, at), b = std::min(row + n, at + r.rows);
+        if (a < b) {
+            HIP_TRY(hipSetDevice(r.dev));
+            HIP_TRY(hipStreamSynchronize(r.stream));
+            HIP_TRY(hipMemcpy((uint8_t *)host_dst + (a - row) * ob, r.d_out[col].p + (a - at) * ob, (b - a) * ob,
+                              hipMemcpyDeviceToHost));
+            // FSST: string_t pointers target the host copy of the part's heap
+            if (col < r.d_heap.size() && r.d_heap[col].p)
+                HIP_TRY(hipMemcpy(r.h_heap[col].p, r.d_heap[col].p, r.d_heap[col].n, hipMemcpyDeviceToHost));
+        }
+        at += r.rows;
+    }
     return 0;
 }
 
-uint64_t fls_device_rows(const fls_table *t) { return t ? t->res_rows : 0; }
+uint64_t fls_device_rows(const fls_table *t) { return t ? resident_rows(t) : 0; }
 
 }  // extern "C"

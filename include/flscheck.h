@@ -26,6 +26,10 @@ extern "C" {
 int fls_check_workload(const char *workload, double scale, uint64_t nrows_total, uint64_t row_begin,
                        uint64_t n, const void *const *d_cols, const uint8_t *out_bytes, int ncols,
                        const void *const *dicts, const int64_t *heap_delta, uint64_t *mismatches);
+/* The same on HIP device `device` (one part of a table resident on several GPUs). */
+int fls_check_workload_on(int device, const char *workload, double scale, uint64_t nrows_total, uint64_t row_begin,
+                          uint64_t n, const void *const *d_cols, const uint8_t *out_bytes, int ncols,
+                          const void *const *dicts, const int64_t *heap_delta, uint64_t *mismatches);
 const char *fls_check_last_error(void);
 
 #ifdef __cplusplus

@@ -178,26 +178,46 @@ int fls_scan_acquire(fls_table *t, fls_rowgroup *out);
 int fls_scan_release(fls_table *t, uint32_t rowgroup);
 
 /* ---- device-resident mode (HBM roofline measurement, bench.py) ---------
- * Upload row groups [rg_begin, rg_end) of the table to the connection's first
- * GPU and allocate HBM output columns for them. */
+ * Upload row groups [rg_begin, rg_end) of the table to HBM, split into
+ * contiguous parts over the connection's GPUs (as a scan shards them; a GPU
+ * gets no part when there are fewer row groups than GPUs), and allocate HBM
+ * output columns for them. */
 int fls_device_upload(fls_table *t, uint32_t rg_begin, uint32_t rg_end);
-/* Enqueue ONE decode launch over every resident vector of the selected
- * columns (col_mask NULL = all) into HBM.  Asynchronous. */
+/* Enqueue ONE decode launch per GPU over every resident vector of the
+ * selected columns (col_mask NULL = all) into HBM.  Asynchronous: the parts
+ * decode concurrently. */
 int fls_device_decode(fls_table *t, const uint8_t *col_mask);
-/* Wait for the table's GPU work; fills *stats if non-NULL (kernel_ms = last
- * launch, kernel_ms_total over the launches since the previous sync). */
+/* Wait for the table's GPU work; fills *stats if non-NULL: values and bytes
+ * summed over the parts, kernel_ms = the last launch, kernel_ms_total over the
+ * launches since the previous sync, a launch timed as its slowest part. */
 int fls_device_sync(fls_table *t, fls_decode_stats *stats);
-/* HBM address and byte size of a resident output column. */
+
+typedef struct {
+    int device;               /* HIP ordinal */
+    uint32_t rg_begin, rg_end;
+    uint64_t first_row;       /* first resident row, relative to the table's first row */
+    uint64_t nrows;
+} fls_device_part_info;
+/* Number of resident parts (GPUs holding row groups) and each one's extent. */
+int fls_device_parts(const fls_table *t);
+int fls_device_part(const fls_table *t, uint32_t part, fls_device_part_info *out);
+/* HBM address and byte size of a resident output column of one part. */
+int fls_device_part_column(fls_table *t, uint32_t part, uint32_t col, void **dev_ptr, uint64_t *nbytes);
+/* String heap of a part's resident FSST VARCHAR column (see fls_device_heap). */
+int fls_device_part_heap(fls_table *t, uint32_t part, uint32_t col, void **dev_ptr, const void **host_ptr,
+                         uint64_t *nbytes);
+/* HBM address and byte size of a resident output column (single-part tables;
+ * FLS_ERR_STATE when the table is split over several GPUs). */
 int fls_device_column(fls_table *t, uint32_t col, void **dev_ptr, uint64_t *nbytes);
 /* String heap of a resident FSST (free-text) VARCHAR column: its HBM address,
  * the host address the column's string_t pointers are based on (the heap's
  * host copy, filled by fls_device_copy_out) and its size.  Returns 1, or 0
  * (pointers NULL) for a column without one. */
 int fls_device_heap(fls_table *t, uint32_t col, void **dev_ptr, const void **host_ptr, uint64_t *nbytes);
-/* Copy rows [row, row+n) (relative to the first resident row) of a decoded
- * column into host memory. */
+/* Copy rows [row, row+n) (relative to the first resident row, counted over
+ * the parts in order) of a decoded column into host memory. */
 int fls_device_copy_out(fls_table *t, uint32_t col, uint64_t row, uint64_t n, void *host_dst);
-/* Rows resident on the device. */
+/* Rows resident on the GPUs (all parts). */
 uint64_t fls_device_rows(const fls_table *t);
 
 #ifdef __cplusplus
