@@ -70,6 +70,12 @@ uint32_t decode_waves(const DecodeGeom &geom);
 // equal tail pieces (dynamic: the waves that finish first take them).
 SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t static_pct, uint32_t pieces_per_wave,
                          std::vector<uint32_t> &pos);
+// Code-parallel FSST kernel variants (bits): kFsstPlain = escape-free rounds
+// skip the escape-state logic; kFsstTwoQ = each symbol OR-ed into both
+// qwords it spans instead of through a 64-bit accumulator; kFsstW6 =
+// registers budgeted for 6 waves per SIMD instead of 4 (the default: 82 ->
+// 80 VGPRs, l_comment 1.012 -> 0.976 ms; the other two measured slower).
+enum : int { kFsstPlain = 1, kFsstTwoQ = 2, kFsstW6 = 8, kFsstDefault = kFsstW6 };
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {
     int bytes_per_lane = 8;       // compressed bytes a lane decodes per round (8 or 16)
@@ -77,6 +83,7 @@ struct FsstLaunch {
     uint32_t *queue = nullptr;    // piece counter (overlapped launches); nullptr: contiguous ranges
     bool reset_queue = true;      // zero it first (false: drain a queue another launch started)
     int waves_per_cu = 0;         // grid: 0 = as many as fit, else at most this many per CU
+    int variant = kFsstDefault;   // code-parallel kernel variant (kFsst* bits; FLS_FSST_VARIANT)
 };
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).

@@ -366,11 +366,18 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS ui
     }
     __syncthreads();
     const uint64_t packed_total = Ov[64], aux_off = Ov[65], total = Ov[66];
-    // ---- DELTA bases after the packed area; padding
+    // ---- DELTA bases after the packed area; padding.  Each wave moves the
+    // bases of its own vectors, which its own lanes wrote to scratch in the
+    // round loop: a wave's global store and later load of the same address
+    // are ordered, while a hand-off of global memory between the waves would
+    // rely on the barrier alone (it waits for LDS traffic, lgkmcnt, not for
+    // stores still in flight, vmcnt).  The block-strided copy this replaces
+    // was the one cross-wave global hand-off in the kernel.
     if (DELTA) {
         const FLS_GLOBAL v4u *src = reinterpret_cast<const FLS_GLOBAL v4u *>(sbases);
         FLS_GLOBAL v4u *dst = reinterpret_cast<FLS_GLOBAL v4u *>(out + aux_off);
-        for (uint32_t i = threadIdx.x; i < 8 * nvec; i += blockDim.x) dst[i] = src[i];
+        for (uint32_t v = w; v < nvec; v += kEncWaves)
+            if (lane < 8) dst[8 * v + lane] = src[8 * v + lane];
     }
     {
         const uint64_t gaps[3][2] = {{meta_off + sizeof(VecMeta) * nvec, packed_off},

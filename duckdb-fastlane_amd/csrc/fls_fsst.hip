@@ -185,6 +185,30 @@ __device__ __forceinline__ uint32_t lane_codes(const Wave &w, const v4u &raw, ui
     return out;
 }
 
+// A round in which no lane holds an escape byte (and that does not start
+// inside an escape): every code is a symbol, so no entry state and no
+// literal selects.
+template <int BPL>
+__device__ __forceinline__ uint32_t lane_codes_plain(const Wave &w, const v4u &raw, uint64_t (&v)[BPL],
+                                                     uint32_t (&n)[BPL]) {
+    uint32_t out = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BPL; ++k) {
+        const uint32_t c = byte_of(raw, k);
+        v[k] = w.sym[c];
+        n[k] = w.len[c];
+        out += n[k];
+    }
+    return out;
+}
+// does any of the lane's BPL bytes equal the escape code 0xFF?  (x has an
+// 0xFF byte iff ~x has a zero byte)
+template <int BPL>
+__device__ __forceinline__ bool has_escape(const v4u &raw) {
+    auto ff = [](uint32_t x) -> uint32_t { return (~x - 0x01010101u) & x & 0x80808080u; };
+    return (BPL == 8 ? (ff(raw.x) | ff(raw.y)) : (ff(raw.x) | ff(raw.y) | ff(raw.z) | ff(raw.w))) != 0;
+}
+
 // string_t of a string of n bytes at ring byte x, host pointer p
 __device__ __forceinline__ v4u make_record_at(const lu8 *ring, uint32_t x, uint32_t n, uint64_t p) {
     const lu32 *r32 = reinterpret_cast<const lu32 *>(ring) + (x >> 2);
@@ -209,7 +233,7 @@ __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t 
     return make_record_at(w.ring, d0 - ring_base, n, ptr_base + d0);
 }
 
-template <int BPL, bool SMALL>
+template <int BPL, bool SMALL, int V>
 __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t base, uint32_t nvals,
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
                             uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err) {
@@ -360,11 +384,14 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         // wait a vmcnt(0): issued at the end of their own round, the stores'
         // latency was exposed every round)
         if (r0 > 0) retire();
-        uint32_t n[BPL], lane_end;
+        uint32_t n[BPL], lane_end = 0;
         uint64_t v[BPL];
-        const uint32_t lane_out = r0 + kRound <= comp_len
-                                      ? lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end)
-                                      : lane_codes<BPL, false>(w, raw, nb, carry_lit, lane, v, n, lane_end);
+        const bool full = r0 + kRound <= comp_len;
+        bool plain = false;
+        if constexpr ((V & kFsstPlain) != 0) plain = full && carry_lit == 0 && __ballot(has_escape<BPL>(raw)) == 0;
+        const uint32_t lane_out = plain  ? lane_codes_plain<BPL>(w, raw, v, n)
+                                  : full ? lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end)
+                                         : lane_codes<BPL, false>(w, raw, nb, carry_lit, lane, v, n, lane_end);
         const uint32_t incl = scan_incl(lane_out, lane);
         // write the round into the ring: normally all 64 lanes at once; when
         // their output would overrun the ring, the lanes that fit first, then
@@ -387,10 +414,27 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             }
             wave_sync();
             if (lane >= l0 && lane < l1) {
-                QwordWriter qw(w.ring, p0 + (incl - lane_out - done));
+                const uint32_t wp = p0 + (incl - lane_out - done);
+                if constexpr ((V & kFsstTwoQ) != 0) {
+                    // every symbol OR-ed into both qwords it spans: the shift
+                    // counts are taken mod 64 by the hardware (8 * p mod 64 is
+                    // the bit offset inside qword p / 8; ~(8p) mod 64 = 63 - it)
+                    FLS_LDS uint64_t *o64 = reinterpret_cast<FLS_LDS uint64_t *>(w.ring);
+                    uint32_t p = wp;
 #pragma unroll
-                for (uint32_t k = 0; k < BPL; ++k) qw.put(v[k], n[k]);
-                qw.finish();
+                    for (uint32_t k = 0; k < BPL; ++k) {
+                        const uint32_t b8 = p << 3;
+                        const uint64_t lo = v[k] << (b8 & 63), hi = (v[k] >> 1) >> (~b8 & 63);
+                        __hip_atomic_fetch_or(o64 + (p >> 3), lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        __hip_atomic_fetch_or(o64 + (p >> 3) + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        p += n[k];
+                    }
+                } else {
+                    QwordWriter qw(w.ring, wp);
+#pragma unroll
+                    for (uint32_t k = 0; k < BPL; ++k) qw.put(v[k], n[k]);
+                    qw.finish();
+                }
             }
             wave_sync();
             out_pos += part;
@@ -419,30 +463,51 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
 
 __device__ __forceinline__ DevChunk load_chunk(const DevChunk *chunks, uint32_t ci) {
     const FLS_GLOBAL v4u *q = reinterpret_cast<const FLS_GLOBAL v4u *>(gptr(chunks + ci));
+    // wave-uniform: the descriptor lives in SGPRs, not in 16 VGPRs
     DevChunk c;
-    v4u *d = reinterpret_cast<v4u *>(&c);
-    d[0] = q[0];
-    d[1] = q[1];
-    d[2] = q[2];
-    d[3] = q[3];
+    uint32_t *d = reinterpret_cast<uint32_t *>(&c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const v4u x = q[k];
+        d[4 * k] = uni(x.x);
+        d[4 * k + 1] = uni(x.y);
+        d[4 * k + 2] = uni(x.z);
+        d[4 * k + 3] = uni(x.w);
+    }
     return c;
 }
 
-// Vectors [item0, item1) of the launch (items numbered chunk by chunk through
-// DevChunk.vec_base): the wave loads a chunk's symbol table once and decodes
-// its vectors in order.
-template <int BPL, bool SMALL>
-__device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t item0,
-                                                     uint32_t item1, uint8_t *lds_generic, uint32_t *err_generic) {
+// The wave's vectors (items numbered chunk by chunk through DevChunk.vec_base):
+// without a queue the contiguous range [item0, item1); with one, pieces of
+// `piece` consecutive items taken from the shared counter until it runs out
+// (a wave's pieces come in increasing order, so its chunk cursor only moves
+// forward).  The wave loads a chunk's symbol table once per stay in it.
+template <int BPL, bool SMALL, bool QUEUE, int V>
+__device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t nitems,
+                                           uint32_t item0, uint32_t item1, uint32_t *queue, uint32_t piece, lu8 *L,
+                                           uint32_t *err_generic) {
     const uint64_t cp = (uint64_t)chunks_generic;
     const DevChunk *chunks = (const DevChunk *)((uint64_t)uni((uint32_t)(cp >> 32)) << 32 | uni((uint32_t)cp));
     const uint64_t ep = (uint64_t)err_generic;
     uint32_t *err = (uint32_t *)((uint64_t)uni((uint32_t)(ep >> 32)) << 32 | uni((uint32_t)ep));
-    lu8 *L = (lu8 *)(size_t)uni((uint32_t)(size_t)lds_generic);
     nchunks = uni(nchunks);
+    const uint32_t lane = __lane_id();
+    // next piece of the queue into [item0, item1); false when none is left
+    // (every wave reaches that exit)
+    auto take = [&]() -> bool {
+        uint32_t p = 0;
+        if (lane == 0) p = atomicAdd(queue, 1u);
+        p = rl(p, 0);
+        if (p >= (nitems + piece - 1) / piece) return false;
+        item0 = p * piece;
+        item1 = min(item0 + piece, nitems);
+        return true;
+    };
+    if constexpr (QUEUE) {
+        if (!take()) return;
+    }
     item0 = uni(item0);
     item1 = uni(item1);
-    const uint32_t lane = __lane_id();
     using Layout = Lds<BPL, SMALL>;
     Wave w;
     w.P = reinterpret_cast<lv4 *>(L + Layout::kOffRing);
@@ -460,7 +525,12 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     uint32_t ci = lo;
     DevChunk c = load_chunk(chunks, ci);
     bool have_table = false;
-    for (uint32_t item = item0; item < item1;) {
+    for (uint32_t item = item0;;) {
+        if (item >= item1) {
+            if constexpr (!QUEUE) break;
+            if (!take()) break;
+            item = item0;
+        }
         const uint32_t v = item - uni(c.vec_base);
         if (v >= uni(c.nvec)) {  // next chunk
             if (++ci >= nchunks) break;
@@ -492,7 +562,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
         const uint32_t nvals = uni(meta->nvals);
         const uint32_t W = uni(min((uint32_t)meta->bw, 32u));
         const uint32_t dbytes = uni(meta->aux_count);
-        fsst_vector<BPL, SMALL>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
+        fsst_vector<BPL, SMALL, V>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
                     (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
                     gptr(c.out) + 16ull * kVectorSize * v, lane, err);
         wave_sync();
@@ -507,39 +577,38 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
 // runs beside the main decode kernel and the full grid that follows it, one
 // atomic per piece, so no vector is decoded twice and late waves find work.
 // (A piece queue for standalone launches measured 2-4 % slower on l_comment
-// at SF10: more symbol-table reloads.)
-// (QUEUE is a template parameter: one kernel holding both loops needed 98
-// VGPRs instead of 82 for <8, small>, one wave per SIMD less.)
-template <int BPL, bool SMALL, bool QUEUE>
-__global__ __launch_bounds__(64, 4) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+// at SF10: more symbol-table reloads.)  The piece loop is the range loop's
+// own (a loop around the range decoder needed 98-124 VGPRs instead of 82).
+#ifndef FLS_FSST_WAVES
+#define FLS_FSST_WAVES 4  // minimum waves per SIMD the register budget must allow
+#endif
+template <int BPL, bool SMALL, bool QUEUE, int V>
+__global__ __launch_bounds__(64, (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                      uint32_t nitems, uint32_t *__restrict__ err,
                                                      uint32_t *__restrict__ queue, uint32_t piece) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw_generic[];
+    // an LDS-typed pointer to the dynamic LDS (a known constant address, so
+    // table and ring offsets fold into the DS instructions' offset fields)
+    lu8 *lds_raw = (lu8 *)lds_raw_generic;
+    uint32_t i0 = 0, i1 = 0;
     if (!QUEUE) {
         const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
         const uint32_t per = (nitems + nwaves - 1) / nwaves;
-        const uint32_t i0 = min(wave * per, nitems), i1 = min(i0 + per, nitems);
-        if (i0 < i1) fsst_range<BPL, SMALL>(chunks, nchunks, i0, i1, lds_raw, err);
-        return;
+        i0 = min(wave * per, nitems);
+        i1 = min(i0 + per, nitems);
+        if (i0 >= i1) return;
     }
-    for (;;) {
-        uint32_t p = 0;
-        if (__lane_id() == 0) p = atomicAdd(queue, 1u);
-        p = rl(p, 0);
-        if (p >= (nitems + piece - 1) / piece) break;  // every wave reaches this exit
-        const uint32_t i0 = p * piece;
-        fsst_range<BPL, SMALL>(chunks, nchunks, i0, min(i0 + piece, nitems), lds_raw, err);
-    }
+    fsst_range<BPL, SMALL, QUEUE, V>(chunks, nchunks, nitems, i0, i1, queue, piece, lds_raw, err);
 }
 
-template <int BPL, bool SMALL, bool QUEUE>
+template <int BPL, bool SMALL, bool QUEUE, int V>
 hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     const uint32_t shmem = Lds<BPL, SMALL>::kWave;
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL, QUEUE>, 64, shmem) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL, QUEUE, V>, 64, shmem) !=
             hipSuccess)
             per_cu = 1;
     }
@@ -552,17 +621,35 @@ hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         if (e != hipSuccess) return e;
     }
     if (getenv("FLS_DEBUG"))
-        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors%s\n", BPL,
-                SMALL ? "small" : "any", grid, per_cu, shmem, nvecs, how.queue ? " (piece queue)" : "");
-    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL, QUEUE>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs,
+        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: variant %d, %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors%s\n",
+                BPL, SMALL ? "small" : "any", V, grid, per_cu, shmem, nvecs, how.queue ? " (piece queue)" : "");
+    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL, QUEUE, V>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs,
                        d_err, how.queue, piece);
     return hipGetLastError();
 }
+template <int BPL, bool SMALL, int V>
+hipError_t launch_fsst_v(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
+                         hipStream_t stream, const FsstLaunch &how) {
+    return how.queue ? launch_fsst_q<BPL, SMALL, true, V>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                     : launch_fsst_q<BPL, SMALL, false, V>(d_chunks, nchunks, nvecs, d_err, stream, how);
+}
+// code-parallel variants (FsstLaunch::variant, FLS_FSST_VARIANT): BPL = 8
+// instantiates the ones A/B-measured (profiles/r2/abenv_fsst_var*.txt),
+// BPL = 16 only the default
 template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
-    return how.queue ? launch_fsst_q<BPL, SMALL, true>(d_chunks, nchunks, nvecs, d_err, stream, how)
-                     : launch_fsst_q<BPL, SMALL, false>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    if constexpr (BPL == 8) {
+        switch (how.variant & 15) {
+        case 0: return launch_fsst_v<BPL, SMALL, 0>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstPlain: return launch_fsst_v<BPL, SMALL, kFsstPlain>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstTwoQ: return launch_fsst_v<BPL, SMALL, kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstW6 | kFsstTwoQ:
+            return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        default: return launch_fsst_v<BPL, SMALL, kFsstW6>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        }
+    }
+    return launch_fsst_v<BPL, SMALL, kFsstDefault>(d_chunks, nchunks, nvecs, d_err, stream, how);
 }
 
 // ============================================================================

@@ -708,6 +708,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     const OverlapSplit ov = overlap_split();
     FsstLaunch small, any;
     small.bytes_per_lane = any.bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
+    if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 15;
     small.small = true;
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && (fc.sp_vecs + fc.cp_vecs) > 0 &&
                          !d_split && !sp && !(policy & POLICY_STATIC);

@@ -46,9 +46,26 @@ def main():
         if any(diffs):
             bad += 1
             print(col[0], diffs, "repeats agree" if all(x == diffs[0] for x in diffs) else "REPEATS DIFFER")
-    # the whole mixed file too
-    cpu = fl.write_image(cols, rowgroup=a.rowgroup).tobytes()
-    same = [fl.write_image(cols, rowgroup=a.rowgroup, device=0).tobytes() == cpu for _ in range(a.reps)]
+    # the whole mixed file too; a differing one is localised: the first
+    # differing byte offsets and the (column, row group) chunks whose decode
+    # (oracle) differs from the CPU file's
+    cpu_img = fl.write_image(cols, rowgroup=a.rowgroup)
+    cpu = cpu_img.tobytes()
+    same = []
+    for _ in range(a.reps):
+        g_img = fl.write_image(cols, rowgroup=a.rowgroup, device=0)
+        g = g_img.tobytes()
+        same.append(g == cpu)
+        if g != cpu:
+            from oracle import flsref as ref
+            x, y = np.frombuffer(cpu, np.uint8), np.frombuffer(g, np.uint8)
+            m = min(len(x), len(y))
+            d = np.nonzero(x[:m] != y[:m])[0]
+            rc, rg_ = ref.RefFile(cpu_img), ref.RefFile(g_img)
+            badc = [(c, r) for c in range(rc.ncols) for r in range(rc.nrowgroups)
+                    if not np.array_equal(rc.decode(c, r), rg_.decode(c, r))]
+            print(f"  differs: sizes {len(x)}/{len(y)}, {d.size} bytes, first at {d[:6].tolist()}; "
+                  f"chunks decoding differently (col, rg): {badc[:12]} ({len(badc)})", flush=True)
     print(f"n={a.n} rowgroup={a.rowgroup} only={a.only} ({len(cols)} columns): mixed file identical:", same,
           "columns differing alone:", bad)
 
