@@ -1,0 +1,49 @@
+"""Register budgets of the shipped gfx950 kernels, read from the built
+library's code-object metadata on the CPU (scripts/kernel_resources.py).
+They pin the occupancy design points DESIGN.md states: the encoder kernels
+spill nothing (a 6-wave build that spilled 6 VGPRs wrote wrong T=32 DELTA
+rows), the main decode kernel fits 4 waves per SIMD,
+the default code-parallel FSST kernel 6."""
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "scripts"))
+LIB = ROOT / "duckdb-fastlane_amd" / "libflsgpu.so"
+
+
+@pytest.fixture(scope="module")
+def res():
+    if not LIB.exists():
+        pytest.skip("libflsgpu.so not built")
+    import kernel_resources
+    r = kernel_resources.resources(str(LIB))
+    assert r, "no gfx950 code object in libflsgpu.so"
+    return r
+
+
+def _find(res, *parts):
+    hits = {k: v for k, v in res.items() if all(p in k for p in parts)}
+    assert hits, parts
+    return hits
+
+
+def test_encoder_kernels_do_not_spill(res):
+    for name, r in _find(res, "encode_kernel").items():
+        assert r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
+    narrow = _find(res, "encode_kernelIj")  # T <= 32: 5 waves per SIMD
+    assert all(r["vgpr"] <= 96 for r in narrow.values()), narrow
+
+
+def test_decode_kernel_fits_four_waves(res):
+    for name, r in _find(res, "decode_kernel").items():
+        assert r["vgpr"] + r["agpr"] <= 128, (name, r)
+
+
+def test_default_fsst_kernel_fits_six_waves(res):
+    # fsst_kernel<8, SMALL, QUEUE, kFsstW6 = 8>
+    hits = _find(res, "fsst_kernelILi8E", "ELi8EEEv")
+    assert len(hits) == 4, hits
+    assert all(r["vgpr"] <= 80 for r in hits.values()), hits
