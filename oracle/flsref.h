@@ -18,6 +18,36 @@
  * known-answer tests, an independent numpy restatement (oracle/flsref_np.py)
  * and the seeded generators' ground truth (integer codecs are lossless).
  *
+ * Upstream facts this restatement assumes (what an upstream .fls fixture or
+ * the cwida/FastLanes sources would have to confirm; each is checked against
+ * the restatement mechanically by the named test):
+ *   F1 interleaved packing: vector = 1024 values, 1024/T lanes; value at
+ *      (row r, lane l) starts in word floor(rW/T)*(1024/T)+l at bit (rW) mod T
+ *      and straddles into the next word of the same lane; W = 0 stores no
+ *      bytes, W = T is the identity layout.  Matches SURVEY.md section 5
+ *      bit for bit (tests/test_oracle.py::test_survey_layout_statements,
+ *      test_kat_pack_t32_w7, test_kat_pack_t64_w64_identity).
+ *   F2 FFOR: value = base + unpacked, wrapping at T bits, base = the
+ *      vector's minimum (sign-extended T-bit); W = bit width of max - min.
+ *   F3 DELTA, unified transposed order FL_ORDER = {0,4,2,6,1,5,3,7}:
+ *      position p = 128a + 16b + l holds tuple 128*FL_ORDER[b] + 16a + l
+ *      (flsref_tau).  Each lane holds one delta chain, tuples blk*16T + l + 16k,
+ *      k = 0..T-1, with one base (its first tuple) per lane, 1024/T bases =
+ *      128 bytes per vector.  For T = 64 the lane's tuple SET equals SURVEY's
+ *      index(r,l) = FL_ORDER[r/8]*16 + (r%8)*128 + l; the ROW ORDER differs by
+ *      the fixed permutation r -> 8*FL_ORDER[r/8] + FL_ORDER[r%8]
+ *      (test_survey_layout_statements).  Which row order upstream stores is
+ *      the open fact; an adapter for the other one is that permutation.
+ *   F4 DICT: codes FFOR-packed at T = 32, value = dict[code]; VARCHAR
+ *      dictionaries decode to DuckDB string_t (16 B, <= 12 bytes inline).
+ *   F5 RLE (FastLanes-RLE): per vector a u16 run index per value, DELTA(T=16)
+ *      coded as in F3, plus the run values; value = runs[index].
+ *   F6 ALP: value = (float)digits * 10^f * 10^-e with per-vector (e, f) and
+ *      exceptions patched by position; FSST: 255-symbol table of <= 8-byte
+ *      symbols, code 255 escapes one literal byte.
+ *   The container around the vectors (FLSAMD01 header, chunk headers, VecMeta,
+ *   footer) is this repo's own; upstream's .fls framing is unknown here.
+ *
  * Call sites of the replaced decode in the reference:
  *   src/fastlanes_facade.cpp:33  fastlanes::connect()
  *   src/fastlanes_facade.cpp:34  Connection::read_fls(path)

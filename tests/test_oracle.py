@@ -106,3 +106,41 @@ def test_numpy_restatement_decodes_container(fl, ref):
     for c, dt in [(0, np.uint64), (1, np.uint32), (2, np.uint16)]:
         got_np = np.array(flsref_np.decode_chunk(f, c, 0), dtype=np.uint64).astype(dt)
         assert np.array_equal(got_np, rf.decode(c, 0).view(dt))
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_survey_layout_statements(ref, T):
+    """SURVEY.md section 5's statements of the FastLanes layout, checked
+    mechanically against the C restatement:
+      * interleaved packing (every T), bit by bit: the W-bit value at (row r,
+        lane l) starts in packed word floor(r W / T) * (1024 / T) + l at bit
+        (r W) mod T and straddles into the next word of the same lane;
+      * unified transposed order (T = 64): SURVEY's index(r, l) =
+        FL_ORDER[r / 8] * 16 + (r % 8) * 128 + l puts in lane l exactly the
+        tuples this restatement does (the delta chain l + 16 k, base tuple l),
+        but in another row order: SURVEY's row r is this layout's row
+        8 FL_ORDER[r / 8] + FL_ORDER[r % 8] of the same lane.  That fixed row
+        permutation is the one layout fact an upstream fixture would decide
+        (oracle/flsref.h, "Upstream facts")."""
+    lanes = 1024 // T
+    rng = np.random.default_rng(100 + T)
+    for W in sorted({1, 3, T // 2 + 1, T - 1, T}):
+        vals = np.array([int.from_bytes(rng.bytes(8), "little") & ((1 << W) - 1) for _ in range(1024)],
+                        dtype=np.uint64)
+        words = np.frombuffer(ref.pack(T, W, vals), dtype=f"<u{T // 8}")
+        assert words.size == W * lanes
+        for p in rng.integers(0, 1024, 64):
+            r, l = divmod(int(p), lanes)
+            k, b = divmod(r * W, T)
+            lo = int(words[k * lanes + l]) >> b
+            if b + W > T:
+                lo |= int(words[(k + 1) * lanes + l]) << (T - b)
+            assert lo & ((1 << W) - 1) == int(vals[p]), (T, W, r, l)
+    if T == 64:
+        order = (0, 4, 2, 6, 1, 5, 3, 7)
+        for l in range(16):
+            survey = [order[r // 8] * 16 + (r % 8) * 128 + l for r in range(64)]
+            ours = [ref.tau(r * 16 + l) for r in range(64)]
+            assert sorted(survey) == sorted(ours) == [l + 16 * k for k in range(64)]
+            for r in range(64):
+                assert survey[r] == ours[8 * order[r // 8] + order[r % 8]]
