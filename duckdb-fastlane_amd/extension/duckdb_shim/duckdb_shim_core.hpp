@@ -163,6 +163,7 @@ public:
     Value() : type_(LogicalType::SQLNULL), is_null_(true) {}
     Value(const string &s) : type_(LogicalType::VARCHAR), is_null_(false), str_(s) {}  // NOLINT
     Value(const char *s) : Value(string(s)) {}                                          // NOLINT
+    Value(const string_t &s) : Value(s.GetString()) {}                                  // NOLINT (DuckDB: Value(string_t))
     static Value INTEGER(int32_t v) { return Value(LogicalType::INTEGER, (int64_t)v); }
     static Value BIGINT(int64_t v) { return Value(LogicalType::BIGINT, v); }
     static Value TINYINT(int8_t v) { return Value(LogicalType::TINYINT, (int64_t)v); }

@@ -342,6 +342,41 @@ void fls_ext_close(fls_ext_db *d) { delete d; }
 
 int fls_ext_has_function(fls_ext_db *d, const char *name) { return d && d->db.table_functions.count(name) ? 1 : 0; }
 
+// 1 when every overload of table function fn registers named parameter name
+// with logical type id type_id (0: any type)
+int fls_ext_has_named_parameter(fls_ext_db *d, const char *fn, const char *name, int type_id) {
+    if (!d) return 0;
+    auto range = d->db.table_functions.equal_range(fn);
+    if (range.first == range.second) return 0;
+    for (auto it = range.first; it != range.second; ++it) {
+        auto p = it->second.named_parameters.find(name);
+        if (p == it->second.named_parameters.end()) return 0;
+        if (type_id && (int)p->second.id() != type_id) return 0;
+    }
+    return 1;
+}
+
+// SELECT name() for a zero-argument scalar function: its one VARCHAR value
+// rendered into buf (cap bytes); -1 when there is no such function
+int fls_ext_scalar0(fls_ext_db *d, const char *name, char *buf, int cap) {
+    if (!d) return -1;
+    auto it = d->db.scalar_functions.find(name);
+    if (it == d->db.scalar_functions.end() || !it->second.arguments.empty()) return -1;
+    try {
+        DataChunk args;
+        args.SetCardinality(1);
+        ExpressionState state;
+        Vector result(it->second.return_type);
+        it->second.function(args, state, result);
+        const string v = result.GetValue(0).ToString();
+        snprintf(buf, cap, "%s", v.c_str());
+        return (int)v.size();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 static std::vector<FilterSpec> make_where(const int *fcols, const char *const *fexprs, int nfilters) {
     std::vector<FilterSpec> w;
     for (int i = 0; i < nfilters; ++i) w.push_back(FilterSpec{fcols[i], fexprs[i] ? fexprs[i] : ""});

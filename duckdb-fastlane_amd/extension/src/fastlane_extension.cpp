@@ -1,9 +1,11 @@
 // fastlane_extension.cpp -- extension entry points (reference
 // src/fastlane_extension.cpp:94-124): the same two C symbols and class.
 // Load registers the reference's compiled `scan_fastlanes` plus what the
-// reference wrote but never registered (:44-90): the typed GPU scan (here
-// `read_fastlanes`, VARCHAR and LIST(VARCHAR)), the .fls/.fastlane replacement
-// scan, and the COPY TO (FORMAT fls | fastlane) writer.
+// reference wrote but never registered (:44-90): the SQL scalar
+// `fastlane_version()` (:32-42, used at examples/basic_usage.sql:8), the typed
+// GPU scan (here `read_fastlanes`, VARCHAR and LIST(VARCHAR)), the
+// .fls/.fastlane replacement scan, and the COPY TO (FORMAT fls | fastlane)
+// writer.
 #define DUCKDB_EXTENSION_MAIN
 
 #include "fastlane_extension.hpp"
@@ -15,7 +17,18 @@
 
 namespace duckdb {
 
+namespace {
+// SELECT fastlane_version(): the reference's constant text
+// (src/fastlane_extension.cpp:38-41), one constant VARCHAR
+void FastlaneVersionFn(DataChunk &, ExpressionState &, Vector &result) {
+    result.SetValue(0, StringVector::AddString(result, "FastLanes Extension v1.0.0"));
+    result.SetVectorType(VectorType::CONSTANT_VECTOR);
+}
+}  // namespace
+
 void FastlaneExtension::Load(DuckDB &db) {
+    ExtensionUtil::RegisterFunction(*db.instance,
+                                    ScalarFunction("fastlane_version", {}, LogicalType::VARCHAR, FastlaneVersionFn));
     ScanFastLanes::Register(*db.instance);
     ext_fastlane::RegisterReadFastlanes(*db.instance);
     ext_fastlane::RegisterFastlaneCopyFunction(*db.instance);

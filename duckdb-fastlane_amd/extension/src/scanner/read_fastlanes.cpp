@@ -394,6 +394,9 @@ TableFunction ReadFastlanesFunction() {
     fn.projection_pushdown = true;
     fn.filter_pushdown = true;
     fn.filter_prune = true;
+    // accepted like the intended scanner's (src/scanner/scan_fastlanes.cpp:156),
+    // which never reads it either: the schema always comes from the footer
+    fn.named_parameters["auto_detect"] = LogicalType::BOOLEAN;
     return fn;
 }
 

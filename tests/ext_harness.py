@@ -43,6 +43,19 @@ class Ext:
     def has_function(self, name: str) -> bool:
         return bool(self.lib.fls_ext_has_function(self.db, name.encode()))
 
+    def has_named_parameter(self, fn: str, name: str, type_id: int = 0) -> bool:
+        f = self.lib.fls_ext_has_named_parameter
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int]
+        return bool(f(self.db, fn.encode(), name.encode(), type_id))
+
+    def scalar0(self, name: str):
+        """SELECT name() for a zero-argument scalar function (None: not registered)"""
+        f = self.lib.fls_ext_scalar0
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int]
+        buf = C.create_string_buffer(256)
+        n = f(self.db, name.encode(), buf, 256)
+        return None if n < 0 else buf.value.decode()
+
     @staticmethod
     def _where(where):
         """where: [(table column, expr)], expr per fls_ext_harness.cpp (e.g.

@@ -40,6 +40,20 @@ def test_registered_functions(ext):
     assert ext.has_function("read_fastlanes")
 
 
+def test_fastlane_version_scalar(ext):
+    # SELECT fastlane_version() (reference src/fastlane_extension.cpp:32-42,
+    # examples/basic_usage.sql:8): the reference's constant text
+    assert ext.scalar0("fastlane_version") == "FastLanes Extension v1.0.0"
+    assert ext.scalar0("no_such_function") is None
+
+
+def test_read_fastlanes_accepts_auto_detect(ext):
+    # named parameter of the intended scanner (src/scanner/scan_fastlanes.cpp:156),
+    # BOOLEAN (LogicalTypeId 2), on both the VARCHAR and the LIST(VARCHAR) overload
+    assert ext.has_named_parameter("read_fastlanes", "auto_detect", 2)
+    assert not ext.has_named_parameter("read_fastlanes", "no_such_option")
+
+
 def test_nonexistent_file_error_verbatim(ext):
     # test/sql/fastlane.test:8-12
     with pytest.raises(ExtError, match="^Failed to open FastLanes file: nonexistent.fls$"):
