@@ -361,7 +361,7 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS ui
             Ov[64] = packed_total;
             Ov[65] = aux_off;
             Ov[66] = total;
-            *(FLS_GLOBAL uint64_t *)c.len_out = total;
+            *(FLS_GLOBAL uint64_t *)c.len_out = total | (uint64_t)(DELTA ? ENC_DELTA : ENC_FFOR) << kEncShift;
         }
     }
     __syncthreads();
@@ -388,6 +388,72 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS ui
     }
 }
 
+// ENC_AUTO on the GPU: the encoding fls_writer.cpp encode_int_chunk(ENC_AUTO)
+// picks, from the same estimates computed the same way -- per vector the
+// FFOR width of the values and of their transposed deltas (the tail padded
+// with the last value, as load_vec does), and the chunk's runs (adjacent
+// values that differ, over its nrows values):
+//   FFOR  sum(128 W + 32)          DELTA sum(128 W + 32 + 128)
+//   RLE   runs (T/8) + nvec (32 + 128 + 640), none when 4 runs > nrows
+//   DICT  the host's estimate (c.est_dict: a distinct count needs a hash set)
+// smallest wins, ties to the earlier of FFOR, DELTA, RLE, DICT.  One extra
+// read of the chunk's values.  Returns the encoding (block-uniform).
+template <int T>
+__device__ uint8_t choose_encoding(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS uint64_t *acc) {
+    using S = Sto<T>;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    FLS_LDS S *V = Vall + w * kVectorSize;
+    const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
+    const uint8_t *in = (const uint8_t *)c.in;
+    if (threadIdx.x < 3) acc[threadIdx.x] = 0;
+    __syncthreads();
+    uint64_t ffor = 0, delta = 0, diffs = 0;  // this wave's sums
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
+        stage_values<T>(in, v, vn, V, lane);
+        wave_sync();
+        S x[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) x[k] = V[lane + 64 * k];
+        const VecStat f = analyze_regs<T>(x);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) x[k] = pos_value<T, true>(V, lane + 64 * k);
+        const VecStat d = analyze_regs<T>(x);
+        ffor += 128u * f.W + 32u;
+        delta += 128u * d.W + 32u + 128u;
+        // values that differ from their predecessor (row 0 of the vector
+        // against the previous vector's last value)
+        uint32_t nd = 0;
+        for (uint32_t j = lane; j < vn; j += 64)
+            if (j > 0) nd += V[j] != V[j - 1] ? 1u : 0u;
+        if (lane == 0 && v > 0) {
+            using U = typename std::conditional<T == 8, uint8_t,
+                      typename std::conditional<T == 16, uint16_t,
+                      typename std::conditional<T == 32, uint32_t, uint64_t>::type>::type>::type;
+            const U last = ((const FLS_GLOBAL U *)in)[(size_t)v * kVectorSize - 1];
+            nd += (S)last != V[0];
+        }
+        for (int o = 32; o >= 1; o >>= 1) nd += __shfl_xor(nd, o, 64);
+        diffs += nd;
+        wave_sync();
+    }
+    if (lane == 0) {
+        __hip_atomic_fetch_add(acc + 0, ffor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(acc + 1, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(acc + 2, diffs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    const uint64_t e_ffor = acc[0], e_delta = acc[1], runs = acc[2] + 1;
+    const uint64_t e_rle = runs * 4 > n ? UINT64_MAX : runs * (T / 8) + (uint64_t)nvec * (32 + 128 + 640);
+    uint64_t best = e_ffor;
+    uint8_t enc = ENC_FFOR;
+    if (e_delta < best) { best = e_delta; enc = ENC_DELTA; }
+    if (e_rle < best) { best = e_rle; enc = ENC_RLE; }
+    if (c.est_dict < best) { best = c.est_dict; enc = ENC_DICT; }
+    __syncthreads();  // acc and V are reused by the encode
+    return enc;
+}
+
 // One kernel per storage width: S = uint64_t for T = 64 chunks, uint32_t for
 // T <= 32 (half the LDS and VGPRs: more waves per SIMD for the narrow types).
 // The narrow kernel runs at 5 waves per SIMD (93 VGPRs, no spills): INT32
@@ -408,7 +474,23 @@ __global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) voi
     FLS_LDS uint32_t *W = (FLS_LDS uint32_t *)Wv;
     FLS_LDS int64_t *B = (FLS_LDS int64_t *)Bv;
     FLS_LDS uint64_t *O = (FLS_LDS uint64_t *)Ov;
-    const bool delta = c.enc == ENC_DELTA;
+    uint8_t enc = c.enc;
+    if (enc == ENC_AUTO) {
+        if constexpr (sizeof(S) == 8) {
+            enc = choose_encoding<64>(c, V, O);
+        } else {
+            switch (c.T) {
+            case 8: enc = choose_encoding<8>(c, V, O); break;
+            case 16: enc = choose_encoding<16>(c, V, O); break;
+            default: enc = choose_encoding<32>(c, V, O); break;
+            }
+        }
+        if (enc != ENC_FFOR && enc != ENC_DELTA) {  // RLE / DICT: the host encodes it
+            if (threadIdx.x == 0) *(FLS_GLOBAL uint64_t *)c.len_out = (uint64_t)enc << kEncShift;
+            return;
+        }
+    }
+    const bool delta = enc == ENC_DELTA;
     if constexpr (sizeof(S) == 8) {
         delta ? encode_chunk<64, true>(c, V, W, B, O) : encode_chunk<64, false>(c, V, W, B, O);
     } else {
@@ -425,7 +507,7 @@ __global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) voi
 uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
     const uint64_t nvec = (nrows + kVectorSize - 1) / kVectorSize;
     const uint64_t packed_off = (sizeof(ChunkHeader) + sizeof(VecMeta) * nvec + 15) & ~15ull;
-    const uint64_t aux = enc == ENC_DELTA ? 128ull * nvec : 0ull;
+    const uint64_t aux = enc == ENC_DELTA || enc == ENC_AUTO ? 128ull * nvec : 0ull;  // AUTO may pick DELTA
     return (packed_off + 128ull * T * nvec + aux + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
 }
 
@@ -503,7 +585,7 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
         c.T = (uint8_t)T;
         c.enc = encoding;
         c.pad[0] = c.pad[1] = 0;
-        c.pad2 = 0;
+        c.est_dict = UINT64_MAX;
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipError_t e = hipMemcpy(d_desc, desc.data(), nrg * sizeof(EncChunk), hipMemcpyHostToDevice);
@@ -516,6 +598,8 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
     float ms = 0;
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
     if (e == hipSuccess) e = hipMemcpy(chunk_lens, d_lens, nrg * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess)  // the kernel puts the encoding in the top byte
+        for (uint64_t i = 0; i < nrg; ++i) chunk_lens[i] &= (1ull << kEncShift) - 1;
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);
     hipFree(d_desc);

@@ -13,10 +13,14 @@ struct EncChunk {
     uint64_t len_out;  // device address of a uint64: the chunk's byte length (written)
     uint64_t scratch;  // device address of enc_scratch_bytes() bytes (the DELTA chain bases)
     uint32_t nrows;    // rows of the chunk (1..65536)
-    uint8_t T, enc;    // packing width 8/16/32/64; ENC_FFOR or ENC_DELTA
+    uint8_t T, enc;    // packing width 8/16/32/64; ENC_FFOR, ENC_DELTA or ENC_AUTO
     uint8_t pad[2];
-    uint64_t pad2;
+    uint64_t est_dict; // ENC_AUTO: the host's DICT size estimate (UINT64_MAX: DICT not worth it)
 };
+// *len_out = chunk bytes | encoding << kEncShift.  ENC_AUTO chunks that choose
+// RLE or DICT are not encoded on the GPU: length 0, the encoding in the top
+// byte, and the host encodes them (fls_writer.cpp GpuEncoder::complete).
+constexpr int kEncShift = 56;
 static_assert(sizeof(EncChunk) == 48, "EncChunk is 48 B");
 
 // Scratch bytes per chunk: 64 x 128 B of DELTA chain bases (their place in

@@ -316,20 +316,78 @@ std::vector<uint8_t> str_dict_bytes(const std::vector<std::string_view> &entries
     return d;
 }
 
-std::vector<uint8_t> enc_dict_str(const uint32_t *offs, const char *bytes, uint32_t n) {
-    std::unordered_map<std::string_view, uint32_t> idx;
+// Dictionary of a chunk's strings in first-appearance order plus the codes,
+// one pass over the rows with an open-addressing table of (hash, entry)
+// (a std::unordered_map<string_view> here cost 2 hash-map passes per row and
+// bounded the ENC_AUTO writer at ~18 M rows/s on 16 threads).  Stops, and
+// returns false, once more than `limit` distinct strings are seen.
+struct StrDict {
     std::vector<std::string_view> entries;
-    std::vector<uint32_t> codes(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        std::string_view s(bytes + offs[i], offs[i + 1] - offs[i]);
-        auto it = idx.find(s);
-        if (it == idx.end()) {
-            it = idx.emplace(s, (uint32_t)entries.size()).first;
-            entries.push_back(s);
-        }
-        codes[i] = it->second;
+    std::vector<uint32_t> codes;
+    uint64_t entry_bytes = 0;  // sum of the entries' lengths
+};
+static inline uint64_t str_hash(const char *p, uint32_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
     }
-    return enc_dict_codes(codes.data(), n, 0, true, str_dict_bytes(entries), (uint32_t)entries.size());
+    uint64_t w = 0;
+    memcpy(&w, p + i, n - i);
+    h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 29);
+}
+bool build_str_dict(const uint32_t *offs, const char *bytes, uint32_t n, uint32_t limit, StrDict &d) {
+    size_t cap = 16;
+    while (cap < 2ull * (std::min(limit, n) + 1)) cap <<= 1;
+    // (hash high 32 bits << 32) | (entry + 1); 0 = empty.  Kept per thread:
+    // fresh 100+ KiB vectors per chunk are mmap'd and page-faulted, and the
+    // faults serialise the column threads
+    thread_local std::vector<uint64_t> slot;
+    slot.assign(cap, 0);
+    const size_t mask = cap - 1;
+    d.entries.clear();
+    d.codes.resize(n);
+    d.entry_bytes = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const char *p = bytes + offs[i];
+        const uint32_t len = offs[i + 1] - offs[i];
+        const uint64_t h = str_hash(p, len);
+        const uint64_t tag = h >> 32 << 32;
+        size_t k = (size_t)h & mask;
+        for (;;) {
+            const uint64_t e = slot[k];
+            if (e == 0) {
+                if (d.entries.size() >= limit) return false;
+                d.entries.emplace_back(p, len);
+                d.entry_bytes += len;
+                slot[k] = tag | d.entries.size();
+                d.codes[i] = (uint32_t)d.entries.size() - 1;
+                break;
+            }
+            if ((e & ~0xFFFFFFFFull) == tag) {
+                const std::string_view &sv = d.entries[(uint32_t)e - 1];
+                if (sv.size() == len && memcmp(sv.data(), p, len) == 0) {
+                    d.codes[i] = (uint32_t)e - 1;
+                    break;
+                }
+            }
+            k = (k + 1) & mask;
+        }
+    }
+    return true;
+}
+
+std::vector<uint8_t> enc_dict_str(const StrDict &d, uint32_t n) {
+    return enc_dict_codes(d.codes.data(), n, 0, true, str_dict_bytes(d.entries), (uint32_t)d.entries.size());
+}
+std::vector<uint8_t> enc_dict_str(const uint32_t *offs, const char *bytes, uint32_t n) {
+    StrDict d;
+    build_str_dict(offs, bytes, n, n, d);
+    return enc_dict_str(d, n);
 }
 
 // ---- FSST (VARCHAR) ----------------------------------------------------------
@@ -506,18 +564,17 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
     return assemble_chunk(ENC_FSST, 32, 0, true, n, vecs, table, (uint32_t)st.n, heap);
 }
 
-// VARCHAR: DICT when the distinct values are few, else FSST
+// VARCHAR: DICT when the distinct values are few (at most n / 8, and their
+// bytes + 4 each under half the chunk's bytes), else FSST.  ENC_AUTO builds
+// the dictionary once: it is the estimate and, when DICT wins, the encoding.
 std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const char *bytes, uint32_t n) {
-    if (enc == ENC_AUTO) {
-        std::unordered_map<std::string_view, uint32_t> seen;
-        uint64_t dict_bytes = 0;
-        for (uint32_t i = 0; i < n && seen.size() <= n / 8; ++i) {
-            std::string_view sv(bytes + offs[i], offs[i + 1] - offs[i]);
-            if (seen.emplace(sv, 0).second) dict_bytes += sv.size() + 4;
-        }
-        enc = seen.size() <= n / 8 && dict_bytes < (uint64_t)(offs[n] - offs[0]) / 2 ? ENC_DICT : ENC_FSST;
-    }
-    return enc == ENC_FSST ? enc_fsst(offs, bytes, n) : enc_dict_str(offs, bytes, n);
+    if (enc == ENC_FSST) return enc_fsst(offs, bytes, n);
+    StrDict d;
+    const bool few = build_str_dict(offs, bytes, n, enc == ENC_AUTO ? n / 8 : n, d);
+    if (enc == ENC_AUTO &&
+        !(few && d.entry_bytes + 4ull * d.entries.size() < (uint64_t)(offs[n] - offs[0]) / 2))
+        return enc_fsst(offs, bytes, n);
+    return enc_dict_str(d, n);
 }
 
 // FastLanes-RLE: per vector run values + run-index vector (u16) DELTA-coded
@@ -748,6 +805,27 @@ size_t est_dict(int T, const uint64_t *vals, uint32_t n) {
     const size_t d = tab.count;
     if (d > 65536) return SIZE_MAX;
     return d * (T / 8) + ((n + 1023) / 1024) * (32 + 128 * (size_t)bitlen(d - 1 ? d - 1 : 0));
+}
+
+// est_dict over a column chunk held in its own width (T/8 bytes per value):
+// the 1,024-value sample reads the typed values directly, so the common
+// high-cardinality case converts nothing (the GPU ENC_AUTO path)
+uint64_t load_typed(const uint8_t *p, int T, uint64_t i) {
+    uint64_t x = 0;
+    memcpy(&x, p + i * (T / 8), T / 8);
+    return x;
+}
+size_t est_dict_typed(int T, const void *data, uint32_t n) {
+    const uint8_t *p = (const uint8_t *)data;
+    if (n > 4096) {
+        uint64_t smp[1024];
+        for (uint32_t i = 0; i < 1024; ++i) smp[i] = load_typed(p, T, (uint64_t)i * n / 1024);
+        std::sort(smp, smp + 1024);
+        if (std::unique(smp, smp + 1024) - smp > 512) return SIZE_MAX;
+    }
+    std::vector<uint64_t> v(n);
+    for (uint32_t i = 0; i < n; ++i) v[i] = load_typed(p, T, i);
+    return est_dict(T, v.data(), n);
 }
 
 struct ColSpec {
@@ -1074,7 +1152,8 @@ struct GpuEncoder {
         size_t rg, col;
         uint64_t in_off, out_off;
         uint32_t nrows;
-        uint8_t T, enc;
+        uint8_t T, enc;         // enc may be ENC_AUTO: the kernel chooses (fls_encode.hip choose_encoding)
+        uint64_t est_dict = UINT64_MAX;  // ENC_AUTO: the DICT estimate (set by the staging pass)
     };
     struct Set {
         uint8_t *h_stage = nullptr, *d_in = nullptr, *d_out = nullptr, *d_scratch = nullptr, *h_out = nullptr;
@@ -1171,7 +1250,8 @@ struct GpuEncoder {
     // rows); stage[c] = where column c's values go in pinned memory (the
     // caller copies them there, together with the column's zone map pass).
     int add(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, size_t rg, uint32_t nrows,
-            int nthreads, std::vector<FileBuilder::RG> &rgs, std::vector<uint8_t *> &stage) {
+            int nthreads, std::vector<FileBuilder::RG> &rgs, std::vector<uint8_t *> &stage,
+            std::vector<uint64_t *> &est_dict) {
         WHIP(hipSetDevice(dev));
         if (!stream) WHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         // capacity for a full batch of row groups like this one (the first
@@ -1197,6 +1277,7 @@ struct GpuEncoder {
             const int rc = ensure(*b, in_rg, out_rg, cols.size());
             if (rc) return rc;
         }
+        const size_t j0 = b->jobs.size();
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
             b->jobs.push_back(Job{rg, c, b->in_used, b->out_used, nrows, (uint8_t)T, specs[c].enc});
@@ -1204,6 +1285,7 @@ struct GpuEncoder {
             b->in_used += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
             b->out_used += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
         }
+        for (size_t k = 0; k < cols.size(); ++k) est_dict[cols[k]] = &b->jobs[j0 + k].est_dict;
         ++b->batched;  // the caller submits a full set once this row group is in rgs
         return 0;
     }
@@ -1225,7 +1307,7 @@ struct GpuEncoder {
             c.T = jb.T;
             c.enc = jb.enc;
             c.pad[0] = c.pad[1] = 0;
-            c.pad2 = 0;
+            c.est_dict = jb.est_dict;
         }
         // T = 64 chunks first (launch_encode); each carries its own addresses
         EncChunk *first = b.h_desc, *last = b.h_desc + b.jobs.size();
@@ -1257,7 +1339,17 @@ struct GpuEncoder {
             for (size_t i; (i = next.fetch_add(1)) < b.jobs.size();) {
                 const Job &jb = b.jobs[i];
                 std::vector<uint8_t> &dst = rgs[jb.rg].chunks[jb.col];
-                dst.assign(b.h_out + jb.out_off, b.h_out + jb.out_off + b.h_lens[i]);
+                const uint64_t len = b.h_lens[i] & ((1ull << kEncShift) - 1);
+                const uint8_t enc = (uint8_t)(b.h_lens[i] >> kEncShift);
+                if (len == 0 && (enc == ENC_RLE || enc == ENC_DICT)) {
+                    // ENC_AUTO chose an encoding the GPU does not write: encode
+                    // it here from the staged values (still in this set)
+                    std::vector<uint64_t> v(jb.nrows);
+                    for (uint32_t r = 0; r < jb.nrows; ++r) v[r] = load_typed(b.h_stage + jb.in_off, jb.T, r);
+                    dst = enc == ENC_RLE ? enc_rle(jb.T, v.data(), jb.nrows) : enc_dict_int(jb.T, v.data(), jb.nrows);
+                    continue;
+                }
+                dst.assign(b.h_out + jb.out_off, b.h_out + jb.out_off + len);
             }
         };
         std::vector<std::thread> th;
@@ -1348,11 +1440,13 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
     // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA
     std::vector<uint8_t> on_gpu(ncols, 0);
     std::vector<uint8_t *> stage(ncols, nullptr);
+    std::vector<uint64_t *> est_dict(ncols, nullptr);
     if (w->gpu.dev >= 0) {
         std::vector<size_t> gcols;
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
-            if (cs.type != TY_VARCHAR && !type_is_float(cs.type) && (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA)) {
+            if (cs.type != TY_VARCHAR && !type_is_float(cs.type) &&
+                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_AUTO)) {
                 gcols.push_back(c);
                 on_gpu[c] = 1;
             }
@@ -1361,7 +1455,8 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
             // room in the batch now; the values are staged below, with the
             // zone maps (the caller's buffers are only valid during this
             // call), and encoded with the batch (GpuEncoder::flush)
-            const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size(), nrows, w->threads, w->fb.rgs, stage);
+            const int rc =
+                w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size(), nrows, w->threads, w->fb.rgs, stage, est_dict);
             if (rc) return rc;
         }
     }
@@ -1376,6 +1471,10 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
         if (on_gpu[c]) {  // encoded by the GPU batch: staging copy and zone map here
             memcpy(stage[c], data[c], (size_t)nrows * (type_value_bits(cs.type) / 8));
             rg.zones[c] = zone_of_typed(cs.type, stage[c], nrows);
+            if (cs.enc == ENC_AUTO) {  // the one ENC_AUTO estimate the GPU does not make
+                const size_t d = est_dict_typed(type_value_bits(cs.type), stage[c], nrows);
+                *est_dict[c] = d == SIZE_MAX ? UINT64_MAX : (uint64_t)d;
+            }
             return;
         }
         const int T = type_value_bits(cs.type);

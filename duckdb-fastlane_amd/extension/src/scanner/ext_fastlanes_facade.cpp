@@ -5,8 +5,10 @@
 // box values row-major as the intended scanner expects
 // (src/scanner/scan_fastlanes.cpp:132-140).  Writes buffer DataChunks into
 // 65,536-row row groups (src/writer/write_fastlane_stream.cpp:21-24) and hand
-// them to the CPU FastLanes writer (include/flswriter.h).
+// them to the FastLanes writer (include/flswriter.h) on a background thread:
+// row group k is encoded while the sink buffers row group k + 1 (one deep).
 #include <cstring>
+#include <future>
 #include <vector>
 
 #include <algorithm>
@@ -39,6 +41,18 @@ public:
     std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
     idx_t wrows = 0;
     idx_t rg_rows = 65536;
+    // the row group being encoded in the background (its buffers) and the
+    // writer call's result
+    std::vector<std::vector<uint8_t>> pcols;
+    std::vector<std::vector<uint32_t>> poffs;
+    std::future<std::string> pending;  // "" or the writer's error (fls_last_error is per thread)
+    // wait for the background row group; false if its encode failed
+    bool wait_pending() {
+        if (!pending.valid()) return true;
+        const std::string e = pending.get();
+        if (!e.empty()) error = "FastLanes writer: " + e;
+        return e.empty();
+    }
 
     void close_read() {
         if (table) fls_table_close(table);
@@ -50,6 +64,7 @@ public:
     bool flush_rowgroup();
     ~Impl() {
         close_read();
+        wait_pending();
         if (writer) fls_writer_free(writer);
     }
 };
@@ -146,8 +161,14 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
                                  const std::vector<std::string> &names) {
     Impl &s = *pImpl;
     if (types.size() != names.size() || types.empty()) return false;
+    s.wait_pending();
     if (s.writer) fls_writer_free(s.writer);
     s.writer = fls_writer_new(0);
+    // integer columns are chosen (ENC_AUTO) and encoded on the first GPU of
+    // the extension's set when one is visible -- the file is byte-identical
+    // to the CPU writer's (FLS_COPY_GPU=0 keeps the CPU)
+    const char *cg = std::getenv("FLS_COPY_GPU");
+    if ((!cg || std::atoi(cg) != 0) && fls_device_count() > 0) fls_writer_set_device(s.writer, GpuDevices()[0]);
     for (size_t c = 0; c < types.size(); ++c) {
         const uint8_t ft = TypeMapping::DuckDBToFastLanes(types[c]);
         if (!ft || fls_writer_add_column(s.writer, names[c].c_str(), ft, types[c].Width(), types[c].Scale(),
@@ -166,21 +187,33 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     return true;
 }
 
+// Hand the buffered row group to the writer on a background thread (after
+// the previous one is done: row groups stay in order) and keep buffering into
+// the previous row group's buffers.
 bool FastLanesFacade::Impl::flush_rowgroup() {
     if (wrows == 0) return true;
-    std::vector<const void *> data(wtypes.size());
-    std::vector<const uint32_t *> offs(wtypes.size(), nullptr);
-    for (size_t c = 0; c < wtypes.size(); ++c) {
-        data[c] = wcols[c].empty() ? (const void *)"" : wcols[c].data();
-        if (wtypes[c].id() == LogicalTypeId::VARCHAR) offs[c] = woffs[c].data();
-    }
-    const bool ok = fls_writer_add_rowgroup(writer, (uint32_t)wrows, data.data(), offs.data()) == 0;
+    if (!wait_pending()) return false;
+    pcols.resize(wtypes.size());
+    poffs.resize(wtypes.size());
+    std::swap(pcols, wcols);
+    std::swap(poffs, woffs);
     for (size_t c = 0; c < wtypes.size(); ++c) {
         wcols[c].clear();
         woffs[c].assign(1, 0);
     }
+    const uint32_t rows = (uint32_t)wrows;
     wrows = 0;
-    return ok;
+    pending = std::async(std::launch::async, [this, rows]() {
+        std::vector<const void *> data(wtypes.size());
+        std::vector<const uint32_t *> offs(wtypes.size(), nullptr);
+        for (size_t c = 0; c < wtypes.size(); ++c) {
+            data[c] = pcols[c].empty() ? (const void *)"" : pcols[c].data();
+            if (wtypes[c].id() == LogicalTypeId::VARCHAR) offs[c] = poffs[c].data();
+        }
+        return fls_writer_add_rowgroup(writer, rows, data.data(), offs.data()) == 0 ? std::string()
+                                                                                  : std::string(fls_last_error());
+    });
+    return true;
 }
 
 // DuckDB's physical width of a fixed-size column (DECIMAL narrows with width)
@@ -253,7 +286,8 @@ bool FastLanesFacade::finalizeFile() {
     Impl &s = *pImpl;
     if (!s.writer) return false;
     bool ok = s.flush_rowgroup();
-    ok = fls_writer_finish_file(s.writer, s.out_path.c_str()) == 0 && ok;
+    ok = s.wait_pending() && ok;
+    ok = ok && fls_writer_finish_file(s.writer, s.out_path.c_str()) == 0;
     fls_writer_free(s.writer);
     s.writer = nullptr;
     return ok;

@@ -9,7 +9,7 @@ COPY ... TO (FORMAT fls) and fls_writer_*.
   3. COPY (SELECT * FROM read_fastlanes(src)) TO dst (FORMAT fls) through the
      executor harness: GPU scan of the source + encode + write (needs a GPU).
 
-    python scripts/writer_bench.py [--scale 1] [--threads 16] [--copy]
+    python scripts/writer_bench.py [--scale 1] [--threads 16] [--copy] [--gpu]
 """
 import argparse
 import os
@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--copy", action="store_true")
+    ap.add_argument("--gpu", action="store_true", help="also the writer with fls_writer_set_device(0)")
     a = ap.parse_args()
     import pkgload
     fl = pkgload.load()
@@ -74,10 +75,14 @@ def main():
                 keep.append(part)
                 data[c] = part.ctypes.data
         parts.append((r1 - r0, data, offs, keep))
-    for th in sorted({1, a.threads}):
+    ref_bytes = None
+    arms = [(th, -1) for th in sorted({1, a.threads})] + ([(a.threads, 0)] if a.gpu else [])
+    for th, dev in arms:
         w = lib.fls_writer_new(0)
         lib.fls_writer_set_threads.argtypes = [C.c_void_p, C.c_int]
         lib.fls_writer_set_threads(w, th)
+        if dev >= 0:  # integer columns chosen (ENC_AUTO) and encoded on the GPU
+            fl._check(lib.fls_writer_set_device(w, dev))
         for name, ty, vals, enc, wd, sc in cols:
             fl._check(lib.fls_writer_add_column(w, name.encode(), ty, wd, sc, enc))
         t0 = time.perf_counter()
@@ -86,11 +91,18 @@ def main():
         p, ln = C.c_void_p(), C.c_uint64()
         fl._check(lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)))
         dt = time.perf_counter() - t0
+        out = C.string_at(p, ln.value)
+        same = ""
+        if ref_bytes is None:
+            ref_bytes = out
+        else:
+            same = ", bytes identical to the 1-thread CPU file" if out == ref_bytes else ", BYTES DIFFER"
         lib.fls_image_free(p)
         lib.fls_writer_free(w)
-        print(f"C-ABI writer (ENC_AUTO, {th} threads), lineitem SF{a.scale:g}: {n} rows x {len(cols)} cols in "
+        where = f"GPU {dev} + {th} threads" if dev >= 0 else f"{th} threads"
+        print(f"C-ABI writer (ENC_AUTO, {where}), lineitem SF{a.scale:g}: {n} rows x {len(cols)} cols in "
               f"{dt:.2f} s = {n / dt / 1e6:.2f} M rows/s, {raw / dt / 1e6:.0f} MB/s of input -> "
-              f"{ln.value / 1e6:.0f} MB (ratio {raw / ln.value:.2f})", flush=True)
+              f"{ln.value / 1e6:.0f} MB (ratio {raw / ln.value:.2f}){same}", flush=True)
     for th in sorted({1, a.threads}):
         t0 = time.perf_counter()
         g = fl.gen_image(wl, a.scale, nthreads=th)

@@ -129,3 +129,69 @@ def test_gpu_encode_device_1e8_keys(fl, gpu):
         part = vals[rg * 65536:(rg + 1) * 65536]
         cpu = fl.write_image([("k", fl.INT64, part, fl.ENC_DELTA)]).tobytes()
         assert d_out.read(rg * slot, lens[rg]) == cpu[256:256 + lens[rg]], rg
+
+
+def _auto_columns(fl, n, rng):
+    """ENC_AUTO columns of every integer type with value shapes that make the
+    chooser pick each of FFOR (random), DELTA (sorted keys), RLE (runs of 50
+    random values) and DICT (few distinct values spread over the whole range)."""
+    cols = []
+    for tn in INT_TYPES:
+        ty = getattr(fl, tn)
+        dt = np.dtype(fl.NP_DTYPE[ty])
+        info = np.iinfo(dt)
+        rand = rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+        keys = np.sort(rng.integers(info.min // 4, info.max // 4, n, dtype=dt))
+        runs = np.repeat(rng.integers(info.min, info.max, n // 50 + 1, dtype=dt, endpoint=True), 50)[:n]
+        spread = rng.integers(info.min, info.max, 6, dtype=dt, endpoint=True)[rng.integers(0, 6, n)]
+        small = rng.integers(0, 3, n).astype(dt)
+        cols += [(f"{tn}_rand", ty, rand, fl.ENC_AUTO), (f"{tn}_keys", ty, keys, fl.ENC_AUTO),
+                 (f"{tn}_runs", ty, runs, fl.ENC_AUTO), (f"{tn}_spread", ty, spread, fl.ENC_AUTO),
+                 (f"{tn}_small", ty, small, fl.ENC_AUTO)]
+    return cols
+
+
+def _chunk_encodings(img: bytes):
+    """{encoding id: count} over the file's chunks (footer walk, fls_format.hpp)"""
+    import struct
+    foff, flen = struct.unpack_from("<QI", img, len(img) - 16)
+    p = foff
+    _, nc, _, nrg, _, _ = struct.unpack_from("<IIQIIQ", img, p)
+    p += 32
+    for _ in range(nc):
+        nl = struct.unpack_from("<H", img, p + 4)[0]
+        p += 6 + nl
+    out = {}
+    for _ in range(nrg):
+        p += 4
+        for _ in range(nc):
+            off, _ln = struct.unpack_from("<QQ", img, p)
+            p += 16
+            e = img[off + 4]
+            out[e] = out.get(e, 0) + 1
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (1024 * 40 + 9, 1024)])
+def test_gpu_writer_auto_bytes_identical(fl, gpu, n, rowgroup):
+    """ENC_AUTO integer columns chosen and encoded on the GPU (RLE / DICT
+    choices encoded by the host from the staged values): the file is the
+    CPU writer's, byte for byte, and every one of the four encodings occurs."""
+    cols = _auto_columns(fl, n, np.random.default_rng(n + 1))
+    cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+    encs = _chunk_encodings(cpu)
+    # (one-vector row groups hold too few values for RLE to beat DICT)
+    for e in (fl.ENC_FFOR, fl.ENC_DELTA, fl.ENC_DICT) + ((fl.ENC_RLE,) if rowgroup > 1024 else ()):
+        assert encs.get(e, 0) > 0, (e, encs)
+
+
+def test_auto_columns_choose_every_encoding(fl):
+    # CPU side of the test above: the shapes really cover all four choices
+    cols = _auto_columns(fl, 20000, np.random.default_rng(20001))
+    encs = _chunk_encodings(fl.write_image(cols, rowgroup=4096).tobytes())
+    for e in (fl.ENC_FFOR, fl.ENC_DELTA, fl.ENC_RLE, fl.ENC_DICT):
+        assert encs.get(e, 0) > 0, (e, encs)
