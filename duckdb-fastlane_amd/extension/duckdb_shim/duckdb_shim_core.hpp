@@ -8,6 +8,7 @@
 // Value casts to VARCHAR, string_t, table-function callbacks, replacement
 // scans, exceptions.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -266,6 +267,8 @@ public:
     buffer_ptr<VectorBuffer> GetAuxiliary() const { return auxiliary_; }
     bool RowIsValid(idx_t i) const { return valid_[i]; }
     void SetValid(idx_t i, bool v) { valid_[i] = v; }
+    // ValidityMask::AllValid over the first n rows (DuckDB: O(1) when no mask is allocated)
+    bool AllValid(idx_t n) const { return std::find(valid_.begin(), valid_.begin() + n, false) == valid_.begin() + n; }
     void SetVectorType(VectorType t) { vtype_ = t; }
     VectorType GetVectorType() const { return vtype_; }
     idx_t Capacity() const { return capacity_; }
@@ -292,6 +295,12 @@ struct FlatVector {
     static void SetData(Vector &v, data_ptr_t data) { v.SetDataPtr(data); }
     static void SetNull(Vector &v, idx_t i, bool is_null) { v.SetValid(i, !is_null); }
     static bool IsNull(const Vector &v, idx_t i) { return !v.RowIsValid(i); }
+    // DuckDB: FlatVector::Validity(v) -> ValidityMask (CheckAllValid(count))
+    struct ValidityView {
+        const Vector &v;
+        bool CheckAllValid(idx_t n) const { return v.AllValid(n); }
+    };
+    static ValidityView Validity(const Vector &v) { return ValidityView{v}; }
 };
 struct StringVector {
     static string_t AddString(Vector &v, const string &s) { return v.AddString(s); }

@@ -230,11 +230,10 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     // '' and a pushed-down IS NULL would match nothing, so refuse it instead of
     // writing a value (nothing of this chunk is appended).
     for (size_t c = 0; c < s.wtypes.size(); ++c)
-        for (idx_t r = 0; r < chunk.size(); ++r)
-            if (FlatVector::IsNull(chunk.data[c], r)) {
-                s.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
-                return false;
-            }
+        if (!FlatVector::Validity(chunk.data[c]).CheckAllValid(chunk.size())) {
+            s.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
+            return false;
+        }
     // column-major: append each column's slice up to the row-group boundary
     // in bulk, then let the writer encode the full row group (column-parallel)
     idx_t r0 = 0;
