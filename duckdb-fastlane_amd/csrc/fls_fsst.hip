@@ -615,7 +615,8 @@ hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
     const int full = cus * std::max(1, per_cu);
     const int grid = std::min<int>(how.waves_per_cu > 0 ? cus * std::min(how.waves_per_cu, per_cu) : full, (int)nvecs);
     // overlapped: pieces of ~1/4 of a wave's share of a full grid, <= 16 vectors
-    const uint32_t piece = std::max<uint32_t>(1, std::min<uint32_t>(16, nvecs / (4u * (uint32_t)full)));
+    uint32_t piece = std::max<uint32_t>(1, std::min<uint32_t>(16, nvecs / (4u * (uint32_t)full)));
+    if (const char *e = getenv("FLS_FSST_PIECE")) piece = (uint32_t)std::max(1, std::min(64, atoi(e)));  // A/B knob
     if (how.queue && how.reset_queue) {
         const hipError_t e = hipMemsetAsync(how.queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;

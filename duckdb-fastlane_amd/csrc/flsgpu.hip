@@ -670,13 +670,22 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
 // Overlap split (launch_all): blocks per CU of the narrow main decode grid
 // and FSST waves per CU of the narrow FSST grid; knobs FLS_OVERLAP_DECODE_BPC /
 // FLS_OVERLAP_FSST_WPC (0 FSST waves = no overlap).
+// Overlap vs one-after-the-other at the per-GPU shares of 1/2/4/8-GPU runs
+// (same-buffer A/B on lineitem_full, profiles/r2/abenv_overlap_scales.txt,
+// abenv_sf12p5.txt, abenv_minvecs.txt): overlapped is faster at SF25 (5.90 vs
+// 6.26 ms), SF50 (12.0 vs 12.9) and SF100 (23.1 vs 26.0); at SF12.5 (286 FSST
+// vectors per CU) it was 3 % slower on one box and 2 % faster on another.  So
+// the default overlaps every launch; FLS_OVERLAP_MIN_VECS_PER_CU runs launches
+// with fewer FSST vectors per CU serially.
 struct OverlapSplit {
     int decode_bpc = 1, fsst_wpc = 16;
+    uint32_t min_vecs_per_cu = 0;
 };
 OverlapSplit overlap_split() {
     OverlapSplit o;
     if (const char *e = getenv("FLS_OVERLAP_DECODE_BPC")) o.decode_bpc = std::max(1, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_FSST_WPC")) o.fsst_wpc = std::max(0, atoi(e));
+    if (const char *e = getenv("FLS_OVERLAP_MIN_VECS_PER_CU")) o.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
     return o;
 }
 
@@ -710,14 +719,16 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     small.bytes_per_lane = any.bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
     if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 15;
     small.small = true;
-    const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && (fc.sp_vecs + fc.cp_vecs) > 0 &&
-                         !d_split && !sp && !(policy & POLICY_STATIC);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const uint64_t fsst_vecs = (uint64_t)fc.sp_vecs + fc.cp_vecs;
+    const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
+                         fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !d_split && !sp &&
+                         !(policy & POLICY_STATIC);
     hipError_t e = hipSuccess;
     if (overlap) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
         DecodeGeom narrow = geom;
         const uint32_t shmem = 4 * (geom.p_bytes + geom.v_bytes);
         narrow.grid = std::min(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), cus * ov.decode_bpc);
