@@ -295,6 +295,15 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         wave_sync();
     }
     if (total != dbytes) bad = true;
+    if constexpr ((V & kFsstZeroFlush) != 0) {
+        // the ring (which staged the packed lengths) starts all zero; from
+        // here on every byte past the decoded ones stays zero: flush() zeroes
+        // the blocks it streams out and retire() the bytes its tail vacates,
+        // so the rounds OR into zeros without zeroing first
+        for (uint32_t q = lane; q < Lds<BPL, SMALL>::kRing / 16; q += 64)
+            reinterpret_cast<lv4 *>(w.ring)[q] = mk4(0, 0, 0, 0);
+        wave_sync();
+    }
     const FLS_GLOBAL FsstVecHeader *hp = reinterpret_cast<const FLS_GLOBAL FsstVecHeader *>(vh);
     const uint32_t heap_off = uni(hp->heap_off), comp_len = uni(hp->comp_len), clen_w = uni(min(hp->clen_w, 32u));
     const uint32_t hlim = min((dbytes + 15) & ~15u, heap_bytes > heap_off ? heap_bytes - heap_off : 0u);
@@ -335,7 +344,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         const uint32_t nblk = (upto - ring_base) >> 4;
         for (uint32_t q = lane; q < nblk; q += 64) {
             const uint32_t g = ring_base + 16 * q;
-            if (g + 16 <= hlim) *reinterpret_cast<ov4 *>(vheap + g) = reinterpret_cast<const lv4 *>(w.ring)[q];
+            const v4u b = reinterpret_cast<const lv4 *>(w.ring)[q];
+            if constexpr ((V & kFsstZeroFlush) != 0) reinterpret_cast<lv4 *>(w.ring)[q] = mk4(0, 0, 0, 0);
+            if (g + 16 <= hlim) *reinterpret_cast<ov4 *>(vheap + g) = b;
             else bad = true;
         }
     };
@@ -369,6 +380,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         if (lane < 8) t = reinterpret_cast<const lu32 *>(w.ring)[src + lane];
         wave_sync();
         if (lane < 8) reinterpret_cast<lu32 *>(w.ring)[lane] = t;
+        if constexpr ((V & kFsstZeroFlush) != 0) {  // the vacated tail bytes back to zero
+            if (lane < 8 && src + lane >= 8) reinterpret_cast<lu32 *>(w.ring)[src + lane] = 0;
+        }
         ring_base = new_base;
         wave_sync();
     };
@@ -406,7 +420,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             const uint32_t part = rl(incl, l1 - 1) - done;
             // zero the ring dwords these lanes OR into, keeping the already
             // decoded bytes below out_pos in the first one
-            {
+            if constexpr ((V & kFsstZeroFlush) == 0) {
                 FLS_LDS uint32_t *r32 = reinterpret_cast<FLS_LDS uint32_t *>(w.ring);
                 const uint32_t z0 = (p0 + 3) >> 2, z1 = ((p0 + part + 7) & ~7u) >> 2;
                 for (uint32_t q = z0 + lane; q < z1; q += 64) r32[q] = 0;
@@ -647,7 +661,11 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         case kFsstTwoQ: return launch_fsst_v<BPL, SMALL, kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstW6 | kFsstTwoQ:
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
-        default: return launch_fsst_v<BPL, SMALL, kFsstW6>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstW6: return launch_fsst_v<BPL, SMALL, kFsstW6>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstZeroFlush:
+            return launch_fsst_v<BPL, SMALL, kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        default:
+            return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
         }
     }
     return launch_fsst_v<BPL, SMALL, kFsstDefault>(d_chunks, nchunks, nvecs, d_err, stream, how);

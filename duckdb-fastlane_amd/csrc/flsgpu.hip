@@ -678,7 +678,9 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
 // the default overlaps every launch; FLS_OVERLAP_MIN_VECS_PER_CU runs launches
 // with fewer FSST vectors per CU serially.
 struct OverlapSplit {
-    int decode_bpc = 1, fsst_wpc = 16;
+    // 12 FSST waves per CU beside 1 decode block: 1.6-2 % faster than 16 at
+    // SF100 and SF12.5 (profiles/r2/abenv_v12.txt)
+    int decode_bpc = 1, fsst_wpc = 12;
     uint32_t min_vecs_per_cu = 0;
 };
 OverlapSplit overlap_split() {
