@@ -41,6 +41,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_ACHIEVABLE_GBS = 6290.0  # measured achievable per GPU (MI355X_MICROARCH.md; SURVEY.md 8(d) "also vs 6.29")
 PCIE_GBS = 63.0         # PCIe Gen5 x16 per GPU, spec (MI355X_MICROARCH.md)
 WORKLOADS = ["lineitem_full", "lineitem", "lineitem_dbl", "c1", "c3", "c4"]
 
@@ -486,6 +487,7 @@ def main(argv=None):
             "hbm_gbs": red["hbm_gbs"],
             "roofline": {"bound": "hbm", "achieved": mean_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": mean_achieved / HBM_PEAK_GBS,
+                         "achievable": HBM_ACHIEVABLE_GBS, "frac_achievable": mean_achieved / HBM_ACHIEVABLE_GBS,
                          "traffic": traffic / 1e9 if traffic else None,
                          "traffic_unit": "GB per launch (HBM, PMC)", "traffic_note": traffic_note,
                          "kernel": "fls::decode_kernel" + (" + fls::fsst_kernel" if args.workload == "lineitem_full"
