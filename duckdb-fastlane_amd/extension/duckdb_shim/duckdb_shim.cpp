@@ -125,7 +125,7 @@ Vector::Vector(LogicalType type, idx_t capacity)
 
 Vector::Vector(Vector &&o) noexcept
     : type_(std::move(o.type_)), capacity_(o.capacity_), data_(std::move(o.data_)), auxiliary_(std::move(o.auxiliary_)),
-      valid_(std::move(o.valid_)), heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
+      valid_(std::move(o.valid_)), may_null_(o.may_null_), heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
     // a moved std::vector keeps its storage, so an owned data pointer stays valid
     data_ptr_ = o.data_ptr_;
     o.data_ptr_ = nullptr;
@@ -137,6 +137,7 @@ void Vector::Reset() {
     data_ptr_ = data_.data();
     auxiliary_.reset();
     std::fill(valid_.begin(), valid_.end(), true);
+    may_null_ = false;
     heap_.clear();
     keep_.clear();
     vtype_ = VectorType::FLAT_VECTOR;
@@ -145,6 +146,7 @@ void Vector::Reset() {
 void Vector::Reference(const Vector &o) {
     type_ = o.type_;
     valid_ = o.valid_;
+    may_null_ = o.may_null_;
     vtype_ = o.vtype_;
     if (o.auxiliary_) {  // foreign data kept alive by its holder: share it
         data_ptr_ = o.data_ptr_;
@@ -173,6 +175,7 @@ void Vector::SetValue(idx_t i, const Value &v) {
     if (i >= capacity_) throw InternalException("Vector::SetValue out of range");
     if (v.IsNull()) {
         valid_[i] = false;
+        may_null_ = true;
         return;
     }
     valid_[i] = true;

@@ -266,9 +266,15 @@ public:
     void Reference(const Vector &other);
     buffer_ptr<VectorBuffer> GetAuxiliary() const { return auxiliary_; }
     bool RowIsValid(idx_t i) const { return valid_[i]; }
-    void SetValid(idx_t i, bool v) { valid_[i] = v; }
-    // ValidityMask::AllValid over the first n rows (DuckDB: O(1) when no mask is allocated)
-    bool AllValid(idx_t n) const { return std::find(valid_.begin(), valid_.begin() + n, false) == valid_.begin() + n; }
+    void SetValid(idx_t i, bool v) {
+        valid_[i] = v;
+        may_null_ |= !v;
+    }
+    // ValidityMask::CheckAllValid over the first n rows (DuckDB: O(1) while no
+    // mask is allocated; here: while no row was ever set invalid since Reset)
+    bool AllValid(idx_t n) const {
+        return !may_null_ || std::find(valid_.begin(), valid_.begin() + n, false) == valid_.begin() + n;
+    }
     void SetVectorType(VectorType t) { vtype_ = t; }
     VectorType GetVectorType() const { return vtype_; }
     idx_t Capacity() const { return capacity_; }
@@ -284,6 +290,7 @@ private:
     data_ptr_t data_ptr_;                 // data_.data(), or foreign memory (SetData)
     buffer_ptr<VectorBuffer> auxiliary_;  // keeps foreign memory alive
     vector<bool> valid_;
+    bool may_null_ = false;               // some row was set invalid since the last Reset
     std::deque<string> heap_;
     vector<shared_ptr<void>> keep_;
     VectorType vtype_ = VectorType::FLAT_VECTOR;

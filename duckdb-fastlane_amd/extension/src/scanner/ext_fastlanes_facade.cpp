@@ -244,10 +244,20 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             const LogicalType &t = s.wtypes[c];
             std::vector<uint8_t> &col = s.wcols[c];
             if (t.id() == LogicalTypeId::VARCHAR) {
+                // sizes first, then one resize and a copy per string (no
+                // per-row capacity checks)
                 const string_t *str = FlatVector::GetData<string_t>(v);
+                std::vector<uint32_t> &offs = s.woffs[c];
+                const size_t o0 = offs.size();
+                offs.resize(o0 + n);
+                uint32_t end = (uint32_t)col.size();
+                for (idx_t r = 0; r < n; ++r) offs[o0 + r] = end += (uint32_t)str[r0 + r].GetSize();
+                size_t at = col.size();
+                col.resize(end);
                 for (idx_t r = r0; r < r0 + n; ++r) {
-                    col.insert(col.end(), str[r].GetData(), str[r].GetData() + str[r].GetSize());
-                    s.woffs[c].push_back((uint32_t)col.size());
+                    const uint32_t len = (uint32_t)str[r].GetSize();
+                    memcpy(col.data() + at, str[r].GetData(), len);
+                    at += len;
                 }
                 continue;
             }
