@@ -1422,6 +1422,9 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (!w->fb.rgs.empty() && w->fb.rgs.back().nrows != w->fb.rowgroup_size)
         return fail(FLS_ERR_STATE, "only the last row group may be short");
+    // test hook: fail the call that would add row group k (error paths of callers)
+    if (const char *f = getenv("FLS_TEST_FAIL_WRITER_RG"))
+        if (w->fb.rgs.size() == (size_t)atoi(f)) return fail(FLS_ERR_STATE, "injected writer failure at row group %s", f);
     const size_t ncols = w->fb.cols.size();
     for (size_t c = 0; c < ncols; ++c) {
         const ColSpec &cs = w->fb.cols[c];

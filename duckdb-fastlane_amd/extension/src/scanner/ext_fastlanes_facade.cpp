@@ -296,7 +296,10 @@ bool FastLanesFacade::finalizeFile() {
     if (!s.writer) return false;
     bool ok = s.flush_rowgroup();
     ok = s.wait_pending() && ok;
-    ok = ok && fls_writer_finish_file(s.writer, s.out_path.c_str()) == 0;
+    if (ok && fls_writer_finish_file(s.writer, s.out_path.c_str()) != 0) {
+        s.error = std::string("FastLanes writer: ") + fls_last_error();
+        ok = false;
+    }
     fls_writer_free(s.writer);
     s.writer = nullptr;
     return ok;

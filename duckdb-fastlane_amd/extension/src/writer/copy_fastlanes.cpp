@@ -99,7 +99,10 @@ void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &, Local
 void CopyFinalize(ClientContext &, FunctionData &, GlobalFunctionData &gstate) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
     std::lock_guard<std::mutex> guard(g.lock);
-    if (!g.facade->finalizeFile()) throw IOException("Failed to finalize FastLanes file: " + g.file_path);
+    if (!g.facade->finalizeFile()) {
+        const std::string &why = g.facade->lastError();
+        throw IOException("Failed to finalize FastLanes file: " + g.file_path + (why.empty() ? std::string() : ": " + why));
+    }
 }
 
 }  // namespace

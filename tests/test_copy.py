@@ -108,3 +108,15 @@ def test_copy_values_roundtrip_cpu(ext, ref, tmpfile):
     assert rf.nrows == n
     assert rf.decode(0, 0).view(np.int32).tolist() == a
     assert rf.strings_column(1) == [x.encode() for x in s]
+
+
+@pytest.mark.parametrize("fail_rg", [0, 1])
+def test_copy_background_writer_failure_is_reported(ext, tmpfile, monkeypatch, fail_rg):
+    """The COPY sink encodes row group k on a background thread while it
+    buffers k+1: a writer failure there must still fail the COPY, with the
+    writer's message, whether it hits a full row group (reported at the next
+    hand-off or at finalize) or the last, partial one (finalize)."""
+    monkeypatch.setenv("FLS_TEST_FAIL_WRITER_RG", str(fail_rg))
+    n = 65536 + 1000
+    with pytest.raises(ExtError, match="injected writer failure at row group %d" % fail_rg):
+        ext.copy_values([("a", "INTEGER", list(range(n)))], tmpfile("fail.fls"))
