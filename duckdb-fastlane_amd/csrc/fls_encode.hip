@@ -388,6 +388,180 @@ __device__ void encode_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS ui
     }
 }
 
+// FastLanes-RLE chunk (fls_writer.cpp enc_rle, byte for byte): per vector the
+// run index of every value (the tail padded with the last value, so it adds
+// no run), DELTA(T = 16)-coded in the unified transposed order and
+// FFOR-packed at T = 16, plus an aux block of 128 B of chain bases (u16) and
+// the run values (T/8 bytes each), 16-aligned per vector.  Two passes over
+// the vectors: the first finds every vector's runs and width (so the packed
+// and aux offsets are known), the second writes each vector at its place.
+// Per vector, lane L takes values [16L, 16L + 16): run starts, a wave scan of
+// their counts, then the run index per value.  No MFMA; HBM-bound like the
+// other encoders (reads T/8 bytes per value twice).
+template <int T>
+__device__ uint32_t run_index(FLS_LDS Sto<T> *V, uint32_t lane, uint32_t (&idx)[16], uint32_t &flags) {
+    using S = Sto<T>;
+    S x[16];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) x[j] = V[16 * lane + j];
+    const S prev = lane > 0 ? V[16 * lane - 1] : x[0];
+    flags = 0;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        const bool start = j == 0 ? (lane == 0 || x[0] != prev) : x[j] != x[j - 1];
+        flags |= start ? 1u << j : 0u;
+        cnt += start ? 1u : 0u;
+        idx[j] = cnt;  // inclusive within the lane
+    }
+    uint32_t incl = cnt;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t base = incl - cnt;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) idx[j] = base + idx[j] - 1;
+    return __shfl(incl, 63, 64);  // the vector's runs
+}
+
+template <int T>
+__device__ void encode_rle_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS uint32_t *Wv, FLS_LDS int64_t *Bv,
+                                 FLS_LDS uint64_t *Ov) {
+    using S = Sto<T>;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    FLS_LDS S *V = Vall + w * kVectorSize;
+    const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
+    const uint8_t *in = (const uint8_t *)c.in;
+    FLS_GLOBAL uint8_t *out = (FLS_GLOBAL uint8_t *)c.out;
+    // the transposed deltas of the run indices (T = 16 chains) in registers,
+    // their FOR base and width
+    auto idx_deltas = [&](uint32_t (&idx)[16], S (&x)[16]) -> VecStat {
+        wave_sync();
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) V[16 * lane + j] = (S)idx[j];
+        wave_sync();
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) x[k] = pos_value<16, true>(V, lane + 64 * k);
+        return analyze_regs<16>(x);
+    };
+    // ---- pass 1: runs and width of every vector
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        stage_values<T>(in, v, min(kVectorSize, n - v * kVectorSize), V, lane);
+        wave_sync();
+        uint32_t idx[16], flags;
+        const uint32_t runs = run_index<T>(V, lane, idx, flags);
+        S x[16];
+        const VecStat st = idx_deltas(idx, x);
+        if (lane == 0) {
+            Wv[v] = st.W;
+            Bv[v] = st.base;
+            Ov[v] = runs;
+        }
+        wave_sync();
+    }
+    __syncthreads();
+    // ---- layout (assemble_chunk): every wave computes the offsets it needs
+    const uint64_t meta_off = sizeof(ChunkHeader);
+    const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
+    const uint32_t pw = lane < nvec ? 128u * Wv[lane] : 0u;
+    const uint32_t va = lane < nvec ? 128u + (uint32_t)Ov[lane] * (T / 8) : 0u;  // aux bytes of vector lane
+    uint32_t pincl = pw, aincl = (va + 15) & ~15u;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(pincl, d, 64), z = __shfl_up(aincl, d, 64);
+        if (lane >= d) { pincl += y; aincl += z; }
+    }
+    const uint32_t poff = pincl - pw, aoff = aincl - ((va + 15) & ~15u);  // exclusive
+    const uint64_t packed_total = __shfl(pincl, 63, 64);
+    const uint64_t aux_off = (packed_off + packed_total + 15) & ~15ull;
+    const uint64_t aux_len = __shfl(aoff, nvec - 1, 64) + __shfl(va, nvec - 1, 64);
+    const uint64_t total = (aux_off + aux_len + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
+    if (w == 0) {
+        if (lane < nvec) {
+            VecMeta m;
+            m.packed_off = poff;
+            m.for_base = Bv[lane];
+            m.aux_off = aoff;
+            m.nvals = (uint16_t)min(kVectorSize, n - lane * kVectorSize);
+            m.bw = (uint8_t)Wv[lane];
+            m.pad = 0;
+            m.aux_count = (uint32_t)Ov[lane];
+            const uint32_t *mw = reinterpret_cast<const uint32_t *>(&m);
+            FLS_GLOBAL uint32_t *dm = reinterpret_cast<FLS_GLOBAL uint32_t *>(out + meta_off + sizeof(VecMeta) * lane);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dm[i] = mw[i];
+        }
+        if (lane == 0) {
+            ChunkHeader h;
+            h.magic = kChunkMagic;
+            h.enc = ENC_RLE;
+            h.T = 16;
+            h.vbits = (uint8_t)T;
+            h.is_str = 0;
+            h.nvec = nvec;
+            h.nvals = n;
+            h.meta_off = meta_off;
+            h.packed_off = packed_off;
+            h.aux_off = aux_off;
+            h.aux_len = aux_len;
+            h.dict_count = 0;
+            h.reserved0 = 0;
+            h.reserved1 = 0;
+            const uint32_t *hw = reinterpret_cast<const uint32_t *>(&h);
+            FLS_GLOBAL uint32_t *dh = reinterpret_cast<FLS_GLOBAL uint32_t *>(out);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dh[i] = hw[i];
+            *(FLS_GLOBAL uint64_t *)c.len_out = total | (uint64_t)ENC_RLE << kEncShift;
+        }
+    }
+    // ---- pass 2: run values, chain bases and packed run-index deltas of
+    // every vector at their places
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
+        const uint32_t p_off = __shfl(poff, v, 64), a_off = __shfl(aoff, v, 64);
+        FLS_GLOBAL uint8_t *aux = out + aux_off + a_off;
+        stage_values<T>(in, v, vn, V, lane);
+        wave_sync();
+        uint32_t idx[16], flags;
+        run_index<T>(V, lane, idx, flags);
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j)
+            if (flags >> j & 1u) {  // run idx[j] starts here: its value
+                const S val = V[16 * lane + j];
+                FLS_GLOBAL uint8_t *rp = aux + 128 + (size_t)idx[j] * (T / 8);
+                if (T == 64) *(FLS_GLOBAL uint64_t *)rp = (uint64_t)val;
+                else if (T == 32) *(FLS_GLOBAL uint32_t *)rp = (uint32_t)val;
+                else if (T == 16) *(FLS_GLOBAL uint16_t *)rp = (uint16_t)val;
+                else *rp = (uint8_t)val;
+            }
+        S x[16];
+        const VecStat st = idx_deltas(idx, x);
+        // chain c's base = run index of its first tuple (blk*256 + l), u16
+        *(FLS_GLOBAL uint16_t *)(aux + 2 * lane) = (uint16_t)V[(lane / 16) * 256 + (lane % 16)];
+        S u[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) u[k] = (S)((x[k] - (S)st.base) & (S)0xFFFFu);
+        wave_sync();
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = u[k];
+        wave_sync();
+        pack_vector<16>(V, st.W, out + packed_off + p_off, lane);
+        // zero padding after this vector's aux block (up to the next one's start)
+        const uint32_t a_end = a_off + 128u + __shfl(va, v, 64) - 128u;
+        const uint32_t a_next = (a_end + 15) & ~15u;
+        if (v + 1 < nvec && lane < a_next - a_end) aux[a_end - a_off + lane] = 0;
+        wave_sync();
+    }
+    // header / meta / packed / aux gaps
+    {
+        const uint64_t gaps[3][2] = {{meta_off + sizeof(VecMeta) * nvec, packed_off},
+                                     {packed_off + packed_total, aux_off},
+                                     {aux_off + aux_len, total}};
+        for (int g = 0; g < 3; ++g)
+            for (uint64_t b = gaps[g][0] + threadIdx.x; b < gaps[g][1]; b += blockDim.x) out[b] = 0;
+    }
+}
+
 // ENC_AUTO on the GPU: the encoding fls_writer.cpp encode_int_chunk(ENC_AUTO)
 // picks, from the same estimates computed the same way -- per vector the
 // FFOR width of the values and of their transposed deltas (the tail padded
@@ -485,11 +659,14 @@ __global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) voi
             default: enc = choose_encoding<32>(c, V, O); break;
             }
         }
-        if (enc != ENC_FFOR && enc != ENC_DELTA) {  // RLE / DICT: the host encodes it
+        if (enc != ENC_FFOR && enc != ENC_DELTA) {
+            // RLE: encode_rle_kernel, launched next, writes the chunk; DICT
+            // (the distinct values sorted) is encoded by the host
             if (threadIdx.x == 0) *(FLS_GLOBAL uint64_t *)c.len_out = (uint64_t)enc << kEncShift;
             return;
         }
     }
+    if (enc == ENC_RLE) return;  // explicit RLE chunks: encode_rle_kernel
     const bool delta = enc == ENC_DELTA;
     if constexpr (sizeof(S) == 8) {
         delta ? encode_chunk<64, true>(c, V, W, B, O) : encode_chunk<64, false>(c, V, W, B, O);
@@ -502,20 +679,64 @@ __global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) voi
     }
 }
 
+// RLE chunks in a kernel of their own (inlined into encode_kernel its
+// registers made the FFOR / DELTA paths spill): explicit ENC_RLE chunks, and
+// ENC_AUTO chunks for which encode_kernel, launched before it on the same
+// stream, chose RLE (length 0, ENC_RLE in the top byte).  Every other chunk's
+// block returns at once.
+// (Its run-index, delta and packing registers get a budget of 2 waves per
+// SIMD: at the FFOR kernel's 4-5 it spilled, and a spilling encoder build is
+// the one that once wrote wrong rows)
+template <typename S>
+__global__ __launch_bounds__(256, 2) void encode_rle_kernel(const EncChunk *__restrict__ chunks, uint32_t nchunks) {
+    __shared__ S Vall[kEncWaves * kVectorSize];
+    __shared__ uint32_t Wv[64];
+    __shared__ int64_t Bv[64];
+    __shared__ uint64_t Ov[67];
+    const EncChunk c = chunks[blockIdx.x];
+    if (c.enc != ENC_RLE) {
+        if (c.enc != ENC_AUTO) return;
+        const uint64_t chosen = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(*(const FLS_GLOBAL uint64_t *)c.len_out >> kEncShift));
+        if (chosen != ENC_RLE || (*(const FLS_GLOBAL uint64_t *)c.len_out & ((1ull << kEncShift) - 1)) != 0) return;
+    }
+    FLS_LDS S *V = (FLS_LDS S *)Vall;
+    FLS_LDS uint32_t *W = (FLS_LDS uint32_t *)Wv;
+    FLS_LDS int64_t *B = (FLS_LDS int64_t *)Bv;
+    FLS_LDS uint64_t *O = (FLS_LDS uint64_t *)Ov;
+    if constexpr (sizeof(S) == 8) {
+        encode_rle_chunk<64>(c, V, W, B, O);
+    } else {
+        switch (c.T) {
+        case 8: encode_rle_chunk<8>(c, V, W, B, O); break;
+        case 16: encode_rle_chunk<16>(c, V, W, B, O); break;
+        default: encode_rle_chunk<32>(c, V, W, B, O); break;
+        }
+    }
+}
+
 }  // namespace
 
 uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
     const uint64_t nvec = (nrows + kVectorSize - 1) / kVectorSize;
     const uint64_t packed_off = (sizeof(ChunkHeader) + sizeof(VecMeta) * nvec + 15) & ~15ull;
-    const uint64_t aux = enc == ENC_DELTA || enc == ENC_AUTO ? 128ull * nvec : 0ull;  // AUTO may pick DELTA
-    return (packed_off + 128ull * T * nvec + aux + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
+    const uint64_t delta = packed_off + 128ull * T * nvec + (enc == ENC_FFOR ? 0ull : 128ull * nvec);
+    // RLE: T = 16 packing, aux = 128 B of bases + up to 1,024 run values per vector
+    const uint64_t rle = packed_off + 128ull * 16 * nvec + nvec * ((128ull + 1024ull * (T / 8) + 15) & ~15ull);
+    const uint64_t need = enc == ENC_RLE ? rle : enc == ENC_AUTO ? std::max(delta, rle) : delta;  // AUTO may pick any
+    return (need + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
 }
 
-hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream) {
+hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle) {
     if (n_wide) hipLaunchKernelGGL(encode_kernel<uint64_t>, dim3(n_wide), dim3(64 * kEncWaves), 0, stream, d_chunks, n_wide);
     if (n_narrow)
         hipLaunchKernelGGL(encode_kernel<uint32_t>, dim3(n_narrow), dim3(64 * kEncWaves), 0, stream, d_chunks + n_wide,
                            n_narrow);
+    if (rle && n_wide)
+        hipLaunchKernelGGL(encode_rle_kernel<uint64_t>, dim3(n_wide), dim3(64 * kEncWaves), 0, stream, d_chunks, n_wide);
+    if (rle && n_narrow)
+        hipLaunchKernelGGL(encode_rle_kernel<uint32_t>, dim3(n_narrow), dim3(64 * kEncWaves), 0, stream,
+                           d_chunks + n_wide, n_narrow);
     return hipGetLastError();
 }
 
@@ -592,7 +813,8 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
     if (e == hipSuccess) e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
     if (e == hipSuccess) e = hipEventRecord(e0, nullptr);
-    if (e == hipSuccess) e = launch_encode(d_desc, T == 64 ? (uint32_t)nrg : 0u, T == 64 ? 0u : (uint32_t)nrg, nullptr);
+    if (e == hipSuccess)
+        e = launch_encode(d_desc, T == 64 ? (uint32_t)nrg : 0u, T == 64 ? 0u : (uint32_t)nrg, nullptr, false);
     if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0;

@@ -32,6 +32,7 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // Encode nchunks chunks (d_chunks in device memory), one block each.
 // Launch over chunks [0, n_wide) of T = 64 and then [n_wide, n_wide + n_narrow)
 // of T <= 32 (one kernel each: u64 or u32 registers and LDS).
-hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream);
+// rle: some chunk is ENC_RLE or ENC_AUTO (encode_rle_kernel follows).
+hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle);
 
 }  // namespace fls

@@ -1315,7 +1315,9 @@ struct GpuEncoder {
             (uint32_t)(std::stable_partition(first, last, [](const EncChunk &c) { return c.T == 64; }) - first);
         WHIP(hipMemcpyAsync(b.d_in, b.h_stage, b.in_used, hipMemcpyHostToDevice, stream));
         WHIP(hipMemcpyAsync(b.d_desc, b.h_desc, b.jobs.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
-        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream));
+        bool rle = false;
+        for (const Job &jb : b.jobs) rle |= jb.enc == ENC_RLE || jb.enc == ENC_AUTO;
+        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream, rle));
         WHIP(hipMemcpyAsync(b.h_lens, b.d_lens, b.jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         // the slots come back in one pinned copy (slots are sized for W = T,
         // so this moves more than the chunks hold, but one large copy beats
@@ -1449,7 +1451,7 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
             if (cs.type != TY_VARCHAR && !type_is_float(cs.type) &&
-                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_AUTO)) {
+                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO)) {
                 gcols.push_back(c);
                 on_gpu[c] = 1;
             }

@@ -195,3 +195,40 @@ def test_auto_columns_choose_every_encoding(fl):
     encs = _chunk_encodings(fl.write_image(cols, rowgroup=4096).tobytes())
     for e in (fl.ENC_FFOR, fl.ENC_DELTA, fl.ENC_RLE, fl.ENC_DICT):
         assert encs.get(e, 0) > 0, (e, encs)
+
+
+def _rle_columns(fl, n, rng):
+    """Explicit ENC_RLE columns of every integer type: long runs, one value,
+    a run per value (1,024 runs per vector, the largest aux block) and runs
+    of random lengths."""
+    cols = []
+    for tn in INT_TYPES:
+        ty = getattr(fl, tn)
+        dt = np.dtype(fl.NP_DTYPE[ty])
+        info = np.iinfo(dt)
+        long_runs = np.repeat(rng.integers(info.min, info.max, n // 700 + 1, dtype=dt, endpoint=True), 700)[:n]
+        const = np.full(n, info.min, dtype=dt)
+        every = rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+        lens = rng.integers(1, 40, n)
+        mixed = np.repeat(rng.integers(info.min, info.max, n, dtype=dt, endpoint=True), lens)[:n]
+        cols += [(f"{tn}_long", ty, long_runs, fl.ENC_RLE), (f"{tn}_const", ty, const, fl.ENC_RLE),
+                 (f"{tn}_every", ty, every, fl.ENC_RLE), (f"{tn}_mixed", ty, mixed, fl.ENC_RLE)]
+    return cols
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (1024 * 3 + 1, 1024), (1, 65536)])
+def test_gpu_writer_rle_bytes_identical(fl, ref, gpu, n, rowgroup):
+    """RLE chunks written by the GPU (encode_rle_kernel) are the CPU writer's
+    bytes, and decode to the input under the oracle."""
+    cols = _rle_columns(fl, n, np.random.default_rng(n + 7))
+    cpu_img = fl.write_image(cols, rowgroup=rowgroup)
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes()
+    cpu = cpu_img.tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+    assert set(_chunk_encodings(cpu)) == {fl.ENC_RLE}
+    rf = ref.RefFile(cpu_img)
+    for c, (_, ty, vals, _) in enumerate(cols):
+        got = np.concatenate([rf.decode(c, r) for r in range(rf.nrowgroups)])
+        assert np.array_equal(got.view(vals.dtype), vals), cols[c][0]
