@@ -147,9 +147,31 @@ def launch(args, argv) -> int:
     prints the JSON line."""
     envs = rank_envs(args.gpus, free_port(), os.environ)
     procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + list(argv), env=e) for e in envs]
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return max(bad, key=abs) if bad else 0
+    return wait_ranks(procs)
+
+
+def wait_ranks(procs, poll_s: float = 0.2, grace_s: float = 30.0) -> int:
+    """Wait for every rank; when one fails, stop the others (they would wait
+    for it at the next barrier forever): SIGTERM, then SIGKILL after grace_s.
+    Returns 0 or the failing rank's status."""
+    first_bad = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if first_bad is None:
+            first_bad = next((rc for rc in rcs if rc not in (None, 0)), None)
+            if first_bad is not None:
+                log(f"launcher: a rank exited with status {first_bad}; stopping the others")
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                deadline = time.monotonic() + grace_s
+        if all(rc is not None for rc in rcs):
+            return first_bad if first_bad is not None else 0
+        if first_bad is not None and time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(poll_s)
 
 
 # ---- measurement pieces -----------------------------------------------------

@@ -74,12 +74,17 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 // skip the escape-state logic; kFsstTwoQ = each symbol OR-ed into both
 // qwords it spans instead of through a 64-bit accumulator; kFsstZeroFlush =
 // the ring is kept zero past the decoded bytes by the flush (no zeroing pass
-// per round); kFsstW6 = registers budgeted for 6 waves per SIMD instead of 4.
+// per round); kFsstW6 = registers budgeted for 6 waves per SIMD instead of 4;
+// kFsstCirc = circular ring indexed by decoded position (no tail move per
+// round; with zero-at-flush).
 // Default kFsstW6 | kFsstZeroFlush (80 VGPRs, no spill in the standalone
 // kernel): l_comment SF10 1.074 -> 1.012 (descriptor in SGPRs) -> 0.969
 // (6-wave budget) -> 0.922 ms (zero at flush); Plain and TwoQ measured slower
 // (profiles/r2/abenv_fsst_var_l_comment.txt).
-enum : int { kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstDefault = kFsstW6 | kFsstZeroFlush };
+enum : int {
+    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16,
+    kFsstDefault = kFsstW6 | kFsstZeroFlush
+};
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {
     int bytes_per_lane = 8;       // compressed bytes a lane decodes per round (8 or 16)

@@ -125,12 +125,14 @@ __device__ __forceinline__ uint32_t entry_state(bool has_plain, uint32_t exit_if
 // Symbols must be masked to their length (the staged table is).  Measured
 // against OR-ing every symbol into both qwords it spans (no accumulator,
 // fewer VALU, twice the ds_or_b64): 1-2 % faster on l_comment.
+// QMask: qword index mask of a circular ring (kFsstCirc), ~0 for a flat one.
+template <uint32_t QMask = ~0u>
 struct QwordWriter {
     FLS_LDS uint64_t *o64;
     uint64_t acc;
     uint32_t q, bits;
     __device__ __forceinline__ QwordWriter(lu8 *ring, uint32_t wp)
-        : o64(reinterpret_cast<FLS_LDS uint64_t *>(ring)), acc(0), q(wp >> 3), bits(8 * (wp & 7)) {}
+        : o64(reinterpret_cast<FLS_LDS uint64_t *>(ring)), acc(0), q((wp >> 3) & QMask), bits(8 * (wp & 7)) {}
     __device__ __forceinline__ void put(uint64_t v, uint32_t n) {  // n <= 8 bytes
         // v << bits spans qwords q (lo) and q + 1 (hi); (v >> 1) >> (63 - bits)
         // is v >> (64 - bits) without the bits == 0 case
@@ -139,7 +141,7 @@ struct QwordWriter {
         __hip_atomic_fetch_or(o64 + q, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         const uint32_t nb = bits + 8 * n;
         const bool e = nb >= 64;
-        q += e ? 1u : 0u;
+        q = (q + (e ? 1u : 0u)) & QMask;
         acc = e ? hi : acc;
         bits = nb & 63;
     }
@@ -209,11 +211,14 @@ __device__ __forceinline__ bool has_escape(const v4u &raw) {
     return (BPL == 8 ? (ff(raw.x) | ff(raw.y)) : (ff(raw.x) | ff(raw.y) | ff(raw.z) | ff(raw.w))) != 0;
 }
 
-// string_t of a string of n bytes at ring byte x, host pointer p
+// string_t of a string of n bytes at ring byte x, host pointer p (DMask:
+// dword index mask of a circular ring, ~0 for a flat one)
+template <uint32_t DMask = ~0u>
 __device__ __forceinline__ v4u make_record_at(const lu8 *ring, uint32_t x, uint32_t n, uint64_t p) {
-    const lu32 *r32 = reinterpret_cast<const lu32 *>(ring) + (x >> 2);
-    const uint32_t sh = x & 3;
-    const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2], w3 = r32[3];
+    const lu32 *r32 = reinterpret_cast<const lu32 *>(ring);
+    const uint32_t i0 = x >> 2, sh = x & 3;
+    const uint32_t w0 = r32[i0 & DMask], w1 = r32[(i0 + 1) & DMask], w2 = r32[(i0 + 2) & DMask],
+                   w3 = r32[(i0 + 3) & DMask];
     const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
     if (n > 12) return mk4(n, b0, (uint32_t)p, (uint32_t)(p >> 32));
     const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
@@ -226,11 +231,13 @@ __device__ __forceinline__ v4u make_record_at(const lu8 *ring, uint32_t x, uint3
     return mk4(n, keep(b0, 0), keep(b1, 4), keep(b2, 8));
 }
 
-// string_t of string i (doff d0, length n) from the ring (ring_base = global
-// position of ring byte 0)
+// string_t of string i (doff d0, length n) from the ring: a flat ring holds
+// byte ring_base at ring byte 0, a circular one (CircBytes) byte g at g mod CircBytes
+template <uint32_t CircBytes>
 __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t n, uint32_t ring_base,
                                            uint64_t ptr_base) {
-    return make_record_at(w.ring, d0 - ring_base, n, ptr_base + d0);
+    if constexpr (CircBytes != 0) return make_record_at<CircBytes / 4 - 1>(w.ring, d0, n, ptr_base + d0);
+    else return make_record_at(w.ring, d0 - ring_base, n, ptr_base + d0);
 }
 
 template <int BPL, bool SMALL, int V>
@@ -238,6 +245,12 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
                             uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err) {
     bool bad = false;
+    // kFsstCirc: a circular ring of kCirc bytes (a power of two) indexed by
+    // decoded byte position mod kCirc, so retire() moves no tail, it only
+    // advances ring_base (needs the zero-at-flush invariant)
+    constexpr uint32_t kCirc = (V & kFsstCirc) ? (Lds<BPL, SMALL>::kRing >= 4096 ? 4096u : 2048u) : 0u;
+    static_assert(!(V & kFsstCirc) || ((V & kFsstZeroFlush) && !(V & kFsstTwoQ)), "kFsstCirc needs zero-at-flush");
+    static_assert(kCirc <= Lds<BPL, SMALL>::kRing, "circular ring fits the ring area");
     // ---- 1. string lengths: u8 lengths (SMALL) or exclusive u32 offsets -----
     W = SMALL ? min(W, 8u) : W;
     const uint32_t n16 = 8 * W;
@@ -330,7 +343,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             const uint64_t m = __ballot(ok);
             const uint32_t n_ok = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);
             if (lane < n_ok)
-                *reinterpret_cast<ov4 *>(out + 16ull * i) = make_record(w, d0, n, ring_base, ptr_base);
+                *reinterpret_cast<ov4 *>(out + 16ull * i) = make_record<kCirc>(w, d0, n, ring_base, ptr_base);
             if constexpr (SMALL) {
                 if (n_ok > 0) str_base += rl(incl, n_ok - 1);
             }
@@ -344,8 +357,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         const uint32_t nblk = (upto - ring_base) >> 4;
         for (uint32_t q = lane; q < nblk; q += 64) {
             const uint32_t g = ring_base + 16 * q;
-            const v4u b = reinterpret_cast<const lv4 *>(w.ring)[q];
-            if constexpr ((V & kFsstZeroFlush) != 0) reinterpret_cast<lv4 *>(w.ring)[q] = mk4(0, 0, 0, 0);
+            const uint32_t slot = kCirc ? (g >> 4) & (kCirc / 16 - 1) : q;
+            const v4u b = reinterpret_cast<const lv4 *>(w.ring)[slot];
+            if constexpr ((V & kFsstZeroFlush) != 0) reinterpret_cast<lv4 *>(w.ring)[slot] = mk4(0, 0, 0, 0);
             if (g + 16 <= hlim) *reinterpret_cast<ov4 *>(vheap + g) = b;
             else bad = true;
         }
@@ -375,6 +389,10 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         const uint32_t new_base = keep_from & ~15u;
         flush(new_base);
         wave_sync();
+        if constexpr (kCirc != 0) {  // the tail stays where it is
+            ring_base = new_base;
+            return;
+        }
         const uint32_t src = (new_base - ring_base) >> 2;
         uint32_t t = 0;
         if (lane < 8) t = reinterpret_cast<const lu32 *>(w.ring)[src + lane];
@@ -410,7 +428,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         // write the round into the ring: normally all 64 lanes at once; when
         // their output would overrun the ring, the lanes that fit first, then
         // retire() to empty the ring and continue (a lane writes <= 8 BPL bytes)
-        constexpr uint32_t kCap = Lds<BPL, SMALL>::kRing - 48;  // slack: qword ORs, retire()'s 32 B tail read
+        // slack: qword ORs, retire()'s 32 B tail read (circular: the bytes
+        // from ring_base to the round's end must not wrap onto ring_base)
+        constexpr uint32_t kCap = kCirc ? kCirc - 16 : Lds<BPL, SMALL>::kRing - 48;
         uint32_t l0 = 0, done = 0;
         for (;;) {
             const uint32_t p0 = out_pos - ring_base;
@@ -428,7 +448,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             }
             wave_sync();
             if (lane >= l0 && lane < l1) {
-                const uint32_t wp = p0 + (incl - lane_out - done);
+                const uint32_t wp = (kCirc ? out_pos : p0) + (incl - lane_out - done);
                 if constexpr ((V & kFsstTwoQ) != 0) {
                     // every symbol OR-ed into both qwords it spans: the shift
                     // counts are taken mod 64 by the hardware (8 * p mod 64 is
@@ -444,7 +464,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                         p += n[k];
                     }
                 } else {
-                    QwordWriter qw(w.ring, wp);
+                    QwordWriter<kCirc ? kCirc / 8 - 1 : ~0u> qw(w.ring, wp);
 #pragma unroll
                     for (uint32_t k = 0; k < BPL; ++k) qw.put(v[k], n[k]);
                     qw.finish();
@@ -469,7 +489,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     }
     // zero the padding of the last block, then flush everything
     const uint32_t end = (out_pos + 15) & ~15u;
-    if (lane < 16 && out_pos + lane < end) w.ring[out_pos - ring_base + lane] = 0;
+    if (lane < 16 && out_pos + lane < end) w.ring[kCirc ? (out_pos + lane) & (kCirc - 1) : out_pos - ring_base + lane] = 0;
     wave_sync();
     flush(end);
     if (bad) atomicOr(err, KERR_FSST);
@@ -655,7 +675,7 @@ template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     if constexpr (BPL == 8) {
-        switch (how.variant & 15) {
+        switch (how.variant & 31) {
         case 0: return launch_fsst_v<BPL, SMALL, 0>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstPlain: return launch_fsst_v<BPL, SMALL, kFsstPlain>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstTwoQ: return launch_fsst_v<BPL, SMALL, kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
@@ -664,6 +684,9 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         case kFsstW6: return launch_fsst_v<BPL, SMALL, kFsstW6>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstZeroFlush:
             return launch_fsst_v<BPL, SMALL, kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstW6 | kFsstZeroFlush | kFsstCirc:
+            return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush | kFsstCirc>(d_chunks, nchunks, nvecs, d_err,
+                                                                                 stream, how);
         default:
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
         }

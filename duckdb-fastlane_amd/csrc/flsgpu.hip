@@ -733,7 +733,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     const OverlapSplit ov = overlap_split();
     FsstLaunch small, any;
     small.bytes_per_lane = any.bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
-    if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 15;
+    if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 31;
     small.small = true;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -1406,6 +1406,8 @@ int fls_connect(const int *devices, int ndevices, fls_connection **out) {
 
 void fls_disconnect(fls_connection *conn) { delete conn; }
 
+}  // extern "C"
+
 namespace {
 // The validated-file cache (MappedFile): the FLS_OPEN_CACHE most recently
 // opened files (default 16, 0 = off) stay mapped with their metadata.  The
@@ -1448,6 +1450,8 @@ FileCache &file_cache() {
     return *c;
 }
 }  // namespace
+
+extern "C" {
 
 int fls_read_fls(fls_connection *conn, const char *path, fls_table **out) {
     if (!conn || !path || !out) return fail(FLS_ERR_ARG, "fls_read_fls: NULL argument");

@@ -54,3 +54,22 @@ def test_gpus_n_spawns_ranks_and_reduces(_built, n):
     assert red["dt"] == 1.0 + 0.25 * (n - 1)                               # the slowest rank's time
     assert red["rowgroups"] == [b - a for a, b in shards]
     assert out["value"] == pytest.approx(600037902 / red["dt"])
+
+
+def test_wait_ranks_stops_the_others_when_one_fails():
+    # rank 1 fails at once; rank 0 would otherwise wait at a barrier for ever
+    import time
+    hang = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(600)"])
+    fail = subprocess.Popen([sys.executable, "-c", "import sys; sys.exit(3)"])
+    t0 = time.monotonic()
+    try:
+        assert bench.wait_ranks([hang, fail], poll_s=0.05, grace_s=5) == 3
+    finally:
+        if hang.poll() is None:
+            hang.kill()
+    assert hang.poll() is not None and time.monotonic() - t0 < 30
+
+
+def test_wait_ranks_all_ok():
+    procs = [subprocess.Popen([sys.executable, "-c", "pass"]) for _ in range(3)]
+    assert bench.wait_ranks(procs, poll_s=0.05) == 0
