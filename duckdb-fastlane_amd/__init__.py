@@ -130,6 +130,8 @@ _sig("fls_writer_new", _P, C.c_uint64)
 _sig("fls_writer_free", None, _P)
 _sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c_uint8, C.c_uint8)
 _sig("fls_writer_add_rowgroup", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P))
+_sig("fls_writer_set_threads", C.c_int, _P, C.c_int)
+_sig("fls_writer_add_rowgroups", C.c_int, _P, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(_P), C.POINTER(_P))
 _sig("fls_writer_set_rowgroup_size", C.c_int, _P, C.c_uint32)
 _sig("fls_writer_set_device", C.c_int, _P, C.c_int)
 _sig("fls_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(_P))
@@ -242,14 +244,19 @@ def gen_dict_string(workload: str, col: int, code: int) -> str | None:
 
 
 # --- writer ----------------------------------------------------------------
-def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: int = -1) -> Image:
+def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: int = -1,
+                batch: int = 1, threads: int = 0) -> Image:
     """columns: list of (name, type, values, encoding[, width, scale]).
     values: numpy int array for integer types, float array for FLOAT/DOUBLE
     (stored bit-exactly), list of str/bytes for VARCHAR.  device >= 0: the
-    FFOR / DELTA integer columns are encoded on that GPU (same bytes)."""
+    FFOR / DELTA integer columns are encoded on that GPU (same bytes).
+    batch > 1: row groups go in `batch` at a time (fls_writer_add_rowgroups;
+    same bytes).  threads > 0: writer threads (fls_writer_set_threads)."""
     w = _lib.fls_writer_new(row_offset)
     try:
         _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))
+        if threads > 0:
+            _check(_lib.fls_writer_set_threads(w, threads))
         if device >= 0:
             _check(_lib.fls_writer_set_device(w, device))
         n = None
@@ -270,25 +277,34 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
                 n = cnt
             elif n != cnt:
                 raise ValueError("columns differ in length")
-        for r0 in range(0, n or 0, rowgroup):
-            r1 = min(n, r0 + rowgroup)
+        nc = len(prepped)
+        starts = list(range(0, n or 0, rowgroup))
+        for b0 in range(0, len(starts), max(1, batch)):
+            grp = starts[b0:b0 + max(1, batch)]
             keep = []
-            data = (_P * len(prepped))()
-            offs = (_P * len(prepped))()
-            for c, (kind, v) in enumerate(prepped):
-                if kind == "i":
-                    part = np.ascontiguousarray(v[r0:r1])
-                    keep.append(part)
-                    data[c] = part.ctypes.data
-                else:
-                    sl = v[r0:r1]
-                    o = np.zeros(len(sl) + 1, dtype=np.uint32)
-                    o[1:] = np.cumsum([len(x) for x in sl], dtype=np.uint64).astype(np.uint32)
-                    buf = np.frombuffer(b"".join(sl) or b"\0", dtype=np.uint8).copy()
-                    keep += [o, buf]
-                    data[c] = buf.ctypes.data
-                    offs[c] = o.ctypes.data
-            _check(_lib.fls_writer_add_rowgroup(w, r1 - r0, data, offs))
+            data = (_P * (nc * len(grp)))()
+            offs = (_P * (nc * len(grp)))()
+            rows = (C.c_uint32 * len(grp))()
+            for k, r0 in enumerate(grp):
+                r1 = min(n, r0 + rowgroup)
+                rows[k] = r1 - r0
+                for c, (kind, v) in enumerate(prepped):
+                    if kind == "i":
+                        part = np.ascontiguousarray(v[r0:r1])
+                        keep.append(part)
+                        data[k * nc + c] = part.ctypes.data
+                    else:
+                        sl = v[r0:r1]
+                        o = np.zeros(len(sl) + 1, dtype=np.uint32)
+                        o[1:] = np.cumsum([len(x) for x in sl], dtype=np.uint64).astype(np.uint32)
+                        buf = np.frombuffer(b"".join(sl) or b"\0", dtype=np.uint8).copy()
+                        keep += [o, buf]
+                        data[k * nc + c] = buf.ctypes.data
+                        offs[k * nc + c] = o.ctypes.data
+            if batch > 1:
+                _check(_lib.fls_writer_add_rowgroups(w, len(grp), rows, data, offs))
+            else:
+                _check(_lib.fls_writer_add_rowgroup(w, rows[0], data, offs))
         p, ln = _P(), C.c_uint64()
         rc = _lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln))
         return _take_image(rc, p, ln)

@@ -12,7 +12,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1243,7 +1245,30 @@ struct GpuEncoder {
             WHIP(hipMalloc((void **)&b.d_scratch, n * enc_scratch_bytes()));
             b.job_cap = n;
         }
+        // add() hands out pointers into jobs (est_dict) that must stay valid
+        // while later row groups join the set (fls_writer_add_rowgroups)
+        b.jobs.reserve(b.job_cap);
         return 0;
+    }
+
+    // Pinned staging / slot bytes columns cols of an nrows row group need.
+    static void need(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, uint32_t nrows,
+                     uint64_t &in_rg, uint64_t &out_rg) {
+        in_rg = out_rg = 0;
+        for (size_t c : cols) {
+            const int T = type_value_bits(specs[c].type);
+            in_rg += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
+            out_rg += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
+        }
+    }
+    // Whether add() would take this row group into the current set without
+    // first submitting it (submitting needs every row group of the set staged).
+    bool has_room(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, uint32_t nrows) const {
+        uint64_t in_rg, out_rg;
+        need(specs, cols, nrows, in_rg, out_rg);
+        const Set &b = sets[cur];
+        return !b.in_flight && b.in_used + in_rg <= b.in_cap && b.out_used + out_rg <= b.out_cap &&
+               b.jobs.size() + cols.size() <= b.job_cap;
     }
 
     // Reserve the current set's room for columns cols of row group rg (nrows
@@ -1256,12 +1281,8 @@ struct GpuEncoder {
         if (!stream) WHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         // capacity for a full batch of row groups like this one (the first
         // row group is the largest: only the last one may be short)
-        uint64_t in_rg = 0, out_rg = 0;
-        for (size_t c : cols) {
-            const int T = type_value_bits(specs[c].type);
-            in_rg += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
-            out_rg += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
-        }
+        uint64_t in_rg, out_rg;
+        need(specs, cols, nrows, in_rg, out_rg);
         if (sets[cur].in_flight) {
             const int rc = complete(sets[cur], rgs, nthreads);
             if (rc) return rc;
@@ -1381,10 +1402,82 @@ struct GpuEncoder {
 #undef WHIP
 };
 
+// The writer's persistent workers: run(n, fn) calls fn(0..n-1) on the calling
+// thread and the workers and returns when every call is done (threads were
+// created per row group before: 15 thread starts per 65,536-row group).
+class WorkerPool {
+public:
+    ~WorkerPool() { stop(); }
+    // nthreads in total, the calling thread included
+    void resize(int nthreads) {
+        const size_t want = (size_t)std::max(0, nthreads - 1);
+        if (want == th_.size()) return;
+        stop();
+        quit_ = false;
+        for (size_t i = 0; i < want; ++i) th_.emplace_back([this] { loop(); });
+    }
+    void run(size_t n, const std::function<void(size_t)> &fn) {
+        if (th_.empty() || n <= 1) {
+            for (size_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0);
+            busy_ = th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void drain() {
+        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    void stop() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+        th_.clear();
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)> *fn_ = nullptr;
+    size_t n_ = 0, busy_ = 0;
+    std::atomic<size_t> next_{0};
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
 struct fls_writer {
     FileBuilder fb;
-    int threads = default_writer_threads();  // column-parallel encode per row group
+    int threads = default_writer_threads();  // (row group, column) tasks run on this many threads
     GpuEncoder gpu;                          // fls_writer_set_device
+    WorkerPool pool;
 };
 
 extern "C" {
@@ -1416,101 +1509,160 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
     return 0;
 }
 
-int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *data,
-                            const uint32_t *const *str_offsets) {
-    if (!w || !data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroup: NULL argument");
-    if (nrows == 0 || nrows > w->fb.rowgroup_size)
-        return fail(FLS_ERR_ARG, "row group needs 1..%u rows, got %u", w->fb.rowgroup_size, nrows);
+}  // extern "C"
+
+namespace {
+struct RgArgs {
+    uint32_t nrows;
+    const void *const *data;
+    const uint32_t *const *offs;
+};
+
+// Append row groups a[0..nrg): every (row group, column) chunk is an
+// independent task on the writer's threads, VARCHAR chunks (the slowest) first,
+// so a row group's slowest column no longer idles the other threads.  With a
+// GPU (fls_writer_set_device) the integer columns are staged into the GPU
+// encoder's current batch by the same tasks; the row groups go in in segments
+// that end where the batch is full or out of room, since a batch is only
+// submitted once every row group in it is staged.
+int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
-    if (!w->fb.rgs.empty() && w->fb.rgs.back().nrows != w->fb.rowgroup_size)
-        return fail(FLS_ERR_STATE, "only the last row group may be short");
-    // test hook: fail the call that would add row group k (error paths of callers)
-    if (const char *f = getenv("FLS_TEST_FAIL_WRITER_RG"))
-        if (w->fb.rgs.size() == (size_t)atoi(f)) return fail(FLS_ERR_STATE, "injected writer failure at row group %s", f);
     const size_t ncols = w->fb.cols.size();
-    for (size_t c = 0; c < ncols; ++c) {
-        const ColSpec &cs = w->fb.cols[c];
-        if (!data[c]) return fail(FLS_ERR_ARG, "column %zu: NULL data", c);
-        if (cs.type == TY_VARCHAR) {
-            if (!str_offsets || !str_offsets[c]) return fail(FLS_ERR_ARG, "column %zu: VARCHAR needs offsets", c);
-            const uint32_t *o = str_offsets[c];
-            for (uint32_t i = 0; i < nrows; ++i)
-                if (o[i + 1] < o[i]) return fail(FLS_ERR_ARG, "column %zu: offsets not monotone", c);
+    const uint32_t rgsz = w->fb.rowgroup_size;
+    // validate every row group before any is added
+    for (uint32_t k = 0; k < nrg; ++k) {
+        const uint32_t nrows = a[k].nrows;
+        if (nrows == 0 || nrows > rgsz) return fail(FLS_ERR_ARG, "row group needs 1..%u rows, got %u", rgsz, nrows);
+        const bool prev_short = k == 0 ? !w->fb.rgs.empty() && w->fb.rgs.back().nrows != rgsz : a[k - 1].nrows != rgsz;
+        if (prev_short) return fail(FLS_ERR_STATE, "only the last row group may be short");
+        if (!a[k].data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroup: NULL argument");
+        // test hook: fail the call that would add row group k (error paths of callers)
+        if (const char *f = getenv("FLS_TEST_FAIL_WRITER_RG"))
+            if (w->fb.rgs.size() + k == (size_t)atoi(f)) return fail(FLS_ERR_STATE, "injected writer failure at row group %s", f);
+        for (size_t c = 0; c < ncols; ++c) {
+            const ColSpec &cs = w->fb.cols[c];
+            if (!a[k].data[c]) return fail(FLS_ERR_ARG, "column %zu: NULL data", c);
+            if (cs.type == TY_VARCHAR) {
+                if (!a[k].offs || !a[k].offs[c]) return fail(FLS_ERR_ARG, "column %zu: VARCHAR needs offsets", c);
+                const uint32_t *o = a[k].offs[c];
+                for (uint32_t i = 0; i < nrows; ++i)
+                    if (o[i + 1] < o[i]) return fail(FLS_ERR_ARG, "column %zu: offsets not monotone", c);
+            }
         }
     }
-    FileBuilder::RG rg;
-    rg.nrows = nrows;
-    rg.chunks.resize(ncols);
-    rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
-    // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA
-    std::vector<uint8_t> on_gpu(ncols, 0);
-    std::vector<uint8_t *> stage(ncols, nullptr);
-    std::vector<uint64_t *> est_dict(ncols, nullptr);
-    if (w->gpu.dev >= 0) {
-        std::vector<size_t> gcols;
+    // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA / RLE / AUTO
+    std::vector<size_t> gcols;
+    if (w->gpu.dev >= 0)
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
             if (cs.type != TY_VARCHAR && !type_is_float(cs.type) &&
-                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO)) {
+                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO))
                 gcols.push_back(c);
-                on_gpu[c] = 1;
-            }
         }
-        if (!gcols.empty()) {
-            // room in the batch now; the values are staged below, with the
-            // zone maps (the caller's buffers are only valid during this
-            // call), and encoded with the batch (GpuEncoder::flush)
-            const int rc =
-                w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size(), nrows, w->threads, w->fb.rgs, stage, est_dict);
-            if (rc) return rc;
-        }
-    }
-    // columns are independent: encode them on up to w->threads threads
-    const double tc = g_prof.on ? WriterProfile::now() : 0;
-    auto encode_col = [&](size_t c) {
+    std::vector<uint8_t> on_gpu(ncols, 0);
+    for (size_t c : gcols) on_gpu[c] = 1;
+    w->pool.resize(w->threads);
+
+    struct Pending {
+        FileBuilder::RG rg;
+        const RgArgs *in;
+        std::vector<uint8_t *> stage;     // GPU columns: where their values go in pinned memory
+        std::vector<uint64_t *> est_dict; // GPU ENC_AUTO columns: the host's DICT estimate
+    };
+    std::vector<Pending> seg;
+    auto encode_col = [&](Pending &p, size_t c) {
         const ColSpec &cs = w->fb.cols[c];
+        const uint32_t nrows = p.in->nrows;
+        const void *data = p.in->data[c];
         if (cs.type == TY_VARCHAR) {
-            rg.chunks[c] = encode_str_chunk(cs.enc, str_offsets[c], (const char *)data[c], nrows);
+            p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows);
             return;
         }
         if (on_gpu[c]) {  // encoded by the GPU batch: staging copy and zone map here
-            memcpy(stage[c], data[c], (size_t)nrows * (type_value_bits(cs.type) / 8));
-            rg.zones[c] = zone_of_typed(cs.type, stage[c], nrows);
+            memcpy(p.stage[c], data, (size_t)nrows * (type_value_bits(cs.type) / 8));
+            p.rg.zones[c] = zone_of_typed(cs.type, p.stage[c], nrows);
             if (cs.enc == ENC_AUTO) {  // the one ENC_AUTO estimate the GPU does not make
-                const size_t d = est_dict_typed(type_value_bits(cs.type), stage[c], nrows);
-                *est_dict[c] = d == SIZE_MAX ? UINT64_MAX : (uint64_t)d;
+                const size_t d = est_dict_typed(type_value_bits(cs.type), p.stage[c], nrows);
+                *p.est_dict[c] = d == SIZE_MAX ? UINT64_MAX : (uint64_t)d;
             }
             return;
         }
         const int T = type_value_bits(cs.type);
         std::vector<uint64_t> v(nrows);
-        const uint8_t *p = (const uint8_t *)data[c];
+        const uint8_t *src = (const uint8_t *)data;
         for (uint32_t i = 0; i < nrows; ++i) {
             uint64_t x = 0;
-            memcpy(&x, p + (size_t)i * (T / 8), T / 8);
+            memcpy(&x, src + (size_t)i * (T / 8), T / 8);
             v[i] = x;
         }
-        rg.chunks[c] = encode_int_chunk(cs.type, cs.enc, v.data(), nrows);
-        rg.zones[c] = zone_of(cs.type, v.data(), nrows);
+        p.rg.chunks[c] = encode_int_chunk(cs.type, cs.enc, v.data(), nrows);
+        p.rg.zones[c] = zone_of(cs.type, v.data(), nrows);
     };
-    const size_t nth = std::min<size_t>(ncols, (size_t)std::max(1, w->threads));
-    if (nth <= 1) {
-        for (size_t c = 0; c < ncols; ++c) encode_col(c);
-    } else {
-        std::atomic<size_t> next{0};
-        auto work = [&]() {
-            for (size_t c; (c = next.fetch_add(1)) < ncols;) encode_col(c);
-        };
-        std::vector<std::thread> th;
-        for (size_t i = 1; i < nth; ++i) th.emplace_back(work);
-        work();
-        for (auto &t : th) t.join();
+    // encode the segment's chunks, then append its row groups in order
+    auto run_seg = [&]() {
+        if (seg.empty()) return;
+        const double tc = g_prof.on ? WriterProfile::now() : 0;
+        std::vector<std::pair<uint32_t, uint32_t>> tasks;  // (row group in segment, column)
+        tasks.reserve(seg.size() * ncols);
+        for (int pass = 0; pass < 2; ++pass)
+            for (uint32_t k = 0; k < seg.size(); ++k)
+                for (uint32_t c = 0; c < ncols; ++c)
+                    if ((w->fb.cols[c].type == TY_VARCHAR) == (pass == 0)) tasks.emplace_back(k, c);
+        w->pool.run(tasks.size(), [&](size_t t) { encode_col(seg[tasks[t].first], tasks[t].second); });
+        for (Pending &p : seg) w->fb.rgs.push_back(std::move(p.rg));
+        seg.clear();
+        if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
+    };
+    seg.reserve(nrg);
+    for (uint32_t k = 0; k < nrg; ++k) {
+        Pending p;
+        p.in = &a[k];
+        p.rg.nrows = a[k].nrows;
+        p.rg.chunks.resize(ncols);
+        p.rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
+        p.stage.assign(ncols, nullptr);
+        p.est_dict.assign(ncols, nullptr);
+        if (!gcols.empty()) {
+            // room in the batch now; the values are staged by the tasks (the
+            // caller's buffers are only valid during this call)
+            if (!w->gpu.has_room(w->fb.cols, gcols, a[k].nrows)) run_seg();
+            const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size() + seg.size(), a[k].nrows, w->threads,
+                                      w->fb.rgs, p.stage, p.est_dict);
+            if (rc) {
+                run_seg();  // the row groups already in the batch stay consistent
+                return rc;
+            }
+        }
+        seg.push_back(std::move(p));
+        // a full batch is encoded once its last row group is in place
+        if (w->gpu.dev >= 0 && w->gpu.full()) {
+            run_seg();
+            const int rc = w->gpu.submit();
+            if (rc) return rc;
+        }
     }
-    if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
-    w->fb.rgs.push_back(std::move(rg));
-    // a full batch is encoded once its last row group is in place
-    if (w->gpu.dev >= 0 && w->gpu.full()) return w->gpu.submit();
+    run_seg();
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *data,
+                            const uint32_t *const *str_offsets) {
+    if (!w || !data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroup: NULL argument");
+    const RgArgs a{nrows, data, str_offsets};
+    return add_rowgroups_impl(w, 1, &a);
+}
+
+int fls_writer_add_rowgroups(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
+                             const uint32_t *const *str_offsets) {
+    if (!w || !nrows || !data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroups: NULL argument");
+    const size_t ncols = w->fb.cols.size();
+    std::vector<RgArgs> a(nrg);
+    for (uint32_t k = 0; k < nrg; ++k)
+        a[k] = RgArgs{nrows[k], data + k * ncols, str_offsets ? str_offsets + k * ncols : nullptr};
+    return add_rowgroups_impl(w, nrg, a.data());
 }
 
 int fls_writer_set_threads(fls_writer *w, int nthreads) {

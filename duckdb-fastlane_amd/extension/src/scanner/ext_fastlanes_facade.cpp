@@ -5,8 +5,9 @@
 // box values row-major as the intended scanner expects
 // (src/scanner/scan_fastlanes.cpp:132-140).  Writes buffer DataChunks into
 // 65,536-row row groups (src/writer/write_fastlane_stream.cpp:21-24) and hand
-// them to the FastLanes writer (include/flswriter.h) on a background thread:
-// row group k is encoded while the sink buffers row group k + 1 (one deep).
+// them to the FastLanes writer (include/flswriter.h) on a background thread,
+// kBatchRowGroups at a time (fls_writer_add_rowgroups encodes their chunks in
+// parallel): a batch is encoded while the sink buffers the next one.
 #include <cstring>
 #include <future>
 #include <vector>
@@ -41,6 +42,10 @@ public:
     std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
     idx_t wrows = 0;
     idx_t rg_rows = 65536;
+    // row groups per writer call (FLS_COPY_BATCH, default 8): one call encodes
+    // every (row group, column) chunk in parallel, so a row group's slowest
+    // column does not idle the writer's other threads
+    idx_t batch_rgs = 8;
     // the row group being encoded in the background (its buffers) and the
     // writer call's result
     std::vector<std::vector<uint8_t>> pcols;
@@ -184,6 +189,7 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.wcols.assign(types.size(), {});
     s.woffs.assign(types.size(), {0});
     s.wrows = 0;
+    if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
     return true;
 }
 
@@ -204,14 +210,30 @@ bool FastLanesFacade::Impl::flush_rowgroup() {
     const uint32_t rows = (uint32_t)wrows;
     wrows = 0;
     pending = std::async(std::launch::async, [this, rows]() {
-        std::vector<const void *> data(wtypes.size());
-        std::vector<const uint32_t *> offs(wtypes.size(), nullptr);
-        for (size_t c = 0; c < wtypes.size(); ++c) {
-            data[c] = pcols[c].empty() ? (const void *)"" : pcols[c].data();
-            if (wtypes[c].id() == LogicalTypeId::VARCHAR) offs[c] = poffs[c].data();
+        // row group k of the batch: fixed-width columns at row k * rg_rows,
+        // VARCHAR columns through their offsets from k * rg_rows (offsets are
+        // into the column's whole byte buffer)
+        const size_t nc = wtypes.size();
+        const uint32_t nrg = (uint32_t)((rows + rg_rows - 1) / rg_rows);
+        std::vector<uint32_t> nrows(nrg);
+        std::vector<const void *> data((size_t)nrg * nc);
+        std::vector<const uint32_t *> offs((size_t)nrg * nc, nullptr);
+        for (uint32_t k = 0; k < nrg; ++k) {
+            const idx_t r0 = (idx_t)k * rg_rows;
+            nrows[k] = (uint32_t)std::min<idx_t>(rg_rows, rows - r0);
+            for (size_t c = 0; c < nc; ++c) {
+                if (wtypes[c].id() == LogicalTypeId::VARCHAR) {
+                    data[k * nc + c] = pcols[c].empty() ? (const void *)"" : pcols[c].data();
+                    offs[k * nc + c] = poffs[c].data() + r0;
+                } else {
+                    const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(wtypes[c]));
+                    data[k * nc + c] = pcols[c].data() + r0 * w;
+                }
+            }
         }
-        return fls_writer_add_rowgroup(writer, rows, data.data(), offs.data()) == 0 ? std::string()
-                                                                                  : std::string(fls_last_error());
+        return fls_writer_add_rowgroups(writer, nrg, nrows.data(), data.data(), offs.data()) == 0
+                   ? std::string()
+                   : std::string(fls_last_error());
     });
     return true;
 }
@@ -235,10 +257,10 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             return false;
         }
     // column-major: append each column's slice up to the row-group boundary
-    // in bulk, then let the writer encode the full row group (column-parallel)
+    // in bulk; a full batch of row groups goes to the writer
     idx_t r0 = 0;
     while (r0 < chunk.size()) {
-        const idx_t n = std::min<idx_t>(chunk.size() - r0, s.rg_rows - s.wrows);
+        const idx_t n = std::min<idx_t>(chunk.size() - r0, s.rg_rows - s.wrows % s.rg_rows);
         for (size_t c = 0; c < s.wtypes.size(); ++c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
@@ -250,6 +272,12 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                 std::vector<uint32_t> &offs = s.woffs[c];
                 const size_t o0 = offs.size();
                 offs.resize(o0 + n);
+                uint64_t bytes = 0;
+                for (idx_t r = 0; r < n; ++r) bytes += str[r0 + r].GetSize();
+                if (col.size() + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
+                    s.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
+                    return false;
+                }
                 uint32_t end = (uint32_t)col.size();
                 for (idx_t r = 0; r < n; ++r) offs[o0 + r] = end += (uint32_t)str[r0 + r].GetSize();
                 size_t at = col.size();
@@ -279,7 +307,14 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
         }
         s.wrows += n;
         r0 += n;
-        if (s.wrows == s.rg_rows && !s.flush_rowgroup()) return false;
+        // at a row-group boundary: hand the batch over when it is full, or
+        // early when a VARCHAR buffer nears the offsets' 32-bit range
+        if (s.wrows % s.rg_rows == 0) {
+            bool big = false;
+            for (size_t c = 0; c < s.wtypes.size(); ++c)
+                big |= s.wtypes[c].id() == LogicalTypeId::VARCHAR && s.wcols[c].size() > (1ull << 30);
+            if ((s.wrows == s.rg_rows * s.batch_rgs || big) && !s.flush_rowgroup()) return false;
+        }
     }
     return true;
 }

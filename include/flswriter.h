@@ -72,6 +72,14 @@ int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_
  * (str_offsets may be NULL when there is no VARCHAR column). */
 int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *data,
                             const uint32_t *const *str_offsets);
+/* Append nrg row groups in one call (rows nrows[k]; data / str_offsets hold
+ * nrg * ncols pointers, row group k's column c at [k * ncols + c], as in
+ * fls_writer_add_rowgroup).  The file is the same as from nrg calls of
+ * fls_writer_add_rowgroup; the (row group, column) chunks are encoded in
+ * parallel across the row groups, so a row group's slowest column does not
+ * idle the other threads (the COPY sink hands over 8 row groups at a time). */
+int fls_writer_add_rowgroups(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
+                             const uint32_t *const *str_offsets);
 /* Assemble the file: to `path`, or into a malloc'ed buffer freed with
  * fls_image_free. */
 int fls_writer_finish_file(fls_writer *w, const char *path);

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--copy", action="store_true")
     ap.add_argument("--gpu", action="store_true", help="also the writer with fls_writer_set_device(0)")
+    ap.add_argument("--batch", type=int, default=8, help="row groups per fls_writer_add_rowgroups call (arm)")
     a = ap.parse_args()
     import pkgload
     fl = pkgload.load()
@@ -76,8 +77,10 @@ def main():
                 data[c] = part.ctypes.data
         parts.append((r1 - r0, data, offs, keep))
     ref_bytes = None
-    arms = [(th, -1) for th in sorted({1, a.threads})] + ([(a.threads, 0)] if a.gpu else [])
-    for th, dev in arms:
+    arms = [(th, -1, 1) for th in sorted({1, a.threads})] + [(a.threads, -1, a.batch)]
+    if a.gpu:
+        arms += [(a.threads, 0, 1), (a.threads, 0, a.batch)]
+    for th, dev, batch in arms:
         w = lib.fls_writer_new(0)
         lib.fls_writer_set_threads.argtypes = [C.c_void_p, C.c_int]
         lib.fls_writer_set_threads(w, th)
@@ -86,8 +89,20 @@ def main():
         for name, ty, vals, enc, wd, sc in cols:
             fl._check(lib.fls_writer_add_column(w, name.encode(), ty, wd, sc, enc))
         t0 = time.perf_counter()
-        for m, data, offs, _ in parts:
-            fl._check(lib.fls_writer_add_rowgroup(w, m, data, offs))
+        if batch == 1:
+            for m, data, offs, _ in parts:
+                fl._check(lib.fls_writer_add_rowgroup(w, m, data, offs))
+        else:  # batch row groups per call: pointer arrays laid out row group by row group
+            nc = len(cols)
+            for b0 in range(0, len(parts), batch):
+                grp = parts[b0:b0 + batch]
+                rows = (C.c_uint32 * len(grp))(*[g[0] for g in grp])
+                data = (C.c_void_p * (nc * len(grp)))()
+                offs = (C.c_void_p * (nc * len(grp)))()
+                for k, (_, d, o, _) in enumerate(grp):
+                    for c in range(nc):
+                        data[k * nc + c], offs[k * nc + c] = d[c], o[c]
+                fl._check(lib.fls_writer_add_rowgroups(w, len(grp), rows, data, offs))
         p, ln = C.c_void_p(), C.c_uint64()
         fl._check(lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)))
         dt = time.perf_counter() - t0
@@ -99,7 +114,8 @@ def main():
             same = ", bytes identical to the 1-thread CPU file" if out == ref_bytes else ", BYTES DIFFER"
         lib.fls_image_free(p)
         lib.fls_writer_free(w)
-        where = f"GPU {dev} + {th} threads" if dev >= 0 else f"{th} threads"
+        where = (f"GPU {dev} + {th} threads" if dev >= 0 else f"{th} threads") + \
+            (f", {batch} row groups per call" if batch > 1 else "")
         print(f"C-ABI writer (ENC_AUTO, {where}), lineitem SF{a.scale:g}: {n} rows x {len(cols)} cols in "
               f"{dt:.2f} s = {n / dt / 1e6:.2f} M rows/s, {raw / dt / 1e6:.0f} MB/s of input -> "
               f"{ln.value / 1e6:.0f} MB (ratio {raw / ln.value:.2f}){same}", flush=True)

@@ -120,3 +120,20 @@ def test_copy_background_writer_failure_is_reported(ext, tmpfile, monkeypatch, f
     n = 65536 + 1000
     with pytest.raises(ExtError, match="injected writer failure at row group %d" % fail_rg):
         ext.copy_values([("a", "INTEGER", list(range(n)))], tmpfile("fail.fls"))
+
+
+@pytest.mark.parametrize("batch", ["1", "2", "8"])
+def test_copy_batches_of_row_groups_cpu(ext, ref, tmpfile, monkeypatch, batch):
+    """The sink hands the writer FLS_COPY_BATCH row groups per call
+    (fls_writer_add_rowgroups): 4 row groups, the last partial, in batches of
+    1, 2 and 8 decode (oracle) to the source values, VARCHAR offsets included."""
+    monkeypatch.setenv("FLS_COPY_BATCH", batch)
+    n = 3 * 65536 + 1000
+    a = [(i * 7919) % 100003 - 50000 for i in range(n)]
+    s = [f"w{i % 7}" * (i % 4) for i in range(n)]
+    dst = tmpfile(f"batch{batch}.fls")
+    assert ext.copy_values([("a", "INTEGER", a), ("s", "VARCHAR", s)], dst) == n
+    rf = ref.RefFile(open(dst, "rb").read())
+    assert rf.nrows == n and rf.nrowgroups == 4
+    assert np.concatenate([rf.decode(0, g) for g in range(4)]).view(np.int32).tolist() == a
+    assert rf.strings_column(1) == [x.encode() for x in s]

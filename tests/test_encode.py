@@ -232,3 +232,17 @@ def test_gpu_writer_rle_bytes_identical(fl, ref, gpu, n, rowgroup):
     for c, (_, ty, vals, _) in enumerate(cols):
         got = np.concatenate([rf.decode(c, r) for r in range(rf.nrowgroups)])
         assert np.array_equal(got.view(vals.dtype), vals), cols[c][0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [5, 16, 40])
+@pytest.mark.parametrize("n,rowgroup", [(1024 * 70 + 3, 1024), (65536 * 2 + 777, 65536)])
+def test_gpu_writer_batched_rowgroups_bytes_identical(fl, gpu, batch, n, rowgroup):
+    """fls_writer_add_rowgroups with the GPU encoder: calls whose row groups
+    span the encoder's 32-row-group batches (a batch is submitted mid-call,
+    once every row group in it is staged) write the CPU writer's bytes."""
+    cols = _auto_columns(fl, n, np.random.default_rng(n + batch)) + \
+        [("s", fl.VARCHAR, ["row %d" % (i % 977) for i in range(n)], fl.ENC_AUTO)]
+    cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0, batch=batch, threads=8).tobytes()
+    assert cpu == dev

@@ -181,3 +181,49 @@ def test_gpu_empty_table_device_paths(fl, gpu):
     assert list(t.scan()) == []
     with pytest.raises(fl.FlsError, match="out of bounds"):
         t.device_upload()
+
+
+def _mixed_columns(fl, n, seed):
+    rng = np.random.default_rng(seed)
+    words = ["alpha", "beta", "gamma", "a much longer string value %d" % seed, ""]
+    return [("k", fl.INT64, np.cumsum(rng.integers(0, 5, n)), fl.ENC_AUTO),
+            ("q", fl.INT32, rng.integers(1, 51, n), fl.ENC_AUTO),
+            ("r", fl.INT16, np.repeat(rng.integers(-9, 9, n // 50 + 1), 50)[:n], fl.ENC_AUTO),
+            ("d", fl.DOUBLE, np.round(rng.random(n) * 1000, 2), fl.ENC_AUTO),
+            ("s", fl.VARCHAR, [words[i] for i in rng.integers(0, len(words), n)], fl.ENC_AUTO),
+            ("t", fl.VARCHAR, ["comment %d of row %d" % (x, i) for i, x in enumerate(rng.integers(0, 10**6, n))],
+             fl.ENC_FSST)]
+
+
+@pytest.mark.parametrize("batch,threads,rgsz,n", [(8, 8, 1024, 9 * 1024 + 17), (3, 4, 2048, 7 * 2048),
+                                                   (16, 1, 1024, 5000), (4, 8, 65536, 65536 * 2 + 5)])
+def test_add_rowgroups_batches_match_single_calls(fl, ref, batch, threads, rgsz, n):
+    # fls_writer_add_rowgroups: (row group, column) tasks across the batch,
+    # the same file as one fls_writer_add_rowgroup call per row group
+    cols = _mixed_columns(fl, n, batch + rgsz)
+    one = fl.write_image(cols, rowgroup=rgsz, threads=1)
+    many = fl.write_image(cols, rowgroup=rgsz, batch=batch, threads=threads)
+    assert bytes(one.view()) == bytes(many.view())
+    rf = ref.RefFile(many)
+    assert rf.nrows == n and rf.nrowgroups == (n + rgsz - 1) // rgsz
+
+
+def test_add_rowgroups_rejects_short_group_before_the_last(fl):
+    import ctypes as C
+    lib = fl.lib
+    w = lib.fls_writer_new(0)
+    try:
+        fl._check(lib.fls_writer_set_rowgroup_size(w, 1024))
+        fl._check(lib.fls_writer_add_column(w, b"v", fl.INT32, 0, 0, fl.ENC_FFOR))
+        a, b = np.arange(1000, dtype=np.int32), np.arange(1024, dtype=np.int32)
+        rows = (C.c_uint32 * 2)(1000, 1024)
+        data = (C.c_void_p * 2)(a.ctypes.data, b.ctypes.data)
+        assert lib.fls_writer_add_rowgroups(w, 2, rows, data, None) != 0
+        assert "short" in fl.last_error()
+        rows = (C.c_uint32 * 2)(1024, 1000)
+        data = (C.c_void_p * 2)(b.ctypes.data, a.ctypes.data)
+        fl._check(lib.fls_writer_add_rowgroups(w, 2, rows, data, None))
+        # nothing may follow a short row group
+        assert lib.fls_writer_add_rowgroups(w, 1, (C.c_uint32 * 1)(1024), (C.c_void_p * 1)(b.ctypes.data), None) != 0
+    finally:
+        lib.fls_writer_free(w)
