@@ -10,6 +10,7 @@
 // parallel): a batch is encoded while the sink buffers the next one.
 #include <cstring>
 #include <future>
+#include <memory>
 #include <vector>
 
 #include <algorithm>
@@ -22,6 +23,36 @@
 
 namespace duckdb {
 namespace ext_fastlane {
+
+// Growable byte buffer whose growth leaves the new bytes uninitialised: the
+// sink overwrites them at once (std::vector::resize would zero them first,
+// doubling the sink's memory traffic).
+class RawBuf {
+public:
+    uint8_t *data() { return p_.get(); }
+    const uint8_t *data() const { return p_.get(); }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    void clear() { n_ = 0; }
+    // k more bytes at the end; returns where they start
+    uint8_t *grow(size_t k) {
+        if (n_ + k > cap_) {
+            const size_t cap = std::max<size_t>({n_ + k, 2 * cap_, 4096});
+            std::unique_ptr<uint8_t[]> q(new uint8_t[cap]);
+            if (n_) memcpy(q.get(), p_.get(), n_);
+            p_ = std::move(q);
+            cap_ = cap;
+        }
+        uint8_t *at = p_.get() + n_;
+        n_ += k;
+        return at;
+    }
+    void shrink(size_t k) { n_ -= k; }
+
+private:
+    std::unique_ptr<uint8_t[]> p_;
+    size_t n_ = 0, cap_ = 0;
+};
 
 class FastLanesFacade::Impl {
 public:
@@ -38,7 +69,7 @@ public:
     std::string error;                               // why the last call returned false (lastError)
     std::vector<LogicalType> wtypes;
     std::vector<std::string> wnames;
-    std::vector<std::vector<uint8_t>> wcols;         // fixed-width buffered rows
+    std::vector<RawBuf> wcols;                       // fixed-width buffered rows / VARCHAR bytes
     std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
     idx_t wrows = 0;
     idx_t rg_rows = 65536;
@@ -48,7 +79,7 @@ public:
     idx_t batch_rgs = 8;
     // the row group being encoded in the background (its buffers) and the
     // writer call's result
-    std::vector<std::vector<uint8_t>> pcols;
+    std::vector<RawBuf> pcols;
     std::vector<std::vector<uint32_t>> poffs;
     std::future<std::string> pending;  // "" or the writer's error (fls_last_error is per thread)
     // wait for the background row group; false if its encode failed
@@ -186,7 +217,8 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.out_path = file_path;
     s.wtypes = types;
     s.wnames = names;
-    s.wcols.assign(types.size(), {});
+    s.wcols.clear();
+    s.wcols.resize(types.size());
     s.woffs.assign(types.size(), {0});
     s.wrows = 0;
     if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
@@ -264,10 +296,11 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
         for (size_t c = 0; c < s.wtypes.size(); ++c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
-            std::vector<uint8_t> &col = s.wcols[c];
+            RawBuf &col = s.wcols[c];
             if (t.id() == LogicalTypeId::VARCHAR) {
-                // sizes first, then one resize and a copy per string (no
-                // per-row capacity checks)
+                // sizes first, then one growth and a copy per string (no
+                // per-row capacity checks; an inlined string is copied as its
+                // whole 12-byte inline field, into 12 bytes of slack)
                 const string_t *str = FlatVector::GetData<string_t>(v);
                 std::vector<uint32_t> &offs = s.woffs[c];
                 const size_t o0 = offs.size();
@@ -280,12 +313,13 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                 }
                 uint32_t end = (uint32_t)col.size();
                 for (idx_t r = 0; r < n; ++r) offs[o0 + r] = end += (uint32_t)str[r0 + r].GetSize();
-                size_t at = col.size();
-                col.resize(end);
+                uint8_t *dst = col.grow(bytes + string_t::INLINE_LENGTH);
+                col.shrink(string_t::INLINE_LENGTH);
                 for (idx_t r = r0; r < r0 + n; ++r) {
-                    const uint32_t len = (uint32_t)str[r].GetSize();
-                    memcpy(col.data() + at, str[r].GetData(), len);
-                    at += len;
+                    const uint32_t len = str[r].GetSize();
+                    if (len <= string_t::INLINE_LENGTH) memcpy(dst, str[r].GetData(), string_t::INLINE_LENGTH);
+                    else memcpy(dst, str[r].GetData(), len);
+                    dst += len;
                 }
                 continue;
             }
@@ -293,9 +327,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
             const idx_t pw = PhysicalWidth(t);
             const uint8_t *src = FlatVector::GetData<uint8_t>(v) + r0 * pw;
-            const size_t at = col.size();
-            col.resize(at + n * w);
-            uint8_t *dst = col.data() + at;
+            uint8_t *dst = col.grow(n * w);
             if (pw == w) {
                 memcpy(dst, src, n * w);
             } else {  // narrow DECIMAL: sign-extend

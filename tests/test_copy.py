@@ -130,7 +130,7 @@ def test_copy_batches_of_row_groups_cpu(ext, ref, tmpfile, monkeypatch, batch):
     monkeypatch.setenv("FLS_COPY_BATCH", batch)
     n = 3 * 65536 + 1000
     a = [(i * 7919) % 100003 - 50000 for i in range(n)]
-    s = [f"w{i % 7}" * (i % 4) for i in range(n)]
+    s = [f"w{i % 7}" * (i % 11) for i in range(n)]  # 0..20 bytes: inlined and pointer string_t
     dst = tmpfile(f"batch{batch}.fls")
     assert ext.copy_values([("a", "INTEGER", a), ("s", "VARCHAR", s)], dst) == n
     rf = ref.RefFile(open(dst, "rb").read())
