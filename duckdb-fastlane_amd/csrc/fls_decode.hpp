@@ -76,13 +76,15 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 // the ring is kept zero past the decoded bytes by the flush (no zeroing pass
 // per round); kFsstW6 = registers budgeted for 6 waves per SIMD instead of 4;
 // kFsstCirc = circular ring indexed by decoded position (no tail move per
-// round; with zero-at-flush).
+// round; with zero-at-flush); kFsstLenFromSym = a symbol's length taken from
+// its bits instead of a second table read, in chunks whose symbols all end in
+// a non-zero byte (the others keep the table read).
 // Default kFsstW6 | kFsstZeroFlush (80 VGPRs, no spill in the standalone
 // kernel): l_comment SF10 1.074 -> 1.012 (descriptor in SGPRs) -> 0.969
 // (6-wave budget) -> 0.922 ms (zero at flush); Plain and TwoQ measured slower
 // (profiles/r2/abenv_fsst_var_l_comment.txt).
 enum : int {
-    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16,
+    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16, kFsstLenFromSym = 32,
     kFsstDefault = kFsstW6 | kFsstZeroFlush
 };
 // How one FSST launch runs (launch_fsst).

@@ -156,7 +156,12 @@ struct QwordWriter {
 // entry is {0, 0} -- and a symbol its length; nothing past the stream end,
 // FULL = no lane of the round reaches it).  Returns the lane's byte count;
 // st_out = the state after its last valid byte (held across an empty tail).
-template <int BPL, bool FULL>
+// Byte count of a staged symbol from its bits (LFS, kFsstLenFromSym): the
+// table is masked to the symbols' lengths, so a symbol whose last byte is not
+// zero has length ceil(bit length / 8), and the escape entry (0) length 0.
+__device__ __forceinline__ uint32_t len_from_sym(uint64_t x) { return (71u - (uint32_t)__clzll((long long)x)) >> 3; }
+
+template <int BPL, bool FULL, bool LFS = false>
 __device__ __forceinline__ uint32_t lane_codes(const Wave &w, const v4u &raw, uint32_t nb, uint32_t carry,
                                                uint32_t lane, uint64_t (&v)[BPL], uint32_t (&n)[BPL],
                                                uint32_t &st_out) {
@@ -167,7 +172,7 @@ __device__ __forceinline__ uint32_t lane_codes(const Wave &w, const v4u &raw, ui
     for (uint32_t k = 0; k < BPL; ++k) {  // all table reads issued together
         code[k] = byte_of(raw, k);
         sy[k] = w.sym[code[k]];
-        sl[k] = w.len[code[k]];
+        sl[k] = LFS ? len_from_sym(sy[k]) : (uint32_t)w.len[code[k]];
         if ((FULL || k < nb) && code[k] != kFsstEscape) last = (int32_t)k;
     }
     const uint32_t end = FULL ? (uint32_t)BPL : nb;
@@ -243,7 +248,8 @@ __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t 
 template <int BPL, bool SMALL, int V>
 __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t base, uint32_t nvals,
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
-                            uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err) {
+                            uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err,
+                            bool table_lfs = false) {
     bool bad = false;
     // kFsstCirc: a circular ring of kCirc bytes (a power of two) indexed by
     // decoded byte position mod kCirc, so retire() moves no tail, it only
@@ -422,7 +428,10 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         bool plain = false;
         if constexpr ((V & kFsstPlain) != 0) plain = full && carry_lit == 0 && __ballot(has_escape<BPL>(raw)) == 0;
         const uint32_t lane_out = plain  ? lane_codes_plain<BPL>(w, raw, v, n)
-                                  : full ? lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end)
+                                  : full ? ((V & kFsstLenFromSym) && table_lfs
+                                                ? lane_codes<BPL, true, (V & kFsstLenFromSym) != 0>(w, raw, nb, carry_lit,
+                                                                                                    lane, v, n, lane_end)
+                                                : lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end))
                                          : lane_codes<BPL, false>(w, raw, nb, carry_lit, lane, v, n, lane_end);
         const uint32_t incl = scan_incl(lane_out, lane);
         // write the round into the ring: normally all 64 lanes at once; when
@@ -559,6 +568,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     uint32_t ci = lo;
     DevChunk c = load_chunk(chunks, ci);
     bool have_table = false;
+    bool table_lfs = false;  // kFsstLenFromSym: every symbol's last byte is non-zero
     for (uint32_t item = item0;;) {
         if (item >= item1) {
             if constexpr (!QUEUE) break;
@@ -580,12 +590,15 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
             wave_sync();
             const FLS_GLOBAL uint64_t *gs = reinterpret_cast<const FLS_GLOBAL uint64_t *>(aux);
             FLS_LDS uint64_t *ls = reinterpret_cast<FLS_LDS uint64_t *>(L + Layout::kOffSym);
+            bool zero_last = false;
             for (uint32_t k = lane; k < 256; k += 64) {
                 const uint32_t n = k == kFsstEscape ? 0u : min((uint32_t)aux[8 * 256 + k], 8u);
-                const uint64_t sy = gs[k];
-                ls[k] = n >= 8 ? sy : sy & ((1ull << (8 * n)) - 1);
+                const uint64_t sy = n >= 8 ? gs[k] : gs[k] & ((1ull << (8 * n)) - 1);
+                ls[k] = sy;
                 L[Layout::kOffLen + k] = (uint8_t)n;
+                zero_last |= n > 0 && ((sy >> (8 * (n - 1))) & 0xFF) == 0;
             }
+            table_lfs = __ballot(zero_last) == 0;
             wave_sync();
             have_table = true;
         }
@@ -598,7 +611,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
         const uint32_t dbytes = uni(meta->aux_count);
         fsst_vector<BPL, SMALL, V>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
                     (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
-                    gptr(c.out) + 16ull * kVectorSize * v, lane, err);
+                    gptr(c.out) + 16ull * kVectorSize * v, lane, err, table_lfs);
         wave_sync();
         ++item;
     }
@@ -675,7 +688,7 @@ template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     if constexpr (BPL == 8) {
-        switch (how.variant & 31) {
+        switch (how.variant & 63) {
         case 0: return launch_fsst_v<BPL, SMALL, 0>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstPlain: return launch_fsst_v<BPL, SMALL, kFsstPlain>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstTwoQ: return launch_fsst_v<BPL, SMALL, kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
@@ -684,6 +697,9 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         case kFsstW6: return launch_fsst_v<BPL, SMALL, kFsstW6>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstZeroFlush:
             return launch_fsst_v<BPL, SMALL, kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstW6 | kFsstZeroFlush | kFsstLenFromSym:
+            return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush | kFsstLenFromSym>(d_chunks, nchunks, nvecs,
+                                                                                       d_err, stream, how);
         case kFsstW6 | kFsstZeroFlush | kFsstCirc:
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush | kFsstCirc>(d_chunks, nchunks, nvecs, d_err,
                                                                                  stream, how);
