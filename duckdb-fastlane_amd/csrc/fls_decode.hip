@@ -779,8 +779,14 @@ __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const D
                                                         uint32_t *__restrict__ err, uint32_t p_bytes,
                                                         uint32_t v_bytes, uint32_t *__restrict__ queue,
                                                         const uint32_t *__restrict__ split, uint32_t npieces,
-                                                        uint32_t shared_queue) {
+                                                        uint32_t flags) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    // flags bit 0: the queue is shared by several grids; bits 1-2: wave issue
+    // priority (s_setprio) for a grid that runs beside the FSST kernel
+    const uint32_t shared_queue = flags & 1u, prio = (flags >> 1) & 3u;
+    if (prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio == 3) __builtin_amdgcn_s_setprio(3);
     const uint32_t w = uni(threadIdx.x >> 6);
     const uint32_t lp = (uint32_t)(size_t)((lu8 *)lds_raw + w * (p_bytes + v_bytes));
     const uint32_t lv = lp + p_bytes;
@@ -869,7 +875,7 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream, uint32_t *d_queue, const uint32_t *d_split, SplitPlan plan,
-                         bool shared_queue) {
+                         bool shared_queue, int prio) {
     if (nchunks == 0) return hipSuccess;
     const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
     int grid;
@@ -884,7 +890,8 @@ hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
-                       geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces, (uint32_t)(shared_queue && d_queue));
+                       geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces,
+                       (uint32_t)(shared_queue && d_queue) | (uint32_t)(prio & 3) << 1);
     return hipGetLastError();
 }
 

@@ -62,7 +62,7 @@ struct SplitPlan {
 // drain it (every chunk from the queue, none static).
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream, uint32_t *d_queue = nullptr, const uint32_t *d_split = nullptr,
-                         SplitPlan plan = SplitPlan(), bool shared_queue = false);
+                         SplitPlan plan = SplitPlan(), bool shared_queue = false, int prio = 0);
 // Waves of a resident decode launch with this LDS geometry.
 uint32_t decode_waves(const DecodeGeom &geom);
 // Split the vectors of h[0, n) over at most nw waves: static_pct % of the

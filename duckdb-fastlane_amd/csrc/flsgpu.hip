@@ -686,22 +686,28 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
 // FLS_OVERLAP_FSST_WPC (0 FSST waves = no overlap).
 // Overlap vs one-after-the-other at the per-GPU shares of 1/2/4/8-GPU runs
 // (same-buffer A/B on lineitem_full, profiles/r2/abenv_overlap_scales.txt,
-// abenv_sf12p5.txt, abenv_minvecs.txt): overlapped is faster at SF25 (5.90 vs
-// 6.26 ms), SF50 (12.0 vs 12.9) and SF100 (23.1 vs 26.0); at SF12.5 (286 FSST
-// vectors per CU) it was 3 % slower on one box and 2 % faster on another.  So
-// the default overlaps every launch; FLS_OVERLAP_MIN_VECS_PER_CU runs launches
-// with fewer FSST vectors per CU serially.
+// abenv_sf12p5.txt, abenv_minvecs.txt, abenv_overlap_grid.txt,
+// abenv_overlap_prio.txt): overlapped is faster at SF25 (5.90 vs 6.26 ms),
+// SF50 (12.0 vs 12.9) and SF100 (23.1 vs 26.0, 23.9 vs 26.4); at SF12.5 (286
+// FSST vectors per CU, the per-GPU share of an 8-GPU run) serial was faster on
+// three boxes of four (3.41 vs 3.46, 3.11 vs 3.18, 3.36 vs 3.45 ms; 3.16 vs
+// 3.09 on the fourth).  So launches with fewer than 400 FSST vectors per CU
+// run serially (FLS_OVERLAP_MIN_VECS_PER_CU).  The main kernel's wave issue
+// priority while overlapped (FLS_OVERLAP_DECODE_PRIO, s_setprio 1-3) measured
+// within 0.1 % of the default.
 struct OverlapSplit {
     // 12 FSST waves per CU beside 1 decode block: 1.6-2 % faster than 16 at
     // SF100 and SF12.5 (profiles/r2/abenv_v12.txt)
     int decode_bpc = 1, fsst_wpc = 12;
-    uint32_t min_vecs_per_cu = 0;
+    uint32_t min_vecs_per_cu = 400;
+    int decode_prio = 0;  // FLS_OVERLAP_DECODE_PRIO: s_setprio of the main kernel's waves while overlapped
 };
 OverlapSplit overlap_split() {
     OverlapSplit o;
     if (const char *e = getenv("FLS_OVERLAP_DECODE_BPC")) o.decode_bpc = std::max(1, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_FSST_WPC")) o.fsst_wpc = std::max(0, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_MIN_VECS_PER_CU")) o.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
+    if (const char *e = getenv("FLS_OVERLAP_DECODE_PRIO")) o.decode_prio = std::min(3, std::max(0, atoi(e)));
     return o;
 }
 
@@ -757,11 +763,13 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
         FsstLaunch ns = small, na = any;
         ns.waves_per_cu = na.waves_per_cu = ov.fsst_wpc;
         // main stream: narrow decode, then full FSST
-        if (e == hipSuccess) e = launch_decode(d_chunks, nmain, d_err, narrow, stream, d_queue, nullptr, SplitPlan(), true);
+        if (e == hipSuccess)
+            e = launch_decode(d_chunks, nmain, d_err, narrow, stream, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
         // side stream: narrow FSST, then full decode
         if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, side->stream, ns);
         if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, side->stream, na);
-        if (e == hipSuccess) e = launch_decode(d_chunks, nmain, d_err, geom, side->stream, d_queue, nullptr, SplitPlan(), true);
+        if (e == hipSuccess)
+            e = launch_decode(d_chunks, nmain, d_err, geom, side->stream, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
         if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, small);
         if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, stream, any);
         if (e == hipSuccess) e = hipEventRecord(side->join, side->stream);

@@ -222,16 +222,22 @@ def test_gpu_alp_fsst_scan_pipeline(fl, ref, gpu, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wl,split", [("lineitem_full", None), ("lineitem_full", "0"), ("lineitem_full", "1,28"),
+@pytest.mark.parametrize("wl,split", [("lineitem_full", "default"), ("lineitem_full", None),
+                                      ("lineitem_full", "0"), ("lineitem_full", "1,28"),
                                       ("lineitem_full", "4,1"), ("lineitem_dbl", None)],
-                         ids=["full-overlap", "full-serial", "full-fsst-wide", "full-fsst-narrow", "dbl"])
+                         ids=["full-default", "full-overlap", "full-serial", "full-fsst-wide", "full-fsst-narrow",
+                              "dbl"])
 def test_gpu_full_fidelity_lineitem(fl, ref, gpu, monkeypatch, wl, split):
     """Full-fidelity lineitem; with FSST columns the table decode overlaps the
-    FSST kernels with the main one (launch_all): default split, serial
-    (FLS_OVERLAP_FSST_WPC=0) and extreme splits must all decode exactly."""
+    FSST kernels with the main one (launch_all): the default split, serial
+    (FLS_OVERLAP_FSST_WPC=0) and extreme splits must all decode exactly.  At
+    SF0.1 the default runs serially (fewer FSST vectors per CU than
+    FLS_OVERLAP_MIN_VECS_PER_CU); the overlapped cases lower that threshold."""
+    if split != "default":
+        monkeypatch.setenv("FLS_OVERLAP_MIN_VECS_PER_CU", "0")
     if split == "0":
         monkeypatch.setenv("FLS_OVERLAP_FSST_WPC", "0")
-    elif split:
+    elif split and split != "default":
         bpc, wpc = split.split(",")
         monkeypatch.setenv("FLS_OVERLAP_DECODE_BPC", bpc)
         monkeypatch.setenv("FLS_OVERLAP_FSST_WPC", wpc)
