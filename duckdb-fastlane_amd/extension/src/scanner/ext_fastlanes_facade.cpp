@@ -8,6 +8,8 @@
 // them to the FastLanes writer (include/flswriter.h) on a background thread,
 // kBatchRowGroups at a time (fls_writer_add_rowgroups encodes their chunks in
 // parallel): a batch is encoded while the sink buffers the next one.
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <future>
 #include <memory>
@@ -23,6 +25,16 @@
 
 namespace duckdb {
 namespace ext_fastlane {
+
+// FLS_COPY_PROFILE=1: where a COPY's time goes (sink copies, waits for the
+// background writer, the final write), printed to stderr at finalizeFile
+struct CopyProfile {
+    bool on = std::getenv("FLS_COPY_PROFILE") != nullptr;
+    double sink = 0, wait = 0, encode = 0, finish = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+};
 
 // Growable byte buffer whose growth leaves the new bytes uninitialised: the
 // sink overwrites them at once (std::vector::resize would zero them first,
@@ -82,10 +94,14 @@ public:
     std::vector<RawBuf> pcols;
     std::vector<std::vector<uint32_t>> poffs;
     std::future<std::string> pending;  // "" or the writer's error (fls_last_error is per thread)
+    CopyProfile prof;
+    double encode_s = 0;  // background writer calls (written by the writer thread, read after get())
     // wait for the background row group; false if its encode failed
     bool wait_pending() {
         if (!pending.valid()) return true;
+        const double t0 = prof.on ? CopyProfile::now() : 0;
         const std::string e = pending.get();
+        if (prof.on) prof.wait += CopyProfile::now() - t0;
         if (!e.empty()) error = "FastLanes writer: " + e;
         return e.empty();
     }
@@ -263,9 +279,10 @@ bool FastLanesFacade::Impl::flush_rowgroup() {
                 }
             }
         }
-        return fls_writer_add_rowgroups(writer, nrg, nrows.data(), data.data(), offs.data()) == 0
-                   ? std::string()
-                   : std::string(fls_last_error());
+        const double t0 = prof.on ? CopyProfile::now() : 0;
+        const int rc = fls_writer_add_rowgroups(writer, nrg, nrows.data(), data.data(), offs.data());
+        if (prof.on) encode_s += CopyProfile::now() - t0;
+        return rc == 0 ? std::string() : std::string(fls_last_error());
     });
     return true;
 }
@@ -278,6 +295,14 @@ static idx_t PhysicalWidth(const LogicalType &t) {
 
 bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     Impl &s = *pImpl;
+    const double t_in = s.prof.on ? CopyProfile::now() : 0;
+    struct Tally {  // sink time of this call, less its waits for the writer
+        Impl &s;
+        double t_in, w_in;
+        ~Tally() {
+            if (s.prof.on) s.prof.sink += CopyProfile::now() - t_in - (s.prof.wait - w_in);
+        }
+    } tally{s, t_in, s.prof.wait};
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
     chunk.Flatten();
     // The container has no validity bitmap yet: a NULL would come back as 0 or
@@ -363,9 +388,16 @@ bool FastLanesFacade::finalizeFile() {
     if (!s.writer) return false;
     bool ok = s.flush_rowgroup();
     ok = s.wait_pending() && ok;
+    const double t0 = s.prof.on ? CopyProfile::now() : 0;
     if (ok && fls_writer_finish_file(s.writer, s.out_path.c_str()) != 0) {
         s.error = std::string("FastLanes writer: ") + fls_last_error();
         ok = false;
+    }
+    if (s.prof.on) {
+        s.prof.finish += CopyProfile::now() - t0;
+        fprintf(stderr, "COPY sink profile: DataChunk copies %.3f s, waits for the writer %.3f s, writer calls %.3f s "
+                        "(background), file assembly + write %.3f s\n",
+                s.prof.sink, s.prof.wait, s.encode_s, s.prof.finish);
     }
     fls_writer_free(s.writer);
     s.writer = nullptr;
