@@ -13,6 +13,7 @@
 #include <cstring>
 #include <future>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include <algorithm>
@@ -81,8 +82,13 @@ public:
     std::string error;                               // why the last call returned false (lastError)
     std::vector<LogicalType> wtypes;
     std::vector<std::string> wnames;
-    std::vector<RawBuf> wcols;                       // fixed-width buffered rows / VARCHAR bytes
-    std::vector<std::vector<uint32_t>> woffs;        // VARCHAR offsets
+    std::vector<RawBuf> wcols;   // fixed-width buffered rows
+    // VARCHAR columns: the sink keeps DuckDB's 16-byte string_t records (one
+    // bulk copy per slice) and the bytes of the non-inlined strings, whose
+    // pointer field it rewrites to their offset in warena; the background
+    // task turns them into the writer's bytes + offsets, a thread per column
+    std::vector<RawBuf> wrec, warena;
+    std::vector<uint64_t> wbytes;  // string bytes per VARCHAR column in the batch
     idx_t wrows = 0;
     idx_t rg_rows = 65536;
     // row groups per writer call (FLS_COPY_BATCH, default 8): one call encodes
@@ -91,7 +97,7 @@ public:
     idx_t batch_rgs = 8;
     // the row group being encoded in the background (its buffers) and the
     // writer call's result
-    std::vector<RawBuf> pcols;
+    std::vector<RawBuf> pcols, prec, parena;
     std::vector<std::vector<uint32_t>> poffs;
     std::future<std::string> pending;  // "" or the writer's error (fls_last_error is per thread)
     CopyProfile prof;
@@ -233,9 +239,11 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.out_path = file_path;
     s.wtypes = types;
     s.wnames = names;
-    s.wcols.clear();
-    s.wcols.resize(types.size());
-    s.woffs.assign(types.size(), {0});
+    for (auto *b : {&s.wcols, &s.wrec, &s.warena}) {
+        b->clear();
+        b->resize(types.size());
+    }
+    s.wbytes.assign(types.size(), 0);
     s.wrows = 0;
     if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
     return true;
@@ -247,17 +255,53 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
 bool FastLanesFacade::Impl::flush_rowgroup() {
     if (wrows == 0) return true;
     if (!wait_pending()) return false;
-    pcols.resize(wtypes.size());
+    for (auto *b : {&pcols, &prec, &parena}) b->resize(wtypes.size());
     poffs.resize(wtypes.size());
     std::swap(pcols, wcols);
-    std::swap(poffs, woffs);
+    std::swap(prec, wrec);
+    std::swap(parena, warena);
     for (size_t c = 0; c < wtypes.size(); ++c) {
         wcols[c].clear();
-        woffs[c].assign(1, 0);
+        wrec[c].clear();
+        warena[c].clear();
+        wbytes[c] = 0;
     }
     const uint32_t rows = (uint32_t)wrows;
     wrows = 0;
     pending = std::async(std::launch::async, [this, rows]() {
+        const double t0 = prof.on ? CopyProfile::now() : 0;
+        // VARCHAR columns: string_t records -> bytes + offsets (a thread per column)
+        auto assemble = [this, rows](size_t c) {
+            const uint8_t *rec = prec[c].data();
+            std::vector<uint32_t> &o = poffs[c];
+            o.resize((size_t)rows + 1);
+            o[0] = 0;
+            for (uint32_t r = 0; r < rows; ++r) {
+                uint32_t len;
+                memcpy(&len, rec + 16ull * r, 4);
+                o[r + 1] = o[r] + len;
+            }
+            RawBuf &col = pcols[c];
+            col.clear();
+            uint8_t *dst = col.grow((size_t)o[rows] + string_t::INLINE_LENGTH);
+            col.shrink(string_t::INLINE_LENGTH);
+            for (uint32_t r = 0; r < rows; ++r) {
+                const uint8_t *x = rec + 16ull * r;
+                const uint32_t len = o[r + 1] - o[r];
+                if (len <= string_t::INLINE_LENGTH) {
+                    memcpy(dst, x + 4, string_t::INLINE_LENGTH);
+                } else {
+                    uint64_t off;
+                    memcpy(&off, x + 8, 8);
+                    memcpy(dst, parena[c].data() + off, len);
+                }
+                dst += len;
+            }
+        };
+        std::vector<std::thread> th;
+        for (size_t c = 0; c < wtypes.size(); ++c)
+            if (wtypes[c].id() == LogicalTypeId::VARCHAR) th.emplace_back(assemble, c);
+        for (auto &t : th) t.join();
         // row group k of the batch: fixed-width columns at row k * rg_rows,
         // VARCHAR columns through their offsets from k * rg_rows (offsets are
         // into the column's whole byte buffer)
@@ -279,7 +323,6 @@ bool FastLanesFacade::Impl::flush_rowgroup() {
                 }
             }
         }
-        const double t0 = prof.on ? CopyProfile::now() : 0;
         const int rc = fls_writer_add_rowgroups(writer, nrg, nrows.data(), data.data(), offs.data());
         if (prof.on) encode_s += CopyProfile::now() - t0;
         return rc == 0 ? std::string() : std::string(fls_last_error());
@@ -323,29 +366,27 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             const LogicalType &t = s.wtypes[c];
             RawBuf &col = s.wcols[c];
             if (t.id() == LogicalTypeId::VARCHAR) {
-                // sizes first, then one growth and a copy per string (no
-                // per-row capacity checks; an inlined string is copied as its
-                // whole 12-byte inline field, into 12 bytes of slack)
-                const string_t *str = FlatVector::GetData<string_t>(v);
-                std::vector<uint32_t> &offs = s.woffs[c];
-                const size_t o0 = offs.size();
-                offs.resize(o0 + n);
+                // the records in one copy; the non-inlined strings' bytes to
+                // the arena, their pointer field := arena offset
+                const string_t *str = FlatVector::GetData<string_t>(v) + r0;
+                uint8_t *rec = s.wrec[c].grow(n * sizeof(string_t));
+                memcpy(rec, str, n * sizeof(string_t));
                 uint64_t bytes = 0;
-                for (idx_t r = 0; r < n; ++r) bytes += str[r0 + r].GetSize();
-                if (col.size() + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
+                for (idx_t r = 0; r < n; ++r) {
+                    const uint32_t len = str[r].GetSize();
+                    bytes += len;
+                    if (len > string_t::INLINE_LENGTH) {
+                        RawBuf &ar = s.warena[c];
+                        const uint64_t off = ar.size();
+                        memcpy(ar.grow(len), str[r].GetData(), len);
+                        memcpy(rec + sizeof(string_t) * r + 8, &off, 8);
+                    }
+                }
+                if (s.wbytes[c] + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
                     s.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
                     return false;
                 }
-                uint32_t end = (uint32_t)col.size();
-                for (idx_t r = 0; r < n; ++r) offs[o0 + r] = end += (uint32_t)str[r0 + r].GetSize();
-                uint8_t *dst = col.grow(bytes + string_t::INLINE_LENGTH);
-                col.shrink(string_t::INLINE_LENGTH);
-                for (idx_t r = r0; r < r0 + n; ++r) {
-                    const uint32_t len = str[r].GetSize();
-                    if (len <= string_t::INLINE_LENGTH) memcpy(dst, str[r].GetData(), string_t::INLINE_LENGTH);
-                    else memcpy(dst, str[r].GetData(), len);
-                    dst += len;
-                }
+                s.wbytes[c] += bytes;
                 continue;
             }
             // the physical bytes (FLOAT/DOUBLE bit-exact for ALP); DECIMAL widened to int64
@@ -369,7 +410,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
         if (s.wrows % s.rg_rows == 0) {
             bool big = false;
             for (size_t c = 0; c < s.wtypes.size(); ++c)
-                big |= s.wtypes[c].id() == LogicalTypeId::VARCHAR && s.wcols[c].size() > (1ull << 30);
+                big |= s.wbytes[c] > (1ull << 30);
             if ((s.wrows == s.rg_rows * s.batch_rgs || big) && !s.flush_rowgroup()) return false;
         }
     }
@@ -395,8 +436,8 @@ bool FastLanesFacade::finalizeFile() {
     }
     if (s.prof.on) {
         s.prof.finish += CopyProfile::now() - t0;
-        fprintf(stderr, "COPY sink profile: DataChunk copies %.3f s, waits for the writer %.3f s, writer calls %.3f s "
-                        "(background), file assembly + write %.3f s\n",
+        fprintf(stderr, "COPY sink profile: DataChunk copies %.3f s, waits for the writer %.3f s, string assembly + "
+                        "writer calls %.3f s (background), file assembly + write %.3f s\n",
                 s.prof.sink, s.prof.wait, s.encode_s, s.prof.finish);
     }
     fls_writer_free(s.writer);
