@@ -31,7 +31,7 @@ namespace ext_fastlane {
 // background writer, the final write), printed to stderr at finalizeFile
 struct CopyProfile {
     bool on = std::getenv("FLS_COPY_PROFILE") != nullptr;
-    double sink = 0, wait = 0, encode = 0, finish = 0;
+    double sink = 0, wait = 0, encode = 0, finish = 0, prep = 0, fixed = 0, str = 0;
     static double now() {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     }
@@ -347,6 +347,13 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
         }
     } tally{s, t_in, s.prof.wait};
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
+    double tp = t_in;
+    auto lap = [&](double &acc) {  // profile: time since the last lap into acc
+        if (!s.prof.on) return;
+        const double t = CopyProfile::now();
+        acc += t - tp;
+        tp = t;
+    };
     chunk.Flatten();
     // The container has no validity bitmap yet: a NULL would come back as 0 or
     // '' and a pushed-down IS NULL would match nothing, so refuse it instead of
@@ -356,6 +363,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             s.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
             return false;
         }
+    lap(s.prof.prep);
     // column-major: append each column's slice up to the row-group boundary
     // in bulk; a full batch of row groups goes to the writer
     idx_t r0 = 0;
@@ -387,6 +395,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                     return false;
                 }
                 s.wbytes[c] += bytes;
+                lap(s.prof.str);
                 continue;
             }
             // the physical bytes (FLOAT/DOUBLE bit-exact for ALP); DECIMAL widened to int64
@@ -402,6 +411,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                     memcpy(dst + 8 * i, &x, 8);
                 }
             }
+            lap(s.prof.fixed);
         }
         s.wrows += n;
         r0 += n;
@@ -436,9 +446,11 @@ bool FastLanesFacade::finalizeFile() {
     }
     if (s.prof.on) {
         s.prof.finish += CopyProfile::now() - t0;
-        fprintf(stderr, "COPY sink profile: DataChunk copies %.3f s, waits for the writer %.3f s, string assembly + "
-                        "writer calls %.3f s (background), file assembly + write %.3f s\n",
-                s.prof.sink, s.prof.wait, s.encode_s, s.prof.finish);
+        fprintf(stderr,
+                "COPY sink profile: DataChunk copies %.3f s (flatten + validity %.3f, fixed-width %.3f, VARCHAR %.3f), "
+                "waits for the writer %.3f s, string assembly + writer calls %.3f s (background), file assembly + "
+                "write %.3f s\n",
+                s.prof.sink, s.prof.prep, s.prof.fixed, s.prof.str, s.prof.wait, s.encode_s, s.prof.finish);
     }
     fls_writer_free(s.writer);
     s.writer = nullptr;
