@@ -573,6 +573,9 @@ using copy_to_sink_t = void (*)(ExecutionContext &, FunctionData &, GlobalFuncti
                                 DataChunk &);
 using copy_to_combine_t = void (*)(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &);
 using copy_to_finalize_t = void (*)(ClientContext &, FunctionData &, GlobalFunctionData &);
+enum class CopyFunctionExecutionMode : uint8_t { REGULAR_COPY_TO_FILE, PARALLEL_COPY_TO_FILE, BATCH_COPY_TO_FILE };
+using copy_to_execution_mode_t = CopyFunctionExecutionMode (*)(bool preserve_insertion_order, bool supports_batch_index);
+using copy_desired_batch_size_t = idx_t (*)(ClientContext &, FunctionData &);
 
 class CopyFunction {
 public:
@@ -585,6 +588,8 @@ public:
     copy_to_sink_t copy_to_sink = nullptr;
     copy_to_combine_t copy_to_combine = nullptr;
     copy_to_finalize_t copy_to_finalize = nullptr;
+    copy_to_execution_mode_t execution_mode = nullptr;
+    copy_desired_batch_size_t desired_batch_size = nullptr;
     std::function<TableFunction()> copy_from_function;  // COPY ... FROM
 };
 

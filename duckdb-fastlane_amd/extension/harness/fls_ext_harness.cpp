@@ -356,6 +356,27 @@ int fls_ext_has_named_parameter(fls_ext_db *d, const char *fn, const char *name,
     return 1;
 }
 
+// The copy function's execution mode for (preserve_insertion_order,
+// supports_batch_index) as DuckDB's planner asks it (0 REGULAR, 1 PARALLEL,
+// 2 BATCH, -1 no callback / no function) and its desired batch size for the
+// given COPY options (-1 without the callback)
+int fls_ext_copy_mode(fls_ext_db *d, const char *fmt, int preserve, int batch_index, const char *const *opt_keys,
+                      const char *const *opt_vals, int nopts, int64_t *batch_rows) {
+    if (!d) return -1;
+    auto it = d->db.copy_functions.find(fmt);
+    if (it == d->db.copy_functions.end() || !it->second.execution_mode) return -1;
+    CopyFunction &cf = it->second;
+    *batch_rows = -1;
+    if (cf.desired_batch_size && cf.copy_to_bind) {
+        CopyInfo info;
+        for (int i = 0; i < nopts; ++i) info.options[StringUtil::Lower(opt_keys[i])].push_back(Value(opt_vals[i]));
+        CopyFunctionBindInput cbin{info};
+        auto bind = cf.copy_to_bind(d->ctx, cbin, vector<string>{"a"}, vector<LogicalType>{LogicalType::INTEGER});
+        *batch_rows = (int64_t)cf.desired_batch_size(d->ctx, *bind);
+    }
+    return (int)cf.execution_mode(preserve != 0, batch_index != 0);
+}
+
 // SELECT name() for a zero-argument scalar function: its one VARCHAR value
 // rendered into buf (cap bytes); -1 when there is no such function
 int fls_ext_scalar0(fls_ext_db *d, const char *name, char *buf, int cap) {

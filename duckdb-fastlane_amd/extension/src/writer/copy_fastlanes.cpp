@@ -96,6 +96,21 @@ void CopySink(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, Lo
 
 void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &) {}
 
+// The reference's mode callback (src/writer/write_fastlane_stream.cpp:251-260)
+// answers PARALLEL without insertion order and BATCH for a batch-index source,
+// but registers no prepare_batch / flush_batch, which DuckDB's batch copy
+// calls; here an ordered COPY keeps the single (REGULAR) sink, and an
+// unordered one runs sinks on every thread, serialised by the global lock.
+CopyFunctionExecutionMode CopyExecutionMode(bool preserve_insertion_order, bool /*supports_batch_index*/) {
+    return preserve_insertion_order ? CopyFunctionExecutionMode::REGULAR_COPY_TO_FILE
+                                    : CopyFunctionExecutionMode::PARALLEL_COPY_TO_FILE;
+}
+
+// Rows per batch: one row group (write_fastlane_stream.cpp:262-265)
+idx_t CopyDesiredBatchSize(ClientContext &, FunctionData &bind_p) {
+    return bind_p.Cast<FastlaneCopyBindData>().row_group_size;
+}
+
 void CopyFinalize(ClientContext &, FunctionData &, GlobalFunctionData &gstate) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
     std::lock_guard<std::mutex> guard(g.lock);
@@ -115,6 +130,8 @@ void RegisterFastlaneCopyFunction(DatabaseInstance &db) {
     fn.copy_to_sink = CopySink;
     fn.copy_to_combine = CopyCombine;
     fn.copy_to_finalize = CopyFinalize;
+    fn.execution_mode = CopyExecutionMode;
+    fn.desired_batch_size = CopyDesiredBatchSize;
     fn.copy_from_function = ReadFastlanesFunction;
     fn.extension = "fls";
     ExtensionUtil::RegisterFunction(db, fn);

@@ -48,6 +48,18 @@ class Ext:
         f.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int]
         return bool(f(self.db, fn.encode(), name.encode(), type_id))
 
+    def copy_mode(self, fmt: str, preserve: bool, batch_index: bool, opts=None):
+        """(execution mode 0/1/2 = REGULAR/PARALLEL/BATCH or -1, desired batch rows or -1)"""
+        f = self.lib.fls_ext_copy_mode
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int,
+                      C.POINTER(C.c_int64)]
+        opts = opts or {}
+        keys = (C.c_char_p * max(1, len(opts)))(*[k.encode() for k in opts])
+        vals = (C.c_char_p * max(1, len(opts)))(*[str(v).encode() for v in opts.values()])
+        rows = C.c_int64()
+        mode = f(self.db, fmt.encode(), int(preserve), int(batch_index), keys, vals, len(opts), C.byref(rows))
+        return mode, rows.value
+
     def scalar0(self, name: str):
         """SELECT name() for a zero-argument scalar function (None: not registered)"""
         f = self.lib.fls_ext_scalar0

@@ -137,3 +137,16 @@ def test_copy_batches_of_row_groups_cpu(ext, ref, tmpfile, monkeypatch, batch):
     assert rf.nrows == n and rf.nrowgroups == 4
     assert np.concatenate([rf.decode(0, g) for g in range(4)]).view(np.int32).tolist() == a
     assert rf.strings_column(1) == [x.encode() for x in s]
+
+
+@pytest.mark.parametrize("fmt", ["fls", "fastlane"])
+def test_copy_execution_mode_and_batch_size(ext, fmt):
+    """Like the reference's registration (src/writer/write_fastlane_stream.cpp:
+    251-265): an unordered COPY runs parallel sinks, the desired batch is one
+    row group (ROW_GROUP_SIZE); an ordered COPY keeps one sink (REGULAR), also
+    for a batch-index source, since no prepare_batch / flush_batch exist."""
+    assert ext.copy_mode(fmt, preserve=False, batch_index=False) == (1, 65536)
+    assert ext.copy_mode(fmt, preserve=False, batch_index=True) == (1, 65536)
+    assert ext.copy_mode(fmt, preserve=True, batch_index=False)[0] == 0
+    assert ext.copy_mode(fmt, preserve=True, batch_index=True)[0] == 0
+    assert ext.copy_mode(fmt, True, True, {"ROW_GROUP_SIZE": 8192}) == (0, 8192)
