@@ -368,7 +368,8 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     // in bulk; a full batch of row groups goes to the writer
     idx_t r0 = 0;
     while (r0 < chunk.size()) {
-        const idx_t n = std::min<idx_t>(chunk.size() - r0, s.rg_rows - s.wrows % s.rg_rows);
+        // (a slice is at most one vector: the VARCHAR path's position list)
+        const idx_t n = std::min<idx_t>({chunk.size() - r0, s.rg_rows - s.wrows % s.rg_rows, STANDARD_VECTOR_SIZE});
         for (size_t c = 0; c < s.wtypes.size(); ++c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
@@ -379,16 +380,24 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                 const string_t *str = FlatVector::GetData<string_t>(v) + r0;
                 uint8_t *rec = s.wrec[c].grow(n * sizeof(string_t));
                 memcpy(rec, str, n * sizeof(string_t));
+                // lengths and the positions of the non-inlined strings without
+                // a data-dependent branch (inlined and pointer strings alternate
+                // unpredictably in a column like l_shipinstruct), then their bytes
+                uint32_t longs[STANDARD_VECTOR_SIZE];
+                uint32_t nl = 0;
                 uint64_t bytes = 0;
                 for (idx_t r = 0; r < n; ++r) {
                     const uint32_t len = str[r].GetSize();
                     bytes += len;
-                    if (len > string_t::INLINE_LENGTH) {
-                        RawBuf &ar = s.warena[c];
-                        const uint64_t off = ar.size();
-                        memcpy(ar.grow(len), str[r].GetData(), len);
-                        memcpy(rec + sizeof(string_t) * r + 8, &off, 8);
-                    }
+                    longs[nl] = (uint32_t)r;
+                    nl += len > string_t::INLINE_LENGTH ? 1u : 0u;
+                }
+                RawBuf &ar = s.warena[c];
+                for (uint32_t i = 0; i < nl; ++i) {
+                    const uint32_t r = longs[i], len = str[r].GetSize();
+                    const uint64_t off = ar.size();
+                    memcpy(ar.grow(len), str[r].GetData(), len);
+                    memcpy(rec + sizeof(string_t) * r + 8, &off, 8);
                 }
                 if (s.wbytes[c] + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
                     s.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
