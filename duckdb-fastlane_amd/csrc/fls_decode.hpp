@@ -78,14 +78,16 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 // kFsstCirc = circular ring indexed by decoded position (no tail move per
 // round; with zero-at-flush); kFsstLenFromSym = a symbol's length taken from
 // its bits instead of a second table read, in chunks whose symbols all end in
-// a non-zero byte (the others keep the table read).
-// Default kFsstW6 | kFsstZeroFlush (80 VGPRs, no spill in the standalone
-// kernel): l_comment SF10 1.074 -> 1.012 (descriptor in SGPRs) -> 0.969
-// (6-wave budget) -> 0.922 ms (zero at flush); Plain and TwoQ measured slower
-// (profiles/r2/abenv_fsst_var_l_comment.txt).
+// a non-zero byte (the others keep the table read); kFsstAbsLds = LDS
+// addresses as integers from 0 (no symbol base added per access).
+// Default kFsstW6 | kFsstZeroFlush | kFsstAbsLds (80 VGPRs, no spill in the
+// standalone kernel): l_comment SF10 1.074 -> 1.012 (descriptor in SGPRs) ->
+// 0.969 (6-wave budget) -> 0.922 ms (zero at flush) -> 1.2 % less (absolute
+// LDS addresses, profiles/r2/abenv_fsst_abslds.txt); Plain, TwoQ, Circ and
+// LenFromSym measured slower (profiles/r2/abenv_fsst_*.txt).
 enum : int {
-    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16, kFsstLenFromSym = 32,
-    kFsstDefault = kFsstW6 | kFsstZeroFlush
+    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16, kFsstLenFromSym = 32, kFsstAbsLds = 64,
+    kFsstDefault = kFsstW6 | kFsstZeroFlush | kFsstAbsLds
 };
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {

@@ -636,7 +636,16 @@ __global__ __launch_bounds__(64, (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_k
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw_generic[];
     // an LDS-typed pointer to the dynamic LDS (a known constant address, so
     // table and ring offsets fold into the DS instructions' offset fields)
-    lu8 *lds_raw = (lu8 *)lds_raw_generic;
+    // kFsstAbsLds: the same addresses as plain integers (the kernel has no
+    // static LDS, so its dynamic LDS starts at address 0; checked), which lets
+    // the compiler fold table and ring offsets without adding a symbol base
+    if constexpr ((V & kFsstAbsLds) != 0) {
+        if ((uint32_t)(size_t)lds_raw_generic != 0u) {
+            if (threadIdx.x == 0) atomicOr(err, KERR_BAD_DESC);
+            return;
+        }
+    }
+    lu8 *lds_raw = (V & kFsstAbsLds) ? (lu8 *)(size_t)0 : (lu8 *)lds_raw_generic;
     uint32_t i0 = 0, i1 = 0;
     if (!QUEUE) {
         const uint32_t nwaves = gridDim.x, wave = blockIdx.x;
@@ -688,7 +697,7 @@ template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     if constexpr (BPL == 8) {
-        switch (how.variant & 63) {
+        switch (how.variant & 127) {
         case 0: return launch_fsst_v<BPL, SMALL, 0>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstPlain: return launch_fsst_v<BPL, SMALL, kFsstPlain>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstTwoQ: return launch_fsst_v<BPL, SMALL, kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
@@ -697,6 +706,8 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         case kFsstW6: return launch_fsst_v<BPL, SMALL, kFsstW6>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstZeroFlush:
             return launch_fsst_v<BPL, SMALL, kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstW6 | kFsstZeroFlush:
+            return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstW6 | kFsstZeroFlush | kFsstLenFromSym:
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush | kFsstLenFromSym>(d_chunks, nchunks, nvecs,
                                                                                        d_err, stream, how);
@@ -704,7 +715,7 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush | kFsstCirc>(d_chunks, nchunks, nvecs, d_err,
                                                                                  stream, how);
         default:
-            return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
+            return launch_fsst_v<BPL, SMALL, kFsstDefault>(d_chunks, nchunks, nvecs, d_err, stream, how);
         }
     }
     return launch_fsst_v<BPL, SMALL, kFsstDefault>(d_chunks, nchunks, nvecs, d_err, stream, how);

@@ -43,7 +43,7 @@ def test_decode_kernel_fits_four_waves(res):
 
 
 def test_default_fsst_kernel_fits_six_waves(res):
-    # fsst_kernel<8, SMALL, QUEUE, kFsstW6 | kFsstZeroFlush = 12>
-    hits = _find(res, "fsst_kernelILi8E", "ELi12EEEv")
+    # fsst_kernel<8, SMALL, QUEUE, kFsstW6 | kFsstZeroFlush | kFsstAbsLds = 76>
+    hits = _find(res, "fsst_kernelILi8E", "ELi76EEEv")
     assert len(hits) == 4, hits
     assert all(r["vgpr"] <= 80 for r in hits.values()), hits
