@@ -79,14 +79,16 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 // round; with zero-at-flush); kFsstLenFromSym = a symbol's length taken from
 // its bits instead of a second table read, in chunks whose symbols all end in
 // a non-zero byte (the others keep the table read); kFsstAbsLds = LDS
-// addresses as integers from 0 (no symbol base added per access).
+// addresses as integers from 0 (no symbol base added per access);
+// kFsstEarlyGather = a round's table reads issued before the previous round's
+// retire() (slower: spills at 6 waves, 5 waves without).
 // Default kFsstW6 | kFsstZeroFlush | kFsstAbsLds (80 VGPRs, no spill in the
 // standalone kernel): l_comment SF10 1.074 -> 1.012 (descriptor in SGPRs) ->
 // 0.969 (6-wave budget) -> 0.922 ms (zero at flush) -> 1.2 % less (absolute
 // LDS addresses, profiles/r2/abenv_fsst_abslds.txt); Plain, TwoQ, Circ and
 // LenFromSym measured slower (profiles/r2/abenv_fsst_*.txt).
 enum : int {
-    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16, kFsstLenFromSym = 32, kFsstAbsLds = 64,
+    kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16, kFsstLenFromSym = 32, kFsstAbsLds = 64, kFsstEarlyGather = 128,
     kFsstDefault = kFsstW6 | kFsstZeroFlush | kFsstAbsLds
 };
 // How one FSST launch runs (launch_fsst).

@@ -161,18 +161,35 @@ struct QwordWriter {
 // zero has length ceil(bit length / 8), and the escape entry (0) length 0.
 __device__ __forceinline__ uint32_t len_from_sym(uint64_t x) { return (71u - (uint32_t)__clzll((long long)x)) >> 3; }
 
+// The table entries of a lane's BPL codes (kFsstEarlyGather: read before the
+// previous round's retire(), so their LDS latency runs under its work).
+template <int BPL>
+struct Gathered {
+    uint64_t sy[BPL];
+    uint32_t sl[BPL];
+};
+template <int BPL>
+__device__ __forceinline__ void gather_codes(const Wave &w, const v4u &raw, Gathered<BPL> &g) {
+#pragma unroll
+    for (uint32_t k = 0; k < BPL; ++k) {
+        const uint32_t c = byte_of(raw, k);
+        g.sy[k] = w.sym[c];
+        g.sl[k] = w.len[c];
+    }
+}
+
 template <int BPL, bool FULL, bool LFS = false>
 __device__ __forceinline__ uint32_t lane_codes(const Wave &w, const v4u &raw, uint32_t nb, uint32_t carry,
                                                uint32_t lane, uint64_t (&v)[BPL], uint32_t (&n)[BPL],
-                                               uint32_t &st_out) {
+                                               uint32_t &st_out, const Gathered<BPL> *pre = nullptr) {
     uint32_t code[BPL], sl[BPL];
     uint64_t sy[BPL];
     int32_t last = -1;  // last non-0xFF byte of the lane's segment
 #pragma unroll
     for (uint32_t k = 0; k < BPL; ++k) {  // all table reads issued together
         code[k] = byte_of(raw, k);
-        sy[k] = w.sym[code[k]];
-        sl[k] = LFS ? len_from_sym(sy[k]) : (uint32_t)w.len[code[k]];
+        sy[k] = pre ? pre->sy[k] : w.sym[code[k]];
+        sl[k] = pre ? pre->sl[k] : LFS ? len_from_sym(sy[k]) : (uint32_t)w.len[code[k]];
         if ((FULL || k < nb) && code[k] != kFsstEscape) last = (int32_t)k;
     }
     const uint32_t end = FULL ? (uint32_t)BPL : nb;
@@ -416,6 +433,11 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, (uint32_t)BPL) : 0u;
         const v4u raw = raw_next;  // the next round's bytes load while this one decodes
         if (r0 + kRound < comp_len) raw_next = load_raw(r0 + kRound);
+        const bool full = r0 + kRound <= comp_len;
+        Gathered<BPL> pre;
+        if constexpr ((V & kFsstEarlyGather) != 0) {
+            if (full) gather_codes<BPL>(w, raw, pre);
+        }
         // the previous round's stores go out now, after this round's load was
         // issued and a whole decode before the next wait (vmcnt counts loads
         // and stores in issue order, and the variable store count makes that
@@ -424,14 +446,14 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         if (r0 > 0) retire();
         uint32_t n[BPL], lane_end = 0;
         uint64_t v[BPL];
-        const bool full = r0 + kRound <= comp_len;
         bool plain = false;
         if constexpr ((V & kFsstPlain) != 0) plain = full && carry_lit == 0 && __ballot(has_escape<BPL>(raw)) == 0;
         const uint32_t lane_out = plain  ? lane_codes_plain<BPL>(w, raw, v, n)
                                   : full ? ((V & kFsstLenFromSym) && table_lfs
                                                 ? lane_codes<BPL, true, (V & kFsstLenFromSym) != 0>(w, raw, nb, carry_lit,
                                                                                                     lane, v, n, lane_end)
-                                                : lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end))
+                                                : lane_codes<BPL, true>(w, raw, nb, carry_lit, lane, v, n, lane_end,
+                                                                        (V & kFsstEarlyGather) ? &pre : nullptr))
                                          : lane_codes<BPL, false>(w, raw, nb, carry_lit, lane, v, n, lane_end);
         const uint32_t incl = scan_incl(lane_out, lane);
         // write the round into the ring: normally all 64 lanes at once; when
@@ -697,7 +719,7 @@ template <int BPL, bool SMALL>
 hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     if constexpr (BPL == 8) {
-        switch (how.variant & 127) {
+        switch (how.variant & 255) {
         case 0: return launch_fsst_v<BPL, SMALL, 0>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstPlain: return launch_fsst_v<BPL, SMALL, kFsstPlain>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstTwoQ: return launch_fsst_v<BPL, SMALL, kFsstTwoQ>(d_chunks, nchunks, nvecs, d_err, stream, how);
@@ -708,6 +730,12 @@ hipError_t launch_fsst_t(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
             return launch_fsst_v<BPL, SMALL, kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case kFsstW6 | kFsstZeroFlush:
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstZeroFlush | kFsstAbsLds | kFsstEarlyGather:
+            return launch_fsst_v<BPL, SMALL, kFsstZeroFlush | kFsstAbsLds | kFsstEarlyGather>(d_chunks, nchunks, nvecs,
+                                                                                            d_err, stream, how);
+        case kFsstDefault | kFsstEarlyGather:
+            return launch_fsst_v<BPL, SMALL, kFsstDefault | kFsstEarlyGather>(d_chunks, nchunks, nvecs, d_err, stream,
+                                                                            how);
         case kFsstW6 | kFsstZeroFlush | kFsstLenFromSym:
             return launch_fsst_v<BPL, SMALL, kFsstW6 | kFsstZeroFlush | kFsstLenFromSym>(d_chunks, nchunks, nvecs,
                                                                                        d_err, stream, how);

@@ -739,7 +739,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     const OverlapSplit ov = overlap_split();
     FsstLaunch small, any;
     small.bytes_per_lane = any.bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
-    if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 127;
+    if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 255;
     small.small = true;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
