@@ -725,14 +725,36 @@ int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj
 // COPY (SELECT * FROM (VALUES ...) t(names)) TO dst (FORMAT format): literal
 // rows, cells[row * ncols + col] as text or NULL for SQL NULL, in one chunk per
 // STANDARD_VECTOR_SIZE rows.  Types: INTEGER, BIGINT, DOUBLE, VARCHAR.
+int fls_ext_copy_values_mt(fls_ext_db *d, const char *format, const char *dst, int ncols, const char *const *names,
+                           const char *const *type_names, int64_t nrows, const char *const *cells,
+                           const char *const *opt_keys, const char *const *opt_vals, int nopts, int nthreads,
+                           uint64_t *rows);
+
 int fls_ext_copy_values(fls_ext_db *d, const char *format, const char *dst, int ncols, const char *const *names,
                         const char *const *type_names, int64_t nrows, const char *const *cells, uint64_t *rows) {
+    return fls_ext_copy_values_mt(d, format, dst, ncols, names, type_names, nrows, cells, nullptr, nullptr, 0, 1,
+                                  rows);
+}
+
+// The same with COPY options and nthreads sink threads, as DuckDB's
+// PhysicalCopyToFile runs a parallel sink: each thread its own local state,
+// chunk k sunk by thread k % nthreads, combine per local state, then finalize.
+// nthreads > 1 needs the function to answer PARALLEL_COPY_TO_FILE for an
+// unordered COPY (preserve_insertion_order = false).
+int fls_ext_copy_values_mt(fls_ext_db *d, const char *format, const char *dst, int ncols, const char *const *names,
+                           const char *const *type_names, int64_t nrows, const char *const *cells,
+                           const char *const *opt_keys, const char *const *opt_vals, int nopts, int nthreads,
+                           uint64_t *rows) {
     try {
         const std::string fmt = StringUtil::Lower(format ? format : "");
         auto it = d->db.copy_functions.find(fmt);
         if (it == d->db.copy_functions.end())
             throw CatalogException("Copy Function with name " + fmt + " does not exist!");
         CopyFunction &cf = it->second;
+        if (nthreads < 1) nthreads = 1;
+        if (nthreads > 1 && (!cf.execution_mode ||
+                             cf.execution_mode(false, false) != CopyFunctionExecutionMode::PARALLEL_COPY_TO_FILE))
+            throw NotImplementedException("harness: " + fmt + " has no parallel COPY sink");
         vector<string> cn;
         vector<LogicalType> ct;
         for (int c = 0; c < ncols; ++c) {
@@ -745,31 +767,52 @@ int fls_ext_copy_values(fls_ext_db *d, const char *format, const char *dst, int 
             else throw BinderException("harness: unsupported VALUES type " + tn);
         }
         CopyInfo info;
+        for (int i = 0; i < nopts; ++i) info.options[StringUtil::Lower(opt_keys[i])].push_back(Value(opt_vals[i]));
         CopyFunctionBindInput cbin{info};
         auto bind = cf.copy_to_bind(d->ctx, cbin, cn, ct);
         auto gstate = cf.copy_to_initialize_global(d->ctx, *bind, dst ? dst : "");
-        ExecutionContext ectx(d->ctx);
-        auto lstate = cf.copy_to_initialize_local(ectx, *bind);
-        DataChunk chunk;
-        chunk.Initialize(ct);
-        for (int64_t r0 = 0; r0 < nrows; r0 += STANDARD_VECTOR_SIZE) {
-            const idx_t n = (idx_t)std::min<int64_t>(STANDARD_VECTOR_SIZE, nrows - r0);
-            chunk.Reset();
-            for (int c = 0; c < ncols; ++c)
-                for (idx_t i = 0; i < n; ++i) {
-                    const char *x = cells[(r0 + (int64_t)i) * ncols + c];
-                    Value v;
-                    if (!x) v = Value();
-                    else if (ct[c].id() == LogicalTypeId::INTEGER) v = Value::INTEGER(std::atoi(x));
-                    else if (ct[c].id() == LogicalTypeId::BIGINT) v = Value::BIGINT(std::atoll(x));
-                    else if (ct[c].id() == LogicalTypeId::DOUBLE) v = Value::DOUBLE(std::atof(x));
-                    else v = Value(std::string(x));
-                    chunk.data[c].SetValue(i, v);
-                }
-            chunk.SetCardinality(n);
-            cf.copy_to_sink(ectx, *bind, *gstate, *lstate, chunk);
+        auto worker = [&](int t) {
+            ExecutionContext ectx(d->ctx);
+            auto lstate = cf.copy_to_initialize_local(ectx, *bind);
+            DataChunk chunk;
+            chunk.Initialize(ct);
+            const int64_t step = (int64_t)STANDARD_VECTOR_SIZE * nthreads;
+            for (int64_t r0 = (int64_t)STANDARD_VECTOR_SIZE * t; r0 < nrows; r0 += step) {
+                const idx_t n = (idx_t)std::min<int64_t>(STANDARD_VECTOR_SIZE, nrows - r0);
+                chunk.Reset();
+                for (int c = 0; c < ncols; ++c)
+                    for (idx_t i = 0; i < n; ++i) {
+                        const char *x = cells[(r0 + (int64_t)i) * ncols + c];
+                        Value v;
+                        if (!x) v = Value();
+                        else if (ct[c].id() == LogicalTypeId::INTEGER) v = Value::INTEGER(std::atoi(x));
+                        else if (ct[c].id() == LogicalTypeId::BIGINT) v = Value::BIGINT(std::atoll(x));
+                        else if (ct[c].id() == LogicalTypeId::DOUBLE) v = Value::DOUBLE(std::atof(x));
+                        else v = Value(std::string(x));
+                        chunk.data[c].SetValue(i, v);
+                    }
+                chunk.SetCardinality(n);
+                cf.copy_to_sink(ectx, *bind, *gstate, *lstate, chunk);
+            }
+            if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
+        };
+        if (nthreads == 1) {
+            worker(0);
+        } else {
+            std::vector<std::thread> pool;
+            std::vector<std::string> errs(nthreads);
+            for (int t = 0; t < nthreads; ++t)
+                pool.emplace_back([&, t] {
+                    try {
+                        worker(t);
+                    } catch (const std::exception &e) {
+                        errs[t] = e.what();
+                    }
+                });
+            for (auto &th : pool) th.join();
+            for (auto &e : errs)
+                if (!e.empty()) throw Exception(e);
         }
-        if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
         cf.copy_to_finalize(d->ctx, *bind, *gstate);
         if (rows) *rows = (uint64_t)nrows;
         return 0;

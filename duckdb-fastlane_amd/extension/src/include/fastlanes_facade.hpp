@@ -51,6 +51,25 @@ public:
     // Not in the reference's header: why the last writeChunk returned false
     // (empty when no reason was recorded), for COPY's error message.
     const std::string &lastError() const;
+
+    // Not in the reference's header: thread-local staging for COPY sinks.
+    // Each sink thread copies its DataChunks into its own Stage; a Stage that
+    // holds a full batch of row groups hands it to the writer (the hand-off is
+    // serialised, the copies are not).  mergeStage moves a Stage's remaining
+    // rows (fewer than one batch) into the facade's own buffers at row-group
+    // boundaries, so only the file's last row group can be short.  With one
+    // sink thread the file's row order is the input order; with several it is
+    // the order batches complete (PARALLEL_COPY_TO_FILE: no order promised).
+    class Stage;
+    struct StageDeleter {
+        void operator()(Stage *st) const;
+    };
+    using StagePtr = std::unique_ptr<Stage, StageDeleter>;
+    StagePtr newStage();
+    bool writeChunk(Stage &stage, DataChunk &chunk);
+    bool mergeStage(Stage &stage);
+    // why the last writeChunk(stage, ...) / mergeStage(stage) returned false
+    const std::string &stageError(const Stage &stage) const;
 };
 
 }  // namespace ext_fastlane

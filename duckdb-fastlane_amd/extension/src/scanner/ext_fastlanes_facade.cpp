@@ -13,6 +13,7 @@
 #include <cstring>
 #include <future>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -82,14 +83,9 @@ public:
     std::string error;                               // why the last call returned false (lastError)
     std::vector<LogicalType> wtypes;
     std::vector<std::string> wnames;
-    std::vector<RawBuf> wcols;   // fixed-width buffered rows
-    // VARCHAR columns: the sink keeps DuckDB's 16-byte string_t records (one
-    // bulk copy per slice) and the bytes of the non-inlined strings, whose
-    // pointer field it rewrites to their offset in warena; the background
-    // task turns them into the writer's bytes + offsets, a thread per column
-    std::vector<RawBuf> wrec, warena;
-    std::vector<uint64_t> wbytes;  // string bytes per VARCHAR column in the batch
-    idx_t wrows = 0;
+    Stage *own = nullptr;  // the serial path's stage (writeChunk(chunk), merges, the last row group)
+    std::mutex hand;       // one batch hand-off at a time (flush_stage)
+    std::mutex merge;      // one mergeStage at a time (it fills `own`)
     idx_t rg_rows = 65536;
     // row groups per writer call (FLS_COPY_BATCH, default 8): one call encodes
     // every (row group, column) chunk in parallel, so a row group's slowest
@@ -119,13 +115,54 @@ public:
         have_rg = eof = false;
         rg_pos = 0;
     }
-    bool flush_rowgroup();
-    ~Impl() {
-        close_read();
-        wait_pending();
-        if (writer) fls_writer_free(writer);
-    }
+    bool flush_stage(Stage &st);
+    bool stage_chunk(Stage &st, DataChunk &chunk, bool profile);
+    bool stage_full(const Stage &st) const;
+    void reset_stage(Stage &st) const;
+    ~Impl();
 };
+
+// Rows buffered by one sink thread for the next batch of row groups.
+class FastLanesFacade::Stage {
+public:
+    std::vector<RawBuf> wcols;  // fixed-width buffered rows
+    // VARCHAR columns: the sink keeps DuckDB's 16-byte string_t records (one
+    // bulk copy per slice) and the bytes of the non-inlined strings, whose
+    // pointer field it rewrites to their offset in warena; the background
+    // task turns them into the writer's bytes + offsets, a thread per column
+    std::vector<RawBuf> wrec, warena;
+    std::vector<uint64_t> wbytes;  // string bytes per VARCHAR column in the batch
+    idx_t wrows = 0;
+    std::string error;
+};
+
+void FastLanesFacade::StageDeleter::operator()(Stage *st) const { delete st; }
+
+FastLanesFacade::Impl::~Impl() {
+    close_read();
+    wait_pending();
+    if (writer) fls_writer_free(writer);
+    delete own;
+}
+
+void FastLanesFacade::Impl::reset_stage(Stage &st) const {
+    for (auto *b : {&st.wcols, &st.wrec, &st.warena}) {
+        b->resize(wtypes.size());
+        for (auto &x : *b) x.clear();
+    }
+    st.wbytes.assign(wtypes.size(), 0);
+    st.wrows = 0;
+}
+
+// at a row-group boundary: a full batch, or a VARCHAR buffer nearing the
+// offsets' 32-bit range, goes to the writer
+bool FastLanesFacade::Impl::stage_full(const Stage &st) const {
+    if (st.wrows == 0 || st.wrows % rg_rows) return false;
+    bool big = false;
+    for (size_t c = 0; c < wtypes.size(); ++c)
+        big |= st.wbytes[c] > (1ull << 30);
+    return st.wrows == rg_rows * batch_rgs || big;
+}
 
 FastLanesFacade::FastLanesFacade() : pImpl(new Impl()) {}
 FastLanesFacade::~FastLanesFacade() = default;
@@ -239,35 +276,29 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.out_path = file_path;
     s.wtypes = types;
     s.wnames = names;
-    for (auto *b : {&s.wcols, &s.wrec, &s.warena}) {
-        b->clear();
-        b->resize(types.size());
-    }
-    s.wbytes.assign(types.size(), 0);
-    s.wrows = 0;
+    if (!s.own) s.own = new Stage();
+    s.reset_stage(*s.own);
     if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
     return true;
 }
 
-// Hand the buffered row group to the writer on a background thread (after
-// the previous one is done: row groups stay in order) and keep buffering into
-// the previous row group's buffers.
-bool FastLanesFacade::Impl::flush_rowgroup() {
-    if (wrows == 0) return true;
-    if (!wait_pending()) return false;
+// Hand a stage's buffered row groups to the writer on a background thread
+// (after the previous batch is done: batches reach the file in hand-off order)
+// and give the stage the previous batch's buffers to keep filling.
+bool FastLanesFacade::Impl::flush_stage(Stage &st) {
+    if (st.wrows == 0) return true;
+    std::lock_guard<std::mutex> guard(hand);
+    if (!wait_pending()) {
+        st.error = error;
+        return false;
+    }
     for (auto *b : {&pcols, &prec, &parena}) b->resize(wtypes.size());
     poffs.resize(wtypes.size());
-    std::swap(pcols, wcols);
-    std::swap(prec, wrec);
-    std::swap(parena, warena);
-    for (size_t c = 0; c < wtypes.size(); ++c) {
-        wcols[c].clear();
-        wrec[c].clear();
-        warena[c].clear();
-        wbytes[c] = 0;
-    }
-    const uint32_t rows = (uint32_t)wrows;
-    wrows = 0;
+    std::swap(pcols, st.wcols);
+    std::swap(prec, st.wrec);
+    std::swap(parena, st.warena);
+    const uint32_t rows = (uint32_t)st.wrows;
+    reset_stage(st);
     pending = std::async(std::launch::async, [this, rows]() {
         const double t0 = prof.on ? CopyProfile::now() : 0;
         // VARCHAR columns: string_t records -> bytes + offsets (a thread per column)
@@ -336,20 +367,23 @@ static idx_t PhysicalWidth(const LogicalType &t) {
     return TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
 }
 
-bool FastLanesFacade::writeChunk(DataChunk &chunk) {
-    Impl &s = *pImpl;
-    const double t_in = s.prof.on ? CopyProfile::now() : 0;
+// Copy a DataChunk into a stage; a full batch goes to the writer.  profile:
+// account the time in prof (the serial path only: prof is not thread-safe).
+bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk, bool profile) {
+    Impl &s = *this;
+    const double t_in = profile ? CopyProfile::now() : 0;
     struct Tally {  // sink time of this call, less its waits for the writer
         Impl &s;
+        bool on;
         double t_in, w_in;
         ~Tally() {
-            if (s.prof.on) s.prof.sink += CopyProfile::now() - t_in - (s.prof.wait - w_in);
+            if (on) s.prof.sink += CopyProfile::now() - t_in - (s.prof.wait - w_in);
         }
-    } tally{s, t_in, s.prof.wait};
+    } tally{s, profile, t_in, s.prof.wait};
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
     double tp = t_in;
     auto lap = [&](double &acc) {  // profile: time since the last lap into acc
-        if (!s.prof.on) return;
+        if (!profile) return;
         const double t = CopyProfile::now();
         acc += t - tp;
         tp = t;
@@ -360,7 +394,7 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     // writing a value (nothing of this chunk is appended).
     for (size_t c = 0; c < s.wtypes.size(); ++c)
         if (!FlatVector::Validity(chunk.data[c]).CheckAllValid(chunk.size())) {
-            s.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
+            st.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
             return false;
         }
     lap(s.prof.prep);
@@ -369,16 +403,16 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     idx_t r0 = 0;
     while (r0 < chunk.size()) {
         // (a slice is at most one vector: the VARCHAR path's position list)
-        const idx_t n = std::min<idx_t>({chunk.size() - r0, s.rg_rows - s.wrows % s.rg_rows, STANDARD_VECTOR_SIZE});
+        const idx_t n = std::min<idx_t>({chunk.size() - r0, s.rg_rows - st.wrows % s.rg_rows, STANDARD_VECTOR_SIZE});
         for (size_t c = 0; c < s.wtypes.size(); ++c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
-            RawBuf &col = s.wcols[c];
+            RawBuf &col = st.wcols[c];
             if (t.id() == LogicalTypeId::VARCHAR) {
                 // the records in one copy; the non-inlined strings' bytes to
                 // the arena, their pointer field := arena offset
                 const string_t *str = FlatVector::GetData<string_t>(v) + r0;
-                uint8_t *rec = s.wrec[c].grow(n * sizeof(string_t));
+                uint8_t *rec = st.wrec[c].grow(n * sizeof(string_t));
                 memcpy(rec, str, n * sizeof(string_t));
                 // lengths and the positions of the non-inlined strings without
                 // a data-dependent branch (inlined and pointer strings alternate
@@ -392,18 +426,18 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
                     longs[nl] = (uint32_t)r;
                     nl += len > string_t::INLINE_LENGTH ? 1u : 0u;
                 }
-                RawBuf &ar = s.warena[c];
+                RawBuf &ar = st.warena[c];
                 for (uint32_t i = 0; i < nl; ++i) {
                     const uint32_t r = longs[i], len = str[r].GetSize();
                     const uint64_t off = ar.size();
                     memcpy(ar.grow(len), str[r].GetData(), len);
                     memcpy(rec + sizeof(string_t) * r + 8, &off, 8);
                 }
-                if (s.wbytes[c] + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
-                    s.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
+                if (st.wbytes[c] + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
+                    st.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
                     return false;
                 }
-                s.wbytes[c] += bytes;
+                st.wbytes[c] += bytes;
                 lap(s.prof.str);
                 continue;
             }
@@ -422,23 +456,85 @@ bool FastLanesFacade::writeChunk(DataChunk &chunk) {
             }
             lap(s.prof.fixed);
         }
-        s.wrows += n;
+        st.wrows += n;
         r0 += n;
-        // at a row-group boundary: hand the batch over when it is full, or
-        // early when a VARCHAR buffer nears the offsets' 32-bit range
-        if (s.wrows % s.rg_rows == 0) {
-            bool big = false;
-            for (size_t c = 0; c < s.wtypes.size(); ++c)
-                big |= s.wbytes[c] > (1ull << 30);
-            if ((s.wrows == s.rg_rows * s.batch_rgs || big) && !s.flush_rowgroup()) return false;
+        if (s.stage_full(st) && !s.flush_stage(st)) return false;
+    }
+    return true;
+}
+
+bool FastLanesFacade::writeChunk(DataChunk &chunk) {
+    Impl &s = *pImpl;
+    if (!s.own) return false;
+    const bool ok = s.stage_chunk(*s.own, chunk, s.prof.on);
+    if (!ok) s.error = s.own->error;
+    return ok;
+}
+
+FastLanesFacade::StagePtr FastLanesFacade::newStage() {
+    Impl &s = *pImpl;
+    StagePtr st(new Stage());
+    s.reset_stage(*st);
+    return st;
+}
+
+bool FastLanesFacade::writeChunk(Stage &stage, DataChunk &chunk) { return pImpl->stage_chunk(stage, chunk, false); }
+
+const std::string &FastLanesFacade::stageError(const Stage &stage) const { return stage.error; }
+
+// Append a stage's rows to `own` a row-group slice at a time (`own` may end a
+// batch mid-merge and hand it over), the non-inlined strings' bytes re-based
+// into own's arena.
+bool FastLanesFacade::mergeStage(Stage &st) {
+    Impl &s = *pImpl;
+    if (!s.writer || !s.own) return false;
+    std::lock_guard<std::mutex> guard(s.merge);
+    Stage &o = *s.own;
+    const size_t nc = s.wtypes.size();
+    idx_t r0 = 0;
+    while (r0 < st.wrows) {
+        const idx_t n = std::min<idx_t>(st.wrows - r0, s.rg_rows - o.wrows % s.rg_rows);
+        for (size_t c = 0; c < nc; ++c) {
+            if (s.wtypes[c].id() == LogicalTypeId::VARCHAR) {
+                const uint8_t *src = st.wrec[c].data() + sizeof(string_t) * r0;
+                uint8_t *rec = o.wrec[c].grow(n * sizeof(string_t));
+                memcpy(rec, src, n * sizeof(string_t));
+                uint64_t bytes = 0;
+                for (idx_t r = 0; r < n; ++r) {
+                    uint32_t len;
+                    memcpy(&len, rec + sizeof(string_t) * r, 4);
+                    bytes += len;
+                    if (len <= string_t::INLINE_LENGTH) continue;
+                    uint64_t off;
+                    memcpy(&off, rec + sizeof(string_t) * r + 8, 8);
+                    const uint64_t at = o.warena[c].size();
+                    memcpy(o.warena[c].grow(len), st.warena[c].data() + off, len);
+                    memcpy(rec + sizeof(string_t) * r + 8, &at, 8);
+                }
+                if (o.wbytes[c] + bytes > UINT32_MAX) {
+                    st.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
+                    return false;
+                }
+                o.wbytes[c] += bytes;
+            } else {
+                const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(s.wtypes[c]));
+                memcpy(o.wcols[c].grow(n * w), st.wcols[c].data() + r0 * w, n * w);
+            }
+        }
+        o.wrows += n;
+        r0 += n;
+        if (s.stage_full(o) && !s.flush_stage(o)) {
+            st.error = o.error;
+            return false;
         }
     }
+    s.reset_stage(st);
     return true;
 }
 
 bool FastLanesFacade::setRowGroupSize(idx_t rows) {
     Impl &s = *pImpl;
-    if (!s.writer || s.wrows != 0 || fls_writer_set_rowgroup_size(s.writer, (uint32_t)rows) != 0) return false;
+    if (!s.writer || !s.own || s.own->wrows != 0 || fls_writer_set_rowgroup_size(s.writer, (uint32_t)rows) != 0) return false;
     s.rg_rows = rows;
     return true;
 }
@@ -446,7 +542,8 @@ bool FastLanesFacade::setRowGroupSize(idx_t rows) {
 bool FastLanesFacade::finalizeFile() {
     Impl &s = *pImpl;
     if (!s.writer) return false;
-    bool ok = s.flush_rowgroup();
+    bool ok = s.own && s.flush_stage(*s.own);
+    if (!ok && s.own) s.error = s.own->error;
     ok = s.wait_pending() && ok;
     const double t0 = s.prof.on ? CopyProfile::now() : 0;
     if (ok && fls_writer_finish_file(s.writer, s.out_path.c_str()) != 0) {

@@ -10,8 +10,6 @@
 // DuckDB's rotate_files hooks) and is rejected at bind time.
 #include "writer/copy_fastlanes.hpp"
 
-#include <mutex>
-
 #include "duckdb/common/string_util.hpp"
 #include "duckdb/main/extension_util.hpp"
 #include "fastlanes_facade.hpp"
@@ -31,11 +29,15 @@ struct FastlaneCopyBindData : public TableFunctionData {
 
 struct FastlaneCopyGlobalState : public GlobalFunctionData {
     std::unique_ptr<FastLanesFacade> facade;
-    std::mutex lock;  // sinks may run on several threads; the writer is not thread-safe
     string file_path;
 };
 
-struct FastlaneCopyLocalState : public LocalFunctionData {};
+// Each sink thread copies its chunks into its own facade stage (created at the
+// first sink: init_local does not see the global state); full batches of row
+// groups go to the writer from the stage, the rest is merged at combine.
+struct FastlaneCopyLocalState : public LocalFunctionData {
+    FastLanesFacade::StagePtr stage;
+};
 
 idx_t ValidRowGroupSize(uint64_t rows) {
     if (rows == 0 || rows > 65536 || rows % 1024)
@@ -85,22 +87,32 @@ unique_ptr<LocalFunctionData> CopyInitLocal(ExecutionContext &, FunctionData &) 
     return make_uniq<FastlaneCopyLocalState>();
 }
 
-void CopySink(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, LocalFunctionData &, DataChunk &input) {
+void CopySink(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, LocalFunctionData &lstate,
+              DataChunk &input) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
-    std::lock_guard<std::mutex> guard(g.lock);
-    if (!g.facade->writeChunk(input)) {
-        const std::string &why = g.facade->lastError();
+    auto &l = lstate.Cast<FastlaneCopyLocalState>();
+    if (!l.stage) l.stage = g.facade->newStage();
+    if (!g.facade->writeChunk(*l.stage, input)) {
+        const std::string &why = g.facade->stageError(*l.stage);
         throw IOException("Failed to write chunk to FastLanes" + (why.empty() ? std::string() : ": " + why));
     }
 }
 
-void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &, LocalFunctionData &) {}
+void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, LocalFunctionData &lstate) {
+    auto &g = gstate.Cast<FastlaneCopyGlobalState>();
+    auto &l = lstate.Cast<FastlaneCopyLocalState>();
+    if (l.stage && !g.facade->mergeStage(*l.stage)) {
+        const std::string &why = g.facade->stageError(*l.stage);
+        throw IOException("Failed to write chunk to FastLanes" + (why.empty() ? std::string() : ": " + why));
+    }
+}
 
 // The reference's mode callback (src/writer/write_fastlane_stream.cpp:251-260)
 // answers PARALLEL without insertion order and BATCH for a batch-index source,
 // but registers no prepare_batch / flush_batch, which DuckDB's batch copy
 // calls; here an ordered COPY keeps the single (REGULAR) sink, and an
-// unordered one runs sinks on every thread, serialised by the global lock.
+// unordered one runs sinks on every thread, each into its own stage (only the
+// hand-off of full batches to the writer is serialised).
 CopyFunctionExecutionMode CopyExecutionMode(bool preserve_insertion_order, bool /*supports_batch_index*/) {
     return preserve_insertion_order ? CopyFunctionExecutionMode::REGULAR_COPY_TO_FILE
                                     : CopyFunctionExecutionMode::PARALLEL_COPY_TO_FILE;
@@ -113,7 +125,6 @@ idx_t CopyDesiredBatchSize(ClientContext &, FunctionData &bind_p) {
 
 void CopyFinalize(ClientContext &, FunctionData &, GlobalFunctionData &gstate) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
-    std::lock_guard<std::mutex> guard(g.lock);
     if (!g.facade->finalizeFile()) {
         const std::string &why = g.facade->lastError();
         throw IOException("Failed to finalize FastLanes file: " + g.file_path + (why.empty() ? std::string() : ": " + why));

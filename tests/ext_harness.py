@@ -155,13 +155,15 @@ class Ext:
             raise ExtError(lib.fls_ext_last_error().decode())
         return rows.value
 
-    def copy_values(self, columns, dst, fmt="fls"):
-        """COPY (SELECT * FROM (VALUES ...)) TO dst (FORMAT fmt): columns =
-        [(name, "INTEGER" | "BIGINT" | "DOUBLE" | "VARCHAR", [values, None = NULL])]."""
+    def copy_values(self, columns, dst, fmt="fls", threads=1, **opts):
+        """COPY (SELECT * FROM (VALUES ...)) TO dst (FORMAT fmt, opts): columns =
+        [(name, "INTEGER" | "BIGINT" | "DOUBLE" | "VARCHAR", [values, None = NULL])].
+        threads > 1: a parallel (unordered) COPY, chunk k sunk by thread k % threads."""
         lib = self.lib
-        lib.fls_ext_copy_values.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p),
-                                            C.POINTER(C.c_char_p), C.c_int64, C.POINTER(C.c_char_p),
-                                            C.POINTER(C.c_uint64)]
+        lib.fls_ext_copy_values_mt.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p),
+                                               C.POINTER(C.c_char_p), C.c_int64, C.POINTER(C.c_char_p),
+                                               C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                               C.POINTER(C.c_uint64)]
         nc = len(columns)
         nr = len(columns[0][2]) if columns else 0
         names = (C.c_char_p * nc)(*[c[0].encode() for c in columns])
@@ -171,9 +173,11 @@ class Ext:
             for j, c in enumerate(columns):
                 v = c[2][r]
                 cells[r * nc + j] = None if v is None else str(v).encode()
+        keys = (C.c_char_p * max(1, len(opts)))(*[k.encode() for k in opts])
+        vals = (C.c_char_p * max(1, len(opts)))(*[str(v).encode() for v in opts.values()])
         rows = C.c_uint64()
-        rc = lib.fls_ext_copy_values(self.db, fmt.encode(), str(dst).encode(), nc, names, types, nr, cells,
-                                     C.byref(rows))
+        rc = lib.fls_ext_copy_values_mt(self.db, fmt.encode(), str(dst).encode(), nc, names, types, nr, cells,
+                                        keys, vals, len(opts), threads, C.byref(rows))
         if rc != 0:
             raise ExtError(lib.fls_ext_last_error().decode())
         return rows.value

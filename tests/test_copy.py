@@ -150,3 +150,38 @@ def test_copy_execution_mode_and_batch_size(ext, fmt):
     assert ext.copy_mode(fmt, preserve=True, batch_index=False)[0] == 0
     assert ext.copy_mode(fmt, preserve=True, batch_index=True)[0] == 0
     assert ext.copy_mode(fmt, True, True, {"ROW_GROUP_SIZE": 8192}) == (0, 8192)
+
+
+@pytest.mark.parametrize("threads,batch", [(1, "8"), (4, "8"), (4, "1"), (3, "3")])
+def test_copy_parallel_sinks_cpu(ext, ref, tmpfile, monkeypatch, threads, batch):
+    """An unordered COPY (PARALLEL_COPY_TO_FILE) runs a sink per thread, each
+    into its own stage; full batches of row groups go to the writer from the
+    stages and the remainders merge at combine.  The file holds every source
+    row exactly once (order unpromised, so compared as a multiset of (a, s)
+    pairs), every row group but the last is full, and with one thread the
+    row order is the input's."""
+    monkeypatch.setenv("FLS_COPY_BATCH", batch)
+    rg = 1024
+    n = 37 * rg + 517
+    a = [(i * 7919) % 100003 - 50000 for i in range(n)]
+    s = [f"p{i % 7}" * (i % 11) for i in range(n)]  # inlined and pointer string_t
+    dst = tmpfile(f"par{threads}_{batch}.fls")
+    assert ext.copy_values([("a", "INTEGER", a), ("s", "VARCHAR", s)], dst, threads=threads,
+                           row_group_size=rg) == n
+    rf = ref.RefFile(open(dst, "rb").read())
+    assert rf.nrows == n and rf.f.rowgroup_size == rg and rf.nrowgroups == -(-n // rg)
+    assert all(rf.rowgroup_rows(g) == rg for g in range(rf.nrowgroups - 1))
+    got_a = np.concatenate([rf.decode(0, g) for g in range(rf.nrowgroups)]).view(np.int32).tolist()
+    got_s = rf.strings_column(1)
+    if threads == 1:
+        assert got_a == a and got_s == [x.encode() for x in s]
+    assert sorted(zip(got_a, got_s)) == sorted(zip(a, (x.encode() for x in s)))
+
+
+def test_copy_parallel_sinks_refuse_nulls_cpu(ext, tmpfile):
+    """A NULL met by any sink thread fails the whole parallel COPY."""
+    n = 5 * 2048
+    vals = list(range(n))
+    vals[3 * 2048 + 5] = None
+    with pytest.raises(ExtError, match='column "a" holds NULL values'):
+        ext.copy_values([("a", "BIGINT", vals)], tmpfile("parnull.fls"), threads=4)
