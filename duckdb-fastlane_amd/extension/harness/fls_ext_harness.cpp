@@ -652,9 +652,22 @@ extern "C" int fls_ext_scan_count(fls_ext_db *d, const char *fn, const char *pat
 // bind -> init_global -> init_local -> sink per chunk -> combine -> finalize,
 // the order DuckDB's PhysicalCopyToFile drives a CopyFunction.  Option values
 // are passed as VARCHAR (DuckDB hands the parsed constants; the bind parses).
+int fls_ext_copy_mt(fls_ext_db *d, const char *fn, const char *src, const int *proj, int nproj, const char *format,
+                    const char *dst, const char *const *opt_keys, const char *const *opt_vals, int nopts,
+                    int nthreads, uint64_t *rows);
+
 int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj, int nproj, const char *format,
                  const char *dst, const char *const *opt_keys, const char *const *opt_vals, int nopts,
                  uint64_t *rows) {
+    return fls_ext_copy_mt(d, fn, src, proj, nproj, format, dst, opt_keys, opt_vals, nopts, 1, rows);
+}
+
+// nthreads > 1: an unordered COPY, the scan on up to nthreads threads (the
+// parallel source) and each thread sinking into its own local state, as
+// DuckDB's pipeline runs PhysicalCopyToFile with PARALLEL_COPY_TO_FILE.
+int fls_ext_copy_mt(fls_ext_db *d, const char *fn, const char *src, const int *proj, int nproj, const char *format,
+                    const char *dst, const char *const *opt_keys, const char *const *opt_vals, int nopts,
+                    int nthreads, uint64_t *rows) {
     try {
         const std::string fmt = StringUtil::Lower(format ? format : "");
         auto it = d->db.copy_functions.find(fmt);
@@ -691,30 +704,52 @@ int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj
         auto bind = cf.copy_to_bind(d->ctx, cbin, vector<string>(names.begin(), names.end()),
                                     vector<LogicalType>(types.begin(), types.end()));
         auto gstate = cf.copy_to_initialize_global(d->ctx, *bind, dst ? dst : "");
+        if (nthreads < 1) nthreads = 1;
+        if (nthreads > 1 && (!cf.execution_mode ||
+                             cf.execution_mode(false, false) != CopyFunctionExecutionMode::PARALLEL_COPY_TO_FILE))
+            throw NotImplementedException("harness: " + fmt + " has no parallel COPY sink");
         ExecutionContext ectx(d->ctx);
-        auto lstate = cf.copy_to_initialize_local(ectx, *bind);
-        DataChunk out;
-        out.Initialize(vector<LogicalType>(types.begin(), types.end()));
-        uint64_t n = 0;
+        // one local state (and projection chunk) per sink thread
+        struct Local {
+            unique_ptr<LocalFunctionData> state;
+            DataChunk out;
+        };
+        std::mutex lmu;
+        std::map<std::thread::id, std::unique_ptr<Local>> locals;
+        auto local = [&]() -> Local & {
+            std::lock_guard<std::mutex> g(lmu);
+            auto &l = locals[std::this_thread::get_id()];
+            if (!l) {
+                l = std::make_unique<Local>();
+                l->state = cf.copy_to_initialize_local(ectx, *bind);
+                l->out.Initialize(vector<LogicalType>(types.begin(), types.end()));
+            }
+            return *l;
+        };
+        std::atomic<uint64_t> n{0};
         std::vector<std::string> n2;
         std::vector<LogicalType> t2;
         execute(d, q, pv, -1, n2, t2, [&](idx_t, DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
+            Local &l = local();
             bool identity = pick.size() == c.ColumnCount() && cnt == c.size();
             for (size_t k = 0; identity && k < pick.size(); ++k) identity = pick[k] == k;
             if (identity) {
-                cf.copy_to_sink(ectx, *bind, *gstate, *lstate, c);
+                cf.copy_to_sink(ectx, *bind, *gstate, *l.state, c);
             } else {
+                DataChunk &out = l.out;
                 out.Reset();
                 for (size_t k = 0; k < pick.size(); ++k)
                     for (idx_t i = 0; i < cnt; ++i) out.data[k].SetValue(i, c.data[pick[k]].GetValue(i));
                 out.SetCardinality(cnt);
-                cf.copy_to_sink(ectx, *bind, *gstate, *lstate, out);
+                cf.copy_to_sink(ectx, *bind, *gstate, *l.state, out);
             }
             n += cnt;
-        });
-        if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
+        }, nthreads);
+        if (locals.empty()) local();  // an empty source still has one sink
+        for (auto &kv : locals)
+            if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *kv.second->state);
         cf.copy_to_finalize(d->ctx, *bind, *gstate);
-        if (rows) *rows = n;
+        if (rows) *rows = n.load();
         return 0;
     } catch (const std::exception &e) {
         g_err = e.what();

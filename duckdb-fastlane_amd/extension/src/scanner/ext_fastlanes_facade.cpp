@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <future>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -86,6 +87,7 @@ public:
     Stage *own = nullptr;  // the serial path's stage (writeChunk(chunk), merges, the last row group)
     std::mutex hand;       // one batch hand-off at a time (flush_stage)
     std::mutex merge;      // one mergeStage at a time (it fills `own`)
+    std::atomic<int> nstages{0};  // stages handed out (FLS_COPY_PROFILE times a lone sink only)
     idx_t rg_rows = 65536;
     // row groups per writer call (FLS_COPY_BATCH, default 8): one call encodes
     // every (row group, column) chunk in parallel, so a row group's slowest
@@ -475,10 +477,14 @@ FastLanesFacade::StagePtr FastLanesFacade::newStage() {
     Impl &s = *pImpl;
     StagePtr st(new Stage());
     s.reset_stage(*st);
+    s.nstages.fetch_add(1);
     return st;
 }
 
-bool FastLanesFacade::writeChunk(Stage &stage, DataChunk &chunk) { return pImpl->stage_chunk(stage, chunk, false); }
+bool FastLanesFacade::writeChunk(Stage &stage, DataChunk &chunk) {
+    Impl &s = *pImpl;
+    return s.stage_chunk(stage, chunk, s.prof.on && s.nstages.load() == 1);
+}
 
 const std::string &FastLanesFacade::stageError(const Stage &stage) const { return stage.error; }
 

@@ -131,11 +131,13 @@ def main():
         with tempfile.TemporaryDirectory() as d:
             src, dst = os.path.join(d, "src.fls"), os.path.join(d, "dst.fls")
             img.write(src)
-            t0 = time.perf_counter()
-            rows = e.copy("read_fastlanes", src, dst, fmt="fls")
-            dt = time.perf_counter() - t0
-            print(f"COPY (SELECT * FROM read_fastlanes) TO (FORMAT fls): {rows} rows in {dt:.2f} s = "
-                  f"{rows / dt / 1e6:.2f} M rows/s", flush=True)
+            for th in sorted({1, a.threads}):
+                t0 = time.perf_counter()
+                rows = e.copy("read_fastlanes", src, dst, fmt="fls", threads=th)
+                dt = time.perf_counter() - t0
+                what = "ordered, one sink" if th == 1 else f"unordered, {th} sink threads"
+                print(f"COPY (SELECT * FROM read_fastlanes) TO (FORMAT fls), {what}: {rows} rows in {dt:.2f} s = "
+                      f"{rows / dt / 1e6:.2f} M rows/s", flush=True)
         e.close()
 
 

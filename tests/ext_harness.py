@@ -137,20 +137,21 @@ class Ext:
         self.lib.fls_ext_has_copy_function.argtypes = [C.c_void_p, C.c_char_p]
         return bool(self.lib.fls_ext_has_copy_function(self.db, name.encode()))
 
-    def copy(self, fn, src, dst, fmt="fls", proj=None, **options):
+    def copy(self, fn, src, dst, fmt="fls", proj=None, threads=1, **options):
         """COPY (SELECT <proj> FROM fn(src)) TO dst (FORMAT fmt, key value ...);
-        returns the number of rows copied."""
+        returns the number of rows copied.  threads > 1: an unordered COPY with
+        a parallel scan and a sink per thread (PARALLEL_COPY_TO_FILE)."""
         lib = self.lib
-        lib.fls_ext_copy.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.c_int, C.c_char_p,
-                                     C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int,
-                                     C.POINTER(C.c_uint64)]
+        lib.fls_ext_copy_mt.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.c_int, C.c_char_p,
+                                        C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                        C.POINTER(C.c_uint64)]
         keys = list(options)
         k = (C.c_char_p * max(1, len(keys)))(*[x.encode() for x in keys])
         v = (C.c_char_p * max(1, len(keys)))(*[str(options[x]).encode() for x in keys])
         p = (C.c_int * len(proj))(*proj) if proj else None
         rows = C.c_uint64()
-        rc = lib.fls_ext_copy(self.db, fn.encode(), str(src).encode(), p, len(proj) if proj else 0, fmt.encode(),
-                              str(dst).encode(), k, v, len(keys), C.byref(rows))
+        rc = lib.fls_ext_copy_mt(self.db, fn.encode(), str(src).encode(), p, len(proj) if proj else 0,
+                                 fmt.encode(), str(dst).encode(), k, v, len(keys), threads, C.byref(rows))
         if rc != 0:
             raise ExtError(lib.fls_ext_last_error().decode())
         return rows.value

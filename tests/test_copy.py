@@ -185,3 +185,26 @@ def test_copy_parallel_sinks_refuse_nulls_cpu(ext, tmpfile):
     vals[3 * 2048 + 5] = None
     with pytest.raises(ExtError, match='column "a" holds NULL values'):
         ext.copy_values([("a", "BIGINT", vals)], tmpfile("parnull.fls"), threads=4)
+
+
+@pytest.mark.gpu
+def test_copy_parallel_from_scan(fl, ext, ref, gpu, li_file, tmpfile):
+    """COPY (SELECT * FROM read_fastlanes(src)) TO dst with a parallel scan and
+    four sink threads: every row once (multiset of (l_orderkey, l_partkey,
+    l_shipmode code) triples vs the generator), only the last row group short."""
+    dst = tmpfile("par.fls")
+    n = ext.copy("read_fastlanes", li_file, dst, threads=4, row_group_size=4096)
+    assert n == 60175
+    f = ref.RefFile(open(dst, "rb").read())
+    assert f.nrows == n and f.nrowgroups == -(-n // 4096)
+    assert all(f.rowgroup_rows(g) == 4096 for g in range(f.nrowgroups - 1))
+    k0 = f.decode_column(0, 4).view(np.int64)
+    k1 = f.decode_column(1, 4).view(np.int32)
+    s14 = f.strings(f.decode_column(14, 4))
+    e0 = fl.gen_values("lineitem", 0, 0, n, np.int64, 0.01)
+    e1 = fl.gen_values("lineitem", 1, 0, n, np.int32, 0.01)
+    codes = fl.gen_values("lineitem", 14, 0, n, np.uint32, 0.01)
+    modes = {int(c): fl.gen_dict_string("lineitem", 14, int(c)).encode() for c in np.unique(codes)}
+    got = sorted(zip(k0.tolist(), k1.tolist(), s14))
+    want = sorted(zip(e0.tolist(), e1.tolist(), (modes[int(c)] for c in codes)))
+    assert got == want
