@@ -13,7 +13,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke rc=$rc: $(tail -1 gpurun_out/smoke_$TAG.log)"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python3 bench.py --steps 20 --cpu-seconds 0 --verify-rowgroups 0 --no-traffic > gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python3 bench.py --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-verify --no-traffic > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec head -3 {} \; ; [ $rc -eq 0 ] || exit $rc
 [ -n "$QUICK" ] && exit 0
 for wl in c3 c4 lineitem_full lineitem_dbl; do
