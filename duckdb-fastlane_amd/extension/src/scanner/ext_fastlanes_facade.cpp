@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <future>
 #include <atomic>
 #include <memory>
@@ -93,21 +94,36 @@ public:
     // every (row group, column) chunk in parallel, so a row group's slowest
     // column does not idle the writer's other threads
     idx_t batch_rgs = 8;
-    // the row group being encoded in the background (its buffers) and the
-    // writer call's result
-    std::vector<RawBuf> pcols, prec, parena;
-    std::vector<std::vector<uint32_t>> poffs;
-    std::future<std::string> pending;  // "" or the writer's error (fls_last_error is per thread)
+    // Batches handed to the writer: each is a background task that assembles
+    // its VARCHAR columns, waits for the previous batch's writer call (the
+    // writer appends row groups in call order) and then calls the writer.  Up
+    // to kMaxInflight batches are queued, so a sink that fills a stage while
+    // the writer is busy keeps going instead of waiting; their buffers are
+    // recycled through `spare`.
+    struct Batch {
+        std::vector<RawBuf> cols, rec, arena;
+        std::vector<std::vector<uint32_t>> offs;
+    };
+    static constexpr size_t kMaxInflight = 3;
+    std::deque<std::shared_future<std::string>> inflight;  // "" or the writer's error (fls_last_error is per thread)
+    std::vector<std::unique_ptr<Batch>> spare;
+    std::mutex spare_mu;
     CopyProfile prof;
-    double encode_s = 0;  // background writer calls (written by the writer thread, read after get())
-    // wait for the background row group; false if its encode failed
-    bool wait_pending() {
-        if (!pending.valid()) return true;
-        const double t0 = prof.on ? CopyProfile::now() : 0;
-        const std::string e = pending.get();
-        if (prof.on) prof.wait += CopyProfile::now() - t0;
-        if (!e.empty()) error = "FastLanes writer: " + e;
-        return e.empty();
+    double encode_s = 0;  // background writer calls (one at a time: the tasks are chained)
+    // wait until at most `keep` batches are in flight; false if one failed
+    bool wait_pending(size_t keep = 0) {
+        bool ok = true;
+        while (inflight.size() > keep) {
+            const double t0 = prof.on ? CopyProfile::now() : 0;
+            const std::string e = inflight.front().get();
+            inflight.pop_front();
+            if (prof.on) prof.wait += CopyProfile::now() - t0;
+            if (!e.empty()) {
+                error = "FastLanes writer: " + e;
+                ok = false;
+            }
+        }
+        return ok;
     }
 
     void close_read() {
@@ -284,29 +300,44 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     return true;
 }
 
-// Hand a stage's buffered row groups to the writer on a background thread
-// (after the previous batch is done: batches reach the file in hand-off order)
-// and give the stage the previous batch's buffers to keep filling.
+// Hand a stage's buffered row groups to the writer as a background task
+// (queued behind at most kMaxInflight - 1 others; the writer calls run in
+// hand-off order) and give the stage a recycled batch's buffers to keep filling.
 bool FastLanesFacade::Impl::flush_stage(Stage &st) {
     if (st.wrows == 0) return true;
     std::lock_guard<std::mutex> guard(hand);
-    if (!wait_pending()) {
+    if (!wait_pending(kMaxInflight - 1)) {
         st.error = error;
         return false;
     }
-    for (auto *b : {&pcols, &prec, &parena}) b->resize(wtypes.size());
-    poffs.resize(wtypes.size());
-    std::swap(pcols, st.wcols);
-    std::swap(prec, st.wrec);
-    std::swap(parena, st.warena);
+    std::unique_ptr<Batch> bp;
+    {
+        std::lock_guard<std::mutex> g(spare_mu);
+        if (!spare.empty()) {
+            bp = std::move(spare.back());
+            spare.pop_back();
+        }
+    }
+    if (!bp) bp.reset(new Batch());
+    Batch *b = bp.release();
+    for (auto *x : {&b->cols, &b->rec, &b->arena}) x->resize(wtypes.size());
+    b->offs.resize(wtypes.size());
+    std::swap(b->cols, st.wcols);
+    std::swap(b->rec, st.wrec);
+    std::swap(b->arena, st.warena);
     const uint32_t rows = (uint32_t)st.wrows;
     reset_stage(st);
-    pending = std::async(std::launch::async, [this, rows]() {
-        const double t0 = prof.on ? CopyProfile::now() : 0;
+    std::shared_future<std::string> prev = inflight.empty() ? std::shared_future<std::string>() : inflight.back();
+    inflight.push_back(std::async(std::launch::async, [this, rows, b, prev]() {
+        std::unique_ptr<Batch> own_b(b);
+        auto recycle = [this, &own_b]() {
+            std::lock_guard<std::mutex> g(spare_mu);
+            spare.push_back(std::move(own_b));
+        };
         // VARCHAR columns: string_t records -> bytes + offsets (a thread per column)
-        auto assemble = [this, rows](size_t c) {
-            const uint8_t *rec = prec[c].data();
-            std::vector<uint32_t> &o = poffs[c];
+        auto assemble = [this, rows, b](size_t c) {
+            const uint8_t *rec = b->rec[c].data();
+            std::vector<uint32_t> &o = b->offs[c];
             o.resize((size_t)rows + 1);
             o[0] = 0;
             for (uint32_t r = 0; r < rows; ++r) {
@@ -314,7 +345,7 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
                 memcpy(&len, rec + 16ull * r, 4);
                 o[r + 1] = o[r] + len;
             }
-            RawBuf &col = pcols[c];
+            RawBuf &col = b->cols[c];
             col.clear();
             uint8_t *dst = col.grow((size_t)o[rows] + string_t::INLINE_LENGTH);
             col.shrink(string_t::INLINE_LENGTH);
@@ -326,7 +357,7 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
                 } else {
                     uint64_t off;
                     memcpy(&off, x + 8, 8);
-                    memcpy(dst, parena[c].data() + off, len);
+                    memcpy(dst, b->arena[c].data() + off, len);
                 }
                 dst += len;
             }
@@ -335,6 +366,15 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
         for (size_t c = 0; c < wtypes.size(); ++c)
             if (wtypes[c].id() == LogicalTypeId::VARCHAR) th.emplace_back(assemble, c);
         for (auto &t : th) t.join();
+        // the writer takes batches in hand-off order; a failed batch fails the rest
+        if (prev.valid()) {
+            const std::string e = prev.get();
+            if (!e.empty()) {
+                recycle();
+                return e;
+            }
+        }
+        const double t0 = prof.on ? CopyProfile::now() : 0;
         // row group k of the batch: fixed-width columns at row k * rg_rows,
         // VARCHAR columns through their offsets from k * rg_rows (offsets are
         // into the column's whole byte buffer)
@@ -348,18 +388,20 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
             nrows[k] = (uint32_t)std::min<idx_t>(rg_rows, rows - r0);
             for (size_t c = 0; c < nc; ++c) {
                 if (wtypes[c].id() == LogicalTypeId::VARCHAR) {
-                    data[k * nc + c] = pcols[c].empty() ? (const void *)"" : pcols[c].data();
-                    offs[k * nc + c] = poffs[c].data() + r0;
+                    data[k * nc + c] = b->cols[c].empty() ? (const void *)"" : b->cols[c].data();
+                    offs[k * nc + c] = b->offs[c].data() + r0;
                 } else {
                     const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(wtypes[c]));
-                    data[k * nc + c] = pcols[c].data() + r0 * w;
+                    data[k * nc + c] = b->cols[c].data() + r0 * w;
                 }
             }
         }
         const int rc = fls_writer_add_rowgroups(writer, nrg, nrows.data(), data.data(), offs.data());
+        std::string e = rc == 0 ? std::string() : std::string(fls_last_error());
         if (prof.on) encode_s += CopyProfile::now() - t0;
-        return rc == 0 ? std::string() : std::string(fls_last_error());
-    });
+        recycle();
+        return e;
+    }).share());
     return true;
 }
 
