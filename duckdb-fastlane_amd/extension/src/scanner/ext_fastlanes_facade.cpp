@@ -538,6 +538,19 @@ bool FastLanesFacade::mergeStage(Stage &st) {
     if (!s.writer || !s.own) return false;
     std::lock_guard<std::mutex> guard(s.merge);
     Stage &o = *s.own;
+    if (o.wrows == 0) {  // nothing to append to (the only sink of an ordered COPY): take the buffers
+        std::swap(o.wcols, st.wcols);
+        std::swap(o.wrec, st.wrec);
+        std::swap(o.warena, st.warena);
+        std::swap(o.wbytes, st.wbytes);
+        std::swap(o.wrows, st.wrows);
+        s.reset_stage(st);
+        if (s.stage_full(o) && !s.flush_stage(o)) {
+            st.error = o.error;
+            return false;
+        }
+        return true;
+    }
     const size_t nc = s.wtypes.size();
     idx_t r0 = 0;
     while (r0 < st.wrows) {
