@@ -8,8 +8,12 @@ input resident in HBM, decoded columns written to HBM): the fused
 decode_kernel plus, for l_comment, the FSST kernel overlapped with it.  The
 default workload is the full 16-column lineitem (l_comment FSST-compressed).
 Row groups are sharded contiguously over ranks with no data-path collective
-(SURVEY.md 8(e)); torch.distributed only brackets the timing (barrier, MAX of
-times, SUM of values) and reduces the per-rank verification.
+(SURVEY.md 8(e)); torch.distributed over gloo (CPU tensors) only brackets the
+timing (barrier, MAX of times, SUM of values) and gathers the per-rank
+verification -- the scan has no exchange step, so no RCCL communicator is
+created.  Rank r runs on GPU (local_rank mod visible GPUs): on a node with
+fewer GPUs than ranks several ranks share one GPU, and config.ranks_per_gpu
+says so (such a line rehearses the split; it is not a scaling point).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lineitem_full]
                     [--scale 100] [--cpu-seconds 10] [--e2e-scale 10]
@@ -65,6 +69,7 @@ def parse(argv=None):
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal on CPU: ranks, shards and the cross-rank reduction over gloo; "
                         "no GPU, no decode (tests/test_bench_launcher.py)")
+    p.add_argument("--dry-run-node-gpus", type=int, default=0, help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
 
@@ -328,15 +333,43 @@ def verify_full(fl, t, args) -> tuple[int, int]:
 # ---- cross-rank reduction -----------------------------------------------------
 # per-rank record: [seconds, values, achieved GB/s, kernel ms, algorithmic
 # bytes per launch, mismatching values, values checked, row groups]
-def gather_ranks(local: list[float], dist_on: bool, device: str) -> list[list[float]]:
+REC_FIELDS = ["seconds", "values", "achieved_gbs", "kernel_ms", "algo_bytes", "mismatches", "values_checked",
+              "rowgroups"]
+
+
+def gather_ranks(local: list[float], dist_on: bool) -> list[list[float]]:
+    """All ranks' records, over gloo (CPU tensors): the bench needs no GPU
+    collective, and gloo works whatever the rank -> GPU mapping is (RCCL
+    refuses two ranks on one device)."""
     if not dist_on:
         return [list(local)]
     import torch
     import torch.distributed as dist
-    x = torch.tensor(local, dtype=torch.float64, device=device)
+    x = torch.tensor(local, dtype=torch.float64)
     allx = [torch.zeros_like(x) for _ in range(dist.get_world_size())]
     dist.all_gather(allx, x)
     return [a.tolist() for a in allx]
+
+
+def gather_objects(obj, dist_on: bool) -> list:
+    if not dist_on:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def rank_device(local_rank: int, ngpus: int) -> int:
+    """The GPU of a rank: its local rank, wrapped over the visible GPUs (a
+    launcher that narrows visibility to one GPU per process gives ngpus=1)."""
+    return local_rank % ngpus if ngpus > 0 else 0
+
+
+def ranks_per_gpu(gpu_ids: list[str]) -> int:
+    """Most ranks sharing one physical GPU (ids = host + device UUID)."""
+    from collections import Counter
+    return max(Counter(gpu_ids).values()) if gpu_ids else 1
 
 
 def reduce_ranks(per_rank: list[list[float]]) -> dict:
@@ -367,11 +400,15 @@ def dry_run(args) -> None:
     rg0, rg1 = shard_range(nrg, rank, world)
     rows = min(nrows, rg1 * 65536) - rg0 * 65536
     local = [1.0 + 0.25 * rank, float(rows), 100.0 * (rank + 1), 1.0, 0.0, 0.0, float(rows), float(rg1 - rg0)]
-    per_rank = gather_ranks(local, world > 1, "cpu")
+    per_rank = gather_ranks(local, world > 1)
+    # the rank -> GPU mapping of a node with args.gpus visible devices, as a GPU run makes it
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ids = gather_objects(f"host:gpu{rank_device(local_rank, args.dry_run_node_gpus or world)}", world > 1)
     if rank == 0:
         red = reduce_ranks(per_rank)
         print(json.dumps({"dry_run": True, "n_gpus": world, "rowgroups": nrg, "rows": nrows,
                           "shards": [list(shard_range(nrg, r, world)) for r in range(world)],
+                          "gpu_ids": ids, "ranks_per_gpu": ranks_per_gpu(ids),
                           "reduced": red, "value": red["values"] / red["dt"]}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -403,12 +440,18 @@ def main(argv=None):
     import torch.distributed as dist
 
     dist_on = world > 1
-    # this rank's GPU: its local rank, unless the launcher already narrowed the
-    # visible devices to one per process
-    dev = local_rank if torch.cuda.device_count() > local_rank else 0
     if dist_on:
-        torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        dist.init_process_group("gloo")   # CPU bracket only: no data-path collective
+    # this rank's GPU: its local rank wrapped over the visible GPUs
+    dev = rank_device(local_rank, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    props = torch.cuda.get_device_properties(dev)
+    gpu_id = f"{socket.gethostname()}:{getattr(props, 'uuid', '')}:{getattr(props, 'pci_bus_id', dev)}"
+    gpu_ids = gather_objects(gpu_id, dist_on)
+    rpg = ranks_per_gpu(gpu_ids)
+    if rank == 0 and rpg > 1:
+        log(f"[launcher] {world} ranks on {len(set(gpu_ids))} GPU(s): {rpg} ranks share a GPU "
+            f"(a rehearsal of the {world}-way split, not a scaling point)")
 
     import pkgload
     fl = pkgload.load()
@@ -462,7 +505,7 @@ def main(argv=None):
 
     local = [dt, float(st.values * args.steps), achieved, avg_ms, float(algo), float(bad), float(checked),
              float(rg1 - rg0)]
-    per_rank = gather_ranks(local, dist_on, "cuda")
+    per_rank = gather_ranks(local, dist_on)
     red = reduce_ranks(per_rank)
     dt, total_vals, bad_total, checked_total = red["dt"], red["values"], red["mismatches"], red["checked"]
     mean_achieved = red["mean_achieved"]
@@ -482,6 +525,7 @@ def main(argv=None):
         cfg = {"workload": args.workload + (f" SF{args.scale:g}" if big else ""),
                "rows": nrows, "columns": t.ncols, "rowgroups": nrg,
                "rowgroups_per_gpu": red["rowgroups"], "parallelism": f"rowgroup-shard x{world}",
+               "ranks_per_gpu": rpg, "physical_gpus": len(set(gpu_ids)),
                "step": "one decode launch over all resident vectors of the shard (HBM -> HBM)",
                "compressed_bytes_rank0": img.len, "decoded_bytes_rank0": int(st.out_bytes),
                "verified_values_bit_exact": checked_total if (bad_total == 0 and checked_total > 0) else 0,
@@ -520,6 +564,10 @@ def main(argv=None):
                                               "out": int(st.out_bytes)},
                          "per_rank": [{"achieved_gbs": r[2], "kernel_ms": r[3], "algo_bytes": r[4]}
                                       for r in per_rank] if world > 1 else None},
+            "per_rank": [dict({"rank": i, "gpu": gpu_ids[i]}, **{k: (int(v) if k in ("values", "mismatches",
+                                                                                    "values_checked", "rowgroups")
+                                                                    else v) for k, v in zip(REC_FIELDS, r)})
+                         for i, r in enumerate(per_rank)] if world > 1 else None,
             "e2e": e2e,
             "cpu_baseline": cpu,
         }

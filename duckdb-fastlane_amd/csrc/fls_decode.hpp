@@ -99,6 +99,8 @@ struct FsstLaunch {
     bool reset_queue = true;      // zero it first (false: drain a queue another launch started)
     int waves_per_cu = 0;         // grid: 0 = as many as fit, else at most this many per CU
     int variant = kFsstDefault;   // code-parallel kernel variant (kFsst* bits; FLS_FSST_VARIANT)
+    bool seg = false;             // the chunks carry segment tables (DevChunk.vbits bit 1): segmented kernel
+    int seg_cap = 4096;           // its ring: decoded bytes per part of a round (4096 or 3072; FLS_FSST_SEG_CAP)
 };
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).

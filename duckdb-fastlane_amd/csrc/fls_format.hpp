@@ -108,6 +108,8 @@ inline uint64_t alp_aux_bytes(uint32_t exc, uint32_t vbits) { return ((2ull * ex
 //   own, codes concatenated; code 255 = next byte is a literal, never the
 //   last code of a string).  The compressed lengths let a decoder start every
 //   string independently (fls_fsst.hip's string-parallel path).
+//   ChunkHeader.reserved0 = kFsstSegCodes when every vector carries a segment
+//   table after its stream (below), else 0.
 constexpr uint32_t kFsstTableBytes = 256 * 8 + 256;
 constexpr uint32_t kFsstEscape = 255;
 struct FsstVecHeader {        // 16 B
@@ -119,6 +121,29 @@ struct FsstVecHeader {        // 16 B
 // compressed stream of a vector, relative to its FsstVecHeader
 inline uint64_t fsst_stream_off(const FsstVecHeader &h) { return sizeof(FsstVecHeader) + 128ull * h.clen_w; }
 static_assert(sizeof(FsstVecHeader) == 16, "FSST vector header is 16 B");
+
+// FSST segment table (round 3; present when ChunkHeader.reserved0 ==
+// kFsstSegCodes, readers that ignore it see the same stream).  The compressed
+// stream of a vector is cut into segments of kFsstSegCodes code bytes (the
+// last one shorter); per vector, 16-byte aligned after the stream:
+//   FsstSegHeader, then u8 seg[nseg], nseg = ceil(comp_len / kFsstSegCodes):
+//   the decoded bytes of segment k's codes and the escape state entering it,
+//   as dlen (state 0, dlen <= 128) or 129 + dlen (state 1: the segment starts
+//   with the literal byte of an escape, so dlen <= 1 + 15 * 8 = 121).
+// With it a GPU lane decodes its own segment at its own output offset with no
+// hand-off from the lanes before it (fls_fsst.hip, the segmented kernel).
+constexpr uint32_t kFsstSegCodes = 16;
+enum : uint32_t { FSST_SEG_HAS_ESCAPE = 1 };  // FsstSegHeader.flags: the stream holds an escape code
+struct FsstSegHeader {        // 16 B
+    uint32_t flags;
+    uint32_t nseg;
+    uint32_t reserved0, reserved1;
+};
+static_assert(sizeof(FsstSegHeader) == 16, "FSST segment header is 16 B");
+inline uint64_t fsst_seg_off(const FsstVecHeader &h) { return fsst_stream_off(h) + ((h.comp_len + 15ull) & ~15ull); }
+inline uint32_t fsst_nseg(uint32_t comp_len) { return (comp_len + kFsstSegCodes - 1) / kFsstSegCodes; }
+inline uint64_t fsst_seg_bytes(uint32_t comp_len) { return sizeof(FsstSegHeader) + ((fsst_nseg(comp_len) + 15ull) & ~15ull); }
+inline uint8_t fsst_seg_value(uint32_t dlen, uint32_t entry_state) { return (uint8_t)(entry_state ? 129 + dlen : dlen); }
 
 static_assert(sizeof(ChunkHeader) == 64, "chunk header is 64 B");
 static_assert(sizeof(VecMeta) == 32, "vector meta is 32 B");

@@ -59,7 +59,7 @@ using lu32 = FLS_LDS uint32_t;
 // u32 offsets doff[1025] -- then u64 symbol[256], u8 length[256] and the ring.
 // The packed string lengths of step 1 are staged in the ring, which is free
 // until the rounds start.
-template <int BPL, bool SMALL>
+template <int BPL, bool SMALL, int SEG = 0>
 struct Lds {
     static constexpr uint32_t kOffD = 0;
     static constexpr uint32_t kOffSym = SMALL ? 1024 : 4112;
@@ -69,7 +69,15 @@ struct Lds {
     static constexpr uint32_t kRound = 64 * BPL;
     // 2 KiB holds a round's output at up to ~4 bytes per code; a round that
     // decodes to more is written in parts (lanes [l0, l1) at a time)
-    static constexpr uint32_t kRing = kPackedMax > 2048 + 64 ? kPackedMax : 2048 + 64;
+    // SEG: a round is 64 segments of 16 codes (about 2.8 KB of l_comment);
+    // kSegCap bytes of decoded output per part, plus the slack a lane may
+    // write past its segment's claimed end (16 codes x 8 B + a qword) when a
+    // corrupt table understates it
+    static constexpr uint32_t kSegCap = SEG > 0 ? (uint32_t)SEG : 4096u;  // SEG = the cap (bytes)
+    static constexpr uint32_t kSegSlack = 16 * 8 + 16;
+    static constexpr uint32_t kRingPlain = kPackedMax > 2048 + 64 ? kPackedMax : 2048 + 64;
+    static constexpr uint32_t kRingSeg = kPackedMax > kSegCap + kSegSlack ? kPackedMax : kSegCap + kSegSlack;
+    static constexpr uint32_t kRing = SEG ? kRingSeg : kRingPlain;
     static constexpr uint32_t kWave = kOffRing + kRing;
     static_assert(kOffSym % 16 == 0 && kOffRing % 16 == 0 && kWave % 16 == 0, "LDS layout alignment");
 };
@@ -233,6 +241,69 @@ __device__ __forceinline__ bool has_escape(const v4u &raw) {
     return (BPL == 8 ? (ff(raw.x) | ff(raw.y)) : (ff(raw.x) | ff(raw.y) | ff(raw.z) | ff(raw.w))) != 0;
 }
 
+// One lane's segment (segmented kernel): its nb (<= 16) code bytes in raw,
+// decoded from escape state st into the ring at byte wp; returns the bytes
+// written, st = the state after its last code.  FULL: all 16 bytes are codes;
+// ESC: the vector holds escape codes (without them every code is a symbol,
+// and a stray escape decodes to nothing -- its staged entry is {0, 0} -- which
+// the byte-count check catches).  Table reads go out 8 codes at a time.
+template <bool FULL, bool ESC>
+__device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, uint32_t nb, uint32_t &st, uint32_t wp) {
+    // an opaque copy: the callers' variants would otherwise share (hoist) the
+    // byte extraction and table addresses of all 16 codes ahead of their
+    // branch, all of them live at once
+    v4u raw = raw_in;
+    asm volatile("" : "+v"(raw.x), "+v"(raw.y), "+v"(raw.z), "+v"(raw.w));
+    // codes per batch of table reads: the general path keeps each code byte
+    // (a literal's value) beside its table entry, so it reads 4 at a time to
+    // stay in the fast path's register budget
+    constexpr uint32_t B = (FULL && !ESC) ? 8 : 4;
+    QwordWriter<> qw(w.ring, wp);
+    uint32_t got = 0;
+#pragma unroll
+    for (uint32_t h = 0; h < 16 / B; ++h) {
+        uint32_t c[B], sl[B];
+        uint64_t sy[B];
+#pragma unroll
+        for (uint32_t k = 0; k < B; ++k) {
+            c[k] = byte_of(raw, B * h + k);
+            sy[k] = w.sym[c[k]];
+            sl[k] = w.len[c[k]];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < B; ++k) {
+            // selects as bit masks (v_bfi), not compares: per-code lane masks
+            // would each take an SGPR pair, and 16 live ones spill
+            uint32_t vlo = (uint32_t)sy[k], vhi = (uint32_t)(sy[k] >> 32), n = sl[k];
+            if constexpr (ESC) {
+                const uint32_t lit = 0u - st;                        // all ones after an escape
+                vlo = (vlo & ~lit) | (c[k] & lit);
+                vhi &= ~lit;
+                n = (n & ~lit) | (1u & lit);
+                uint32_t ns = ((c[k] + 1u) >> 8) & ~st;             // an escape code, not a literal
+                if constexpr (!FULL) {
+                    const uint32_t in = 0u - (((B * h + k) - nb) >> 31);  // all ones iff Bh + k < nb
+                    ns = (ns & in) | (st & ~in);
+                }
+                st = ns;
+            }
+            if constexpr (!FULL) {
+                const uint32_t in = 0u - (((B * h + k) - nb) >> 31);
+                vlo &= in;
+                vhi &= in;
+                n &= in;
+            }
+            qw.put((uint64_t)vhi << 32 | vlo, n);
+            got += n;
+        }
+        // the next batch's table reads stay behind this batch's writes:
+        // hoisted, their values would be live across them (spills)
+        wave_sync();
+    }
+    qw.finish();
+    return got;
+}
+
 // string_t of a string of n bytes at ring byte x, host pointer p (DMask:
 // dword index mask of a circular ring, ~0 for a flat one)
 template <uint32_t DMask = ~0u>
@@ -262,18 +333,21 @@ __device__ __forceinline__ v4u make_record(const Wave &w, uint32_t d0, uint32_t 
     else return make_record_at(w.ring, d0 - ring_base, n, ptr_base + d0);
 }
 
-template <int BPL, bool SMALL, int V>
+template <int BPL, bool SMALL, int V, int SEG = 0>
 __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t base, uint32_t nvals,
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
                             uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err,
                             bool table_lfs = false) {
+    static_assert(!SEG || (BPL == 16 && (V & kFsstZeroFlush) && !(V & (kFsstCirc | kFsstTwoQ | kFsstEarlyGather))),
+                  "the segmented kernel: 16 codes per lane, zero-at-flush ring, accumulator writer");
+    using Layout = Lds<BPL, SMALL, SEG>;
     bool bad = false;
     // kFsstCirc: a circular ring of kCirc bytes (a power of two) indexed by
     // decoded byte position mod kCirc, so retire() moves no tail, it only
     // advances ring_base (needs the zero-at-flush invariant)
-    constexpr uint32_t kCirc = (V & kFsstCirc) ? (Lds<BPL, SMALL>::kRing >= 4096 ? 4096u : 2048u) : 0u;
+    constexpr uint32_t kCirc = (V & kFsstCirc) ? (Layout::kRing >= 4096 ? 4096u : 2048u) : 0u;
     static_assert(!(V & kFsstCirc) || ((V & kFsstZeroFlush) && !(V & kFsstTwoQ)), "kFsstCirc needs zero-at-flush");
-    static_assert(kCirc <= Lds<BPL, SMALL>::kRing, "circular ring fits the ring area");
+    static_assert(kCirc <= Layout::kRing, "circular ring fits the ring area");
     // ---- 1. string lengths: u8 lengths (SMALL) or exclusive u32 offsets -----
     W = SMALL ? min(W, 8u) : W;
     const uint32_t n16 = 8 * W;
@@ -336,7 +410,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         // here on every byte past the decoded ones stays zero: flush() zeroes
         // the blocks it streams out and retire() the bytes its tail vacates,
         // so the rounds OR into zeros without zeroing first
-        for (uint32_t q = lane; q < Lds<BPL, SMALL>::kRing / 16; q += 64)
+        for (uint32_t q = lane; q < Layout::kRing / 16; q += 64)
             reinterpret_cast<lv4 *>(w.ring)[q] = mk4(0, 0, 0, 0);
         wave_sync();
     }
@@ -389,7 +463,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     };
 
     // ---- 2-4. code-parallel rounds -----------------------------------------
-    constexpr uint32_t kRound = Lds<BPL, SMALL>::kRound;
+    constexpr uint32_t kRound = Layout::kRound;
     // a lane's compressed bytes of the round starting at r0 (zeros past the end)
     auto load_raw = [&](uint32_t r0) -> v4u {
         const uint32_t idx0 = r0 + BPL * lane;
@@ -427,6 +501,65 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         ring_base = new_base;
         wave_sync();
     };
+    if constexpr (SEG) {
+        // ---- segmented rounds: lane l decodes segment 64r + l (16 codes) at
+        // the ring offset the segment table gives, from the escape state it
+        // gives: no gathered lengths to scan first, no entry-state hand-off
+        const uint32_t soff = sizeof(FsstVecHeader) + 128 * clen_w + ((comp_len + 15) & ~15u);
+        const FLS_GLOBAL FsstSegHeader *shp = reinterpret_cast<const FLS_GLOBAL FsstSegHeader *>(vh + soff);
+        const uint32_t nseg = (comp_len + kFsstSegCodes - 1) / kFsstSegCodes;
+        const bool vec_esc = (uni(shp->flags) & FSST_SEG_HAS_ESCAPE) != 0;
+        if (uni(shp->nseg) != nseg) bad = true;
+        gu8 *segv = vh + soff + sizeof(FsstSegHeader);
+        auto load_seg = [&](uint32_t r0) -> uint32_t {
+            const uint32_t k = (r0 >> 4) + lane;
+            return k < nseg ? (uint32_t)segv[k] : 0u;
+        };
+        v4u raw_next = load_raw(0);
+        uint32_t sv_next = load_seg(0);
+        for (uint32_t r0 = 0; r0 < comp_len; r0 += kRound) {
+            const uint32_t idx0 = r0 + 16 * lane;
+            const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, 16u) : 0u;
+            const v4u raw = raw_next;
+            const uint32_t sv = sv_next;
+            if (r0 + kRound < comp_len) {
+                raw_next = load_raw(r0 + kRound);
+                sv_next = load_seg(r0 + kRound);
+            }
+            const bool full = r0 + kRound <= comp_len;
+            if (r0 > 0) retire();   // the previous round's stores, after this round's loads
+            const uint32_t entry = sv > 128 ? 1u : 0u;
+            const uint32_t dl = entry ? sv - 129 : sv;
+            const uint32_t incl = scan_incl(dl, lane);
+            uint32_t st = entry, l0 = 0, done = 0;
+            for (;;) {  // the lanes whose output fits the ring, then the rest
+                const uint32_t p0 = out_pos - ring_base;
+                const bool fits = lane < l0 || p0 + (incl - done) <= Layout::kSegCap;
+                const uint64_t fm = __ballot(fits);
+                const uint32_t l1 = ~fm == 0 ? 64u : (uint32_t)__builtin_ctzll(~fm);
+                const uint32_t part = rl(incl, l1 - 1) - done;
+                wave_sync();
+                if (lane >= l0 && lane < l1) {
+                    const uint32_t wp = p0 + (incl - dl - done);
+                    const uint32_t got = !full   ? seg_lane<false, true>(w, raw, nb, st, wp)
+                                         : vec_esc ? seg_lane<true, true>(w, raw, nb, st, wp)
+                                                   : seg_lane<true, false>(w, raw, nb, st, wp);
+                    if (got != dl) bad = true;
+                }
+                wave_sync();
+                out_pos += part;
+                done += part;
+                if (l1 == 64) break;
+                retire();
+                l0 = l1;
+            }
+            // a lane's exit state is the entry state of the segment after it
+            const uint32_t nxt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 1) & 63) << 2), (int)entry);
+            if (lane < 63 && idx0 + 16 < comp_len && st != nxt) bad = true;
+            if (lane == 0 && entry != carry_lit) bad = true;
+            carry_lit = rl(st, min(63u, (comp_len - 1 - r0) / 16));
+        }
+    } else {
     v4u raw_next = load_raw(0);
     for (uint32_t r0 = 0; r0 < comp_len; r0 += kRound) {
         const uint32_t idx0 = r0 + BPL * lane;
@@ -461,7 +594,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         // retire() to empty the ring and continue (a lane writes <= 8 BPL bytes)
         // slack: qword ORs, retire()'s 32 B tail read (circular: the bytes
         // from ring_base to the round's end must not wrap onto ring_base)
-        constexpr uint32_t kCap = kCirc ? kCirc - 16 : Lds<BPL, SMALL>::kRing - 48;
+        constexpr uint32_t kCap = kCirc ? kCirc - 16 : Layout::kRingPlain - 48;
         uint32_t l0 = 0, done = 0;
         for (;;) {
             const uint32_t p0 = out_pos - ring_base;
@@ -511,6 +644,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         // state after the round's last valid byte (lane 63 unless the stream ends here)
         carry_lit = rl(lane_end, min(63u, (comp_len - 1 - r0) / BPL));
     }
+    }  // SEG
     if (carry_lit) bad = true;  // stream ends inside an escape
     retire();
     if (next_str < nvals) {     // lengths claim more bytes than the stream holds
@@ -547,7 +681,7 @@ __device__ __forceinline__ DevChunk load_chunk(const DevChunk *chunks, uint32_t 
 // `piece` consecutive items taken from the shared counter until it runs out
 // (a wave's pieces come in increasing order, so its chunk cursor only moves
 // forward).  The wave loads a chunk's symbol table once per stay in it.
-template <int BPL, bool SMALL, bool QUEUE, int V>
+template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
 __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint32_t nchunks, uint32_t nitems,
                                            uint32_t item0, uint32_t item1, uint32_t *queue, uint32_t piece, lu8 *L,
                                            uint32_t *err_generic) {
@@ -573,7 +707,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     }
     item0 = uni(item0);
     item1 = uni(item1);
-    using Layout = Lds<BPL, SMALL>;
+    using Layout = Lds<BPL, SMALL, SEG>;
     Wave w;
     w.P = reinterpret_cast<lv4 *>(L + Layout::kOffRing);
     w.D = reinterpret_cast<lu32 *>(L + Layout::kOffD);
@@ -631,7 +765,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
         const uint32_t nvals = uni(meta->nvals);
         const uint32_t W = uni(min((uint32_t)meta->bw, 32u));
         const uint32_t dbytes = uni(meta->aux_count);
-        fsst_vector<BPL, SMALL, V>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
+        fsst_vector<BPL, SMALL, V, SEG>(w, chunk + c.packed_off + poff, W, base, nvals, dbytes, aux + aoff,
                     (FLS_GLOBAL uint8_t *)(size_t)c.dict, c.heap_bytes, c.heap_host,
                     gptr(c.out) + 16ull * kVectorSize * v, lane, err, table_lfs);
         wave_sync();
@@ -651,8 +785,11 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
 #ifndef FLS_FSST_WAVES
 #define FLS_FSST_WAVES 4  // minimum waves per SIMD the register budget must allow
 #endif
-template <int BPL, bool SMALL, bool QUEUE, int V>
-__global__ __launch_bounds__(64, (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+#ifndef FLS_FSST_SEG_WAVES
+#define FLS_FSST_SEG_WAVES 6  // the segmented kernel: 80 VGPRs, no spill (LDS admits 5-6 waves per SIMD)
+#endif
+template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
+__global__ __launch_bounds__(64, SEG ? FLS_FSST_SEG_WAVES : (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                      uint32_t nitems, uint32_t *__restrict__ err,
                                                      uint32_t *__restrict__ queue, uint32_t piece) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw_generic[];
@@ -676,17 +813,17 @@ __global__ __launch_bounds__(64, (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_k
         i1 = min(i0 + per, nitems);
         if (i0 >= i1) return;
     }
-    fsst_range<BPL, SMALL, QUEUE, V>(chunks, nchunks, nitems, i0, i1, queue, piece, lds_raw, err);
+    fsst_range<BPL, SMALL, QUEUE, V, SEG>(chunks, nchunks, nitems, i0, i1, queue, piece, lds_raw, err);
 }
 
-template <int BPL, bool SMALL, bool QUEUE, int V>
+template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
 hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
-    const uint32_t shmem = Lds<BPL, SMALL>::kWave;
+    const uint32_t shmem = Lds<BPL, SMALL, SEG>::kWave;
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL, QUEUE, V>, 64, shmem) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_kernel<BPL, SMALL, QUEUE, V, SEG>, 64, shmem) !=
             hipSuccess)
             per_cu = 1;
     }
@@ -700,9 +837,10 @@ hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
         if (e != hipSuccess) return e;
     }
     if (getenv("FLS_DEBUG"))
-        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s>: variant %d, %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors%s\n",
-                BPL, SMALL ? "small" : "any", V, grid, per_cu, shmem, nvecs, how.queue ? " (piece queue)" : "");
-    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL, QUEUE, V>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs,
+        fprintf(stderr, "DEBUG: fsst_kernel<%d,%s%s>: variant %d, %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors%s\n",
+                BPL, SMALL ? "small" : "any", SEG ? ",seg" : "", V, grid, per_cu, shmem, nvecs,
+                how.queue ? " (piece queue)" : "");
+    hipLaunchKernelGGL((fsst_kernel<BPL, SMALL, QUEUE, V, SEG>), dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs,
                        d_err, how.queue, piece);
     return hipGetLastError();
 }
@@ -1061,6 +1199,17 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, const FsstLaunch &how) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
+    if (how.seg) {  // segmented kernel: 16 codes per lane per round; ring cap 4096 B or (A/B) 3072 B
+        if (how.seg_cap == 3072)
+            return how.queue ? (how.small ? launch_fsst_q<16, true, true, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                          : launch_fsst_q<16, false, true, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how))
+                             : (how.small ? launch_fsst_q<16, true, false, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                          : launch_fsst_q<16, false, false, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how));
+        return how.queue ? (how.small ? launch_fsst_q<16, true, true, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                      : launch_fsst_q<16, false, true, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how))
+                         : (how.small ? launch_fsst_q<16, true, false, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                      : launch_fsst_q<16, false, false, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how));
+    }
     if (how.bytes_per_lane == 16)
         return how.small ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream, how)
                          : launch_fsst_t<16, false>(d_chunks, nchunks, nvecs, d_err, stream, how);

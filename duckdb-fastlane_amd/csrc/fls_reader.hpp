@@ -96,10 +96,18 @@ inline const char *validate_chunk(const uint8_t *img, const FileMeta &m, uint32_
             if (fh.clen_w > 32 || !fits(vm.aux_off, fsst_stream_off(fh) + fh.comp_len, h.aux_len) ||
                 fh.heap_off % 16 || fh.heap_off + (uint64_t)vm.aux_count > h.reserved1)
                 return "FSST vector out of bounds";
+            if (h.reserved0 == kFsstSegCodes) {  // segment table after the stream
+                if (!fits(vm.aux_off, fsst_seg_off(fh) + fsst_seg_bytes(fh.comp_len), h.aux_len))
+                    return "FSST segment table out of bounds";
+                FsstSegHeader sh;
+                memcpy(&sh, img + ch.off + h.aux_off + vm.aux_off + fsst_seg_off(fh), sizeof(sh));
+                if (sh.nseg != fsst_nseg(fh.comp_len)) return "bad FSST segment table";
+            }
         }
     }
     if (h.enc == ENC_FSST) {
         if (h.aux_len < kFsstTableBytes || h.dict_count > 255) return "bad FSST symbol table";
+        if (h.reserved0 != 0 && h.reserved0 != kFsstSegCodes) return "bad FSST segment size";
         for (uint32_t k = 0; k < h.dict_count; ++k) {
             const uint8_t l = img[ch.off + h.aux_off + 8 * 256 + k];
             if (l < 1 || l > 8) return "bad FSST symbol length";

@@ -120,7 +120,7 @@ void align_to(std::vector<uint8_t> &b, size_t a) {
 std::vector<uint8_t> assemble_chunk(uint8_t enc, uint8_t T, uint8_t vbits, bool is_str,
                                     uint32_t nvals, std::vector<VecOut> &vecs,
                                     const std::vector<uint8_t> &chunk_aux, uint32_t dict_count,
-                                    uint64_t reserved1 = 0) {
+                                    uint64_t reserved1 = 0, uint32_t reserved0 = 0) {
     ChunkHeader h{};
     h.magic = kChunkMagic;
     h.enc = enc;
@@ -153,6 +153,7 @@ std::vector<uint8_t> assemble_chunk(uint8_t enc, uint8_t T, uint8_t vbits, bool 
     }
     h.aux_len = aux.size();
     h.dict_count = dict_count;
+    h.reserved0 = reserved0;
     h.reserved1 = reserved1;
     size_t total = h.aux_off + aux.size();
     total = (total + kChunkAlign - 1) & ~size_t(kChunkAlign - 1);
@@ -520,6 +521,29 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
     return st;
 }
 
+// The segment table of a vector's code stream (fls_format.hpp): per
+// kFsstSegCodes code bytes the bytes they decode to and the escape state
+// entering them, so a GPU lane can decode its segment with no hand-off.
+void fsst_segments(const FsstTable &st, const std::vector<uint8_t> &comp, uint8_t *out) {
+    FsstSegHeader sh{};
+    sh.nseg = fsst_nseg((uint32_t)comp.size());
+    uint8_t *seg = out + sizeof(sh);
+    uint32_t state = 0;  // 1: the next byte is an escape's literal
+    for (uint32_t k = 0; k < sh.nseg; ++k) {
+        const uint32_t entry = state;
+        uint32_t d = 0;
+        const size_t e = std::min<size_t>(comp.size(), (size_t)(k + 1) * kFsstSegCodes);
+        for (size_t j = (size_t)k * kFsstSegCodes; j < e; ++j) {
+            const uint8_t c = comp[j];
+            if (state) { d += 1; state = 0; }
+            else if (c == kFsstEscape) { state = 1; sh.flags |= FSST_SEG_HAS_ESCAPE; }
+            else d += st.len[c];
+        }
+        seg[k] = fsst_seg_value(d, entry);
+    }
+    memcpy(out, &sh, sizeof(sh));
+}
+
 std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n) {
     const FsstTable st = fsst_build(offs, bytes, n);
     std::vector<uint8_t> table(kFsstTableBytes, 0);
@@ -557,13 +581,14 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
         const int Wc = ffor_prepare(32, clens, cbase, u);
         vh.clen_base = (uint32_t)cbase;
         vh.clen_w = (uint32_t)Wc;
-        o.aux.assign(fsst_stream_off(vh) + comp.size(), 0);
+        o.aux.assign(fsst_seg_off(vh) + fsst_seg_bytes(vh.comp_len), 0);
         memcpy(o.aux.data(), &vh, sizeof(vh));
         pack(32, Wc, u, o.aux.data() + sizeof(vh));
         if (!comp.empty()) memcpy(o.aux.data() + fsst_stream_off(vh), comp.data(), comp.size());
+        fsst_segments(st, comp, o.aux.data() + fsst_seg_off(vh));
         heap += (dbytes + 15) & ~15ull;
     }
-    return assemble_chunk(ENC_FSST, 32, 0, true, n, vecs, table, (uint32_t)st.n, heap);
+    return assemble_chunk(ENC_FSST, 32, 0, true, n, vecs, table, (uint32_t)st.n, heap, kFsstSegCodes);
 }
 
 // VARCHAR: DICT when the distinct values are few (at most n / 8, and their

@@ -207,10 +207,25 @@ namespace {
 // whole 16 B blocks of a stream whose last block may end inside it.
 constexpr uint64_t kImagePad = 256;
 
-// FSST chunks of a launch: string-parallel (nsp chunks, sp_vecs vectors), then
-// code-parallel (cp_vecs vectors)
+// FSST chunks of a launch, one kernel group after another (order_for_launch):
+// 0 = segment tables and every string <= 255 bytes, 1 = segment tables,
+// 2 = strings <= 255 bytes, 3 = the rest (DevChunk.vbits: bit 0 = small
+// strings, bit 1 = segment tables); each group numbers its vectors through
+// DevChunk.vec_base.
+constexpr int kFsstGroups = 4;
+inline int fsst_group(uint8_t vbits) { return vbits == 3 ? 0 : vbits == 2 ? 1 : vbits == 1 ? 2 : 3; }
 struct FsstCounts {
-    uint32_t nsp = 0, sp_vecs = 0, cp_vecs = 0;
+    uint32_t n[kFsstGroups] = {}, vecs[kFsstGroups] = {};
+    uint32_t first(int g) const {
+        uint32_t f = 0;
+        for (int k = 0; k < g; ++k) f += n[k];
+        return f;
+    }
+    uint64_t total_vecs() const {
+        uint64_t t = 0;
+        for (int k = 0; k < kFsstGroups; ++k) t += vecs[k];
+        return t;
+    }
 };
 
 // Per-chunk algorithmic byte accounting (roofline numerator).
@@ -555,13 +570,18 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
             memcpy(&fh, t->img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
             bc->packed += 128ull * vm.bw + 128ull * fh.clen_w + fh.comp_len;
             bc->meta += sizeof(fh);
+            if (h.reserved0 == kFsstSegCodes) bc->meta += sizeof(FsstSegHeader) + fsst_nseg(fh.comp_len);
             // string-parallel kernel iff every string of the chunk is <= 255
             // bytes, decompressed and compressed (bounds from the two FFOR streams)
             const uint64_t dmax = (uint64_t)vm.for_base + (vm.bw >= 32 ? 0xFFFFFFFFull : (1ull << vm.bw) - 1);
             const uint64_t cmax = (uint64_t)fh.clen_base + (fh.clen_w >= 32 ? 0xFFFFFFFFull : (1ull << fh.clen_w) - 1);
             if (vm.for_base < 0 || dmax > 255 || cmax > 255) sp = false;
         }
-        d.vbits = sp ? 1 : 0;
+        // bit 1: segment tables (the segmented kernel; FLS_FSST_SEG=0 keeps
+        // the code-parallel one, an A/B knob)
+        const char *sg = getenv("FLS_FSST_SEG");
+        const bool seg = h.reserved0 == kFsstSegCodes && !(sg && atoi(sg) == 0);
+        d.vbits = (sp ? 1 : 0) | (seg ? 2 : 0);
         return d;  // separate kernels, fixed LDS layouts
     }
     bc->out += (uint64_t)h.nvals * d.ob;
@@ -595,6 +615,8 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // arms run on the same buffers): 0 = work queue, largest chunks first
 // (default); bit 0 = static grid-stride split; bit 1 = keep column order.
 // bit 2 = full-width register prefetch for every chunk (descriptor max_w = T).
+// bit 3 = FSST chunks with segment tables on the code-parallel kernel
+// (FLS_FSST_SEG=0) instead of the segmented one.
 // bit 4 = FSST rounds of 16 compressed bytes per lane instead of 8.
 // bit 5 = balanced static split of vectors over the resident waves, chunks in
 // file (row-group-major) order (balanced_split).  bit 6 = work queue even for
@@ -602,8 +624,8 @@ bool is_fsst(const fls_table *t, uint32_t rg, uint32_t c) { return t->meta.rgs[r
 // <= 255 bytes on the string-parallel kernel (default: every FSST chunk on the
 // code-parallel kernel; same-buffer A/B profiles/r1/abenv_fsst_cp.txt).
 enum : int {
-    POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST16 = 16, POLICY_BALANCED = 32,
-    POLICY_QUEUE = 64, POLICY_FSST_SP = 128
+    POLICY_STATIC = 1, POLICY_NO_LPT = 2, POLICY_FULL_PREFETCH = 4, POLICY_FSST_NOSEG = 8, POLICY_FSST16 = 16,
+    POLICY_BALANCED = 32, POLICY_QUEUE = 64, POLICY_FSST_SP = 128
 };
 // Balanced-split knobs, folded into the policy word (so a change rebuilds the
 // cached launch list): FLS_STATIC_PCT = % of the bytes split statically
@@ -619,7 +641,11 @@ int decode_policy() {
     // launch list is rebuilt: fold it in so a change rebuilds it
     const char *bp = getenv("FLS_BLOCKS_PER_CU");
     const int bpc = bp ? std::min(127, std::max(0, atoi(bp))) : 0;
-    return (e ? (atoi(e) & 0xFF) : 0) | pct << 8 | pieces << 16 | bpc << 24;
+    // FLS_FSST_SEG=0 (make_devchunk: FSST chunks with segment tables go to the
+    // code-parallel kernel) changes the descriptors: fold it in too
+    const char *sg = getenv("FLS_FSST_SEG");
+    const int noseg = sg && atoi(sg) == 0 ? POLICY_FSST_NOSEG : 0;
+    return ((e ? (atoi(e) & 0xFF) : 0) | noseg) | pct << 8 | pieces << 16 | bpc << 24;
 }
 
 // Policy for one launch: the default (no distribution bits) switches to the
@@ -641,7 +667,9 @@ int launch_policy(int policy, const std::vector<DevChunk> &v, DecodeGeom &geom) 
 // returns how many lead (main kernel) and the FSST counts
 uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int policy) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
-    auto sp_end = std::stable_partition(mid, v.end(), [](const DevChunk &d) { return d.vbits == 1; });
+    std::stable_sort(mid, v.end(), [](const DevChunk &a, const DevChunk &b) {
+        return fsst_group(a.vbits) < fsst_group(b.vbits);
+    });
     if (policy & POLICY_FULL_PREFETCH)
         for (auto it = v.begin(); it != mid; ++it) it->max_w = it->T;
     if (policy & POLICY_BALANCED) {
@@ -655,14 +683,11 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int policy) 
         });
     }
     *fc = FsstCounts();
-    fc->nsp = (uint32_t)(sp_end - mid);
-    for (auto it = mid; it != sp_end; ++it) {
-        it->vec_base = fc->sp_vecs;
-        fc->sp_vecs += it->nvec;
-    }
-    for (auto it = sp_end; it != v.end(); ++it) {
-        it->vec_base = fc->cp_vecs;
-        fc->cp_vecs += it->nvec;
+    for (auto it = mid; it != v.end(); ++it) {
+        const int g = fsst_group(it->vbits);
+        it->vec_base = fc->vecs[g];
+        fc->vecs[g] += it->nvec;
+        fc->n[g]++;
     }
     return (uint32_t)(mid - v.begin());
 }
@@ -711,8 +736,8 @@ OverlapSplit overlap_split() {
     return o;
 }
 
-// d_queue[0] = main decode work queue, [1] / [2] = FSST piece counters of the
-// small-string and the other FSST chunks.
+// d_queue[0] = main decode work queue, [1 + g] = FSST piece counter of kernel
+// group g (FsstCounts).
 //
 // Without a side stream (scan batches) the FSST kernels follow the main one
 // on its stream.  With one (a table decode), the FSST kernels (VALU-bound)
@@ -730,22 +755,31 @@ OverlapSplit overlap_split() {
 // (2 blocks + 8..12 waves: 24.7 ms).  The kernel trace shows the overlap phase
 // moving ~4.9 TB/s together, below the 5.6 TB/s of the main kernel alone: the
 // two compete for the CUs' LDS and issue slots as well as for HBM.
+constexpr uint32_t kQueueWords = 1 + kFsstGroups;
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
                       uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
                       SplitPlan plan, const SideStream *side = nullptr) {
     const uint32_t *d_split = plan.waves ? reinterpret_cast<const uint32_t *>(d_chunks + ntotal) : nullptr;
-    const uint32_t ncp = ntotal - nmain - fc.nsp;
     const bool sp = (policy & POLICY_FSST_SP) != 0;
     const OverlapSplit ov = overlap_split();
-    FsstLaunch small, any;
-    small.bytes_per_lane = any.bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
-    if (const char *fv = getenv("FLS_FSST_VARIANT")) small.variant = any.variant = atoi(fv) & 255;
-    small.small = true;
+    FsstLaunch how[kFsstGroups];
+    for (int g = 0; g < kFsstGroups; ++g) {
+        how[g].bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
+        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv) & 255;
+        how[g].small = g == 0 || g == 2;
+        how[g].seg = g < 2;
+        if (const char *sc = getenv("FLS_FSST_SEG_CAP")) how[g].seg_cap = atoi(sc);
+    }
+    auto launch_group = [&](int g, hipStream_t st, const FsstLaunch &h) -> hipError_t {
+        const DevChunk *dc = d_chunks + nmain + fc.first(g);
+        if (g == 2 && sp && !h.queue) return launch_fsst_sp(dc, fc.n[g], fc.vecs[g], d_err, st);
+        return launch_fsst(dc, fc.n[g], fc.vecs[g], d_err, st, h);
+    };
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
-    const uint64_t fsst_vecs = (uint64_t)fc.sp_vecs + fc.cp_vecs;
+    const uint64_t fsst_vecs = fc.total_vecs();
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
                          fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !d_split && !sp &&
                          !(policy & POLICY_STATIC);
@@ -754,35 +788,32 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
         DecodeGeom narrow = geom;
         const uint32_t shmem = 4 * (geom.p_bytes + geom.v_bytes);
         narrow.grid = std::min(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), cus * ov.decode_bpc);
-        e = hipMemsetAsync(d_queue, 0, 3 * sizeof(uint32_t), stream);
+        e = hipMemsetAsync(d_queue, 0, kQueueWords * sizeof(uint32_t), stream);
         if (e == hipSuccess) e = hipEventRecord(side->fork, stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(side->stream, side->fork, 0);
-        small.queue = d_queue + 1;
-        any.queue = d_queue + 2;
-        small.reset_queue = any.reset_queue = false;
-        FsstLaunch ns = small, na = any;
-        ns.waves_per_cu = na.waves_per_cu = ov.fsst_wpc;
+        FsstLaunch narrow_how[kFsstGroups];
+        for (int g = 0; g < kFsstGroups; ++g) {
+            how[g].queue = d_queue + 1 + g;
+            how[g].reset_queue = false;
+            narrow_how[g] = how[g];
+            narrow_how[g].waves_per_cu = ov.fsst_wpc;
+        }
         // main stream: narrow decode, then full FSST
         if (e == hipSuccess)
             e = launch_decode(d_chunks, nmain, d_err, narrow, stream, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
         // side stream: narrow FSST, then full decode
-        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, side->stream, ns);
-        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, side->stream, na);
+        for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, side->stream, narrow_how[g]);
         if (e == hipSuccess)
             e = launch_decode(d_chunks, nmain, d_err, geom, side->stream, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
-        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, small);
-        if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, stream, any);
+        for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, stream, how[g]);
         if (e == hipSuccess) e = hipEventRecord(side->join, side->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join, 0);
         return e;
     }
     e = launch_decode(d_chunks, nmain, d_err, geom, stream, (policy & POLICY_STATIC) ? nullptr : d_queue, d_split, plan);
-    // FSST chunks whose strings are all <= 255 bytes (first group): the
-    // code-parallel kernel with u8 string lengths, or the string-parallel one
-    if (e == hipSuccess)
-        e = sp ? launch_fsst_sp(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream)
-               : launch_fsst(d_chunks + nmain, fc.nsp, fc.sp_vecs, d_err, stream, small);
-    if (e == hipSuccess) e = launch_fsst(d_chunks + nmain + fc.nsp, ncp, fc.cp_vecs, d_err, stream, any);
+    // FSST groups in order; chunks whose strings are all <= 255 bytes without
+    // segment tables go to the string-parallel kernel under POLICY_FSST_SP
+    for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, stream, how[g]);
     return e;
 }
 
@@ -1115,7 +1146,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     HIP_TRY(sl.d_chunks.alloc(d.dev, kk));
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
-    HIP_TRY(sl.queue.alloc(d.dev, 3));
+    HIP_TRY(sl.queue.alloc(d.dev, kQueueWords));
     HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
                        plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
@@ -1722,7 +1753,7 @@ int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask) {
         }
     }
     // queue counters and the side stream exist before the timed region
-    HIP_TRY(r.queue.alloc(r.dev, 3));
+    HIP_TRY(r.queue.alloc(r.dev, kQueueWords));
     if (!r.side.stream) {
         HIP_TRY(hipStreamCreateWithFlags(&r.side.stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&r.side.fork, hipEventDisableTiming));

@@ -372,6 +372,33 @@ static int64_t fsst_expand(const uint8_t *table, const uint8_t *c, uint32_t clen
     return (int64_t)o;
 }
 
+/* The segment table after a vector's code stream (round-3 container, chunk
+ * header reserved0 == 16; the GPU's segmented FSST kernel reads it, this
+ * decoder does not need it): for every 16 code bytes, the bytes they decode to
+ * and whether they start with an escape's literal, as dlen or 129 + dlen.
+ * Recomputed here from the stream by the sequential decoder's own state
+ * machine and compared; 0 = consistent.  Serves fastlanes_facade.cpp:48
+ * (materialize), whose FSST step the kernel restates lane-parallel. */
+static int fsst_check_segments(const uint8_t *table, const uint8_t *cs, uint32_t clen, const uint8_t *seg_area)
+{
+    const uint32_t nseg = (clen + 15) / 16;
+    if (rd32(seg_area + 4) != nseg) return -1;
+    uint32_t has_esc = 0, st = 0;
+    for (uint32_t k = 0; k < nseg; ++k) {
+        const uint32_t entry = st;
+        uint32_t d = 0;
+        for (uint32_t j = 16 * k; j < clen && j < 16 * k + 16; ++j) {
+            if (st) { d += 1; st = 0; }
+            else if (cs[j] == 255) { st = 1; has_esc = 1; }
+            else d += table[8 * 256 + cs[j]];
+        }
+        const uint32_t want = entry ? 129 + d : d;
+        if (want > 255 || seg_area[16 + k] != want) return -1;
+    }
+    if ((rd32(seg_area) & 1) != has_esc) return -1;
+    return 0;
+}
+
 int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, uint32_t *offs,
                               uint8_t *heap, uint64_t cap)
 {
@@ -423,6 +450,7 @@ int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, u
         uint64_t cu[1024];
         flsref_unpack(32, (int)cw, vh + 16, cu);
         const uint8_t *cs = vh + 16 + 128 * (size_t)cw;
+        if (rd32(ch + 52) == 16 && fsst_check_segments(aux, cs, clen, cs + ((clen + 15u) & ~15u)) != 0) return -1;
         /* every string is compressed on its own: expand string by string */
         uint64_t sum = 0, cpos = 0;
         for (uint32_t i = 0; i < vn; ++i) {

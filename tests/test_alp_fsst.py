@@ -180,8 +180,21 @@ def test_gpu_alp_fsst_device_resident(fl, ref, gpu, n):
             assert np.array_equal(out[c], bits(vals)), name
 
 
+# FSST kernels: the segmented one (default for files with segment tables,
+# ring cap 4096 or 3072 bytes) and the round-2 code-parallel one (files
+# without them, or FLS_FSST_SEG=0)
+FSST_KERNELS = {"seg": {}, "seg3072": {"FLS_FSST_SEG_CAP": "3072"}, "cp": {"FLS_FSST_SEG": "0"}}
+
+
+def _use_kernel(monkeypatch, kernel):
+    for k, v in FSST_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
+
+
 @pytest.mark.gpu
-def test_gpu_fsst_escape_heavy_and_long_strings(fl, ref, gpu):
+@pytest.mark.parametrize("kernel", list(FSST_KERNELS))
+def test_gpu_fsst_escape_heavy_and_long_strings(fl, ref, gpu, monkeypatch, kernel):
+    _use_kernel(monkeypatch, kernel)
     rng = np.random.default_rng(3)
     n = 20000
     s = []
@@ -281,8 +294,10 @@ def test_fsst_escape_at_round_boundary_roundtrip(fl, ref, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", list(FSST_KERNELS))
 @pytest.mark.parametrize("maxsym", ["1", "8", "255"])
-def test_gpu_fsst_escape_at_round_boundary(fl, ref, gpu, monkeypatch, maxsym):
+def test_gpu_fsst_escape_at_round_boundary(fl, ref, gpu, monkeypatch, maxsym, kernel):
+    _use_kernel(monkeypatch, kernel)
     monkeypatch.setenv("FLS_FSST_MAX_SYMBOLS", maxsym)
     s = _boundary_strings() * 3
     img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
@@ -312,9 +327,14 @@ def _sp_tables(fl, rng):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("policy", ["128", "0"], ids=["string_parallel", "code_parallel"])
+@pytest.mark.parametrize("policy", ["128", "0", "seg", "seg3072"],
+                         ids=["string_parallel", "code_parallel", "segmented", "segmented3072"])
 def test_gpu_fsst_string_and_code_parallel_agree(fl, ref, gpu, monkeypatch, capfd, policy):
-    monkeypatch.setenv("FLS_DECODE_POLICY", policy)
+    if policy.startswith("seg"):
+        _use_kernel(monkeypatch, policy)
+    else:
+        monkeypatch.setenv("FLS_DECODE_POLICY", policy)
+        _use_kernel(monkeypatch, "cp")
     monkeypatch.setenv("FLS_DEBUG", "1")
     for name, s in _sp_tables(fl, np.random.default_rng(21)):
         img = fl.write_image([("s", fl.VARCHAR, s, fl.ENC_FSST)])
@@ -322,12 +342,16 @@ def test_gpu_fsst_string_and_code_parallel_agree(fl, ref, gpu, monkeypatch, capf
         rf = ref.RefFile(img)
         assert_strings_equal(fl, rf, 0, out[0])
         err = capfd.readouterr().err
-        # which kernels ran: every chunk is code-parallel by default (u8 string
-        # lengths when all strings are <= 255 bytes); policy 128 sends those
-        # chunks to the string-parallel kernel
+        # which kernels ran: chunks with segment tables (every file written
+        # now) take the segmented kernel; without it (FLS_FSST_SEG=0) they are
+        # code-parallel (u8 string lengths when all strings are <= 255 bytes),
+        # and policy 128 sends those to the string-parallel kernel
+        seg = policy.startswith("seg")
         assert ("fsst_sp_kernel" in err) == (policy == "128"), name
         assert ("fsst_kernel<8,small>" in err) == (policy == "0"), name
-        assert ("fsst_kernel<8,any>" in err) == (name == "mixed_rg"), name
+        assert ("fsst_kernel<8,any>" in err) == (name == "mixed_rg" and not seg), name
+        assert ("fsst_kernel<16,small,seg>" in err) == seg, name
+        assert ("fsst_kernel<16,any,seg>" in err) == (name == "mixed_rg" and seg), name
 
 
 @pytest.mark.gpu
@@ -342,31 +366,108 @@ def test_gpu_fsst_string_parallel_scan_pipeline(fl, ref, gpu, monkeypatch):
         assert fl.string_t_decode(got[15]) == rf.strings_rg(15, first // 65536)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("field", ["clen_base", "comp_len"])
-@pytest.mark.parametrize("policy", ["128", "0"], ids=["string_parallel", "code_parallel"])
-def test_gpu_fsst_corrupt_compressed_lengths_reported(fl, ref, gpu, monkeypatch, field, policy):
-    """A compressed-length stream that disagrees with the code stream (the
-    string-parallel kernel's string starts) is clamped and reported by the
-    string-parallel kernel.  The code-parallel kernel never reads the
-    per-string compressed lengths: it decodes such a vector exactly, and
-    reports a code stream shortened under the strings' lengths."""
-    monkeypatch.setenv("FLS_DECODE_POLICY", policy)
-    s = fsst_text(5000, np.random.default_rng(6))
-    img = fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)])
-    raw = bytearray(img.tobytes())
+def _fsst_vec0(raw):
+    """(chunk offset, FsstVecHeader offset, comp_len, clen_w) of vector 0 of the first chunk."""
     off = _chunk_header(raw)
     aux_off = struct.unpack_from("<Q", raw, off + 32)[0]
     meta = off + struct.unpack_from("<Q", raw, off + 16)[0]
     vh = off + aux_off + struct.unpack_from("<Q", raw, meta + 16)[0]
+    comp_len, _, clen_w = struct.unpack_from("<III", raw, vh + 4)
+    return off, vh, comp_len, clen_w
+
+
+def _seg_area(raw):
+    _, vh, comp_len, clen_w = _fsst_vec0(raw)
+    return vh + 16 + 128 * clen_w + ((comp_len + 15) & ~15), comp_len
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field", ["clen_base", "comp_len"])
+@pytest.mark.parametrize("policy", ["128", "0", "seg"], ids=["string_parallel", "code_parallel", "segmented"])
+def test_gpu_fsst_corrupt_compressed_lengths_reported(fl, ref, gpu, monkeypatch, field, policy):
+    """A compressed-length stream that disagrees with the code stream (the
+    string-parallel kernel's string starts) is clamped and reported by the
+    string-parallel kernel.  The code-parallel and segmented kernels never
+    read the per-string compressed lengths: they decode such a vector exactly,
+    and report a code stream shortened under the strings' lengths (or the
+    reader rejects it first, when the shorter stream no longer matches the
+    segment table's count)."""
+    if policy == "seg":
+        _use_kernel(monkeypatch, "seg")
+    else:
+        monkeypatch.setenv("FLS_DECODE_POLICY", policy)
+        _use_kernel(monkeypatch, "cp")
+    s = fsst_text(5000, np.random.default_rng(6))
+    img = fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)])
+    raw = bytearray(img.tobytes())
+    _, vh, comp_len, _ = _fsst_vec0(raw)
+    if field == "comp_len" and comp_len % 16 == 1:
+        pytest.skip("the shorter stream needs one segment fewer: rejected by the reader")
     at = vh + (8 if field == "clen_base" else 4)
     struct.pack_into("<I", raw, at, struct.unpack_from("<I", raw, at)[0] - 1)
     t = fl.Connection().read_image(bytes(raw))
     t.device_upload()
     t.device_decode()
-    if field == "clen_base" and policy == "0":
+    if field == "clen_base" and policy != "128":
         t.device_sync()
         assert_strings_equal(fl, ref.RefFile(img), 0, t.device_copy_out(0))
         return
+    with pytest.raises(fl.FlsError, match="corrupt"):
+        t.device_sync()
+
+
+def test_fsst_segment_tables_written_and_pinned(fl, ref, monkeypatch):
+    """Every FSST chunk carries a segment table (chunk header reserved0 = 16);
+    the oracle recomputes it from the code stream with its own sequential
+    state machine when it decodes, and rejects a table that disagrees."""
+    monkeypatch.setenv("FLS_FSST_MAX_SYMBOLS", "8")           # escapes in the stream
+    s = fsst_text(3000, np.random.default_rng(8)) + [b"\xff" * 7, b"Zz\x01" * 30] * 100
+    s = [x if isinstance(x, bytes) else x.encode() for x in s]
+    raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
+    off = _chunk_header(raw)
+    assert struct.unpack_from("<I", raw, off + 52)[0] == 16
+    area, comp_len = _seg_area(raw)
+    flags, nseg = struct.unpack_from("<II", raw, area)
+    assert nseg == (comp_len + 15) // 16 and flags & 1 == 1
+    segs = np.frombuffer(bytes(raw[area + 16: area + 16 + nseg]), np.uint8)
+    assert (segs > 128).any()                                  # some segment starts with a literal
+    assert ref.RefFile(bytes(raw)).strings_column(0) == s
+    for k, delta in ((0, 1), (nseg // 2, -1)):
+        bad = bytearray(raw)
+        bad[area + 16 + k] = (bad[area + 16 + k] + delta) & 0xFF
+        with pytest.raises(Exception):
+            ref.RefFile(bytes(bad)).strings_column(0)
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, area, 0)                       # claims no escape codes
+    with pytest.raises(Exception):
+        ref.RefFile(bytes(bad)).strings_column(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("what", ["dlen_up", "dlen_down", "entry", "no_escape_flag"])
+def test_gpu_fsst_corrupt_segment_table_reported(fl, ref, gpu, monkeypatch, what):
+    """The segmented kernel checks every lane's decoded byte count against its
+    segment's entry and every exit state against the next entry: a table that
+    disagrees with the stream is reported, never silently decoded."""
+    monkeypatch.setenv("FLS_FSST_MAX_SYMBOLS", "8")
+    s = fsst_text(5000, np.random.default_rng(12)) + [b"\xffQ" * 9] * 200
+    raw = bytearray(fl.write_image([("c", fl.VARCHAR, s, fl.ENC_FSST)]).tobytes())
+    area, comp_len = _seg_area(raw)
+    nseg = (comp_len + 15) // 16
+    segs = raw[area + 16: area + 16 + nseg]
+    if what == "dlen_up":
+        k = next(i for i in range(nseg) if 0 < segs[i] < 128)
+        raw[area + 16 + k] += 1
+    elif what == "dlen_down":
+        k = next(i for i in range(nseg) if 0 < segs[i] <= 128)
+        raw[area + 16 + k] -= 1
+    elif what == "entry":
+        k = next(i for i in range(nseg) if segs[i] <= 120)
+        raw[area + 16 + k] += 129                                 # claims a literal start
+    else:
+        struct.pack_into("<I", raw, area, 0)
+    t = fl.Connection().read_image(bytes(raw))
+    t.device_upload()
+    t.device_decode()
     with pytest.raises(fl.FlsError, match="corrupt"):
         t.device_sync()

@@ -1,8 +1,9 @@
 """bench.py's multi-GPU entry point, rehearsed on CPU:
 `bench.py --gpus N` without a torch.distributed launcher starts N ranks
 itself; each rank takes its contiguous row-group shard and the per-rank
-records go through the same all_gather + reduction a GPU run uses (gloo here,
-RCCL on the GPUs): job time = slowest rank, values = sum over ranks."""
+records go through the same gloo all_gather + reduction a GPU run uses (the
+bench creates no RCCL communicator): job time = slowest rank, values = sum
+over ranks.  test_bench_two_ranks_one_gpu runs the real thing on the GPU."""
 import json
 import os
 import subprocess
@@ -54,6 +55,49 @@ def test_gpus_n_spawns_ranks_and_reduces(_built, n):
     assert red["dt"] == 1.0 + 0.25 * (n - 1)                               # the slowest rank's time
     assert red["rowgroups"] == [b - a for a, b in shards]
     assert out["value"] == pytest.approx(600037902 / red["dt"])
+    assert out["ranks_per_gpu"] == 1 and len(set(out["gpu_ids"])) == n   # one GPU per rank on an n-GPU node
+
+
+def test_rank_device_wraps_over_visible_gpus():
+    assert [bench.rank_device(r, 8) for r in range(8)] == list(range(8))
+    assert [bench.rank_device(r, 1) for r in range(4)] == [0, 0, 0, 0]     # narrowed / 1-GPU lease
+    assert [bench.rank_device(r, 2) for r in range(4)] == [0, 1, 0, 1]
+    assert bench.ranks_per_gpu(["a", "b", "a", "a"]) == 3 and bench.ranks_per_gpu(["a", "b"]) == 1
+
+
+def test_two_ranks_share_one_gpu_dry_run(_built):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dry-run", "--dry-run-node-gpus",
+                        "1", "--workload", "lineitem", "--scale", "1"],
+                       capture_output=True, text=True, env=env, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["ranks_per_gpu"] == 2 and out["gpu_ids"] == ["host:gpu0", "host:gpu0"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu(_built):
+    """bench.py --gpus 2 end to end on the GPU (both ranks on GPU 0 of a 1-GPU
+    lease): each rank decodes and verifies its contiguous shard; the line
+    carries both ranks' records and every value of the table is verified."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, "-u", str(ROOT / "bench.py"), "--gpus", "2", "--scale", "1",
+                        "--steps", "3", "--warmup", "1", "--cpu-seconds", "0", "--e2e-scale", "0", "--no-traffic"],
+                       capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    cfg = out["config"]
+    assert out["n_gpus"] == 2 and cfg["rows"] == 6001215 and cfg["columns"] == 16
+    assert cfg["rowgroups_per_gpu"] == [46, 46] and cfg["parallelism"] == "rowgroup-shard x2"
+    assert cfg["ranks_per_gpu"] * cfg["physical_gpus"] >= 2
+    pr = out["per_rank"]
+    assert [p["rank"] for p in pr] == [0, 1] and [p["rowgroups"] for p in pr] == [46, 46]
+    assert all(p["mismatches"] == 0 for p in pr)
+    assert sum(p["values_checked"] for p in pr) == 6001215 * 16
+    assert cfg["verified_values_bit_exact"] == 6001215 * 16 and cfg["verified_mismatches"] == 0
+    assert out["value"] > 0 and sum(p["values"] for p in pr) == 6001215 * 16 * 3
 
 
 def test_wait_ranks_stops_the_others_when_one_fails():

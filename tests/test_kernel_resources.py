@@ -3,7 +3,8 @@ library's code-object metadata on the CPU (scripts/kernel_resources.py).
 They pin the occupancy design points DESIGN.md states: the encoder kernels
 spill nothing (a 6-wave build that spilled 6 VGPRs wrote wrong T=32 DELTA
 rows), the main decode kernel fits 4 waves per SIMD,
-the default code-parallel FSST kernel 6."""
+the default code-parallel FSST kernel 6, the segmented FSST kernel 6 with no
+spill."""
 import sys
 from pathlib import Path
 
@@ -44,6 +45,14 @@ def test_decode_kernel_fits_four_waves(res):
 
 def test_default_fsst_kernel_fits_six_waves(res):
     # fsst_kernel<8, SMALL, QUEUE, kFsstW6 | kFsstZeroFlush | kFsstAbsLds = 76>
-    hits = _find(res, "fsst_kernelILi8E", "ELi76EEEv")
+    hits = _find(res, "fsst_kernelILi8E", "ELi76ELi0EEEv")
     assert len(hits) == 4, hits
     assert all(r["vgpr"] <= 80 for r in hits.values()), hits
+
+
+def test_segmented_fsst_kernel_fits_six_waves_without_spill(res):
+    # fsst_kernel<16, SMALL, QUEUE, 76, ring cap 3072 | 4096>
+    hits = {**_find(res, "fsst_kernelILi16E", "ELi76ELi4096EEEv"), **_find(res, "fsst_kernelILi16E", "ELi76ELi3072EEEv")}
+    assert len(hits) == 8, hits
+    for name, r in hits.items():
+        assert r["vgpr"] <= 80 and r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
