@@ -89,7 +89,24 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
 // LenFromSym measured slower (profiles/r2/abenv_fsst_*.txt).
 enum : int {
     kFsstPlain = 1, kFsstTwoQ = 2, kFsstZeroFlush = 4, kFsstW6 = 8, kFsstCirc = 16, kFsstLenFromSym = 32, kFsstAbsLds = 64, kFsstEarlyGather = 128,
-    kFsstDefault = kFsstW6 | kFsstZeroFlush | kFsstAbsLds
+    kFsstDefault = kFsstW6 | kFsstZeroFlush | kFsstAbsLds,
+    // segmented kernel (FsstLaunch::seg): bit 0 = store a qword only once
+    // complete (kFsstSegSparse), bit 1 = two-qword writer (kFsstTwoQ)
+    kFsstSegSparse = kFsstPlain,
+    // bit 5 = symbol length packed into the staged symbol's top byte
+    // (tables of symbols <= 7 bytes only; kFsstSegPackedLen)
+    kFsstSegPackedLen = kFsstLenFromSym,
+    // bit 4 = all 16 table reads of a lane's segment issued together on the
+    // fast path (kFsstSegWide)
+    kFsstSegWide = kFsstCirc,
+    // bit 7 = two consecutive segments (32 codes) per lane per round
+    // (kFsstSegDouble)
+    kFsstSegDouble = kFsstEarlyGather,
+    // bit 8 = string_t records in whole batches of 64 strings (kFsstSegBatch)
+    kFsstSegBatch = 256,
+    // cost ablations of the segmented kernel (wrong output, timing only):
+    // no string_t records / no heap flush / no ring writes
+    kFsstAblateRecords = 512, kFsstAblateFlush = 1024, kFsstAblateWrite = 2048
 };
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {
@@ -100,7 +117,7 @@ struct FsstLaunch {
     int waves_per_cu = 0;         // grid: 0 = as many as fit, else at most this many per CU
     int variant = kFsstDefault;   // code-parallel kernel variant (kFsst* bits; FLS_FSST_VARIANT)
     bool seg = false;             // the chunks carry segment tables (DevChunk.vbits bit 1): segmented kernel
-    int seg_cap = 4096;           // its ring: decoded bytes per part of a round (4096 or 3072; FLS_FSST_SEG_CAP)
+    int seg_cap = 4096;           // its ring: decoded bytes per part of a round (4096 or 5120; FLS_FSST_SEG_CAP)
 };
 // Launch the FSST string decode over nchunks FSST chunks holding nvecs vectors
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).

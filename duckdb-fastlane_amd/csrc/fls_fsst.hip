@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
@@ -62,7 +63,9 @@ using lu32 = FLS_LDS uint32_t;
 template <int BPL, bool SMALL, int SEG = 0>
 struct Lds {
     static constexpr uint32_t kOffD = 0;
-    static constexpr uint32_t kOffSym = SMALL ? 1024 : 4112;
+    // string lengths / offsets: SMALL u8 lengths (1 KB), SMALL segmented
+    // u16 offsets mod 65536 (1025 entries), others u32 offsets (1025 entries)
+    static constexpr uint32_t kOffSym = SMALL ? (SEG ? 2064 : 1024) : 4112;
     static constexpr uint32_t kOffLen = kOffSym + 2048;
     static constexpr uint32_t kOffRing = kOffLen + 256;
     static constexpr uint32_t kPackedMax = SMALL ? 128 * 8 + 128 : 128 * 32 + 128;  // W <= 8 | 32, + zero row
@@ -74,7 +77,7 @@ struct Lds {
     // write past its segment's claimed end (16 codes x 8 B + a qword) when a
     // corrupt table understates it
     static constexpr uint32_t kSegCap = SEG > 0 ? (uint32_t)SEG : 4096u;  // SEG = the cap (bytes)
-    static constexpr uint32_t kSegSlack = 16 * 8 + 16;
+    static constexpr uint32_t kSegSlack = 2 * 16 * 8 + 16;   // up to 2 segments per lane
     static constexpr uint32_t kRingPlain = kPackedMax > 2048 + 64 ? kPackedMax : 2048 + 64;
     static constexpr uint32_t kRingSeg = kPackedMax > kSegCap + kSegSlack ? kPackedMax : kSegCap + kSegSlack;
     static constexpr uint32_t kRing = SEG ? kRingSeg : kRingPlain;
@@ -247,8 +250,74 @@ __device__ __forceinline__ bool has_escape(const v4u &raw) {
 // ESC: the vector holds escape codes (without them every code is a symbol,
 // and a stray escape decodes to nothing -- its staged entry is {0, 0} -- which
 // the byte-count check catches).  Table reads go out 8 codes at a time.
-template <bool FULL, bool ESC>
-__device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, uint32_t nb, uint32_t &st, uint32_t wp) {
+// Every symbol OR-ed into both qwords it spans (kFsstTwoQ: one more ds_or_b64
+// per code, half the VALU of the accumulator's carry logic)
+struct TwoQWriter {
+    FLS_LDS uint64_t *o64;
+    uint32_t p;
+    __device__ __forceinline__ TwoQWriter(lu8 *ring, uint32_t wp) : o64(reinterpret_cast<FLS_LDS uint64_t *>(ring)), p(wp) {}
+    __device__ __forceinline__ void put(uint64_t v, uint32_t n) {
+        // shift counts are taken mod 64 by the hardware: 8p mod 64 is the bit
+        // offset inside qword p / 8, ~(8p) mod 64 = 63 - it
+        const uint32_t b8 = p << 3;
+        const uint64_t lo = v << (b8 & 63), hi = (v >> 1) >> (~b8 & 63);
+        __hip_atomic_fetch_or(o64 + (p >> 3), lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_or(o64 + (p >> 3) + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        p += n;
+    }
+    __device__ __forceinline__ void finish() {}
+};
+
+// The accumulator writer, storing only when a qword is complete (kFsstSegSparse):
+// ~1 lane in 4 takes part in a code step's ds_or_b64 instead of all 64, which
+// is where the LDS bank conflicts of the per-code OR came from
+struct SparseWriter {
+    FLS_LDS uint64_t *o64;
+    uint64_t acc;
+    uint32_t q, bits;
+    __device__ __forceinline__ SparseWriter(lu8 *ring, uint32_t wp)
+        : o64(reinterpret_cast<FLS_LDS uint64_t *>(ring)), acc(0), q(wp >> 3), bits(8 * (wp & 7)) {}
+    __device__ __forceinline__ void put(uint64_t v, uint32_t n) {
+        const uint64_t lo = v << bits, hi = (v >> 1) >> (63 - bits);
+        acc |= lo;
+        const uint32_t nb = bits + 8 * n;
+        if (nb >= 64) {
+            __hip_atomic_fetch_or(o64 + q, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            ++q;
+            acc = hi;
+        }
+        bits = nb & 63;
+    }
+    __device__ __forceinline__ void finish() {
+        if (bits) __hip_atomic_fetch_or(o64 + q, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+};
+
+// PL: the staged table holds each symbol's length in its top byte (symbols of
+// at most 7 bytes, kFsstSegPackedLen): one table read per code instead of two
+// FB: codes per batch of table reads on the fast path (FULL, no escapes): 8,
+// or all 16 issued together (kFsstSegWide)
+// cost ablation (kFsstAblateWrite, wrong output): the symbols are read and
+// summed but never written
+struct NullWriter {
+    uint64_t acc = 0;
+    lu8 *ring;
+    uint32_t wp;
+    __device__ __forceinline__ NullWriter(lu8 *r, uint32_t p) : ring(r), wp(p) {}
+    __device__ __forceinline__ void put(uint64_t v, uint32_t n) { acc += v + n; }
+    __device__ __forceinline__ void finish() {
+        if (acc == 0x123456789ull) ring[wp] = 1;  // keeps the reads alive
+    }
+};
+template <int WR>   // 0 accumulator, 1 two-qword, 2 sparse, 3 none (ablation)
+using SegWriter = typename std::conditional<
+    WR == 1, TwoQWriter,
+    typename std::conditional<WR == 2, SparseWriter,
+                              typename std::conditional<WR == 3, NullWriter, QwordWriter<>>::type>::type>::type;
+
+template <bool FULL, bool ESC, int WR = 0, bool PL = false, uint32_t FB = 8>
+__device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, uint32_t nb, uint32_t &st,
+                                             SegWriter<WR> &qw) {
     // an opaque copy: the callers' variants would otherwise share (hoist) the
     // byte extraction and table addresses of all 16 codes ahead of their
     // branch, all of them live at once
@@ -257,8 +326,7 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
     // codes per batch of table reads: the general path keeps each code byte
     // (a literal's value) beside its table entry, so it reads 4 at a time to
     // stay in the fast path's register budget
-    constexpr uint32_t B = (FULL && !ESC) ? 8 : 4;
-    QwordWriter<> qw(w.ring, wp);
+    constexpr uint32_t B = (FULL && !ESC) ? FB : 4;
     uint32_t got = 0;
 #pragma unroll
     for (uint32_t h = 0; h < 16 / B; ++h) {
@@ -268,7 +336,12 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
         for (uint32_t k = 0; k < B; ++k) {
             c[k] = byte_of(raw, B * h + k);
             sy[k] = w.sym[c[k]];
-            sl[k] = w.len[c[k]];
+            if constexpr (PL) {
+                sl[k] = (uint32_t)(sy[k] >> 56);
+                sy[k] &= 0x00FFFFFFFFFFFFFFull;
+            } else {
+                sl[k] = w.len[c[k]];
+            }
         }
 #pragma unroll
         for (uint32_t k = 0; k < B; ++k) {
@@ -300,7 +373,6 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
         // hoisted, their values would be live across them (spills)
         wave_sync();
     }
-    qw.finish();
     return got;
 }
 
@@ -338,14 +410,14 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                             uint32_t dbytes, gu8 *vh, FLS_GLOBAL uint8_t *heap, uint32_t heap_bytes,
                             uint64_t heap_host, FLS_GLOBAL uint8_t *out, uint32_t lane, uint32_t *err,
                             bool table_lfs = false) {
-    static_assert(!SEG || (BPL == 16 && (V & kFsstZeroFlush) && !(V & (kFsstCirc | kFsstTwoQ | kFsstEarlyGather))),
-                  "the segmented kernel: 16 codes per lane, zero-at-flush ring, accumulator writer");
+    static_assert(!SEG || (BPL == 16 && (V & kFsstZeroFlush)),
+                  "the segmented kernel: 16 codes per lane, zero-at-flush ring");
     using Layout = Lds<BPL, SMALL, SEG>;
     bool bad = false;
     // kFsstCirc: a circular ring of kCirc bytes (a power of two) indexed by
     // decoded byte position mod kCirc, so retire() moves no tail, it only
     // advances ring_base (needs the zero-at-flush invariant)
-    constexpr uint32_t kCirc = (V & kFsstCirc) ? (Layout::kRing >= 4096 ? 4096u : 2048u) : 0u;
+    constexpr uint32_t kCirc = (!SEG && (V & kFsstCirc)) ? (Layout::kRing >= 4096 ? 4096u : 2048u) : 0u;
     static_assert(!(V & kFsstCirc) || ((V & kFsstZeroFlush) && !(V & kFsstTwoQ)), "kFsstCirc needs zero-at-flush");
     static_assert(kCirc <= Layout::kRing, "circular ring fits the ring area");
     // ---- 1. string lengths: u8 lengths (SMALL) or exclusive u32 offsets -----
@@ -356,7 +428,37 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     if (lane < 8) w.P[n16 + lane] = mk4(0, 0, 0, 0);
     wave_sync();
     uint32_t total = 0;
-    if constexpr (SMALL) {
+    if constexpr (SMALL && SEG) {
+        // u8 lengths staged in the ring past the packed words, then each lane
+        // turns 16 consecutive ones into u16 exclusive offsets (mod 65536:
+        // finalize_seg rebuilds the high bits, strings being <= 255 bytes)
+        lu32 *L8 = reinterpret_cast<lu32 *>(w.ring + 2048);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t ci = lane + 64 * j;
+            const v4u v = add_base<32>(unpack_chunk<32>(w.P, W, ci), base);
+            const uint32_t b0 = 4 * ci < nvals ? v.x & 255 : 0, b1 = 4 * ci + 1 < nvals ? v.y & 255 : 0;
+            const uint32_t b2 = 4 * ci + 2 < nvals ? v.z & 255 : 0, b3 = 4 * ci + 3 < nvals ? v.w & 255 : 0;
+            L8[ci] = b0 | b1 << 8 | b2 << 16 | b3 << 24;
+        }
+        wave_sync();
+        const v4u q = reinterpret_cast<const lv4 *>(L8)[lane];
+        const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+        uint32_t a[16], run = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            a[k] = run;
+            run += (wd[k >> 2] >> (8 * (k & 3))) & 255;
+        }
+        const uint32_t incl = scan_incl(run, lane);
+        const uint32_t excl = incl - run;
+        lu32 *D32 = reinterpret_cast<lu32 *>(w.D);
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) D32[8 * lane + k / 2] = ((excl + a[k]) & 0xFFFF) | (excl + a[k + 1]) << 16;
+        if (lane == 63) reinterpret_cast<FLS_LDS uint16_t *>(w.D)[1024] = (uint16_t)incl;
+        total = rl(incl, 63);
+        wave_sync();
+    } else if constexpr (SMALL) {
         uint32_t run = 0;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
@@ -449,9 +551,125 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         }
         if constexpr (!SMALL) str_base = next_str < nvals ? uni(w.D[next_str]) : out_pos;
     };
+    // Segmented kernel: records in whole batches of 64 strings (no partial
+    // batch per round; the ring keeps an unfinished batch's bytes), offsets
+    // read straight from D (no length scan), the record assembled without
+    // branches.  force: also a partial batch (vector end, ring full).
+    auto finalize_seg = [&](bool force) {
+        if constexpr ((V & kFsstAblateRecords) != 0) {  // cost ablation (wrong output): no records
+            next_str = nvals;
+            return;
+        }
+        if constexpr ((V & kFsstSegBatch) == 0) {
+            // two batches of 64 strings per pass (strings i and i + 64 of
+            // every lane): both offset reads, then both sets of ring reads are
+            // in flight together, two LDS round trips per 128 records
+            while (next_str < nvals) {
+                uint32_t d0[2], n[2], rel1[2];
+                bool ok[2];
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t i = next_str + 64 * h + lane;
+                    uint32_t r0, r1;  // string start / end relative to str_base
+                    if constexpr (SMALL) {   // u16 offsets mod 65536: 128 strings span < 32 KB
+                        const FLS_LDS uint16_t *D16 = reinterpret_cast<const FLS_LDS uint16_t *>(w.D);
+                        const uint32_t b16 = D16[next_str];
+                        r0 = (D16[min(i, nvals)] - b16) & 0xFFFF;
+                        r1 = (D16[min(i + 1, nvals)] - b16) & 0xFFFF;
+                    } else {
+                        r0 = w.D[min(i, nvals)] - str_base;
+                        r1 = w.D[min(i + 1, nvals)] - str_base;
+                    }
+                    d0[h] = str_base + r0;
+                    n[h] = r1 - r0;
+                    rel1[h] = r1;
+                    ok[h] = i < nvals && d0[h] + min(n[h], 12u) <= out_pos;
+                }
+                const uint64_t ma = __ballot(ok[0]), mb = __ballot(ok[1]);
+                const uint32_t na = ~ma == 0 ? 64u : (uint32_t)__builtin_ctzll(~ma);
+                const uint32_t nb = na < 64 ? 0u : ~mb == 0 ? 64u : (uint32_t)__builtin_ctzll(~mb);
+                const lu32 *r32 = reinterpret_cast<const lu32 *>(w.ring);
+                uint32_t wd[2][4];
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {  // (lanes past the complete ones read harmless ring words)
+                    const uint32_t i0 = min(d0[h] - ring_base, Layout::kRing - 16) >> 2;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) wd[h][k] = r32[i0 + k];
+                }
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    if (lane < (h ? nb : na)) {
+                        const uint32_t sh = (d0[h] - ring_base) & 3, nn = n[h];
+                        const uint32_t b0 = __builtin_amdgcn_alignbyte(wd[h][1], wd[h][0], sh);
+                        const uint32_t b1 = __builtin_amdgcn_alignbyte(wd[h][2], wd[h][1], sh);
+                        const uint32_t b2 = __builtin_amdgcn_alignbyte(wd[h][3], wd[h][2], sh);
+                        auto keep = [nn](uint32_t word, uint32_t first) -> uint32_t {  // bytes [first, nn) of 4
+                            const uint32_t c = nn > first ? min(nn - first, 4u) : 0u;
+                            return c >= 4 ? word : word & ((1u << (8 * c)) - 1u);
+                        };
+                        const uint64_t p = ptr_base + d0[h];
+                        const bool inl = nn <= 12;
+                        *reinterpret_cast<ov4 *>(out + 16ull * (next_str + 64 * h + lane)) =
+                            mk4(nn, inl ? keep(b0, 0) : b0, inl ? keep(b1, 4) : (uint32_t)p,
+                                inl ? keep(b2, 8) : (uint32_t)(p >> 32));
+                    }
+                }
+                const uint32_t tot = na + nb;
+                if (nb > 0) str_base += rl(rel1[1], nb - 1);
+                else if (na > 0) str_base += rl(rel1[0], na - 1);
+                next_str += tot;
+                if (tot < 128) break;
+            }
+            return;
+        }
+        while (next_str < nvals) {
+            const uint32_t i = next_str + lane;
+            const bool valid = i < nvals;
+            uint32_t rel0, rel1;  // string start / end relative to str_base
+            if constexpr (SMALL) {
+                const FLS_LDS uint16_t *D16 = reinterpret_cast<const FLS_LDS uint16_t *>(w.D);
+                const uint32_t a = D16[min(i, nvals)], b = D16[min(i + 1, nvals)];
+                const uint32_t b16 = rl(a, 0);
+                rel0 = (a - b16) & 0xFFFF;
+                rel1 = (b - b16) & 0xFFFF;
+            } else {
+                rel0 = w.D[min(i, nvals)] - str_base;
+                rel1 = w.D[min(i + 1, nvals)] - str_base;
+            }
+            const uint32_t d0 = str_base + rel0, n = rel1 - rel0;
+            const bool ok = valid && d0 + min(n, 12u) <= out_pos;
+            const uint64_t m = __ballot(ok), vm = __ballot(valid);
+            // kFsstSegBatch: wait for the whole batch, unless its bytes fill
+            // half the ring (long strings: a batch of 64 may not fit the ring
+            // at all); measured slower (the kept tail moves every round)
+            if ((V & kFsstSegBatch) && !force && m != vm && out_pos - str_base <= Layout::kSegCap / 2) break;
+            const uint32_t n_ok = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);
+            if (lane < n_ok) {
+                const lu32 *r32 = reinterpret_cast<const lu32 *>(w.ring);
+                const uint32_t x = d0 - ring_base, i0 = x >> 2, sh = x & 3;
+                const uint32_t w0 = r32[i0], w1 = r32[i0 + 1], w2 = r32[i0 + 2], w3 = r32[i0 + 3];
+                const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                auto keep = [n](uint32_t word, uint32_t first) -> uint32_t {  // bytes [first, n) of 4
+                    const uint32_t c = n > first ? min(n - first, 4u) : 0u;
+                    return c >= 4 ? word : word & ((1u << (8 * c)) - 1u);
+                };
+                const uint64_t p = ptr_base + d0;
+                const bool inl = n <= 12;
+                *reinterpret_cast<ov4 *>(out + 16ull * i) =
+                    mk4(n, inl ? keep(b0, 0) : b0, inl ? keep(b1, 4) : (uint32_t)p, inl ? keep(b2, 8) : (uint32_t)(p >> 32));
+            }
+            if (n_ok > 0) str_base += rl(rel1, n_ok - 1);
+            next_str += n_ok;
+            if (n_ok < 64) break;
+        }
+    };
     // stream complete 16 B blocks below `upto` (16-aligned) to the heap
     auto flush = [&](uint32_t upto) {
-        const uint32_t nblk = (upto - ring_base) >> 4;
+        // (a ring never holds more than kRing bytes: the clamp bounds the
+        // loop whatever a corrupt stream did to the positions)
+        const uint32_t nblk = (V & kFsstAblateFlush) ? 0u : min((upto - ring_base) >> 4, Layout::kRing / 16);
         for (uint32_t q = lane; q < nblk; q += 64) {
             const uint32_t g = ring_base + 16 * q;
             const uint32_t slot = kCirc ? (g >> 4) & (kCirc / 16 - 1) : q;
@@ -480,6 +698,57 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     };
     // string_t records of the strings decoded so far, complete 16 B blocks of
     // the ring to the heap, the unfinished tail (< 32 B) to the ring start
+    // segmented kernel's flush: up to 4 blocks per lane per pass, all ring
+    // reads in flight before the zeroing and the heap stores
+    auto flush_seg = [&](uint32_t upto) {
+        const uint32_t nblk = (V & kFsstAblateFlush) ? 0u : min((upto - ring_base) >> 4, Layout::kRing / 16);
+        lv4 *r16 = reinterpret_cast<lv4 *>(w.ring);
+        for (uint32_t q0 = 0; q0 < nblk; q0 += 256) {
+            v4u b[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t q = q0 + 64 * j + lane;
+                b[j] = q < nblk ? r16[q] : mk4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t q = q0 + 64 * j + lane;
+                if (q < nblk) {
+                    r16[q] = mk4(0, 0, 0, 0);
+                    const uint32_t g = ring_base + 16 * q;
+                    if (g + 16 <= hlim) *reinterpret_cast<ov4 *>(vheap + g) = b[j];
+                    else bad = true;
+                }
+            }
+        }
+    };
+    // segmented kernel: the kept tail (an unfinished batch of strings, up to
+    // a few KB) moves to the ring start 1 KB at a time, the bytes it vacates
+    // back to zero
+    auto retire_seg = [&](bool force) {
+        finalize_seg(force);
+        const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
+        const uint32_t new_base = keep_from & ~15u;
+        flush_seg(new_base);
+        wave_sync();
+        const uint32_t src = min(new_base - ring_base, Layout::kRing);
+        const uint32_t len = min((out_pos - new_base + 15) & ~15u, Layout::kRing - 16);
+        lv4 *r16 = reinterpret_cast<lv4 *>(w.ring);
+        if (src > 0) {
+            for (uint32_t o = 0; o < len; o += 1024) {
+                const uint32_t k = (o >> 4) + lane;
+                v4u t = mk4(0, 0, 0, 0);
+                if (16 * k < len) t = r16[(src >> 4) + k];
+                wave_sync();
+                if (16 * k < len) r16[k] = t;
+                wave_sync();
+            }
+            // vacated: [max(src, len), src + len)
+            for (uint32_t b = max(src, len) + 16 * lane; b < src + len; b += 1024) r16[b >> 4] = mk4(0, 0, 0, 0);
+        }
+        ring_base = new_base;
+        wave_sync();
+    };
     auto retire = [&]() {
         finalize();
         const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
@@ -511,53 +780,94 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
         const bool vec_esc = (uni(shp->flags) & FSST_SEG_HAS_ESCAPE) != 0;
         if (uni(shp->nseg) != nseg) bad = true;
         gu8 *segv = vh + soff + sizeof(FsstSegHeader);
-        auto load_seg = [&](uint32_t r0) -> uint32_t {
-            const uint32_t k = (r0 >> 4) + lane;
+        // NS consecutive segments per lane (kFsstSegDouble: 2, a round of
+        // 2048 codes, so the per-round work is spread over twice the codes)
+        constexpr uint32_t NS = (V & kFsstSegDouble) ? 2 : 1;
+        constexpr uint32_t kRoundSeg = 64 * 16 * NS;
+        const uint32_t n16 = (comp_len + 15) >> 4;
+        auto load_seg = [&](uint32_t r0, uint32_t j) -> uint32_t {
+            const uint32_t k = (r0 >> 4) + NS * lane + j;
             return k < nseg ? (uint32_t)segv[k] : 0u;
         };
-        v4u raw_next = load_raw(0);
-        uint32_t sv_next = load_seg(0);
-        for (uint32_t r0 = 0; r0 < comp_len; r0 += kRound) {
-            const uint32_t idx0 = r0 + 16 * lane;
-            const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, 16u) : 0u;
-            const v4u raw = raw_next;
-            const uint32_t sv = sv_next;
-            if (r0 + kRound < comp_len) {
-                raw_next = load_raw(r0 + kRound);
-                sv_next = load_seg(r0 + kRound);
+        auto load_codes = [&](uint32_t r0, uint32_t j) -> v4u {
+            const uint32_t k = (r0 >> 4) + NS * lane + j;
+            return k < n16 ? comp[k] : mk4(0, 0, 0, 0);
+        };
+        v4u raw_next[NS];
+        uint32_t sv_next[NS];
+#pragma unroll
+        for (uint32_t j = 0; j < NS; ++j) {
+            raw_next[j] = load_codes(0, j);
+            sv_next[j] = load_seg(0, j);
+        }
+        constexpr int WR = (V & kFsstAblateWrite) ? 3 : (V & kFsstTwoQ) ? 1 : (V & kFsstSegSparse) ? 2 : 0;
+        constexpr bool PL = (V & kFsstSegPackedLen) != 0;
+        constexpr uint32_t FB = (V & kFsstSegWide) ? 16 : 8;
+        for (uint32_t r0 = 0; r0 < comp_len; r0 += kRoundSeg) {
+            const uint32_t idx0 = r0 + 16 * NS * lane;
+            v4u raw[NS];
+            uint32_t dlj[NS], entj[NS], dl = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < NS; ++j) {
+                raw[j] = raw_next[j];
+                entj[j] = sv_next[j] > 128 ? 1u : 0u;
+                dlj[j] = entj[j] ? sv_next[j] - 129 : sv_next[j];
+                dl += dlj[j];
             }
-            const bool full = r0 + kRound <= comp_len;
-            if (r0 > 0) retire();   // the previous round's stores, after this round's loads
-            const uint32_t entry = sv > 128 ? 1u : 0u;
-            const uint32_t dl = entry ? sv - 129 : sv;
+            if (r0 + kRoundSeg < comp_len) {
+#pragma unroll
+                for (uint32_t j = 0; j < NS; ++j) {
+                    raw_next[j] = load_codes(r0 + kRoundSeg, j);
+                    sv_next[j] = load_seg(r0 + kRoundSeg, j);
+                }
+            }
+            const bool full = r0 + kRoundSeg <= comp_len;
+            if (r0 > 0) retire_seg(false);   // the previous round's stores, after this round's loads
+            const uint32_t entry = entj[0];
             const uint32_t incl = scan_incl(dl, lane);
-            uint32_t st = entry, l0 = 0, done = 0;
+            uint32_t st = entry, l0 = 0, done = 0, guard = 0;
             for (;;) {  // the lanes whose output fits the ring, then the rest
+                if (++guard > 130) {  // at most 64 parts + 64 retires: a corrupt table
+                    bad = true;
+                    break;
+                }
                 const uint32_t p0 = out_pos - ring_base;
                 const bool fits = lane < l0 || p0 + (incl - done) <= Layout::kSegCap;
                 const uint64_t fm = __ballot(fits);
                 const uint32_t l1 = ~fm == 0 ? 64u : (uint32_t)__builtin_ctzll(~fm);
+                if (l1 == l0) {  // nothing fits beside the kept tail: retire it first
+                    retire_seg(true);
+                    continue;    // then the tail is < 32 B and lane l0 (<= 256 B) fits
+                }
                 const uint32_t part = rl(incl, l1 - 1) - done;
                 wave_sync();
                 if (lane >= l0 && lane < l1) {
-                    const uint32_t wp = p0 + (incl - dl - done);
-                    const uint32_t got = !full   ? seg_lane<false, true>(w, raw, nb, st, wp)
-                                         : vec_esc ? seg_lane<true, true>(w, raw, nb, st, wp)
-                                                   : seg_lane<true, false>(w, raw, nb, st, wp);
-                    if (got != dl) bad = true;
+                    SegWriter<WR> qw(w.ring, p0 + (incl - dl - done));
+#pragma unroll
+                    for (uint32_t j = 0; j < NS; ++j) {
+                        if (j > 0 && st != entj[j]) bad = true;   // the state between a lane's segments
+                        st = entj[j];
+                        const uint32_t e0 = idx0 + 16 * j;
+                        const uint32_t nb = e0 < comp_len ? min(comp_len - e0, 16u) : 0u;
+                        const uint32_t got = !full   ? seg_lane<false, true, WR, PL>(w, raw[j], nb, st, qw)
+                                             : vec_esc ? seg_lane<true, true, WR, PL>(w, raw[j], nb, st, qw)
+                                                       : seg_lane<true, false, WR, PL, FB>(w, raw[j], nb, st, qw);
+                        if (got != dlj[j]) bad = true;
+                    }
+                    qw.finish();
                 }
                 wave_sync();
                 out_pos += part;
                 done += part;
                 if (l1 == 64) break;
-                retire();
+                retire_seg(true);
                 l0 = l1;
             }
             // a lane's exit state is the entry state of the segment after it
             const uint32_t nxt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 1) & 63) << 2), (int)entry);
-            if (lane < 63 && idx0 + 16 < comp_len && st != nxt) bad = true;
+            if (lane < 63 && idx0 + 16 * NS < comp_len && st != nxt) bad = true;
             if (lane == 0 && entry != carry_lit) bad = true;
-            carry_lit = rl(st, min(63u, (comp_len - 1 - r0) / 16));
+            carry_lit = rl(st, min(63u, (comp_len - 1 - r0) / (16 * NS)));
         }
     } else {
     v4u raw_next = load_raw(0);
@@ -646,7 +956,8 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     }
     }  // SEG
     if (carry_lit) bad = true;  // stream ends inside an escape
-    retire();
+    if constexpr (SEG) retire_seg(true);
+    else retire();
     if (next_str < nvals) {     // lengths claim more bytes than the stream holds
         bad = true;
         for (uint32_t i = next_str + lane; i < nvals; i += 64)
@@ -746,15 +1057,19 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
             wave_sync();
             const FLS_GLOBAL uint64_t *gs = reinterpret_cast<const FLS_GLOBAL uint64_t *>(aux);
             FLS_LDS uint64_t *ls = reinterpret_cast<FLS_LDS uint64_t *>(L + Layout::kOffSym);
-            bool zero_last = false;
+            bool zero_last = false, long8 = false;
             for (uint32_t k = lane; k < 256; k += 64) {
                 const uint32_t n = k == kFsstEscape ? 0u : min((uint32_t)aux[8 * 256 + k], 8u);
                 const uint64_t sy = n >= 8 ? gs[k] : gs[k] & ((1ull << (8 * n)) - 1);
-                ls[k] = sy;
+                // kFsstSegPackedLen: the length rides in the top byte (the
+                // host sends only tables of symbols <= 7 bytes)
+                ls[k] = (SEG && (V & kFsstSegPackedLen)) ? sy | (uint64_t)n << 56 : sy;
                 L[Layout::kOffLen + k] = (uint8_t)n;
                 zero_last |= n > 0 && ((sy >> (8 * (n - 1))) & 0xFF) == 0;
+                long8 |= n >= 8;
             }
             table_lfs = __ballot(zero_last) == 0;
+            if (SEG && (V & kFsstSegPackedLen) && __ballot(long8) != 0 && lane == 0) atomicOr(err, KERR_BAD_DESC);
             wave_sync();
             have_table = true;
         }
@@ -786,10 +1101,10 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
 #define FLS_FSST_WAVES 4  // minimum waves per SIMD the register budget must allow
 #endif
 #ifndef FLS_FSST_SEG_WAVES
-#define FLS_FSST_SEG_WAVES 6  // the segmented kernel: 80 VGPRs, no spill (LDS admits 5-6 waves per SIMD)
+#define FLS_FSST_SEG_WAVES 5  // the segmented kernel: 96 VGPRs, no spill (its LDS admits about 5 waves per SIMD)
 #endif
 template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
-__global__ __launch_bounds__(64, SEG ? FLS_FSST_SEG_WAVES : (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+__global__ __launch_bounds__(64, SEG ? ((V & kFsstSegDouble) ? 4 : FLS_FSST_SEG_WAVES) : (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                      uint32_t nitems, uint32_t *__restrict__ err,
                                                      uint32_t *__restrict__ queue, uint32_t piece) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw_generic[];
@@ -828,7 +1143,9 @@ hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
             per_cu = 1;
     }
     const int full = cus * std::max(1, per_cu);
-    const int grid = std::min<int>(how.waves_per_cu > 0 ? cus * std::min(how.waves_per_cu, per_cu) : full, (int)nvecs);
+    int wpc = how.waves_per_cu;
+    if (const char *e = getenv("FLS_FSST_WPC"); e && wpc == 0) wpc = std::max(0, atoi(e));  // A/B knob (standalone launches)
+    const int grid = std::min<int>(wpc > 0 ? cus * std::min(wpc, per_cu) : full, (int)nvecs);
     // overlapped: pieces of ~1/4 of a wave's share of a full grid, <= 16 vectors
     uint32_t piece = std::max<uint32_t>(1, std::min<uint32_t>(16, nvecs / (4u * (uint32_t)full)));
     if (const char *e = getenv("FLS_FSST_PIECE")) piece = (uint32_t)std::max(1, std::min(64, atoi(e)));  // A/B knob
@@ -1196,19 +1513,43 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
     return hipGetLastError();
 }
 
+// the segmented kernel's instantiations: variant V, ring cap CAP
+template <int V, int CAP>
+hipError_t launch_seg(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err, hipStream_t stream,
+                      const FsstLaunch &how) {
+    return how.queue ? (how.small ? launch_fsst_q<16, true, true, V, CAP>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                  : launch_fsst_q<16, false, true, V, CAP>(d_chunks, nchunks, nvecs, d_err, stream, how))
+                     : (how.small ? launch_fsst_q<16, true, false, V, CAP>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                  : launch_fsst_q<16, false, false, V, CAP>(d_chunks, nchunks, nvecs, d_err, stream, how));
+}
+
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, const FsstLaunch &how) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
-    if (how.seg) {  // segmented kernel: 16 codes per lane per round; ring cap 4096 B or (A/B) 3072 B
-        if (how.seg_cap == 3072)
-            return how.queue ? (how.small ? launch_fsst_q<16, true, true, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how)
-                                          : launch_fsst_q<16, false, true, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how))
-                             : (how.small ? launch_fsst_q<16, true, false, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how)
-                                          : launch_fsst_q<16, false, false, kFsstDefault, 3072>(d_chunks, nchunks, nvecs, d_err, stream, how));
-        return how.queue ? (how.small ? launch_fsst_q<16, true, true, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how)
-                                      : launch_fsst_q<16, false, true, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how))
-                         : (how.small ? launch_fsst_q<16, true, false, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how)
-                                      : launch_fsst_q<16, false, false, kFsstDefault, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how));
+    if (how.seg) {  // segmented kernel; variants and ring caps for A/B (FLS_FSST_VARIANT, FLS_FSST_SEG_CAP)
+        constexpr int SPLW = kFsstDefault | kFsstSegSparse | kFsstSegPackedLen | kFsstSegWide;
+        constexpr int SPLWD = SPLW | kFsstSegDouble;
+        constexpr int SPLWB = SPLW | kFsstSegBatch;
+        // default: sparse stores, packed lengths, 16 reads in flight, records
+        // in whole batches, ring cap 5120 (same-buffer A/B on l_comment SF10,
+        // profiles/r3/abenv_fsst_r3j.txt, abenv_fsst_r3l.txt: 2 % ahead of the
+        // same without batches, 2-3 % ahead of the code-parallel kernel)
+        switch (how.variant) {
+        case SPLWD:
+            return launch_seg<SPLWD, 6144>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLWB:
+        case kFsstDefault:
+            return launch_seg<SPLWB, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLW | kFsstAblateRecords:
+            return launch_seg<SPLW | kFsstAblateRecords, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLW | kFsstAblateFlush:
+            return launch_seg<SPLW | kFsstAblateFlush, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLW | kFsstAblateWrite:
+            return launch_seg<SPLW | kFsstAblateWrite, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        default:
+            return how.seg_cap == 5120 ? launch_seg<SPLW, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how)
+                                       : launch_seg<SPLW, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        }
     }
     if (how.bytes_per_lane == 16)
         return how.small ? launch_fsst_t<16, true>(d_chunks, nchunks, nvecs, d_err, stream, how)

@@ -443,11 +443,20 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
     const char *ms = getenv("FLS_FSST_MAX_SYMBOLS");
     const int max_symbols = ms ? std::max(0, std::min(255, atoi(ms))) : 255;
     // sample: whole strings at evenly spaced rows, about 16 KiB
+    const char *se = getenv("FLS_FSST_SAMPLE");
+    const uint64_t sample_bytes = se ? std::max(1024, atoi(se)) : 16384;
+    const char *re = getenv("FLS_FSST_ROUNDS");
+    const int rounds = re ? std::max(1, atoi(re)) : 5;
+    const char *ml = getenv("FLS_FSST_MAX_LEN");
+    // symbols of at most 7 bytes (FSST allows 8): the GPU's segmented kernel
+    // keeps a symbol's length in its top byte, one table read per code; on
+    // l_comment the 8th byte bought 0.6 % of compression
+    const uint32_t max_len = ml ? (uint32_t)std::max(1, std::min(8, atoi(ml))) : 7;
     std::vector<std::pair<uint32_t, uint32_t>> smp;  // (offset, length)
     const uint64_t total = offs[n] - offs[0];
-    const uint32_t step = (uint32_t)std::max<uint64_t>(1, total / 16384);  // rows between samples
+    const uint32_t step = (uint32_t)std::max<uint64_t>(1, total / sample_bytes);  // rows between samples
     uint64_t taken = 0;
-    for (uint32_t i = 0; i < n && taken < 16384; i += step) {
+    for (uint32_t i = 0; i < n && taken < sample_bytes; i += step) {
         smp.emplace_back(offs[i], offs[i + 1] - offs[i]);
         taken += offs[i + 1] - offs[i];
     }
@@ -461,7 +470,7 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
     struct KeyHash {
         size_t operator()(const Key &k) const { return (size_t)(k.sym * 0x9E3779B97F4A7C15ull ^ k.len); }
     };
-    for (int round = 0; round < 5; ++round) {
+    for (int round = 0; round < rounds; ++round) {
         st.index();
         // ids: 0..n-1 symbols, 256 + b escaped byte b
         std::vector<uint64_t> c1(512, 0);
@@ -499,8 +508,8 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
             uint32_t l1, l2;
             sym_of((int)(kv.first >> 9), s1, l1);
             sym_of((int)(kv.first & 511), s2, l2);
-            if (l1 >= 8) continue;
-            const uint32_t l = std::min<uint32_t>(8, l1 + l2);
+            if (l1 >= max_len) continue;
+            const uint32_t l = std::min<uint32_t>(max_len, l1 + l2);
             uint64_t sy = s1 | (s2 << (8 * l1));
             if (l < 8) sy &= (1ull << (8 * l)) - 1;
             add(sy, l, kv.second * l);
@@ -515,6 +524,43 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
             st.sym[st.n] = c.first.sym;
             st.len[st.n] = (uint8_t)c.first.len;
             st.n++;
+        }
+    }
+    // Every byte value that occurs in the chunk gets a one-byte symbol when
+    // the table has room for all of them (it always does for text: l_comment
+    // uses 35 byte values), displacing the lowest-gain multi-byte symbols.  A
+    // byte the sample missed would otherwise be escaped wherever it occurs:
+    // two code bytes instead of one, and the GPU decoder's slower escape path
+    // for every vector holding one.  Tables capped below 255 symbols
+    // (FLS_FSST_MAX_SYMBOLS, tests forcing escapes) are left as built.
+    if (max_symbols == 255) {
+        bool seen[256] = {};
+        const uint8_t *b = (const uint8_t *)bytes;
+        for (uint64_t i = offs[0]; i < offs[n]; ++i) seen[b[i]] = true;
+        bool single[256] = {};
+        int nsingle = 0;
+        for (int c = 0; c < st.n; ++c)
+            if (st.len[c] == 1) single[st.sym[c] & 0xFF] = true;
+        std::vector<uint8_t> missing;
+        for (int v = 0; v < 256; ++v) {
+            nsingle += seen[v] ? 1 : 0;
+            if (seen[v] && !single[v]) missing.push_back((uint8_t)v);
+        }
+        if (!missing.empty() && nsingle <= max_symbols) {
+            // candidates are in decreasing gain order: replace from the end,
+            // skipping one-byte symbols (they stay)
+            int c = st.n;
+            for (uint8_t v : missing) {
+                if (st.n < max_symbols) {
+                    st.sym[st.n] = v;
+                    st.len[st.n] = 1;
+                    st.n++;
+                    continue;
+                }
+                do { --c; } while (st.len[c] == 1);
+                st.sym[c] = v;
+                st.len[c] = 1;
+            }
         }
     }
     st.index();

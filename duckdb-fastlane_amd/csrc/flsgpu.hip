@@ -579,8 +579,13 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
         }
         // bit 1: segment tables (the segmented kernel; FLS_FSST_SEG=0 keeps
         // the code-parallel one, an A/B knob)
+        // and symbols of at most 7 bytes (the segmented kernel stages each
+        // symbol with its length in the top byte)
         const char *sg = getenv("FLS_FSST_SEG");
-        const bool seg = h.reserved0 == kFsstSegCodes && !(sg && atoi(sg) == 0);
+        bool short_syms = true;
+        const uint8_t *lens = t->img + ch.off + h.aux_off + 8 * 256;
+        for (uint32_t k = 0; k < h.dict_count && k < 255; ++k) short_syms &= lens[k] <= 7;
+        const bool seg = h.reserved0 == kFsstSegCodes && short_syms && !(sg && atoi(sg) == 0);
         d.vbits = (sp ? 1 : 0) | (seg ? 2 : 0);
         return d;  // separate kernels, fixed LDS layouts
     }
@@ -765,7 +770,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     FsstLaunch how[kFsstGroups];
     for (int g = 0; g < kFsstGroups; ++g) {
         how[g].bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
-        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv) & 255;
+        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv) & 0xFFFF;
         how[g].small = g == 0 || g == 2;
         how[g].seg = g < 2;
         if (const char *sc = getenv("FLS_FSST_SEG_CAP")) how[g].seg_cap = atoi(sc);

@@ -3,8 +3,8 @@ library's code-object metadata on the CPU (scripts/kernel_resources.py).
 They pin the occupancy design points DESIGN.md states: the encoder kernels
 spill nothing (a 6-wave build that spilled 6 VGPRs wrote wrong T=32 DELTA
 rows), the main decode kernel fits 4 waves per SIMD,
-the default code-parallel FSST kernel 6, the segmented FSST kernel 6 with no
-spill."""
+the default code-parallel FSST kernel 6, the segmented FSST kernel 5 (its LDS
+admits about that many) with no spill."""
 import sys
 from pathlib import Path
 
@@ -50,9 +50,9 @@ def test_default_fsst_kernel_fits_six_waves(res):
     assert all(r["vgpr"] <= 80 for r in hits.values()), hits
 
 
-def test_segmented_fsst_kernel_fits_six_waves_without_spill(res):
-    # fsst_kernel<16, SMALL, QUEUE, 76, ring cap 3072 | 4096>
-    hits = {**_find(res, "fsst_kernelILi16E", "ELi76ELi4096EEEv"), **_find(res, "fsst_kernelILi16E", "ELi76ELi3072EEEv")}
-    assert len(hits) == 8, hits
+def test_segmented_fsst_kernel_fits_five_waves_without_spill(res):
+    # fsst_kernel<16, SMALL, QUEUE, the default seg variant 381, ring cap 5120>
+    hits = _find(res, "fsst_kernelILi16E", "ELi381ELi5120EEEv")
+    assert len(hits) == 4, hits
     for name, r in hits.items():
-        assert r["vgpr"] <= 80 and r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
+        assert r["vgpr"] <= 96 and r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
