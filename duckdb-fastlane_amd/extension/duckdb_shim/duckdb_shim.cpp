@@ -237,3 +237,106 @@ string StringUtil::Lower(const string &s) {
 }
 
 }  // namespace duckdb
+
+// ---- residual filters ------------------------------------------------------
+namespace duckdb {
+
+namespace {
+const SelectionVector &incremental_sel() {
+    static const SelectionVector s;  // empty: identity
+    return s;
+}
+
+// -1 / 0 / 1 for comparable non-null values of one logical type
+int compare_values(const Value &a, const Value &b) {
+    switch (a.type().id()) {
+    case LogicalTypeId::VARCHAR: {
+        const string x = a.GetValue<string>(), y = b.GetValue<string>();
+        return x < y ? -1 : x > y ? 1 : 0;
+    }
+    case LogicalTypeId::FLOAT: case LogicalTypeId::DOUBLE: {
+        const double x = a.GetDouble(), y = b.GetDouble();
+        if (x != x || y != y) return (x != x) - (y != y);  // NaN sorts above everything, NaN = NaN
+        return x < y ? -1 : x > y ? 1 : 0;
+    }
+    case LogicalTypeId::UBIGINT: {
+        const uint64_t x = a.GetValue<uint64_t>(), y = b.GetValue<uint64_t>();
+        return x < y ? -1 : x > y ? 1 : 0;
+    }
+    default: {
+        const int64_t x = a.GetInt64(), y = b.GetInt64();
+        return x < y ? -1 : x > y ? 1 : 0;
+    }
+    }
+}
+
+bool eval_filter(const TableFilter &f, const Value &v) {
+    switch (f.filter_type) {
+    case TableFilterType::IS_NULL: return v.IsNull();
+    case TableFilterType::IS_NOT_NULL: return !v.IsNull();
+    case TableFilterType::CONSTANT_COMPARISON: {
+        auto &c = f.Cast<ConstantFilter>();
+        if (v.IsNull() || c.constant.IsNull()) return false;
+        const int r = compare_values(v, c.constant);
+        switch (c.comparison_type) {
+        case ExpressionType::COMPARE_EQUAL: return r == 0;
+        case ExpressionType::COMPARE_NOTEQUAL: return r != 0;
+        case ExpressionType::COMPARE_LESSTHAN: return r < 0;
+        case ExpressionType::COMPARE_LESSTHANOREQUALTO: return r <= 0;
+        case ExpressionType::COMPARE_GREATERTHAN: return r > 0;
+        case ExpressionType::COMPARE_GREATERTHANOREQUALTO: return r >= 0;
+        }
+        return false;
+    }
+    case TableFilterType::IN_FILTER:
+        if (v.IsNull()) return false;
+        for (auto &x : f.Cast<InFilter>().values)
+            if (!x.IsNull() && compare_values(v, x) == 0) return true;
+        return false;
+    case TableFilterType::CONJUNCTION_AND:
+        for (auto &ch : f.Cast<ConjunctionAndFilter>().child_filters)
+            if (!eval_filter(*ch, v)) return false;
+        return true;
+    case TableFilterType::CONJUNCTION_OR:
+        for (auto &ch : f.Cast<ConjunctionOrFilter>().child_filters)
+            if (eval_filter(*ch, v)) return true;
+        return false;
+    case TableFilterType::EXPRESSION_FILTER: return f.Cast<ExpressionFilter>().expr->EvaluateRow(v);
+    default: return true;  // optional / dynamic: may be skipped, DuckDB re-checks above the scan
+    }
+}
+}  // namespace
+
+void Vector::ToUnifiedFormat(idx_t, UnifiedVectorFormat &format) const {
+    format.sel = &incremental_sel();
+    format.data = GetData();
+}
+
+unique_ptr<TableFilterState> TableFilterState::Initialize(ClientContext &, const TableFilter &) {
+    return make_uniq<TableFilterState>();
+}
+
+idx_t ColumnSegment::FilterSelection(SelectionVector &sel, Vector &vector, UnifiedVectorFormat &, const TableFilter &filter,
+                                     TableFilterState &, idx_t, idx_t &approved_tuple_count) {
+    idx_t kept = 0;
+    for (idx_t i = 0; i < approved_tuple_count; ++i) {
+        const idx_t row = sel.get_index(i);
+        if (eval_filter(filter, vector.GetValue(row))) sel.set_index(kept++, row);
+    }
+    approved_tuple_count = kept;
+    return kept;
+}
+
+void DataChunk::Slice(const SelectionVector &sel, idx_t count) {
+    vector<Vector> nd;
+    nd.reserve(data.size());
+    for (auto &v : data) {
+        Vector nv(v.GetType());
+        for (idx_t i = 0; i < count; ++i) nv.SetValue(i, v.GetValue(sel.get_index(i)));
+        nd.push_back(std::move(nv));
+    }
+    data.swap(nd);
+    count_ = count;
+}
+
+}  // namespace duckdb

@@ -36,6 +36,7 @@ using optional_ptr = T *;
 using idx_t = uint64_t;
 using column_t = uint64_t;
 using data_ptr_t = uint8_t *;
+using const_data_ptr_t = const uint8_t *;
 
 constexpr idx_t STANDARD_VECTOR_SIZE = 2048;
 constexpr column_t COLUMN_IDENTIFIER_ROW_ID = (column_t)-1;
@@ -275,6 +276,7 @@ public:
     bool AllValid(idx_t n) const {
         return !may_null_ || std::find(valid_.begin(), valid_.begin() + n, false) == valid_.begin() + n;
     }
+    void ToUnifiedFormat(idx_t count, struct UnifiedVectorFormat &format) const;
     void SetVectorType(VectorType t) { vtype_ = t; }
     VectorType GetVectorType() const { return vtype_; }
     idx_t Capacity() const { return capacity_; }
@@ -345,6 +347,9 @@ public:
         for (auto &v : data) t.push_back(v.GetType());
         return t;
     }
+    // keep rows sel[0, count) (DuckDB turns the vectors into dictionary
+    // vectors over the same data; the shim copies the selected rows)
+    void Slice(const class SelectionVector &sel, idx_t count);
 
 private:
     idx_t count_ = 0;
@@ -467,6 +472,53 @@ public:
         }
         it->second->Cast<ConjunctionAndFilter>().child_filters.push_back(std::move(filter));
     }
+};
+
+// ---- residual filters: what DuckDB's own scans use for filters a scan
+// cannot apply natively (v1.3.2 planner/filter/expression_filter.hpp,
+// planner/table_filter_state.hpp, storage/table/column_segment.hpp,
+// common/types/selection_vector.hpp).  The shim evaluates row by row through
+// Value; Expression here is a stand-in the harness builds (DuckDB's
+// ExpressionFilter holds a bound planner Expression run by an executor).
+using sel_t = uint32_t;
+class SelectionVector {
+public:
+    SelectionVector() = default;
+    explicit SelectionVector(idx_t count) : sel_(count) {
+        for (idx_t i = 0; i < count; ++i) sel_[i] = (sel_t)i;
+    }
+    idx_t get_index(idx_t i) const { return sel_.empty() ? i : sel_[i]; }
+    void set_index(idx_t i, idx_t loc) { sel_[i] = (sel_t)loc; }
+
+private:
+    vector<sel_t> sel_;
+};
+struct UnifiedVectorFormat {
+    const SelectionVector *sel = nullptr;
+    const_data_ptr_t data = nullptr;
+};
+class Expression {
+public:
+    virtual ~Expression() = default;
+    virtual bool EvaluateRow(const Value &v) const = 0;  // shim stand-in
+};
+class ExpressionFilter : public TableFilter {
+public:
+    static constexpr TableFilterType TYPE = TableFilterType::EXPRESSION_FILTER;
+    explicit ExpressionFilter(unique_ptr<Expression> e) : TableFilter(TYPE), expr(std::move(e)) {}
+    unique_ptr<Expression> expr;
+};
+struct TableFilterState {
+    virtual ~TableFilterState() = default;
+    static unique_ptr<TableFilterState> Initialize(ClientContext &context, const TableFilter &filter);
+};
+class ColumnSegment {
+public:
+    // keep the approved_tuple_count rows of sel for which the filter holds
+    // (sel compacted in place); returns the new approved_tuple_count
+    static idx_t FilterSelection(SelectionVector &sel, Vector &vector, UnifiedVectorFormat &vdata,
+                                 const TableFilter &filter, TableFilterState &filter_state, idx_t scan_count,
+                                 idx_t &approved_tuple_count);
 };
 
 struct TableFunctionBindInput {

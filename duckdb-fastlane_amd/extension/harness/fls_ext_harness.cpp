@@ -16,7 +16,35 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
+
+#include "fastlanes_facade.hpp"  // ext_fastlane::FastLanesFacade (include/fastlanes_facade.hpp)
+
+// Source compatibility with the reference's declaration
+// (src/include/fastlanes_facade.hpp:33-44): code that takes these members'
+// addresses compiles against this facade unchanged.
+static_assert(std::is_same<decltype(&duckdb::ext_fastlane::FastLanesFacade::finalizeFile),
+                           void (duckdb::ext_fastlane::FastLanesFacade::*)()>::value,
+              "void finalizeFile(), as the reference declares it");
+static_assert(std::is_same<decltype(&duckdb::ext_fastlane::FastLanesFacade::openFile),
+                           bool (duckdb::ext_fastlane::FastLanesFacade::*)(const std::string &)>::value,
+              "bool openFile(const std::string &)");
+static_assert(std::is_same<decltype(&duckdb::ext_fastlane::FastLanesFacade::getColumnTypes),
+                           std::vector<duckdb::LogicalType> (duckdb::ext_fastlane::FastLanesFacade::*)()>::value,
+              "std::vector<LogicalType> getColumnTypes()");
+static_assert(std::is_same<decltype(&duckdb::ext_fastlane::FastLanesFacade::getColumnNames),
+                           std::vector<std::string> (duckdb::ext_fastlane::FastLanesFacade::*)()>::value,
+              "std::vector<std::string> getColumnNames()");
+static_assert(std::is_same<decltype(static_cast<bool (duckdb::ext_fastlane::FastLanesFacade::*)(
+                                        std::vector<duckdb::Value> &, duckdb::idx_t &)>(
+                               &duckdb::ext_fastlane::FastLanesFacade::readNextChunk)),
+                           bool (duckdb::ext_fastlane::FastLanesFacade::*)(std::vector<duckdb::Value> &,
+                                                                           duckdb::idx_t &)>::value,
+              "bool readNextChunk(std::vector<Value> &, idx_t &)");
+static_assert(std::is_same<decltype(&duckdb::ext_fastlane::FastLanesFacade::closeFile),
+                           void (duckdb::ext_fastlane::FastLanesFacade::*)()>::value,
+              "void closeFile()");
 
 #include "duckdb.hpp"
 
@@ -94,6 +122,9 @@ TableFunction *lookup(fls_ext_db *d, Query &q) {
 //   "OR <op> v|<op> v|..."             -> ConjunctionOrFilter of ConstantFilters
 //   "ISNULL" / "ISNOTNULL"             -> IsNullFilter / IsNotNullFilter
 //   "OPT <expr>"                       -> OptionalFilter(<expr>)
+//   "EXPR MOD m r" / "EXPR LIKE s"     -> ExpressionFilter (v % m == r / VARCHAR
+//                                         contains s): a filter the engine cannot
+//                                         evaluate, applied on the host
 // Several filters on one column AND together (TableFilterSet::PushFilter).
 // Constants are cast to the column type, as DuckDB's binder does before
 // pushing a comparison down: DATE 'YYYY-MM-DD', DECIMAL '12.34', 'nan'.
@@ -167,8 +198,28 @@ std::vector<std::string> split(const std::string &s, char sep) {
     }
 }
 
+// the shim's stand-in for a bound expression (DuckDB: `col % m = r`, `col LIKE '%s%'`)
+struct ModExpression : public Expression {
+    int64_t m, r;
+    ModExpression(int64_t m, int64_t r) : m(m), r(r) {}
+    bool EvaluateRow(const Value &v) const override { return !v.IsNull() && v.GetInt64() % m == r; }
+};
+struct ContainsExpression : public Expression {
+    std::string sub;
+    explicit ContainsExpression(std::string s) : sub(std::move(s)) {}
+    bool EvaluateRow(const Value &v) const override {
+        return !v.IsNull() && v.GetValue<std::string>().find(sub) != std::string::npos;
+    }
+};
+
 unique_ptr<TableFilter> parse_filter(const std::string &e, const LogicalType &type) {
     auto head = [&](const char *kw) { return e.rfind(kw, 0) == 0; };
+    if (head("EXPR MOD ")) {
+        long long m = 0, r = 0;
+        if (sscanf(e.c_str() + 9, "%lld %lld", &m, &r) != 2 || m == 0) throw BinderException("harness: bad '" + e + "'");
+        return make_uniq<ExpressionFilter>(make_uniq<ModExpression>(m, r));
+    }
+    if (head("EXPR LIKE ")) return make_uniq<ExpressionFilter>(make_uniq<ContainsExpression>(e.substr(10)));
     if (e == "ISNULL") return make_uniq<IsNullFilter>();
     if (e == "ISNOTNULL") return make_uniq<IsNotNullFilter>();
     if (head("OPT ")) return make_uniq<OptionalFilter>(parse_filter(e.substr(4), type));
@@ -474,6 +525,63 @@ const char *fls_ext_result_value(const fls_ext_result *r, int64_t row, int col) 
     return r->valid[row][col] ? r->cells[row][col].c_str() : nullptr;
 }
 void fls_ext_result_free(fls_ext_result *r) { delete r; }
+
+// The typed facade's read API exactly as the reference's intended scanner
+// drives it (src/scanner/scan_fastlanes.cpp:82-83,126: openFile,
+// getColumnTypes / getColumnNames at bind, then readNextChunk(values,
+// rows_read) until it returns false): every boxed value as Value::ToString
+// (NULL -> a null cell), the rows of each readNextChunk call in chunk_rows
+// (up to max_chunks of them, *nchunks = the number of calls that returned
+// rows).  max_rows < 0: the whole file.
+int fls_ext_facade_read(const char *path, int64_t max_rows, fls_ext_result **out, int64_t *chunk_rows,
+                        int max_chunks, int *nchunks) {
+    using duckdb::ext_fastlane::FastLanesFacade;
+    *out = nullptr;
+    *nchunks = 0;
+    FastLanesFacade f;
+    if (!f.openFile(path)) {
+        g_err = std::string("openFile failed: ") + path;
+        return -1;
+    }
+    const std::vector<duckdb::LogicalType> types = f.getColumnTypes();
+    const std::vector<std::string> names = f.getColumnNames();
+    if (types.size() != names.size() || types.empty()) {
+        g_err = "getColumnTypes / getColumnNames disagree";
+        return -1;
+    }
+    auto *r = new fls_ext_result;
+    r->names = names;
+    for (auto &t : types) r->types.push_back(t.ToString());
+    const size_t nc = types.size();
+    std::vector<duckdb::Value> vals;
+    duckdb::idx_t n = 0;
+    int k = 0;
+    while (f.readNextChunk(vals, n)) {
+        if (vals.size() != n * nc || n == 0 || n > STANDARD_VECTOR_SIZE) {
+            g_err = "readNextChunk: " + std::to_string(vals.size()) + " values for " + std::to_string(n) + " rows";
+            delete r;
+            return -1;
+        }
+        if (k < max_chunks) chunk_rows[k] = (int64_t)n;
+        ++k;
+        for (duckdb::idx_t i = 0; i < n; ++i) {
+            std::vector<std::string> row(nc);
+            std::vector<char> ok(nc, 1);
+            for (size_t c = 0; c < nc; ++c) {
+                const duckdb::Value &v = vals[i * nc + c];
+                if (v.IsNull()) ok[c] = 0;
+                else row[c] = v.ToString();
+            }
+            r->cells.push_back(std::move(row));
+            r->valid.push_back(std::move(ok));
+        }
+        if (max_rows >= 0 && (int64_t)r->cells.size() >= max_rows) break;
+    }
+    f.closeFile();
+    *nchunks = k;
+    *out = r;
+    return 0;
+}
 
 // Stream a query without materialising it: rows, a checksum of the result
 // and wall seconds.  The checksum is a polynomial hash per column over the

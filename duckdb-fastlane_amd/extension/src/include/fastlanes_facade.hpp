@@ -43,14 +43,17 @@ public:
     // Not in the reference's header: rows per row group for the COPY option
     // ROW_GROUP_SIZE (multiple of 1024, <= 65536); call after createFile.
     bool setRowGroupSize(idx_t rows);
-    // Returns void in the reference's header; bool here so COPY can report
-    // write errors (a void caller ignores it).
-    bool finalizeFile();
+    // void, as the reference declares it (src/include/fastlanes_facade.hpp:44);
+    // whether the file was written: finalizeOk(), why not: lastError().
+    void finalizeFile();
 
     bool isValid() const;
-    // Not in the reference's header: why the last writeChunk returned false
-    // (empty when no reason was recorded), for COPY's error message.
+    // Not in the reference's header: why the last writeChunk or finalizeFile
+    // failed (empty when no reason was recorded), for COPY's error message.
     const std::string &lastError() const;
+    // Not in the reference's header: true iff the last finalizeFile wrote the
+    // file.
+    bool finalizeOk() const;
 
     // Not in the reference's header: thread-local staging for COPY sinks.
     // Each sink thread copies its DataChunks into its own Stage; a Stage that

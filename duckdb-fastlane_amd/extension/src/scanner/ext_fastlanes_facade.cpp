@@ -83,6 +83,7 @@ public:
     fls_writer *writer = nullptr;
     std::string out_path;
     std::string error;                               // why the last call returned false (lastError)
+    bool finalized_ok = false;                       // the last finalizeFile wrote the file (finalizeOk)
     std::vector<LogicalType> wtypes;
     std::vector<std::string> wnames;
     Stage *own = nullptr;  // the serial path's stage (writeChunk(chunk), merges, the last row group)
@@ -600,9 +601,13 @@ bool FastLanesFacade::setRowGroupSize(idx_t rows) {
     return true;
 }
 
-bool FastLanesFacade::finalizeFile() {
+void FastLanesFacade::finalizeFile() {
     Impl &s = *pImpl;
-    if (!s.writer) return false;
+    s.finalized_ok = false;
+    if (!s.writer) {
+        s.error = "finalizeFile without createFile";
+        return;
+    }
     bool ok = s.own && s.flush_stage(*s.own);
     if (!ok && s.own) s.error = s.own->error;
     ok = s.wait_pending() && ok;
@@ -621,8 +626,10 @@ bool FastLanesFacade::finalizeFile() {
     }
     fls_writer_free(s.writer);
     s.writer = nullptr;
-    return ok;
+    s.finalized_ok = ok;
 }
+
+bool FastLanesFacade::finalizeOk() const { return pImpl->finalized_ok; }
 
 }  // namespace ext_fastlane
 }  // namespace duckdb

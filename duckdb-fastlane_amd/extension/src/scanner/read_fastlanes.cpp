@@ -31,12 +31,15 @@
 #include "duckdb/parser/expression/constant_expression.hpp"
 #include "duckdb/parser/expression/function_expression.hpp"
 #include "duckdb/parser/tableref/table_function_ref.hpp"
+#include "duckdb/common/types/selection_vector.hpp"
 #include "duckdb/planner/filter/conjunction_filter.hpp"
 #include "duckdb/planner/filter/constant_filter.hpp"
 #include "duckdb/planner/filter/in_filter.hpp"
 #include "duckdb/planner/filter/null_filter.hpp"
 #include "duckdb/planner/filter/optional_filter.hpp"
 #include "duckdb/planner/table_filter.hpp"
+#include "duckdb/planner/table_filter_state.hpp"
+#include "duckdb/storage/table/column_segment.hpp"
 #include "table_function/read_fastlanes.hpp"
 #include "type_mapping.hpp"
 
@@ -76,6 +79,15 @@ struct ReadGlobalState : public GlobalTableFunctionState {
     std::vector<uint8_t> mask;           // delivered table columns
     std::vector<fls_predicate> preds;    // pushed-down filter (empty: none)
     std::deque<string> pred_strs;        // VARCHAR constants the predicates point at
+    // pushed-down filters the engine cannot evaluate (e.g. EXPRESSION_FILTER):
+    // applied on the host to every delivered chunk the way DuckDB's own scans
+    // apply them (ColumnSegment::FilterSelection), so the query never fails
+    // on an unknown filter and no row that fails one is delivered
+    struct Residual {
+        column_t id;
+        const TableFilter *filter;  // owned by DuckDB's TableFilterSet (lives for the query)
+    };
+    vector<Residual> residual;
     std::vector<idx_t> rg_base;          // batch index of each file's first row group
     std::vector<std::shared_ptr<OpenTable>> tables;  // opened (mapped) at init, scanned in order
     idx_t total_rowgroups = 0;
@@ -99,6 +111,7 @@ struct RowGroupPin : public VectorBuffer {
 };
 
 struct ReadLocalState : public LocalTableFunctionState {
+    vector<unique_ptr<TableFilterState>> residual_state;  // one per ReadGlobalState::residual (per thread)
     buffer_ptr<RowGroupPin> pin;         // the row group being emitted (nullptr: none)
     fls_rowgroup rg{};
     idx_t rg_pos = 0;
@@ -150,29 +163,30 @@ unique_ptr<FunctionData> ReadBind(ClientContext &, TableFunctionBindInput &input
     return std::move(bind);
 }
 
-uint8_t CompareOp(ExpressionType t) {
+// engine comparison of a DuckDB one; false: none (the filter stays on the host)
+bool CompareOp(ExpressionType t, uint8_t &op) {
     switch (t) {
-    case ExpressionType::COMPARE_EQUAL: return FLS_CMP_EQ;
-    case ExpressionType::COMPARE_NOTEQUAL: return FLS_CMP_NE;
-    case ExpressionType::COMPARE_LESSTHAN: return FLS_CMP_LT;
-    case ExpressionType::COMPARE_LESSTHANOREQUALTO: return FLS_CMP_LE;
-    case ExpressionType::COMPARE_GREATERTHAN: return FLS_CMP_GT;
-    case ExpressionType::COMPARE_GREATERTHANOREQUALTO: return FLS_CMP_GE;
-    default: throw NotImplementedException("read_fastlanes: unsupported comparison in pushed-down filter");
+    case ExpressionType::COMPARE_EQUAL: op = FLS_CMP_EQ; return true;
+    case ExpressionType::COMPARE_NOTEQUAL: op = FLS_CMP_NE; return true;
+    case ExpressionType::COMPARE_LESSTHAN: op = FLS_CMP_LT; return true;
+    case ExpressionType::COMPARE_LESSTHANOREQUALTO: op = FLS_CMP_LE; return true;
+    case ExpressionType::COMPARE_GREATERTHAN: op = FLS_CMP_GT; return true;
+    case ExpressionType::COMPARE_GREATERTHANOREQUALTO: op = FLS_CMP_GE; return true;
+    default: return false;
     }
 }
 
-// `col <op> constant` with the constant in the column's physical type
-fls_predicate MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v, const LogicalType &type,
-                       std::deque<string> &strs) {
-    fls_predicate p;
+// `col <op> constant` with the constant in the column's physical type; false:
+// a type the engine does not compare (the filter stays on the host)
+bool MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v, const LogicalType &type,
+              std::deque<string> &strs, fls_predicate &p) {
     memset(&p, 0, sizeof(p));
     p.col = col;
     p.clause = clause;
     p.op = op;
     if (v.IsNull()) {  // a comparison with NULL is never true
         p.op = FLS_CMP_IS_NULL;
-        return p;
+        return true;
     }
     switch (type.id()) {
     case LogicalTypeId::TINYINT: case LogicalTypeId::SMALLINT: case LogicalTypeId::INTEGER:
@@ -208,26 +222,32 @@ fls_predicate MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v
         p.str = strs.back().data();
         p.str_len = strs.back().size();
         break;
-    default: throw NotImplementedException("read_fastlanes: unsupported filter type " + type.ToString());
+    default: return false;
     }
-    return p;
+    return true;
 }
 
-// one clause of OR-ed terms (constants, IN lists, IS [NOT] NULL)
-void AddOrTerms(const TableFilter &f, uint32_t col, uint32_t clause, const LogicalType &type,
+// one clause of OR-ed terms (constants, IN lists, IS [NOT] NULL); false: a
+// term the engine cannot evaluate
+bool AddOrTerms(const TableFilter &f, uint32_t col, uint32_t clause, const LogicalType &type,
                 std::vector<fls_predicate> &out, std::deque<string> &strs) {
+    fls_predicate p;
     switch (f.filter_type) {
     case TableFilterType::CONSTANT_COMPARISON: {
         auto &c = f.Cast<ConstantFilter>();
-        out.push_back(MakeTerm(col, clause, CompareOp(c.comparison_type), c.constant, type, strs));
+        uint8_t op;
+        if (!CompareOp(c.comparison_type, op) || !MakeTerm(col, clause, op, c.constant, type, strs, p)) return false;
+        out.push_back(p);
         break;
     }
     case TableFilterType::IN_FILTER:
-        for (auto &v : f.Cast<InFilter>().values) out.push_back(MakeTerm(col, clause, FLS_CMP_EQ, v, type, strs));
+        for (auto &v : f.Cast<InFilter>().values) {
+            if (!MakeTerm(col, clause, FLS_CMP_EQ, v, type, strs, p)) return false;
+            out.push_back(p);
+        }
         break;
     case TableFilterType::IS_NULL:
     case TableFilterType::IS_NOT_NULL: {
-        fls_predicate p;
         memset(&p, 0, sizeof(p));
         p.col = col;
         p.clause = clause;
@@ -236,26 +256,29 @@ void AddOrTerms(const TableFilter &f, uint32_t col, uint32_t clause, const Logic
         break;
     }
     case TableFilterType::CONJUNCTION_OR:
-        for (auto &ch : f.Cast<ConjunctionOrFilter>().child_filters) AddOrTerms(*ch, col, clause, type, out, strs);
+        for (auto &ch : f.Cast<ConjunctionOrFilter>().child_filters)
+            if (!AddOrTerms(*ch, col, clause, type, out, strs)) return false;
         break;
-    default: throw NotImplementedException("read_fastlanes: unsupported filter inside OR");
+    default: return false;
     }
+    return true;
 }
 
-// TableFilter on one column -> clauses (AND of ORs)
-void AddFilter(const TableFilter &f, uint32_t col, const LogicalType &type, uint32_t &clause,
+// TableFilter on one column -> clauses (AND of ORs); false: some part the
+// engine cannot evaluate (the caller keeps the whole filter on the host)
+bool AddFilter(const TableFilter &f, uint32_t col, const LogicalType &type, uint32_t &clause,
                std::vector<fls_predicate> &out, std::deque<string> &strs) {
     switch (f.filter_type) {
     case TableFilterType::CONJUNCTION_AND:
-        for (auto &ch : f.Cast<ConjunctionAndFilter>().child_filters) AddFilter(*ch, col, type, clause, out, strs);
-        break;
+        for (auto &ch : f.Cast<ConjunctionAndFilter>().child_filters)
+            if (!AddFilter(*ch, col, type, clause, out, strs)) return false;
+        return true;
     case TableFilterType::OPTIONAL_FILTER:  // optional by definition: DuckDB re-checks it above the scan
-        break;
+        return true;
     case TableFilterType::CONSTANT_COMPARISON: case TableFilterType::IN_FILTER: case TableFilterType::IS_NULL:
     case TableFilterType::IS_NOT_NULL: case TableFilterType::CONJUNCTION_OR:
-        AddOrTerms(f, col, clause++, type, out, strs);
-        break;
-    default: throw NotImplementedException("read_fastlanes: unsupported pushed-down filter type");
+        return AddOrTerms(f, col, clause++, type, out, strs);
+    default: return false;  // EXPRESSION_FILTER, STRUCT_EXTRACT, DYNAMIC_FILTER, ...
     }
 }
 
@@ -279,7 +302,15 @@ unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFuncti
             const column_t id = state->column_ids[entry.first];
             if (id == COLUMN_IDENTIFIER_ROW_ID || id >= bind.cols.size())
                 throw NotImplementedException("read_fastlanes: filter on a non-table column");
-            AddFilter(*entry.second, (uint32_t)id, bind.types[id], clause, state->preds, state->pred_strs);
+            // the engine takes the column's filter whole or not at all
+            const size_t n0 = state->preds.size();
+            const uint32_t c0 = clause;
+            if (!AddFilter(*entry.second, (uint32_t)id, bind.types[id], clause, state->preds, state->pred_strs)) {
+                state->preds.resize(n0);
+                clause = c0;
+                state->residual.push_back({id, entry.second.get()});
+                state->mask[id] = 1;  // the host needs the column's values
+            }
         }
     }
     // fail early on unreadable or schema-incompatible files
@@ -305,9 +336,12 @@ unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFuncti
     return std::move(state);
 }
 
-unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &, TableFunctionInitInput &,
-                                                  GlobalTableFunctionState *) {
-    return make_uniq<ReadLocalState>();
+unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &context, TableFunctionInitInput &,
+                                                  GlobalTableFunctionState *gstate) {
+    auto l = make_uniq<ReadLocalState>();
+    for (auto &r : gstate->Cast<ReadGlobalState>().residual)
+        l->residual_state.push_back(TableFilterState::Initialize(context.client, *r.filter));
+    return std::move(l);
 }
 
 // give back the local state's row group and claim the next one (in file and
@@ -338,47 +372,70 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
     }
 }
 
+// rows [rg_pos, rg_pos + n) of table column id into vec: a reference to the
+// pinned row group (zero-copy) or, for DECIMAL(w<=9), the engine's int64
+// narrowed to DuckDB's physical width
+void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector &vec, idx_t n) {
+    const idx_t ob = bind.cols[id].out_bytes;
+    const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
+    const idx_t phys = vec.GetType().PhysicalSize();
+    if (phys == ob) {
+        FlatVector::SetData(vec, (data_ptr_t)src);
+        vec.SetAuxiliary(l.pin);
+        return;
+    }
+    const int64_t *v = (const int64_t *)src;
+    if (phys == 4) {
+        int32_t *d = FlatVector::GetData<int32_t>(vec);
+        for (idx_t i = 0; i < n; ++i) d[i] = (int32_t)v[i];
+    } else {
+        int16_t *d = FlatVector::GetData<int16_t>(vec);
+        for (idx_t i = 0; i < n; ++i) d[i] = (int16_t)v[i];
+    }
+}
+
 void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
     const auto &bind = data.bind_data->Cast<ReadBindData>();
     auto &g = data.global_state->Cast<ReadGlobalState>();
     auto &l = data.local_state->Cast<ReadLocalState>();
-    output.Reset();
-    // (a filtered row group can deliver no rows)
-    while (!(l.pin && l.rg_pos < l.rg.nrows)) {
-        if (!NextRowGroup(bind, g, l)) {
-            output.SetCardinality(0);
-            return;
-        }
-    }
-    const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, l.rg.nrows - l.rg_pos);
-    for (idx_t j = 0; j < output.ColumnCount(); ++j) {
-        const column_t id = j < g.out_ids.size() ? g.column_ids[g.out_ids[j]] : j;
-        Vector &vec = output.data[j];
-        if (id == COLUMN_IDENTIFIER_ROW_ID) {
-            int64_t *rid = FlatVector::GetData<int64_t>(vec);
-            for (idx_t i = 0; i < n; ++i)
-                rid[i] = (int64_t)(l.rg.first_row + (l.rg.sel ? l.rg.sel[l.rg_pos + i] : l.rg_pos + i));
-            continue;
-        }
-        const idx_t ob = bind.cols[id].out_bytes;
-        const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
-        const idx_t phys = vec.GetType().PhysicalSize();
-        if (phys == ob) {  // zero-copy: reference the pinned row group
-            FlatVector::SetData(vec, (data_ptr_t)src);
-            vec.SetAuxiliary(l.pin);
-        } else {  // DECIMAL(w<=9): the int64 scaled value narrowed to DuckDB's physical width
-            const int64_t *v = (const int64_t *)src;
-            if (phys == 4) {
-                int32_t *d = FlatVector::GetData<int32_t>(vec);
-                for (idx_t i = 0; i < n; ++i) d[i] = (int32_t)v[i];
-            } else {
-                int16_t *d = FlatVector::GetData<int16_t>(vec);
-                for (idx_t i = 0; i < n; ++i) d[i] = (int16_t)v[i];
+    for (;;) {  // until a chunk with rows (host-side filters can empty one) or the end
+        output.Reset();
+        // (a filtered row group can deliver no rows)
+        while (!(l.pin && l.rg_pos < l.rg.nrows)) {
+            if (!NextRowGroup(bind, g, l)) {
+                output.SetCardinality(0);
+                return;
             }
         }
+        const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, l.rg.nrows - l.rg_pos);
+        for (idx_t j = 0; j < output.ColumnCount(); ++j) {
+            const column_t id = j < g.out_ids.size() ? g.column_ids[g.out_ids[j]] : j;
+            Vector &vec = output.data[j];
+            if (id == COLUMN_IDENTIFIER_ROW_ID) {
+                int64_t *rid = FlatVector::GetData<int64_t>(vec);
+                for (idx_t i = 0; i < n; ++i)
+                    rid[i] = (int64_t)(l.rg.first_row + (l.rg.sel ? l.rg.sel[l.rg_pos + i] : l.rg_pos + i));
+                continue;
+            }
+            EmitColumn(bind, l, id, vec, n);
+        }
+        idx_t approved = n;
+        if (!g.residual.empty()) {
+            SelectionVector sel(n);
+            for (size_t k = 0; k < g.residual.size() && approved > 0; ++k) {
+                const auto &r = g.residual[k];
+                Vector col(bind.types[r.id]);
+                EmitColumn(bind, l, r.id, col, n);
+                UnifiedVectorFormat vdata;
+                col.ToUnifiedFormat(n, vdata);
+                ColumnSegment::FilterSelection(sel, col, vdata, *r.filter, *l.residual_state[k], n, approved);
+            }
+            if (approved < n) output.Slice(sel, approved);
+        }
+        l.rg_pos += n;
+        output.SetCardinality(approved);
+        if (approved > 0) return;
     }
-    l.rg_pos += n;
-    output.SetCardinality(n);
 }
 
 OperatorPartitionData ReadPartitionData(ClientContext &, TableFunctionGetPartitionInput &input) {

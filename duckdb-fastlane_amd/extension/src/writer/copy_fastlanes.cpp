@@ -125,7 +125,8 @@ idx_t CopyDesiredBatchSize(ClientContext &, FunctionData &bind_p) {
 
 void CopyFinalize(ClientContext &, FunctionData &, GlobalFunctionData &gstate) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
-    if (!g.facade->finalizeFile()) {
+    g.facade->finalizeFile();
+    if (!g.facade->finalizeOk()) {
         const std::string &why = g.facade->lastError();
         throw IOException("Failed to finalize FastLanes file: " + g.file_path + (why.empty() ? std::string() : ": " + why));
     }

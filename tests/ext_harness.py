@@ -196,6 +196,33 @@ class Ext:
             raise ExtError(lib.fls_ext_last_error().decode())
         return rows.value, sec.value
 
+    def facade_read(self, path, max_rows=-1, max_chunks=4096):
+        """ext_fastlane::FastLanesFacade's read API (openFile, getColumnTypes,
+        getColumnNames, readNextChunk(vector<Value>&, idx_t&)) as the
+        reference's intended scanner drives it: (names, types, rows as lists of
+        str/None, rows per readNextChunk call)."""
+        lib = self.lib
+        f = lib.fls_ext_facade_read
+        f.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.c_int,
+                      C.POINTER(C.c_int)]
+        out = C.c_void_p()
+        chunks = (C.c_int64 * max_chunks)()
+        nch = C.c_int()
+        if f(str(path).encode(), max_rows, C.byref(out), chunks, max_chunks, C.byref(nch)) != 0:
+            raise ExtError(lib.fls_ext_last_error().decode())
+        r = out.value
+        try:
+            nc = lib.fls_ext_result_cols(r)
+            names = [lib.fls_ext_result_name(r, c).decode() for c in range(nc)]
+            types = [lib.fls_ext_result_type(r, c).decode() for c in range(nc)]
+            rows = []
+            for i in range(lib.fls_ext_result_rows(r)):
+                rows.append([None if (v := lib.fls_ext_result_value(r, i, c)) is None else v.decode()
+                             for c in range(nc)])
+            return names, types, rows, list(chunks[:min(nch.value, max_chunks)])
+        finally:
+            lib.fls_ext_result_free(r)
+
     def scan_hold(self, fn, path, threads=1):
         """Scan keeping a reference to every chunk until the end, then hash
         them (same checksum as scan_count): (rows, checksum, seconds)."""

@@ -264,3 +264,84 @@ def test_read_fastlanes_delivery_rate_zero_copy(fl, ext, gpu, tmpfile):
         n, sec = ext.scan_rows("read_fastlanes", p, threads=th)
         assert n == 6001215
         print(f"read_fastlanes zero-copy DataChunks SF1, {th} threads: {n / sec / 1e6:.1f} M rows/s")
+
+
+# ---- row a13: the typed facade's read API, and config C1 through DataChunks ----
+def _expected_cells(fl, ref, img, wl, scale, n):
+    """Every value of a generated table as DuckDB renders it (Value::ToString)."""
+    import datetime
+    rf = ref.RefFile(img)
+    epoch = datetime.date(1970, 1, 1)
+    cols = []
+    for c in range(rf.ncols):
+        name, ty, width, sc = rf.column(c)
+        if ty == fl.VARCHAR:
+            if wl == "lineitem_full" and name == "l_comment":
+                cols.append([x.decode() for x in fl.gen_strings(wl, c, 0, n, scale)])
+            else:
+                codes = fl.gen_values(wl, c, 0, n, np.uint32, scale)
+                lut = {}
+                cols.append([lut.setdefault(int(k), fl.gen_dict_string(wl, c, int(k))) for k in codes])
+        elif ty == fl.DATE:
+            v = fl.gen_values(wl, c, 0, n, np.int32, scale)
+            cols.append([(epoch + datetime.timedelta(days=int(x))).isoformat() for x in v])
+        elif ty == fl.DECIMAL:
+            v = fl.gen_values(wl, c, 0, n, np.int64, scale)
+            cols.append([("-" if x < 0 else "") + f"{abs(int(x)) // 10 ** sc}.{abs(int(x)) % 10 ** sc:0{sc}d}"
+                         for x in v])
+        else:
+            cols.append([str(int(x)) for x in fl.gen_values(wl, c, 0, n, fl.NP_DTYPE[ty], scale)])
+    return [list(r) for r in zip(*cols)]
+
+
+def test_facade_read_api_symbol_exported(ext):
+    # the signatures are pinned at compile time (static_asserts in the harness
+    # against the reference's declaration, incl. void finalizeFile())
+    assert hasattr(ext.lib, "fls_ext_facade_read")
+    with pytest.raises(ExtError, match="openFile failed"):
+        ext.facade_read("/nonexistent/x.fls")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl,scale", [("lineitem", 0.02), ("lineitem_full", 0.012)])
+def test_typed_facade_read_api_every_value(fl, ref, ext, gpu, tmpfile, wl, scale):
+    """ext_fastlane::FastLanesFacade::openFile / getColumnTypes / getColumnNames
+    / readNextChunk(vector<Value>&, idx_t&) -- the interface the reference's
+    intended scanner calls (src/scanner/scan_fastlanes.cpp:82-83,126) -- over
+    a multi-row-group lineitem file: every boxed value equals the generator's,
+    chunks hold <= STANDARD_VECTOR_SIZE rows and never straddle a row group."""
+    img = fl.gen_image(wl, scale)
+    p = tmpfile(f"{wl}.fls")
+    img.write(p)
+    n = fl.gen_nrows(wl, scale)
+    assert n > 65536                                       # >= 2 row groups
+    names, types, rows, chunks = ext.facade_read(p)
+    q_names, q_types, _ = ext.query("read_fastlanes", p, limit=0)
+    assert names == q_names and types == q_types           # same schema as the table function binds
+    assert len(rows) == n and sum(chunks) == n
+    assert all(0 < k <= 2048 for k in chunks)
+    bounds = np.cumsum([0] + chunks)
+    assert all(not (b0 < 65536 * g < b1) for b0, b1 in zip(bounds, bounds[1:]) for g in range(1, n // 65536 + 1))
+    want = _expected_cells(fl, ref, img, wl, scale, n)
+    bad = [i for i in range(n) if rows[i] != want[i]]
+    assert not bad, (bad[:3], rows[bad[0]], want[bad[0]])
+
+
+@pytest.mark.gpu
+def test_config_c1_through_read_fastlanes_datachunks(fl, ext, gpu, tmpfile):
+    """BASELINE config C1 (1,000,000 INT32 rows, W=7 FFOR: 16 row groups, the
+    last 16,960 rows) delivered as DuckDB DataChunks by read_fastlanes, every
+    value vs the generator (the C-ABI path is test_gpu_decode.py's)."""
+    img = fl.gen_image("c1")
+    p = tmpfile("c1.fls")
+    img.write(p)
+    names, types, rows = ext.query("read_fastlanes", p)
+    assert len(names) == 1 and types == ["INTEGER"]
+    want = fl.gen_values("c1", 0, 0, 1000000, np.int32)
+    assert len(rows) == 1000000
+    got = np.array([int(r[0]) for r in rows], dtype=np.int64)
+    assert np.array_equal(got, want.astype(np.int64))
+    assert 1000000 - 15 * 65536 == 16960
+    r2, h2, _ = ext.scan_count("read_fastlanes", p)
+    r3, h3, _ = ext.scan_count("read_fastlanes", p, threads=4)   # parallel scan, batch-index order
+    assert r2 == r3 == 1000000 and h2 == h3

@@ -142,11 +142,22 @@ def test_filter_argument_errors(fl, lineitem):
 
 
 def test_read_fastlanes_unsupported_filter_shape(fl, ext, tmpfile):
+    """A shape the engine cannot evaluate (an optional filter inside an OR)
+    used to fail the query with NotImplementedException; it now binds and is
+    applied on the host (the optional branch conservatively true: DuckDB
+    re-checks optional filters above the scan)."""
     p = tmpfile("li.fls")
     fl.gen_image(WL, 0.01).write(p)
-    from ext_harness import ExtError
-    with pytest.raises(ExtError, match="unsupported filter inside OR"):
-        ext.query("read_fastlanes", p, proj=[0], where=[(C_LINE, "OR OPT = 1|= 2")])
+    names, _, rows = ext.query("read_fastlanes", p, proj=[0], limit=0, where=[(C_LINE, "OR OPT = 1|= 2")])
+    assert names == ["l_orderkey"] and rows == []
+
+
+@pytest.mark.gpu
+def test_read_fastlanes_unsupported_filter_shape_rows(fl, ext, gpu, tmpfile):
+    p = tmpfile("li.fls")
+    fl.gen_image(WL, 0.01).write(p)
+    _, _, rows = ext.query("read_fastlanes", p, proj=[0], where=[(C_LINE, "OR OPT = 1|= 2")])
+    assert len(rows) == fl.gen_nrows(WL, 0.01)   # a superset, never fewer rows than the filter keeps
 
 
 # ---------------------------------------------------------------- GPU tests
@@ -310,3 +321,54 @@ def test_gpu_read_fastlanes_where_everything_pruned(fl, gpu, ext, tmpfile):
     n, h, _ = ext.scan_count("read_fastlanes", p, proj=[C_OKEY], where=[(C_MODE, "= SHIP")])
     assert n == int(sum(fl.gen_dict_string(WL, C_MODE, int(k)) == "SHIP"
                         for k in fl.gen_values(WL, C_MODE, 0, fl.gen_nrows(WL, 0.01), np.uint32, 0.01)))
+
+
+# ---- filters the engine cannot evaluate stay correct (host-side residuals) ----
+def test_unknown_filter_evaluated_on_host_without_gpu_is_bind_safe(fl, tmp_path):
+    """Binding a scan with an EXPRESSION_FILTER no longer throws
+    NotImplementedException: the filter is kept for the host."""
+    from ext_harness import Ext
+    p = str(tmp_path / "x.fls")
+    fl.write_image([("a", fl.INT32, np.arange(5000, dtype=np.int32), fl.ENC_FFOR)]).write(p)
+    e = Ext()
+    try:
+        names, types, rows = e.query("read_fastlanes", p, limit=0, where=[(0, "EXPR MOD 7 3")])
+        assert names == ["a"] and rows == []
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 3])
+def test_expression_filter_applied_on_host(fl, gpu, tmp_path, threads):
+    """An EXPRESSION_FILTER (DuckDB pushes these only when asked; a real
+    engine's scan must then honour them) is evaluated on the host over every
+    delivered chunk, AND-ed with the engine's pushed-down predicates, also on
+    a column that is filtered but not projected (filter_prune)."""
+    from ext_harness import Ext
+    n = 3 * 65536 + 777
+    a = np.arange(n, dtype=np.int64) * 3 + 1
+    b = (np.arange(n) % 1000).astype(np.int32)
+    txt = [f"w{i % 97}x" for i in range(n)]
+    p = str(tmp_path / "e.fls")
+    fl.write_image([("a", fl.INT64, a, fl.ENC_DELTA), ("b", fl.INT32, b, fl.ENC_FFOR),
+                    ("t", fl.VARCHAR, txt, fl.ENC_AUTO)]).write(p)
+    e = Ext()
+    try:
+        _, _, rows = e.query("read_fastlanes", p, threads=threads, where=[(0, "EXPR MOD 7 3")])
+        want = [i for i in range(n) if a[i] % 7 == 3]
+        assert [int(r[0]) for r in rows] == [int(a[i]) for i in want]
+        # host residual AND engine predicate, on the filtered-only column b
+        _, _, rows = e.query("read_fastlanes", p, proj=[0], threads=threads,
+                             where=[(0, "EXPR MOD 5 1"), (1, "< 300")])
+        want = [i for i in range(n) if a[i] % 5 == 1 and b[i] < 300]
+        assert [int(r[0]) for r in rows] == [int(a[i]) for i in want]
+        # VARCHAR residual; a filter that rejects every row of some chunks
+        _, _, rows = e.query("read_fastlanes", p, proj=[2, 1], threads=threads, where=[(2, "EXPR LIKE w13x")])
+        want = [i for i in range(n) if txt[i] == "w13x"]
+        assert [r[0] for r in rows] == ["w13x"] * len(want)
+        assert [int(r[1]) for r in rows] == [int(b[i]) for i in want]
+        _, _, rows = e.query("read_fastlanes", p, threads=threads, where=[(1, "EXPR MOD 1000 999999")])
+        assert rows == []
+    finally:
+        e.close()
