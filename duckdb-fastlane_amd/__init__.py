@@ -96,6 +96,7 @@ _sig("fls_version", C.c_char_p)
 _sig("fls_device_count", C.c_int)
 _sig("fls_connect", C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(_P))
 _sig("fls_disconnect", None, _P)
+_sig("fls_connection_trim", C.c_int, _P, C.c_uint64, C.POINTER(C.c_uint64))
 _sig("fls_read_fls", C.c_int, _P, C.c_char_p, C.POINTER(_P))
 _sig("fls_read_fls_image", C.c_int, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P))
 _sig("fls_table_close", None, _P)
@@ -375,6 +376,13 @@ class Connection:
             _check(_lib.fls_connect(None, 0, C.byref(h)))
         self.h = h.value
         self.devices = list(devices) if devices else [0]
+
+    def trim(self, keep_bytes: int = 0) -> int:
+        """Free idle scan pipelines down to keep_bytes of pinned memory per
+        GPU; returns the pinned bytes still idle."""
+        left = C.c_uint64()
+        _check(_lib.fls_connection_trim(self.h, keep_bytes, C.byref(left)))
+        return left.value
 
     def read_fls(self, path: str) -> "Table":
         h = _P()

@@ -19,6 +19,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <memory>
 #include <string>
@@ -360,15 +361,57 @@ struct ScanCtx {
     std::condition_variable cv;
 };
 
+// Pinned bytes a host batch holds (its columns, FSST heaps, selection).
+size_t pinned_bytes(const HostBatch &b) {
+    size_t t = b.h_counts.n * sizeof(uint32_t) + b.h_sel.n * sizeof(uint32_t);
+    for (auto &x : b.h_out) t += x.n;
+    for (auto &x : b.h_heap) t += x.n;
+    return t;
+}
+size_t pinned_bytes(const ScanDev &d) {
+    size_t t = 0;
+    for (auto &b : d.batches) t += pinned_bytes(*b);
+    for (auto &sl : d.slots) t += sl.h_chunks.n * sizeof(DevChunk) + sl.h_stage.n + sl.h_fdesc.n;
+    return t;
+}
+
 // What a connection keeps between scans: idle per-GPU pipelines (at most
-// kIdlePerDev per GPU, each with at most kKeepBatches pinned host batches)
-// and the staging copy threads.  Tables share it by reference, so it lives
-// until the connection and every table opened on it are closed.
+// kIdlePerDev per GPU) and the staging copy threads.  The idle pipelines'
+// pinned host batches are capped by BYTES per GPU (FLS_IDLE_PINNED_MB, default
+// 512; 0 keeps none): a batch is up to 8 row groups of every delivered column,
+// about 150 MB at lineitem_full widths, so a count cap alone let a long-lived
+// process (DuckDB) keep ~1 GB of page-locked memory per GPU.  fls_connection_trim
+// frees the idle pipelines on demand.  Tables share ConnRes by reference, so
+// it lives until the connection and every table opened on it are closed.
 struct ConnRes {
-    static constexpr size_t kIdlePerDev = 2, kKeepBatches = 8;
+    static constexpr size_t kIdlePerDev = 2;
     std::mutex mu;
     std::vector<std::unique_ptr<ScanDev>> idle;
     CopyPool copy;
+    static size_t idle_cap_bytes() {
+        const char *e = getenv("FLS_IDLE_PINNED_MB");
+        return (size_t)(e ? std::max(0L, atol(e)) : 512L) << 20;
+    }
+    // free idle pipelines until the pinned bytes they hold on GPU dev (every
+    // GPU: dev < 0) are at most keep (caller holds mu)
+    void trim_locked(int dev, size_t keep) {
+        std::map<int, size_t> held;
+        for (size_t i = idle.size(); i-- > 0;) {
+            ScanDev &d = *idle[i];
+            if (dev >= 0 && d.dev != dev) continue;
+            // drop batches of this pipeline while over the cap, then the pipeline
+            while (!d.batches.empty() && held[d.dev] + pinned_bytes(d) > keep) {
+                d.batches.pop_back();
+                d.free_batches.clear();
+                for (auto &b : d.batches) d.free_batches.push_back(b.get());
+            }
+            if (held[d.dev] + pinned_bytes(d) > keep) {
+                idle.erase(idle.begin() + (long)i);
+                continue;
+            }
+            held[d.dev] += pinned_bytes(d);
+        }
+    }
     std::unique_ptr<ScanDev> take(int dev) {
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -393,13 +436,22 @@ struct ConnRes {
             sl.busy = sl.starved = false;
             sl.hb = nullptr;
         }
-        while (d->batches.size() > kKeepBatches) d->batches.pop_back();
         d->free_batches.clear();
         for (auto &b : d->batches) d->free_batches.push_back(b.get());
         std::lock_guard<std::mutex> lk(mu);
         size_t same = 0;
         for (auto &x : idle) same += x->dev == d->dev;
-        if (same < kIdlePerDev) idle.push_back(std::move(d));
+        if (same >= kIdlePerDev) return;
+        const int dev = d->dev;
+        idle.push_back(std::move(d));
+        trim_locked(dev, idle_cap_bytes());
+    }
+    // pinned bytes the idle pipelines hold (all GPUs)
+    size_t idle_pinned() {
+        std::lock_guard<std::mutex> lk(mu);
+        size_t t = 0;
+        for (auto &d : idle) t += pinned_bytes(*d);
+        return t;
     }
 };
 
@@ -1449,6 +1501,16 @@ int fls_connect(const int *devices, int ndevices, fls_connection **out) {
 }
 
 void fls_disconnect(fls_connection *conn) { delete conn; }
+
+int fls_connection_trim(fls_connection *conn, uint64_t keep_bytes, uint64_t *idle_bytes) {
+    if (!conn) return fail(FLS_ERR_ARG, "fls_connection_trim: NULL connection");
+    {
+        std::lock_guard<std::mutex> lk(conn->res->mu);
+        conn->res->trim_locked(-1, (size_t)keep_bytes);
+    }
+    if (idle_bytes) *idle_bytes = conn->res->idle_pinned();
+    return 0;
+}
 
 }  // extern "C"
 

@@ -11,6 +11,7 @@
 #include "fastlane_extension.hpp"
 
 #include "duckdb.hpp"
+#include "gpu_devices.hpp"
 #include "scan_fastlanes.hpp"
 #include "table_function/read_fastlanes.hpp"
 #include "writer/copy_fastlanes.hpp"
@@ -24,11 +25,21 @@ void FastlaneVersionFn(DataChunk &, ExpressionState &, Vector &result) {
     result.SetValue(0, StringVector::AddString(result, "FastLanes Extension v1.0.0"));
     result.SetVectorType(VectorType::CONSTANT_VECTOR);
 }
+// SELECT fastlane_release_memory(): not in the reference.  Hands the pinned
+// host memory the GPU scan keeps between queries back to the OS; returns the
+// pinned bytes still held (0).
+void FastlaneReleaseMemoryFn(DataChunk &, ExpressionState &, Vector &result) {
+    const uint64_t left = ext_fastlane::TrimSharedConnections(0);
+    result.SetValue(0, Value::BIGINT((int64_t)left));
+    result.SetVectorType(VectorType::CONSTANT_VECTOR);
+}
 }  // namespace
 
 void FastlaneExtension::Load(DuckDB &db) {
     ExtensionUtil::RegisterFunction(*db.instance,
                                     ScalarFunction("fastlane_version", {}, LogicalType::VARCHAR, FastlaneVersionFn));
+    ExtensionUtil::RegisterFunction(
+        *db.instance, ScalarFunction("fastlane_release_memory", {}, LogicalType::BIGINT, FastlaneReleaseMemoryFn));
     ScanFastLanes::Register(*db.instance);
     ext_fastlane::RegisterReadFastlanes(*db.instance);
     ext_fastlane::RegisterFastlaneCopyFunction(*db.instance);

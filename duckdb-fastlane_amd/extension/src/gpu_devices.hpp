@@ -31,21 +31,45 @@ inline std::vector<int> GpuDevices() {
     return d;
 }
 
-// The engine connection over GpuDevices(), one per device set for the whole
-// process: every file the extension opens shares it, so its per-GPU scan
-// pipelines (streams, device slots, pinned host batches) and staging threads
-// carry over from one query to the next.  Never closed (process lifetime).
+// The engine connections, one per device set for the whole process.
+struct SharedConnections {
+    std::mutex mu;
+    std::map<std::vector<int>, fls_connection *> conns;
+    static SharedConnections &Get() {
+        static auto *s = new SharedConnections();  // process lifetime (tables may outlive static destruction order)
+        return *s;
+    }
+};
+
+// The engine connection over GpuDevices(): every file the extension opens
+// shares it, so its per-GPU scan pipelines (streams, device slots, pinned
+// host batches) and staging threads carry over from one query to the next.
+// The pinned memory idle pipelines keep is capped per GPU by the engine
+// (FLS_IDLE_PINNED_MB) and handed back by TrimSharedConnections (SQL:
+// fastlane_release_memory()).
 inline fls_connection *SharedConnection() {
-    static std::mutex mu;
-    static auto *conns = new std::map<std::vector<int>, fls_connection *>();
+    auto &s = SharedConnections::Get();
     const std::vector<int> devs = GpuDevices();
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = conns->find(devs);
-    if (it != conns->end()) return it->second;
+    std::lock_guard<std::mutex> lk(s.mu);
+    auto it = s.conns.find(devs);
+    if (it != s.conns.end()) return it->second;
     fls_connection *c = nullptr;
     if (fls_connect(devs.data(), (int)devs.size(), &c) != 0) return nullptr;
-    (*conns)[devs] = c;
+    s.conns[devs] = c;
     return c;
+}
+
+// Free the idle scan pipelines of every shared connection down to keep_bytes
+// of pinned memory per GPU; returns the pinned bytes still idle.
+inline uint64_t TrimSharedConnections(uint64_t keep_bytes) {
+    auto &s = SharedConnections::Get();
+    std::lock_guard<std::mutex> lk(s.mu);
+    uint64_t left = 0;
+    for (auto &kv : s.conns) {
+        uint64_t idle = 0;
+        if (fls_connection_trim(kv.second, keep_bytes, &idle) == 0) left += idle;
+    }
+    return left;
 }
 
 }  // namespace ext_fastlane

@@ -124,6 +124,13 @@ int fls_device_memcpy(int device, void *dst, const void *src, uint64_t bytes, in
  * (NULL/0 = device 0). */
 int fls_connect(const int *devices, int ndevices, fls_connection **out);
 void fls_disconnect(fls_connection *conn);
+/* Free the connection's idle scan pipelines (streams, device slots, pinned
+ * host batches kept for the next scan) down to keep_bytes of pinned memory
+ * per GPU (0: all of them); idle_bytes (may be NULL) receives what stays.
+ * Idle pinned memory is also capped per GPU when a scan ends
+ * (FLS_IDLE_PINNED_MB, default 512).  Not in the reference: a long-lived
+ * host (DuckDB) uses it to hand page-locked memory back. */
+int fls_connection_trim(fls_connection *conn, uint64_t keep_bytes, uint64_t *idle_bytes);
 
 /* Connection::read_fls(): parse footer + schema (no GPU work). */
 int fls_read_fls(fls_connection *conn, const char *path, fls_table **out);

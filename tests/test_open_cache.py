@@ -48,3 +48,42 @@ def test_rewritten_file_is_reread_and_revalidated(fl, tmp_path):
     os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000))
     with pytest.raises(Exception):
         _open(fl, p)
+
+
+def test_release_memory_hook_registered(_built):
+    """fastlane_release_memory(): the SQL hook that hands idle pinned memory back."""
+    import sys
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).parent))
+    from ext_harness import Ext
+    e = Ext()
+    try:
+        assert e.scalar0("fastlane_release_memory") == "0"
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_idle_pinned_memory_capped_and_trimmed(fl, gpu, monkeypatch):
+    """A scan's pipeline goes back to the connection when its table closes;
+    the pinned host batches it keeps are capped by bytes per GPU
+    (FLS_IDLE_PINNED_MB) and fls_connection_trim frees them on demand."""
+    import numpy as np
+    img = fl.gen_image("lineitem", 0.2)   # 19 row groups: several 8-row-group batches
+    conn = fl.Connection([0])
+    monkeypatch.setenv("FLS_IDLE_PINNED_MB", "4096")
+    t = conn.read_image(img)
+    nrg = t.nrowgroups
+    rows = sum(1 for _ in t.scan())
+    t.close()
+    big = conn.trim(1 << 62)              # nothing freed, report what is idle
+    assert rows == nrg and big > 64 << 20
+    monkeypatch.setenv("FLS_IDLE_PINNED_MB", "64")
+    t = conn.read_image(img)
+    sum(1 for _ in t.scan())
+    t.close()
+    assert conn.trim(1 << 62) <= 64 << 20   # capped when the scan handed its pipeline back
+    assert conn.trim(0) == 0                # and all of it released on demand
+    t = conn.read_image(img)                # a later scan builds a new pipeline
+    assert sum(1 for _ in t.scan()) == nrg
+    t.close()
+    conn.close()
