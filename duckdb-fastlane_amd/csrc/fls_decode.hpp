@@ -35,6 +35,10 @@ static_assert(sizeof(DevChunk) == 64, "DevChunk is 64 B");
 
 // error flags raised by the kernel (corrupt codes / run indices are clamped)
 enum : uint32_t { KERR_DICT_CODE = 1, KERR_RUN_INDEX = 2, KERR_BAD_DESC = 4, KERR_FSST = 8 };
+// (16: KERR_FILTER_STR, fls_filter.hpp) an FSST kernel built with
+// kFsstAbsLds found its dynamic LDS not at address 0: a build problem, not
+// corrupt data (the launcher checks the kernel's static LDS first)
+enum : uint32_t { KERR_LDS_BASE = 32 };
 
 // Per-launch LDS geometry: per-wave packed staging (>= 128*maxW + 128 bytes)
 // and decoded-vector scratch (path dependent), both multiples of 16; grid = 0

@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(64, SEG ? ((V & kFsstSegDouble) ? 4 : FLS_FSST_SEG_
     // the compiler fold table and ring offsets without adding a symbol base
     if constexpr ((V & kFsstAbsLds) != 0) {
         if ((uint32_t)(size_t)lds_raw_generic != 0u) {
-            if (threadIdx.x == 0) atomicOr(err, KERR_BAD_DESC);
+            if (threadIdx.x == 0) atomicOr(err, KERR_LDS_BASE);
             return;
         }
     }
@@ -1135,6 +1135,21 @@ template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
 hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
     const uint32_t shmem = Lds<BPL, SMALL, SEG>::kWave;
+    if constexpr ((V & kFsstAbsLds) != 0) {
+        // the variant addresses its dynamic LDS from 0, which holds only for a
+        // kernel without static LDS: refuse to launch one that has some
+        static const bool lds_at_zero = [] {
+            hipFuncAttributes a{};
+            return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(fsst_kernel<BPL, SMALL, QUEUE, V, SEG>)) ==
+                       hipSuccess &&
+                   a.sharedSizeBytes == 0;
+        }();
+        if (!lds_at_zero) {
+            fprintf(stderr, "fsst_kernel<%d,%d,%d,%d,%d>: static LDS present or attributes unavailable; the "
+                            "kFsstAbsLds variant cannot run\n", BPL, (int)SMALL, (int)QUEUE, V, SEG);
+            return hipErrorInvalidDeviceFunction;
+        }
+    }
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;

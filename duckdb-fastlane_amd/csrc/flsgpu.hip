@@ -1320,6 +1320,7 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         uint32_t err = 0;
         HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
+        if (err & KERR_LDS_BASE) return fail(FLS_ERR_DEVICE, "FSST kernel: dynamic LDS not at address 0 (flags 0x%x)", err);
         if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
         return 0;
     };
@@ -1929,6 +1930,7 @@ int fls_device_sync(fls_table *t, fls_decode_stats *stats) {
         stats->launches = t->launches;
     }
     for (auto &r : t->resident) r->ev_used = 0;
+    if (err & KERR_LDS_BASE) return fail(FLS_ERR_DEVICE, "FSST kernel: dynamic LDS not at address 0 (flags 0x%x)", err);
     if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
     return 0;
 }

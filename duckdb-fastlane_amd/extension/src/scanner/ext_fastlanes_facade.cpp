@@ -95,6 +95,12 @@ public:
     // every (row group, column) chunk in parallel, so a row group's slowest
     // column does not idle the writer's other threads
     idx_t batch_rgs = 8;
+    // Bytes all sink stages together may buffer (FLS_COPY_STAGED_MB, default
+    // 1024): past it, a stage hands its row groups over at its next row-group
+    // boundary, so an unordered COPY on many threads stays within the budget
+    // plus one row group per stage instead of batch_rgs row groups per thread.
+    uint64_t staged_budget = 1ull << 30;
+    std::atomic<uint64_t> staged{0}, staged_peak{0};  // bytes buffered by all stages (account)
     // Batches handed to the writer: each is a background task that assembles
     // its VARCHAR columns, waits for the previous batch's writer call (the
     // writer appends row groups in call order) and then calls the writer.  Up
@@ -103,7 +109,8 @@ public:
     // recycled through `spare`.
     struct Batch {
         std::vector<RawBuf> cols, rec, arena;
-        std::vector<std::vector<uint32_t>> offs;
+        std::vector<std::vector<uint32_t>> offs;  // per row group k: rows_k + 1 offsets from k * (rg_rows + 1)
+        std::vector<std::vector<uint64_t>> base;  // per row group: its first byte in cols[c]
     };
     static constexpr size_t kMaxInflight = 3;
     std::deque<std::shared_future<std::string>> inflight;  // "" or the writer's error (fls_last_error is per thread)
@@ -111,14 +118,15 @@ public:
     std::mutex spare_mu;
     CopyProfile prof;
     double encode_s = 0;  // background writer calls (one at a time: the tasks are chained)
-    // wait until at most `keep` batches are in flight; false if one failed
-    bool wait_pending(size_t keep = 0) {
+    // wait until at most `keep` batches are in flight, the time into *wait
+    // (a profiled stage's own counter); false if one failed
+    bool wait_pending(size_t keep = 0, double *wait = nullptr) {
         bool ok = true;
         while (inflight.size() > keep) {
-            const double t0 = prof.on ? CopyProfile::now() : 0;
+            const double t0 = wait ? CopyProfile::now() : 0;
             const std::string e = inflight.front().get();
             inflight.pop_front();
-            if (prof.on) prof.wait += CopyProfile::now() - t0;
+            if (wait) *wait += CopyProfile::now() - t0;
             if (!e.empty()) {
                 error = "FastLanes writer: " + e;
                 ok = false;
@@ -135,8 +143,10 @@ public:
         rg_pos = 0;
     }
     bool flush_stage(Stage &st);
-    bool stage_chunk(Stage &st, DataChunk &chunk, bool profile);
-    bool stage_full(const Stage &st) const;
+    bool stage_chunk(Stage &st, DataChunk &chunk);
+    bool stage_full(Stage &st);
+    static uint64_t staged_bytes(const Stage &st);
+    void account(Stage &st);
     void reset_stage(Stage &st) const;
     ~Impl();
 };
@@ -150,9 +160,16 @@ public:
     // pointer field it rewrites to their offset in warena; the background
     // task turns them into the writer's bytes + offsets, a thread per column
     std::vector<RawBuf> wrec, warena;
-    std::vector<uint64_t> wbytes;  // string bytes per VARCHAR column in the batch
+    // string bytes per VARCHAR column in the stage's last (partial) row group:
+    // the writer's offsets are 32-bit per row group
+    std::vector<uint64_t> wbytes;
     idx_t wrows = 0;
     std::string error;
+    uint64_t accounted = 0;  // this stage's bytes in Impl::staged
+    // FLS_COPY_PROFILE times one stage (the first handed out, or the serial
+    // path's): only its thread writes prof, and its writer waits count here
+    bool profile = false;
+    double wait = 0;
 };
 
 void FastLanesFacade::StageDeleter::operator()(Stage *st) const { delete st; }
@@ -173,14 +190,29 @@ void FastLanesFacade::Impl::reset_stage(Stage &st) const {
     st.wrows = 0;
 }
 
-// at a row-group boundary: a full batch, or a VARCHAR buffer nearing the
-// offsets' 32-bit range, goes to the writer
-bool FastLanesFacade::Impl::stage_full(const Stage &st) const {
+uint64_t FastLanesFacade::Impl::staged_bytes(const Stage &st) {
+    uint64_t bytes = 0;
+    for (auto *b : {&st.wcols, &st.wrec, &st.warena})
+        for (auto &x : *b) bytes += x.size();
+    return bytes;
+}
+
+// bring the stages' byte total up to date with this stage's buffers
+void FastLanesFacade::Impl::account(Stage &st) {
+    const uint64_t now = staged_bytes(st);
+    const uint64_t total = staged.fetch_add(now - st.accounted) + (now - st.accounted);  // mod 2^64
+    st.accounted = now;
+    uint64_t peak = staged_peak.load();
+    while (total > peak && !staged_peak.compare_exchange_weak(peak, total)) {
+    }
+}
+
+// at a row-group boundary: a full batch, or any stage's rows while all stages
+// together are over the staged-bytes budget, go to the writer
+bool FastLanesFacade::Impl::stage_full(Stage &st) {
+    account(st);
     if (st.wrows == 0 || st.wrows % rg_rows) return false;
-    bool big = false;
-    for (size_t c = 0; c < wtypes.size(); ++c)
-        big |= st.wbytes[c] > (1ull << 30);
-    return st.wrows == rg_rows * batch_rgs || big;
+    return st.wrows >= rg_rows * batch_rgs || staged.load() > staged_budget;
 }
 
 FastLanesFacade::FastLanesFacade() : pImpl(new Impl()) {}
@@ -297,7 +329,11 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.wnames = names;
     if (!s.own) s.own = new Stage();
     s.reset_stage(*s.own);
+    s.own->accounted = 0;
+    s.staged = 0;
+    s.staged_peak = 0;
     if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
+    if (const char *b = std::getenv("FLS_COPY_STAGED_MB")) s.staged_budget = (uint64_t)std::max(1, std::atoi(b)) << 20;
     return true;
 }
 
@@ -307,7 +343,7 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
 bool FastLanesFacade::Impl::flush_stage(Stage &st) {
     if (st.wrows == 0) return true;
     std::lock_guard<std::mutex> guard(hand);
-    if (!wait_pending(kMaxInflight - 1)) {
+    if (!wait_pending(kMaxInflight - 1, st.profile ? &st.wait : nullptr)) {
         st.error = error;
         return false;
     }
@@ -323,11 +359,13 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
     Batch *b = bp.release();
     for (auto *x : {&b->cols, &b->rec, &b->arena}) x->resize(wtypes.size());
     b->offs.resize(wtypes.size());
+    b->base.resize(wtypes.size());
     std::swap(b->cols, st.wcols);
     std::swap(b->rec, st.wrec);
     std::swap(b->arena, st.warena);
     const uint32_t rows = (uint32_t)st.wrows;
     reset_stage(st);
+    account(st);
     std::shared_future<std::string> prev = inflight.empty() ? std::shared_future<std::string>() : inflight.back();
     inflight.push_back(std::async(std::launch::async, [this, rows, b, prev]() {
         std::unique_ptr<Batch> own_b(b);
@@ -335,24 +373,37 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
             std::lock_guard<std::mutex> g(spare_mu);
             spare.push_back(std::move(own_b));
         };
-        // VARCHAR columns: string_t records -> bytes + offsets (a thread per column)
-        auto assemble = [this, rows, b](size_t c) {
+        const uint32_t nrg = (uint32_t)((rows + rg_rows - 1) / rg_rows);
+        // VARCHAR columns: string_t records -> bytes + offsets, the offsets
+        // restarting at 0 in each row group (the sink keeps a row group's
+        // strings under 4 GiB); a thread per column
+        auto assemble = [this, rows, nrg, b](size_t c) {
             const uint8_t *rec = b->rec[c].data();
             std::vector<uint32_t> &o = b->offs[c];
-            o.resize((size_t)rows + 1);
-            o[0] = 0;
-            for (uint32_t r = 0; r < rows; ++r) {
-                uint32_t len;
-                memcpy(&len, rec + 16ull * r, 4);
-                o[r + 1] = o[r] + len;
+            std::vector<uint64_t> &base = b->base[c];
+            o.resize((size_t)rows + nrg);
+            base.resize(nrg);
+            uint64_t total = 0;
+            for (uint32_t k = 0; k < nrg; ++k) {
+                const idx_t r0 = (idx_t)k * rg_rows, n = std::min<idx_t>(rg_rows, rows - r0);
+                uint32_t *ok = o.data() + (size_t)k * (rg_rows + 1);
+                ok[0] = 0;
+                for (idx_t i = 0; i < n; ++i) {
+                    uint32_t len;
+                    memcpy(&len, rec + 16ull * (r0 + i), 4);
+                    ok[i + 1] = ok[i] + len;
+                }
+                base[k] = total;
+                total += ok[n];
             }
             RawBuf &col = b->cols[c];
             col.clear();
-            uint8_t *dst = col.grow((size_t)o[rows] + string_t::INLINE_LENGTH);
+            uint8_t *dst = col.grow((size_t)total + string_t::INLINE_LENGTH);
             col.shrink(string_t::INLINE_LENGTH);
             for (uint32_t r = 0; r < rows; ++r) {
                 const uint8_t *x = rec + 16ull * r;
-                const uint32_t len = o[r + 1] - o[r];
+                uint32_t len;
+                memcpy(&len, x, 4);
                 if (len <= string_t::INLINE_LENGTH) {
                     memcpy(dst, x + 4, string_t::INLINE_LENGTH);
                 } else {
@@ -377,10 +428,8 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
         }
         const double t0 = prof.on ? CopyProfile::now() : 0;
         // row group k of the batch: fixed-width columns at row k * rg_rows,
-        // VARCHAR columns through their offsets from k * rg_rows (offsets are
-        // into the column's whole byte buffer)
+        // VARCHAR columns at their row group's first byte, with its offsets
         const size_t nc = wtypes.size();
-        const uint32_t nrg = (uint32_t)((rows + rg_rows - 1) / rg_rows);
         std::vector<uint32_t> nrows(nrg);
         std::vector<const void *> data((size_t)nrg * nc);
         std::vector<const uint32_t *> offs((size_t)nrg * nc, nullptr);
@@ -389,8 +438,8 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
             nrows[k] = (uint32_t)std::min<idx_t>(rg_rows, rows - r0);
             for (size_t c = 0; c < nc; ++c) {
                 if (wtypes[c].id() == LogicalTypeId::VARCHAR) {
-                    data[k * nc + c] = b->cols[c].empty() ? (const void *)"" : b->cols[c].data();
-                    offs[k * nc + c] = b->offs[c].data() + r0;
+                    data[k * nc + c] = b->cols[c].empty() ? (const void *)"" : b->cols[c].data() + b->base[c][k];
+                    offs[k * nc + c] = b->offs[c].data() + (size_t)k * (rg_rows + 1);
                 } else {
                     const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(wtypes[c]));
                     data[k * nc + c] = b->cols[c].data() + r0 * w;
@@ -412,19 +461,20 @@ static idx_t PhysicalWidth(const LogicalType &t) {
     return TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
 }
 
-// Copy a DataChunk into a stage; a full batch goes to the writer.  profile:
-// account the time in prof (the serial path only: prof is not thread-safe).
-bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk, bool profile) {
+// Copy a DataChunk into a stage; a full batch goes to the writer (a
+// profiled stage accounts its time in prof).
+bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
     Impl &s = *this;
+    const bool profile = st.profile;
     const double t_in = profile ? CopyProfile::now() : 0;
     struct Tally {  // sink time of this call, less its waits for the writer
         Impl &s;
-        bool on;
+        const Stage &st;
         double t_in, w_in;
         ~Tally() {
-            if (on) s.prof.sink += CopyProfile::now() - t_in - (s.prof.wait - w_in);
+            if (st.profile) s.prof.sink += CopyProfile::now() - t_in - (st.wait - w_in);
         }
-    } tally{s, profile, t_in, s.prof.wait};
+    } tally{s, st, t_in, st.wait};
     if (!s.writer || chunk.ColumnCount() != s.wtypes.size()) return false;
     double tp = t_in;
     auto lap = [&](double &acc) {  // profile: time since the last lap into acc
@@ -503,6 +553,7 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk, bool profil
         }
         st.wrows += n;
         r0 += n;
+        if (st.wrows % s.rg_rows == 0) st.wbytes.assign(s.wtypes.size(), 0);
         if (s.stage_full(st) && !s.flush_stage(st)) return false;
     }
     return true;
@@ -511,7 +562,8 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk, bool profil
 bool FastLanesFacade::writeChunk(DataChunk &chunk) {
     Impl &s = *pImpl;
     if (!s.own) return false;
-    const bool ok = s.stage_chunk(*s.own, chunk, s.prof.on);
+    s.own->profile = s.prof.on;
+    const bool ok = s.stage_chunk(*s.own, chunk);
     if (!ok) s.error = s.own->error;
     return ok;
 }
@@ -520,13 +572,14 @@ FastLanesFacade::StagePtr FastLanesFacade::newStage() {
     Impl &s = *pImpl;
     StagePtr st(new Stage());
     s.reset_stage(*st);
-    s.nstages.fetch_add(1);
+    st->profile = s.prof.on && s.nstages.fetch_add(1) == 0;
+    if (!s.prof.on) s.nstages.fetch_add(1);
     return st;
 }
 
 bool FastLanesFacade::writeChunk(Stage &stage, DataChunk &chunk) {
     Impl &s = *pImpl;
-    return s.stage_chunk(stage, chunk, s.prof.on && s.nstages.load() == 1);
+    return s.stage_chunk(stage, chunk);
 }
 
 const std::string &FastLanesFacade::stageError(const Stage &stage) const { return stage.error; }
@@ -538,6 +591,10 @@ bool FastLanesFacade::mergeStage(Stage &st) {
     Impl &s = *pImpl;
     if (!s.writer || !s.own) return false;
     std::lock_guard<std::mutex> guard(s.merge);
+    if (st.profile) {
+        s.prof.wait += st.wait;
+        st.wait = 0;
+    }
     Stage &o = *s.own;
     if (o.wrows == 0) {  // nothing to append to (the only sink of an ordered COPY): take the buffers
         std::swap(o.wcols, st.wcols);
@@ -545,6 +602,7 @@ bool FastLanesFacade::mergeStage(Stage &st) {
         std::swap(o.warena, st.warena);
         std::swap(o.wbytes, st.wbytes);
         std::swap(o.wrows, st.wrows);
+        std::swap(o.accounted, st.accounted);
         s.reset_stage(st);
         if (s.stage_full(o) && !s.flush_stage(o)) {
             st.error = o.error;
@@ -585,12 +643,14 @@ bool FastLanesFacade::mergeStage(Stage &st) {
         }
         o.wrows += n;
         r0 += n;
+        if (o.wrows % s.rg_rows == 0) o.wbytes.assign(nc, 0);
         if (s.stage_full(o) && !s.flush_stage(o)) {
             st.error = o.error;
             return false;
         }
     }
     s.reset_stage(st);
+    s.account(st);
     return true;
 }
 
@@ -610,7 +670,8 @@ void FastLanesFacade::finalizeFile() {
     }
     bool ok = s.own && s.flush_stage(*s.own);
     if (!ok && s.own) s.error = s.own->error;
-    ok = s.wait_pending() && ok;
+    double final_wait = 0;
+    ok = s.wait_pending(0, s.prof.on ? &final_wait : nullptr) && ok;
     const double t0 = s.prof.on ? CopyProfile::now() : 0;
     if (ok && fls_writer_finish_file(s.writer, s.out_path.c_str()) != 0) {
         s.error = std::string("FastLanes writer: ") + fls_last_error();
@@ -618,11 +679,13 @@ void FastLanesFacade::finalizeFile() {
     }
     if (s.prof.on) {
         s.prof.finish += CopyProfile::now() - t0;
+        s.prof.wait += s.own->wait + final_wait;  // + the profiled stage's (mergeStage)
         fprintf(stderr,
                 "COPY sink profile: DataChunk copies %.3f s (flatten + validity %.3f, fixed-width %.3f, VARCHAR %.3f), "
                 "waits for the writer %.3f s, string assembly + writer calls %.3f s (background), file assembly + "
-                "write %.3f s\n",
-                s.prof.sink, s.prof.prep, s.prof.fixed, s.prof.str, s.prof.wait, s.encode_s, s.prof.finish);
+                "write %.3f s; peak staged %llu bytes\n",
+                s.prof.sink, s.prof.prep, s.prof.fixed, s.prof.str, s.prof.wait, s.encode_s, s.prof.finish,
+                (unsigned long long)s.staged_peak.load());
     }
     fls_writer_free(s.writer);
     s.writer = nullptr;

@@ -8,6 +8,8 @@ combine, finalize).  CPU tests: registration and option errors (they fail at
 bind, before any scan).  GPU tests: COPY (SELECT ... FROM read_fastlanes(src))
 round trips, checked with the oracle on the written file and against the
 workload generators."""
+import re
+
 import numpy as np
 import pytest
 
@@ -176,6 +178,39 @@ def test_copy_parallel_sinks_cpu(ext, ref, tmpfile, monkeypatch, threads, batch)
     if threads == 1:
         assert got_a == a and got_s == [x.encode() for x in s]
     assert sorted(zip(got_a, got_s)) == sorted(zip(a, (x.encode() for x in s)))
+
+
+@pytest.mark.parametrize("budget_mb", [None, "1"])
+def test_copy_many_sinks_bounded_staging_cpu(ext, ref, tmpfile, monkeypatch, capfd, budget_mb):
+    """36 sink threads each buffering up to FLS_COPY_BATCH = 8 row groups
+    would stage ~9 MB here; past FLS_COPY_STAGED_MB (all stages together) a
+    stage hands its rows over at its next row-group boundary, so the peak
+    stays within the budget plus one row group per stage.  Every row arrives
+    exactly once either way."""
+    monkeypatch.setenv("FLS_COPY_PROFILE", "1")
+    if budget_mb:
+        monkeypatch.setenv("FLS_COPY_STAGED_MB", budget_mb)
+    else:
+        monkeypatch.delenv("FLS_COPY_STAGED_MB", raising=False)
+    rg, threads = 1024, 36
+    n = threads * 8 * rg + 77
+    a = [(i * 104729) % 1000003 for i in range(n)]
+    s = [f"q{i % 13}" * (i % 9) for i in range(n)]  # 0..27 bytes: inlined and arena strings
+    dst = tmpfile(f"many_{budget_mb}.fls")
+    capfd.readouterr()
+    assert ext.copy_values([("a", "BIGINT", a), ("s", "VARCHAR", s)], dst, threads=threads,
+                           row_group_size=rg) == n
+    err = capfd.readouterr().err
+    m = re.search(r"peak staged (\d+) bytes", err)
+    assert m, err
+    peak = int(m.group(1))
+    rg_bytes = rg * (8 + 16) + max(sum(len(x) for x in s[k:k + rg] if len(x) > 12) for k in range(0, n, rg))
+    if budget_mb:
+        assert peak <= (int(budget_mb) << 20) + threads * rg_bytes
+    rf = ref.RefFile(open(dst, "rb").read())
+    assert rf.nrows == n
+    got_a = np.concatenate([rf.decode(0, g) for g in range(rf.nrowgroups)]).view(np.int64).tolist()
+    assert sorted(zip(got_a, rf.strings_column(1))) == sorted(zip(a, (x.encode() for x in s)))
 
 
 def test_copy_parallel_sinks_refuse_nulls_cpu(ext, tmpfile):
