@@ -27,15 +27,17 @@ _lib = C.CDLL(str(LIB_PATH))
 
 # --- enums (include/flswriter.h) -------------------------------------------
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64 = 1, 2, 3, 4, 5, 6, 7, 8
-DATE, DECIMAL, FLOAT, DOUBLE, VARCHAR = 10, 11, 12, 13, 20
+BOOLEAN, DATE, DECIMAL, FLOAT, DOUBLE, VARCHAR, BLOB = 9, 10, 11, 12, 13, 20, 21
+STRING_TYPES = (VARCHAR, BLOB)
 ENC_AUTO, ENC_FFOR, ENC_DELTA, ENC_DICT, ENC_RLE, ENC_ALP, ENC_FSST = 0, 1, 2, 3, 4, 5, 7
 
 NP_DTYPE = {INT8: np.int8, INT16: np.int16, INT32: np.int32, INT64: np.int64,
             UINT8: np.uint8, UINT16: np.uint16, UINT32: np.uint32, UINT64: np.uint64,
-            DATE: np.int32, DECIMAL: np.int64, FLOAT: np.float32, DOUBLE: np.float64}
+            BOOLEAN: np.uint8, DATE: np.int32, DECIMAL: np.int64, FLOAT: np.float32, DOUBLE: np.float64}
 TYPE_NAMES = {INT8: "TINYINT", INT16: "SMALLINT", INT32: "INTEGER", INT64: "BIGINT",
               UINT8: "UTINYINT", UINT16: "USMALLINT", UINT32: "UINTEGER", UINT64: "UBIGINT",
-              DATE: "DATE", DECIMAL: "DECIMAL", FLOAT: "FLOAT", DOUBLE: "DOUBLE", VARCHAR: "VARCHAR"}
+              DATE: "DATE", DECIMAL: "DECIMAL", FLOAT: "FLOAT", DOUBLE: "DOUBLE", VARCHAR: "VARCHAR",
+              BOOLEAN: "BOOLEAN", BLOB: "BLOB"}
 ROWGROUP = 65536
 
 
@@ -266,7 +268,7 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
             name, ty, vals, enc = spec[:4]
             width, scale = (spec[4], spec[5]) if len(spec) > 4 else (0, 0)
             _check(_lib.fls_writer_add_column(w, name.encode(), ty, width, scale, enc))
-            if ty == VARCHAR:
+            if ty in STRING_TYPES:
                 bs = [v.encode() if isinstance(v, str) else bytes(v) for v in vals]
                 prepped.append(("s", bs))
                 cnt = len(bs)
@@ -508,7 +510,7 @@ class Table:
             ty = sch[col][1] if 0 <= col < len(sch) else None
             if val is None or ty is None:
                 pass
-            elif ty == VARCHAR:
+            elif ty in STRING_TYPES:
                 b = val.encode() if isinstance(val, str) else bytes(val)
                 buf = C.create_string_buffer(b, len(b) + 1)
                 keep.append(buf)

@@ -762,7 +762,7 @@ uint64_t fls_encode_slot_bytes(uint8_t type, uint8_t encoding, uint32_t rowgroup
 int fls_encode_device(int device, uint8_t type, uint8_t encoding, const void *d_values, uint64_t nrows,
                       uint32_t rowgroup_rows, void *d_out, uint64_t *chunk_lens, float *kernel_ms) {
     const int T = type_value_bits(type);
-    if (T == 0 || type_is_float(type) || type == TY_VARCHAR)
+    if (T == 0 || type_is_float(type) || type_is_string(type))
         return fail(FLS_ERR_ARG, "fls_encode_device: integer types only (type %u)", type);
     if (encoding != ENC_FFOR && encoding != ENC_DELTA)
         return fail(FLS_ERR_ARG, "fls_encode_device: FFOR or DELTA only (encoding %u)", encoding);

@@ -39,16 +39,18 @@ enum Encoding : uint8_t {
 enum TypeId : uint8_t {
     TY_INT8 = 1, TY_INT16 = 2, TY_INT32 = 3, TY_INT64 = 4,
     TY_UINT8 = 5, TY_UINT16 = 6, TY_UINT32 = 7, TY_UINT64 = 8,
+    TY_BOOLEAN = 9,   // u8 0 / 1 (DuckDB bool), FFOR-packed like UINT8 (W <= 1)
     TY_DATE = 10,     // int32 days since 1970-01-01 (DuckDB date_t)
     TY_DECIMAL = 11,  // int64 scaled integer (DuckDB DECIMAL(w<=18, s))
     TY_FLOAT = 12,    // IEEE binary32 (FastLanes flt_col_t)
     TY_DOUBLE = 13,   // IEEE binary64 (FastLanes dbl_col_t)
     TY_VARCHAR = 20,  // DICT or FSST strings, decoded to DuckDB string_t (16 B)
+    TY_BLOB = 21,     // byte strings: VARCHAR's layout and encodings (DuckDB BLOB)
 };
 
 inline int type_value_bits(uint8_t t) {
     switch (t) {
-    case TY_INT8: case TY_UINT8: return 8;
+    case TY_INT8: case TY_UINT8: case TY_BOOLEAN: return 8;
     case TY_INT16: case TY_UINT16: return 16;
     case TY_INT32: case TY_UINT32: case TY_DATE: case TY_FLOAT: return 32;
     case TY_INT64: case TY_UINT64: case TY_DECIMAL: case TY_DOUBLE: return 64;
@@ -56,8 +58,9 @@ inline int type_value_bits(uint8_t t) {
     }
 }
 inline bool type_is_float(uint8_t t) { return t == TY_FLOAT || t == TY_DOUBLE; }
+inline bool type_is_string(uint8_t t) { return t == TY_VARCHAR || t == TY_BLOB; }
 // bytes per decoded value in the output column (string_t = 16 B)
-inline int type_out_bytes(uint8_t t) { return t == TY_VARCHAR ? 16 : type_value_bits(t) / 8; }
+inline int type_out_bytes(uint8_t t) { return type_is_string(t) ? 16 : type_value_bits(t) / 8; }
 inline bool type_valid(uint8_t t) { return type_out_bytes(t) > 0; }
 
 struct ChunkHeader {          // 64 B, at the start of every column chunk

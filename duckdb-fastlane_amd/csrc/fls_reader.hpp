@@ -54,7 +54,7 @@ inline const char *validate_chunk(const uint8_t *img, const FileMeta &m, uint32_
     if (h.T != 8 && h.T != 16 && h.T != 32 && h.T != 64) return "bad packing width";
     if ((h.enc < ENC_FFOR || h.enc > ENC_ALP) && h.enc != ENC_FSST) return "bad encoding";
     const uint8_t ty = m.cols[c].type;
-    const bool is_str = ty == TY_VARCHAR;
+    const bool is_str = type_is_string(ty);
     if ((bool)h.is_str != is_str) return "chunk/column type mismatch";
     if (is_str ? (h.enc != ENC_DICT && h.enc != ENC_FSST) : h.vbits != type_value_bits(ty))
         return "chunk/column type mismatch";
@@ -228,7 +228,7 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
             z.resize(ncols);
             rd(p + 8 + (uint64_t)r * ncols * sizeof(ZoneMap), z.data(), ncols * sizeof(ZoneMap));
             for (uint32_t c = 0; c < ncols; ++c)
-                if (m.cols[c].type == TY_VARCHAR) z[c].flags = 0;
+                if (type_is_string(m.cols[c].type)) z[c].flags = 0;
         }
     }
     return "";

@@ -1161,7 +1161,7 @@ std::vector<uint8_t> encode_gen_chunk(const Workload &w, int c, const std::vecto
         gen_comments(w, vals[0], n, offs, bytes);
         return enc_fsst(offs.data(), bytes.data(), n);
     }
-    if (cs.type == TY_VARCHAR) {
+    if (type_is_string(cs.type)) {
         std::vector<std::string_view> d;
         gen_dict(w, c, d);
         std::vector<uint32_t> codes(vals.begin(), vals.end());
@@ -1566,14 +1566,14 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
     if (!w || !name) return fail(FLS_ERR_ARG, "fls_writer_add_column: NULL argument");
     if (!type_valid(type)) return fail(FLS_ERR_ARG, "fls_writer_add_column: unsupported type %u", type);
     if (encoding > ENC_FSST || encoding == 6) return fail(FLS_ERR_ARG, "fls_writer_add_column: bad encoding %u", encoding);
-    if (type == TY_VARCHAR && encoding != ENC_AUTO && encoding != ENC_DICT && encoding != ENC_FSST)
-        return fail(FLS_ERR_ARG, "fls_writer_add_column: VARCHAR supports DICT and FSST");
+    if (type_is_string(type) && encoding != ENC_AUTO && encoding != ENC_DICT && encoding != ENC_FSST)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: VARCHAR/BLOB support DICT and FSST");
     if (type_is_float(type) && encoding != ENC_AUTO && encoding != ENC_ALP)
         return fail(FLS_ERR_ARG, "fls_writer_add_column: FLOAT/DOUBLE support ALP");
     if (!type_is_float(type) && encoding == ENC_ALP)
         return fail(FLS_ERR_ARG, "fls_writer_add_column: ALP needs FLOAT/DOUBLE");
-    if (type != TY_VARCHAR && encoding == ENC_FSST)
-        return fail(FLS_ERR_ARG, "fls_writer_add_column: FSST needs VARCHAR");
+    if (!type_is_string(type) && encoding == ENC_FSST)
+        return fail(FLS_ERR_ARG, "fls_writer_add_column: FSST needs VARCHAR/BLOB");
     if (!w->fb.rgs.empty()) return fail(FLS_ERR_STATE, "fls_writer_add_column: after first row group");
     if (strlen(name) > 65535) return fail(FLS_ERR_ARG, "column name too long");
     w->fb.cols.push_back(ColSpec{name, type, width, scale, encoding});
@@ -1613,11 +1613,17 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
             if (!a[k].data[c]) return fail(FLS_ERR_ARG, "column %zu: NULL data", c);
-            if (cs.type == TY_VARCHAR) {
+            if (type_is_string(cs.type)) {
                 if (!a[k].offs || !a[k].offs[c]) return fail(FLS_ERR_ARG, "column %zu: VARCHAR needs offsets", c);
                 const uint32_t *o = a[k].offs[c];
                 for (uint32_t i = 0; i < nrows; ++i)
                     if (o[i + 1] < o[i]) return fail(FLS_ERR_ARG, "column %zu: offsets not monotone", c);
+            }
+            if (cs.type == TY_BOOLEAN) {  // DuckDB's bool bytes: 0 or 1
+                const uint8_t *b = (const uint8_t *)a[k].data[c];
+                uint8_t any = 0;
+                for (uint32_t i = 0; i < nrows; ++i) any |= b[i];
+                if (any > 1) return fail(FLS_ERR_ARG, "column %zu: BOOLEAN bytes must be 0 or 1", c);
             }
         }
     }
@@ -1626,7 +1632,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     if (w->gpu.dev >= 0)
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
-            if (cs.type != TY_VARCHAR && !type_is_float(cs.type) &&
+            if (!type_is_string(cs.type) && !type_is_float(cs.type) &&
                 (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO))
                 gcols.push_back(c);
         }
@@ -1645,7 +1651,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         const ColSpec &cs = w->fb.cols[c];
         const uint32_t nrows = p.in->nrows;
         const void *data = p.in->data[c];
-        if (cs.type == TY_VARCHAR) {
+        if (type_is_string(cs.type)) {
             p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows);
             return;
         }
@@ -1678,7 +1684,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         for (int pass = 0; pass < 2; ++pass)
             for (uint32_t k = 0; k < seg.size(); ++k)
                 for (uint32_t c = 0; c < ncols; ++c)
-                    if ((w->fb.cols[c].type == TY_VARCHAR) == (pass == 0)) tasks.emplace_back(k, c);
+                    if ((type_is_string(w->fb.cols[c].type)) == (pass == 0)) tasks.emplace_back(k, c);
         w->pool.run(tasks.size(), [&](size_t t) { encode_col(seg[tasks[t].first], tasks[t].second); });
         for (Pending &p : seg) w->fb.rgs.push_back(std::move(p.rg));
         seg.clear();
@@ -1850,7 +1856,7 @@ int fls_gen_values(const char *workload, double scale, uint64_t nrows, int col, 
     if (col < 0 || col >= (int)w.cols.size() || !out) return fail(FLS_ERR_ARG, "bad column %d", col);
     if (col == w.comment_col) return fail(FLS_ERR_ARG, "column %d holds strings: use fls_gen_strings", col);
     if (row_begin + n > w.nrows) return fail(FLS_ERR_ARG, "rows out of range");
-    const int vb = w.cols[col].type == TY_VARCHAR ? 4 : type_value_bits(w.cols[col].type) / 8;
+    const int vb = type_is_string(w.cols[col].type) ? 4 : type_value_bits(w.cols[col].type) / 8;
     std::vector<std::vector<uint64_t>> vals;
     uint8_t *o = (uint8_t *)out;
     for (uint64_t r = 0; r < n;) {
@@ -1866,7 +1872,7 @@ int64_t fls_gen_strings(const char *workload, double scale, uint64_t nrows, int 
                         uint32_t *offs, char *bytes, uint64_t cap) {
     Workload w;
     if (!make_workload(workload, scale, nrows, w)) return fail(FLS_ERR_ARG, "unknown workload '%s'", workload ? workload : "(null)");
-    if (col < 0 || col >= (int)w.cols.size() || w.cols[col].type != TY_VARCHAR || !offs)
+    if (col < 0 || col >= (int)w.cols.size() || !type_is_string(w.cols[col].type) || !offs)
         return fail(FLS_ERR_ARG, "column %d is not a VARCHAR column", col);
     if (row_begin + n > w.nrows) return fail(FLS_ERR_ARG, "rows out of range");
     uint64_t o = 0;

@@ -568,7 +568,7 @@ int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBu
     std::vector<StrT> host;
     for (uint32_t r = rg0; r < rg1; ++r)
         for (uint32_t c = 0; c < ncols; ++c) {
-            if (t->meta.cols[c].type != TY_VARCHAR) continue;
+            if (!type_is_string(t->meta.cols[c].type)) continue;
             const ChunkRef &ch = t->meta.rgs[r].chunks[c];
             if (ch.hdr.enc != ENC_DICT) continue;  // FSST strings are decoded on the GPU
             const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
@@ -1407,7 +1407,7 @@ int to_terms(const fls_table *t, const fls_predicate *p, uint32_t n, std::vector
         h.clause = p[i].clause;
         h.op = p[i].op;
         const uint8_t ty = t->meta.cols[h.col].type;
-        if (ty == TY_VARCHAR) {
+        if (type_is_string(ty)) {
             h.kind = FK_STR;
             if (p[i].str_len && !p[i].str) return fail(FLS_ERR_ARG, "filter on column %u: NULL string", h.col);
             if (p[i].str_len > 0xFFFFFFFFull) return fail(FLS_ERR_ARG, "filter string too long");

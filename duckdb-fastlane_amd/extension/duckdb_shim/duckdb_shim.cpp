@@ -22,6 +22,7 @@ const LogicalType LogicalType::DATE(LogicalTypeId::DATE);
 const LogicalType LogicalType::FLOAT(LogicalTypeId::FLOAT);
 const LogicalType LogicalType::DOUBLE(LogicalTypeId::DOUBLE);
 const LogicalType LogicalType::VARCHAR(LogicalTypeId::VARCHAR);
+const LogicalType LogicalType::BLOB(LogicalTypeId::BLOB);
 
 idx_t LogicalType::PhysicalSize() const {
     switch (id_) {
@@ -31,7 +32,7 @@ idx_t LogicalType::PhysicalSize() const {
     case LogicalTypeId::FLOAT: return 4;
     case LogicalTypeId::BIGINT: case LogicalTypeId::UBIGINT: case LogicalTypeId::DOUBLE: return 8;
     case LogicalTypeId::DECIMAL: return width_ <= 4 ? 2 : width_ <= 9 ? 4 : 8;
-    case LogicalTypeId::VARCHAR: return 16;
+    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: case LogicalTypeId::BLOB: return 16;
     default: return 8;
     }
 }
@@ -53,6 +54,8 @@ string LogicalType::ToString() const {
     case LogicalTypeId::DOUBLE: return "DOUBLE";
     case LogicalTypeId::DECIMAL: return "DECIMAL(" + std::to_string(width_) + "," + std::to_string(scale_) + ")";
     case LogicalTypeId::VARCHAR: return "VARCHAR";
+    case LogicalTypeId::CHAR: return "CHAR";
+    case LogicalTypeId::BLOB: return "BLOB";
     case LogicalTypeId::LIST: return (child_ ? child_->ToString() : string("?")) + "[]";
     default: return "INVALID";
     }
@@ -88,6 +91,23 @@ string decimal_to_string(int64_t v, uint8_t scale) {
     return (neg ? "-" : "") + std::to_string(a / p) + "." + frac;
 }
 
+// DuckDB's Blob::ToString: printable ASCII as is, other bytes (and the
+// quote and backslash characters) as \xHH
+string blob_to_string(const string &b) {
+    static const char *hex = "0123456789ABCDEF";
+    string r;
+    for (unsigned char c : b) {
+        if (c >= 32 && c <= 126 && c != '\\' && c != '\'' && c != '"') {
+            r += (char)c;
+        } else {
+            r += "\\x";
+            r += hex[c >> 4];
+            r += hex[c & 15];
+        }
+    }
+    return r;
+}
+
 // DuckDB prints doubles with the shortest round-tripping representation
 string double_to_string(double v) {
     char buf[64];
@@ -103,7 +123,8 @@ string double_to_string(double v) {
 string Value::ToString() const {
     if (is_null_) return "NULL";
     switch (type_.id()) {
-    case LogicalTypeId::VARCHAR: return str_;
+    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: return str_;
+    case LogicalTypeId::BLOB: return blob_to_string(str_);
     case LogicalTypeId::BOOLEAN: return int_ ? "true" : "false";
     case LogicalTypeId::UBIGINT: return std::to_string((uint64_t)int_);
     case LogicalTypeId::DATE: return date_to_string((int32_t)int_);
@@ -158,7 +179,8 @@ void Vector::Reference(const Vector &o) {
     capacity_ = o.capacity_;
     data_ptr_ = data_.data();
     keep_ = o.keep_;
-    if (type_.id() == LogicalTypeId::VARCHAR) {  // strings of o's heap into this one's
+    if (type_.PhysicalSize() == 16 && type_.id() != LogicalTypeId::DECIMAL &&
+        type_.id() != LogicalTypeId::LIST) {  // strings of o's heap into this one's
         string_t *sv = reinterpret_cast<string_t *>(data_ptr_);
         for (idx_t i = 0; i < capacity_; ++i)
             if (valid_[i] && sv[i].GetSize() > string_t::INLINE_LENGTH) sv[i] = AddString(sv[i].GetString());
@@ -181,9 +203,15 @@ void Vector::SetValue(idx_t i, const Value &v) {
     valid_[i] = true;
     uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     switch (type_.id()) {
-    case LogicalTypeId::VARCHAR: {
+    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: {
         // implicit cast to VARCHAR, as DuckDB's Vector::SetValue does
         string_t s = AddString(v.GetValue<string>());
+        memcpy(p, &s, sizeof(s));
+        break;
+    }
+    case LogicalTypeId::BLOB: {
+        if (v.type().id() != LogicalTypeId::BLOB) throw InternalException("Vector::SetValue: BLOB needs a BLOB value");
+        string_t s = AddString(StringValue::Get(v));
         memcpy(p, &s, sizeof(s));
         break;
     }
@@ -201,7 +229,12 @@ Value Vector::GetValue(idx_t i) const {
     const uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     auto ld = [p](auto x) { memcpy(&x, p, sizeof(x)); return x; };
     switch (type_.id()) {
-    case LogicalTypeId::VARCHAR: return Value(ld(string_t()).GetString());
+    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: return Value(ld(string_t()).GetString());
+    case LogicalTypeId::BLOB: {
+        const string_t s = ld(string_t());
+        return Value::BLOB((const uint8_t *)s.GetData(), s.GetSize());
+    }
+    case LogicalTypeId::BOOLEAN: return Value::BOOLEAN(ld(uint8_t()) != 0);
     case LogicalTypeId::TINYINT: return Value::TINYINT(ld(int8_t()));
     case LogicalTypeId::SMALLINT: return Value::SMALLINT(ld(int16_t()));
     case LogicalTypeId::INTEGER: return Value::INTEGER(ld(int32_t()));
@@ -250,6 +283,10 @@ const SelectionVector &incremental_sel() {
 // -1 / 0 / 1 for comparable non-null values of one logical type
 int compare_values(const Value &a, const Value &b) {
     switch (a.type().id()) {
+    case LogicalTypeId::BLOB: {
+        const string &x = StringValue::Get(a), &y = StringValue::Get(b);  // bytes compare as unsigned (memcmp)
+        return x < y ? -1 : x > y ? 1 : 0;
+    }
     case LogicalTypeId::VARCHAR: {
         const string x = a.GetValue<string>(), y = b.GetValue<string>();
         return x < y ? -1 : x > y ? 1 : 0;

@@ -83,7 +83,7 @@ public:
 // ---- types -----------------------------------------------------------------
 enum class LogicalTypeId : uint8_t {
     INVALID = 0, SQLNULL, BOOLEAN, TINYINT, SMALLINT, INTEGER, BIGINT, UTINYINT, USMALLINT, UINTEGER,
-    UBIGINT, DATE, FLOAT, DOUBLE, DECIMAL, VARCHAR, LIST
+    UBIGINT, DATE, FLOAT, DOUBLE, DECIMAL, VARCHAR, LIST, CHAR, BLOB
 };
 
 struct LogicalType {
@@ -114,7 +114,7 @@ struct LogicalType {
     string ToString() const;
 
     static const LogicalType SQLNULL, BOOLEAN, TINYINT, SMALLINT, INTEGER, BIGINT, UTINYINT, USMALLINT,
-        UINTEGER, UBIGINT, DATE, FLOAT, DOUBLE, VARCHAR;
+        UINTEGER, UBIGINT, DATE, FLOAT, DOUBLE, VARCHAR, BLOB;
 
 private:
     LogicalTypeId id_;
@@ -178,6 +178,13 @@ public:
     static Value DECIMAL(int64_t v, uint8_t w, uint8_t s) { return Value(LogicalType::DECIMAL(w, s), v); }
     static Value FLOAT(float v) { Value x(LogicalType::FLOAT, 0); x.dbl_ = v; return x; }
     static Value DOUBLE(double v) { Value x(LogicalType::DOUBLE, 0); x.dbl_ = v; return x; }
+    static Value BOOLEAN(bool v) { return Value(LogicalType::BOOLEAN, (int64_t)v); }
+    // DuckDB's Value::BLOB(const_data_ptr_t, idx_t): the raw bytes
+    static Value BLOB(const uint8_t *data, idx_t len) {
+        Value x(LogicalType::BLOB, 0);
+        x.str_.assign((const char *)data, len);
+        return x;
+    }
     static Value LIST(const LogicalType &child, vector<Value> items) {
         Value x(LogicalType::LIST(child), 0);
         x.list_ = std::move(items);
@@ -196,6 +203,8 @@ public:
     // DuckDB's VARCHAR rendering of the value (the cast Vector::SetValue applies)
     string ToString() const;
 
+    friend struct StringValue;
+
 private:
     Value(LogicalType t, int64_t v) : type_(std::move(t)), is_null_(false), int_(v) {}
     LogicalType type_;
@@ -204,6 +213,10 @@ private:
     double dbl_ = 0;
     string str_;
     vector<Value> list_;
+};
+// DuckDB StringValue::Get: the bytes of a VARCHAR or BLOB value
+struct StringValue {
+    static const string &Get(const Value &v) { return v.str_; }
 };
 template <>
 inline string Value::GetValue<string>() const { return is_null_ ? string() : (type_.id() == LogicalTypeId::VARCHAR ? str_ : ToString()); }
@@ -629,6 +642,28 @@ enum class CopyFunctionExecutionMode : uint8_t { REGULAR_COPY_TO_FILE, PARALLEL_
 using copy_to_execution_mode_t = CopyFunctionExecutionMode (*)(bool preserve_insertion_order, bool supports_batch_index);
 using copy_desired_batch_size_t = idx_t (*)(ClientContext &, FunctionData &);
 
+// DuckDB common/optional_idx.hpp
+class optional_idx {
+public:
+    optional_idx() = default;
+    optional_idx(idx_t i) : i_(i) {}  // NOLINT (implicit like DuckDB)
+    bool IsValid() const { return i_ != kInvalid; }
+    idx_t GetIndex() const {
+        if (!IsValid()) throw InternalException("Attempting to get the index of an optional_idx that is not set");
+        return i_;
+    }
+
+private:
+    static constexpr idx_t kInvalid = ~(idx_t)0;
+    idx_t i_ = kInvalid;
+};
+// file rotation (v1.3.2 function/copy_function.hpp): rotate_files says the COPY
+// writes a directory of files; rotate_next_file, asked before every sink, says
+// the current file is complete
+using copy_rotate_files_t = bool (*)(FunctionData &bind_data, const optional_idx &file_size_bytes);
+using copy_rotate_next_file_t = bool (*)(GlobalFunctionData &gstate, FunctionData &bind_data,
+                                         const optional_idx &file_size_bytes);
+
 class CopyFunction {
 public:
     explicit CopyFunction(string name) : name(std::move(name)) {}
@@ -642,6 +677,8 @@ public:
     copy_to_finalize_t copy_to_finalize = nullptr;
     copy_to_execution_mode_t execution_mode = nullptr;
     copy_desired_batch_size_t desired_batch_size = nullptr;
+    copy_rotate_files_t rotate_files = nullptr;
+    copy_rotate_next_file_t rotate_next_file = nullptr;
     std::function<TableFunction()> copy_from_function;  // COPY ... FROM
 };
 

@@ -7,13 +7,17 @@
 // duckdb/ submodule is empty, .gitmodules:1-4).  SQL-level operators the
 // reference test uses (COUNT, LIMIT, LIKE, LENGTH) are applied by the tests on
 // the returned rows.
+#include <sys/stat.h>
+
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -172,7 +176,13 @@ Value parse_constant(const std::string &t, const LogicalType &type) {
     }
     case LogicalTypeId::FLOAT: return Value::FLOAT(std::strtof(t.c_str(), nullptr));
     case LogicalTypeId::DOUBLE: return Value::DOUBLE(std::strtod(t.c_str(), nullptr));
-    case LogicalTypeId::VARCHAR: return Value(t);
+    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: return Value(t);
+    case LogicalTypeId::BOOLEAN: return Value::BOOLEAN(t == "true" || t == "1");
+    case LogicalTypeId::BLOB: {  // the harness passes BLOB bytes as hex digits
+        std::string b;
+        for (size_t i = 0; i + 1 < t.size(); i += 2) b += (char)std::stoi(t.substr(i, 2), nullptr, 16);
+        return Value::BLOB((const uint8_t *)b.data(), b.size());
+    }
     default: throw NotImplementedException("harness: no constant for " + type.ToString());
     }
 }
@@ -770,6 +780,63 @@ int fls_ext_copy(fls_ext_db *d, const char *fn, const char *src, const int *proj
     return fls_ext_copy_mt(d, fn, src, proj, nproj, format, dst, opt_keys, opt_vals, nopts, 1, rows);
 }
 
+}  // extern "C"
+
+// DuckDB's PhysicalCopyToFile target for a COPY without PARTITION_BY: one
+// global state, or, when the function rotates files (rotate_files), a
+// directory of files dst/data_0.<ext>, data_1.<ext>, ... (DuckDB's default
+// FILENAME_PATTERN) where every sink first asks rotate_next_file under the
+// global lock and a full file is finalized once its in-flight sinks are done
+// (WriteRotateInternal).
+struct CopyTarget {
+    struct File {
+        unique_ptr<GlobalFunctionData> g;
+        std::shared_mutex rw;  // sinks into this file: shared; its finalize: exclusive
+    };
+    fls_ext_db *d;
+    CopyFunction &cf;
+    FunctionData &bind;
+    std::string dst;
+    bool rotate = false;
+    idx_t next = 0;
+    std::mutex mu;
+    std::shared_ptr<File> cur;
+    CopyTarget(fls_ext_db *d_, CopyFunction &cf_, FunctionData &bind_, const char *dst_)
+        : d(d_), cf(cf_), bind(bind_), dst(dst_ ? dst_ : "") {
+        rotate = cf.rotate_files && cf.rotate_files(bind, optional_idx());
+        if (rotate && mkdir(dst.c_str(), 0777) != 0 && errno != EEXIST)
+            throw IOException("Cannot create directory \"" + dst + "\"");
+        cur = open();
+    }
+    std::shared_ptr<File> open() {
+        auto f = std::make_shared<File>();
+        const std::string path = rotate ? dst + "/data_" + std::to_string(next++) + "." + cf.extension : dst;
+        f->g = cf.copy_to_initialize_global(d->ctx, bind, path);
+        return f;
+    }
+    template <class F>
+    void write(F &&fun) {
+        for (;;) {
+            std::unique_lock<std::mutex> g(mu);
+            std::shared_ptr<File> f = cur;
+            if (rotate && cf.rotate_next_file && cf.rotate_next_file(*f->g, bind, optional_idx())) {
+                cur = open();
+                g.unlock();
+                std::unique_lock<std::shared_mutex> x(f->rw);
+                cf.copy_to_finalize(d->ctx, bind, *f->g);
+                continue;
+            }
+            std::shared_lock<std::shared_mutex> in(f->rw);
+            g.unlock();
+            fun(*f->g);
+            return;
+        }
+    }
+    void finalize() { cf.copy_to_finalize(d->ctx, bind, *cur->g); }
+};
+
+extern "C" {
+
 // nthreads > 1: an unordered COPY, the scan on up to nthreads threads (the
 // parallel source) and each thread sinking into its own local state, as
 // DuckDB's pipeline runs PhysicalCopyToFile with PARALLEL_COPY_TO_FILE.
@@ -811,7 +878,7 @@ int fls_ext_copy_mt(fls_ext_db *d, const char *fn, const char *src, const int *p
         CopyFunctionBindInput cbin{info};
         auto bind = cf.copy_to_bind(d->ctx, cbin, vector<string>(names.begin(), names.end()),
                                     vector<LogicalType>(types.begin(), types.end()));
-        auto gstate = cf.copy_to_initialize_global(d->ctx, *bind, dst ? dst : "");
+        CopyTarget target(d, cf, *bind, dst);
         if (nthreads < 1) nthreads = 1;
         if (nthreads > 1 && (!cf.execution_mode ||
                              cf.execution_mode(false, false) != CopyFunctionExecutionMode::PARALLEL_COPY_TO_FILE))
@@ -841,22 +908,23 @@ int fls_ext_copy_mt(fls_ext_db *d, const char *fn, const char *src, const int *p
             Local &l = local();
             bool identity = pick.size() == c.ColumnCount() && cnt == c.size();
             for (size_t k = 0; identity && k < pick.size(); ++k) identity = pick[k] == k;
-            if (identity) {
-                cf.copy_to_sink(ectx, *bind, *gstate, *l.state, c);
-            } else {
+            DataChunk *sunk = &c;
+            if (!identity) {
                 DataChunk &out = l.out;
                 out.Reset();
                 for (size_t k = 0; k < pick.size(); ++k)
                     for (idx_t i = 0; i < cnt; ++i) out.data[k].SetValue(i, c.data[pick[k]].GetValue(i));
                 out.SetCardinality(cnt);
-                cf.copy_to_sink(ectx, *bind, *gstate, *l.state, out);
+                sunk = &out;
             }
+            target.write([&](GlobalFunctionData &g) { cf.copy_to_sink(ectx, *bind, g, *l.state, *sunk); });
             n += cnt;
         }, nthreads);
         if (locals.empty()) local();  // an empty source still has one sink
         for (auto &kv : locals)
-            if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *kv.second->state);
-        cf.copy_to_finalize(d->ctx, *bind, *gstate);
+            if (cf.copy_to_combine)
+                target.write([&](GlobalFunctionData &g) { cf.copy_to_combine(ectx, *bind, g, *kv.second->state); });
+        target.finalize();
         if (rows) *rows = n.load();
         return 0;
     } catch (const std::exception &e) {
@@ -903,17 +971,28 @@ int fls_ext_copy_values_mt(fls_ext_db *d, const char *format, const char *dst, i
         for (int c = 0; c < ncols; ++c) {
             const std::string tn = StringUtil::Upper(type_names[c]);
             cn.emplace_back(names[c]);
+            unsigned w = 0, sc = 0;
             if (tn == "INTEGER") ct.push_back(LogicalType::INTEGER);
             else if (tn == "BIGINT") ct.push_back(LogicalType::BIGINT);
             else if (tn == "DOUBLE") ct.push_back(LogicalType::DOUBLE);
             else if (tn == "VARCHAR") ct.push_back(LogicalType::VARCHAR);
+            else if (tn == "BOOLEAN") ct.push_back(LogicalType::BOOLEAN);
+            else if (tn == "BLOB") ct.push_back(LogicalType::BLOB);
+            else if (tn == "CHAR") ct.push_back(LogicalType(LogicalTypeId::CHAR));
+            else if (tn == "TINYINT") ct.push_back(LogicalType::TINYINT);
+            else if (tn == "SMALLINT") ct.push_back(LogicalType::SMALLINT);
+            else if (tn == "UTINYINT") ct.push_back(LogicalType::UTINYINT);
+            else if (tn == "UBIGINT") ct.push_back(LogicalType::UBIGINT);
+            else if (tn == "FLOAT") ct.push_back(LogicalType::FLOAT);
+            else if (tn == "DATE") ct.push_back(LogicalType::DATE);
+            else if (sscanf(tn.c_str(), "DECIMAL(%u,%u)", &w, &sc) == 2) ct.push_back(LogicalType::DECIMAL(w, sc));
             else throw BinderException("harness: unsupported VALUES type " + tn);
         }
         CopyInfo info;
         for (int i = 0; i < nopts; ++i) info.options[StringUtil::Lower(opt_keys[i])].push_back(Value(opt_vals[i]));
         CopyFunctionBindInput cbin{info};
         auto bind = cf.copy_to_bind(d->ctx, cbin, cn, ct);
-        auto gstate = cf.copy_to_initialize_global(d->ctx, *bind, dst ? dst : "");
+        CopyTarget target(d, cf, *bind, dst);
         auto worker = [&](int t) {
             ExecutionContext ectx(d->ctx);
             auto lstate = cf.copy_to_initialize_local(ectx, *bind);
@@ -931,13 +1010,15 @@ int fls_ext_copy_values_mt(fls_ext_db *d, const char *format, const char *dst, i
                         else if (ct[c].id() == LogicalTypeId::INTEGER) v = Value::INTEGER(std::atoi(x));
                         else if (ct[c].id() == LogicalTypeId::BIGINT) v = Value::BIGINT(std::atoll(x));
                         else if (ct[c].id() == LogicalTypeId::DOUBLE) v = Value::DOUBLE(std::atof(x));
-                        else v = Value(std::string(x));
+                        else if (ct[c].id() == LogicalTypeId::VARCHAR) v = Value(std::string(x));
+                        else v = parse_constant(x, ct[c]);
                         chunk.data[c].SetValue(i, v);
                     }
                 chunk.SetCardinality(n);
-                cf.copy_to_sink(ectx, *bind, *gstate, *lstate, chunk);
+                target.write([&](GlobalFunctionData &g) { cf.copy_to_sink(ectx, *bind, g, *lstate, chunk); });
             }
-            if (cf.copy_to_combine) cf.copy_to_combine(ectx, *bind, *gstate, *lstate);
+            if (cf.copy_to_combine)
+                target.write([&](GlobalFunctionData &g) { cf.copy_to_combine(ectx, *bind, g, *lstate); });
         };
         if (nthreads == 1) {
             worker(0);
@@ -956,7 +1037,7 @@ int fls_ext_copy_values_mt(fls_ext_db *d, const char *format, const char *dst, i
             for (auto &e : errs)
                 if (!e.empty()) throw Exception(e);
         }
-        cf.copy_to_finalize(d->ctx, *bind, *gstate);
+        target.finalize();
         if (rows) *rows = (uint64_t)nrows;
         return 0;
     } catch (const std::exception &e) {

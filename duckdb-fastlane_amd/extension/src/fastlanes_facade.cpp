@@ -111,6 +111,18 @@ static void RenderCell(Vector &vec, idx_t out_row, const fls_column_info &ci, co
         FlatVector::GetData<string_t>(vec)[out_row] = StringVector::AddString(vec, Value::DOUBLE(x).ToString());
         return;
     }
+    case FLS_BOOLEAN: {
+        const uint8_t b = ((const uint8_t *)col)[row];
+        FlatVector::GetData<string_t>(vec)[out_row] = StringVector::AddString(vec, Value::BOOLEAN(b != 0).ToString());
+        return;
+    }
+    case FLS_BLOB: {  // byte strings: DuckDB's BLOB -> VARCHAR rendering
+        string_t s;
+        memcpy(&s, (const uint8_t *)col + 16 * row, 16);
+        FlatVector::GetData<string_t>(vec)[out_row] =
+            StringVector::AddString(vec, Value::BLOB((const uint8_t *)s.GetData(), s.GetSize()).ToString());
+        return;
+    }
     case FLS_VARCHAR: {  // str_col_t / FLSStrColumn
         string_t s;
         memcpy(&s, (const uint8_t *)col + 16 * row, 16);

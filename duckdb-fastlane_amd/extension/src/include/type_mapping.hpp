@@ -24,6 +24,11 @@ struct TypeMapping {
     // bytes of one decoded value as delivered by the engine (string_t = 16)
     static idx_t GetFastLanesTypeSize(uint8_t fls_type);
     static bool IsSupported(const LogicalType &type) { return DuckDBToFastLanes(type) != 0; }
+    // a column written as byte strings (VARCHAR, CHAR, BLOB: 16-byte string_t)
+    static bool IsString(const LogicalType &type) {
+        const uint8_t t = DuckDBToFastLanes(type);
+        return t == 20 || t == 21;  // FLS_VARCHAR, FLS_BLOB
+    }
 };
 
 }  // namespace ext_fastlane

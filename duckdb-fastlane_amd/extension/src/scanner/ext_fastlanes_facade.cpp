@@ -262,10 +262,16 @@ static Value BoxValue(const fls_column_info &ci, const void *col, idx_t row) {
     case FLS_DECIMAL: return Value::DECIMAL(ld(int64_t()), ci.width ? ci.width : 18, ci.scale);
     case FLS_FLOAT: return Value::FLOAT(ld(float()));
     case FLS_DOUBLE: return Value::DOUBLE(ld(double()));
+    case FLS_BOOLEAN: return Value::BOOLEAN(ld(uint8_t()) != 0);
     case FLS_VARCHAR: {
         string_t s;
         memcpy(&s, p + 16 * row, 16);
         return Value(s.GetString());
+    }
+    case FLS_BLOB: {
+        string_t s;
+        memcpy(&s, p + 16 * row, 16);
+        return Value::BLOB((const uint8_t *)s.GetData(), s.GetSize());
     }
     default: return Value();
     }
@@ -416,7 +422,7 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
         };
         std::vector<std::thread> th;
         for (size_t c = 0; c < wtypes.size(); ++c)
-            if (wtypes[c].id() == LogicalTypeId::VARCHAR) th.emplace_back(assemble, c);
+            if (TypeMapping::IsString(wtypes[c])) th.emplace_back(assemble, c);
         for (auto &t : th) t.join();
         // the writer takes batches in hand-off order; a failed batch fails the rest
         if (prev.valid()) {
@@ -437,7 +443,7 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
             const idx_t r0 = (idx_t)k * rg_rows;
             nrows[k] = (uint32_t)std::min<idx_t>(rg_rows, rows - r0);
             for (size_t c = 0; c < nc; ++c) {
-                if (wtypes[c].id() == LogicalTypeId::VARCHAR) {
+                if (TypeMapping::IsString(wtypes[c])) {
                     data[k * nc + c] = b->cols[c].empty() ? (const void *)"" : b->cols[c].data() + b->base[c][k];
                     offs[k * nc + c] = b->offs[c].data() + (size_t)k * (rg_rows + 1);
                 } else {
@@ -503,7 +509,7 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
             RawBuf &col = st.wcols[c];
-            if (t.id() == LogicalTypeId::VARCHAR) {
+            if (TypeMapping::IsString(t)) {
                 // the records in one copy; the non-inlined strings' bytes to
                 // the arena, their pointer field := arena offset
                 const string_t *str = FlatVector::GetData<string_t>(v) + r0;
@@ -615,7 +621,7 @@ bool FastLanesFacade::mergeStage(Stage &st) {
     while (r0 < st.wrows) {
         const idx_t n = std::min<idx_t>(st.wrows - r0, s.rg_rows - o.wrows % s.rg_rows);
         for (size_t c = 0; c < nc; ++c) {
-            if (s.wtypes[c].id() == LogicalTypeId::VARCHAR) {
+            if (TypeMapping::IsString(s.wtypes[c])) {
                 const uint8_t *src = st.wrec[c].data() + sizeof(string_t) * r0;
                 uint8_t *rec = o.wrec[c].grow(n * sizeof(string_t));
                 memcpy(rec, src, n * sizeof(string_t));

@@ -197,6 +197,9 @@ bool MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v, const L
     case LogicalTypeId::UBIGINT:
         p.value = v.GetValue<uint64_t>();
         break;
+    case LogicalTypeId::BOOLEAN:  // u8 0 / 1
+        p.value = v.GetValue<bool>() ? 1 : 0;
+        break;
     case LogicalTypeId::DATE:
         p.value = (uint64_t)(int64_t)v.GetValue<date_t>().days;
         break;
@@ -217,6 +220,12 @@ bool MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v, const L
         memcpy(&p.value, &d, 8);
         break;
     }
+    case LogicalTypeId::BLOB:  // the constant's bytes (StringValue::Get), compared unsigned like DuckDB
+        if (v.type().id() != LogicalTypeId::BLOB) return false;
+        strs.push_back(StringValue::Get(v));
+        p.str = strs.back().data();
+        p.str_len = strs.back().size();
+        break;
     case LogicalTypeId::VARCHAR:
         strs.push_back(v.GetValue<string>());
         p.str = strs.back().data();

@@ -6,10 +6,16 @@
 // row, :27), the same error texts.  Rows go through
 // ext_fastlane::FastLanesFacade::createFile/writeChunk/finalizeFile into the CPU
 // FastLanes writer (per-chunk encoding choice: FFOR / DELTA / DICT / RLE).
-// ROW_GROUPS_PER_FILE rotation is not supported by this writer (it would need
-// DuckDB's rotate_files hooks) and is rejected at bind time.
+// ROW_GROUPS_PER_FILE rotates files as the reference registers it (:96-97,
+// :267-289, rotate_files / rotate_next_file): DuckDB then writes a directory of
+// files and asks, before every sink, whether the current file holds its row
+// groups.
 #include "writer/copy_fastlanes.hpp"
 
+#include <atomic>
+#include <mutex>
+
+#include "duckdb/common/optional_idx.hpp"
 #include "duckdb/common/string_util.hpp"
 #include "duckdb/main/extension_util.hpp"
 #include "fastlanes_facade.hpp"
@@ -24,12 +30,18 @@ struct FastlaneCopyBindData : public TableFunctionData {
     vector<LogicalType> sql_types;
     vector<string> column_names;
     idx_t row_group_size = 65536;
+    optional_idx row_groups_per_file;
     static constexpr idx_t BYTES_PER_ROW = 1024;
 };
 
 struct FastlaneCopyGlobalState : public GlobalFunctionData {
     std::unique_ptr<FastLanesFacade> facade;
     string file_path;
+    // rotation: rows sunk into this file (current_rowgroup = rows / row group
+    // size), through the facade's serial path so that the file holds exactly
+    // the rows sunk into it when DuckDB finalizes it
+    std::atomic<idx_t> rows{0};
+    std::mutex serial;
 };
 
 // Each sink thread copies its chunks into its own facade stage (created at the
@@ -61,7 +73,9 @@ unique_ptr<FunctionData> CopyBind(ClientContext &, CopyFunctionBindInput &input,
                                        ? ValidRowGroupSize(std::max<uint64_t>(1024, x / FastlaneCopyBindData::BYTES_PER_ROW / 1024 * 1024))
                                        : ValidRowGroupSize(x);
         } else if (name == "row_groups_per_file") {
-            throw BinderException("ROW_GROUPS_PER_FILE is not supported by the FastLanes writer");
+            const uint64_t x = (uint64_t)std::stoull(v.ToString());
+            if (x == 0) throw BinderException("ROW_GROUPS_PER_FILE must be at least 1");
+            bind->row_groups_per_file = x;
         } else {
             throw BinderException("Unknown option for FastLanes: " + StringUtil::Upper(name));
         }
@@ -87,10 +101,20 @@ unique_ptr<LocalFunctionData> CopyInitLocal(ExecutionContext &, FunctionData &) 
     return make_uniq<FastlaneCopyLocalState>();
 }
 
-void CopySink(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate, LocalFunctionData &lstate,
+void CopySink(ExecutionContext &, FunctionData &bind_p, GlobalFunctionData &gstate, LocalFunctionData &lstate,
               DataChunk &input) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
     auto &l = lstate.Cast<FastlaneCopyLocalState>();
+    if (bind_p.Cast<FastlaneCopyBindData>().row_groups_per_file.IsValid()) {
+        // rotating: no per-thread stage may carry rows past this file's finalize
+        std::lock_guard<std::mutex> guard(g.serial);
+        if (!g.facade->writeChunk(input)) {
+            const std::string &why = g.facade->lastError();
+            throw IOException("Failed to write chunk to FastLanes" + (why.empty() ? std::string() : ": " + why));
+        }
+        g.rows += input.size();
+        return;
+    }
     if (!l.stage) l.stage = g.facade->newStage();
     if (!g.facade->writeChunk(*l.stage, input)) {
         const std::string &why = g.facade->stageError(*l.stage);
@@ -116,6 +140,22 @@ void CopyCombine(ExecutionContext &, FunctionData &, GlobalFunctionData &gstate,
 CopyFunctionExecutionMode CopyExecutionMode(bool preserve_insertion_order, bool /*supports_batch_index*/) {
     return preserve_insertion_order ? CopyFunctionExecutionMode::REGULAR_COPY_TO_FILE
                                     : CopyFunctionExecutionMode::PARALLEL_COPY_TO_FILE;
+}
+
+// The reference's rotation callbacks (write_fastlane_stream.cpp:267-289): a
+// directory of files when ROW_GROUPS_PER_FILE is set (FILE_SIZE_BYTES too,
+// which the reference never rotates on: DuckDB's own size check is absent
+// for it, and so here), the next file once this one holds that many row
+// groups
+bool CopyRotateFiles(FunctionData &bind_p, const optional_idx &file_size_bytes) {
+    return file_size_bytes.IsValid() || bind_p.Cast<FastlaneCopyBindData>().row_groups_per_file.IsValid();
+}
+
+bool CopyRotateNextFile(GlobalFunctionData &gstate, FunctionData &bind_p, const optional_idx &) {
+    auto &bind = bind_p.Cast<FastlaneCopyBindData>();
+    if (!bind.row_groups_per_file.IsValid()) return false;
+    const idx_t current_rowgroup = gstate.Cast<FastlaneCopyGlobalState>().rows.load() / bind.row_group_size;
+    return current_rowgroup >= bind.row_groups_per_file.GetIndex();
 }
 
 // Rows per batch: one row group (write_fastlane_stream.cpp:262-265)
@@ -144,6 +184,8 @@ void RegisterFastlaneCopyFunction(DatabaseInstance &db) {
     fn.copy_to_finalize = CopyFinalize;
     fn.execution_mode = CopyExecutionMode;
     fn.desired_batch_size = CopyDesiredBatchSize;
+    fn.rotate_files = CopyRotateFiles;
+    fn.rotate_next_file = CopyRotateNextFile;
     fn.copy_from_function = ReadFastlanesFunction;
     fn.extension = "fls";
     ExtensionUtil::RegisterFunction(db, fn);

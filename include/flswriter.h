@@ -28,7 +28,9 @@ typedef struct fls_writer fls_writer;
 enum fls_type {
     FLS_INT8 = 1, FLS_INT16 = 2, FLS_INT32 = 3, FLS_INT64 = 4,
     FLS_UINT8 = 5, FLS_UINT16 = 6, FLS_UINT32 = 7, FLS_UINT64 = 8,
-    FLS_DATE = 10, FLS_DECIMAL = 11, FLS_FLOAT = 12, FLS_DOUBLE = 13, FLS_VARCHAR = 20
+    FLS_BOOLEAN = 9,  /* u8 0/1, DuckDB bool (reference type_mapping.cpp:13-14) */
+    FLS_DATE = 10, FLS_DECIMAL = 11, FLS_FLOAT = 12, FLS_DOUBLE = 13, FLS_VARCHAR = 20,
+    FLS_BLOB = 21     /* byte strings, VARCHAR's layout (reference type_mapping.cpp:40-42, BYTE_ARRAY) */
 };
 /* Encodings; FLS_ENC_AUTO picks per chunk: the smallest of FFOR/DELTA/DICT/RLE
  * for integers, ALP for FLOAT/DOUBLE, DICT or FSST for VARCHAR. */

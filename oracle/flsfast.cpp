@@ -43,7 +43,7 @@ namespace {
 constexpr uint32_t kVec = 1024;
 constexpr uint32_t FL_ORDER[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 enum { ENC_FFOR = 1, ENC_DELTA = 2, ENC_DICT = 3, ENC_RLE = 4, ENC_ALP = 5, ENC_FSST = 7 };
-enum { TY_FLOAT = 12, TY_DOUBLE = 13, TY_VARCHAR = 20 };
+enum { TY_BOOLEAN = 9, TY_FLOAT = 12, TY_DOUBLE = 13, TY_VARCHAR = 20, TY_BLOB = 21 };
 
 constexpr uint32_t tau(uint32_t p) { return 128u * FL_ORDER[(p >> 4) & 7] + 16u * ((p >> 7) & 7) + (p & 15); }
 
@@ -155,11 +155,11 @@ struct File {
 
 uint32_t out_bytes(uint8_t t) {
     switch (t) {
-    case 1: case 5: return 1;
+    case 1: case 5: case TY_BOOLEAN: return 1;
     case 2: case 6: return 2;
     case 3: case 7: case 10: case TY_FLOAT: return 4;
     case 4: case 8: case 11: case TY_DOUBLE: return 8;
-    case TY_VARCHAR: return 16;
+    case TY_VARCHAR: case TY_BLOB: return 16;
     default: return 0;
     }
 }

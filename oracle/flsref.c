@@ -40,8 +40,8 @@ static const uint32_t FL_ORDER[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 enum { ENC_FFOR = 1, ENC_DELTA = 2, ENC_DICT = 3, ENC_RLE = 4, ENC_ALP = 5, ENC_FSST = 7 };
 enum {
     TY_INT8 = 1, TY_INT16 = 2, TY_INT32 = 3, TY_INT64 = 4,
-    TY_UINT8 = 5, TY_UINT16 = 6, TY_UINT32 = 7, TY_UINT64 = 8,
-    TY_DATE = 10, TY_DECIMAL = 11, TY_FLOAT = 12, TY_DOUBLE = 13, TY_VARCHAR = 20
+    TY_UINT8 = 5, TY_UINT16 = 6, TY_UINT32 = 7, TY_UINT64 = 8, TY_BOOLEAN = 9,
+    TY_DATE = 10, TY_DECIMAL = 11, TY_FLOAT = 12, TY_DOUBLE = 13, TY_VARCHAR = 20, TY_BLOB = 21
 };
 
 /* ALP: 10^i and the nearest binary64/binary32 to 10^-i */
@@ -202,11 +202,11 @@ int64_t flsref_rowgroup_rows(const flsref_file *f, uint32_t rg)
 static int value_bytes(int type)
 {
     switch (type) {
-    case TY_INT8: case TY_UINT8: return 1;
+    case TY_INT8: case TY_UINT8: case TY_BOOLEAN: return 1;
     case TY_INT16: case TY_UINT16: return 2;
     case TY_INT32: case TY_UINT32: case TY_DATE: case TY_FLOAT: return 4;
     case TY_INT64: case TY_UINT64: case TY_DECIMAL: case TY_DOUBLE: return 8;
-    case TY_VARCHAR: return 16;
+    case TY_VARCHAR: case TY_BLOB: return 16;
     default: return 0;
     }
 }
@@ -406,7 +406,7 @@ int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, u
     int type, w, s, nl;
     const char *nm;
     flsref_column(f, col, &type, &w, &s, &nm, &nl);
-    if (type != TY_VARCHAR) return -1;
+    if (type != TY_VARCHAR && type != TY_BLOB) return -1;
     const uint8_t *rgp = rg_desc(f, rg);
     const uint32_t rg_rows = rd32(rgp);
     const uint64_t coff = rd64(rgp + 4 + 16 * (size_t)col);

@@ -86,14 +86,14 @@ def assert_column_equal(fl, rf, c: int, got: np.ndarray, base_ptr: int):
     try:
         exp = rf.decode_column(c, nthreads=8)
     except ValueError:              # FSST: strings are not inside the image
-        assert ty == 20
+        assert ty in (20, 21)
         assert_strings_equal(fl, rf, c, got)
         return
-    if ty == 20:
+    if ty in (20, 21):
         exp = expected_string_t(rf, exp, base_ptr)
     assert got.shape == exp.shape, (name, got.shape, exp.shape)
     if not np.array_equal(got, exp):
-        w = 16 if ty == 20 else rf.out_width(c)
+        w = 16 if ty in (20, 21) else rf.out_width(c)
         bad = np.nonzero((got.reshape(-1, w) != exp.reshape(-1, w)).any(axis=1))[0]
         raise AssertionError(f"column {name}: {len(bad)} mismatching rows, first {bad[:8]}")
 

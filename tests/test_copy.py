@@ -8,6 +8,7 @@ combine, finalize).  CPU tests: registration and option errors (they fail at
 bind, before any scan).  GPU tests: COPY (SELECT ... FROM read_fastlanes(src))
 round trips, checked with the oracle on the written file and against the
 workload generators."""
+import os
 import re
 
 import numpy as np
@@ -40,7 +41,7 @@ def test_copy_functions_registered(ext):
     ({"chunk_size": 131072}, "ROW_GROUP_SIZE must be a multiple of 1024"),
     ({"row_group_size": 0}, "ROW_GROUP_SIZE must be a multiple of 1024"),
     ({"row_group_size": 8192, "row_group_size_bytes": 1 << 24}, "mutually exclusive"),
-    ({"row_groups_per_file": 2}, "ROW_GROUPS_PER_FILE is not supported"),
+    ({"row_groups_per_file": 0}, "ROW_GROUPS_PER_FILE must be at least 1"),
     ({"compression": "zstd"}, "^Unknown option for FastLanes: COMPRESSION$"),
 ])
 def test_copy_option_errors(ext, li_file, tmpfile, opts, msg):
@@ -211,6 +212,53 @@ def test_copy_many_sinks_bounded_staging_cpu(ext, ref, tmpfile, monkeypatch, cap
     assert rf.nrows == n
     got_a = np.concatenate([rf.decode(0, g) for g in range(rf.nrowgroups)]).view(np.int64).tolist()
     assert sorted(zip(got_a, rf.strings_column(1))) == sorted(zip(a, (x.encode() for x in s)))
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_copy_row_groups_per_file_rotates_cpu(ext, ref, tmpfile, threads):
+    """ROW_GROUPS_PER_FILE (reference write_fastlane_stream.cpp:96-97,
+    :267-289): the COPY target becomes a directory of data_<i>.fls files, and
+    DuckDB opens the next file once the current one holds that many row
+    groups (asked before each sink, so a file can end past the boundary by
+    the chunks in flight).  Every row lands in exactly one file; one sink
+    thread keeps the order and fills every file but the last with exactly
+    ROW_GROUPS_PER_FILE row groups."""
+    rg, per = 1024, 2
+    n = 5 * rg + 300
+    a = [(i * 37) % 1009 for i in range(n)]
+    s = [f"r{i % 9}" * (i % 6) for i in range(n)]
+    d = tmpfile(f"rot{threads}")
+    assert ext.copy_values([("a", "BIGINT", a), ("s", "VARCHAR", s)], d, threads=threads,
+                           row_group_size=rg, row_groups_per_file=per) == n
+    files = sorted(os.listdir(d), key=lambda f: int(f[5:-4]))
+    assert files == [f"data_{i}.fls" for i in range(len(files))]
+    got, sizes = [], []
+    for f in files:
+        rf = ref.RefFile(open(os.path.join(d, f), "rb").read())
+        sizes.append(rf.nrows)
+        assert rf.f.rowgroup_size == rg
+        va = np.concatenate([rf.decode(0, g) for g in range(rf.nrowgroups)]).view(np.int64).tolist()
+        got += list(zip(va, rf.strings_column(1)))
+    exp = list(zip(a, (x.encode() for x in s)))
+    if threads == 1:
+        assert sizes == [per * rg, per * rg, n - 2 * per * rg] and got == exp
+    else:
+        assert min(sizes) > 0 and max(sizes) <= per * rg + threads * 2048
+    assert sorted(got) == sorted(exp)
+
+
+@pytest.mark.gpu
+def test_copy_rotated_files_read_back_with_glob(ext, gpu, tmpfile):
+    """read_fastlanes('dir/*.fls') over a rotated COPY's files returns every
+    row once (the multi-file scan reads them as one table)."""
+    rg = 1024
+    n = 7 * rg + 5
+    d = tmpfile("rotg")
+    assert ext.copy_values([("a", "BIGINT", list(range(n)))], d, threads=2, row_group_size=rg,
+                           row_groups_per_file=3) == n
+    assert len(os.listdir(d)) >= 2
+    names, types, rows = ext.query("read_fastlanes", os.path.join(d, "*.fls"), threads=2)
+    assert types == ["BIGINT"] and sorted(int(r[0]) for r in rows) == list(range(n))
 
 
 def test_copy_parallel_sinks_refuse_nulls_cpu(ext, tmpfile):

@@ -28,7 +28,7 @@ def _digests(rf):
     out = []
     for c in range(rf.ncols):
         raw = rf.decode_column(c, 2)
-        data = b"\0".join(rf.strings(raw)) if rf.column(c)[1] == 20 else raw.tobytes()
+        data = b"\0".join(rf.strings(raw)) if rf.column(c)[1] in (20, 21) else raw.tobytes()
         out.append(hashlib.sha1(data).hexdigest())
     return out
 
@@ -95,7 +95,7 @@ def test_two_rank_shards_cover_table(_built, wl, scale, nrows):
             raw = full.decode_column(c, 2)
             w = full.out_width(c)
             part = raw[lo * w:hi * w]
-            data = b"\0".join(full.strings(part)) if full.column(c)[1] == 20 else part.tobytes()
+            data = b"\0".join(full.strings(part)) if full.column(c)[1] in (20, 21) else part.tobytes()
             exp.append(hashlib.sha1(data).hexdigest())
         assert exp == sums
 
