@@ -74,13 +74,13 @@ def test_auto_picks_compact_encodings(fl, ref):
 
 
 def test_writer_errors(fl):
-    with pytest.raises(fl.FlsError, match="VARCHAR supports DICT and FSST"):
+    with pytest.raises(fl.FlsError, match="VARCHAR/BLOB support DICT and FSST"):
         fl.write_image([("s", fl.VARCHAR, ["a"], fl.ENC_FFOR)])
     with pytest.raises(fl.FlsError, match="FLOAT/DOUBLE support ALP"):
         fl.write_image([("d", fl.DOUBLE, [1.5], fl.ENC_FFOR)])
     with pytest.raises(fl.FlsError, match="ALP needs FLOAT/DOUBLE"):
         fl.write_image([("i", fl.INT32, [1], fl.ENC_ALP)])
-    with pytest.raises(fl.FlsError, match="FSST needs VARCHAR"):
+    with pytest.raises(fl.FlsError, match="FSST needs VARCHAR/BLOB"):
         fl.write_image([("i", fl.INT64, [1], fl.ENC_FSST)])
     with pytest.raises(fl.FlsError, match="unsupported type"):
         fl.write_image([("x", 99, [1], fl.ENC_FFOR)])
