@@ -142,11 +142,11 @@ string Value::ToString() const {
 
 Vector::Vector(LogicalType type, idx_t capacity)
     : type_(std::move(type)), capacity_(capacity), data_(capacity * type_.PhysicalSize(), 0),
-      data_ptr_(data_.data()), valid_(capacity, true) {}
+      data_ptr_(data_.data()), validity_(capacity) {}
 
 Vector::Vector(Vector &&o) noexcept
     : type_(std::move(o.type_)), capacity_(o.capacity_), data_(std::move(o.data_)), auxiliary_(std::move(o.auxiliary_)),
-      valid_(std::move(o.valid_)), may_null_(o.may_null_), heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
+      validity_(std::move(o.validity_)), heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
     // a moved std::vector keeps its storage, so an owned data pointer stays valid
     data_ptr_ = o.data_ptr_;
     o.data_ptr_ = nullptr;
@@ -157,8 +157,7 @@ Vector::Vector(Vector &&o) noexcept
 void Vector::Reset() {
     data_ptr_ = data_.data();
     auxiliary_.reset();
-    std::fill(valid_.begin(), valid_.end(), true);
-    may_null_ = false;
+    validity_.Reset();
     heap_.clear();
     keep_.clear();
     vtype_ = VectorType::FLAT_VECTOR;
@@ -166,8 +165,7 @@ void Vector::Reset() {
 
 void Vector::Reference(const Vector &o) {
     type_ = o.type_;
-    valid_ = o.valid_;
-    may_null_ = o.may_null_;
+    validity_ = o.validity_;  // shared words, as DuckDB's Reference shares the validity buffer
     vtype_ = o.vtype_;
     if (o.auxiliary_) {  // foreign data kept alive by its holder: share it
         data_ptr_ = o.data_ptr_;
@@ -183,7 +181,7 @@ void Vector::Reference(const Vector &o) {
         type_.id() != LogicalTypeId::LIST) {  // strings of o's heap into this one's
         string_t *sv = reinterpret_cast<string_t *>(data_ptr_);
         for (idx_t i = 0; i < capacity_; ++i)
-            if (valid_[i] && sv[i].GetSize() > string_t::INLINE_LENGTH) sv[i] = AddString(sv[i].GetString());
+            if (validity_.RowIsValid(i) && sv[i].GetSize() > string_t::INLINE_LENGTH) sv[i] = AddString(sv[i].GetString());
     }
 }
 
@@ -196,11 +194,10 @@ string_t Vector::AddString(const string &s) {
 void Vector::SetValue(idx_t i, const Value &v) {
     if (i >= capacity_) throw InternalException("Vector::SetValue out of range");
     if (v.IsNull()) {
-        valid_[i] = false;
-        may_null_ = true;
+        validity_.SetInvalid(i);
         return;
     }
-    valid_[i] = true;
+    validity_.SetValid(i);
     uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     switch (type_.id()) {
     case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: {
@@ -225,7 +222,7 @@ void Vector::SetValue(idx_t i, const Value &v) {
 }
 
 Value Vector::GetValue(idx_t i) const {
-    if (!valid_[i]) return Value();
+    if (!validity_.RowIsValid(i)) return Value();
     const uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     auto ld = [p](auto x) { memcpy(&x, p, sizeof(x)); return x; };
     switch (type_.id()) {
@@ -347,6 +344,7 @@ bool eval_filter(const TableFilter &f, const Value &v) {
 void Vector::ToUnifiedFormat(idx_t, UnifiedVectorFormat &format) const {
     format.sel = &incremental_sel();
     format.data = GetData();
+    format.validity = validity_;
 }
 
 unique_ptr<TableFilterState> TableFilterState::Initialize(ClientContext &, const TableFilter &) {

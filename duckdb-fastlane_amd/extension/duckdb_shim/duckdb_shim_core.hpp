@@ -260,6 +260,60 @@ buffer_ptr<T> make_buffer(Args &&...args) {
     return std::make_shared<T>(std::forward<Args>(args)...);
 }
 
+// DuckDB common/types/validity_mask.hpp: one bit per row (1 = valid) in
+// 64-bit words, no words allocated while every row is valid
+using validity_t = uint64_t;
+class ValidityMask {
+public:
+    static constexpr idx_t BITS_PER_VALUE = 64;
+    explicit ValidityMask(idx_t capacity = STANDARD_VECTOR_SIZE) : capacity_(capacity) {}
+    static idx_t EntryCount(idx_t count) { return (count + BITS_PER_VALUE - 1) / BITS_PER_VALUE; }
+    bool AllValid() const { return !data_; }
+    bool CheckAllValid(idx_t count) const {
+        if (!data_) return true;
+        for (idx_t i = 0; i < count / BITS_PER_VALUE; ++i)
+            if (data_[i] != ~validity_t(0)) return false;
+        const idx_t rest = count % BITS_PER_VALUE;
+        return !rest || (data_[count / BITS_PER_VALUE] | (~validity_t(0) << rest)) == ~validity_t(0);
+    }
+    validity_t *GetData() const { return data_; }
+    // own words for capacity rows, every row valid
+    void Initialize(idx_t capacity) {
+        capacity_ = capacity;
+        owned_ = std::make_shared<vector<validity_t>>(EntryCount(capacity), ~validity_t(0));
+        data_ = owned_->data();
+    }
+    void Initialize() { Initialize(capacity_); }
+    void Reset() {
+        data_ = nullptr;
+        owned_.reset();
+    }
+    bool RowIsValid(idx_t row) const { return !data_ || ((data_[row / BITS_PER_VALUE] >> (row % BITS_PER_VALUE)) & 1); }
+    void SetInvalid(idx_t row) {
+        if (!data_) Initialize();
+        data_[row / BITS_PER_VALUE] &= ~(validity_t(1) << (row % BITS_PER_VALUE));
+    }
+    void SetValid(idx_t row) {
+        if (data_) data_[row / BITS_PER_VALUE] |= validity_t(1) << (row % BITS_PER_VALUE);
+    }
+    void Set(idx_t row, bool valid) { valid ? SetValid(row) : SetInvalid(row); }
+    // a private copy of other's words
+    void Copy(const ValidityMask &other, idx_t count) {
+        if (!other.data_) {
+            Reset();
+            return;
+        }
+        Initialize(std::max(capacity_, count));
+        std::copy(other.data_, other.data_ + EntryCount(count), data_);
+    }
+    idx_t Capacity() const { return capacity_; }
+
+private:
+    idx_t capacity_;
+    validity_t *data_ = nullptr;
+    shared_ptr<vector<validity_t>> owned_;
+};
+
 class Vector {
 public:
     explicit Vector(LogicalType type, idx_t capacity = STANDARD_VECTOR_SIZE);
@@ -279,16 +333,10 @@ public:
     // the shim's own storage is not shareable, so owned data is copied
     void Reference(const Vector &other);
     buffer_ptr<VectorBuffer> GetAuxiliary() const { return auxiliary_; }
-    bool RowIsValid(idx_t i) const { return valid_[i]; }
-    void SetValid(idx_t i, bool v) {
-        valid_[i] = v;
-        may_null_ |= !v;
-    }
-    // ValidityMask::CheckAllValid over the first n rows (DuckDB: O(1) while no
-    // mask is allocated; here: while no row was ever set invalid since Reset)
-    bool AllValid(idx_t n) const {
-        return !may_null_ || std::find(valid_.begin(), valid_.begin() + n, false) == valid_.begin() + n;
-    }
+    bool RowIsValid(idx_t i) const { return validity_.RowIsValid(i); }
+    void SetValid(idx_t i, bool v) { validity_.Set(i, v); }
+    ValidityMask &Validity() { return validity_; }
+    const ValidityMask &Validity() const { return validity_; }
     void ToUnifiedFormat(idx_t count, struct UnifiedVectorFormat &format) const;
     void SetVectorType(VectorType t) { vtype_ = t; }
     VectorType GetVectorType() const { return vtype_; }
@@ -304,8 +352,7 @@ private:
     vector<uint8_t> data_;
     data_ptr_t data_ptr_;                 // data_.data(), or foreign memory (SetData)
     buffer_ptr<VectorBuffer> auxiliary_;  // keeps foreign memory alive
-    vector<bool> valid_;
-    bool may_null_ = false;               // some row was set invalid since the last Reset
+    ValidityMask validity_;
     std::deque<string> heap_;
     vector<shared_ptr<void>> keep_;
     VectorType vtype_ = VectorType::FLAT_VECTOR;
@@ -317,12 +364,9 @@ struct FlatVector {
     static void SetData(Vector &v, data_ptr_t data) { v.SetDataPtr(data); }
     static void SetNull(Vector &v, idx_t i, bool is_null) { v.SetValid(i, !is_null); }
     static bool IsNull(const Vector &v, idx_t i) { return !v.RowIsValid(i); }
-    // DuckDB: FlatVector::Validity(v) -> ValidityMask (CheckAllValid(count))
-    struct ValidityView {
-        const Vector &v;
-        bool CheckAllValid(idx_t n) const { return v.AllValid(n); }
-    };
-    static ValidityView Validity(const Vector &v) { return ValidityView{v}; }
+    static ValidityMask &Validity(Vector &v) { return v.Validity(); }
+    static const ValidityMask &Validity(const Vector &v) { return v.Validity(); }
+    static void SetValidity(Vector &v, const ValidityMask &m) { v.Validity() = m; }
 };
 struct StringVector {
     static string_t AddString(Vector &v, const string &s) { return v.AddString(s); }
@@ -509,6 +553,7 @@ private:
 struct UnifiedVectorFormat {
     const SelectionVector *sel = nullptr;
     const_data_ptr_t data = nullptr;
+    ValidityMask validity;
 };
 class Expression {
 public:

@@ -153,14 +153,19 @@ def test_filters_on_boolean_and_blob(ext, gpu, tmpfile):
 
 @pytest.mark.gpu
 def test_scan_fastlanes_and_facade_render_boolean_blob(ext, gpu, tmpfile):
-    """scan_fastlanes (the reference facade: every column as VARCHAR) renders
-    BOOLEAN as true/false and BLOB as DuckDB's escaped text; the typed facade
+    """scan_fastlanes (the reference facade: its first column as VARCHAR)
+    renders BOOLEAN as true/false and BLOB as DuckDB's escaped text (BLOB
+    copied to the front with COPY (SELECT x, b ...)); the typed facade
     read API boxes Value::BOOLEAN / Value::BLOB."""
     n = 3000
     dst, b, x, ch = _copy_types(ext, tmpfile, n)
+    # the reference's scan_fastlanes binds one VARCHAR column, "data" (the first)
     _, types, rows = ext.query("scan_fastlanes", dst)
-    assert types == ["VARCHAR"] * 4
-    assert rows == [["true" if b[i] else "false", _duck_blob(x[i]), ch[i], str(i)] for i in range(n)]
+    assert types == ["VARCHAR"] and rows == [["true" if b[i] else "false"] for i in range(n)]
+    blob_first = tmpfile("blob_first.fls")
+    assert ext.copy("read_fastlanes", dst, blob_first, proj=[1, 0]) == n
+    _, types, rows = ext.query("scan_fastlanes", blob_first)
+    assert types == ["VARCHAR"] and rows == [[_duck_blob(x[i])] for i in range(n)]
     names, ftypes, frows, _ = ext.facade_read(dst)
     assert ftypes == ["BOOLEAN", "BLOB", "VARCHAR", "BIGINT"]
     assert frows == [["true" if b[i] else "false", _duck_blob(x[i]), ch[i], str(i)] for i in range(n)]
