@@ -56,7 +56,8 @@ class ColumnInfo(C.Structure):
 class RowGroup(C.Structure):
     _fields_ = [("rowgroup", C.c_uint32), ("nrows", C.c_uint32), ("first_row", C.c_uint64),
                 ("ncols", C.c_uint32), ("columns", C.POINTER(C.c_void_p)),
-                ("nrows_scanned", C.c_uint32), ("sel", C.POINTER(C.c_uint32))]
+                ("nrows_scanned", C.c_uint32), ("sel", C.POINTER(C.c_uint32)),
+                ("validity", C.POINTER(C.c_void_p))]
 
 
 class Predicate(C.Structure):
@@ -67,7 +68,7 @@ class Predicate(C.Structure):
 # fls_cmp (include/flsgpu.h)
 EQ, NE, LT, LE, GT, GE, IS_NULL, IS_NOT_NULL = range(8)
 OPS = {"=": EQ, "==": EQ, "!=": NE, "<>": NE, "<": LT, "<=": LE, ">": GT, ">=": GE,
-       "is_null": IS_NULL, "is_not_null": IS_NOT_NULL}
+       "is_null": IS_NULL, "is_not_null": IS_NOT_NULL, "false": 8}
 
 
 class DecodeStats(C.Structure):
@@ -117,6 +118,7 @@ _sig("fls_scan_filter", C.c_int, _P, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_scan_pruned", C.c_int, _P)
 _sig("fls_table_zonemap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
      C.POINTER(C.c_uint32))
+_sig("fls_table_validity", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)))
 _sig("fls_rowgroup_may_match", C.c_int, _P, C.c_uint32, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_device_upload", C.c_int, _P, C.c_uint32, C.c_uint32)
 _sig("fls_device_decode", C.c_int, _P, C.POINTER(C.c_uint8))
@@ -135,6 +137,8 @@ _sig("fls_writer_add_column", C.c_int, _P, C.c_char_p, C.c_uint8, C.c_uint8, C.c
 _sig("fls_writer_add_rowgroup", C.c_int, _P, C.c_uint32, C.POINTER(_P), C.POINTER(_P))
 _sig("fls_writer_set_threads", C.c_int, _P, C.c_int)
 _sig("fls_writer_add_rowgroups", C.c_int, _P, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(_P), C.POINTER(_P))
+_sig("fls_writer_add_rowgroups_v", C.c_int, _P, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(_P), C.POINTER(_P),
+     C.POINTER(_P))
 _sig("fls_writer_set_rowgroup_size", C.c_int, _P, C.c_uint32)
 _sig("fls_writer_set_device", C.c_int, _P, C.c_int)
 _sig("fls_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(_P))
@@ -251,7 +255,9 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
                 batch: int = 1, threads: int = 0) -> Image:
     """columns: list of (name, type, values, encoding[, width, scale]).
     values: numpy int array for integer types, float array for FLOAT/DOUBLE
-    (stored bit-exactly), list of str/bytes for VARCHAR.  device >= 0: the
+    (stored bit-exactly), list of str/bytes for VARCHAR.  NULLs: None entries
+    of a list, or the masked entries of a numpy.ma array (the rows' validity
+    goes to fls_writer_add_rowgroups_v).  device >= 0: the
     FFOR / DELTA integer columns are encoded on that GPU (same bytes).
     batch > 1: row groups go in `batch` at a time (fls_writer_add_rowgroups;
     same bytes).  threads > 0: writer threads (fls_writer_set_threads)."""
@@ -268,13 +274,20 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
             name, ty, vals, enc = spec[:4]
             width, scale = (spec[4], spec[5]) if len(spec) > 4 else (0, 0)
             _check(_lib.fls_writer_add_column(w, name.encode(), ty, width, scale, enc))
+            valid = None
+            if isinstance(vals, np.ma.MaskedArray):
+                valid = ~np.ma.getmaskarray(vals)
+                vals = vals.filled(0)
+            elif isinstance(vals, list) and any(v is None for v in vals):
+                valid = np.array([v is not None for v in vals], dtype=bool)
+                vals = [(b"" if ty in STRING_TYPES else 0) if v is None else v for v in vals]
             if ty in STRING_TYPES:
                 bs = [v.encode() if isinstance(v, str) else bytes(v) for v in vals]
-                prepped.append(("s", bs))
+                prepped.append(("s", bs, valid))
                 cnt = len(bs)
             else:
                 arr = np.ascontiguousarray(np.asarray(vals).astype(NP_DTYPE[ty]))
-                prepped.append(("i", arr))
+                prepped.append(("i", arr, valid))
                 cnt = len(arr)
             if n is None:
                 n = cnt
@@ -287,11 +300,17 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
             keep = []
             data = (_P * (nc * len(grp)))()
             offs = (_P * (nc * len(grp)))()
+            vmask = (_P * (nc * len(grp)))()
             rows = (C.c_uint32 * len(grp))()
             for k, r0 in enumerate(grp):
                 r1 = min(n, r0 + rowgroup)
                 rows[k] = r1 - r0
-                for c, (kind, v) in enumerate(prepped):
+                for c, (kind, v, valid) in enumerate(prepped):
+                    if valid is not None:
+                        words = np.packbits(valid[r0:r1], bitorder="little")
+                        words = np.concatenate([words, np.zeros((-len(words)) % 8, np.uint8)]).view(np.uint64)
+                        keep.append(words)
+                        vmask[k * nc + c] = words.ctypes.data
                     if kind == "i":
                         part = np.ascontiguousarray(v[r0:r1])
                         keep.append(part)
@@ -304,7 +323,9 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
                         keep += [o, buf]
                         data[k * nc + c] = buf.ctypes.data
                         offs[k * nc + c] = o.ctypes.data
-            if batch > 1:
+            if any(p[2] is not None for p in prepped):
+                _check(_lib.fls_writer_add_rowgroups_v(w, len(grp), rows, data, offs, vmask))
+            elif batch > 1:
                 _check(_lib.fls_writer_add_rowgroups(w, len(grp), rows, data, offs))
             else:
                 _check(_lib.fls_writer_add_rowgroup(w, rows[0], data, offs))
@@ -479,6 +500,40 @@ class Table:
             a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(rg.nrows * ob,))
             cols.append(a.copy() if copy else a)
         return cols
+
+    @staticmethod
+    def _rg_valid(rg: RowGroup):
+        """per column: bool per delivered row (False = NULL), or None when every
+        delivered row is valid (fls_rowgroup.validity)"""
+        out = []
+        for c in range(rg.ncols):
+            p = rg.validity[c] if rg.validity else None
+            if not p:
+                out.append(None)
+                continue
+            nw = (rg.nrows + 63) // 64
+            w = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint64)), shape=(max(1, nw),))
+            out.append(np.unpackbits(w.view(np.uint8), bitorder="little")[:rg.nrows].astype(bool))
+        return out
+
+    def scan_nulls(self, cols=None, rg_begin=0, rg_end=None):
+        """scan() that also yields each row group's validity and selection:
+        (first_row, arrays, valid per column (None: no NULL), sel or None)"""
+        if rg_end is None:
+            rg_end = self.nrowgroups
+        _check(_lib.fls_scan_begin(self.h, _mask(self, cols), rg_begin, rg_end))
+        out = RowGroup()
+        while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
+            sel = np.ctypeslib.as_array(out.sel, shape=(out.nrows,)).copy() if out.sel and out.nrows else None
+            yield out.first_row, self._rg_arrays(out), self._rg_valid(out), sel
+
+    def validity(self, rg: int, col: int):
+        """fls_table_validity: the chunk's validity words, or None (no NULL)"""
+        p = C.POINTER(C.c_uint64)()
+        if _check(_lib.fls_table_validity(self.h, rg, col, C.byref(p))) == 0:
+            return None
+        n = self.rowgroup_rows(rg)
+        return np.ctypeslib.as_array(p, shape=(16 * ((n + 1023) // 1024),)).copy()
 
     def materialize(self, rg: int, cols=None):
         out = RowGroup()

@@ -76,7 +76,11 @@ __device__ __forceinline__ int cmp_string(const DevTerm &t, const uint8_t *p, bo
 }
 
 __device__ __forceinline__ bool eval_term(const DevTerm &t, uint64_t row, bool &bad) {
-    if (t.op >= OP_IS_NULL) return t.op == OP_IS_NOT_NULL;
+    // one word per 64 rows: a wave's lanes read the same word (a broadcast)
+    const bool valid = !t.valid || ((t.valid[row >> 6] >> (row & 63)) & 1);
+    if (t.op == OP_FALSE) return false;
+    if (t.op >= OP_IS_NULL) return (t.op == OP_IS_NOT_NULL) == valid;
+    if (!valid) return false;  // a NULL row satisfies no comparison
     const uint8_t *p = t.col + row * t.ob;
     int c;
     switch (t.kind) {

@@ -14,8 +14,8 @@
 // The comparison semantics are DuckDB's, shared by both sides: signed /
 // unsigned integers, IEEE floats with NaN equal to NaN and above every
 // number and -0 == 0, strings compared bytewise (memcmp order, a proper
-// prefix sorts first).  The format has no NULLs: IS NULL never holds,
-// IS NOT NULL always does.
+// prefix sorts first).  NULL rows (the chunks' validity bitmaps) satisfy
+// IS NULL and no comparison, as in DuckDB; IS NOT NULL holds for the rest.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -30,7 +30,8 @@ enum FilterKind : uint8_t {
     FK_STR = 3,    // VARCHAR (string_t records)
 };
 enum FilterOp : uint8_t {
-    OP_EQ = 0, OP_NE = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_IS_NULL = 6, OP_IS_NOT_NULL = 7
+    OP_EQ = 0, OP_NE = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_IS_NULL = 6, OP_IS_NOT_NULL = 7,
+    OP_FALSE = 8  // no row (col <op> NULL)
 };
 
 __host__ __device__ inline bool op_holds(uint8_t op, int c) {
@@ -42,6 +43,7 @@ __host__ __device__ inline bool op_holds(uint8_t op, int c) {
     case OP_GT: return c > 0;
     case OP_GE: return c >= 0;
     case OP_IS_NULL: return false;
+    case OP_FALSE: return false;
     default: return true;  // IS NOT NULL
     }
 }
@@ -77,7 +79,8 @@ struct DevTerm {              // 64 B
     uint32_t str_len;
     uint8_t kind, op, ob;     // FilterKind, FilterOp, bytes per decoded value
     uint8_t end_clause;       // 1 on the last term of a clause
-    uint8_t pad[8];
+    const uint64_t *valid;    // the column's validity words for the batch rows (HBM), or
+                              // NULL when no row of the batch is NULL
 };
 static_assert(sizeof(DevTerm) == 64, "DevTerm is 64 B");
 

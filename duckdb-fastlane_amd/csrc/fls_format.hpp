@@ -148,6 +148,24 @@ inline uint32_t fsst_nseg(uint32_t comp_len) { return (comp_len + kFsstSegCodes 
 inline uint64_t fsst_seg_bytes(uint32_t comp_len) { return sizeof(FsstSegHeader) + ((fsst_nseg(comp_len) + 15ull) & ~15ull); }
 inline uint8_t fsst_seg_value(uint32_t dlen, uint32_t entry_state) { return (uint8_t)(entry_state ? 129 + dlen : dlen); }
 
+// Validity (NULLs, round 3).  A chunk with at least one NULL row sets
+// kChunkValidity in ChunkHeader.reserved0 and ends with nvec x 128 B of
+// bitmaps, 16-aligned at chunk_len - 128 * nvec: bit i of u64 word j of vector
+// v is 1 when row 1024 v + 64 j + i is valid (DuckDB's ValidityMask layout,
+// so a row group's bitmaps are its validity mask); bits past nvals are 0.
+// VecMeta.pad bit 0 (kVecHasNull) marks the vectors holding a NULL.  The
+// encoded values at NULL rows are placeholders the writer chose so they cost
+// nothing to encode (the chunk's previous valid value, 0 before the first;
+// the empty string): every reader masks them with the bitmap.  A chunk without
+// NULLs is byte-identical to a round-2 chunk.
+constexpr uint32_t kChunkValidity = 1u << 31;
+constexpr uint8_t kVecHasNull = 1;
+constexpr uint32_t kValidityVecBytes = kVectorSize / 8;  // 128
+inline bool chunk_has_validity(const ChunkHeader &h) { return (h.reserved0 & kChunkValidity) != 0; }
+// ChunkHeader.reserved0 without the validity flag (FSST: kFsstSegCodes or 0)
+inline uint32_t chunk_seg_codes(const ChunkHeader &h) { return h.reserved0 & ~kChunkValidity; }
+inline uint64_t validity_off(uint64_t chunk_len, uint32_t nvec) { return chunk_len - (uint64_t)kValidityVecBytes * nvec; }
+
 static_assert(sizeof(ChunkHeader) == 64, "chunk header is 64 B");
 static_assert(sizeof(VecMeta) == 32, "vector meta is 32 B");
 static_assert(alignof(VecMeta) == 8 && alignof(ChunkHeader) == 8, "natural alignment, no padding");
@@ -172,8 +190,10 @@ constexpr uint32_t kZoneMagic = 0x50414D5Au;  // "ZMAP"
 // signed integers (INT*, DATE, DECIMAL) as int64, unsigned as uint64,
 // FLOAT/DOUBLE as the IEEE bits of a double over the non-NaN values (NaN
 // sorts above every number, as in DuckDB).  VARCHAR has none: DICT chunks are
-// pruned on their dictionary instead.
-enum : uint32_t { ZM_VALID = 1, ZM_HAS_NAN = 2, ZM_ALL_NAN = 4 };
+// pruned on their dictionary instead.  Over the valid rows only: ZM_HAS_NULL
+// when the chunk has a NULL, ZM_ALL_NULL (and no ZM_VALID) when every row is
+// NULL; string columns carry these two flags alone.
+enum : uint32_t { ZM_VALID = 1, ZM_HAS_NAN = 2, ZM_ALL_NAN = 4, ZM_HAS_NULL = 8, ZM_ALL_NULL = 16 };
 struct ZoneMap {              // 24 B
     uint64_t min, max;
     uint32_t flags;

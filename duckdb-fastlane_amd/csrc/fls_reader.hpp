@@ -96,7 +96,7 @@ inline const char *validate_chunk(const uint8_t *img, const FileMeta &m, uint32_
             if (fh.clen_w > 32 || !fits(vm.aux_off, fsst_stream_off(fh) + fh.comp_len, h.aux_len) ||
                 fh.heap_off % 16 || fh.heap_off + (uint64_t)vm.aux_count > h.reserved1)
                 return "FSST vector out of bounds";
-            if (h.reserved0 == kFsstSegCodes) {  // segment table after the stream
+            if (chunk_seg_codes(h) == kFsstSegCodes) {  // segment table after the stream
                 if (!fits(vm.aux_off, fsst_seg_off(fh) + fsst_seg_bytes(fh.comp_len), h.aux_len))
                     return "FSST segment table out of bounds";
                 FsstSegHeader sh;
@@ -107,12 +107,18 @@ inline const char *validate_chunk(const uint8_t *img, const FileMeta &m, uint32_
     }
     if (h.enc == ENC_FSST) {
         if (h.aux_len < kFsstTableBytes || h.dict_count > 255) return "bad FSST symbol table";
-        if (h.reserved0 != 0 && h.reserved0 != kFsstSegCodes) return "bad FSST segment size";
+        if (chunk_seg_codes(h) != 0 && chunk_seg_codes(h) != kFsstSegCodes) return "bad FSST segment size";
         for (uint32_t k = 0; k < h.dict_count; ++k) {
             const uint8_t l = img[ch.off + h.aux_off + 8 * 256 + k];
             if (l < 1 || l > 8) return "bad FSST symbol length";
         }
         if (h.reserved1 > (1ull << 32)) return "FSST heap too large";
+    }
+    if (h.enc != ENC_FSST && chunk_seg_codes(h) != 0) return "bad chunk flags";
+    if (chunk_has_validity(h)) {  // bitmaps at the chunk's end, after everything else
+        if (ch.len < (uint64_t)kValidityVecBytes * h.nvec + sizeof(ChunkHeader)) return "validity out of bounds";
+        const uint64_t vo = validity_off(ch.len, h.nvec);
+        if (vo % 16 || vo < h.aux_off + h.aux_len || vo < h.meta_off + 32ull * h.nvec) return "validity out of bounds";
     }
     if (h.enc == ENC_DICT) {
         if (h.dict_count == 0) return "empty dictionary";
@@ -228,7 +234,7 @@ inline std::string parse_file(const uint8_t *img, uint64_t len, FileMeta &m) {
             z.resize(ncols);
             rd(p + 8 + (uint64_t)r * ncols * sizeof(ZoneMap), z.data(), ncols * sizeof(ZoneMap));
             for (uint32_t c = 0; c < ncols; ++c)
-                if (type_is_string(m.cols[c].type)) z[c].flags = 0;
+                if (type_is_string(m.cols[c].type)) z[c].flags &= ZM_HAS_NULL | ZM_ALL_NULL;
         }
     }
     return "";

@@ -7,6 +7,7 @@
 // (src/writer/write_fastlane.cpp:227, src/include/fastlanes_facade.hpp:39-43)
 // and the producer of every benchmark / test input (fls_gen.hpp).
 #include <algorithm>
+#include <cstddef>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -941,6 +942,13 @@ struct FileBuilder {
         uint32_t nrows;
         std::vector<std::vector<uint8_t>> chunks;
         std::vector<ZoneMap> zones;  // per column (VARCHAR: none)
+        // per column: the chunk's validity bitmaps (nvec x 128 B) when it has
+        // a NULL, else empty; appended to the chunk by finish()
+        std::vector<std::vector<uint64_t>> valid;
+        uint64_t chunk_len(size_t c) const {
+            const uint64_t n = chunks[c].size();
+            return c < valid.size() && !valid[c].empty() ? ((n + 15) & ~15ull) + 8ull * valid[c].size() : n;
+        }
     };
     std::vector<RG> rgs;
 
@@ -962,7 +970,7 @@ struct FileBuilder {
         for (auto &r : rgs) {
             put(&r.nrows, 4);
             for (size_t c = 0; c < cols.size(); ++c, ++k) {
-                uint64_t off = chunk_offs[k], len = r.chunks[c].size();
+                uint64_t off = chunk_offs[k], len = r.chunk_len(c);
                 put(&off, 8);
                 put(&len, 8);
             }
@@ -976,12 +984,36 @@ struct FileBuilder {
         return f;
     }
 
+    // A chunk's validity (fls_format.hpp): the bitmaps at its end, the flag in
+    // its header and the has-NULL mark of each vector holding a NULL.
+    static void append_validity(uint8_t *chunk, uint64_t enc_len, uint64_t len, const std::vector<uint64_t> &w) {
+        memcpy(chunk + len - 8 * w.size(), w.data(), 8 * w.size());
+        ChunkHeader h;
+        memcpy(&h, chunk, sizeof(h));
+        h.reserved0 |= kChunkValidity;
+        memcpy(chunk, &h, sizeof(h));
+        for (uint32_t v = 0; v < h.nvec; ++v) {
+            const uint32_t n = std::min<uint32_t>(kVectorSize, h.nvals - v * kVectorSize);
+            bool null = false;
+            for (uint32_t j = 0; j < 16; ++j) {
+                const uint32_t r0 = 64 * j;
+                const uint64_t live = r0 >= n ? 0 : (n - r0 >= 64 ? ~0ull : ((1ull << (n - r0)) - 1));
+                null |= (w[16 * v + j] & live) != live;
+            }
+            if (null) chunk[h.meta_off + 32ull * v + offsetof(VecMeta, pad)] |= kVecHasNull;
+        }
+        (void)enc_len;
+    }
+
     // Assemble into one malloc'ed image; chunk buffers are released as copied.
     int finish(uint8_t **img, uint64_t *len, int nthreads) {
         std::vector<uint64_t> offs;
         uint64_t off = 256;  // 8 B magic + 8 B version, padded to the chunk alignment
         for (auto &r : rgs)
-            for (auto &c : r.chunks) { offs.push_back(off); off += c.size(); }
+            for (size_t c = 0; c < r.chunks.size(); ++c) {
+                offs.push_back(off);
+                off += (r.chunk_len(c) + 15) & ~15ull;  // chunks start 16-aligned
+            }
         std::vector<uint8_t> ft = footer(offs);
         const uint64_t foot_off = off;
         const uint64_t total = off + ft.size() + 16;
@@ -999,7 +1031,12 @@ struct FileBuilder {
             for (size_t r; (r = next.fetch_add(1)) < rgs.size();) {
                 for (size_t c = 0; c < rgs[r].chunks.size(); ++c) {
                     auto &ch = rgs[r].chunks[c];
-                    memcpy(buf + offs[rg_first[r] + c], ch.data(), ch.size());
+                    uint8_t *dst = buf + offs[rg_first[r] + c];
+                    const uint64_t len = rgs[r].chunk_len(c);
+                    memcpy(dst, ch.data(), ch.size());
+                    memset(dst + ch.size(), 0, ((len + 15) & ~15ull) - ch.size());
+                    if (c < rgs[r].valid.size() && !rgs[r].valid[c].empty())
+                        append_validity(dst, ch.size(), len, rgs[r].valid[c]);
                     std::vector<uint8_t>().swap(ch);
                 }
             }
@@ -1587,7 +1624,43 @@ struct RgArgs {
     uint32_t nrows;
     const void *const *data;
     const uint32_t *const *offs;
+    const uint64_t *const *valid = nullptr;  // per column: validity words, or NULL (all valid)
 };
+
+// The chunk bitmaps of n rows from the caller's validity words (bits past n
+// cleared); false when every row is valid.  nnull: NULL rows.
+bool chunk_validity(const uint64_t *in, uint32_t n, std::vector<uint64_t> &w, uint32_t &nnull) {
+    nnull = 0;
+    if (!in) return false;
+    const uint32_t nw = (n + 63) / 64;
+    for (uint32_t j = 0; j < nw; ++j) {
+        const uint32_t r0 = 64 * j;
+        const uint64_t live = n - r0 >= 64 ? ~0ull : ((1ull << (n - r0)) - 1);
+        nnull += (uint32_t)__builtin_popcountll(~in[j] & live);
+    }
+    if (!nnull) return false;
+    w.assign(16ull * ((n + kVectorSize - 1) / kVectorSize), 0);
+    for (uint32_t j = 0; j < nw; ++j) {
+        const uint32_t r0 = 64 * j;
+        w[j] = in[j] & (n - r0 >= 64 ? ~0ull : ((1ull << (n - r0)) - 1));
+    }
+    return true;
+}
+inline bool row_valid(const std::vector<uint64_t> &w, uint32_t i) { return (w[i / 64] >> (i % 64)) & 1; }
+
+// Placeholders at NULL rows (fls_format.hpp): the previous valid value, the
+// first valid one for leading NULLs, 0 when every row is NULL; w bytes each.
+void fill_nulls(uint8_t *vals, uint32_t w, uint32_t n, const std::vector<uint64_t> &valid) {
+    uint32_t first = 0;
+    while (first < n && !row_valid(valid, first)) ++first;
+    if (first == n) {
+        memset(vals, 0, (size_t)n * w);
+        return;
+    }
+    for (uint32_t i = 0; i < first; ++i) memcpy(vals + (size_t)i * w, vals + (size_t)first * w, w);
+    for (uint32_t i = first + 1; i < n; ++i)
+        if (!row_valid(valid, i)) memcpy(vals + (size_t)i * w, vals + (size_t)(i - 1) * w, w);
+}
 
 // Append row groups a[0..nrg): every (row group, column) chunk is an
 // independent task on the writer's threads, VARCHAR chunks (the slowest) first,
@@ -1651,13 +1724,38 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         const ColSpec &cs = w->fb.cols[c];
         const uint32_t nrows = p.in->nrows;
         const void *data = p.in->data[c];
+        // NULLs: the chunk's bitmaps, placeholders at the NULL rows, zone-map flags
+        uint32_t nnull = 0;
+        const bool nulls = chunk_validity(p.in->valid ? p.in->valid[c] : nullptr, nrows, p.rg.valid[c], nnull);
+        const std::vector<uint64_t> &vw = p.rg.valid[c];
+        auto null_flags = [&](ZoneMap &z) {
+            if (!nulls) return;
+            z.flags |= ZM_HAS_NULL;
+            if (nnull == nrows) z = ZoneMap{0, 0, ZM_HAS_NULL | ZM_ALL_NULL, 0};
+        };
         if (type_is_string(cs.type)) {
-            p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows);
+            if (!nulls) {
+                p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows);
+                return;
+            }
+            // NULL rows as empty strings
+            const uint32_t *o = p.in->offs[c];
+            std::vector<uint32_t> no(nrows + 1, 0);
+            std::string bytes;
+            for (uint32_t i = 0; i < nrows; ++i) {
+                if (row_valid(vw, i)) bytes.append((const char *)data + o[i], o[i + 1] - o[i]);
+                no[i + 1] = (uint32_t)bytes.size();
+            }
+            p.rg.chunks[c] = encode_str_chunk(cs.enc, no.data(), bytes.data(), nrows);
+            null_flags(p.rg.zones[c]);
             return;
         }
+        const uint32_t vbytes = type_value_bits(cs.type) / 8;
         if (on_gpu[c]) {  // encoded by the GPU batch: staging copy and zone map here
-            memcpy(p.stage[c], data, (size_t)nrows * (type_value_bits(cs.type) / 8));
+            memcpy(p.stage[c], data, (size_t)nrows * vbytes);
+            if (nulls) fill_nulls(p.stage[c], vbytes, nrows, vw);
             p.rg.zones[c] = zone_of_typed(cs.type, p.stage[c], nrows);
+            null_flags(p.rg.zones[c]);
             if (cs.enc == ENC_AUTO) {  // the one ENC_AUTO estimate the GPU does not make
                 const size_t d = est_dict_typed(type_value_bits(cs.type), p.stage[c], nrows);
                 *p.est_dict[c] = d == SIZE_MAX ? UINT64_MAX : (uint64_t)d;
@@ -1672,8 +1770,10 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             memcpy(&x, src + (size_t)i * (T / 8), T / 8);
             v[i] = x;
         }
+        if (nulls) fill_nulls((uint8_t *)v.data(), 8, nrows, vw);
         p.rg.chunks[c] = encode_int_chunk(cs.type, cs.enc, v.data(), nrows);
         p.rg.zones[c] = zone_of(cs.type, v.data(), nrows);
+        null_flags(p.rg.zones[c]);
     };
     // encode the segment's chunks, then append its row groups in order
     auto run_seg = [&]() {
@@ -1697,6 +1797,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         p.rg.nrows = a[k].nrows;
         p.rg.chunks.resize(ncols);
         p.rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
+        p.rg.valid.assign(ncols, {});
         p.stage.assign(ncols, nullptr);
         p.est_dict.assign(ncols, nullptr);
         if (!gcols.empty()) {
@@ -1734,11 +1835,17 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
 
 int fls_writer_add_rowgroups(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
                              const uint32_t *const *str_offsets) {
+    return fls_writer_add_rowgroups_v(w, nrg, nrows, data, str_offsets, nullptr);
+}
+
+int fls_writer_add_rowgroups_v(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
+                               const uint32_t *const *str_offsets, const uint64_t *const *validity) {
     if (!w || !nrows || !data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroups: NULL argument");
     const size_t ncols = w->fb.cols.size();
     std::vector<RgArgs> a(nrg);
     for (uint32_t k = 0; k < nrg; ++k)
-        a[k] = RgArgs{nrows[k], data + k * ncols, str_offsets ? str_offsets + k * ncols : nullptr};
+        a[k] = RgArgs{nrows[k], data + k * ncols, str_offsets ? str_offsets + k * ncols : nullptr,
+                      validity ? validity + k * ncols : nullptr};
     return add_rowgroups_impl(w, nrg, a.data());
 }
 

@@ -265,6 +265,10 @@ struct HostBatch {
     uint32_t nvec = 0;                    // vectors of the batch
     bool sel_ready = false;               // sel_off computed from h_counts
     std::vector<uint32_t> sel_off;        // per row group of the batch (+1): first selected row
+    // per (rg - rg0) * ncols + col: the delivered rows' validity words (NULL:
+    // all valid) -- the file image's bitmaps, or, filtered, gathered into vbits
+    std::vector<const uint64_t *> valid_ptrs;
+    std::vector<std::vector<uint64_t>> vbits;
 };
 
 struct Slot {                       // one batch of row groups in flight
@@ -288,6 +292,7 @@ struct Slot {                       // one batch of row groups in flight
     DevBuf<uint32_t> d_counts;      // selected rows per vector
     PinBuf<uint8_t> h_fdesc;        // DevTerm[] + DevOut[] + constant strings
     DevBuf<uint8_t> d_fdesc;
+    std::vector<DevBuf<uint64_t>> d_valid;  // per filtered column with a NULL: batch validity words
 };
 
 // One GPU's scan pipeline: streams, the two device slots and the pinned
@@ -560,6 +565,14 @@ namespace {
 
 int out_bytes_of(const fls_table *t, uint32_t c) { return type_out_bytes(t->meta.cols[c].type); }
 
+// The validity bitmaps of chunk (rg, c) in the host image, or nullptr when the
+// chunk has no NULL (fls_format.hpp "Validity")
+const uint64_t *chunk_validity_host(const fls_table *t, uint32_t rg, uint32_t c) {
+    const ChunkRef &ch = t->meta.rgs[rg].chunks[c];
+    if (!chunk_has_validity(ch.hdr)) return nullptr;
+    return (const uint64_t *)(t->img + ch.off + validity_off(ch.len, ch.hdr.nvec));
+}
+
 // Build host string_t tables for the VARCHAR chunks of [rg0, rg1) and upload.
 int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBuf<StrT> &tab,
                   std::vector<uint64_t> &offs) {
@@ -622,7 +635,7 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
             memcpy(&fh, t->img + ch.off + h.aux_off + vm.aux_off, sizeof(fh));
             bc->packed += 128ull * vm.bw + 128ull * fh.clen_w + fh.comp_len;
             bc->meta += sizeof(fh);
-            if (h.reserved0 == kFsstSegCodes) bc->meta += sizeof(FsstSegHeader) + fsst_nseg(fh.comp_len);
+            if (chunk_seg_codes(h) == kFsstSegCodes) bc->meta += sizeof(FsstSegHeader) + fsst_nseg(fh.comp_len);
             // string-parallel kernel iff every string of the chunk is <= 255
             // bytes, decompressed and compressed (bounds from the two FFOR streams)
             const uint64_t dmax = (uint64_t)vm.for_base + (vm.bw >= 32 ? 0xFFFFFFFFull : (1ull << vm.bw) - 1);
@@ -637,7 +650,7 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
         bool short_syms = true;
         const uint8_t *lens = t->img + ch.off + h.aux_off + 8 * 256;
         for (uint32_t k = 0; k < h.dict_count && k < 255; ++k) short_syms &= lens[k] <= 7;
-        const bool seg = h.reserved0 == kFsstSegCodes && short_syms && !(sg && atoi(sg) == 0);
+        const bool seg = chunk_seg_codes(h) == kFsstSegCodes && short_syms && !(sg && atoi(sg) == 0);
         d.vbits = (sp ? 1 : 0) | (seg ? 2 : 0);
         return d;  // separate kernels, fixed LDS layouts
     }
@@ -896,10 +909,14 @@ namespace {
 
 // May any row of row group rg satisfy term h?  (zone maps / dictionary)
 bool term_may_match(const fls_table *t, uint32_t rg, const HostTerm &h) {
-    if (h.op == OP_IS_NULL) return false;  // the format has no NULLs
-    if (h.op == OP_IS_NOT_NULL) return true;
     const RowGroupMeta &r = t->meta.rgs[rg];
     const ChunkRef &ch = r.chunks[h.col];
+    // NULLs: the chunk's validity flag, and the zone map's all-NULL mark
+    const bool all_null = !r.zones.empty() && (r.zones[h.col].flags & ZM_ALL_NULL);
+    if (h.op == OP_FALSE) return false;
+    if (h.op == OP_IS_NULL) return chunk_has_validity(ch.hdr);
+    if (h.op == OP_IS_NOT_NULL) return !all_null;
+    if (all_null) return false;  // no valid row to compare
     if (h.kind == FK_STR) {
         if (ch.hdr.enc != ENC_DICT) return true;  // FSST: no statistics
         const uint8_t *aux = t->img + ch.off + ch.hdr.aux_off;
@@ -1055,6 +1072,31 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
         o.ob = (uint32_t)out_bytes_of(t, c);
         outs.push_back(o);
     }
+    // validity words of the batch rows for every filtered column with a NULL
+    // in the batch (row groups start at whole vectors: rows / 64 words apart)
+    sl.d_valid.resize(ncols);
+    std::vector<uint8_t> need(ncols, 0);
+    for (auto &h : s.terms) need[h.col] = 1;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        bool any = false;
+        for (uint32_t r = sl.rg0; need[c] && r < sl.rg0 + sl.nrg; ++r)
+            any = any || chunk_has_validity(t->meta.rgs[r].chunks[c].hdr);
+        if (!any) {
+            need[c] = 0;
+            continue;
+        }
+        HIP_TRY(sl.d_valid[c].alloc(d.dev, (rows + 63) / 64 + 16));
+        for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) {
+            const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+            uint64_t *dst = sl.d_valid[c].p + (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) / 64;
+            const size_t bytes = (size_t)kValidityVecBytes * ch.hdr.nvec;
+            if (chunk_has_validity(ch.hdr))
+                HIP_TRY(hipMemcpyAsync(dst, sl.d_in.p + (ch.off - in_lo) + validity_off(ch.len, ch.hdr.nvec), bytes,
+                                       hipMemcpyDeviceToDevice, sl.stream));
+            else
+                HIP_TRY(hipMemsetAsync(dst, 0xFF, bytes, sl.stream));
+        }
+    }
     const size_t nt = s.terms.size(), no = outs.size();
     size_t str_bytes = 0;
     for (auto &h : s.terms) str_bytes += (h.str.size() + 15) & ~size_t(15);
@@ -1074,6 +1116,7 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
         dt.op = h.op;
         dt.ob = (uint8_t)out_bytes_of(t, h.col);
         dt.end_clause = (i + 1 == nt || s.terms[i + 1].clause != h.clause) ? 1 : 0;
+        dt.valid = need[h.col] ? sl.d_valid[h.col].p : nullptr;
         if (h.kind == FK_STR) {
             memcpy(fd + so, h.str.data(), h.str.size());
             dt.str = sl.d_fdesc.p + so;
@@ -1224,6 +1267,12 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     }
     HIP_TRY(hipEventRecord(sl.done, sl.stream));
     hb.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
+    hb.valid_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
+    hb.vbits.resize((size_t)sl.nrg * ncols);
+    if (!filtered)  // every row delivered: the image's bitmaps are the validity masks
+        for (uint32_t r = 0; r < sl.nrg; ++r)
+            for (uint32_t c = 0; c < ncols; ++c)
+                if (col_selected(s.mask, c)) hb.valid_ptrs[(size_t)r * ncols + c] = chunk_validity_host(t, sl.rg0 + r, c);
     if (!filtered)
         for (uint32_t r = 0; r < sl.nrg; ++r)
             for (uint32_t c = 0; c < ncols; ++c)
@@ -1344,6 +1393,25 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         out->sel = hb->h_sel.p + hb->sel_off[i];
     }
     out->columns = hb->col_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
+    out->validity = hb->valid_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
+    if (out->sel) {  // filtered: the delivered rows' validity, gathered through sel
+        const size_t i0 = (size_t)(rg - hb->rg0) * ncols;
+        for (uint32_t c = 0; c < ncols; ++c) {
+            const uint64_t *img = col_selected(s.mask, c) ? chunk_validity_host(t, rg, c) : nullptr;
+            hb->valid_ptrs[i0 + c] = nullptr;
+            if (!img) continue;
+            std::vector<uint64_t> &w = hb->vbits[i0 + c];
+            w.assign(std::max<size_t>(1, (out->nrows + 63) / 64), 0);
+            bool any_null = false;
+            for (uint32_t i = 0; i < out->nrows; ++i) {
+                const uint32_t r = out->sel[i];
+                const uint64_t b = (img[r >> 6] >> (r & 63)) & 1;
+                w[i >> 6] |= b << (i & 63);
+                any_null |= !b;
+            }
+            if (any_null) hb->valid_ptrs[i0 + c] = w.data();
+        }
+    }
     std::lock_guard<std::mutex> lk(s.mu);
     s.out.emplace_back(rg, hb);
     if (++hb->handed == hb->nrg) {
@@ -1401,7 +1469,7 @@ int to_terms(const fls_table *t, const fls_predicate *p, uint32_t n, std::vector
     if (n && !p) return fail(FLS_ERR_ARG, "fls_scan_filter: NULL predicates");
     for (uint32_t i = 0; i < n; ++i) {
         if (p[i].col >= t->meta.cols.size()) return fail(FLS_ERR_ARG, "filter column %u out of range", p[i].col);
-        if (p[i].op > FLS_CMP_IS_NOT_NULL) return fail(FLS_ERR_ARG, "filter operator %u unknown", p[i].op);
+        if (p[i].op > FLS_CMP_FALSE) return fail(FLS_ERR_ARG, "filter operator %u unknown", p[i].op);
         HostTerm h;
         h.col = p[i].col;
         h.clause = p[i].clause;
@@ -1698,11 +1766,19 @@ int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *m
     if (!t || rg >= t->meta.rgs.size() || col >= t->meta.cols.size())
         return fail(FLS_ERR_ARG, "zone map (%u, %u) out of range", rg, col);
     const auto &z = t->meta.rgs[rg].zones;
-    if (z.empty() || !(z[col].flags & ZM_VALID)) return 0;
+    if (z.empty() || !(z[col].flags & (ZM_VALID | ZM_HAS_NULL | ZM_ALL_NULL))) return 0;
     if (min) *min = z[col].min;
     if (max) *max = z[col].max;
     if (flags) *flags = z[col].flags;
     return 1;
+}
+
+int fls_table_validity(const fls_table *t, uint32_t rg, uint32_t col, const uint64_t **words) {
+    if (!t || rg >= t->meta.rgs.size() || col >= t->meta.cols.size())
+        return fail(FLS_ERR_ARG, "validity (%u, %u) out of range", rg, col);
+    const uint64_t *w = chunk_validity_host(t, rg, col);
+    if (words) *words = w;
+    return w ? 1 : 0;
 }
 
 int fls_rowgroup_may_match(const fls_table *t, uint32_t rg, const fls_predicate *preds, uint32_t n) {

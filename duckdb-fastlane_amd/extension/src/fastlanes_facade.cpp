@@ -150,7 +150,15 @@ bool FastLanesFacade::readNextChunk(DataChunk &result) {
         for (idx_t c = 0; c < ncols; ++c) {
             Vector &vec = result.data[c];
             const void *col = s.rg.columns[c];
-            for (idx_t i = 0; i < n; ++i) RenderCell(vec, i, s.cols[c], col, s.current_row + i);
+            const uint64_t *valid = s.rg.validity ? s.rg.validity[c] : nullptr;
+            for (idx_t i = 0; i < n; ++i) {
+                const idx_t row = s.current_row + i;
+                if (valid && !((valid[row / 64] >> (row % 64)) & 1)) {
+                    FlatVector::SetNull(vec, i, true);  // a NULL row, as the reference's monostate (:113-117)
+                    continue;
+                }
+                RenderCell(vec, i, s.cols[c], col, row);
+            }
         }
         s.current_row += n;
         return true;

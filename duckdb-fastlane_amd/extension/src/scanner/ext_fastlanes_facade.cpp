@@ -109,6 +109,7 @@ public:
     // recycled through `spare`.
     struct Batch {
         std::vector<RawBuf> cols, rec, arena;
+        std::vector<RawBuf> valid;  // per column: validity words of the batch rows, or empty (no NULL)
         std::vector<std::vector<uint32_t>> offs;  // per row group k: rows_k + 1 offsets from k * (rg_rows + 1)
         std::vector<std::vector<uint64_t>> base;  // per row group: its first byte in cols[c]
     };
@@ -160,6 +161,9 @@ public:
     // pointer field it rewrites to their offset in warena; the background
     // task turns them into the writer's bytes + offsets, a thread per column
     std::vector<RawBuf> wrec, warena;
+    // per column: validity words of the buffered rows (DuckDB's layout, bit r
+    // = row r), allocated at the column's first NULL; empty: every row valid
+    std::vector<RawBuf> wvalid;
     // string bytes per VARCHAR column in the stage's last (partial) row group:
     // the writer's offsets are 32-bit per row group
     std::vector<uint64_t> wbytes;
@@ -182,7 +186,7 @@ FastLanesFacade::Impl::~Impl() {
 }
 
 void FastLanesFacade::Impl::reset_stage(Stage &st) const {
-    for (auto *b : {&st.wcols, &st.wrec, &st.warena}) {
+    for (auto *b : {&st.wcols, &st.wrec, &st.warena, &st.wvalid}) {
         b->resize(wtypes.size());
         for (auto &x : *b) x.clear();
     }
@@ -192,7 +196,7 @@ void FastLanesFacade::Impl::reset_stage(Stage &st) const {
 
 uint64_t FastLanesFacade::Impl::staged_bytes(const Stage &st) {
     uint64_t bytes = 0;
-    for (auto *b : {&st.wcols, &st.wrec, &st.warena})
+    for (auto *b : {&st.wcols, &st.wrec, &st.warena, &st.wvalid})
         for (auto &x : *b) bytes += x.size();
     return bytes;
 }
@@ -295,7 +299,12 @@ bool FastLanesFacade::readNextChunk(std::vector<Value> &values, idx_t &rows_read
     const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, s.rg.nrows - s.rg_pos);
     values.reserve(n * s.cols.size());
     for (idx_t r = 0; r < n; ++r)
-        for (size_t c = 0; c < s.cols.size(); ++c) values.push_back(BoxValue(s.cols[c], s.rg.columns[c], s.rg_pos + r));
+        for (size_t c = 0; c < s.cols.size(); ++c) {
+            const idx_t row = s.rg_pos + r;
+            const uint64_t *valid = s.rg.validity ? s.rg.validity[c] : nullptr;
+            values.push_back(valid && !((valid[row / 64] >> (row % 64)) & 1) ? Value()
+                                                                               : BoxValue(s.cols[c], s.rg.columns[c], row));
+        }
     s.rg_pos += n;
     rows_read = n;
     return true;
@@ -363,12 +372,13 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
     }
     if (!bp) bp.reset(new Batch());
     Batch *b = bp.release();
-    for (auto *x : {&b->cols, &b->rec, &b->arena}) x->resize(wtypes.size());
+    for (auto *x : {&b->cols, &b->rec, &b->arena, &b->valid}) x->resize(wtypes.size());
     b->offs.resize(wtypes.size());
     b->base.resize(wtypes.size());
     std::swap(b->cols, st.wcols);
     std::swap(b->rec, st.wrec);
     std::swap(b->arena, st.warena);
+    std::swap(b->valid, st.wvalid);
     const uint32_t rows = (uint32_t)st.wrows;
     reset_stage(st);
     account(st);
@@ -452,13 +462,36 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
                 }
             }
         }
-        const int rc = fls_writer_add_rowgroups(writer, nrg, nrows.data(), data.data(), offs.data());
+        // NULLs: row group k's validity words from word k * rg_rows / 64
+        std::vector<const uint64_t *> valid((size_t)nrg * nc, nullptr);
+        for (uint32_t k = 0; k < nrg; ++k)
+            for (size_t c = 0; c < nc; ++c)
+                if (!b->valid[c].empty())
+                    valid[k * nc + c] = (const uint64_t *)b->valid[c].data() + (size_t)k * rg_rows / 64;
+        const int rc = fls_writer_add_rowgroups_v(writer, nrg, nrows.data(), data.data(), offs.data(), valid.data());
         std::string e = rc == 0 ? std::string() : std::string(fls_last_error());
         if (prof.on) encode_s += CopyProfile::now() - t0;
         recycle();
         return e;
     }).share());
     return true;
+}
+
+// Validity of stage rows [at, at + n) from `valid(i)` for i < n: the stage's
+// words are allocated (every earlier row valid) at the column's first NULL
+// and grow with the rows from then on (new words all valid).
+template <class F>
+static void StageValidity(RawBuf &words, idx_t at, idx_t n, bool any_null, F &&valid) {
+    if (!any_null && words.empty()) return;
+    const size_t need = 8 * ((at + n + 63) / 64);
+    if (words.size() < need) {
+        const size_t more = need - words.size();
+        memset(words.grow(more), 0xFF, more);
+    }
+    if (!any_null) return;
+    uint64_t *w = (uint64_t *)words.data();
+    for (idx_t i = 0; i < n; ++i)
+        if (!valid(i)) w[(at + i) / 64] &= ~(1ull << ((at + i) % 64));
 }
 
 // DuckDB's physical width of a fixed-size column (DECIMAL narrows with width)
@@ -490,14 +523,6 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
         tp = t;
     };
     chunk.Flatten();
-    // The container has no validity bitmap yet: a NULL would come back as 0 or
-    // '' and a pushed-down IS NULL would match nothing, so refuse it instead of
-    // writing a value (nothing of this chunk is appended).
-    for (size_t c = 0; c < s.wtypes.size(); ++c)
-        if (!FlatVector::Validity(chunk.data[c]).CheckAllValid(chunk.size())) {
-            st.error = "column \"" + s.wnames[c] + "\" holds NULL values, which the FastLanes writer cannot store";
-            return false;
-        }
     lap(s.prof.prep);
     // column-major: append each column's slice up to the row-group boundary
     // in bulk; a full batch of row groups goes to the writer
@@ -509,12 +534,19 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
             RawBuf &col = st.wcols[c];
+            const ValidityMask &mask = FlatVector::Validity(v);
+            const bool nulls = !mask.AllValid();
+            StageValidity(st.wvalid[c], st.wrows, n, nulls, [&](idx_t i) { return mask.RowIsValid(r0 + i); });
             if (TypeMapping::IsString(t)) {
-                // the records in one copy; the non-inlined strings' bytes to
-                // the arena, their pointer field := arena offset
-                const string_t *str = FlatVector::GetData<string_t>(v) + r0;
+                // the records in one copy (a NULL row's record, undefined in
+                // DuckDB, becomes the empty string); the non-inlined strings'
+                // bytes to the arena, their pointer field := arena offset
                 uint8_t *rec = st.wrec[c].grow(n * sizeof(string_t));
-                memcpy(rec, str, n * sizeof(string_t));
+                memcpy(rec, FlatVector::GetData<string_t>(v) + r0, n * sizeof(string_t));
+                if (nulls)
+                    for (idx_t r = 0; r < n; ++r)
+                        if (!mask.RowIsValid(r0 + r)) memset(rec + sizeof(string_t) * r, 0, sizeof(string_t));
+                const string_t *str = (const string_t *)rec;
                 // lengths and the positions of the non-inlined strings without
                 // a data-dependent branch (inlined and pointer strings alternate
                 // unpredictably in a column like l_shipinstruct), then their bytes
@@ -606,6 +638,7 @@ bool FastLanesFacade::mergeStage(Stage &st) {
         std::swap(o.wcols, st.wcols);
         std::swap(o.wrec, st.wrec);
         std::swap(o.warena, st.warena);
+        std::swap(o.wvalid, st.wvalid);
         std::swap(o.wbytes, st.wbytes);
         std::swap(o.wrows, st.wrows);
         std::swap(o.accounted, st.accounted);
@@ -621,6 +654,11 @@ bool FastLanesFacade::mergeStage(Stage &st) {
     while (r0 < st.wrows) {
         const idx_t n = std::min<idx_t>(st.wrows - r0, s.rg_rows - o.wrows % s.rg_rows);
         for (size_t c = 0; c < nc; ++c) {
+            const RawBuf &sv = st.wvalid[c];
+            StageValidity(o.wvalid[c], o.wrows, n, !sv.empty(), [&](idx_t i) {
+                const idx_t r = r0 + i;
+                return ((((const uint64_t *)sv.data())[r / 64] >> (r % 64)) & 1) != 0;
+            });
             if (TypeMapping::IsString(s.wtypes[c])) {
                 const uint8_t *src = st.wrec[c].data() + sizeof(string_t) * r0;
                 uint8_t *rec = o.wrec[c].grow(n * sizeof(string_t));

@@ -185,7 +185,7 @@ bool MakeTerm(uint32_t col, uint32_t clause, uint8_t op, const Value &v, const L
     p.clause = clause;
     p.op = op;
     if (v.IsNull()) {  // a comparison with NULL is never true
-        p.op = FLS_CMP_IS_NULL;
+        p.op = FLS_CMP_FALSE;
         return true;
     }
     switch (type.id()) {
@@ -386,6 +386,13 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
 // narrowed to DuckDB's physical width
 void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector &vec, idx_t n) {
     const idx_t ob = bind.cols[id].out_bytes;
+    // NULLs: the delivered rows' validity words (rg_pos is a multiple of
+    // STANDARD_VECTOR_SIZE, so whole words)
+    if (const uint64_t *valid = l.rg.validity ? l.rg.validity[id] : nullptr) {
+        auto &mask = FlatVector::Validity(vec);
+        mask.Initialize(STANDARD_VECTOR_SIZE);
+        memcpy(mask.GetData(), valid + l.rg_pos / 64, ValidityMask::EntryCount(n) * sizeof(validity_t));
+    }
     const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
     const idx_t phys = vec.GetType().PhysicalSize();
     if (phys == ob) {

@@ -74,6 +74,13 @@ typedef struct fls_rowgroup {
     const uint32_t *sel;          /* filtered scan: the delivered rows' indices
                                      within the row group (ascending); NULL
                                      when every row is delivered */
+    const uint64_t *const *validity; /* ncols pointers: the delivered rows'
+                                     validity mask in DuckDB's layout (bit i
+                                     of word i / 64 set when delivered row i
+                                     is not NULL), or NULL when every
+                                     delivered row is valid (and for columns
+                                     not selected).  Values at NULL rows are
+                                     placeholders.  Valid as long as columns. */
 } fls_rowgroup;
 
 /* Pushed-down filter term: `column <op> constant` (DuckDB TableFilterSet:
@@ -82,7 +89,8 @@ typedef struct fls_rowgroup {
  * Terms with equal `clause` are OR-ed, clauses are AND-ed. */
 typedef enum fls_cmp {
     FLS_CMP_EQ = 0, FLS_CMP_NE = 1, FLS_CMP_LT = 2, FLS_CMP_LE = 3, FLS_CMP_GT = 4, FLS_CMP_GE = 5,
-    FLS_CMP_IS_NULL = 6, FLS_CMP_IS_NOT_NULL = 7
+    FLS_CMP_IS_NULL = 6, FLS_CMP_IS_NOT_NULL = 7,
+    FLS_CMP_FALSE = 8             /* holds for no row (a comparison with a NULL constant) */
 } fls_cmp;
 typedef struct fls_predicate {
     uint32_t col;                 /* table column */
@@ -167,8 +175,16 @@ int fls_scan_filter(fls_table *t, const fls_predicate *preds, uint32_t n);
 int fls_scan_pruned(const fls_table *t);
 /* Zone map of column col in row group rg: 1 and *min / *max (int64, uint64
  * or double bits by column type, see fls_predicate.value; FLOAT widened to
- * double) when present, 0 when the file has none for it. */
+ * double) and *flags (1 valid, 2 / 4 has / all NaN, 8 / 16 has / all NULL;
+ * min / max over the non-NULL rows) when present, 0 when the file has none
+ * for it. */
 int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *min, uint64_t *max, uint32_t *flags);
+/* Validity of column col in row group rg: 1 and *words = its bitmaps in the
+ * host image (16 u64 words per 1024-row vector, DuckDB's layout: bit i of
+ * word j set when row 64 j + i is valid) when the chunk holds a NULL, 0 (and
+ * *words = NULL) when every row is valid.  Valid while the table is open;
+ * for consumers of the device-resident columns (fls_device_column). */
+int fls_table_validity(const fls_table *t, uint32_t rg, uint32_t col, const uint64_t **words);
 /* May a row of row group rg satisfy the filter?  (1 yes / 0 no; host only) */
 int fls_rowgroup_may_match(const fls_table *t, uint32_t rg, const fls_predicate *preds, uint32_t n);
 

@@ -82,6 +82,14 @@ int fls_writer_add_rowgroup(fls_writer *w, uint32_t nrows, const void *const *da
  * idle the other threads (the COPY sink hands over 8 row groups at a time). */
 int fls_writer_add_rowgroups(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
                              const uint32_t *const *str_offsets);
+/* The same with NULLs: validity[k * ncols + c] is row group k's validity mask
+ * of column c in DuckDB's layout (u64 words, bit i of word j set when row
+ * 64 j + i is valid) or NULL when every row is valid; validity itself may be
+ * NULL.  Values (and string bytes) at NULL rows are ignored.  A chunk with a
+ * NULL stores its bitmaps (csrc/fls_format.hpp, "Validity"); replaces the
+ * reference writer's NULL tracking (src/writer/write_fastlane.cpp:207-208). */
+int fls_writer_add_rowgroups_v(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
+                               const uint32_t *const *str_offsets, const uint64_t *const *validity);
 /* Assemble the file: to `path`, or into a malloc'ed buffer freed with
  * fls_image_free. */
 int fls_writer_finish_file(fls_writer *w, const char *path);

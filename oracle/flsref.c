@@ -250,6 +250,35 @@ static void delta_vector(int T, const uint64_t *u, uint64_t for_base,
     }
 }
 
+int flsref_validity(const flsref_file *f, uint32_t col, uint32_t rg, uint64_t *words)
+{
+    if (col >= f->ncols || rg >= f->nrowgroups) return -1;
+    const uint8_t *rgp = rg_desc(f, rg);
+    const uint64_t coff = rd64(rgp + 4 + 16 * (size_t)col);
+    const uint64_t clen = rd64(rgp + 4 + 16 * (size_t)col + 8);
+    if (coff + clen > f->len || clen < 64) return -1;
+    const uint8_t *ch = f->img + coff;
+    if (!(rd32(ch + 52) & 0x80000000u)) return 0;
+    const uint32_t nvec = rd32(ch + 8), nvals = rd32(ch + 12);
+    if (clen < 64 + 128ull * nvec) return -1;
+    const uint8_t *bits = ch + clen - 128ull * nvec;
+    const uint8_t *meta = ch + rd64(ch + 16);
+    for (uint32_t v = 0; v < nvec; ++v) {
+        const uint32_t n = nvals - 1024 * v < 1024 ? nvals - 1024 * v : 1024;
+        int has_null = 0;
+        for (uint32_t j = 0; j < 16; ++j) {
+            const uint64_t w = rd64(bits + 128ull * v + 8 * j);
+            const uint32_t r0 = 64 * j;
+            const uint64_t live = r0 >= n ? 0 : (n - r0 >= 64 ? ~0ull : ((1ull << (n - r0)) - 1));
+            if (w & ~live) return -1;            /* bits past the rows */
+            if ((w & live) != live) has_null = 1;
+            words[16 * (size_t)v + j] = w;
+        }
+        if (has_null != (meta[32 * (size_t)v + 27] & 1)) return -1;  /* VecMeta.pad */
+    }
+    return 1;
+}
+
 int64_t flsref_decode(const flsref_file *f, uint32_t col, uint32_t rg, void *out_v)
 {
     uint8_t *out = (uint8_t *)out_v;
@@ -450,7 +479,7 @@ int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, u
         uint64_t cu[1024];
         flsref_unpack(32, (int)cw, vh + 16, cu);
         const uint8_t *cs = vh + 16 + 128 * (size_t)cw;
-        if (rd32(ch + 52) == 16 && fsst_check_segments(aux, cs, clen, cs + ((clen + 15u) & ~15u)) != 0) return -1;
+        if ((rd32(ch + 52) & 0x7FFFFFFFu) == 16 && fsst_check_segments(aux, cs, clen, cs + ((clen + 15u) & ~15u)) != 0) return -1;
         /* every string is compressed on its own: expand string by string */
         uint64_t sum = 0, cpos = 0;
         for (uint32_t i = 0; i < vn; ++i) {

@@ -123,6 +123,14 @@ int64_t flsref_decode_strings(const flsref_file *f, uint32_t col, uint32_t rg, u
  * nthreads > 1 decodes row groups in parallel (CPU baseline).  Returns rows. */
 int64_t flsref_decode_column(const flsref_file *f, uint32_t col, void *out, int nthreads);
 
+/* Validity of column col, row group rg (NULLs; csrc/fls_format.hpp): when the
+ * chunk carries bitmaps (ChunkHeader.reserved0 bit 31), words receives
+ * 16 * nvec u64 words (bit i of word j: row 64 j + i valid) and 1 is
+ * returned; 0 when every row is valid (words untouched); -1 when the bitmaps
+ * are out of bounds, set bits past the chunk's rows, or disagree with the
+ * vectors' has-NULL marks (VecMeta.pad bit 0). */
+int flsref_validity(const flsref_file *f, uint32_t col, uint32_t rg, uint64_t *words);
+
 /* Bytes per output value of column col (1/2/4/8, or 16 for VARCHAR pairs). */
 int flsref_out_width(const flsref_file *f, uint32_t col);
 

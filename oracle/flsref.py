@@ -43,6 +43,8 @@ _lib.flsref_decode_column.restype = C.c_int64
 _lib.flsref_decode_column.argtypes = [C.POINTER(_File), C.c_uint32, C.c_void_p, C.c_int]
 _lib.flsref_decode_strings.restype = C.c_int64
 _lib.flsref_decode_strings.argtypes = [C.POINTER(_File), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64]
+_lib.flsref_validity.restype = C.c_int
+_lib.flsref_validity.argtypes = [C.POINTER(_File), C.c_uint32, C.c_uint32, C.c_void_p]
 _lib.flsref_out_width.restype = C.c_int
 _lib.flsref_out_width.argtypes = [C.POINTER(_File), C.c_uint32]
 
@@ -157,6 +159,26 @@ class RefFile:
 
         with ThreadPoolExecutor(max(1, nthreads)) as ex:
             return sum(ex.map(one, range(self.nrowgroups)))
+
+    def validity(self, c: int, rg: int):
+        """The chunk's validity words (u64, bit i of word j = row 64 j + i
+        valid), or None when every row is valid (flsref_validity)."""
+        n = self.rowgroup_rows(rg)
+        words = np.zeros(16 * ((n + 1023) // 1024), dtype=np.uint64)
+        got = _lib.flsref_validity(C.byref(self.f), c, rg, words.ctypes.data)
+        if got < 0:
+            raise ValueError(f"flsref_validity failed on col {c} rg {rg}")
+        return words if got == 1 else None
+
+    def valid_column(self, c: int) -> np.ndarray:
+        """bool per row of column c: True where the row is not NULL"""
+        parts = []
+        for rg in range(self.nrowgroups):
+            n = self.rowgroup_rows(rg)
+            w = self.validity(c, rg)
+            parts.append(np.ones(n, dtype=bool) if w is None
+                         else np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(bool))
+        return np.concatenate(parts) if parts else np.zeros(0, dtype=bool)
 
     def strings_column(self, c: int) -> list[bytes]:
         out = []
