@@ -200,6 +200,16 @@ def test_scan_delivers_validity_unfiltered_and_filtered(fl, gpu, rowgroup):
     t.set_filter([])
 
 
+def _shortest_g(t):
+    """the harness's DOUBLE -> VARCHAR rendering: the shortest %g that reads back"""
+    x = float(t)
+    for p in range(1, 18):
+        r = "%.*g" % (p, x)
+        if float(r) == x:
+            return r
+    return repr(x)
+
+
 def _nullable_values(n, seed):
     """COPY ... VALUES columns with NULLs (cells as text, None = NULL) and the
     text DuckDB renders for each cell"""
@@ -221,7 +231,7 @@ def _nullable_values(n, seed):
     ]
     shown = {
         "i": lambda t: t, "big": lambda t: t, "s": lambda t: t, "b": lambda t: t, "z": lambda t: t,
-        "d": lambda t: ("%r" % float(t)).rstrip("0").rstrip(".") if "." in ("%r" % float(t)) else "%r" % float(t),
+        "d": _shortest_g,
         "x": lambda t: "".join(chr(c) if 32 <= c <= 126 and chr(c) not in "\\'\"" else "\\x%02X" % c
                                for c in bytes.fromhex(t)),
         "m": lambda t: t,
