@@ -57,7 +57,8 @@ class RowGroup(C.Structure):
     _fields_ = [("rowgroup", C.c_uint32), ("nrows", C.c_uint32), ("first_row", C.c_uint64),
                 ("ncols", C.c_uint32), ("columns", C.POINTER(C.c_void_p)),
                 ("nrows_scanned", C.c_uint32), ("sel", C.POINTER(C.c_uint32)),
-                ("validity", C.POINTER(C.c_void_p))]
+                ("validity", C.POINTER(C.c_void_p)), ("dict", C.POINTER(C.c_void_p)),
+                ("dict_size", C.POINTER(C.c_uint32)), ("dict_width", C.POINTER(C.c_uint8))]
 
 
 class Predicate(C.Structure):
@@ -118,6 +119,7 @@ _sig("fls_scan_filter", C.c_int, _P, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_scan_pruned", C.c_int, _P)
 _sig("fls_table_zonemap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
      C.POINTER(C.c_uint32))
+_sig("fls_scan_dict_codes", C.c_int, _P, C.c_int)
 _sig("fls_table_validity", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)))
 _sig("fls_rowgroup_may_match", C.c_int, _P, C.c_uint32, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_device_upload", C.c_int, _P, C.c_uint32, C.c_uint32)
@@ -494,6 +496,8 @@ class Table:
                 cols.append(None)
                 continue
             ob = sch[c][4]
+            if rg.dict and rg.dict[c]:
+                ob = rg.dict_width[c]  # dictionary codes (fls_scan_dict_codes)
             if rg.nrows == 0:
                 cols.append(np.zeros(0, dtype=np.uint8))
                 continue
@@ -526,6 +530,31 @@ class Table:
         while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
             sel = np.ctypeslib.as_array(out.sel, shape=(out.nrows,)).copy() if out.sel and out.nrows else None
             yield out.first_row, self._rg_arrays(out), self._rg_valid(out), sel
+
+    def dict_codes(self, enable: bool = True):
+        """fls_scan_dict_codes: the next scan delivers DICT string columns as
+        codes (scan_dicts yields their dictionaries)"""
+        _check(_lib.fls_scan_dict_codes(self.h, int(enable)))
+
+    def scan_dicts(self, cols=None, rg_begin=0, rg_end=None):
+        """scan() yielding (first_row, arrays, dicts): dicts[c] is the row
+        group's dictionary (string_t records, bytes) for a coded column, whose
+        array then holds its codes (u8 / u16), else None"""
+        if rg_end is None:
+            rg_end = self.nrowgroups
+        _check(_lib.fls_scan_begin(self.h, _mask(self, cols), rg_begin, rg_end))
+        out = RowGroup()
+        while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
+            dicts = []
+            for c in range(out.ncols):
+                p = out.dict[c] if out.dict else None
+                dicts.append(None if not p else np.ctypeslib.as_array(
+                    C.cast(p, C.POINTER(C.c_uint8)), shape=(16 * out.dict_size[c],)).copy())
+            arrays = self._rg_arrays(out)
+            for c, dct in enumerate(dicts):
+                if dct is not None:
+                    arrays[c] = arrays[c].view(np.uint8 if out.dict_width[c] == 1 else np.uint16)
+            yield out.first_row, arrays, dicts
 
     def validity(self, rg: int, col: int):
         """fls_table_validity: the chunk's validity words, or None (no NULL)"""

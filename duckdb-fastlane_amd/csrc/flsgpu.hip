@@ -269,6 +269,12 @@ struct HostBatch {
     // all valid) -- the file image's bitmaps, or, filtered, gathered into vbits
     std::vector<const uint64_t *> valid_ptrs;
     std::vector<std::vector<uint64_t>> vbits;
+    // dictionary-coded delivery (fls_scan_dict_codes): per column the bytes
+    // delivered per row (string_t 16, or a code width 1 / 2), per (rg - rg0) *
+    // ncols + col the host string_t dictionary and its size (NULL: not coded)
+    std::vector<uint8_t> ob;
+    std::vector<const void *> dict_ptrs;
+    std::vector<uint32_t> dict_sizes;
 };
 
 struct Slot {                       // one batch of row groups in flight
@@ -300,6 +306,8 @@ struct Slot {                       // one batch of row groups in flight
 // (ConnRes::take) and the table gives it back when it closes, so the next
 // table -- a new DuckDB query -- starts without stream creation, hipMalloc or
 // hipHostMalloc.
+constexpr size_t kIdent16 = 256;  // ScanDev::ident: where the u16 identity table starts
+
 struct ScanDev {
     int dev = -1;
     hipStream_t stream = nullptr;
@@ -311,6 +319,10 @@ struct ScanDev {
     std::vector<HostBatch *> free_batches;
     DevBuf<StrT> strtab;
     std::vector<uint64_t> strtab_off;
+    std::vector<StrT> h_strtab;     // host copy of strtab (the dictionaries coded columns reference)
+    // identity "dictionaries" a coded column gathers its codes from: u8 0..255
+    // at byte 0, u16 0..65535 at byte kIdent16
+    DevBuf<uint8_t> ident;
     DevBuf<uint32_t> err;
     int grid = 0;
     ScanDev() = default;
@@ -346,6 +358,7 @@ struct ScanCtx {
     std::vector<uint8_t> mask;      // delivered columns
     std::vector<uint8_t> dmask;     // decoded columns (delivered + filter columns)
     std::vector<HostTerm> terms;    // filter of this scan, sorted by clause (empty: none)
+    bool dict_codes = false;        // deliver DICT string chunks as codes + dictionary
     std::vector<uint32_t> rgs;      // row groups to scan, in order (pruned ones left out)
     uint32_t cur = 0;               // next position in rgs to hand out
     uint32_t pruned = 0;
@@ -558,6 +571,7 @@ struct fls_table {
 
     ScanCtx scan, mat;
     std::vector<HostTerm> filter;   // fls_scan_filter: applies to the next fls_scan_begin
+    bool dict_codes = false;        // fls_scan_dict_codes: applies to the next fls_scan_begin
     ~fls_table();
 };
 
@@ -575,10 +589,10 @@ const uint64_t *chunk_validity_host(const fls_table *t, uint32_t rg, uint32_t c)
 
 // Build host string_t tables for the VARCHAR chunks of [rg0, rg1) and upload.
 int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBuf<StrT> &tab,
-                  std::vector<uint64_t> &offs) {
+                  std::vector<uint64_t> &offs, std::vector<StrT> &host) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     offs.assign((size_t)(rg1 - rg0) * ncols, UINT64_MAX);
-    std::vector<StrT> host;
+    host.clear();
     for (uint32_t r = rg0; r < rg1; ++r)
         for (uint32_t c = 0; c < ncols; ++c) {
             if (!type_is_string(t->meta.cols[c].type)) continue;
@@ -601,8 +615,11 @@ int build_strtabs(const fls_table *t, int dev, uint32_t rg0, uint32_t rg1, DevBu
 }
 
 // Describe chunk (rg, col) located at d_chunk_base (device) for the kernel.
+// code_w (1 or 2): a DICT string chunk delivered as its codes, gathered from
+// the identity table d_ident instead of the string_t dictionary
 DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint8_t *d_chunk, const uint8_t *d_dict,
-                       uint8_t *d_out, ByteCount *bc, uint8_t *d_heap = nullptr, const uint8_t *h_heap = nullptr) {
+                       uint8_t *d_out, ByteCount *bc, uint8_t *d_heap = nullptr, const uint8_t *h_heap = nullptr,
+                       uint32_t code_w = 0, const uint8_t *d_ident = nullptr) {
     const ChunkRef &ch = t->meta.rgs[rg].chunks[col];
     const ChunkHeader &h = ch.hdr;
     DevChunk d;
@@ -619,6 +636,10 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
     d.vbits = h.vbits;
     d.ob = (uint8_t)out_bytes_of(t, col);
     if (h.enc == ENC_DICT) d.dict = h.is_str ? d_dict : d_chunk + h.aux_off;
+    if (code_w && h.enc == ENC_DICT && h.is_str) {
+        d.ob = (uint8_t)code_w;
+        d.dict = code_w == 1 ? d_ident : d_ident + kIdent16;
+    }
     bc->values += h.nvals;
     if (h.enc == ENC_FSST) {
         d.dict = d_heap;
@@ -668,7 +689,7 @@ DevChunk make_devchunk(const fls_table *t, uint32_t rg, uint32_t col, const uint
         if (h.enc == ENC_ALP && alp_exceptions(vm.aux_count))
             bc->meta += alp_aux_bytes(alp_exceptions(vm.aux_count), h.vbits);
     }
-    if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? 16 : h.vbits / 8);
+    if (h.enc == ENC_DICT) bc->meta += (uint64_t)h.dict_count * (h.is_str ? d.ob : h.vbits / 8);
     d.max_w = max_w;
     uint32_t pb, vb;
     chunk_lds_need(h.enc, h.T, d.ob, h.dict_count, max_w, pb, vb);
@@ -991,6 +1012,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         for (uint32_t c = 0; c < ncols; ++c) s.mask[c] = col_mask[c] ? 1 : 0;
     s.terms.clear();
     if (filter) s.terms = *filter;
+    s.dict_codes = filter != nullptr && t->dict_codes;  // scans (not materialize) only
     s.dmask = s.mask;
     for (auto &h : s.terms)
         if (h.op < OP_IS_NULL) s.dmask[h.col] = 1;
@@ -1038,8 +1060,15 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         d.next_p = d.p0;
         d.rg0 = d.p0 < d.p1 ? s.rgs[d.p0] : 0;
         d.rg1 = d.p0 < d.p1 ? s.rgs[d.p1 - 1] + 1 : 0;
-        int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off);
+        int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off, d.h_strtab);
         if (rc) return rc;
+        if (s.dict_codes && !d.ident.p) {
+            std::vector<uint8_t> id(kIdent16 + 2 * 65536);
+            for (uint32_t i = 0; i < 256; ++i) id[i] = (uint8_t)i;
+            for (uint32_t i = 0; i < 65536; ++i) memcpy(&id[kIdent16 + 2 * i], &i, 2);
+            HIP_TRY(d.ident.alloc(d.dev, id.size()));
+            HIP_TRY(hipMemcpy(d.ident.p, id.data(), id.size(), hipMemcpyHostToDevice));
+        }
         HIP_TRY(d.err.alloc(d.dev, 1));
         HIP_TRY(hipMemsetAsync(d.err.p, 0, sizeof(uint32_t), d.stream));
         HIP_TRY(hipStreamSynchronize(d.stream));
@@ -1069,7 +1098,7 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
         memset(&o, 0, sizeof(o));
         o.src = sl.d_out[c].p;
         o.dst = sl.hb->h_out[c].p;
-        o.ob = (uint32_t)out_bytes_of(t, c);
+        o.ob = sl.hb->ob[c];
         outs.push_back(o);
     }
     // validity words of the batch rows for every filtered column with a NULL
@@ -1200,6 +1229,32 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         src = sl.h_stage.p;
     }
     HIP_TRY(hipMemcpyAsync(sl.d_in.p, src, hi - lo, hipMemcpyHostToDevice, sl.stream));
+    // dictionary-coded delivery: a delivered DICT string column no filter term
+    // reads goes over PCIe as 1- or 2-byte codes when every chunk of the batch
+    // is DICT (DuckDB dictionary vectors over the host string_t dictionaries)
+    hb.ob.assign(ncols, 0);
+    hb.dict_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
+    hb.dict_sizes.assign((size_t)sl.nrg * ncols, 0);
+    std::vector<uint8_t> code_w(ncols, 0), in_term(ncols, 0);
+    for (auto &h : s.terms) in_term[h.col] = 1;
+    for (uint32_t c = 0; c < ncols; ++c) {
+        hb.ob[c] = (uint8_t)out_bytes_of(t, c);
+        if (!s.dict_codes || !col_selected(s.mask, c) || in_term[c] || !type_is_string(t->meta.cols[c].type)) continue;
+        bool all = true;
+        uint32_t maxd = 0;
+        for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) {
+            const ChunkHeader &h = t->meta.rgs[r].chunks[c].hdr;
+            all = all && h.enc == ENC_DICT;
+            maxd = std::max(maxd, h.dict_count);
+        }
+        if (!all || maxd > 65536) continue;
+        code_w[c] = hb.ob[c] = maxd <= 256 ? 1 : 2;
+        for (uint32_t r = 0; r < sl.nrg; ++r) {
+            const size_t i = (size_t)r * ncols + c;
+            hb.dict_ptrs[i] = d.h_strtab.data() + d.strtab_off[(size_t)(sl.rg0 + r - d.rg0) * ncols + c];
+            hb.dict_sizes[i] = t->meta.rgs[sl.rg0 + r].chunks[c].hdr.dict_count;
+        }
+    }
     // 2. decode into the slot's device columns (FSST columns also into a heap)
     const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
     sl.heap_bytes.assign(ncols, 0);
@@ -1228,12 +1283,11 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const ChunkRef &ch = t->meta.rgs[r].chunks[c];
             const uint64_t so = d.strtab_off[(size_t)(r - d.rg0) * ncols + c];
             const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
-            uint8_t *out = sl.d_out[c].p +
-                           (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * out_bytes_of(t, c);
+            uint8_t *out = sl.d_out[c].p + (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * hb.ob[c];
             const uint64_t ho = hoff[(size_t)(r - sl.rg0) * ncols + c];
             list.push_back(make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc,
                                          sl.heap_bytes[c] ? sl.d_heap[c].p + ho : nullptr,
-                                         sl.heap_bytes[c] ? hb.h_heap[c].p + ho : nullptr));
+                                         sl.heap_bytes[c] ? hb.h_heap[c].p + ho : nullptr, code_w[c], d.ident.p));
         }
     }
     FsstCounts fsst;
@@ -1260,8 +1314,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
         if (!filtered)
-            HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, sl.d_out[c].p, rows * out_bytes_of(t, c), hipMemcpyDeviceToHost,
-                                   sl.stream));
+            HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, sl.d_out[c].p, rows * hb.ob[c], hipMemcpyDeviceToHost, sl.stream));
         if (sl.heap_bytes[c])
             HIP_TRY(hipMemcpyAsync(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
     }
@@ -1278,8 +1331,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             for (uint32_t c = 0; c < ncols; ++c)
                 if (col_selected(s.mask, c))
                     hb.col_ptrs[(size_t)r * ncols + c] =
-                        hb.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) *
-                                            out_bytes_of(t, c);
+                        hb.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) * hb.ob[c];
     sl.busy = true;
     return 0;
 }
@@ -1325,7 +1377,7 @@ void batch_selection(fls_table *t, ScanCtx &s, HostBatch &hb) {
     for (uint32_t r = 0; r < hb.nrg; ++r)
         for (uint32_t c = 0; c < ncols; ++c)
             if (col_selected(s.mask, c))
-                hb.col_ptrs[(size_t)r * ncols + c] = hb.h_out[c].p + (uint64_t)hb.sel_off[r] * out_bytes_of(t, c);
+                hb.col_ptrs[(size_t)r * ncols + c] = hb.h_out[c].p + (uint64_t)hb.sel_off[r] * hb.ob[c];
     hb.sel_ready = true;
 }
 
@@ -1394,6 +1446,9 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     }
     out->columns = hb->col_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
     out->validity = hb->valid_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
+    out->dict = hb->dict_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
+    out->dict_size = hb->dict_sizes.data() + (size_t)(rg - hb->rg0) * ncols;
+    out->dict_width = hb->ob.data();
     if (out->sel) {  // filtered: the delivered rows' validity, gathered through sel
         const size_t i0 = (size_t)(rg - hb->rg0) * ncols;
         for (uint32_t c = 0; c < ncols; ++c) {
@@ -1773,6 +1828,12 @@ int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *m
     return 1;
 }
 
+int fls_scan_dict_codes(fls_table *t, int enable) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_dict_codes: NULL table");
+    t->dict_codes = enable != 0;
+    return 0;
+}
+
 int fls_table_validity(const fls_table *t, uint32_t rg, uint32_t col, const uint64_t **words) {
     if (!t || rg >= t->meta.rgs.size() || col >= t->meta.cols.size())
         return fail(FLS_ERR_ARG, "validity (%u, %u) out of range", rg, col);
@@ -1820,7 +1881,8 @@ int upload_part(fls_table *t, Resident &r) {
     r.base = lo;
     HIP_TRY(r.img.alloc(r.dev, hi - lo + kImagePad));
     HIP_TRY(hipMemcpy(r.img.p, t->img + lo, hi - lo, hipMemcpyHostToDevice));
-    int rc = build_strtabs(t, r.dev, r.rg0, r.rg1, r.strtab, r.strtab_off);
+    std::vector<StrT> host;  // (the resident part keeps only the device tables)
+    int rc = build_strtabs(t, r.dev, r.rg0, r.rg1, r.strtab, r.strtab_off, host);
     if (rc) return rc;
     HIP_TRY(r.err.alloc(r.dev, 1));
     HIP_TRY(hipMemset(r.err.p, 0, sizeof(uint32_t)));

@@ -144,9 +144,41 @@ Vector::Vector(LogicalType type, idx_t capacity)
     : type_(std::move(type)), capacity_(capacity), data_(capacity * type_.PhysicalSize(), 0),
       data_ptr_(data_.data()), validity_(capacity) {}
 
+Vector::Vector(LogicalType type, data_ptr_t data)
+    : type_(std::move(type)), capacity_(STANDARD_VECTOR_SIZE), data_ptr_(data), validity_(STANDARD_VECTOR_SIZE) {}
+
+void Vector::Slice(const Vector &other, const SelectionVector &sel, idx_t count) {
+    auto child = std::make_shared<Vector>(other.GetType(), (idx_t)0);
+    child->Reference(other);
+    Reset();
+    type_ = other.GetType();
+    child_ = std::move(child);
+    dict_sel_ = sel;
+    vtype_ = VectorType::DICTIONARY_VECTOR;
+    (void)count;
+}
+
+void Vector::Flatten(idx_t count) {
+    if (vtype_ != VectorType::DICTIONARY_VECTOR) return;
+    const idx_t w = type_.PhysicalSize();
+    std::shared_ptr<Vector> child = std::move(child_);
+    const SelectionVector sel = dict_sel_;
+    Reset();  // own storage, all valid
+    if (data_.size() < count * w) data_.resize(count * w);
+    capacity_ = std::max(capacity_, count);
+    data_ptr_ = data_.data();
+    for (idx_t i = 0; i < count; ++i) {
+        const idx_t j = sel.get_index(i);
+        if (!child->RowIsValid(j)) validity_.SetInvalid(i);
+        memcpy(data_ptr_ + i * w, child->GetData() + j * w, w);
+    }
+    keep_.push_back(child);  // strings still point into the dictionary's memory
+}
+
 Vector::Vector(Vector &&o) noexcept
     : type_(std::move(o.type_)), capacity_(o.capacity_), data_(std::move(o.data_)), auxiliary_(std::move(o.auxiliary_)),
-      validity_(std::move(o.validity_)), heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
+      validity_(std::move(o.validity_)), child_(std::move(o.child_)), dict_sel_(std::move(o.dict_sel_)),
+      heap_(std::move(o.heap_)), keep_(std::move(o.keep_)), vtype_(o.vtype_) {
     // a moved std::vector keeps its storage, so an owned data pointer stays valid
     data_ptr_ = o.data_ptr_;
     o.data_ptr_ = nullptr;
@@ -158,12 +190,21 @@ void Vector::Reset() {
     data_ptr_ = data_.data();
     auxiliary_.reset();
     validity_.Reset();
+    child_.reset();
+    dict_sel_ = SelectionVector();
     heap_.clear();
     keep_.clear();
     vtype_ = VectorType::FLAT_VECTOR;
 }
 
 void Vector::Reference(const Vector &o) {
+    if (o.vtype_ == VectorType::DICTIONARY_VECTOR) {  // share the dictionary and the selection
+        type_ = o.type_;
+        child_ = o.child_;
+        dict_sel_ = o.dict_sel_;
+        vtype_ = o.vtype_;
+        return;
+    }
     type_ = o.type_;
     validity_ = o.validity_;  // shared words, as DuckDB's Reference shares the validity buffer
     vtype_ = o.vtype_;
@@ -222,6 +263,7 @@ void Vector::SetValue(idx_t i, const Value &v) {
 }
 
 Value Vector::GetValue(idx_t i) const {
+    if (vtype_ == VectorType::DICTIONARY_VECTOR) return child_->GetValue(dict_sel_.get_index(i));
     if (!validity_.RowIsValid(i)) return Value();
     const uint8_t *p = data_ptr_ + i * type_.PhysicalSize();
     auto ld = [p](auto x) { memcpy(&x, p, sizeof(x)); return x; };
@@ -342,6 +384,12 @@ bool eval_filter(const TableFilter &f, const Value &v) {
 }  // namespace
 
 void Vector::ToUnifiedFormat(idx_t, UnifiedVectorFormat &format) const {
+    if (vtype_ == VectorType::DICTIONARY_VECTOR) {
+        format.sel = &dict_sel_;
+        format.data = child_->GetData();
+        format.validity = child_->Validity();
+        return;
+    }
     format.sel = &incremental_sel();
     format.data = GetData();
     format.validity = validity_;

@@ -237,7 +237,7 @@ inline date_t Value::GetValue<date_t>() const { return date_t{(int32_t)int_}; }
 
 
 // ---- vectors ---------------------------------------------------------------
-enum class VectorType : uint8_t { FLAT_VECTOR, CONSTANT_VECTOR };
+enum class VectorType : uint8_t { FLAT_VECTOR, CONSTANT_VECTOR, DICTIONARY_VECTOR };
 
 // DuckDB v1.3.2 common/types/vector_buffer.hpp: a buffer a Vector can hold
 // on to.  OPAQUE_BUFFER subclasses keep foreign memory alive while a vector
@@ -259,6 +259,27 @@ template <class T, class... Args>
 buffer_ptr<T> make_buffer(Args &&...args) {
     return std::make_shared<T>(std::forward<Args>(args)...);
 }
+
+using sel_t = uint32_t;
+// DuckDB common/types/selection_vector.hpp: row indices, owned (shared by
+// copies, like DuckDB's SelectionData buffer) or borrowed (SelectionVector(sel_t *))
+class SelectionVector {
+public:
+    SelectionVector() = default;
+    explicit SelectionVector(sel_t *sel) : ptr_(sel) {}
+    explicit SelectionVector(idx_t count) : owned_(std::make_shared<vector<sel_t>>(count)) {
+        for (idx_t i = 0; i < count; ++i) (*owned_)[i] = (sel_t)i;
+        ptr_ = owned_->data();
+    }
+    idx_t get_index(idx_t i) const { return ptr_ ? ptr_[i] : i; }
+    void set_index(idx_t i, idx_t loc) { ptr_[i] = (sel_t)loc; }
+    sel_t *data() { return ptr_; }
+    const sel_t *data() const { return ptr_; }
+
+private:
+    sel_t *ptr_ = nullptr;
+    shared_ptr<vector<sel_t>> owned_;
+};
 
 // DuckDB common/types/validity_mask.hpp: one bit per row (1 = valid) in
 // 64-bit words, no words allocated while every row is valid
@@ -317,6 +338,9 @@ private:
 class Vector {
 public:
     explicit Vector(LogicalType type, idx_t capacity = STANDARD_VECTOR_SIZE);
+    // DuckDB Vector(const LogicalType &, data_ptr_t): a flat vector over
+    // memory it does not own
+    Vector(LogicalType type, data_ptr_t data);
     Vector(Vector &&o) noexcept;
     Vector(const Vector &) = delete;
     Vector &operator=(const Vector &) = delete;
@@ -333,8 +357,18 @@ public:
     // the shim's own storage is not shareable, so owned data is copied
     void Reference(const Vector &other);
     buffer_ptr<VectorBuffer> GetAuxiliary() const { return auxiliary_; }
-    bool RowIsValid(idx_t i) const { return validity_.RowIsValid(i); }
+    bool RowIsValid(idx_t i) const {
+        return vtype_ == VectorType::DICTIONARY_VECTOR ? child_->RowIsValid(dict_sel_.get_index(i))
+                                                       : validity_.RowIsValid(i);
+    }
     void SetValid(idx_t i, bool v) { validity_.Set(i, v); }
+    // DuckDB Vector::Slice(other, sel, count): this becomes a DICTIONARY_VECTOR,
+    // row i = other's row sel[i] (other is referenced, not copied)
+    void Slice(const Vector &other, const SelectionVector &sel, idx_t count);
+    // DuckDB Vector::Flatten(count): a dictionary vector materialised flat
+    void Flatten(idx_t count);
+    const Vector &DictionaryChild() const { return *child_; }
+    const SelectionVector &DictionarySel() const { return dict_sel_; }
     ValidityMask &Validity() { return validity_; }
     const ValidityMask &Validity() const { return validity_; }
     void ToUnifiedFormat(idx_t count, struct UnifiedVectorFormat &format) const;
@@ -353,9 +387,16 @@ private:
     data_ptr_t data_ptr_;                 // data_.data(), or foreign memory (SetData)
     buffer_ptr<VectorBuffer> auxiliary_;  // keeps foreign memory alive
     ValidityMask validity_;
+    shared_ptr<Vector> child_;        // DICTIONARY_VECTOR: the dictionary
+    SelectionVector dict_sel_;        // ... and the rows' entries
     std::deque<string> heap_;
     vector<shared_ptr<void>> keep_;
     VectorType vtype_ = VectorType::FLAT_VECTOR;
+};
+
+struct DictionaryVector {
+    static const SelectionVector &SelVector(const Vector &v) { return v.DictionarySel(); }
+    static const Vector &Child(const Vector &v) { return v.DictionaryChild(); }
 };
 
 struct FlatVector {
@@ -385,7 +426,9 @@ public:
         count_ = 0;
     }
     void Initialize(const vector<LogicalType> &types) { InitializeEmpty(types); }
-    void Flatten() {}  // shim vectors are always flat
+    void Flatten() {  // DuckDB DataChunk::Flatten: every vector flat
+        for (auto &v : data) v.Flatten(count_);
+    }
     void Reset() {
         for (auto &v : data) v.Reset();
         count_ = 0;
@@ -537,19 +580,6 @@ public:
 // common/types/selection_vector.hpp).  The shim evaluates row by row through
 // Value; Expression here is a stand-in the harness builds (DuckDB's
 // ExpressionFilter holds a bound planner Expression run by an executor).
-using sel_t = uint32_t;
-class SelectionVector {
-public:
-    SelectionVector() = default;
-    explicit SelectionVector(idx_t count) : sel_(count) {
-        for (idx_t i = 0; i < count; ++i) sel_[i] = (sel_t)i;
-    }
-    idx_t get_index(idx_t i) const { return sel_.empty() ? i : sel_[i]; }
-    void set_index(idx_t i, idx_t loc) { sel_[i] = (sel_t)loc; }
-
-private:
-    vector<sel_t> sel_;
-};
 struct UnifiedVectorFormat {
     const SelectionVector *sel = nullptr;
     const_data_ptr_t data = nullptr;

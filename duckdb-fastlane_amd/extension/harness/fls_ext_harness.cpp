@@ -620,8 +620,9 @@ ChunkHash hash_chunk(DataChunk &c, const std::vector<size_t> &pick, idx_t cnt) {
     r.n = cnt;
     for (size_t k : pick) {
         Vector &v = c.data[k];
+        v.Flatten(cnt);  // dictionary vectors (read_fastlanes' DICT string columns)
         uint64_t h = 0, pw = 1;
-        if (v.GetType().id() == LogicalTypeId::VARCHAR) {
+        if (v.GetType().id() == LogicalTypeId::VARCHAR || v.GetType().id() == LogicalTypeId::BLOB) {
             const string_t *s = FlatVector::GetData<string_t>(v);
             for (idx_t i = 0; i < cnt; ++i, pw *= kPoly) {
                 uint64_t f = 1469598103934665603ull;

@@ -19,6 +19,7 @@
 #include <glob.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -364,7 +365,12 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
             auto t = std::move(g.tables[g.file_idx]);  // opened by InitGlobal
             if (fls_scan_filter(t->table, g.preds.data(), (uint32_t)g.preds.size()) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
-            if (fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
+            // DICT string columns as codes + dictionary (DuckDB dictionary
+            // vectors: 1-2 bytes per row over PCIe instead of a 16-byte
+            // string_t); FLS_READ_DICT=0 delivers string_t (A/B knob)
+            static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
+            if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 ||
+                fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             g.cur = std::move(t);
         }
@@ -392,6 +398,27 @@ void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector
         auto &mask = FlatVector::Validity(vec);
         mask.Initialize(STANDARD_VECTOR_SIZE);
         memcpy(mask.GetData(), valid + l.rg_pos / 64, ValidityMask::EntryCount(n) * sizeof(validity_t));
+    }
+    if (const void *dict = l.rg.dict ? l.rg.dict[id] : nullptr) {  // dictionary codes
+        const uint8_t w = l.rg.dict_width[id];
+        const uint8_t *codes = (const uint8_t *)l.rg.columns[id] + l.rg_pos * w;
+        auto code = [codes, w](idx_t i) -> sel_t {
+            return w == 1 ? codes[i] : (sel_t)(codes[2 * i] | (uint32_t)codes[2 * i + 1] << 8);
+        };
+        const string_t *entries = (const string_t *)dict;
+        if (l.rg.validity && l.rg.validity[id]) {  // NULLs: flat strings beside the validity set above
+            string_t *d = FlatVector::GetData<string_t>(vec);
+            for (idx_t i = 0; i < n; ++i) d[i] = entries[code(i)];
+            return;
+        }
+        // the row group's dictionary as a vector over the engine's string_t
+        // records, the rows a selection of it
+        Vector dict_vec(vec.GetType(), (data_ptr_t)dict);
+        dict_vec.SetAuxiliary(l.pin);
+        SelectionVector sel(n);
+        for (idx_t i = 0; i < n; ++i) sel.set_index(i, code(i));
+        vec.Slice(dict_vec, sel, n);
+        return;
     }
     const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
     const idx_t phys = vec.GetType().PhysicalSize();

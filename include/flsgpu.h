@@ -81,6 +81,15 @@ typedef struct fls_rowgroup {
                                      delivered row is valid (and for columns
                                      not selected).  Values at NULL rows are
                                      placeholders.  Valid as long as columns. */
+    const void *const *dict;      /* ncols pointers (fls_scan_dict_codes): for a
+                                     column delivered as dictionary codes in
+                                     this row group, its dictionary as 16-byte
+                                     string_t records (host); columns[c] then
+                                     holds one code per delivered row,
+                                     dict_width[c] bytes each (1 or 2, little
+                                     endian).  NULL for other columns. */
+    const uint32_t *dict_size;    /* ncols: entries of dict[c] */
+    const uint8_t *dict_width;    /* ncols: bytes per delivered value */
 } fls_rowgroup;
 
 /* Pushed-down filter term: `column <op> constant` (DuckDB TableFilterSet:
@@ -179,6 +188,12 @@ int fls_scan_pruned(const fls_table *t);
  * min / max over the non-NULL rows) when present, 0 when the file has none
  * for it. */
 int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *min, uint64_t *max, uint32_t *flags);
+/* Dictionary-coded delivery for the next fls_scan_begin (enable != 0): a
+ * delivered VARCHAR / BLOB column no filter term reads, whose chunks in a
+ * batch are all DICT, crosses PCIe as 1- or 2-byte codes instead of 16-byte
+ * string_t records (fls_rowgroup.dict / dict_width); what a DuckDB
+ * dictionary vector needs.  Off by default. */
+int fls_scan_dict_codes(fls_table *t, int enable);
 /* Validity of column col in row group rg: 1 and *words = its bitmaps in the
  * host image (16 u64 words per 1024-row vector, DuckDB's layout: bit i of
  * word j set when row 64 j + i is valid) when the chunk holds a NULL, 0 (and
