@@ -416,7 +416,13 @@ void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector
         Vector dict_vec(vec.GetType(), (data_ptr_t)dict);
         dict_vec.SetAuxiliary(l.pin);
         SelectionVector sel(n);
-        for (idx_t i = 0; i < n; ++i) sel.set_index(i, code(i));
+        sel_t *sd = sel.data();  // u8 / u16 -> sel_t widening, vectorisable
+        if (w == 1) {
+            for (idx_t i = 0; i < n; ++i) sd[i] = codes[i];
+        } else {
+            const uint16_t *c16 = (const uint16_t *)codes;  // 2-byte aligned: rg_pos is even
+            for (idx_t i = 0; i < n; ++i) sd[i] = c16[i];
+        }
         vec.Slice(dict_vec, sel, n);
         return;
     }
