@@ -69,6 +69,20 @@ __device__ __forceinline__ uint32_t tau_d(uint32_t p) {
     return (rb << 7) | (((p >> 7) & 7) << 4) | (p & 15);
 }
 __device__ __forceinline__ uint32_t rl(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+// The wave's index in the block, wave-uniform: as an SGPR its LDS and input
+// offsets are scalar too.  Held in a VGPR (FLS_ENC_VECTOR_WAVE_INDEX, the
+// round-2 code) the narrow kernel needed 93 VGPRs, and its 6-wave build spilled
+// the wave's LDS base (w * 4096) to one 8-byte scratch slot whose store sat
+// inside the prefetch branch of a full next vector: waves that skipped the
+// branch reloaded a stale slot.  Scalar: 80 VGPRs, no
+// spill at 5 or 6 waves per SIMD.
+__device__ __forceinline__ uint32_t wave_index() {
+#ifdef FLS_ENC_VECTOR_WAVE_INDEX
+    return threadIdx.x >> 6;
+#else
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#endif
+}
 // min and max together: two independent shuffle chains, one latency
 __device__ __forceinline__ void wave_minmax_i64(int64_t &mn, int64_t &mx) {
     for (int d = 32; d >= 1; d >>= 1) {
@@ -231,7 +245,7 @@ template <int T, bool DELTA>
 __device__ void encode_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS uint32_t *Wv,
                              FLS_LDS int64_t *Bv, FLS_LDS uint64_t *Ov) {
     using S = Sto<T>;
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = wave_index();
     FLS_LDS S *V = Vall + w * kVectorSize;
     const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
     const uint8_t *in = (const uint8_t *)c.in;
@@ -429,7 +443,7 @@ template <int T>
 __device__ void encode_rle_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS uint32_t *Wv, FLS_LDS int64_t *Bv,
                                  FLS_LDS uint64_t *Ov) {
     using S = Sto<T>;
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = wave_index();
     FLS_LDS S *V = Vall + w * kVectorSize;
     const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
     const uint8_t *in = (const uint8_t *)c.in;
@@ -575,7 +589,7 @@ __device__ void encode_rle_chunk(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LD
 template <int T>
 __device__ uint8_t choose_encoding(const EncChunk &c, FLS_LDS Sto<T> *Vall, FLS_LDS uint64_t *acc) {
     using S = Sto<T>;
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = wave_index();
     FLS_LDS S *V = Vall + w * kVectorSize;
     const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
     const uint8_t *in = (const uint8_t *)c.in;

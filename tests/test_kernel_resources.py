@@ -35,7 +35,7 @@ def test_encoder_kernels_do_not_spill(res):
     for name, r in {**_find(res, "encode_kernel"), **_find(res, "encode_rle_kernel")}.items():
         assert r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
     narrow = _find(res, "encode_kernelIj")  # T <= 32: 5 waves per SIMD
-    assert all(r["vgpr"] <= 96 for r in narrow.values()), narrow
+    assert all(r["vgpr"] <= 80 for r in narrow.values()), narrow  # 6 waves per SIMD fit (scalar wave index)
 
 
 def test_decode_kernel_fits_four_waves(res):
