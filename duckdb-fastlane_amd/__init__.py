@@ -58,7 +58,8 @@ class RowGroup(C.Structure):
                 ("ncols", C.c_uint32), ("columns", C.POINTER(C.c_void_p)),
                 ("nrows_scanned", C.c_uint32), ("sel", C.POINTER(C.c_uint32)),
                 ("validity", C.POINTER(C.c_void_p)), ("dict", C.POINTER(C.c_void_p)),
-                ("dict_size", C.POINTER(C.c_uint32)), ("dict_width", C.POINTER(C.c_uint8))]
+                ("dict_size", C.POINTER(C.c_uint32)), ("dict_width", C.POINTER(C.c_uint8)),
+                ("narrow", C.POINTER(C.c_uint8)), ("narrow_base", C.POINTER(C.c_uint64))]
 
 
 class Predicate(C.Structure):
@@ -120,6 +121,7 @@ _sig("fls_scan_pruned", C.c_int, _P)
 _sig("fls_table_zonemap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
      C.POINTER(C.c_uint32))
 _sig("fls_scan_dict_codes", C.c_int, _P, C.c_int)
+_sig("fls_scan_narrow", C.c_int, _P, C.c_int)
 _sig("fls_table_validity", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)))
 _sig("fls_rowgroup_may_match", C.c_int, _P, C.c_uint32, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_device_upload", C.c_int, _P, C.c_uint32, C.c_uint32)
@@ -496,12 +498,20 @@ class Table:
                 cols.append(None)
                 continue
             ob = sch[c][4]
-            if rg.dict and rg.dict[c]:
-                ob = rg.dict_width[c]  # dictionary codes (fls_scan_dict_codes)
+            narrowed = bool(rg.narrow and rg.narrow[c])
+            if (rg.dict and rg.dict[c]) or narrowed:
+                ob = rg.dict_width[c]  # dictionary codes / narrowed values
             if rg.nrows == 0:
                 cols.append(np.zeros(0, dtype=np.uint8))
                 continue
             a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(rg.nrows * ob,))
+            if narrowed:  # widen: value = base + narrow (mod 2^64), in the column's width
+                full = sch[c][4]
+                w = a.view({1: np.uint8, 2: np.uint16, 4: np.uint32}[ob]).astype(np.uint64)
+                v = (w + np.uint64(rg.narrow_base[c])).astype(np.uint64)
+                a = v.view(np.uint8).reshape(-1, 8)[:, :full].reshape(-1).copy()
+                cols.append(a)
+                continue
             cols.append(a.copy() if copy else a)
         return cols
 
@@ -530,6 +540,11 @@ class Table:
         while _check(_lib.fls_scan_next(self.h, C.byref(out))) == 1:
             sel = np.ctypeslib.as_array(out.sel, shape=(out.nrows,)).copy() if out.sel and out.nrows else None
             yield out.first_row, self._rg_arrays(out), self._rg_valid(out), sel
+
+    def narrow(self, enable: bool = True):
+        """fls_scan_narrow: the next scan delivers integer columns narrowed to
+        their row groups' ranges (scan() widens them back)"""
+        _check(_lib.fls_scan_narrow(self.h, int(enable)))
 
     def dict_codes(self, enable: bool = True):
         """fls_scan_dict_codes: the next scan delivers DICT string columns as

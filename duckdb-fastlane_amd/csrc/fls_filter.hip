@@ -163,7 +163,34 @@ __global__ __launch_bounds__(256) void compact_kernel(const DevOut *__restrict__
     }
 }
 
+// one 1024-row tile of one narrowed column per block, 4 rows per thread
+__global__ __launch_bounds__(256) void narrow_kernel(const DevNarrow *__restrict__ cols, uint32_t nrows,
+                                                     uint32_t rg_rows) {
+    const DevNarrow c = cols[blockIdx.y];
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t row = (uint64_t)blockIdx.x * 1024 + k * 256 + threadIdx.x;
+        if (row >= nrows) return;
+        const uint8_t *p = c.src + row * c.ob;
+        const uint64_t v = c.sign ? (uint64_t)load_int(p, c.ob) : load_uint(p, c.ob);
+        const uint64_t d = v - c.base[row / rg_rows];
+        uint8_t *q = c.dst + row * c.nw;
+        switch (c.nw) {
+        case 1: *q = (uint8_t)d; break;
+        case 2: *(uint16_t *)q = (uint16_t)d; break;
+        default: *(uint32_t *)q = (uint32_t)d; break;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_narrow(const DevNarrow *d_cols, uint32_t ncols, uint32_t nrows, uint32_t rg_rows,
+                         hipStream_t stream) {
+    if (ncols == 0 || nrows == 0 || rg_rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(narrow_kernel, dim3((nrows + 1023) / 1024, ncols), dim3(256), 0, stream, d_cols, nrows,
+                       rg_rows);
+    return hipGetLastError();
+}
 
 hipError_t launch_filter(const DevTerm *d_terms, uint32_t nterms, uint32_t nrows, uint64_t *d_mask,
                          uint32_t *d_counts, uint32_t *d_err, hipStream_t stream) {

@@ -105,4 +105,20 @@ hipError_t launch_filter(const DevTerm *d_terms, uint32_t nterms, uint32_t nrows
 hipError_t launch_compact(const DevOut *d_outs, uint32_t nouts, const uint64_t *d_mask, const uint32_t *d_counts,
                           uint32_t nrows, uint32_t rg_rows, uint32_t *sel, hipStream_t stream);
 
+// Narrowed delivery (fls_scan_narrow): an integer column of a batch whose
+// values, per row group, lie in [base, base + 2^(8 nw)) crosses PCIe as the
+// nw-byte differences value - base (the host adds the base back).  Reads ob
+// bytes and writes nw per row: HBM-side work that saves (ob - nw) bytes of
+// PCIe per row.
+struct DevNarrow {            // 32 B
+    const uint8_t *src;       // decoded column of the batch (HBM, ob bytes per row)
+    uint8_t *dst;             // narrowed copy (HBM, nw bytes per row)
+    const uint64_t *base;     // per row group of the batch (row / rg_rows): the value subtracted
+    uint8_t ob, nw, sign;     // widths; sign: values sign-extend from ob bytes
+    uint8_t pad[5];
+};
+static_assert(sizeof(DevNarrow) == 32, "DevNarrow is 32 B");
+hipError_t launch_narrow(const DevNarrow *d_cols, uint32_t ncols, uint32_t nrows, uint32_t rg_rows,
+                         hipStream_t stream);
+
 }  // namespace fls

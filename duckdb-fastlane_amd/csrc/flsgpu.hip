@@ -275,6 +275,10 @@ struct HostBatch {
     std::vector<uint8_t> ob;
     std::vector<const void *> dict_ptrs;
     std::vector<uint32_t> dict_sizes;
+    // narrowed delivery (fls_scan_narrow): per column 1 when it crosses PCIe
+    // as value - base in ob bytes, per (rg - rg0) * ncols + col that base
+    std::vector<uint8_t> narrowed;
+    std::vector<uint64_t> nbase;
 };
 
 struct Slot {                       // one batch of row groups in flight
@@ -299,6 +303,9 @@ struct Slot {                       // one batch of row groups in flight
     PinBuf<uint8_t> h_fdesc;        // DevTerm[] + DevOut[] + constant strings
     DevBuf<uint8_t> d_fdesc;
     std::vector<DevBuf<uint64_t>> d_valid;  // per filtered column with a NULL: batch validity words
+    std::vector<DevBuf<uint8_t>> d_narrow;  // per narrowed column: its narrowed copy
+    PinBuf<uint8_t> h_ndesc;                // DevNarrow[] + per-row-group bases
+    DevBuf<uint8_t> d_ndesc;
 };
 
 // One GPU's scan pipeline: streams, the two device slots and the pinned
@@ -359,6 +366,7 @@ struct ScanCtx {
     std::vector<uint8_t> dmask;     // decoded columns (delivered + filter columns)
     std::vector<HostTerm> terms;    // filter of this scan, sorted by clause (empty: none)
     bool dict_codes = false;        // deliver DICT string chunks as codes + dictionary
+    bool narrow = false;            // deliver integer columns narrowed to their row groups' ranges
     std::vector<uint32_t> rgs;      // row groups to scan, in order (pruned ones left out)
     uint32_t cur = 0;               // next position in rgs to hand out
     uint32_t pruned = 0;
@@ -572,6 +580,7 @@ struct fls_table {
     ScanCtx scan, mat;
     std::vector<HostTerm> filter;   // fls_scan_filter: applies to the next fls_scan_begin
     bool dict_codes = false;        // fls_scan_dict_codes: applies to the next fls_scan_begin
+    bool narrow = false;            // fls_scan_narrow: applies to the next fls_scan_begin
     ~fls_table();
 };
 
@@ -1013,6 +1022,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
     s.terms.clear();
     if (filter) s.terms = *filter;
     s.dict_codes = filter != nullptr && t->dict_codes;  // scans (not materialize) only
+    s.narrow = filter != nullptr && t->narrow;
     s.dmask = s.mask;
     for (auto &h : s.terms)
         if (h.op < OP_IS_NULL) s.dmask[h.col] = 1;
@@ -1096,7 +1106,7 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
         if (!col_selected(s.mask, c)) continue;
         DevOut o;
         memset(&o, 0, sizeof(o));
-        o.src = sl.d_out[c].p;
+        o.src = sl.hb->narrowed[c] ? sl.d_narrow[c].p : sl.d_out[c].p;
         o.dst = sl.hb->h_out[c].p;
         o.ob = sl.hb->ob[c];
         outs.push_back(o);
@@ -1255,6 +1265,30 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             hb.dict_sizes[i] = t->meta.rgs[sl.rg0 + r].chunks[c].hdr.dict_count;
         }
     }
+    // the decode's bytes per row (string_t / code width / the type's width);
+    // hb.ob below is what crosses PCIe
+    const std::vector<uint8_t> dob = hb.ob;
+    // narrowed delivery: an integer column whose row groups' zone maps bound
+    // every value within 2^8 / 2^16 / 2^32 of the row group's minimum crosses
+    // PCIe as value - minimum in 1 / 2 / 4 bytes (narrow_kernel after the decode)
+    hb.narrowed.assign(ncols, 0);
+    hb.nbase.assign((size_t)sl.nrg * ncols, 0);
+    for (uint32_t c = 0; s.narrow && c < ncols; ++c) {
+        const uint8_t ty = t->meta.cols[c].type;
+        if (!col_selected(s.mask, c) || type_is_string(ty) || type_is_float(ty) || hb.ob[c] < 2) continue;
+        bool ok = true;
+        uint64_t range = 0;
+        for (uint32_t r = sl.rg0; ok && r < sl.rg0 + sl.nrg; ++r) {
+            const auto &zs = t->meta.rgs[r].zones;
+            ok = !zs.empty() && (zs[c].flags & ZM_VALID) && !(zs[c].flags & ZM_ALL_NULL);
+            if (ok) range = std::max<uint64_t>(range, zs[c].max - zs[c].min);
+        }
+        const uint8_t nw = range < (1ull << 8) ? 1 : range < (1ull << 16) ? 2 : range < (1ull << 32) ? 4 : 8;
+        if (!ok || nw >= hb.ob[c]) continue;
+        hb.ob[c] = nw;
+        hb.narrowed[c] = 1;
+        for (uint32_t r = 0; r < sl.nrg; ++r) hb.nbase[(size_t)r * ncols + c] = t->meta.rgs[sl.rg0 + r].zones[c].min;
+    }
     // 2. decode into the slot's device columns (FSST columns also into a heap)
     const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
     sl.heap_bytes.assign(ncols, 0);
@@ -1283,7 +1317,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const ChunkRef &ch = t->meta.rgs[r].chunks[c];
             const uint64_t so = d.strtab_off[(size_t)(r - d.rg0) * ncols + c];
             const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
-            uint8_t *out = sl.d_out[c].p + (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * hb.ob[c];
+            uint8_t *out = sl.d_out[c].p + (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * dob[c];
             const uint64_t ho = hoff[(size_t)(r - sl.rg0) * ncols + c];
             list.push_back(make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc,
                                          sl.heap_bytes[c] ? sl.d_heap[c].p + ho : nullptr,
@@ -1305,6 +1339,35 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                        plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
                           t->meta.rgs[sl.rg0].first_row;
+    // 2b. narrowed columns: value - base into their narrow copies
+    {
+        std::vector<uint32_t> nc;
+        for (uint32_t c = 0; c < ncols; ++c)
+            if (hb.narrowed[c]) nc.push_back(c);
+        if (!nc.empty()) {
+            sl.d_narrow.resize(ncols);
+            const size_t bytes = nc.size() * (sizeof(DevNarrow) + 8ull * sl.nrg);
+            HIP_TRY(sl.h_ndesc.alloc(bytes));
+            HIP_TRY(sl.d_ndesc.alloc(d.dev, bytes));
+            DevNarrow *dn = (DevNarrow *)sl.h_ndesc.p;
+            uint64_t *bases = (uint64_t *)(sl.h_ndesc.p + nc.size() * sizeof(DevNarrow));
+            for (size_t k = 0; k < nc.size(); ++k) {
+                const uint32_t c = nc[k];
+                HIP_TRY(sl.d_narrow[c].alloc(d.dev, max_rows * hb.ob[c]));
+                memset(&dn[k], 0, sizeof(DevNarrow));
+                dn[k].src = sl.d_out[c].p;
+                dn[k].dst = sl.d_narrow[c].p;
+                dn[k].base = (const uint64_t *)(sl.d_ndesc.p + nc.size() * sizeof(DevNarrow)) + k * sl.nrg;
+                dn[k].ob = dob[c];
+                dn[k].nw = hb.ob[c];
+                dn[k].sign = type_is_signed(t->meta.cols[c].type) ? 1 : 0;
+                for (uint32_t r = 0; r < sl.nrg; ++r) bases[k * sl.nrg + r] = hb.nbase[(size_t)r * ncols + c];
+            }
+            HIP_TRY(hipMemcpyAsync(sl.d_ndesc.p, sl.h_ndesc.p, bytes, hipMemcpyHostToDevice, sl.stream));
+            HIP_TRY(launch_narrow((const DevNarrow *)sl.d_ndesc.p, (uint32_t)nc.size(), (uint32_t)rows,
+                                  t->meta.rowgroup_size, sl.stream));
+        }
+    }
     if (filtered) {
         // 3a. select + compact the qualifying rows straight into pinned host memory
         int rc = enqueue_filter(t, s, d, sl, rows, lo, hi - lo);
@@ -1314,7 +1377,8 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
         if (!filtered)
-            HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, sl.d_out[c].p, rows * hb.ob[c], hipMemcpyDeviceToHost, sl.stream));
+            HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, hb.narrowed[c] ? sl.d_narrow[c].p : sl.d_out[c].p, rows * hb.ob[c],
+                                   hipMemcpyDeviceToHost, sl.stream));
         if (sl.heap_bytes[c])
             HIP_TRY(hipMemcpyAsync(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
     }
@@ -1449,6 +1513,8 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     out->dict = hb->dict_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
     out->dict_size = hb->dict_sizes.data() + (size_t)(rg - hb->rg0) * ncols;
     out->dict_width = hb->ob.data();
+    out->narrow = hb->narrowed.data();
+    out->narrow_base = hb->nbase.data() + (size_t)(rg - hb->rg0) * ncols;
     if (out->sel) {  // filtered: the delivered rows' validity, gathered through sel
         const size_t i0 = (size_t)(rg - hb->rg0) * ncols;
         for (uint32_t c = 0; c < ncols; ++c) {
@@ -1826,6 +1892,12 @@ int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *m
     if (max) *max = z[col].max;
     if (flags) *flags = z[col].flags;
     return 1;
+}
+
+int fls_scan_narrow(fls_table *t, int enable) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_narrow: NULL table");
+    t->narrow = enable != 0;
+    return 0;
 }
 
 int fls_scan_dict_codes(fls_table *t, int enable) {

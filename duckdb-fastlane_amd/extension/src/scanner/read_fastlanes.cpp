@@ -369,7 +369,11 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
             // vectors: 1-2 bytes per row over PCIe instead of a 16-byte
             // string_t); FLS_READ_DICT=0 delivers string_t (A/B knob)
             static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
-            if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 ||
+            // integer columns narrowed to their row groups' ranges (value -
+            // base in 1-4 bytes, widened here); FLS_READ_NARROW=0 turns it off
+            static const bool narrow =
+                !(std::getenv("FLS_READ_NARROW") && std::atoi(std::getenv("FLS_READ_NARROW")) == 0);
+            if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 || fls_scan_narrow(t->table, narrow ? 1 : 0) != 0 ||
                 fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             g.cur = std::move(t);
@@ -426,8 +430,32 @@ void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector
         vec.Slice(dict_vec, sel, n);
         return;
     }
-    const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
     const idx_t phys = vec.GetType().PhysicalSize();
+    if (l.rg.narrow && l.rg.narrow[id]) {  // narrowed: value = base + difference, into DuckDB's width
+        const uint8_t w = l.rg.dict_width[id];
+        const uint64_t base = l.rg.narrow_base[id];
+        const uint8_t *q = (const uint8_t *)l.rg.columns[id] + l.rg_pos * w;
+        uint8_t *d = FlatVector::GetData<uint8_t>(vec);
+        auto widen = [&](auto narrow_t, auto phys_t) {
+            using N = decltype(narrow_t);
+            using P = decltype(phys_t);
+            const N *src = (const N *)q;
+            P *dst = (P *)d;
+            for (idx_t i = 0; i < n; ++i) dst[i] = (P)(base + src[i]);
+        };
+        auto by_phys = [&](auto narrow_t) {
+            switch (phys) {
+            case 2: widen(narrow_t, uint16_t()); break;
+            case 4: widen(narrow_t, uint32_t()); break;
+            default: widen(narrow_t, uint64_t()); break;
+            }
+        };
+        if (w == 1) by_phys(uint8_t());
+        else if (w == 2) by_phys(uint16_t());
+        else by_phys(uint32_t());
+        return;
+    }
+    const uint8_t *src = (const uint8_t *)l.rg.columns[id] + l.rg_pos * ob;
     if (phys == ob) {
         FlatVector::SetData(vec, (data_ptr_t)src);
         vec.SetAuxiliary(l.pin);

@@ -90,6 +90,11 @@ typedef struct fls_rowgroup {
                                      endian).  NULL for other columns. */
     const uint32_t *dict_size;    /* ncols: entries of dict[c] */
     const uint8_t *dict_width;    /* ncols: bytes per delivered value */
+    const uint8_t *narrow;        /* ncols (fls_scan_narrow): 1 when columns[c]
+                                     holds value - narrow_base[c] as an
+                                     unsigned dict_width[c]-byte integer (the
+                                     value, mod 2^64, is their sum) */
+    const uint64_t *narrow_base;  /* ncols: this row group's base */
 } fls_rowgroup;
 
 /* Pushed-down filter term: `column <op> constant` (DuckDB TableFilterSet:
@@ -194,6 +199,13 @@ int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *m
  * string_t records (fls_rowgroup.dict / dict_width); what a DuckDB
  * dictionary vector needs.  Off by default. */
 int fls_scan_dict_codes(fls_table *t, int enable);
+/* Narrowed delivery for the next fls_scan_begin (enable != 0): a delivered
+ * integer / DATE / DECIMAL column whose zone maps put every value of a
+ * batch's row groups within 2^8, 2^16 or 2^32 of its row group's minimum
+ * crosses PCIe as the 1-, 2- or 4-byte difference (fls_rowgroup.narrow /
+ * narrow_base); the consumer adds the base back while filling its vectors.
+ * Off by default. */
+int fls_scan_narrow(fls_table *t, int enable);
 /* Validity of column col in row group rg: 1 and *words = its bitmaps in the
  * host image (16 u64 words per 1024-row vector, DuckDB's layout: bit i of
  * word j set when row 64 j + i is valid) when the chunk holds a NULL, 0 (and

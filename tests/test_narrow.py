@@ -1,0 +1,69 @@
+"""Narrowed delivery (fls_scan_narrow): integer, DATE and DECIMAL columns
+cross PCIe as value - (their row group's zone-map minimum) in 1, 2 or 4
+bytes, and the consumer adds the base back (read_fastlanes: while filling
+DuckDB's vectors).  The delivered values must be byte-identical to the full
+width delivery, filtered or not, NULL placeholders included."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _scan(t, narrow, filt=None):
+    t.set_filter(filt or [])
+    t.narrow(narrow)
+    out = None
+    for first, arrays in t.scan():
+        if out is None:
+            out = [[] for _ in arrays]
+        for c, a in enumerate(arrays):
+            out[c].append(a)
+    t.narrow(False)
+    t.set_filter([])
+    return [np.concatenate(x) if x else np.zeros(0, np.uint8) for x in out]
+
+
+@pytest.mark.parametrize("wl,filt", [("lineitem", None), ("lineitem", [(10, ">=", 9000)]),
+                                     ("lineitem_full", None)])
+def test_narrowed_scan_matches_full_width(fl, gpu, wl, filt):
+    t = fl.Connection([0]).read_image(fl.gen_image(wl, 0.02))
+    full = _scan(t, False, filt)
+    nar = _scan(t, True, filt)
+    sch = t.schema()
+    for c in range(t.ncols):
+        if sch[c][1] in (fl.VARCHAR, fl.BLOB):
+            continue  # string_t records: pointers compared by content elsewhere
+        assert np.array_equal(full[c], nar[c]), sch[c][0]
+
+
+def test_narrowed_widths_used(fl, gpu):
+    """lineitem's DECIMAL / DATE / small-range columns do go narrow"""
+    import ctypes as C
+    t = fl.Connection([0]).read_image(fl.gen_image("lineitem", 0.02))
+    t.narrow(True)
+    fl._check(fl.lib.fls_scan_begin(t.h, None, 0, t.nrowgroups))
+    rg = fl.RowGroup()
+    assert fl._check(fl.lib.fls_scan_next(t.h, C.byref(rg))) == 1
+    widths = {t.column(c).name.decode(): (rg.narrow[c], rg.dict_width[c]) for c in range(t.ncols)}
+    assert widths["l_quantity"] == (1, 2) and widths["l_discount"] == (1, 1) and widths["l_tax"] == (1, 1)
+    assert widths["l_shipdate"][0] == 1 and widths["l_shipdate"][1] == 2
+    assert widths["l_returnflag"][0] == 0       # strings are never narrowed
+    t.narrow(False)
+
+
+def test_narrowed_nullable_and_negative(fl, gpu):
+    """signed ranges around zero, NULL placeholders and all-NULL chunks"""
+    rng = np.random.default_rng(3)
+    n = 3 * 65536 + 99
+    a = rng.integers(-1000, 1000, n).astype(np.int32)
+    b = (rng.integers(0, 1 << 20, n) - (1 << 40)).astype(np.int64)
+    m = rng.random(n) < 0.2
+    z = np.ma.array(np.arange(n, dtype=np.int64), mask=np.ones(n, bool))
+    img = fl.write_image([("a", fl.INT32, np.ma.array(a, mask=m), fl.ENC_FFOR), ("b", fl.INT64, b, fl.ENC_AUTO),
+                          ("z", fl.INT64, z, fl.ENC_FFOR)])
+    t = fl.Connection([0]).read_image(img)
+    for filt in (None, [(0, ">", 0)], [(0, "is_null", None)]):
+        full = _scan(t, False, filt)
+        nar = _scan(t, True, filt)
+        for c in range(3):
+            assert np.array_equal(full[c], nar[c]), (filt, c)
