@@ -456,7 +456,23 @@ private:
 };
 
 // ---- functions -------------------------------------------------------------
-class ClientContext {};
+class ClientContext {
+public:
+    int32_t threads = 1;  // the shim's stand-in for the database's worker threads (SET threads)
+};
+// DuckDB parallel/task_scheduler.hpp: NumberOfThreads()
+class TaskScheduler {
+public:
+    static TaskScheduler &GetScheduler(ClientContext &context) {
+        static thread_local TaskScheduler s;
+        s.n_ = context.threads;
+        return s;
+    }
+    int32_t NumberOfThreads() const { return n_; }
+
+private:
+    int32_t n_ = 1;
+};
 class ExecutionContext {
 public:
     ClientContext &client;

@@ -258,6 +258,7 @@ void execute(fls_ext_db *d, Query &q, const std::vector<int> &proj, int64_t limi
              std::vector<LogicalType> &types, Sink sink, int nthreads = 1,
              const std::vector<FilterSpec> &where = {}) {
     TableFunction *f = lookup(d, q);
+    d->ctx.threads = std::max(1, nthreads);  // the database's worker threads for this query
     named_parameter_map_t named;
     TableFunctionBindInput bin{q.args, named};
     vector<LogicalType> rtypes;

@@ -29,6 +29,7 @@
 #include "duckdb/common/exception.hpp"
 #include "duckdb/common/string_util.hpp"
 #include "duckdb/main/extension_util.hpp"
+#include "duckdb/parallel/task_scheduler.hpp"
 #include "duckdb/parser/expression/constant_expression.hpp"
 #include "duckdb/parser/expression/function_expression.hpp"
 #include "duckdb/parser/tableref/table_function_ref.hpp"
@@ -79,6 +80,7 @@ struct ReadGlobalState : public GlobalTableFunctionState {
     vector<idx_t> out_ids;               // output column -> position in column_ids
     std::vector<uint8_t> mask;           // delivered table columns
     std::vector<fls_predicate> preds;    // pushed-down filter (empty: none)
+    bool narrow = false;                 // narrowed delivery of integer columns (fls_scan_narrow)
     std::deque<string> pred_strs;        // VARCHAR constants the predicates point at
     // pushed-down filters the engine cannot evaluate (e.g. EXPRESSION_FILTER):
     // applied on the host to every delivered chunk the way DuckDB's own scans
@@ -292,9 +294,15 @@ bool AddFilter(const TableFilter &f, uint32_t col, const LogicalType &type, uint
     }
 }
 
-unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &, TableFunctionInitInput &input) {
+unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &context, TableFunctionInitInput &input) {
     const auto &bind = input.bind_data->Cast<ReadBindData>();
     auto state = make_uniq<ReadGlobalState>();
+    // Narrowed delivery trades host work (adding the base back while filling
+    // each vector) for PCIe bytes: it pays when the scan is link-bound, with
+    // several threads to widen (lineitem_full SF10: 16 threads 4.3 -> 5.6-5.9e8
+    // rows/s; one thread 3.9 -> 2.7e8).  FLS_READ_NARROW=1 / 0 forces it.
+    const char *nv = std::getenv("FLS_READ_NARROW");
+    state->narrow = nv ? std::atoi(nv) != 0 : TaskScheduler::GetScheduler(context).NumberOfThreads() >= 4;
     state->column_ids = input.column_ids;
     if (input.projection_ids.empty()) {
         for (idx_t i = 0; i < input.column_ids.size(); ++i) state->out_ids.push_back(i);
@@ -370,10 +378,8 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
             // string_t); FLS_READ_DICT=0 delivers string_t (A/B knob)
             static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
             // integer columns narrowed to their row groups' ranges (value -
-            // base in 1-4 bytes, widened here); FLS_READ_NARROW=0 turns it off
-            static const bool narrow =
-                !(std::getenv("FLS_READ_NARROW") && std::atoi(std::getenv("FLS_READ_NARROW")) == 0);
-            if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 || fls_scan_narrow(t->table, narrow ? 1 : 0) != 0 ||
+            // base in 1-4 bytes, widened in EmitColumn), see ReadInitGlobal
+            if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 || fls_scan_narrow(t->table, g.narrow ? 1 : 0) != 0 ||
                 fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             g.cur = std::move(t);

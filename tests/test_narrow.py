@@ -67,3 +67,26 @@ def test_narrowed_nullable_and_negative(fl, gpu):
         nar = _scan(t, True, filt)
         for c in range(3):
             assert np.array_equal(full[c], nar[c]), (filt, c)
+
+
+@pytest.mark.parametrize("wl", ["lineitem", "lineitem_full"])
+def test_read_fastlanes_narrowed_checksum(fl, gpu, tmpfile, wl):
+    """read_fastlanes narrows at >= 4 scan threads (ReadInitGlobal): its
+    DataChunks hash the same as the 1-thread (full-width) scan, every value
+    of every column (the harness checksum is thread-count independent), with
+    and without a pushed-down filter."""
+    import sys
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).parent))
+    from ext_harness import Ext
+    p = tmpfile(f"{wl}.fls")
+    fl.gen_image(wl, 0.02).write(p)
+    e = Ext()
+    try:
+        one = e.scan_count("read_fastlanes", p, threads=1)
+        many = e.scan_count("read_fastlanes", p, threads=4)
+        assert one[:2] == many[:2]
+        w1 = e.scan_count("read_fastlanes", p, threads=1, where=[(4, "< 24")])
+        w4 = e.scan_count("read_fastlanes", p, threads=4, where=[(4, "< 24")])
+        assert w1[:2] == w4[:2] and 0 < w1[0] < one[0]
+    finally:
+        e.close()
