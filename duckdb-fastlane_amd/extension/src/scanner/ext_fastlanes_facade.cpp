@@ -477,6 +477,16 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
     return true;
 }
 
+// String bytes one row group of a column may hold (the writer's offsets are
+// 32-bit per row group); FLS_TEST_STRING_LIMIT lowers it for tests
+static uint64_t StringLimit() {
+    static const uint64_t lim = [] {
+        const char *e = std::getenv("FLS_TEST_STRING_LIMIT");
+        return e ? std::strtoull(e, nullptr, 10) : (uint64_t)UINT32_MAX;
+    }();
+    return lim;
+}
+
 // Validity of stage rows [at, at + n) from `valid(i)` for i < n: the stage's
 // words are allocated (every earlier row valid) at the column's first NULL
 // and grow with the rows from then on (new words all valid).
@@ -566,7 +576,7 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
                     memcpy(ar.grow(len), str[r].GetData(), len);
                     memcpy(rec + sizeof(string_t) * r + 8, &off, 8);
                 }
-                if (st.wbytes[c] + bytes > UINT32_MAX) {  // the writer's offsets are 32-bit
+                if (st.wbytes[c] + bytes > StringLimit()) {  // the writer's offsets are 32-bit
                     st.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
                     return false;
                 }
@@ -675,7 +685,7 @@ bool FastLanesFacade::mergeStage(Stage &st) {
                     memcpy(o.warena[c].grow(len), st.warena[c].data() + off, len);
                     memcpy(rec + sizeof(string_t) * r + 8, &at, 8);
                 }
-                if (o.wbytes[c] + bytes > UINT32_MAX) {
+                if (o.wbytes[c] + bytes > StringLimit()) {
                     st.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
                     return false;
                 }

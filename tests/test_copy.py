@@ -307,3 +307,32 @@ def test_copy_parallel_from_scan(fl, ext, ref, gpu, li_file, tmpfile):
     got = sorted(zip(k0.tolist(), k1.tolist(), s14))
     want = sorted(zip(e0.tolist(), e1.tolist(), (modes[int(c)] for c in codes)))
     assert got == want
+
+
+def test_copy_string_limit_is_per_row_group_cpu(tmpfile):
+    """The writer's string offsets are 32-bit per row group (the sink restarts
+    them at every row group of a batch): with the limit lowered to 100 KB by
+    a test hook, a batch of row groups holding 60 KB of strings each is
+    written, and a row group holding 150 KB fails with the per-row-group
+    message.  (Run in a child process: the hook is read once.)"""
+    import subprocess
+    import sys
+    code = f"""
+import sys; sys.path.insert(0, 'tests')
+from ext_harness import Ext, ExtError
+e = Ext()
+rg = 1024
+ok = [("x" * 60) for _ in range(4 * rg)]            # 60 KB per row group, 240 KB per batch
+assert e.copy_values([("s", "VARCHAR", ok)], {tmpfile('ok.fls')!r}, row_group_size=rg) == len(ok)
+big = [("y" * 150) for _ in range(rg)]               # 150 KB in one row group
+try:
+    e.copy_values([("s", "VARCHAR", big)], {tmpfile('big.fls')!r}, row_group_size=rg)
+    print("no error")
+except ExtError as x:
+    print(str(x))
+"""
+    root = str(__import__("pathlib").Path(__file__).parents[1])
+    out = subprocess.run([sys.executable, "-c", code], env={**os.environ, "FLS_TEST_STRING_LIMIT": "100000"},
+                         capture_output=True, text=True, timeout=120, cwd=root)
+    assert out.returncode == 0, out.stderr
+    assert 'column "s" holds more than 4 GiB of strings in one row group' in out.stdout, out.stdout
