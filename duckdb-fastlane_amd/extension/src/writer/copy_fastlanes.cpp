@@ -163,8 +163,11 @@ idx_t CopyDesiredBatchSize(ClientContext &, FunctionData &bind_p) {
     return bind_p.Cast<FastlaneCopyBindData>().row_group_size;
 }
 
-void CopyFinalize(ClientContext &, FunctionData &, GlobalFunctionData &gstate) {
+void CopyFinalize(ClientContext &, FunctionData &bind_p, GlobalFunctionData &gstate) {
     auto &g = gstate.Cast<FastlaneCopyGlobalState>();
+    // rotating: DuckDB asks rotate_next_file before the combine calls too, so
+    // the last rotation can open a file nothing is sunk into; it is not written
+    if (bind_p.Cast<FastlaneCopyBindData>().row_groups_per_file.IsValid() && g.rows.load() == 0) return;
     g.facade->finalizeFile();
     if (!g.facade->finalizeOk()) {
         const std::string &why = g.facade->lastError();
