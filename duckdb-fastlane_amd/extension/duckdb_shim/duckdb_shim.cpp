@@ -167,11 +167,26 @@ void Vector::Flatten(idx_t count) {
     if (data_.size() < count * w) data_.resize(count * w);
     capacity_ = std::max(capacity_, count);
     data_ptr_ = data_.data();
-    for (idx_t i = 0; i < count; ++i) {
-        const idx_t j = sel.get_index(i);
-        if (!child->RowIsValid(j)) validity_.SetInvalid(i);
-        memcpy(data_ptr_ + i * w, child->GetData() + j * w, w);
+    // typed gathers (DuckDB's flatten is a typed copy too)
+    const uint8_t *src = child->GetData();
+    auto gather = [&](auto x) {
+        using T = decltype(x);
+        T *d = reinterpret_cast<T *>(data_ptr_);
+        const T *c = reinterpret_cast<const T *>(src);
+        for (idx_t i = 0; i < count; ++i) d[i] = c[sel.get_index(i)];
+    };
+    switch (w) {
+    case 1: gather(uint8_t()); break;
+    case 2: gather(uint16_t()); break;
+    case 4: gather(uint32_t()); break;
+    case 8: gather(uint64_t()); break;
+    case 16: gather(string_t()); break;
+    default:
+        for (idx_t i = 0; i < count; ++i) memcpy(data_ptr_ + i * w, src + sel.get_index(i) * w, w);
     }
+    if (!child->Validity().AllValid())
+        for (idx_t i = 0; i < count; ++i)
+            if (!child->RowIsValid(sel.get_index(i))) validity_.SetInvalid(i);
     keep_.push_back(child);  // strings still point into the dictionary's memory
 }
 
