@@ -532,7 +532,21 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
         acc += t - tp;
         tp = t;
     };
-    chunk.Flatten();
+    // A dictionary vector of strings (read_fastlanes' DICT columns) is read
+    // through its selection: one gather of its records into the stage instead
+    // of a flatten and a copy.  Every other vector is flattened.
+    const size_t ncol = s.wtypes.size();
+    std::vector<UnifiedVectorFormat> uf(ncol);
+    std::vector<uint8_t> by_sel(ncol, 0);
+    for (size_t c = 0; c < ncol; ++c) {
+        Vector &v = chunk.data[c];
+        if (v.GetVectorType() == VectorType::DICTIONARY_VECTOR && TypeMapping::IsString(s.wtypes[c])) {
+            v.ToUnifiedFormat(chunk.size(), uf[c]);
+            by_sel[c] = 1;
+        } else {
+            v.Flatten(chunk.size());
+        }
+    }
     lap(s.prof.prep);
     // column-major: append each column's slice up to the row-group boundary
     // in bulk; a full batch of row groups goes to the writer
@@ -544,18 +558,27 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
             RawBuf &col = st.wcols[c];
-            const ValidityMask &mask = FlatVector::Validity(v);
+            const ValidityMask &mask = by_sel[c] ? uf[c].validity : FlatVector::Validity(v);
+            const SelectionVector *sel = by_sel[c] ? uf[c].sel : nullptr;
+            auto row = [&](idx_t i) -> idx_t { return sel ? sel->get_index(r0 + i) : r0 + i; };
             const bool nulls = !mask.AllValid();
-            StageValidity(st.wvalid[c], st.wrows, n, nulls, [&](idx_t i) { return mask.RowIsValid(r0 + i); });
+            StageValidity(st.wvalid[c], st.wrows, n, nulls, [&](idx_t i) { return mask.RowIsValid(row(i)); });
             if (TypeMapping::IsString(t)) {
-                // the records in one copy (a NULL row's record, undefined in
-                // DuckDB, becomes the empty string); the non-inlined strings'
-                // bytes to the arena, their pointer field := arena offset
+                // the records in one copy or, for a dictionary vector, one
+                // gather (a NULL row's record, undefined in DuckDB, becomes the
+                // empty string); the non-inlined strings' bytes to the arena,
+                // their pointer field := arena offset
                 uint8_t *rec = st.wrec[c].grow(n * sizeof(string_t));
-                memcpy(rec, FlatVector::GetData<string_t>(v) + r0, n * sizeof(string_t));
+                if (sel) {
+                    const string_t *d = (const string_t *)uf[c].data;
+                    string_t *o = (string_t *)rec;
+                    for (idx_t r = 0; r < n; ++r) o[r] = d[sel->get_index(r0 + r)];
+                } else {
+                    memcpy(rec, FlatVector::GetData<string_t>(v) + r0, n * sizeof(string_t));
+                }
                 if (nulls)
                     for (idx_t r = 0; r < n; ++r)
-                        if (!mask.RowIsValid(r0 + r)) memset(rec + sizeof(string_t) * r, 0, sizeof(string_t));
+                        if (!mask.RowIsValid(row(r))) memset(rec + sizeof(string_t) * r, 0, sizeof(string_t));
                 const string_t *str = (const string_t *)rec;
                 // lengths and the positions of the non-inlined strings without
                 // a data-dependent branch (inlined and pointer strings alternate
