@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--copy", action="store_true")
+    ap.add_argument("--copy-only", action="store_true", help="only the COPY leg")
     ap.add_argument("--gpu", action="store_true", help="also the writer with fls_writer_set_device(0)")
     ap.add_argument("--batch", type=int, default=8, help="row groups per fls_writer_add_rowgroups call (arm)")
     a = ap.parse_args()
@@ -38,6 +39,8 @@ def main():
     wl = "lineitem"
     n = fl.gen_nrows(wl, a.scale)
     img = fl.gen_image(wl, a.scale, nthreads=a.threads)
+    if a.copy_only:
+        return copy_leg(fl, a, img)
     t = fl.Connection([0]).read_image(img)
     sch = t.schema()
     cols = []
@@ -126,6 +129,11 @@ def main():
         print(f"generate + encode (fls_gen_image), {th} threads: {n / dt / 1e6:.1f} M rows/s "
               f"({g.len / 1e6:.0f} MB in {dt:.2f} s)", flush=True)
     if a.copy:
+        copy_leg(fl, a, img)
+
+
+def copy_leg(fl, a, img):
+    if True:
         from ext_harness import Ext
         e = Ext()
         with tempfile.TemporaryDirectory() as d:
