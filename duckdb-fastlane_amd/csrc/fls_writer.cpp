@@ -417,10 +417,16 @@ struct FsstTable {
             std::stable_sort(v.begin(), v.end(), [this](uint8_t a, uint8_t b) { return len[a] > len[b]; });
     }
     // longest symbol matching at p (r bytes left), or -1
+    // the longest symbol matching at p (r bytes left), or -1: one 8-byte load
+    // of the input and a masked compare per candidate (a symbol's bytes past
+    // its length are zero) instead of a memcmp call each
     int match(const uint8_t *p, size_t r) const {
+        uint64_t w = 0;
+        memcpy(&w, p, r >= 8 ? 8 : r);
         for (uint8_t c : by_first[p[0]]) {
             const uint32_t L = len[c];
-            if (L <= r && memcmp(&sym[c], p, L) == 0) return c;
+            const uint64_t m = L >= 8 ? ~0ull : (1ull << (8 * L)) - 1;
+            if (L <= r && ((w ^ sym[c]) & m) == 0) return c;
         }
         return -1;
     }
