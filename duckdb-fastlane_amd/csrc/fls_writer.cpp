@@ -410,19 +410,59 @@ struct FsstTable {
     int n = 0;
     std::vector<uint8_t> by_first[256];  // codes starting with a byte, longest first
 
+    // the final table's codes of length >= 2 by their first two bytes (CSR,
+    // each list longest first as in by_first) and its one-byte symbol per
+    // byte: the compressor then tries the few symbols that share a position's
+    // first two bytes instead of every symbol sharing its first byte (text
+    // puts 50+ symbols behind ' ')
+    std::vector<uint32_t> start2;       // 65536 + 1 offsets into codes2
+    std::vector<uint8_t> codes2;
+    int16_t one[256];
+
     void index() {
         for (auto &v : by_first) v.clear();
         for (int c = 0; c < n; ++c) by_first[sym[c] & 0xFF].push_back((uint8_t)c);
         for (auto &v : by_first)
             std::stable_sort(v.begin(), v.end(), [this](uint8_t a, uint8_t b) { return len[a] > len[b]; });
     }
-    // longest symbol matching at p (r bytes left), or -1
+    void index2() {
+        start2.assign(65537, 0);
+        for (int b = 0; b < 256; ++b) one[b] = -1;
+        for (int b = 0; b < 256; ++b)
+            for (uint8_t c : by_first[b]) {
+                if (len[c] >= 2) start2[(sym[c] & 0xFFFF) + 1]++;
+                else if (one[b] < 0) one[b] = c;  // the first one-byte symbol by_first would reach
+            }
+        for (uint32_t k = 0; k < 65536; ++k) start2[k + 1] += start2[k];
+        codes2.assign(start2[65536], 0);
+        std::vector<uint32_t> fill(start2.begin(), start2.end() - 1);
+        for (int b = 0; b < 256; ++b)  // by_first order: longest first, then code order
+            for (uint8_t c : by_first[b])
+                if (len[c] >= 2) codes2[fill[sym[c] & 0xFFFF]++] = c;
+    }
+    // the same longest match as match(), through the two-byte index
+    int match2(const uint8_t *p, size_t r) const {
+        if (r >= 2) {
+            uint64_t w = 0;
+            if (r >= 8) memcpy(&w, p, 8);
+            else memcpy(&w, p, r);
+            const uint32_t k = (uint32_t)(w & 0xFFFF);
+            for (uint32_t j = start2[k]; j < start2[k + 1]; ++j) {
+                const uint8_t c = codes2[j];
+                const uint32_t L = len[c];
+                const uint64_t m = L >= 8 ? ~0ull : (1ull << (8 * L)) - 1;
+                if (L <= r && ((w ^ sym[c]) & m) == 0) return c;
+            }
+        }
+        return one[p[0]];
+    }
     // the longest symbol matching at p (r bytes left), or -1: one 8-byte load
     // of the input and a masked compare per candidate (a symbol's bytes past
     // its length are zero) instead of a memcmp call each
     int match(const uint8_t *p, size_t r) const {
         uint64_t w = 0;
-        memcpy(&w, p, r >= 8 ? 8 : r);
+        if (r >= 8) memcpy(&w, p, 8);  // (a fixed-size copy is one load; a variable one is a call)
+        else memcpy(&w, p, r);
         for (uint8_t c : by_first[p[0]]) {
             const uint32_t L = len[c];
             const uint64_t m = L >= 8 ? ~0ull : (1ull << (8 * L)) - 1;
@@ -432,7 +472,7 @@ struct FsstTable {
     }
     void compress(const uint8_t *p, size_t n_, std::vector<uint8_t> &out) const {
         for (size_t i = 0; i < n_;) {
-            const int c = match(p + i, n_ - i);
+            const int c = match2(p + i, n_ - i);
             if (c >= 0) {
                 out.push_back((uint8_t)c);
                 i += len[c];
@@ -474,14 +514,15 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
         bool operator==(const Key &o) const { return sym == o.sym && len == o.len; }
         bool operator<(const Key &o) const { return sym != o.sym ? sym < o.sym : len < o.len; }
     };
-    struct KeyHash {
-        size_t operator()(const Key &k) const { return (size_t)(k.sym * 0x9E3779B97F4A7C15ull ^ k.len); }
-    };
     for (int round = 0; round < rounds; ++round) {
         st.index();
+        st.index2();
         // ids: 0..n-1 symbols, 256 + b escaped byte b
         std::vector<uint64_t> c1(512, 0);
-        std::unordered_map<uint32_t, uint64_t> c2;
+        // adjacent-pair counts: a flat 512 x 512 table (the pairs that occur
+        // listed once each) instead of a hash map
+        thread_local std::vector<uint32_t> c2(512 * 512, 0);
+        std::vector<uint32_t> pairs;
         auto sym_of = [&](int id, uint64_t &s, uint32_t &l) {
             if (id < 256) { s = st.sym[id]; l = st.len[id]; }
             else { s = (uint64_t)(id - 256); l = 1; }
@@ -490,19 +531,22 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
             const uint8_t *p = (const uint8_t *)bytes + sp.first;
             int prev = -1;
             for (uint32_t i = 0; i < sp.second;) {
-                const int c = st.match(p + i, sp.second - i);
+                const int c = st.match2(p + i, sp.second - i);
                 const int id = c >= 0 ? c : 256 + p[i];
                 i += c >= 0 ? st.len[c] : 1;
                 c1[id]++;
-                if (prev >= 0) c2[((uint32_t)prev << 9) | (uint32_t)id]++;
+                if (prev >= 0) {
+                    const uint32_t k = ((uint32_t)prev << 9) | (uint32_t)id;
+                    if (c2[k]++ == 0) pairs.push_back(k);
+                }
                 prev = id;
             }
         }
-        std::unordered_map<Key, uint64_t, KeyHash> gain;  // candidate symbol -> gain
-        auto add = [&](uint64_t sym, uint32_t l, uint64_t g) {
-            uint64_t &x = gain[Key{sym, l}];
-            x = std::max(x, g);
-        };
+        // candidate symbol -> gain (the largest of its occurrences), kept as a
+        // list merged by sorting rather than a hash map
+        std::vector<std::pair<Key, uint64_t>> gain;
+        gain.reserve(512 + pairs.size());
+        auto add = [&](uint64_t sym, uint32_t l, uint64_t g) { gain.push_back({Key{sym, l}, g}); };
         for (int id = 0; id < 512; ++id) {
             if (!c1[id]) continue;
             uint64_t sy;
@@ -510,18 +554,26 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
             sym_of(id, sy, l);
             add(sy, l, c1[id] * l);
         }
-        for (auto &kv : c2) {
+        for (uint32_t k : pairs) {
+            const uint64_t cnt = c2[k];
+            c2[k] = 0;  // (the table is all zero again for the next round)
             uint64_t s1, s2;
             uint32_t l1, l2;
-            sym_of((int)(kv.first >> 9), s1, l1);
-            sym_of((int)(kv.first & 511), s2, l2);
+            sym_of((int)(k >> 9), s1, l1);
+            sym_of((int)(k & 511), s2, l2);
             if (l1 >= max_len) continue;
             const uint32_t l = std::min<uint32_t>(max_len, l1 + l2);
             uint64_t sy = s1 | (s2 << (8 * l1));
             if (l < 8) sy &= (1ull << (8 * l)) - 1;
-            add(sy, l, kv.second * l);
+            add(sy, l, cnt * l);
         }
-        std::vector<std::pair<Key, uint64_t>> cand(gain.begin(), gain.end());
+        std::sort(gain.begin(), gain.end(), [](const auto &a, const auto &b) {
+            return a.first < b.first || (a.first == b.first && a.second > b.second);
+        });
+        std::vector<std::pair<Key, uint64_t>> cand;  // one entry per key, its largest gain
+        cand.reserve(gain.size());
+        for (auto &g : gain)
+            if (cand.empty() || !(cand.back().first == g.first)) cand.push_back(g);
         std::sort(cand.begin(), cand.end(), [](const auto &a, const auto &b) {
             return a.second != b.second ? a.second > b.second : a.first < b.first;
         });
@@ -571,6 +623,7 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
         }
     }
     st.index();
+    st.index2();
     return st;
 }
 
