@@ -31,12 +31,13 @@ def main():
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--copy", action="store_true")
     ap.add_argument("--copy-only", action="store_true", help="only the COPY leg")
+    ap.add_argument("--workload", default="lineitem", help="lineitem | lineitem_full (l_comment FSST)")
     ap.add_argument("--gpu", action="store_true", help="also the writer with fls_writer_set_device(0)")
     ap.add_argument("--batch", type=int, default=8, help="row groups per fls_writer_add_rowgroups call (arm)")
     a = ap.parse_args()
     import pkgload
     fl = pkgload.load()
-    wl = "lineitem"
+    wl = a.workload
     n = fl.gen_nrows(wl, a.scale)
     img = fl.gen_image(wl, a.scale, nthreads=a.threads)
     if a.copy_only:
@@ -46,7 +47,11 @@ def main():
     cols = []
     raw = 0
     for c, (name, ty, w, s, ob) in enumerate(sch):
-        if ty == fl.VARCHAR:
+        if ty == fl.VARCHAR and fl.gen_dict_string(wl, c, 0) is None:  # l_comment: free text
+            vals = [x.decode() for x in fl.gen_strings(wl, c, 0, n, a.scale)]
+            raw += sum(len(x) for x in vals)
+            cols.append((name, ty, vals, fl.ENC_AUTO, w, s))
+        elif ty == fl.VARCHAR:
             codes = fl.gen_values(wl, c, 0, n, np.uint32, a.scale)
             words = []
             while (x := fl.gen_dict_string(wl, c, len(words))) is not None:
