@@ -110,7 +110,10 @@ enum : int {
     kFsstSegBatch = 256,
     // cost ablations of the segmented kernel (wrong output, timing only):
     // no string_t records / no heap flush / no ring writes
-    kFsstAblateRecords = 512, kFsstAblateFlush = 1024, kFsstAblateWrite = 2048
+    kFsstAblateRecords = 512, kFsstAblateFlush = 1024, kFsstAblateWrite = 2048,
+    // bit 12 = lean writer and records (kFsstSegLean): lengths staged in bits,
+    // fewer VALU per code and per string_t record
+    kFsstSegLean = 4096
 };
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {

@@ -309,11 +309,60 @@ struct NullWriter {
         if (acc == 0x123456789ull) ring[wp] = 1;  // keeps the reads alive
     }
 };
-template <int WR>   // 0 accumulator, 1 two-qword, 2 sparse, 3 none (ablation)
+// The sparse writer with lengths in bits (kFsstSegLean: the staged table's
+// top byte holds 8 x the symbol length, so no multiply per code), the ring
+// position kept as the byte address of the open qword plus a bit offset, and
+// the carry out of a completed qword as one shift (the bit offset is >= 8
+// whenever a qword completes: symbols are <= 7 bytes).  The staged symbol's
+// top byte is masked off by the caller.
+struct LeanWriter {
+    lu8 *ring;
+    uint64_t acc;
+    uint32_t a, b, start;   // open qword's ring byte, bit offset in it, start position (bits)
+    __device__ __forceinline__ LeanWriter(lu8 *r, uint32_t wp)
+        : ring(r), acc(0), a(wp & ~7u), b(8 * (wp & 7)), start(8 * wp) {}
+    __device__ __forceinline__ void put(uint64_t v, uint32_t bl) {  // bl = 8 x length, <= 56
+        acc |= v << b;
+        const uint32_t nb = b + bl;
+        if (nb >= 64) {
+            __hip_atomic_fetch_or(reinterpret_cast<FLS_LDS uint64_t *>(ring + a), acc, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+            a += 8;
+            acc = v >> (64 - b);
+        }
+        b = nb & 63;
+    }
+    // an entry as staged (8 x length in the top byte): the length is added
+    // straight from the top byte (one v_add_u32_sdwa), then the high dword
+    // masked in place -- the empty asm orders the two, otherwise the compiler
+    // masks into a new register first and copies the low dword beside it
+    __device__ __forceinline__ void put_tagged(uint32_t lo, uint32_t hi) {
+        uint32_t nb = b + (hi >> 24);
+        asm("" : "+v"(hi), "+v"(nb));
+        hi &= 0x00FFFFFFu;
+        const uint64_t v = (uint64_t)hi << 32 | lo;
+        acc |= v << b;
+        if (nb >= 64) {
+            __hip_atomic_fetch_or(reinterpret_cast<FLS_LDS uint64_t *>(ring + a), acc, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+            a += 8;
+            acc = v >> (64 - b);
+        }
+        b = nb & 63;
+    }
+    __device__ __forceinline__ void finish() {
+        if (b) __hip_atomic_fetch_or(reinterpret_cast<FLS_LDS uint64_t *>(ring + a), acc, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __device__ __forceinline__ uint32_t bytes() const { return (8 * a + b - start) >> 3; }
+};
+template <int WR>   // 0 accumulator, 1 two-qword, 2 sparse, 3 none (ablation), 4 lean
 using SegWriter = typename std::conditional<
     WR == 1, TwoQWriter,
-    typename std::conditional<WR == 2, SparseWriter,
-                              typename std::conditional<WR == 3, NullWriter, QwordWriter<>>::type>::type>::type;
+    typename std::conditional<
+        WR == 2, SparseWriter,
+        typename std::conditional<WR == 3, NullWriter,
+                                  typename std::conditional<WR == 4, LeanWriter, QwordWriter<>>::type>::type>::type>::type;
 
 template <bool FULL, bool ESC, int WR = 0, bool PL = false, uint32_t FB = 8>
 __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, uint32_t nb, uint32_t &st,
@@ -327,6 +376,10 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
     // (a literal's value) beside its table entry, so it reads 4 at a time to
     // stay in the fast path's register budget
     constexpr uint32_t B = (FULL && !ESC) ? FB : 4;
+    // lean writer: lengths in bits (the staged top byte is 8 x the length)
+    constexpr bool LEAN = WR == 4;
+    static_assert(!LEAN || PL, "the lean writer reads packed lengths");
+    constexpr uint32_t kLitLen = LEAN ? 8u : 1u;
     uint32_t got = 0;
 #pragma unroll
     for (uint32_t h = 0; h < 16 / B; ++h) {
@@ -336,7 +389,9 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
         for (uint32_t k = 0; k < B; ++k) {
             c[k] = byte_of(raw, B * h + k);
             sy[k] = w.sym[c[k]];
-            if constexpr (PL) {
+            if constexpr (LEAN && FULL && !ESC) {
+                sl[k] = 0;   // put_tagged() reads the length from the entry
+            } else if constexpr (PL) {
                 sl[k] = (uint32_t)(sy[k] >> 56);
                 sy[k] &= 0x00FFFFFFFFFFFFFFull;
             } else {
@@ -352,7 +407,7 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
                 const uint32_t lit = 0u - st;                        // all ones after an escape
                 vlo = (vlo & ~lit) | (c[k] & lit);
                 vhi &= ~lit;
-                n = (n & ~lit) | (1u & lit);
+                n = (n & ~lit) | (kLitLen & lit);
                 uint32_t ns = ((c[k] + 1u) >> 8) & ~st;             // an escape code, not a literal
                 if constexpr (!FULL) {
                     const uint32_t in = 0u - (((B * h + k) - nb) >> 31);  // all ones iff Bh + k < nb
@@ -366,13 +421,18 @@ __device__ __forceinline__ uint32_t seg_lane(const Wave &w, const v4u &raw_in, u
                 vhi &= in;
                 n &= in;
             }
+            if constexpr (LEAN && FULL && !ESC) {
+                qw.put_tagged(vlo, vhi);
+                continue;
+            }
             qw.put((uint64_t)vhi << 32 | vlo, n);
-            got += n;
+            if constexpr (!LEAN) got += n;
         }
         // the next batch's table reads stay behind this batch's writes:
         // hoisted, their values would be live across them (spills)
         wave_sync();
     }
+    if constexpr (LEAN) return qw.bytes();
     return got;
 }
 
@@ -648,17 +708,34 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                 const lu32 *r32 = reinterpret_cast<const lu32 *>(w.ring);
                 const uint32_t x = d0 - ring_base, i0 = x >> 2, sh = x & 3;
                 const uint32_t w0 = r32[i0], w1 = r32[i0 + 1], w2 = r32[i0 + 2], w3 = r32[i0 + 3];
-                const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-                auto keep = [n](uint32_t word, uint32_t first) -> uint32_t {  // bytes [first, n) of 4
-                    const uint32_t c = n > first ? min(n - first, 4u) : 0u;
-                    return c >= 4 ? word : word & ((1u << (8 * c)) - 1u);
-                };
                 const uint64_t p = ptr_base + d0;
                 const bool inl = n <= 12;
-                *reinterpret_cast<ov4 *>(out + 16ull * i) =
-                    mk4(n, inl ? keep(b0, 0) : b0, inl ? keep(b1, 4) : (uint32_t)p, inl ? keep(b2, 8) : (uint32_t)(p >> 32));
+                if constexpr ((V & kFsstSegLean) != 0) {
+                    // one v_perm_b32 per word aligns and masks: selector byte
+                    // j is sh + j (a byte of the ring dword pair) while
+                    // 4k + j < n, else 12 (a zero byte); the bytes at or past
+                    // the length come from a 64-bit shift of ones by
+                    // 8 x clamp(n - 4k, 0, 4) (amounts 0..32, no wrap)
+                    const uint32_t base = 0x03020100u + sh * 0x01010101u, t = 8 * n;
+                    auto word = [&](uint32_t hi, uint32_t lo, int k) -> uint32_t {
+                        const uint32_t sk = (uint32_t)min(max((int)t - 32 * k, 0), 32);
+                        const uint32_t past = (uint32_t)(0xFFFFFFFFull << sk);
+                        const uint32_t sel = (past & 0x0C0C0C0Cu) | (~past & base);
+                        return __builtin_amdgcn_perm(hi, lo, sel);
+                    };
+                    *reinterpret_cast<ov4 *>(out + 16ull * i) =
+                        mk4(n, word(w1, w0, 0), inl ? word(w2, w1, 1) : (uint32_t)p, inl ? word(w3, w2, 2) : (uint32_t)(p >> 32));
+                } else {
+                    const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                    const uint32_t b1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                    const uint32_t b2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                    auto keep = [n](uint32_t word, uint32_t first) -> uint32_t {  // bytes [first, n) of 4
+                        const uint32_t c = n > first ? min(n - first, 4u) : 0u;
+                        return c >= 4 ? word : word & ((1u << (8 * c)) - 1u);
+                    };
+                    *reinterpret_cast<ov4 *>(out + 16ull * i) =
+                        mk4(n, inl ? keep(b0, 0) : b0, inl ? keep(b1, 4) : (uint32_t)p, inl ? keep(b2, 8) : (uint32_t)(p >> 32));
+                }
             }
             if (n_ok > 0) str_base += rl(rel1, n_ok - 1);
             next_str += n_ok;
@@ -800,7 +877,8 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             raw_next[j] = load_codes(0, j);
             sv_next[j] = load_seg(0, j);
         }
-        constexpr int WR = (V & kFsstAblateWrite) ? 3 : (V & kFsstTwoQ) ? 1 : (V & kFsstSegSparse) ? 2 : 0;
+        constexpr int WR = (V & kFsstAblateWrite) ? 3 : (V & kFsstTwoQ) ? 1 : (V & kFsstSegLean) ? 4 : (V & kFsstSegSparse) ? 2 : 0;
+        static_assert(WR != 4 || !(V & kFsstSegDouble), "the lean writer counts one segment");
         constexpr bool PL = (V & kFsstSegPackedLen) != 0;
         constexpr uint32_t FB = (V & kFsstSegWide) ? 16 : 8;
         for (uint32_t r0 = 0; r0 < comp_len; r0 += kRoundSeg) {
@@ -1063,7 +1141,8 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
                 const uint64_t sy = n >= 8 ? gs[k] : gs[k] & ((1ull << (8 * n)) - 1);
                 // kFsstSegPackedLen: the length rides in the top byte (the
                 // host sends only tables of symbols <= 7 bytes)
-                ls[k] = (SEG && (V & kFsstSegPackedLen)) ? sy | (uint64_t)n << 56 : sy;
+                // (kFsstSegLean: 8 x the length, the bit count)
+                ls[k] = (SEG && (V & kFsstSegPackedLen)) ? sy | (uint64_t)((V & kFsstSegLean) ? 8 * n : n) << 56 : sy;
                 L[Layout::kOffLen + k] = (uint8_t)n;
                 zero_last |= n > 0 && ((sy >> (8 * (n - 1))) & 0xFF) == 0;
                 long8 |= n >= 8;
@@ -1548,13 +1627,17 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
         // default: sparse stores, packed lengths, 16 reads in flight, records
         // in whole batches, ring cap 5120 (same-buffer A/B on l_comment SF10,
         // profiles/r3/abenv_fsst_r3j.txt, abenv_fsst_r3l.txt: 2 % ahead of the
-        // same without batches, 2-3 % ahead of the code-parallel kernel)
+        // same without batches, 2-3 % ahead of the code-parallel kernel), and
+        // the lean writer and records (abenv_fsst_lean_r3za.txt: 0.847 against
+        // 0.920 ms without)
         switch (how.variant) {
         case SPLWD:
             return launch_seg<SPLWD, 6144>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLWB:
-        case kFsstDefault:
             return launch_seg<SPLWB, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case kFsstDefault:
+        case SPLWB | kFsstSegLean:
+            return launch_seg<SPLWB | kFsstSegLean, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLW | kFsstAblateRecords:
             return launch_seg<SPLW | kFsstAblateRecords, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLW | kFsstAblateFlush:

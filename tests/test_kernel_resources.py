@@ -51,8 +51,8 @@ def test_default_fsst_kernel_fits_six_waves(res):
 
 
 def test_segmented_fsst_kernel_fits_five_waves_without_spill(res):
-    # fsst_kernel<16, SMALL, QUEUE, the default seg variant 381, ring cap 5120>
-    hits = _find(res, "fsst_kernelILi16E", "ELi381ELi5120EEEv")
+    # fsst_kernel<16, SMALL, QUEUE, the default seg variant 381 | kFsstSegLean = 4477, ring cap 5120>
+    hits = _find(res, "fsst_kernelILi16E", "ELi4477ELi5120EEEv")
     assert len(hits) == 4, hits
     for name, r in hits.items():
         assert r["vgpr"] <= 96 and r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
