@@ -113,7 +113,15 @@ enum : int {
     kFsstAblateRecords = 512, kFsstAblateFlush = 1024, kFsstAblateWrite = 2048,
     // bit 12 = lean writer and records (kFsstSegLean): lengths staged in bits,
     // fewer VALU per code and per string_t record
-    kFsstSegLean = 4096
+    kFsstSegLean = 4096,
+    // bit 13 = 8 KB of LDS per wave (kFsstSegD8: string lengths kept as u8,
+    // offsets scanned per batch of records; no separate length table; ring
+    // cap 4832), so 20 waves fit a CU instead of 16
+    kFsstSegD8 = 8192,
+    // bit 14 = lazy ring compaction (kFsstSegLazy): a round's retire streams
+    // the finished blocks to the heap where they lie and moves the kept tail
+    // to the ring start only when the ring is past half full
+    kFsstSegLazy = 16384
 };
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {

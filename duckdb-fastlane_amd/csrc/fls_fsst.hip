@@ -60,14 +60,17 @@ using lu32 = FLS_LDS uint32_t;
 // u32 offsets doff[1025] -- then u64 symbol[256], u8 length[256] and the ring.
 // The packed string lengths of step 1 are staged in the ring, which is free
 // until the rounds start.
-template <int BPL, bool SMALL, int SEG = 0>
+template <int BPL, bool SMALL, int SEG = 0, bool D8 = false>
 struct Lds {
     static constexpr uint32_t kOffD = 0;
     // string lengths / offsets: SMALL u8 lengths (1 KB), SMALL segmented
-    // u16 offsets mod 65536 (1025 entries), others u32 offsets (1025 entries)
-    static constexpr uint32_t kOffSym = SMALL ? (SEG ? 2064 : 1024) : 4112;
+    // u16 offsets mod 65536 (1025 entries) or u8 lengths (D8), others u32
+    // offsets (1025 entries)
+    static constexpr uint32_t kOffSym = SMALL ? ((SEG && !D8) ? 2064 : 1024) : 4112;
     static constexpr uint32_t kOffLen = kOffSym + 2048;
-    static constexpr uint32_t kOffRing = kOffLen + 256;
+    // D8: no length table (the segmented kernel reads lengths packed in the
+    // staged symbols)
+    static constexpr uint32_t kOffRing = kOffLen + (D8 ? 0 : 256);
     static constexpr uint32_t kPackedMax = SMALL ? 128 * 8 + 128 : 128 * 32 + 128;  // W <= 8 | 32, + zero row
     static constexpr uint32_t kRound = 64 * BPL;
     // 2 KiB holds a round's output at up to ~4 bytes per code; a round that
@@ -472,7 +475,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                             bool table_lfs = false) {
     static_assert(!SEG || (BPL == 16 && (V & kFsstZeroFlush)),
                   "the segmented kernel: 16 codes per lane, zero-at-flush ring");
-    using Layout = Lds<BPL, SMALL, SEG>;
+    constexpr bool D8 = SMALL && SEG && (V & kFsstSegD8) != 0;
+    static_assert(!D8 || ((V & kFsstSegBatch) && (V & kFsstSegPackedLen)), "u8 lengths: batched records, packed lengths");
+    using Layout = Lds<BPL, SMALL, SEG, D8>;
     bool bad = false;
     // kFsstCirc: a circular ring of kCirc bytes (a power of two) indexed by
     // decoded byte position mod kCirc, so retire() moves no tail, it only
@@ -488,7 +493,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     if (lane < 8) w.P[n16 + lane] = mk4(0, 0, 0, 0);
     wave_sync();
     uint32_t total = 0;
-    if constexpr (SMALL && SEG) {
+    if constexpr (SMALL && SEG && !D8) {
         // u8 lengths staged in the ring past the packed words, then each lane
         // turns 16 consecutive ones into u16 exclusive offsets (mod 65536:
         // finalize_seg rebuilds the high bits, strings being <= 255 bytes)
@@ -686,7 +691,11 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
             const uint32_t i = next_str + lane;
             const bool valid = i < nvals;
             uint32_t rel0, rel1;  // string start / end relative to str_base
-            if constexpr (SMALL) {
+            if constexpr (D8) {  // u8 lengths: offsets by a wave scan
+                const uint32_t n8 = valid ? (uint32_t)reinterpret_cast<const lu8 *>(w.D)[i] : 0u;
+                rel1 = scan_incl(n8, lane);
+                rel0 = rel1 - n8;
+            } else if constexpr (SMALL) {
                 const FLS_LDS uint16_t *D16 = reinterpret_cast<const FLS_LDS uint16_t *>(w.D);
                 const uint32_t a = D16[min(i, nvals)], b = D16[min(i + 1, nvals)];
                 const uint32_t b16 = rl(a, 0);
@@ -777,9 +786,16 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     // the ring to the heap, the unfinished tail (< 32 B) to the ring start
     // segmented kernel's flush: up to 4 blocks per lane per pass, all ring
     // reads in flight before the zeroing and the heap stores
+    // (kFsstSegLazy: blocks [flushed, upto), which lie from ring slot
+    // (flushed - ring_base) / 16 on)
+    uint32_t flushed = 0;
     auto flush_seg = [&](uint32_t upto) {
-        const uint32_t nblk = (V & kFsstAblateFlush) ? 0u : min((upto - ring_base) >> 4, Layout::kRing / 16);
-        lv4 *r16 = reinterpret_cast<lv4 *>(w.ring);
+        constexpr bool kLazy = (V & kFsstSegLazy) != 0;
+        const uint32_t from = kLazy ? flushed : ring_base;
+        const uint32_t q_off = (from - ring_base) >> 4;
+        const uint32_t nblk = (V & kFsstAblateFlush) ? 0u : min((upto - from) >> 4, Layout::kRing / 16 - min(q_off, Layout::kRing / 16));
+        lv4 *r16 = reinterpret_cast<lv4 *>(w.ring) + (kLazy ? q_off : 0u);
+        if constexpr (kLazy) flushed = max(flushed, upto);
         for (uint32_t q0 = 0; q0 < nblk; q0 += 256) {
             v4u b[4];
 #pragma unroll
@@ -792,7 +808,7 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                 const uint32_t q = q0 + 64 * j + lane;
                 if (q < nblk) {
                     r16[q] = mk4(0, 0, 0, 0);
-                    const uint32_t g = ring_base + 16 * q;
+                    const uint32_t g = from + 16 * q;
                     if (g + 16 <= hlim) *reinterpret_cast<ov4 *>(vheap + g) = b[j];
                     else bad = true;
                 }
@@ -802,12 +818,13 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
     // segmented kernel: the kept tail (an unfinished batch of strings, up to
     // a few KB) moves to the ring start 1 KB at a time, the bytes it vacates
     // back to zero
-    auto retire_seg = [&](bool force) {
+    auto retire_seg = [&](bool force, bool compact = true) {
         finalize_seg(force);
         const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
         const uint32_t new_base = keep_from & ~15u;
         flush_seg(new_base);
         wave_sync();
+        if (!compact) return;   // kFsstSegLazy: the tail stays where it is
         const uint32_t src = min(new_base - ring_base, Layout::kRing);
         const uint32_t len = min((out_pos - new_base + 15) & ~15u, Layout::kRing - 16);
         lv4 *r16 = reinterpret_cast<lv4 *>(w.ring);
@@ -900,7 +917,9 @@ __device__ void fsst_vector(const Wave &w, gu8 *packed_vec, uint32_t W, uint32_t
                 }
             }
             const bool full = r0 + kRoundSeg <= comp_len;
-            if (r0 > 0) retire_seg(false);   // the previous round's stores, after this round's loads
+            // the previous round's stores, after this round's loads
+            // (kFsstSegLazy: the tail moves only once the ring is half full)
+            if (r0 > 0) retire_seg(false, !(V & kFsstSegLazy) || out_pos - ring_base > Layout::kSegCap / 2);
             const uint32_t entry = entj[0];
             const uint32_t incl = scan_incl(dl, lane);
             uint32_t st = entry, l0 = 0, done = 0, guard = 0;
@@ -1096,7 +1115,8 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
     }
     item0 = uni(item0);
     item1 = uni(item1);
-    using Layout = Lds<BPL, SMALL, SEG>;
+    constexpr bool D8 = SMALL && SEG && (V & kFsstSegD8) != 0;
+    using Layout = Lds<BPL, SMALL, SEG, D8>;
     Wave w;
     w.P = reinterpret_cast<lv4 *>(L + Layout::kOffRing);
     w.D = reinterpret_cast<lu32 *>(L + Layout::kOffD);
@@ -1143,7 +1163,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
                 // host sends only tables of symbols <= 7 bytes)
                 // (kFsstSegLean: 8 x the length, the bit count)
                 ls[k] = (SEG && (V & kFsstSegPackedLen)) ? sy | (uint64_t)((V & kFsstSegLean) ? 8 * n : n) << 56 : sy;
-                L[Layout::kOffLen + k] = (uint8_t)n;
+                if constexpr (!D8) L[Layout::kOffLen + k] = (uint8_t)n;
                 zero_last |= n > 0 && ((sy >> (8 * (n - 1))) & 0xFF) == 0;
                 long8 |= n >= 8;
             }
@@ -1213,7 +1233,7 @@ __global__ __launch_bounds__(64, SEG ? ((V & kFsstSegDouble) ? 4 : FLS_FSST_SEG_
 template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
 hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                          hipStream_t stream, const FsstLaunch &how) {
-    const uint32_t shmem = Lds<BPL, SMALL, SEG>::kWave;
+    const uint32_t shmem = Lds<BPL, SMALL, SEG, SMALL && SEG && (V & kFsstSegD8) != 0>::kWave;
     if constexpr ((V & kFsstAbsLds) != 0) {
         // the variant addresses its dynamic LDS from 0, which holds only for a
         // kernel without static LDS: refuse to launch one that has some
@@ -1638,6 +1658,12 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
         case kFsstDefault:
         case SPLWB | kFsstSegLean:
             return launch_seg<SPLWB | kFsstSegLean, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLWB | kFsstSegLean | kFsstSegLazy:
+            return launch_seg<SPLWB | kFsstSegLean | kFsstSegLazy, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLWB | kFsstSegLean | kFsstSegD8 | kFsstSegLazy:
+            return launch_seg<SPLWB | kFsstSegLean | kFsstSegD8 | kFsstSegLazy, 4832>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLWB | kFsstSegLean | kFsstSegD8:
+            return launch_seg<SPLWB | kFsstSegLean | kFsstSegD8, 4832>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLW | kFsstAblateRecords:
             return launch_seg<SPLW | kFsstAblateRecords, 4096>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLW | kFsstAblateFlush:
