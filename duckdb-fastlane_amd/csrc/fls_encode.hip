@@ -729,7 +729,67 @@ __global__ __launch_bounds__(256, 2) void encode_rle_kernel(const EncChunk *__re
     }
 }
 
+// One lane per string.  The table is staged in LDS; a lane reads its string
+// 8 bytes at a time from two aligned qwords (the L1 serves the overlap of
+// consecutive steps) and writes its codes byte by byte into its own region.
+__global__ __launch_bounds__(256) void fsst_compress_kernel(const uint8_t *__restrict__ bytes,
+                                                            const uint32_t *__restrict__ offs, uint32_t n,
+                                                            const FsstCTable *__restrict__ tab,
+                                                            uint8_t *__restrict__ codes, uint32_t *__restrict__ clen) {
+    __shared__ FsstCTable t;
+    {
+        const v4u *src = reinterpret_cast<const v4u *>(tab);
+        v4u *dst = reinterpret_cast<v4u *>(&t);
+        for (uint32_t k = threadIdx.x; k < sizeof(FsstCTable) / 16; k += blockDim.x) dst[k] = src[k];
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t p = offs[i];
+    const uint32_t e = offs[i + 1];
+    uint8_t *out = codes + 2ull * p;
+    uint32_t o = 0;
+    while (p < e) {
+        const uint32_t r = e - p;
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(bytes + (p & ~7u));
+        const uint32_t sh = 8 * (p & 7);
+        const uint64_t lo = q[0], hi = q[1];
+        uint64_t w = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+        if (r < 8) w &= (1ull << (8 * r)) - 1;
+        int c = -1;
+        if (r >= 2) {
+            const uint32_t b = fsst_cbucket((uint32_t)(w & 0xFFFF));
+            for (uint32_t j = t.start[b], j1 = t.start[b + 1]; j < j1; ++j) {
+                const uint32_t cc = t.codes[j], L = t.len[cc];
+                const uint64_t m = L >= 8 ? ~0ull : (1ull << (8 * L)) - 1;
+                if (L <= r && ((w ^ t.sym[cc]) & m) == 0) {
+                    c = (int)cc;
+                    break;
+                }
+            }
+        }
+        if (c < 0) c = t.one[w & 0xFF];
+        if (c >= 0) {
+            out[o++] = (uint8_t)c;
+            p += max(1u, (uint32_t)t.len[c]);
+        } else {
+            out[o++] = (uint8_t)kFsstEscape;
+            out[o++] = (uint8_t)(w & 0xFF);
+            ++p;
+        }
+    }
+    clen[i] = o;
+}
+
 }  // namespace
+
+hipError_t launch_fsst_compress(const uint8_t *d_bytes, const uint32_t *d_offs, uint32_t n, const FsstCTable *d_tab,
+                                uint8_t *d_codes, uint32_t *d_clen, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(fsst_compress_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_bytes, d_offs, n, d_tab,
+                       d_codes, d_clen);
+    return hipGetLastError();
+}
 
 uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
     const uint64_t nvec = (nrows + kVectorSize - 1) / kVectorSize;

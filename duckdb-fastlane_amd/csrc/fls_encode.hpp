@@ -35,4 +35,29 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // rle: some chunk is ENC_RLE or ENC_AUTO (encode_rle_kernel follows).
 hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle);
 
+// GPU FSST compression (writer side of ENC_FSST chunks; fls_writer.cpp
+// enc_fsst).  The host builds the chunk's symbol table from its sample
+// (fsst_build) and lays it out as an FsstCTable; the GPU applies it, one lane
+// per string, with the host compressor's greedy longest match
+// (FsstTable::match2), so the code bytes are the host's.  Codes of length >= 2
+// sit in buckets of their first two bytes (fsst_cbucket), each bucket's codes
+// in the order the host tries them (length descending, then code), so the
+// first full match in a bucket is the host's match.
+constexpr uint32_t kFsstCBuckets = 1024;
+struct FsstCTable {
+    uint64_t sym[256];                   // symbols, zero past their length
+    uint8_t len[256];                    // their lengths (1..8)
+    int16_t one[256];                    // the one-byte symbol of each byte value, -1: escape it
+    uint16_t start[kFsstCBuckets + 1];   // bucket b's codes: codes[start[b] .. start[b + 1])
+    uint8_t codes[256];
+    uint8_t pad[14];
+};
+static_assert(sizeof(FsstCTable) % 16 == 0, "FsstCTable is copied in 16 B words");
+__host__ __device__ inline uint32_t fsst_cbucket(uint32_t two_bytes) { return (two_bytes * 0x9E3779B1u) >> 22; }
+// Compress strings [offs[i], offs[i + 1]) of d_bytes (offsets from 0, d_bytes
+// 8-aligned and readable 16 bytes past offs[n]): string i's codes go to
+// d_codes + 2 * offs[i] (room for every byte escaped), their count to d_clen[i].
+hipError_t launch_fsst_compress(const uint8_t *d_bytes, const uint32_t *d_offs, uint32_t n, const FsstCTable *d_tab,
+                                uint8_t *d_codes, uint32_t *d_clen, hipStream_t stream);
+
 }  // namespace fls

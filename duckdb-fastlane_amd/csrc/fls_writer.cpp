@@ -650,8 +650,162 @@ void fsst_segments(const FsstTable &st, const std::vector<uint8_t> &comp, uint8_
     memcpy(out, &sh, sizeof(sh));
 }
 
-std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n) {
+// GPU FSST compression (fls_writer_set_device): the chunk's table is built
+// here, the strings are compressed on the GPU (launch_fsst_compress, the same
+// greedy longest match as FsstTable::compress, so the same code bytes) and
+// the vectors are assembled here as for the host compressor.  One context per
+// concurrently encoding worker (its own stream and buffers), from a free list.
+struct FsstGpuCtx {
+    hipStream_t stream = nullptr;
+    uint8_t *h_in = nullptr, *d_in = nullptr, *h_codes = nullptr, *d_codes = nullptr;
+    uint32_t *h_offs = nullptr, *d_offs = nullptr, *h_clen = nullptr, *d_clen = nullptr;
+    FsstCTable *h_tab = nullptr, *d_tab = nullptr;
+    size_t in_cap = 0, n_cap = 0;
+
+    void release() {
+        if (stream) hipStreamSynchronize(stream);
+        hipHostFree(h_in);
+        hipHostFree(h_codes);
+        hipHostFree(h_offs);
+        hipHostFree(h_clen);
+        hipHostFree(h_tab);
+        hipFree(d_in);
+        hipFree(d_codes);
+        hipFree(d_offs);
+        hipFree(d_clen);
+        hipFree(d_tab);
+        if (stream) hipStreamDestroy(stream);
+        *this = FsstGpuCtx();
+    }
+#define FHIP(expr)                                                                                  \
+    do {                                                                                            \
+        const hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+    // compress strings [offs[0], offs[n]) of bytes with table st: string i's
+    // codes at h_codes + 2 * (offs[i] - offs[0]), their count h_clen[i]
+    int run(int dev, const FsstTable &st, const uint32_t *offs, const char *bytes, uint32_t n) {
+        FHIP(hipSetDevice(dev));
+        if (!stream) FHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        const size_t nb = offs[n] - offs[0];
+        if (nb + 16 > in_cap) {
+            hipHostFree(h_in);
+            hipHostFree(h_codes);
+            hipFree(d_in);
+            hipFree(d_codes);
+            h_in = h_codes = d_in = d_codes = nullptr;
+            in_cap = 0;
+            const size_t cap = std::max<size_t>(nb + 16, 1 << 20) * 5 / 4;
+            FHIP(hipHostMalloc((void **)&h_in, cap, 0));
+            FHIP(hipHostMalloc((void **)&h_codes, 2 * cap, 0));
+            FHIP(hipMalloc((void **)&d_in, cap));
+            FHIP(hipMalloc((void **)&d_codes, 2 * cap));
+            in_cap = cap;
+        }
+        if (n + 1 > n_cap) {
+            hipHostFree(h_offs);
+            hipHostFree(h_clen);
+            hipFree(d_offs);
+            hipFree(d_clen);
+            h_offs = h_clen = d_offs = d_clen = nullptr;
+            n_cap = 0;
+            FHIP(hipHostMalloc((void **)&h_offs, 4ull * (n + 1), 0));
+            FHIP(hipHostMalloc((void **)&h_clen, 4ull * (n + 1), 0));
+            FHIP(hipMalloc((void **)&d_offs, 4ull * (n + 1)));
+            FHIP(hipMalloc((void **)&d_clen, 4ull * (n + 1)));
+            n_cap = n + 1;
+        }
+        if (!h_tab) {
+            FHIP(hipHostMalloc((void **)&h_tab, sizeof(FsstCTable), 0));
+            FHIP(hipMalloc((void **)&d_tab, sizeof(FsstCTable)));
+        }
+        memcpy(h_in, bytes + offs[0], nb);
+        memset(h_in + nb, 0, 16);
+        for (uint32_t i = 0; i <= n; ++i) h_offs[i] = offs[i] - offs[0];
+        // the table: codes of length >= 2 bucketed by their first two bytes in
+        // the order the host's two-byte index lists them (by_first order)
+        FsstCTable &t = *h_tab;
+        memset(&t, 0, sizeof(t));
+        memcpy(t.sym, st.sym, sizeof(t.sym));
+        memcpy(t.len, st.len, sizeof(t.len));
+        memcpy(t.one, st.one, sizeof(t.one));
+        uint32_t cnt[kFsstCBuckets + 1] = {};
+        for (int b = 0; b < 256; ++b)
+            for (uint8_t c : st.by_first[b])
+                if (st.len[c] >= 2) cnt[fsst_cbucket((uint32_t)(st.sym[c] & 0xFFFF)) + 1]++;
+        for (uint32_t k = 0; k < kFsstCBuckets; ++k) cnt[k + 1] += cnt[k];
+        for (uint32_t k = 0; k <= kFsstCBuckets; ++k) t.start[k] = (uint16_t)cnt[k];
+        for (int b = 0; b < 256; ++b)
+            for (uint8_t c : st.by_first[b])
+                if (st.len[c] >= 2) t.codes[cnt[fsst_cbucket((uint32_t)(st.sym[c] & 0xFFFF))]++] = c;
+        FHIP(hipMemcpyAsync(d_in, h_in, nb + 16, hipMemcpyHostToDevice, stream));
+        FHIP(hipMemcpyAsync(d_offs, h_offs, 4ull * (n + 1), hipMemcpyHostToDevice, stream));
+        FHIP(hipMemcpyAsync(d_tab, h_tab, sizeof(FsstCTable), hipMemcpyHostToDevice, stream));
+        FHIP(launch_fsst_compress(d_in, d_offs, n, d_tab, d_codes, d_clen, stream));
+        FHIP(hipMemcpyAsync(h_clen, d_clen, 4ull * n, hipMemcpyDeviceToHost, stream));
+        FHIP(hipMemcpyAsync(h_codes, d_codes, 2 * nb, hipMemcpyDeviceToHost, stream));
+        FHIP(hipStreamSynchronize(stream));
+        for (uint32_t i = 0; i < n; ++i)
+            if (h_clen[i] > 2ull * (h_offs[i + 1] - h_offs[i]))
+                return fail(FLS_ERR_DEVICE, "GPU FSST compression: string %u: %u codes for %u bytes", i, h_clen[i],
+                            h_offs[i + 1] - h_offs[i]);
+        return 0;
+    }
+#undef FHIP
+};
+struct FsstGpu {
+    int dev = -1;
+    std::mutex mu;
+    std::vector<FsstGpuCtx *> idle, all;
+    std::atomic<int> err{0};   // first failure's code (the message is in the failing thread's fls_last_error)
+    std::string err_msg;
+    FsstGpuCtx *take() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (idle.empty()) {
+            all.push_back(new FsstGpuCtx());
+            return all.back();
+        }
+        FsstGpuCtx *g = idle.back();
+        idle.pop_back();
+        return g;
+    }
+    void give(FsstGpuCtx *g) {
+        std::lock_guard<std::mutex> lk(mu);
+        idle.push_back(g);
+    }
+    void failed(int rc) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (err.load() == 0) {
+            err_msg = fls_last_error();
+            err.store(rc);
+        }
+    }
+    void release() {
+        if (dev >= 0) hipSetDevice(dev);
+        for (FsstGpuCtx *g : all) {
+            g->release();
+            delete g;
+        }
+        all.clear();
+        idle.clear();
+        err.store(0);
+    }
+    ~FsstGpu() { release(); }
+};
+
+// gpu: compress on that GPU (fls_writer_set_device); a failure is recorded in
+// gpu->err (the caller reports it) and leaves an empty chunk
+std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n, FsstGpu *gpu = nullptr) {
     const FsstTable st = fsst_build(offs, bytes, n);
+    FsstGpuCtx *g = nullptr;
+    if (gpu) {
+        g = gpu->take();
+        if (const int rc = g->run(gpu->dev, st, offs, bytes, n)) {
+            gpu->give(g);
+            gpu->failed(rc);
+            return {};
+        }
+    }
     std::vector<uint8_t> table(kFsstTableBytes, 0);
     memcpy(table.data(), st.sym, 8 * 256);
     memcpy(table.data() + 8 * 256, st.len, 256);
@@ -665,7 +819,12 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
         comp.clear();
         for (uint32_t i = 0; i < 1024; ++i) {
             const size_t c0 = comp.size();
-            if (i < vn) st.compress((const uint8_t *)bytes + offs[b + i], offs[b + i + 1] - offs[b + i], comp);
+            if (i < vn && g) {
+                const uint8_t *cs = g->h_codes + 2ull * (offs[b + i] - offs[0]);
+                comp.insert(comp.end(), cs, cs + g->h_clen[b + i]);
+            } else if (i < vn) {
+                st.compress((const uint8_t *)bytes + offs[b + i], offs[b + i + 1] - offs[b + i], comp);
+            }
             clens[i] = comp.size() - c0;
         }
         for (uint32_t i = 0; i < 1024; ++i) lens[i] = i < vn ? offs[b + i + 1] - offs[b + i] : 0;
@@ -694,19 +853,21 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
         fsst_segments(st, comp, o.aux.data() + fsst_seg_off(vh));
         heap += (dbytes + 15) & ~15ull;
     }
+    if (g) gpu->give(g);
     return assemble_chunk(ENC_FSST, 32, 0, true, n, vecs, table, (uint32_t)st.n, heap, kFsstSegCodes);
 }
 
 // VARCHAR: DICT when the distinct values are few (at most n / 8, and their
 // bytes + 4 each under half the chunk's bytes), else FSST.  ENC_AUTO builds
 // the dictionary once: it is the estimate and, when DICT wins, the encoding.
-std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const char *bytes, uint32_t n) {
-    if (enc == ENC_FSST) return enc_fsst(offs, bytes, n);
+std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const char *bytes, uint32_t n,
+                                      FsstGpu *gpu = nullptr) {
+    if (enc == ENC_FSST) return enc_fsst(offs, bytes, n, gpu);
     StrDict d;
     const bool few = build_str_dict(offs, bytes, n, enc == ENC_AUTO ? n / 8 : n, d);
     if (enc == ENC_AUTO &&
         !(few && d.entry_bytes + 4ull * d.entries.size() < (uint64_t)(offs[n] - offs[0]) / 2))
-        return enc_fsst(offs, bytes, n);
+        return enc_fsst(offs, bytes, n, gpu);
     return enc_dict_str(d, n);
 }
 
@@ -1644,6 +1805,7 @@ struct fls_writer {
     FileBuilder fb;
     int threads = default_writer_threads();  // (row group, column) tasks run on this many threads
     GpuEncoder gpu;                          // fls_writer_set_device
+    FsstGpu fsst_gpu;                        // fls_writer_set_device: FSST chunks compressed on the GPU
     WorkerPool pool;
 };
 
@@ -1771,6 +1933,9 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     std::vector<uint8_t> on_gpu(ncols, 0);
     for (size_t c : gcols) on_gpu[c] = 1;
     w->pool.resize(w->threads);
+    // FSST chunks compressed on the GPU (FLS_WRITER_FSST_GPU=0: on the host)
+    const char *fg = getenv("FLS_WRITER_FSST_GPU");
+    FsstGpu *fsst_gpu = w->fsst_gpu.dev >= 0 && !(fg && atoi(fg) == 0) ? &w->fsst_gpu : nullptr;
 
     struct Pending {
         FileBuilder::RG rg;
@@ -1794,7 +1959,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         };
         if (type_is_string(cs.type)) {
             if (!nulls) {
-                p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows);
+                p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows, fsst_gpu);
                 return;
             }
             // NULL rows as empty strings
@@ -1805,7 +1970,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
                 if (row_valid(vw, i)) bytes.append((const char *)data + o[i], o[i + 1] - o[i]);
                 no[i + 1] = (uint32_t)bytes.size();
             }
-            p.rg.chunks[c] = encode_str_chunk(cs.enc, no.data(), bytes.data(), nrows);
+            p.rg.chunks[c] = encode_str_chunk(cs.enc, no.data(), bytes.data(), nrows, fsst_gpu);
             null_flags(p.rg.zones[c]);
             return;
         }
@@ -1845,9 +2010,19 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
                 for (uint32_t c = 0; c < ncols; ++c)
                     if ((type_is_string(w->fb.cols[c].type)) == (pass == 0)) tasks.emplace_back(k, c);
         w->pool.run(tasks.size(), [&](size_t t) { encode_col(seg[tasks[t].first], tasks[t].second); });
+        if (fsst_gpu && fsst_gpu->err.load()) {  // reported by seg_failed(); no row group of the segment is added
+            seg.clear();
+            return;
+        }
         for (Pending &p : seg) w->fb.rgs.push_back(std::move(p.rg));
         seg.clear();
         if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
+    };
+    // a GPU FSST compression that failed in the last segment
+    auto seg_failed = [&]() -> int {
+        if (!fsst_gpu || !fsst_gpu->err.load()) return 0;
+        const int rc = fsst_gpu->err.exchange(0);
+        return fail(rc, "%s", fsst_gpu->err_msg.c_str());
     };
     seg.reserve(nrg);
     for (uint32_t k = 0; k < nrg; ++k) {
@@ -1863,6 +2038,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             // room in the batch now; the values are staged by the tasks (the
             // caller's buffers are only valid during this call)
             if (!w->gpu.has_room(w->fb.cols, gcols, a[k].nrows)) run_seg();
+            if (const int rc = seg_failed()) return rc;
             const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size() + seg.size(), a[k].nrows, w->threads,
                                       w->fb.rgs, p.stage, p.est_dict);
             if (rc) {
@@ -1874,12 +2050,13 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         // a full batch is encoded once its last row group is in place
         if (w->gpu.dev >= 0 && w->gpu.full()) {
             run_seg();
+            if (const int rc = seg_failed()) return rc;
             const int rc = w->gpu.submit();
             if (rc) return rc;
         }
     }
     run_seg();
-    return 0;
+    return seg_failed();
 }
 }  // namespace
 
@@ -1918,11 +2095,14 @@ int fls_writer_set_device(fls_writer *w, int device) {
     if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_device: NULL writer");
     w->gpu.release();
     w->gpu.dev = -1;
+    w->fsst_gpu.release();
+    w->fsst_gpu.dev = -1;
     if (device < 0) return 0;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device >= n)
         return fail(FLS_ERR_DEVICE, "fls_writer_set_device: no GPU %d (%d visible)", device, n);
     w->gpu.dev = device;
+    w->fsst_gpu.dev = device;
     return 0;
 }
 

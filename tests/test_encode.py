@@ -246,3 +246,51 @@ def test_gpu_writer_batched_rowgroups_bytes_identical(fl, gpu, batch, n, rowgrou
     cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
     dev = fl.write_image(cols, rowgroup=rowgroup, device=0, batch=batch, threads=8).tobytes()
     assert cpu == dev
+
+
+def _fsst_columns(fl, n, rng):
+    """VARCHAR / BLOB columns the writer FSST-compresses: l_comment text, short
+    and empty strings, strings longer than 255 bytes, random binary bytes
+    (every byte value, zeros included), NULLs (written as empty strings)."""
+    words = [b"carefully", b"regular", b"deposits", b"haggle", b"ironic", b" ", b"the", b"quickly", b"final", b"."]
+    text = [b" ".join(words[j] for j in rng.integers(0, len(words), rng.integers(1, 9))) for _ in range(n)]
+    short = [bytes(rng.integers(97, 100, rng.integers(0, 4), dtype=np.uint8)) for _ in range(n)]
+    long = [b"x" * int(rng.integers(0, 600)) + bytes(rng.integers(97, 123, 7, dtype=np.uint8)) for _ in range(n)]
+    binary = [bytes(rng.integers(0, 256, rng.integers(0, 40), dtype=np.uint8)) for _ in range(n)]
+    nulls = [None if i % 5 == 0 else text[i] for i in range(n)]
+    return [("text", fl.VARCHAR, text, fl.ENC_FSST), ("short", fl.VARCHAR, short, fl.ENC_FSST),
+            ("long", fl.VARCHAR, long, fl.ENC_FSST), ("bin", fl.BLOB, binary, fl.ENC_FSST),
+            ("nulls", fl.VARCHAR, nulls, fl.ENC_FSST), ("auto", fl.VARCHAR, text, fl.ENC_AUTO)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"FLS_FSST_MAX_SYMBOLS": "8"}, {"FLS_FSST_MAX_LEN": "8"},
+                                 {"FLS_FSST_MAX_SYMBOLS": "0"}])
+@pytest.mark.parametrize("n,rowgroup", [(20000, 4096), (1, 65536), (3000, 1024)])
+def test_gpu_writer_fsst_bytes_identical(fl, gpu, monkeypatch, env, n, rowgroup):
+    """FSST chunks compressed on the GPU (fls_writer_set_device: the host builds
+    the table, the GPU applies the greedy longest match) are byte-identical to
+    the host compressor's, escapes (small tables) and 8-byte symbols included."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cols = _fsst_columns(fl, n, np.random.default_rng(n))
+    cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0, threads=4).tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+    monkeypatch.setenv("FLS_WRITER_FSST_GPU", "0")   # the knob that keeps FSST on the host
+    assert fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes() == cpu
+
+
+@pytest.mark.gpu
+def test_gpu_writer_fsst_lineitem_comment_decodes(fl, ref, gpu):
+    """l_comment through the GPU compressor: byte-identical to the host's and
+    decoded exactly by the GPU scan."""
+    from helpers import assert_column_equal, gpu_decode_all
+    n = 65536 * 2 + 100
+    ss = fl.gen_strings("lineitem_full", 15, 0, n, scale=1)
+    cols = [("l_comment", fl.VARCHAR, ss, fl.ENC_FSST)]
+    img = fl.write_image(cols, device=0, threads=8)
+    assert img.tobytes() == fl.write_image(cols).tobytes()
+    t, st, out = gpu_decode_all(fl, img)
+    assert_column_equal(fl, ref.RefFile(img), 0, out[0], img.ptr)
