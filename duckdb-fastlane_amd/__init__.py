@@ -122,6 +122,8 @@ _sig("fls_table_zonemap", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uin
      C.POINTER(C.c_uint32))
 _sig("fls_scan_dict_codes", C.c_int, _P, C.c_int)
 _sig("fls_scan_narrow", C.c_int, _P, C.c_int)
+_sig("fls_scan_defer_records", C.c_int, _P, C.c_int)
+_sig("fls_scan_build_records", C.c_int, _P, C.POINTER(RowGroup))
 _sig("fls_table_validity", C.c_int, _P, C.c_uint32, C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)))
 _sig("fls_rowgroup_may_match", C.c_int, _P, C.c_uint32, C.POINTER(Predicate), C.c_uint32)
 _sig("fls_device_upload", C.c_int, _P, C.c_uint32, C.c_uint32)

@@ -279,6 +279,16 @@ struct HostBatch {
     // as value - base in ob bytes, per (rg - rg0) * ncols + col that base
     std::vector<uint8_t> narrowed;
     std::vector<uint64_t> nbase;
+    // FSST columns delivered as string lengths (fls_scan_narrow, unfiltered
+    // scans): per column the length width (0: string_t records cross PCIe);
+    // per (rg - rg0) * ncols + col the row group's heap offset in h_heap; the
+    // string_t records rebuilt on the consumer's thread (scan_acquire) into
+    // h_rec; narrow_out = narrowed with these columns cleared (the consumer
+    // sees string_t)
+    std::vector<uint8_t> strlen_w, narrow_out, ob_out;
+    std::vector<uint64_t> heap_off;
+    std::vector<std::unique_ptr<uint8_t[]>> h_rec;
+    std::vector<uint64_t> h_rec_cap;      // rows h_rec[c] holds
 };
 
 struct Slot {                       // one batch of row groups in flight
@@ -367,6 +377,7 @@ struct ScanCtx {
     std::vector<HostTerm> terms;    // filter of this scan, sorted by clause (empty: none)
     bool dict_codes = false;        // deliver DICT string chunks as codes + dictionary
     bool narrow = false;            // deliver integer columns narrowed to their row groups' ranges
+    bool defer_records = false;     // FSST-as-lengths records built by fls_scan_build_records, not scan_acquire
     std::vector<uint32_t> rgs;      // row groups to scan, in order (pruned ones left out)
     uint32_t cur = 0;               // next position in rgs to hand out
     uint32_t pruned = 0;
@@ -581,6 +592,7 @@ struct fls_table {
     std::vector<HostTerm> filter;   // fls_scan_filter: applies to the next fls_scan_begin
     bool dict_codes = false;        // fls_scan_dict_codes: applies to the next fls_scan_begin
     bool narrow = false;            // fls_scan_narrow: applies to the next fls_scan_begin
+    bool defer_records = false;     // fls_scan_defer_records: applies to the next fls_scan_begin
     ~fls_table();
 };
 
@@ -1023,6 +1035,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
     if (filter) s.terms = *filter;
     s.dict_codes = filter != nullptr && t->dict_codes;  // scans (not materialize) only
     s.narrow = filter != nullptr && t->narrow;
+    s.defer_records = filter != nullptr && t->defer_records;
     s.dmask = s.mask;
     for (auto &h : s.terms)
         if (h.op < OP_IS_NULL) s.dmask[h.col] = 1;
@@ -1289,6 +1302,47 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         hb.narrowed[c] = 1;
         for (uint32_t r = 0; r < sl.nrg; ++r) hb.nbase[(size_t)r * ncols + c] = t->meta.rgs[sl.rg0 + r].zones[c].min;
     }
+    // FSST columns as string lengths: the narrow kernel takes the low 1 / 2 /
+    // 4 bytes of each string_t record's length word (base 0); the records are
+    // rebuilt over the copied heap on the consumer's thread (scan_acquire).
+    // Unfiltered scans only (a filtered batch compacts its rows, and the heap
+    // offsets of the delivered strings need every row's length).
+    // Opt-in (FLS_SCAN_STRLEN=1): measured neutral on the 16-CPU GPU box,
+    // where a narrowed 16-thread read_fastlanes is bound by host work rather
+    // than by the link (lineitem_full SF10: 5.72e8 rows/s with, 5.71e8
+    // without; profiles/r3/bench_e2e_strlen_r3zj.json, bench_r3zc.json).
+    hb.strlen_w.assign(ncols, 0);
+    const char *sle = getenv("FLS_SCAN_STRLEN");
+    const bool strlen_on = sle && atoi(sle) != 0;
+    for (uint32_t c = 0; strlen_on && s.narrow && s.terms.empty() && c < ncols; ++c) {
+        if (!col_selected(s.mask, c) || !type_is_string(t->meta.cols[c].type) || hb.ob[c] != 16) continue;
+        bool ok = true;
+        uint64_t maxlen = 0;
+        for (uint32_t r = sl.rg0; ok && r < sl.rg0 + sl.nrg; ++r) {
+            ok = is_fsst(t, r, c);
+            const ChunkRef &ch = t->meta.rgs[r].chunks[c];
+            const uint8_t *meta = t->img + ch.off + ch.hdr.meta_off;
+            for (uint32_t v = 0; ok && v < ch.hdr.nvec; ++v) {
+                VecMeta vm;
+                memcpy(&vm, meta + 32ull * v, 32);
+                ok = vm.for_base >= 0 && vm.bw <= 32;
+                maxlen = std::max<uint64_t>(maxlen, (uint64_t)vm.for_base + (vm.bw >= 32 ? 0xFFFFFFFFull : (1ull << vm.bw) - 1));
+            }
+        }
+        if (!ok) continue;
+        const uint8_t nw = maxlen <= 0xFF ? 1 : maxlen <= 0xFFFF ? 2 : 4;
+        hb.ob[c] = nw;
+        hb.narrowed[c] = 1;
+        hb.strlen_w[c] = nw;
+        for (uint32_t r = 0; r < sl.nrg; ++r) hb.nbase[(size_t)r * ncols + c] = 0;
+    }
+    hb.narrow_out = hb.narrowed;
+    hb.ob_out = hb.ob;
+    for (uint32_t c = 0; c < ncols; ++c)
+        if (hb.strlen_w[c]) {
+            hb.narrow_out[c] = 0;
+            hb.ob_out[c] = 16;
+        }
     // 2. decode into the slot's device columns (FSST columns also into a heap)
     const uint64_t max_rows = (uint64_t)s.batch * t->meta.rowgroup_size;
     sl.heap_bytes.assign(ncols, 0);
@@ -1306,9 +1360,20 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         }
         if (sl.heap_bytes[c]) {
             HIP_TRY(sl.d_heap[c].alloc(d.dev, sl.heap_bytes[c]));
-            HIP_TRY(hb.h_heap[c].alloc(sl.heap_bytes[c]));
+            // (+16: scan_acquire reads a string's first 16 bytes whole)
+            HIP_TRY(hb.h_heap[c].alloc(sl.heap_bytes[c] + 16));
         }
     }
+    hb.heap_off = hoff;
+    hb.h_rec.resize(ncols);
+    hb.h_rec_cap.resize(ncols, 0);
+    for (uint32_t c = 0; c < ncols; ++c)
+        if (hb.strlen_w[c] && hb.h_rec_cap[c] < max_rows) {
+            hb.h_rec[c].reset(new (std::nothrow) uint8_t[max_rows * 16]);
+            if (!hb.h_rec[c]) return fail(FLS_ERR_NOMEM, "scan: no host memory for %llu string records",
+                                          (unsigned long long)max_rows);
+            hb.h_rec_cap[c] = max_rows;
+        }
     std::vector<DevChunk> list;
     ByteCount bc;
     for (uint32_t c = 0; c < ncols; ++c) {
@@ -1398,6 +1463,57 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                         hb.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) * hb.ob[c];
     sl.busy = true;
     return 0;
+}
+
+void build_records(const fls_table *t, HostBatch &hb, uint32_t rg) {
+    // FSST columns delivered as lengths: this row group's string_t records,
+    // rebuilt here (the consumer's thread) over the pinned heap copy -- inline
+    // bytes for strings of <= 12 bytes, else a 4-byte prefix and the pointer --
+    // vector by vector from each vector's heap offset (FsstVecHeader.heap_off)
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    for (uint32_t c = 0; c < ncols && !hb.strlen_w.empty(); ++c) {
+        const uint8_t nw = hb.strlen_w[c];
+        if (!nw) continue;
+        const uint64_t i0 = t->meta.rgs[rg].first_row - t->meta.rgs[hb.rg0].first_row;
+        const uint8_t *L = hb.h_out[c].p + i0 * nw;
+        uint8_t *R = hb.h_rec[c].get() + i0 * 16;
+        const ChunkRef &ch = t->meta.rgs[rg].chunks[c];
+        const uint8_t *meta = t->img + ch.off + ch.hdr.meta_off;
+        const uint8_t *heap = hb.h_heap[c].p + hb.heap_off[(size_t)(rg - hb.rg0) * ncols + c];
+        const uint32_t nrows = t->meta.rgs[rg].nrows;
+        for (uint32_t v = 0; v < ch.hdr.nvec; ++v) {
+            VecMeta vm;
+            memcpy(&vm, meta + 32ull * v, 32);
+            FsstVecHeader fh;
+            memcpy(&fh, t->img + ch.off + ch.hdr.aux_off + vm.aux_off, sizeof(fh));
+            const uint8_t *hp = heap + fh.heap_off;
+            uint64_t pos = 0;
+            const uint32_t r1 = std::min(nrows, (v + 1) * kVectorSize);
+            for (uint32_t i = v * kVectorSize; i < r1; ++i) {
+                const uint32_t n = nw == 1 ? L[i] : nw == 2 ? ((const uint16_t *)L)[i] : ((const uint32_t *)L)[i];
+                uint64_t a, b;
+                memcpy(&a, hp + pos, 8);
+                memcpy(&b, hp + pos + 8, 8);
+                uint32_t w[4];
+                w[0] = n;
+                if (n <= 12) {
+                    a &= n >= 8 ? ~0ull : (1ull << (8 * n)) - 1;
+                    b &= n <= 8 ? 0ull : (1ull << (8 * (n - 8))) - 1;
+                    w[1] = (uint32_t)a;
+                    w[2] = (uint32_t)(a >> 32);
+                    w[3] = (uint32_t)b;
+                } else {
+                    const uint64_t p = (uint64_t)(uintptr_t)(hp + pos);
+                    w[1] = (uint32_t)a;
+                    w[2] = (uint32_t)p;
+                    w[3] = (uint32_t)(p >> 32);
+                }
+                memcpy(R + 16ull * i, w, 16);
+                pos += n;
+            }
+        }
+        hb.col_ptrs[(size_t)(rg - hb.rg0) * ncols + c] = R;
+    }
 }
 
 int scan_start(fls_table *t, ScanCtx &s) {
@@ -1512,9 +1628,10 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     out->validity = hb->valid_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
     out->dict = hb->dict_ptrs.data() + (size_t)(rg - hb->rg0) * ncols;
     out->dict_size = hb->dict_sizes.data() + (size_t)(rg - hb->rg0) * ncols;
-    out->dict_width = hb->ob.data();
-    out->narrow = hb->narrowed.data();
+    out->dict_width = hb->ob_out.data();
+    out->narrow = hb->narrow_out.data();
     out->narrow_base = hb->nbase.data() + (size_t)(rg - hb->rg0) * ncols;
+    if (!s.defer_records) build_records(t, *hb, rg);
     if (out->sel) {  // filtered: the delivered rows' validity, gathered through sel
         const size_t i0 = (size_t)(rg - hb->rg0) * ncols;
         for (uint32_t c = 0; c < ncols; ++c) {
@@ -1897,6 +2014,25 @@ int fls_table_zonemap(const fls_table *t, uint32_t rg, uint32_t col, uint64_t *m
 int fls_scan_narrow(fls_table *t, int enable) {
     if (!t) return fail(FLS_ERR_ARG, "fls_scan_narrow: NULL table");
     t->narrow = enable != 0;
+    return 0;
+}
+
+int fls_scan_defer_records(fls_table *t, int enable) {
+    if (!t) return fail(FLS_ERR_ARG, "fls_scan_defer_records: NULL table");
+    t->defer_records = enable != 0;
+    return 0;
+}
+
+int fls_scan_build_records(fls_table *t, const fls_rowgroup *rg) {
+    if (!t || !rg) return fail(FLS_ERR_ARG, "fls_scan_build_records: NULL argument");
+    HostBatch *hb = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(t->scan.mu);
+        for (const auto &o : t->scan.out)
+            if (o.first == rg->rowgroup) hb = o.second;
+    }
+    if (!hb) return fail(FLS_ERR_ARG, "fls_scan_build_records: row group %u is not held by this scan", rg->rowgroup);
+    if (t->scan.defer_records) build_records(t, *hb, rg->rowgroup);
     return 0;
 }
 

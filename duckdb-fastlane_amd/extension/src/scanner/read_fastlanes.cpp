@@ -117,6 +117,7 @@ struct ReadLocalState : public LocalTableFunctionState {
     vector<unique_ptr<TableFilterState>> residual_state;  // one per ReadGlobalState::residual (per thread)
     buffer_ptr<RowGroupPin> pin;         // the row group being emitted (nullptr: none)
     fls_rowgroup rg{};
+    fls_table *table = nullptr;          // the table rg came from (held by pin)
     idx_t rg_pos = 0;
     idx_t batch_index = 0;
 };
@@ -379,7 +380,10 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
             static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
             // integer columns narrowed to their row groups' ranges (value -
             // base in 1-4 bytes, widened in EmitColumn), see ReadInitGlobal
+            // narrowed scans deliver FSST columns as lengths; their string_t
+            // records are built by this thread after the lock (ReadFunction)
             if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 || fls_scan_narrow(t->table, g.narrow ? 1 : 0) != 0 ||
+                fls_scan_defer_records(t->table, 1) != 0 ||
                 fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             g.cur = std::move(t);
@@ -387,6 +391,7 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
         const int rc = fls_scan_acquire(g.cur->table, &l.rg);
         if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
         if (rc == 1) {
+            l.table = g.cur->table;
             l.pin = make_buffer<RowGroupPin>(g.cur, l.rg.rowgroup);
             l.rg_pos = 0;
             l.batch_index = g.rg_base[g.file_idx] + l.rg.rowgroup;
@@ -489,6 +494,10 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
                 output.SetCardinality(0);
                 return;
             }
+            // FSST columns delivered as lengths: their string_t records, on
+            // this thread after NextRowGroup's lock (fls_scan_defer_records)
+            if (fls_scan_build_records(l.table, &l.rg) != 0)
+                throw IOException(string("FastLanes scan failed: ") + fls_last_error());
         }
         const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, l.rg.nrows - l.rg_pos);
         for (idx_t j = 0; j < output.ColumnCount(); ++j) {

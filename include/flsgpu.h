@@ -206,6 +206,18 @@ int fls_scan_dict_codes(fls_table *t, int enable);
  * narrow_base); the consumer adds the base back while filling its vectors.
  * Off by default. */
 int fls_scan_narrow(fls_table *t, int enable);
+/* With fls_scan_narrow and FLS_SCAN_STRLEN=1 in the environment (opt-in:
+ * measured neutral where the consumer, not the link, is the bound), an
+ * unfiltered scan also delivers FSST string columns
+ * as their lengths (1, 2 or 4 bytes per row) plus the string heap, and the
+ * string_t records are rebuilt on the host; fls_rowgroup shows them as
+ * ordinary string_t columns.  fls_scan_acquire builds them unless
+ * fls_scan_defer_records(t, 1) was set before fls_scan_begin: then the
+ * consumer calls fls_scan_build_records(t, &rg) for each acquired row group
+ * before reading its string columns (so a consumer that serialises its
+ * acquires builds them in parallel, outside its lock). */
+int fls_scan_defer_records(fls_table *t, int enable);
+int fls_scan_build_records(fls_table *t, const fls_rowgroup *rg);
 /* Validity of column col in row group rg: 1 and *words = its bitmaps in the
  * host image (16 u64 words per 1024-row vector, DuckDB's layout: bit i of
  * word j set when row 64 j + i is valid) when the chunk holds a NULL, 0 (and

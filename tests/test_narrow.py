@@ -36,6 +36,92 @@ def test_narrowed_scan_matches_full_width(fl, gpu, wl, filt):
         assert np.array_equal(full[c], nar[c]), sch[c][0]
 
 
+def _scan_strings(fl, t, narrow, threads_cols):
+    """string columns decoded to bytes while each row group is held (the
+    records point into the scan's pinned heaps)"""
+    t.set_filter([])
+    t.narrow(narrow)
+    out = {c: [] for c in threads_cols}
+    for first, arrays in t.scan():
+        for c in threads_cols:
+            out[c] += fl.string_t_decode(arrays[c])
+    t.narrow(False)
+    return out
+
+
+@pytest.fixture
+def strlen_on(monkeypatch):
+    monkeypatch.setenv("FLS_SCAN_STRLEN", "1")   # FSST-as-lengths delivery is opt-in
+
+
+@pytest.mark.parametrize("scale", [0.02, 0.25])
+def test_fsst_lengths_delivery_matches_records(fl, gpu, strlen_on, scale):
+    """FSST columns cross PCIe as string lengths when narrowed (unfiltered
+    scans) and their string_t records are rebuilt on the host over the pinned
+    heap: every string equals the one the GPU-built records give, inline
+    (<= 12 bytes) and pointer records alike; the row group reports string_t
+    (not narrowed, 16 bytes per value)"""
+    import ctypes as C
+    t = fl.Connection([0]).read_image(fl.gen_image("lineitem_full", scale))
+    sch = t.schema()
+    sc = [c for c in range(t.ncols) if sch[c][0] == "l_comment"]
+    full = _scan_strings(fl, t, False, sc)
+    nar = _scan_strings(fl, t, True, sc)
+    for c in sc:
+        assert len(full[c]) == t.nrows and full[c] == nar[c]
+        assert full[c][:3] == fl.gen_strings("lineitem_full", c, 0, 3, scale=scale)
+    t.narrow(True)
+    fl._check(fl.lib.fls_scan_begin(t.h, None, 0, t.nrowgroups))
+    rg = fl.RowGroup()
+    assert fl._check(fl.lib.fls_scan_next(t.h, C.byref(rg))) == 1
+    assert (rg.narrow[sc[0]], rg.dict_width[sc[0]]) == (0, 16)
+    t.narrow(False)
+
+
+def test_fsst_lengths_deferred_records(fl, gpu, strlen_on):
+    """fls_scan_defer_records: acquire hands the row group out without its
+    records; fls_scan_build_records (the consumer, outside its own lock)
+    builds them -- the same strings as the immediate build"""
+    import ctypes as C
+    t = fl.Connection([0]).read_image(fl.gen_image("lineitem_full", 0.02))
+    c = [k for k in range(t.ncols) if t.schema()[k][0] == "l_comment"][0]
+    want = _scan_strings(fl, t, False, [c])[c]
+    t.narrow(True)
+    fl._check(fl.lib.fls_scan_defer_records(t.h, 1))
+    fl._check(fl.lib.fls_scan_begin(t.h, None, 0, t.nrowgroups))
+    rg = fl.RowGroup()
+    got = []
+    while fl._check(fl.lib.fls_scan_acquire(t.h, C.byref(rg))) == 1:
+        fl._check(fl.lib.fls_scan_build_records(t.h, C.byref(rg)))
+        p = C.cast(rg.columns[c], C.POINTER(C.c_uint8))
+        got += fl.string_t_decode(np.ctypeslib.as_array(p, shape=(16 * rg.nrows,)).copy())
+        fl._check(fl.lib.fls_scan_release(t.h, rg.rowgroup))
+    assert fl.lib.fls_scan_build_records(t.h, C.byref(rg)) < 0   # not held any more
+    fl._check(fl.lib.fls_scan_defer_records(t.h, 0))
+    t.narrow(False)
+    assert got == want
+
+
+def test_fsst_lengths_short_and_long_strings(fl, gpu, strlen_on):
+    """lengths of 1, 2 and 4 bytes (strings up to 255, 65535 and beyond),
+    empty strings and NULLs, each column through the host-built records"""
+    rng = np.random.default_rng(11)
+    n = 2 * 65536 + 500
+    words = [b"ab", b"xyz", b"0123456789", b"", b"q" * 13]
+    short = [b"".join(words[j] for j in rng.integers(0, 5, rng.integers(0, 6))) for _ in range(n)]
+    mid = [(b"m" * int(rng.integers(0, 700))) if i % 97 == 0 else short[i] for i in range(n)]
+    big = [(b"B" * 70000) if i == 5 else short[i] for i in range(n)]
+    nul = [None if i % 7 == 0 else short[i] for i in range(n)]
+    cols = [("s", fl.VARCHAR, short, fl.ENC_FSST), ("m", fl.VARCHAR, mid, fl.ENC_FSST),
+            ("b", fl.BLOB, big, fl.ENC_FSST), ("n", fl.VARCHAR, nul, fl.ENC_FSST)]
+    t = fl.Connection([0]).read_image(fl.write_image(cols))
+    full = _scan_strings(fl, t, False, range(4))
+    nar = _scan_strings(fl, t, True, range(4))
+    for c, (_, _, vals, _) in enumerate(cols):
+        assert nar[c] == full[c]
+        assert nar[c] == [b"" if v is None else v for v in vals]
+
+
 def test_narrowed_widths_used(fl, gpu):
     """lineitem's DECIMAL / DATE / small-range columns do go narrow"""
     import ctypes as C
