@@ -829,14 +829,19 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
 // FSST vectors per CU, the per-GPU share of an 8-GPU run) serial was faster on
 // three boxes of four (3.41 vs 3.46, 3.11 vs 3.18, 3.36 vs 3.45 ms; 3.16 vs
 // 3.09 on the fourth).  So launches with fewer than 400 FSST vectors per CU
-// run serially (FLS_OVERLAP_MIN_VECS_PER_CU).  The main kernel's wave issue
+// ran serially (FLS_OVERLAP_MIN_VECS_PER_CU).  With round 3's faster FSST
+// kernel serial also wins at SF25 (572 vectors per CU: 6.41 vs 6.51 ms) and
+// at SF12.5 against every split tried (3.22 vs 3.34-3.45 ms;
+// profiles/r3/abenv_sf25_split_r3zl.txt, abenv_sf12_split_r3zl.txt), so the
+// threshold is 800 (SF50 = 1,144 and SF100 = 2,288 vectors per CU stay
+// overlapped, as measured before).  The main kernel's wave issue
 // priority while overlapped (FLS_OVERLAP_DECODE_PRIO, s_setprio 1-3) measured
 // within 0.1 % of the default.
 struct OverlapSplit {
     // 12 FSST waves per CU beside 1 decode block: 1.6-2 % faster than 16 at
     // SF100 and SF12.5 (profiles/r2/abenv_v12.txt)
     int decode_bpc = 1, fsst_wpc = 12;
-    uint32_t min_vecs_per_cu = 400;
+    uint32_t min_vecs_per_cu = 800;
     int decode_prio = 0;  // FLS_OVERLAP_DECODE_PRIO: s_setprio of the main kernel's waves while overlapped
 };
 OverlapSplit overlap_split() {

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out/r3
 timeout -k 10 500 python -u scripts/ab_env.py --workload lineitem_full --scale 12.5 --rounds 9 \
-   --arms "ser:FLS_OVERLAP_MIN_VECS_PER_CU=400" "ovl12:FLS_OVERLAP_MIN_VECS_PER_CU=0" \
+   --arms "ser:FLS_OVERLAP_MIN_VECS_PER_CU=100000" "ovl12:FLS_OVERLAP_MIN_VECS_PER_CU=0" \
           "ovl8:FLS_OVERLAP_MIN_VECS_PER_CU=0,FLS_OVERLAP_FSST_WPC=8" "ovl4:FLS_OVERLAP_MIN_VECS_PER_CU=0,FLS_OVERLAP_FSST_WPC=4" \
           "ovl12b2:FLS_OVERLAP_MIN_VECS_PER_CU=0,FLS_OVERLAP_DECODE_BPC=2" > gpurun_out/r3/abenv_sf12_split_r3zl.txt 2>&1 &&
 timeout -k 10 500 python -u scripts/ab_env.py --workload lineitem_full --scale 25 --rounds 7 \
