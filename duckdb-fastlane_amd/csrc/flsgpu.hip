@@ -833,8 +833,9 @@ SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const Decode
 // kernel serial also wins at SF25 (572 vectors per CU: 6.41 vs 6.51 ms) and
 // at SF12.5 against every split tried (3.22 vs 3.34-3.45 ms;
 // profiles/r3/abenv_sf25_split_r3zl.txt, abenv_sf12_split_r3zl.txt), so the
-// threshold is 800 (SF50 = 1,144 and SF100 = 2,288 vectors per CU stay
-// overlapped, as measured before).  The main kernel's wave issue
+// threshold is 800; SF50 (1,144 vectors per CU) and SF100 (2,288) stay
+// overlapped: 11.17 vs 11.82 and 22.14 vs 23.80 ms (abenv_sf50_split_r3zm.txt,
+// abenv_sf100_split_r3zm.txt).  The main kernel's wave issue
 // priority while overlapped (FLS_OVERLAP_DECODE_PRIO, s_setprio 1-3) measured
 // within 0.1 % of the default.
 struct OverlapSplit {
