@@ -121,7 +121,10 @@ enum : int {
     // bit 14 = lazy ring compaction (kFsstSegLazy): a round's retire streams
     // the finished blocks to the heap where they lie and moves the kept tail
     // to the ring start only when the ring is past half full
-    kFsstSegLazy = 16384
+    kFsstSegLazy = 16384,
+    // bit 15 = registers budgeted for 4 waves per SIMD (128 VGPRs) instead of
+    // 5: the LDS admits only 16 waves per CU anyway (kFsstSegW4)
+    kFsstSegW4 = 32768
 };
 // How one FSST launch runs (launch_fsst).
 struct FsstLaunch {

@@ -1203,7 +1203,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks_generic, uint3
 #define FLS_FSST_SEG_WAVES 5  // the segmented kernel: 96 VGPRs, no spill (its LDS admits about 5 waves per SIMD)
 #endif
 template <int BPL, bool SMALL, bool QUEUE, int V, int SEG = 0>
-__global__ __launch_bounds__(64, SEG ? ((V & kFsstSegDouble) ? 4 : FLS_FSST_SEG_WAVES) : (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
+__global__ __launch_bounds__(64, SEG ? (((V & kFsstSegDouble) || (V & kFsstSegW4)) ? 4 : FLS_FSST_SEG_WAVES) : (V & kFsstW6) ? 6 : FLS_FSST_WAVES) void fsst_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                      uint32_t nitems, uint32_t *__restrict__ err,
                                                      uint32_t *__restrict__ queue, uint32_t piece) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw_generic[];
@@ -1658,6 +1658,8 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
         case kFsstDefault:
         case SPLWB | kFsstSegLean:
             return launch_seg<SPLWB | kFsstSegLean, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
+        case SPLWB | kFsstSegLean | kFsstSegW4:
+            return launch_seg<SPLWB | kFsstSegLean | kFsstSegW4, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLWB | kFsstSegLean | kFsstSegLazy:
             return launch_seg<SPLWB | kFsstSegLean | kFsstSegLazy, 5120>(d_chunks, nchunks, nvecs, d_err, stream, how);
         case SPLWB | kFsstSegLean | kFsstSegD8 | kFsstSegLazy:
