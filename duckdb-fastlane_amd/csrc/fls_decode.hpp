@@ -141,6 +141,11 @@ struct FsstLaunch {
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, const FsstLaunch &how);
+// Whether this build holds the FSST kernel for (variant, segmented, bytes per
+// lane): the product build only each kernel's default (kFsstDefault, 8 bytes
+// per lane for the code-parallel one); the experiment library (`make lab`,
+// fls_fsst_lab.hip) every variant.  launch_fsst refuses the others.
+bool fsst_variant_built(int variant, bool seg, int bytes_per_lane);
 // Launch the string-parallel FSST decode over nchunks FSST chunks whose
 // strings are all <= 255 bytes (DevChunk.vbits = 1), nvecs vectors numbered
 // through DevChunk.vec_base (fls_fsst.hip).

@@ -165,14 +165,21 @@ __global__ __launch_bounds__(256) void compact_kernel(const DevOut *__restrict__
 
 // one 1024-row tile of one narrowed column per block, 4 rows per thread
 __global__ __launch_bounds__(256) void narrow_kernel(const DevNarrow *__restrict__ cols, uint32_t nrows,
-                                                     uint32_t rg_rows) {
+                                                     uint32_t rg_rows, uint32_t *__restrict__ err) {
     const DevNarrow c = cols[blockIdx.y];
+    bool bad = false;
     for (uint32_t k = 0; k < 4; ++k) {
         const uint64_t row = (uint64_t)blockIdx.x * 1024 + k * 256 + threadIdx.x;
-        if (row >= nrows) return;
+        if (row >= nrows) break;
         const uint8_t *p = c.src + row * c.ob;
-        const uint64_t v = c.sign ? (uint64_t)load_int(p, c.ob) : load_uint(p, c.ob);
+        // (a string_t record, ob 16, narrows its 4-byte length word)
+        const uint32_t vb = c.ob == 16 ? 4u : c.ob;
+        const uint64_t v = c.sign ? (uint64_t)load_int(p, vb) : load_uint(p, vb);
         const uint64_t d = v - c.base[row / rg_rows];
+        // the difference must fit nw bytes: the zone maps bound a sound file's
+        // values (NULL placeholders included), so a value outside them is
+        // reported, never truncated into a wrong integer
+        bad |= (d >> (8 * c.nw)) != 0;
         uint8_t *q = c.dst + row * c.nw;
         switch (c.nw) {
         case 1: *q = (uint8_t)d; break;
@@ -180,15 +187,16 @@ __global__ __launch_bounds__(256) void narrow_kernel(const DevNarrow *__restrict
         default: *(uint32_t *)q = (uint32_t)d; break;
         }
     }
+    if (__ballot(bad) != 0 && __lane_id() == 0) atomicOr(err, KERR_NARROW);
 }
 
 }  // namespace
 
 hipError_t launch_narrow(const DevNarrow *d_cols, uint32_t ncols, uint32_t nrows, uint32_t rg_rows,
-                         hipStream_t stream) {
+                         uint32_t *d_err, hipStream_t stream) {
     if (ncols == 0 || nrows == 0 || rg_rows == 0) return hipSuccess;
     hipLaunchKernelGGL(narrow_kernel, dim3((nrows + 1023) / 1024, ncols), dim3(256), 0, stream, d_cols, nrows,
-                       rg_rows);
+                       rg_rows, d_err);
     return hipGetLastError();
 }
 

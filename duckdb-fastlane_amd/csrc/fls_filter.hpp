@@ -95,6 +95,9 @@ struct DevOut {               // 32 B
 static_assert(sizeof(DevOut) == 32, "DevOut is 32 B");
 
 enum : uint32_t { KERR_FILTER_STR = 16 };
+// a narrowed column's decoded value outside [base, base + 2^(8 nw)): the zone
+// maps the narrowing trusted do not bound the data (corrupt or foreign file)
+enum : uint32_t { KERR_NARROW = 64 };
 
 // Selection mask (one bit per row: 16 x u64 words per 1024-row vector) and
 // per-vector counts for the nrows decoded rows of a batch.
@@ -119,6 +122,6 @@ struct DevNarrow {            // 32 B
 };
 static_assert(sizeof(DevNarrow) == 32, "DevNarrow is 32 B");
 hipError_t launch_narrow(const DevNarrow *d_cols, uint32_t ncols, uint32_t nrows, uint32_t rg_rows,
-                         hipStream_t stream);
+                         uint32_t *d_err, hipStream_t stream);
 
 }  // namespace fls

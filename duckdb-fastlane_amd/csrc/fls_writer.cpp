@@ -616,7 +616,8 @@ FsstTable fsst_build(const uint32_t *offs, const char *bytes, uint32_t n) {
                     st.n++;
                     continue;
                 }
-                do { --c; } while (st.len[c] == 1);
+                do { --c; } while (c > 0 && st.len[c] == 1);
+                if (c < 0 || st.len[c] == 1) break;  // no multi-byte symbol left to replace
                 st.sym[c] = v;
                 st.len[c] = 1;
             }
@@ -685,6 +686,9 @@ struct FsstGpuCtx {
     // compress strings [offs[0], offs[n]) of bytes with table st: string i's
     // codes at h_codes + 2 * (offs[i] - offs[0]), their count h_clen[i]
     int run(int dev, const FsstTable &st, const uint32_t *offs, const char *bytes, uint32_t n) {
+        // test hook: a failed device compression (the writer's error path)
+        if (const char *f = getenv("FLS_TEST_FAIL_FSST_GPU"); f && atoi(f) != 0)
+            return fail(FLS_ERR_DEVICE, "injected GPU FSST compression failure");
         FHIP(hipSetDevice(dev));
         if (!stream) FHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         const size_t nb = offs[n] - offs[0];
@@ -1807,6 +1811,11 @@ struct fls_writer {
     GpuEncoder gpu;                          // fls_writer_set_device
     FsstGpu fsst_gpu;                        // fls_writer_set_device: FSST chunks compressed on the GPU
     WorkerPool pool;
+    // a failure that left work queued for row groups that were dropped (the
+    // GPU encoder's batch holds jobs indexed by them): every later add or
+    // finish fails with this instead of completing those jobs
+    int broken = 0;
+    std::string broken_msg;
 };
 
 extern "C" {
@@ -1892,6 +1901,7 @@ void fill_nulls(uint8_t *vals, uint32_t w, uint32_t n, const std::vector<uint64_
 // submitted once every row group in it is staged.
 int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
+    if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
     const size_t ncols = w->fb.cols.size();
     const uint32_t rgsz = w->fb.rowgroup_size;
     // validate every row group before any is added
@@ -2019,9 +2029,15 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
     };
     // a GPU FSST compression that failed in the last segment
+    // The segment's row groups were dropped, but the GPU encoder's current
+    // batch (and a set in flight) may hold jobs indexed by them: the writer is
+    // marked failed, so no later call completes those jobs into row groups
+    // that do not exist (or into the wrong ones).
     auto seg_failed = [&]() -> int {
         if (!fsst_gpu || !fsst_gpu->err.load()) return 0;
         const int rc = fsst_gpu->err.exchange(0);
+        w->broken = rc;
+        w->broken_msg = fsst_gpu->err_msg;
         return fail(rc, "%s", fsst_gpu->err_msg.c_str());
     };
     seg.reserve(nrg);
@@ -2119,6 +2135,7 @@ int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows) {
 int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
     if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
+    if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
     if (w->gpu.dev >= 0) {
         const int rc = w->gpu.finish(w->fb.rgs, w->threads);
         if (rc) return rc;

@@ -873,6 +873,30 @@ OverlapSplit overlap_split() {
 // (2 blocks + 8..12 waves: 24.7 ms).  The kernel trace shows the overlap phase
 // moving ~4.9 TB/s together, below the 5.6 TB/s of the main kernel alone: the
 // two compete for the CUs' LDS and issue slots as well as for HBM.
+// The FSST kernels a launch with this policy and FLS_FSST_VARIANT would run
+// must be in this build: the product library holds each kernel's default only
+// (fls_fsst.hip), the experiment library every variant (make lab).  A stale
+// tuning variable fails the decode with FLS_ERR_CONFIG instead of running a
+// kernel it did not ask for.
+int fsst_config_check(int policy) {
+    int variant = kFsstDefault;
+    const char *fv = getenv("FLS_FSST_VARIANT");
+    if (fv) {
+        char *end = nullptr;
+        const long v = strtol(fv, &end, 10);
+        if (end == fv || *end != 0 || v < 0 || v > 0xFFFF)
+            return fail(FLS_ERR_CONFIG, "FLS_FSST_VARIANT=%s is not a variant number", fv);
+        variant = (int)v;
+    }
+    const int bpl = (policy & POLICY_FSST16) ? 16 : 8;
+    if (!fsst_variant_built(variant, true, bpl) || !fsst_variant_built(variant, false, bpl))
+        return fail(FLS_ERR_CONFIG,
+                    "FSST kernel variant %d (%d bytes per lane) is not in this build: the product library holds the "
+                    "default kernels only; experiments need FLS_LIB=libflsgpu_lab.so (make lab)%s",
+                    variant, bpl, fv ? " -- unset FLS_FSST_VARIANT" : "");
+    return 0;
+}
+
 constexpr uint32_t kQueueWords = 1 + kFsstGroups;
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
                       uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
@@ -883,7 +907,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     FsstLaunch how[kFsstGroups];
     for (int g = 0; g < kFsstGroups; ++g) {
         how[g].bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
-        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv) & 0xFFFF;
+        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv) & 0xFFFF;  // fsst_config_check'ed
         how[g].small = g == 0 || g == 2;
         how[g].seg = g < 2;
         if (const char *sc = getenv("FLS_FSST_SEG_CAP")) how[g].seg_cap = atoi(sc);
@@ -1406,6 +1430,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(sl.queue.alloc(d.dev, kQueueWords));
+    if (const int rc = fsst_config_check(policy)) return rc;
     HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
                        plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
@@ -1436,7 +1461,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             }
             HIP_TRY(hipMemcpyAsync(sl.d_ndesc.p, sl.h_ndesc.p, bytes, hipMemcpyHostToDevice, sl.stream));
             HIP_TRY(launch_narrow((const DevNarrow *)sl.d_ndesc.p, (uint32_t)nc.size(), (uint32_t)rows,
-                                  t->meta.rowgroup_size, sl.stream));
+                                  t->meta.rowgroup_size, d.err.p, sl.stream));
         }
     }
     if (filtered) {
@@ -1607,6 +1632,8 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         uint32_t err = 0;
         HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
+        if (err & KERR_NARROW)
+            return fail(FLS_ERR_FORMAT, "corrupt chunk: a value outside its zone map in a narrowed column (flags 0x%x)", err);
         if (err & KERR_LDS_BASE) return fail(FLS_ERR_DEVICE, "FSST kernel: dynamic LDS not at address 0 (flags 0x%x)", err);
         if (err) return fail(FLS_ERR_FORMAT, "corrupt chunk detected while decoding (flags 0x%x)", err);
         return 0;
@@ -2179,6 +2206,7 @@ int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask) {
         HIP_TRY(hipEventCreateWithFlags(&r.side.fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&r.side.join, hipEventDisableTiming));
     }
+    if (const int rc = fsst_config_check(r.lpolicy)) return rc;
     hipEvent_t e0 = r.ev_pool[r.ev_used], e1 = r.ev_pool[r.ev_used + 1];
     r.ev_used += 2;
     HIP_TRY(hipEventRecord(e0, r.stream));

@@ -416,11 +416,16 @@ unique_ptr<TableFilterState> TableFilterState::Initialize(ClientContext &, const
 
 idx_t ColumnSegment::FilterSelection(SelectionVector &sel, Vector &vector, UnifiedVectorFormat &, const TableFilter &filter,
                                      TableFilterState &, idx_t, idx_t &approved_tuple_count) {
+    // as DuckDB's: reads the incoming selection (rows 0..approved-1 of it,
+    // so every one of them must be set) and hands back a new one
+    SelectionVector new_sel(approved_tuple_count);
     idx_t kept = 0;
     for (idx_t i = 0; i < approved_tuple_count; ++i) {
         const idx_t row = sel.get_index(i);
-        if (eval_filter(filter, vector.GetValue(row))) sel.set_index(kept++, row);
+        if (row >= vector.Capacity()) throw InternalException("FilterSelection: selection index out of range");
+        if (eval_filter(filter, vector.GetValue(row))) new_sel.set_index(kept++, row);
     }
+    sel.Initialize(new_sel);
     approved_tuple_count = kept;
     return kept;
 }

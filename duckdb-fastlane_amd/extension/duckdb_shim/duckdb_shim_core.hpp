@@ -13,6 +13,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <limits>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -267,9 +268,21 @@ class SelectionVector {
 public:
     SelectionVector() = default;
     explicit SelectionVector(sel_t *sel) : ptr_(sel) {}
-    explicit SelectionVector(idx_t count) : owned_(std::make_shared<vector<sel_t>>(count)) {
-        for (idx_t i = 0; i < count; ++i) (*owned_)[i] = (sel_t)i;
+    // DuckDB allocates the buffer and leaves it uninitialised (a DEBUG build
+    // fills it with sel_t max): poisoned here too, so code that reads an
+    // index it never wrote fails under the shim as it would in DuckDB
+    explicit SelectionVector(idx_t count)
+        : owned_(std::make_shared<vector<sel_t>>(count, std::numeric_limits<sel_t>::max())) {
         ptr_ = owned_->data();
+    }
+    // DuckDB's SelectionVector::Initialize(sel_t *) / (const SelectionVector &)
+    void Initialize(sel_t *sel) {
+        owned_.reset();
+        ptr_ = sel;
+    }
+    void Initialize(const SelectionVector &other) {
+        owned_ = other.owned_;
+        ptr_ = other.ptr_;
     }
     idx_t get_index(idx_t i) const { return ptr_ ? ptr_[i] : i; }
     void set_index(idx_t i, idx_t loc) { ptr_[i] = (sel_t)loc; }

@@ -424,6 +424,9 @@ void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector
         if (l.rg.validity && l.rg.validity[id]) {  // NULLs: flat strings beside the validity set above
             string_t *d = FlatVector::GetData<string_t>(vec);
             for (idx_t i = 0; i < n; ++i) d[i] = entries[code(i)];
+            // long strings point into the mapped file image: keep the row
+            // group (and its table) alive as long as the vector
+            vec.SetAuxiliary(l.pin);
             return;
         }
         // the row group's dictionary as a vector over the engine's string_t
@@ -513,7 +516,11 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
         }
         idx_t approved = n;
         if (!g.residual.empty()) {
+            // DuckDB's FilterSelection reads the incoming selection before it
+            // writes one (SelectionVector(n) leaves the buffer uninitialised):
+            // start from the identity over the chunk's rows
             SelectionVector sel(n);
+            for (idx_t i = 0; i < n; ++i) sel.set_index(i, i);
             for (size_t k = 0; k < g.residual.size() && approved > 0; ++k) {
                 const auto &r = g.residual[k];
                 Vector col(bind.types[r.id]);

@@ -49,7 +49,8 @@ typedef enum fls_status {
     FLS_ERR_ARG = -3,       /* bad argument (index out of range, NULL) */
     FLS_ERR_DEVICE = -4,    /* HIP runtime error or no usable GPU */
     FLS_ERR_STATE = -5,     /* call out of order (e.g. decode before upload) */
-    FLS_ERR_NOMEM = -6
+    FLS_ERR_NOMEM = -6,
+    FLS_ERR_CONFIG = -7     /* an FLS_* tuning variable names a kernel this build does not hold */
 } fls_status;
 
 typedef struct fls_connection fls_connection;

@@ -1,24 +1,86 @@
 #!/bin/bash
-# Round checkpoint: GPU tests, smoke, default bench (with PMC traffic), rocprof
-# kernel stats of the default bench, config 3/4 and ALP/FSST bench lines,
-# per-column rates.  usage: gpu_round.sh <tag>
-TAG=${1:-r}
-cd $GRAFT_REPO_ROOT
+# GPU-box runner (the one script gpurun calls): every step under its own time
+# limit, steps chained so the first failure ends the call.
+#
+#   bash scripts/gpu_round.sh <tag> <mode> [<mode> ...]
+#
+# modes:
+#   test        full `pytest -m gpu` suite, then __graft_entry__.smoke()
+#   pytest:<k>  the gpu tests matching -k <k>
+#   bench       default bench (lineitem_full SF100, PMC traffic) + rocprofv3
+#               kernel trace / stats of the same command
+#   shares      per-GPU shares of the 4- and 8-GPU runs (SF25, SF12.5)
+#   configs     bench lines of the other configurations (c3, c4, lineitem, lineitem_dbl)
+#   percol      per-column rates, lineitem_full SF10
+#   ab:<variants>:<workload>:<scale>:<cols>[:<rounds>]
+#               interleaved same-process A/B of library builds (scripts/ab.py;
+#               `base` = libflsgpu.so, `lab` = libflsgpu_lab.so ...)
+#   abenv:<workload>:<scale>:<cols>:<arms>
+#               same-buffer A/B of runtime knobs (scripts/ab_env.py; arms
+#               name=ENV=V,ENV2=V2;name2=...)
+#   e2e         read_fastlanes DataChunk delivery, 1 and 16 threads, phase profile
+#   launcher2   bench.py --gpus 2 rehearsal (both ranks on the one GPU)
+# Results go to gpurun_out/<mode>_<tag>.*; copy what is judged to profiles/.
+TAG=${1:?tag}
+shift
+cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-make -s -C duckdb-fastlane_amd && make -s -C oracle || exit 1
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rA -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
-rc=$?; echo "pytest gpu rc=$rc: $(tail -1 gpurun_out/pytest_gpu_$TAG.log)"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
-rc=$?; echo "smoke rc=$rc: $(tail -1 gpurun_out/smoke_$TAG.log)"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log
-rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python3 bench.py --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-verify --no-traffic > gpurun_out/prof_$TAG.log 2>&1
-rc=$?; echo "rocprof rc=$rc"; find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec head -3 {} \; ; [ $rc -eq 0 ] || exit $rc
-[ -n "$QUICK" ] && exit 0
-for wl in c3 c4 lineitem_full lineitem_dbl; do
-  timeout -k 10 500 python bench.py --workload $wl --steps 10 --cpu-seconds 5 > gpurun_out/bench_${wl}_$TAG.json 2> gpurun_out/bench_${wl}_$TAG.log
-  rc=$?; echo "bench $wl rc=$rc"; python3 -c "import json;d=json.load(open('gpurun_out/bench_${wl}_$TAG.json'));print(d['value'],d['roofline']['achieved'],d['roofline']['frac'],d['roofline']['traffic'])"; [ $rc -eq 0 ] || exit $rc
+O=gpurun_out
+PYT="python -u -m pytest tests -m gpu -q -rA -x -p no:cacheprovider --timeout 120 --timeout-method thread"
+step() {  # step <timeout> <log> <cmd...>: run, report, stop the call on failure
+    local t=$1 log=$2; shift 2
+    timeout -k 10 "$t" "$@" > "$log" 2>&1
+    local rc=$?
+    echo "[$TAG] $* -> rc=$rc ($(tail -1 "$log" | cut -c1-200))"
+    return $rc
+}
+for mode in "$@"; do
+  case "$mode" in
+  test)
+    step 600 $O/pytest_gpu_$TAG.log $PYT || exit $?
+    step 300 $O/smoke_$TAG.log python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+  pytest:*)
+    k=${mode#pytest:}
+    step 600 $O/pytest_${k//[^A-Za-z0-9_]/_}_$TAG.log $PYT -k "$k" || exit $? ;;
+  bench)
+    timeout -k 10 500 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.log
+    rc=$?; echo "[$TAG] bench rc=$rc"; cat $O/bench_$TAG.json; [ $rc -eq 0 ] || exit $rc
+    step 400 $O/prof_$TAG.log rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o kt --output-format csv -- \
+        python3 bench.py --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-verify --no-traffic || exit $?
+    find $O/prof_$TAG -name "*kernel_stats.csv" -exec head -4 {} \; ;;
+  shares)
+    for sf in 25 12.5; do
+      timeout -k 10 400 python bench.py --scale $sf --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-traffic \
+          > $O/bench_sf${sf}_$TAG.json 2> $O/bench_sf${sf}_$TAG.log
+      rc=$?; python3 -c "import json;d=json.load(open('$O/bench_sf${sf}_$TAG.json'));print('sf$sf', d['ms_per_step'], d['roofline']['frac'])"
+      [ $rc -eq 0 ] || exit $rc
+    done ;;
+  configs)
+    for wl in c3 c4 lineitem lineitem_dbl; do
+      timeout -k 10 500 python bench.py --workload $wl --steps 10 --cpu-seconds 5 > $O/bench_${wl}_$TAG.json 2> $O/bench_${wl}_$TAG.log
+      rc=$?; echo "[$TAG] bench $wl rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      python3 -c "import json;d=json.load(open('$O/bench_${wl}_$TAG.json'));print(d['value'],d['roofline']['achieved'],d['roofline']['frac'],d['roofline']['traffic'])"
+    done ;;
+  percol)
+    step 300 $O/percol_$TAG.txt python scripts/percol.py --workload lineitem_full --scale 10 || exit $? ;;
+  ab:*)
+    IFS=: read -r _ vars wl sc cols rounds <<< "$mode"
+    step 600 $O/ab_${TAG}_${wl}_${sc}.txt python scripts/ab.py --variants "$vars" --workload "$wl" --scale "$sc" \
+        --cols "$cols" --rounds "${rounds:-7}" || exit $?
+    grep -v amdgpu.ids $O/ab_${TAG}_${wl}_${sc}.txt ;;
+  abenv:*)
+    IFS=: read -r _ wl sc cols arms <<< "$mode"
+    step 600 $O/abenv_${TAG}_${wl}_${sc}.txt python scripts/ab_env.py --workload "$wl" --scale "$sc" --cols "$cols" \
+        --arms $(echo "$arms" | tr ';' ' ') || exit $?
+    grep -v amdgpu.ids $O/abenv_${TAG}_${wl}_${sc}.txt ;;
+  e2e)
+    step 600 $O/e2e_phases_$TAG.txt python scripts/e2e_phases.py --scale 10 || exit $? ;;
+  launcher2)
+    timeout -k 10 600 python bench.py --gpus 2 --scale 1 --steps 5 --cpu-seconds 0 --e2e-scale 0 --no-traffic \
+        > $O/bench_gpus2_$TAG.json 2> $O/bench_gpus2_$TAG.log
+    rc=$?; echo "[$TAG] launcher2 rc=$rc"; cat $O/bench_gpus2_$TAG.json; [ $rc -eq 0 ] || exit $rc ;;
+  *)
+    echo "unknown mode $mode"; exit 2 ;;
+  esac
 done
-timeout -k 10 300 python scripts/percol.py --workload lineitem_full --scale 10 > gpurun_out/percol_$TAG.txt 2>&1
-rc=$?; echo "percol rc=$rc"; grep -v amdgpu gpurun_out/percol_$TAG.txt; exit $rc

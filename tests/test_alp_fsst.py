@@ -471,3 +471,24 @@ def test_gpu_fsst_corrupt_segment_table_reported(fl, ref, gpu, monkeypatch, what
     t.device_decode()
     with pytest.raises(fl.FlsError, match="corrupt"):
         t.device_sync()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["381", "893", "1405", "2429", "0", "garbage"],
+                         ids=["seg-nolean", "ablate-records", "ablate-flush", "ablate-write", "cp-v0", "not-a-number"])
+def test_gpu_fsst_unknown_variant_refused(fl, gpu, monkeypatch, variant):
+    """the product library holds the default FSST kernels
+    only.  A tuning variable naming any other variant (the cost ablations,
+    whose output is wrong by design, among them) fails the decode with
+    FLS_ERR_CONFIG instead of silently running something else."""
+    img = fl.write_image([("s", fl.VARCHAR, fsst_text(3000, np.random.default_rng(9)), fl.ENC_FSST)])
+    t = fl.Connection().read_image(img)
+    t.device_upload()
+    monkeypatch.setenv("FLS_FSST_VARIANT", variant)
+    with pytest.raises(fl.FlsError, match="FLS_FSST_VARIANT|not in this build") as ei:
+        t.device_decode()
+        t.device_sync()
+    assert ei.value.code == -7
+    monkeypatch.delenv("FLS_FSST_VARIANT")
+    t.device_decode()
+    t.device_sync()   # the default decodes again

@@ -6,6 +6,8 @@ writer is a stub, src/writer/write_fastlane_stream.cpp:65-314)."""
 import numpy as np
 import pytest
 
+from helpers import fsst_text
+
 INT_TYPES = ["INT8", "INT16", "INT32", "INT64", "UINT8", "UINT16", "UINT32", "UINT64", "DATE", "DECIMAL"]
 
 
@@ -294,3 +296,47 @@ def test_gpu_writer_fsst_lineitem_comment_decodes(fl, ref, gpu):
     assert img.tobytes() == fl.write_image(cols).tobytes()
     t, st, out = gpu_decode_all(fl, img)
     assert_column_equal(fl, ref.RefFile(img), 0, out[0], img.ptr)
+
+
+def _add_rg(fl, w, ints, strs):
+    """one row group of (INTEGER, VARCHAR) straight through the C-ABI writer"""
+    import ctypes as C
+    o = np.zeros(len(strs) + 1, dtype=np.uint32)
+    o[1:] = np.cumsum([len(s) for s in strs])
+    buf = np.frombuffer(b"".join(strs) or b"\0", dtype=np.uint8).copy()
+    ints = np.ascontiguousarray(ints, dtype=np.int32)
+    data = (C.c_void_p * 2)(ints.ctypes.data, buf.ctypes.data)
+    offs = (C.c_void_p * 2)(None, o.ctypes.data)
+    return fl.lib.fls_writer_add_rowgroup(w, len(ints), data, offs)
+
+
+@pytest.mark.gpu
+def test_gpu_writer_fsst_failure_marks_writer_failed(fl, gpu, monkeypatch):
+    """a failed GPU FSST compression drops its segment's
+    row groups while the GPU encoder's batch still holds the integer column's
+    jobs for them.  The writer is then marked failed: a later add or finish
+    returns an error instead of completing those jobs into row groups that do
+    not exist (heap corruption) or into the wrong ones."""
+    import ctypes as C
+    rng = np.random.default_rng(5)
+    n = 4096
+    strs = [s.encode() for s in fsst_text(n, rng)]
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_set_rowgroup_size(w, n) == 0
+        assert fl.lib.fls_writer_set_device(w, 0) == 0
+        assert fl.lib.fls_writer_add_column(w, b"i", fl.INTEGER, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_add_column(w, b"s", fl.VARCHAR, 0, 0, fl.ENC_FSST) == 0
+        ints = rng.integers(0, 1000, n)
+        assert _add_rg(fl, w, ints, strs) == 0          # a healthy row group in the GPU batch
+        monkeypatch.setenv("FLS_TEST_FAIL_FSST_GPU", "1")
+        assert _add_rg(fl, w, ints, strs) < 0           # its FSST chunk fails on the device
+        assert b"injected" in fl.lib.fls_last_error()
+        monkeypatch.delenv("FLS_TEST_FAIL_FSST_GPU")
+        assert _add_rg(fl, w, ints, strs) < 0           # the writer stays failed
+        assert b"failed earlier" in fl.lib.fls_last_error()
+        p, ln = C.c_void_p(), C.c_uint64()
+        assert fl.lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)) < 0
+        assert b"failed earlier" in fl.lib.fls_last_error()
+    finally:
+        fl.lib.fls_writer_free(w)

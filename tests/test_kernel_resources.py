@@ -44,15 +44,29 @@ def test_decode_kernel_fits_four_waves(res):
 
 
 def test_default_fsst_kernel_fits_six_waves(res):
-    # fsst_kernel<8, SMALL, QUEUE, kFsstW6 | kFsstZeroFlush | kFsstAbsLds = 76>
-    hits = _find(res, "fsst_kernelILi8E", "ELi76ELi0EEEv")
+    # fsst_kernel<Kind::Cp, SMALL, QUEUE>: the code-parallel kernel (chunks without segment tables)
+    hits = _find(res, "fsst_kernelILNS0_4KindE1E")
     assert len(hits) == 4, hits
-    assert all(r["vgpr"] <= 80 for r in hits.values()), hits
+    assert all(r["vgpr"] <= 80 and r["vgpr_spill"] == 0 for r in hits.values()), hits
 
 
 def test_segmented_fsst_kernel_fits_five_waves_without_spill(res):
-    # fsst_kernel<16, SMALL, QUEUE, the default seg variant 381 | kFsstSegLean = 4477, ring cap 5120>
-    hits = _find(res, "fsst_kernelILi16E", "ELi4477ELi5120EEEv")
+    # fsst_kernel<Kind::Seg, SMALL, QUEUE>: the segmented kernel (every chunk the writer produces)
+    hits = _find(res, "fsst_kernelILNS0_4KindE0E")
     assert len(hits) == 4, hits
     for name, r in hits.items():
         assert r["vgpr"] <= 96 and r["vgpr_spill"] == 0 and r["scratch"] == 0, (name, r)
+
+
+def test_product_library_holds_only_the_default_fsst_kernels(res):
+    """the wrong-output cost ablations and the losing
+    variants live in the experiment library (csrc/fls_fsst_lab.hip, make lab)
+    only.  The product library's FSST kernels are exactly the segmented and
+    code-parallel kernels (small / any strings x range / piece queue) plus the
+    string-parallel policy kernel and the writer's compressor."""
+    fsst = sorted(k for k in res if "fsst" in k)
+    decoders = [k for k in fsst if "fsst_kernel" in k]
+    assert len(decoders) == 8, decoders
+    assert all("4KindE" in k for k in decoders), decoders   # no variant / ring-cap template arguments
+    others = [k for k in fsst if "fsst_kernel" not in k]
+    assert sorted(o.split("fsst_")[1].split("_kernel")[0] for o in others) == ["compress", "sp"], others
