@@ -404,11 +404,16 @@ def dry_run(args) -> None:
     # the rank -> GPU mapping of a node with args.gpus visible devices, as a GPU run makes it
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ids = gather_objects(f"host:gpu{rank_device(local_rank, args.dry_run_node_gpus or world)}", world > 1)
+    # host threads each rank's encode would use: the node's usable cores split
+    # over the ranks on the node, exactly as main() computes them
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    threads = gather_objects(host_threads(args, local_world if world > 1 else 1), world > 1)
     if rank == 0:
         red = reduce_ranks(per_rank)
         print(json.dumps({"dry_run": True, "n_gpus": world, "rowgroups": nrg, "rows": nrows,
                           "shards": [list(shard_range(nrg, r, world)) for r in range(world)],
-                          "gpu_ids": ids, "ranks_per_gpu": ranks_per_gpu(ids),
+                          "gpu_ids": ids, "ranks_per_gpu": ranks_per_gpu(ids), "host_threads": threads,
+                          "usable_cores": host_cores()["usable"],
                           "reduced": red, "value": red["values"] / red["dt"]}), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -58,6 +58,34 @@ def test_gpus_n_spawns_ranks_and_reduces(_built, n):
     assert out["ranks_per_gpu"] == 1 and len(set(out["gpu_ids"])) == n   # one GPU per rank on an n-GPU node
 
 
+def test_gpus_8_node_rehearsal(_built):
+    """the driver's 8-GPU run must not be the first time
+    this configuration executes.  Eight ranks over gloo on the CPU, as on an
+    8-GPU node (--dry-run-node-gpus 8): SF100's 9,156 row groups split
+    1,144 / 1,145, contiguous and in rank order; one GPU per rank; each rank's
+    encode threads are the node's usable cores divided by 8; only rank 0
+    prints, and the reduction takes the slowest rank's time and every rank's
+    values."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "8", "--dry-run", "--dry-run-node-gpus",
+                        "8", "--workload", "lineitem_full", "--scale", "100"],
+                       capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["rowgroups"] == 9156 and out["rows"] == 600037902
+    sizes = [b - a for a, b in out["shards"]]
+    assert sorted(set(sizes)) == [1144, 1145] and sum(sizes) == 9156
+    assert sizes.count(1145) == 9156 - 8 * 1144
+    assert out["shards"][0][0] == 0 and out["shards"][-1][1] == 9156
+    assert all(a[1] == b[0] for a, b in zip(out["shards"], out["shards"][1:]))
+    assert out["gpu_ids"] == [f"host:gpu{r}" for r in range(8)] and out["ranks_per_gpu"] == 1
+    assert out["host_threads"] == [max(1, out["usable_cores"] // 8)] * 8
+    red = out["reduced"]
+    assert red["values"] == 600037902 and red["rowgroups"] == sizes and red["dt"] == 1.0 + 0.25 * 7
+
+
 def test_rank_device_wraps_over_visible_gpus():
     assert [bench.rank_device(r, 8) for r in range(8)] == list(range(8))
     assert [bench.rank_device(r, 1) for r in range(4)] == [0, 0, 0, 0]     # narrowed / 1-GPU lease
