@@ -325,7 +325,7 @@ def test_gpu_writer_fsst_failure_marks_writer_failed(fl, gpu, monkeypatch):
     try:
         assert fl.lib.fls_writer_set_rowgroup_size(w, n) == 0
         assert fl.lib.fls_writer_set_device(w, 0) == 0
-        assert fl.lib.fls_writer_add_column(w, b"i", fl.INTEGER, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_add_column(w, b"i", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
         assert fl.lib.fls_writer_add_column(w, b"s", fl.VARCHAR, 0, 0, fl.ENC_FSST) == 0
         ints = rng.integers(0, 1000, n)
         assert _add_rg(fl, w, ints, strs) == 0          # a healthy row group in the GPU batch
