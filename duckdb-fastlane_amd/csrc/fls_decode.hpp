@@ -133,6 +133,7 @@ struct FsstLaunch {
     uint32_t *queue = nullptr;    // piece counter (overlapped launches); nullptr: contiguous ranges
     bool reset_queue = true;      // zero it first (false: drain a queue another launch started)
     int waves_per_cu = 0;         // grid: 0 = as many as fit, else at most this many per CU
+    int grid_cus = 0;             // grid: the CUs it may run on (a CU-masked stream); 0 = all
     int variant = kFsstDefault;   // code-parallel kernel variant (kFsst* bits; FLS_FSST_VARIANT)
     bool seg = false;             // the chunks carry segment tables (DevChunk.vbits bit 1): segmented kernel
     int seg_cap = 4096;           // its ring: decoded bytes per part of a round (4096 or 5120; FLS_FSST_SEG_CAP)

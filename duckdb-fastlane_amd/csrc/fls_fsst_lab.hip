@@ -1269,6 +1269,7 @@ hipError_t launch_fsst_q(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nv
             hipSuccess)
             per_cu = 1;
     }
+    if (how.grid_cus > 0) cus = std::min(cus, how.grid_cus);   // a CU-masked stream
     const int full = cus * std::max(1, per_cu);
     int wpc = how.waves_per_cu;
     if (const char *e = getenv("FLS_FSST_WPC"); e && wpc == 0) wpc = std::max(0, atoi(e));  // A/B knob (standalone launches)

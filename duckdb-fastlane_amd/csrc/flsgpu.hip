@@ -11,6 +11,7 @@
 //     runs ahead of the consumer (DuckDB's scan thread).
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -503,6 +504,26 @@ struct fls_connection {
 struct SideStream {
     hipStream_t stream = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // CU-partitioned overlap (FLS_OVERLAP_CU_SPLIT = m): two streams whose
+    // kernels may only use disjoint CU sets -- set A (CU index mod 32 < m) for
+    // the main decode, set B for FSST -- made on first use for that m
+    int cu_m = 0;
+    hipStream_t cu_a = nullptr, cu_b = nullptr;
+    hipEvent_t join_a = nullptr, join_b = nullptr;
+    void release_cu() {
+        for (hipStream_t *st : {&cu_a, &cu_b})
+            if (*st) {
+                hipStreamSynchronize(*st);
+                hipStreamDestroy(*st);
+                *st = nullptr;
+            }
+        for (hipEvent_t *e : {&join_a, &join_b})
+            if (*e) {
+                hipEventDestroy(*e);
+                *e = nullptr;
+            }
+        cu_m = 0;
+    }
 };
 
 namespace {
@@ -551,6 +572,7 @@ struct Resident {
         if (side.stream) hipStreamDestroy(side.stream);
         if (side.fork) hipEventDestroy(side.fork);
         if (side.join) hipEventDestroy(side.join);
+        side.release_cu();
         for (auto e : ev_pool) hipEventDestroy(e);
     }
 };
@@ -844,9 +866,14 @@ struct OverlapSplit {
     int decode_bpc = 1, fsst_wpc = 12;
     uint32_t min_vecs_per_cu = 800;
     int decode_prio = 0;  // FLS_OVERLAP_DECODE_PRIO: s_setprio of the main kernel's waves while overlapped
+    // FLS_OVERLAP_CU_SPLIT = m in 1..31: the main decode starts on the CUs whose
+    // index mod 32 is < m, FSST on the others, each kind alone on its CUs
+    // (0 = the co-resident split above)
+    int cu_split = 0;
 };
 OverlapSplit overlap_split() {
     OverlapSplit o;
+    if (const char *e = getenv("FLS_OVERLAP_CU_SPLIT")) o.cu_split = std::min(31, std::max(0, atoi(e)));
     if (const char *e = getenv("FLS_OVERLAP_DECODE_BPC")) o.decode_bpc = std::max(1, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_FSST_WPC")) o.fsst_wpc = std::max(0, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_MIN_VECS_PER_CU")) o.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
@@ -898,6 +925,77 @@ int fsst_config_check(int policy) {
 }
 
 constexpr uint32_t kQueueWords = 1 + kFsstGroups;
+
+// CU-partitioned overlap: the main decode (HBM-bound) and the FSST kernels
+// (VALU / LDS-bound) each start alone on their own CU set instead of sharing
+// every CU's LDS and issue slots (the co-resident split lost to running them
+// one after the other at the 8-GPU share, profiles/r3/abenv_sf12_split_r3zl.txt):
+//   stream A (CUs with index mod 32 < m): full decode grid, then FSST;
+//   stream B (the other CUs):             full FSST grid, then decode.
+// Both kinds drain shared queues, so whichever set finishes its kind first
+// joins the other.  A mask that takes m of every 32 CU indices gives each XCD
+// the same share whether the mask's bits run XCD by XCD or round-robin over
+// the XCDs (m a multiple of 8).
+template <class LaunchGroup>
+hipError_t launch_cu_split(const DevChunk *d_chunks, uint32_t nmain, const FsstCounts &fc, uint32_t *d_err,
+                           const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, SideStream *side,
+                           const OverlapSplit &ov, int cus, const FsstLaunch (&how)[kFsstGroups],
+                           LaunchGroup &launch_group) {
+    const int m = ov.cu_split;
+    uint32_t mask_a[8] = {}, mask_b[8] = {};
+    int na = 0, nb = 0;
+    for (int i = 0; i < std::min(cus, 256); ++i) {
+        if (i % 32 < m) {
+            mask_a[i / 32] |= 1u << (i % 32);
+            ++na;
+        } else {
+            mask_b[i / 32] |= 1u << (i % 32);
+            ++nb;
+        }
+    }
+    if (na == 0 || nb == 0) return hipErrorInvalidValue;
+    if (side->cu_m != m) {
+        side->release_cu();
+        hipError_t e = hipExtStreamCreateWithCUMask(&side->cu_a, 8, mask_a);
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&side->cu_b, 8, mask_b);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&side->join_a, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&side->join_b, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            side->release_cu();
+            return e;
+        }
+        side->cu_m = m;
+    }
+    const uint32_t shmem = 4 * (geom.p_bytes + geom.v_bytes);
+    const int bpc = std::max(1, (geom.grid > 0 ? geom.grid : decode_grid_size(shmem)) / std::max(1, cus));
+    DecodeGeom ga = geom, gb = geom;
+    ga.grid = na * bpc;
+    gb.grid = nb * bpc;
+    FsstLaunch ha[kFsstGroups], hb[kFsstGroups];
+    for (int g = 0; g < kFsstGroups; ++g) {
+        ha[g] = hb[g] = how[g];
+        ha[g].queue = hb[g].queue = d_queue + 1 + g;
+        ha[g].reset_queue = hb[g].reset_queue = false;
+        ha[g].grid_cus = na;
+        hb[g].grid_cus = nb;
+    }
+    hipError_t e = hipMemsetAsync(d_queue, 0, kQueueWords * sizeof(uint32_t), stream);
+    if (e == hipSuccess) e = hipEventRecord(side->fork, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side->cu_a, side->fork, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side->cu_b, side->fork, 0);
+    if (e == hipSuccess)
+        e = launch_decode(d_chunks, nmain, d_err, ga, side->cu_a, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
+    for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, side->cu_b, hb[g]);
+    if (e == hipSuccess)
+        e = launch_decode(d_chunks, nmain, d_err, gb, side->cu_b, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
+    for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, side->cu_a, ha[g]);
+    if (e == hipSuccess) e = hipEventRecord(side->join_a, side->cu_a);
+    if (e == hipSuccess) e = hipEventRecord(side->join_b, side->cu_b);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join_a, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join_b, 0);
+    return e;
+}
+
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
                       uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
                       SplitPlan plan, const SideStream *side = nullptr) {
@@ -922,6 +1020,10 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const uint64_t fsst_vecs = fc.total_vecs();
+    if (ov.cu_split > 0 && side && side->stream && nmain > 0 && fsst_vecs > 0 && !d_split && !sp &&
+        !(policy & POLICY_STATIC))
+        return launch_cu_split(d_chunks, nmain, fc, d_err, geom, stream, d_queue, const_cast<SideStream *>(side),
+                               ov, cus, how, launch_group);
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
                          fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !d_split && !sp &&
                          !(policy & POLICY_STATIC);

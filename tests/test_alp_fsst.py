@@ -237,9 +237,10 @@ def test_gpu_alp_fsst_scan_pipeline(fl, ref, gpu, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("wl,split", [("lineitem_full", "default"), ("lineitem_full", None),
                                       ("lineitem_full", "0"), ("lineitem_full", "1,28"),
-                                      ("lineitem_full", "4,1"), ("lineitem_dbl", None)],
+                                      ("lineitem_full", "4,1"), ("lineitem_full", "cu8"),
+                                      ("lineitem_full", "cu24"), ("lineitem_dbl", None)],
                          ids=["full-default", "full-overlap", "full-serial", "full-fsst-wide", "full-fsst-narrow",
-                              "dbl"])
+                              "full-cu-split8", "full-cu-split24", "dbl"])
 def test_gpu_full_fidelity_lineitem(fl, ref, gpu, monkeypatch, wl, split):
     """Full-fidelity lineitem; with FSST columns the table decode overlaps the
     FSST kernels with the main one (launch_all): the default split, serial
@@ -250,6 +251,8 @@ def test_gpu_full_fidelity_lineitem(fl, ref, gpu, monkeypatch, wl, split):
         monkeypatch.setenv("FLS_OVERLAP_MIN_VECS_PER_CU", "0")
     if split == "0":
         monkeypatch.setenv("FLS_OVERLAP_FSST_WPC", "0")
+    elif split and split.startswith("cu"):   # CU-partitioned overlap (FLS_OVERLAP_CU_SPLIT)
+        monkeypatch.setenv("FLS_OVERLAP_CU_SPLIT", split[2:])
     elif split and split != "default":
         bpc, wpc = split.split(",")
         monkeypatch.setenv("FLS_OVERLAP_DECODE_BPC", bpc)
