@@ -23,6 +23,7 @@ const LogicalType LogicalType::FLOAT(LogicalTypeId::FLOAT);
 const LogicalType LogicalType::DOUBLE(LogicalTypeId::DOUBLE);
 const LogicalType LogicalType::VARCHAR(LogicalTypeId::VARCHAR);
 const LogicalType LogicalType::BLOB(LogicalTypeId::BLOB);
+const LogicalType LogicalType::BIT(LogicalTypeId::BIT);
 
 idx_t LogicalType::PhysicalSize() const {
     switch (id_) {
@@ -32,7 +33,7 @@ idx_t LogicalType::PhysicalSize() const {
     case LogicalTypeId::FLOAT: return 4;
     case LogicalTypeId::BIGINT: case LogicalTypeId::UBIGINT: case LogicalTypeId::DOUBLE: return 8;
     case LogicalTypeId::DECIMAL: return width_ <= 4 ? 2 : width_ <= 9 ? 4 : 8;
-    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: case LogicalTypeId::BLOB: return 16;
+    case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: case LogicalTypeId::BLOB: case LogicalTypeId::BIT: return 16;
     default: return 8;
     }
 }
@@ -56,6 +57,7 @@ string LogicalType::ToString() const {
     case LogicalTypeId::VARCHAR: return "VARCHAR";
     case LogicalTypeId::CHAR: return "CHAR";
     case LogicalTypeId::BLOB: return "BLOB";
+    case LogicalTypeId::BIT: return "BIT";
     case LogicalTypeId::LIST: return (child_ ? child_->ToString() : string("?")) + "[]";
     default: return "INVALID";
     }
@@ -108,6 +110,15 @@ string blob_to_string(const string &b) {
     return r;
 }
 
+// DuckDB's Bit::ToString: the bits after the padding, most significant first
+string bit_to_string(const string &b) {
+    string r;
+    if (b.size() < 2) return r;
+    const unsigned pad = (uint8_t)b[0];
+    for (size_t i = pad; i < 8 * (b.size() - 1); ++i) r += ((uint8_t)b[1 + i / 8] >> (7 - i % 8)) & 1 ? '1' : '0';
+    return r;
+}
+
 // DuckDB prints doubles with the shortest round-tripping representation
 string double_to_string(double v) {
     char buf[64];
@@ -125,6 +136,7 @@ string Value::ToString() const {
     switch (type_.id()) {
     case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: return str_;
     case LogicalTypeId::BLOB: return blob_to_string(str_);
+    case LogicalTypeId::BIT: return bit_to_string(str_);
     case LogicalTypeId::BOOLEAN: return int_ ? "true" : "false";
     case LogicalTypeId::UBIGINT: return std::to_string((uint64_t)int_);
     case LogicalTypeId::DATE: return date_to_string((int32_t)int_);
@@ -262,8 +274,9 @@ void Vector::SetValue(idx_t i, const Value &v) {
         memcpy(p, &s, sizeof(s));
         break;
     }
-    case LogicalTypeId::BLOB: {
-        if (v.type().id() != LogicalTypeId::BLOB) throw InternalException("Vector::SetValue: BLOB needs a BLOB value");
+    case LogicalTypeId::BLOB: case LogicalTypeId::BIT: {
+        if (v.type().id() != type_.id())
+            throw InternalException("Vector::SetValue: " + type_.ToString() + " needs a " + type_.ToString() + " value");
         string_t s = AddString(StringValue::Get(v));
         memcpy(p, &s, sizeof(s));
         break;
@@ -287,6 +300,10 @@ Value Vector::GetValue(idx_t i) const {
     case LogicalTypeId::BLOB: {
         const string_t s = ld(string_t());
         return Value::BLOB((const uint8_t *)s.GetData(), s.GetSize());
+    }
+    case LogicalTypeId::BIT: {
+        const string_t s = ld(string_t());
+        return Value::BIT((const uint8_t *)s.GetData(), s.GetSize());
     }
     case LogicalTypeId::BOOLEAN: return Value::BOOLEAN(ld(uint8_t()) != 0);
     case LogicalTypeId::TINYINT: return Value::TINYINT(ld(int8_t()));

@@ -84,7 +84,7 @@ public:
 // ---- types -----------------------------------------------------------------
 enum class LogicalTypeId : uint8_t {
     INVALID = 0, SQLNULL, BOOLEAN, TINYINT, SMALLINT, INTEGER, BIGINT, UTINYINT, USMALLINT, UINTEGER,
-    UBIGINT, DATE, FLOAT, DOUBLE, DECIMAL, VARCHAR, LIST, CHAR, BLOB
+    UBIGINT, DATE, FLOAT, DOUBLE, DECIMAL, VARCHAR, LIST, CHAR, BLOB, BIT
 };
 
 struct LogicalType {
@@ -115,7 +115,7 @@ struct LogicalType {
     string ToString() const;
 
     static const LogicalType SQLNULL, BOOLEAN, TINYINT, SMALLINT, INTEGER, BIGINT, UTINYINT, USMALLINT,
-        UINTEGER, UBIGINT, DATE, FLOAT, DOUBLE, VARCHAR, BLOB;
+        UINTEGER, UBIGINT, DATE, FLOAT, DOUBLE, VARCHAR, BLOB, BIT;
 
 private:
     LogicalTypeId id_;
@@ -181,6 +181,13 @@ public:
     static Value DOUBLE(double v) { Value x(LogicalType::DOUBLE, 0); x.dbl_ = v; return x; }
     static Value BOOLEAN(bool v) { return Value(LogicalType::BOOLEAN, (int64_t)v); }
     // DuckDB's Value::BLOB(const_data_ptr_t, idx_t): the raw bytes
+    // DuckDB's BIT value: the bitstring's bytes (byte 0 = padding bit count,
+    // the padding bits at the top of byte 1 set), as Bit::ToBit stores them
+    static Value BIT(const uint8_t *data, idx_t len) {
+        Value x(LogicalType::BIT, 0);
+        x.str_.assign((const char *)data, len);
+        return x;
+    }
     static Value BLOB(const uint8_t *data, idx_t len) {
         Value x(LogicalType::BLOB, 0);
         x.str_.assign((const char *)data, len);

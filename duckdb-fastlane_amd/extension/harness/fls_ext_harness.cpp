@@ -178,6 +178,16 @@ Value parse_constant(const std::string &t, const LogicalType &type) {
     case LogicalTypeId::DOUBLE: return Value::DOUBLE(std::strtod(t.c_str(), nullptr));
     case LogicalTypeId::VARCHAR: case LogicalTypeId::CHAR: return Value(t);
     case LogicalTypeId::BOOLEAN: return Value::BOOLEAN(t == "true" || t == "1");
+    case LogicalTypeId::BIT: {  // '0' / '1' text -> DuckDB's bitstring (Bit::ToBit)
+        const size_t n = t.size();
+        const unsigned pad = (unsigned)((8 - n % 8) % 8);
+        std::string b(1 + (n + pad) / 8, '\0');
+        b[0] = (char)pad;
+        for (unsigned i = 0; i < pad; ++i) b[1] |= (char)(1u << (7 - i));      // padding bits are set
+        for (size_t i = 0; i < n; ++i)
+            if (t[i] == '1') b[1 + (pad + i) / 8] |= (char)(1u << (7 - (pad + i) % 8));
+        return Value::BIT((const uint8_t *)b.data(), b.size());
+    }
     case LogicalTypeId::BLOB: {  // the harness passes BLOB bytes as hex digits
         std::string b;
         for (size_t i = 0; i + 1 < t.size(); i += 2) b += (char)std::stoi(t.substr(i, 2), nullptr, 16);
@@ -980,6 +990,7 @@ int fls_ext_copy_values_mt(fls_ext_db *d, const char *format, const char *dst, i
             else if (tn == "VARCHAR") ct.push_back(LogicalType::VARCHAR);
             else if (tn == "BOOLEAN") ct.push_back(LogicalType::BOOLEAN);
             else if (tn == "BLOB") ct.push_back(LogicalType::BLOB);
+            else if (tn == "BIT") ct.push_back(LogicalType::BIT);
             else if (tn == "CHAR") ct.push_back(LogicalType(LogicalTypeId::CHAR));
             else if (tn == "TINYINT") ct.push_back(LogicalType::TINYINT);
             else if (tn == "SMALLINT") ct.push_back(LogicalType::SMALLINT);

@@ -44,7 +44,8 @@ uint8_t TypeMapping::DuckDBToFastLanes(const LogicalType &type) {
     case LogicalTypeId::DECIMAL: return type.Width() <= 18 ? FLS_DECIMAL : 0;
     case LogicalTypeId::VARCHAR:
     case LogicalTypeId::CHAR: return FLS_VARCHAR;  // read back as VARCHAR, as the reference (:35-36, :89-90)
-    case LogicalTypeId::BLOB: return FLS_BLOB;     // BYTE_ARRAY (:40-42, :93-94)
+    case LogicalTypeId::BLOB:                      // BYTE_ARRAY (:40-42, :93-94)
+    case LogicalTypeId::BIT: return FLS_BLOB;      // the bitstring's bytes; read back as BLOB, as the reference (:41-42)
     case LogicalTypeId::FLOAT: return FLS_FLOAT;    // ALP
     case LogicalTypeId::DOUBLE: return FLS_DOUBLE;  // ALP
     default: return 0;

@@ -169,3 +169,60 @@ def test_scan_fastlanes_and_facade_render_boolean_blob(ext, gpu, tmpfile):
     names, ftypes, frows, _ = ext.facade_read(dst)
     assert ftypes == ["BOOLEAN", "BLOB", "VARCHAR", "BIGINT"]
     assert frows == [["true" if b[i] else "false", _duck_blob(x[i]), ch[i], str(i)] for i in range(n)]
+
+
+# ---- BIT: stored as its bitstring bytes, read back as BLOB (reference
+# src/type_mapping.cpp:41-42 maps LogicalTypeId::BIT to BYTE_ARRAY, and
+# BYTE_ARRAY back to BLOB at :93-94) ----
+def _bitstring(bits: str) -> bytes:
+    """DuckDB's BIT storage (Bit::ToBit): byte 0 = padding bit count, then the
+    bits most significant first, the padding bits at the top of byte 1 set"""
+    pad = (8 - len(bits) % 8) % 8
+    full = "1" * pad + bits
+    return bytes([pad]) + int(full, 2).to_bytes(len(full) // 8, "big")
+
+
+def _bits(n, rng):
+    out = ["".join("01"[int(b)] for b in rng.integers(0, 2, int(k))) for k in rng.integers(1, 70, n)]
+    out[0] = "1"
+    if n > 1:
+        out[1] = "0" * 64
+    return out
+
+
+def test_bitstring_helper_matches_duckdb_layout():
+    assert _bitstring("1") == bytes([7, 0xFF])                     # 7 padding ones, then 1
+    assert _bitstring("0") == bytes([7, 0xFE])
+    assert _bitstring("01010101") == bytes([0, 0x55])
+    assert _bitstring("101") == bytes([5, 0b11111101])
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_copy_bit_column_stored_as_blob_cpu(ext, ref, tmpfile, threads):
+    """COPY of a BIT column: the file's column is BLOB (the writer has no BIT
+    type, as the reference's FastLanes has none) holding each value's
+    bitstring bytes; the oracle decodes them."""
+    n = 9000
+    bits = _bits(n, np.random.default_rng(11))
+    dst = tmpfile("bits.fls")
+    assert ext.copy_values([("v", "BIT", bits), ("k", "BIGINT", list(range(n)))], dst, threads=threads) == n
+    rf = ref.RefFile(open(dst, "rb").read())
+    assert [rf.column(c)[1] for c in range(2)] == [21, 4]
+    got_k = np.concatenate([rf.decode(1, g) for g in range(rf.nrowgroups)]).view(np.int64)
+    rows = sorted(zip(got_k.tolist(), rf.strings_column(0)))
+    assert rows == [(i, _bitstring(bits[i])) for i in range(n)]
+
+
+@pytest.mark.gpu
+def test_read_fastlanes_bit_roundtrip_as_blob(ext, gpu, tmpfile):
+    """COPY of a BIT column -> read_fastlanes on the GPU
+    gives a BLOB column whose bytes are the BIT values' bitstrings, every row
+    (the reference reads its BYTE_ARRAY columns back as BLOB)."""
+    n = 70000
+    bits = _bits(n, np.random.default_rng(12))
+    dst = tmpfile("bits_gpu.fls")
+    assert ext.copy_values([("v", "BIT", bits), ("k", "BIGINT", list(range(n)))], dst) == n
+    names, types, rows = ext.query("read_fastlanes", dst, threads=2)
+    assert names == ["v", "k"] and types == ["BLOB", "BIGINT"]
+    rows.sort(key=lambda r: int(r[1]))
+    assert rows == [[_duck_blob(_bitstring(bits[i])), str(i)] for i in range(n)]
