@@ -18,6 +18,7 @@
 #   abenv:<workload>:<scale>:<cols>:<arms>
 #               same-buffer A/B of runtime knobs (scripts/ab_env.py; arms
 #               name=ENV=V,ENV2=V2;name2=...)
+#   fsstsq:<kernel>[:<scale>]  SQ counters of an FSST kernel on l_comment (3 PMC passes)
 #   e2e         read_fastlanes DataChunk delivery, 1 and 16 threads, phase profile
 #   launcher2   bench.py --gpus 2 rehearsal (both ranks on the one GPU)
 # Results go to gpurun_out/<mode>_<tag>.*; copy what is judged to profiles/.
@@ -74,6 +75,19 @@ for mode in "$@"; do
     step 600 $O/abenv_${TAG}_${wl}_${sc}.txt python scripts/ab_env.py --workload "$wl" --scale "$sc" --cols "$cols" \
         --arms $(echo "$arms" | tr ';' ' ') || exit $?
     grep -v amdgpu.ids $O/abenv_${TAG}_${wl}_${sc}.txt ;;
+  fsstsq:*)   # fsstsq:<kernel substring>[:<scale>]: SQ counters of an FSST kernel on l_comment, 3 PMC passes
+    IFS=: read -r _ kern sc <<< "$mode"
+    P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU"
+    P2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_WAVES"
+    P3="SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU"
+    i=0
+    for P in "$P1" "$P2" "$P3"; do
+      i=$((i+1))
+      timeout -k 10 -s KILL 120 rocprofv3 --pmc $P -d $O/fsq_${TAG}_$i -o pmc --output-format csv -- \
+          python3 scripts/fsst_prof.py --scale "${sc:-10}" > $O/fsq_${TAG}_$i.log 2>&1
+      rc=$?; echo "[$TAG] pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/fsq_${TAG}_$i.log; exit $rc; }
+    done
+    python3 scripts/pmc_summary.py "$kern" $O/fsq_${TAG}_1 $O/fsq_${TAG}_2 $O/fsq_${TAG}_3 | tee $O/fsst_sq_$TAG.txt ;;
   e2e)
     step 600 $O/e2e_phases_$TAG.txt python scripts/e2e_phases.py --scale 10 || exit $? ;;
   launcher2)
