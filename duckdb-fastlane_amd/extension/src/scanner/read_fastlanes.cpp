@@ -19,6 +19,9 @@
 #include <glob.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -49,6 +52,44 @@ namespace duckdb {
 namespace ext_fastlane {
 
 namespace {
+
+// FLS_READ_PROFILE=1: where a scan thread's time goes (summed over threads,
+// printed to stderr when the query's global state goes away): waiting for
+// the claim lock, inside fls_scan_acquire (the GPU pipeline's hand-over),
+// building deferred string_t records, filling the DataChunks by kind, and
+// returning row groups (the RowGroupPin release).
+struct ReadProfile {
+    enum Phase { kLockWait, kAcquire, kRecords, kRelease, kEmitRef, kEmitDict, kEmitNarrow, kEmitCopy, kValidity,
+                 kResidual, kScanTotal, kNumPhases };
+    std::atomic<uint64_t> ns[kNumPhases] = {};
+    std::atomic<uint64_t> rowgroups{0}, chunks{0}, rows{0};
+    static bool on() {  // read per query (InitGlobal)
+        const char *e = std::getenv("FLS_READ_PROFILE");
+        return e && std::atoi(e) != 0;
+    }
+    static uint64_t now() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void print(idx_t threads) {
+        static const char *names[kNumPhases] = {"lock wait", "fls_scan_acquire", "string_t records", "row-group release",
+                                                "emit zero-copy", "emit dictionary", "emit narrowed (widen)",
+                                                "emit copy (decimal)", "validity", "residual filters", "ReadScan total"};
+        fprintf(stderr, "read_fastlanes profile: %llu row groups, %llu chunks, %llu rows, %llu threads (seconds summed over threads)\n",
+                (unsigned long long)rowgroups.load(), (unsigned long long)chunks.load(), (unsigned long long)rows.load(),
+                (unsigned long long)threads);
+        for (int k = 0; k < kNumPhases; ++k) fprintf(stderr, "  %-24s %9.4f s\n", names[k], ns[k].load() * 1e-9);
+    }
+};
+struct PhaseTimer {
+    ReadProfile *p;
+    int k;
+    uint64_t t0;
+    PhaseTimer(ReadProfile *prof, int phase) : p(prof), k(phase), t0(prof ? ReadProfile::now() : 0) {}
+    ~PhaseTimer() {
+        if (p) p->ns[k] += ReadProfile::now() - t0;
+    }
+};
 
 // An open file on the process-wide engine connection (SharedConnection: its
 // scan pipelines and pinned buffers carry over between queries).
@@ -98,6 +139,11 @@ struct ReadGlobalState : public GlobalTableFunctionState {
     idx_t file_idx = 0;
     std::shared_ptr<OpenTable> cur;      // file being scanned (nullptr: open the next)
     idx_t MaxThreads() const override { return std::max<idx_t>(1, total_rowgroups); }
+    std::unique_ptr<ReadProfile> prof;   // FLS_READ_PROFILE
+    std::atomic<idx_t> threads{0};
+    ~ReadGlobalState() override {
+        if (prof) prof->print(threads.load());
+    }
 };
 
 // A delivered row group's pinned buffers, held by the local state while it
@@ -298,6 +344,7 @@ bool AddFilter(const TableFilter &f, uint32_t col, const LogicalType &type, uint
 unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &context, TableFunctionInitInput &input) {
     const auto &bind = input.bind_data->Cast<ReadBindData>();
     auto state = make_uniq<ReadGlobalState>();
+    if (ReadProfile::on()) state->prof.reset(new ReadProfile());
     // Narrowed delivery trades host work (adding the base back while filling
     // each vector) for PCIe bytes: it pays when the scan is link-bound, with
     // several threads to widen (lineitem_full SF10: 16 threads 4.3 -> 5.6-5.9e8
@@ -358,6 +405,7 @@ unique_ptr<GlobalTableFunctionState> ReadInitGlobal(ClientContext &context, Tabl
 unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &context, TableFunctionInitInput &,
                                                   GlobalTableFunctionState *gstate) {
     auto l = make_uniq<ReadLocalState>();
+    gstate->Cast<ReadGlobalState>().threads++;
     for (auto &r : gstate->Cast<ReadGlobalState>().residual)
         l->residual_state.push_back(TableFilterState::Initialize(context.client, *r.filter));
     return std::move(l);
@@ -366,8 +414,14 @@ unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &context, Tab
 // give back the local state's row group and claim the next one (in file and
 // row-group order over all threads); false at the end of all files
 bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &l) {
-    l.pin.reset();  // released now unless a chunk DuckDB still holds references it
+    ReadProfile *prof = g.prof.get();
+    {
+        PhaseTimer t(prof, ReadProfile::kRelease);
+        l.pin.reset();  // released now unless a chunk DuckDB still holds references it
+    }
+    const uint64_t tw = prof ? ReadProfile::now() : 0;
     std::lock_guard<std::mutex> guard(g.lock);
+    if (prof) prof->ns[ReadProfile::kLockWait] += ReadProfile::now() - tw;
     while (true) {
         if (!g.cur) {
             if (g.file_idx >= bind.files.size()) return false;
@@ -388,9 +442,14 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
             g.cur = std::move(t);
         }
-        const int rc = fls_scan_acquire(g.cur->table, &l.rg);
+        int rc;
+        {
+            PhaseTimer t(prof, ReadProfile::kAcquire);
+            rc = fls_scan_acquire(g.cur->table, &l.rg);
+        }
         if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
         if (rc == 1) {
+            if (prof) prof->rowgroups++;
             l.table = g.cur->table;
             l.pin = make_buffer<RowGroupPin>(g.cur, l.rg.rowgroup);
             l.rg_pos = 0;
@@ -405,15 +464,22 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
 // rows [rg_pos, rg_pos + n) of table column id into vec: a reference to the
 // pinned row group (zero-copy) or, for DECIMAL(w<=9), the engine's int64
 // narrowed to DuckDB's physical width
-void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector &vec, idx_t n) {
+void EmitColumn(const ReadBindData &bind, ReadLocalState &l, column_t id, Vector &vec, idx_t n,
+                ReadProfile *prof = nullptr) {
     const idx_t ob = bind.cols[id].out_bytes;
     // NULLs: the delivered rows' validity words (rg_pos is a multiple of
     // STANDARD_VECTOR_SIZE, so whole words)
     if (const uint64_t *valid = l.rg.validity ? l.rg.validity[id] : nullptr) {
+        PhaseTimer t(prof, ReadProfile::kValidity);
         auto &mask = FlatVector::Validity(vec);
         mask.Initialize(STANDARD_VECTOR_SIZE);
         memcpy(mask.GetData(), valid + l.rg_pos / 64, ValidityMask::EntryCount(n) * sizeof(validity_t));
     }
+    const bool is_dict = l.rg.dict && l.rg.dict[id];
+    const bool is_narrow = !is_dict && l.rg.narrow && l.rg.narrow[id];
+    PhaseTimer t(prof, is_dict ? ReadProfile::kEmitDict
+                       : is_narrow ? ReadProfile::kEmitNarrow
+                       : vec.GetType().PhysicalSize() == ob ? ReadProfile::kEmitRef : ReadProfile::kEmitCopy);
     if (const void *dict = l.rg.dict ? l.rg.dict[id] : nullptr) {  // dictionary codes
         const uint8_t w = l.rg.dict_width[id];
         const uint8_t *codes = (const uint8_t *)l.rg.columns[id] + l.rg_pos * w;
@@ -489,6 +555,8 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
     const auto &bind = data.bind_data->Cast<ReadBindData>();
     auto &g = data.global_state->Cast<ReadGlobalState>();
     auto &l = data.local_state->Cast<ReadLocalState>();
+    ReadProfile *prof = g.prof.get();
+    PhaseTimer total(prof, ReadProfile::kScanTotal);
     for (;;) {  // until a chunk with rows (host-side filters can empty one) or the end
         output.Reset();
         // (a filtered row group can deliver no rows)
@@ -499,6 +567,7 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
             }
             // FSST columns delivered as lengths: their string_t records, on
             // this thread after NextRowGroup's lock (fls_scan_defer_records)
+            PhaseTimer t(prof, ReadProfile::kRecords);
             if (fls_scan_build_records(l.table, &l.rg) != 0)
                 throw IOException(string("FastLanes scan failed: ") + fls_last_error());
         }
@@ -512,10 +581,11 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
                     rid[i] = (int64_t)(l.rg.first_row + (l.rg.sel ? l.rg.sel[l.rg_pos + i] : l.rg_pos + i));
                 continue;
             }
-            EmitColumn(bind, l, id, vec, n);
+            EmitColumn(bind, l, id, vec, n, prof);
         }
         idx_t approved = n;
         if (!g.residual.empty()) {
+            PhaseTimer t(prof, ReadProfile::kResidual);
             // DuckDB's FilterSelection reads the incoming selection before it
             // writes one (SelectionVector(n) leaves the buffer uninitialised):
             // start from the identity over the chunk's rows
@@ -532,6 +602,10 @@ void ReadScan(ClientContext &, TableFunctionInput &data, DataChunk &output) {
             if (approved < n) output.Slice(sel, approved);
         }
         l.rg_pos += n;
+        if (prof) {
+            prof->chunks++;
+            prof->rows += approved;
+        }
         output.SetCardinality(approved);
         if (approved > 0) return;
     }

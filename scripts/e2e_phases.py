@@ -66,6 +66,12 @@ def main():
                 n, sec = e.scan_rows("read_fastlanes", path, threads=th)
                 print(f"DataChunks {th} threads rep {rep}: {n} rows in {sec * 1e3:.1f} ms = {n / sec / 1e6:.1f} M rows/s",
                       flush=True)
+        # the phase profile of the N-thread scan (read_fastlanes.cpp ReadProfile, printed on stderr)
+        os.environ["FLS_READ_PROFILE"] = "1"
+        sys.stderr.flush()
+        n, sec = e.scan_rows("read_fastlanes", path, threads=a.threads)
+        print(f"DataChunks {a.threads} threads, profiled: {n / sec / 1e6:.1f} M rows/s", flush=True)
+        del os.environ["FLS_READ_PROFILE"]
         e.close()
     finally:
         os.unlink(path)
