@@ -674,13 +674,17 @@ __global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) voi
             }
         }
         if (enc != ENC_FFOR && enc != ENC_DELTA) {
-            // RLE: encode_rle_kernel, launched next, writes the chunk; DICT
-            // (the distinct values sorted) is encoded by the host
+            // RLE: encode_rle_kernel, launched next, writes the chunk; DICT:
+            // dict_encode_kernel (or the host, without a table)
             if (threadIdx.x == 0) *(FLS_GLOBAL uint64_t *)c.len_out = (uint64_t)enc << kEncShift;
             return;
         }
     }
     if (enc == ENC_RLE) return;  // explicit RLE chunks: encode_rle_kernel
+    if (enc == ENC_DICT) {       // explicit DICT chunks: dict_encode_kernel (or the host)
+        if (threadIdx.x == 0) *(FLS_GLOBAL uint64_t *)c.len_out = (uint64_t)ENC_DICT << kEncShift;
+        return;
+    }
     const bool delta = enc == ENC_DELTA;
     if constexpr (sizeof(S) == 8) {
         delta ? encode_chunk<64, true>(c, V, W, B, O) : encode_chunk<64, false>(c, V, W, B, O);
@@ -727,6 +731,320 @@ __global__ __launch_bounds__(256, 2) void encode_rle_kernel(const EncChunk *__re
         default: encode_rle_chunk<32>(c, V, W, B, O); break;
         }
     }
+}
+
+
+// ============================================================================
+// DICT chunks of integer columns (fls_writer.cpp enc_dict_int, byte for byte):
+// the chunk's distinct values sorted by their signed T-bit value form the
+// dictionary (T/8 bytes each, the chunk's aux area), and each value's code --
+// its position in the dictionary -- is FFOR-packed at T = 32 per vector, the
+// tail padded with the last code.  Two kernels around encode_kernel:
+//   dict_analyze_kernel: the distinct values of every ENC_DICT chunk and of
+//     every ENC_AUTO chunk whose DICT estimate the GPU makes (kEstDictGpu):
+//     first the CPU writer's 1,024-value sample rule (a chunk of more than
+//     4,096 values whose sample holds more than 512 distinct values gets no
+//     estimate), then every value into an open-addressing table in HBM
+//     (atomicCAS on the key), and the estimate d T/8 + nvec (32 + 128
+//     bitlen(d - 1)) -- est_dict's, so ENC_AUTO picks what the CPU picks;
+//   dict_encode_kernel: for chunks that came out of encode_kernel as DICT,
+//     the table's keys into LDS, a bitonic sort by signed value, each key's
+//     position written back into the table as its code, then per vector the
+//     values' codes looked up, FFOR-analysed and packed as encode_chunk does.
+// Integer work bound by the table probes (L2-resident: 1.5 MB per 65,536-row
+// chunk) and the input reads; no MFMA.
+// ============================================================================
+constexpr uint64_t kDictEmpty = ~0ull;   // an empty slot (the value ~0 itself is kept in the header)
+struct DictHeader {                      // the table's first 64 bytes
+    uint32_t count;                      // distinct values in keys[] (kDictEmpty excluded)
+    uint32_t has_empty;                  // the value ~0ull (T = 64 only) occurs
+    uint32_t empty_code;                 // its code (dict_encode_kernel)
+    uint32_t pad[13];
+};
+static_assert(sizeof(DictHeader) == 64, "DICT table header is 64 B");
+
+__device__ __forceinline__ uint64_t dict_hash(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+// value i of a chunk (zero-extended T-bit)
+__device__ __forceinline__ uint64_t load_value(const uint8_t *in, uint32_t T, uint64_t i) {
+    switch (T) {
+    case 8: return ((const FLS_GLOBAL uint8_t *)in)[i];
+    case 16: return ((const FLS_GLOBAL uint16_t *)in)[i];
+    case 32: return ((const FLS_GLOBAL uint32_t *)in)[i];
+    default: return ((const FLS_GLOBAL uint64_t *)in)[i];
+    }
+}
+// Bitonic sort of the n (a power of two) keys of K ascending, by the block.
+__device__ __forceinline__ void block_bitonic(FLS_LDS uint64_t *K, uint32_t n) {
+    for (uint32_t k = 2; k <= n; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = K[i], b = K[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? a > b : a < b) {
+                        K[i] = b;
+                        K[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+__device__ __forceinline__ uint32_t block_sum(uint32_t x, FLS_LDS uint32_t *red) {
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += red[w];
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(256) void dict_analyze_kernel(EncChunk *__restrict__ chunks) {
+    __shared__ uint64_t smp[1024];
+    __shared__ uint32_t red[4];
+    __shared__ uint32_t cnt, has_empty;
+    EncChunk &cref = chunks[blockIdx.x];
+    const EncChunk c = cref;
+    const bool auto_est = c.enc == ENC_AUTO && c.est_dict == kEstDictGpu;
+    if (!c.dict_tab || !(c.enc == ENC_DICT || auto_est)) return;
+    const uint32_t n = c.nrows, T = c.T, nvec = (n + kVectorSize - 1) / kVectorSize;
+    const uint8_t *in = (const uint8_t *)c.in;
+    FLS_LDS uint64_t *S = (FLS_LDS uint64_t *)smp;
+    if (auto_est && n > 4096) {
+        // the CPU's sample: values i n / 1024, i < 1024, more than 512 distinct = no DICT
+        for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) S[i] = load_value(in, T, (uint64_t)i * n / 1024);
+        __syncthreads();
+        block_bitonic(S, 1024);
+        uint32_t dd = 0;
+        for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) dd += (i == 0 || S[i] != S[i - 1]) ? 1u : 0u;
+        dd = block_sum(dd, (FLS_LDS uint32_t *)red);
+        if (dd > 512) {
+            if (threadIdx.x == 0) cref.est_dict = UINT64_MAX;
+            return;
+        }
+    }
+    DictHeader *hdr = (DictHeader *)c.dict_tab;
+    uint64_t *keys = (uint64_t *)(c.dict_tab + sizeof(DictHeader));
+    const uint32_t cap = enc_dict_cap(n), mask = cap - 1;
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) keys[i] = kDictEmpty;
+    if (threadIdx.x == 0) {
+        cnt = 0;
+        has_empty = 0;
+    }
+    __syncthreads();  // (also orders the block's key stores before its CAS probes)
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t x = load_value(in, T, i);
+        if (x == kDictEmpty) {
+            has_empty = 1;
+            continue;
+        }
+        uint32_t h = (uint32_t)dict_hash(x) & mask;
+        for (uint32_t probe = 0; probe < cap; ++probe) {
+            const uint64_t old = atomicCAS((unsigned long long *)(keys + h), (unsigned long long)kDictEmpty,
+                                           (unsigned long long)x);
+            if (old == kDictEmpty) {
+                atomicAdd(&cnt, 1u);
+                break;
+            }
+            if (old == x) break;
+            h = (h + 1) & mask;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        hdr->count = cnt;
+        hdr->has_empty = has_empty;
+        if (auto_est) {
+            const uint64_t d = (uint64_t)cnt + has_empty;
+            const uint64_t dm1 = d - 1 ? d - 1 : 0;
+            const uint32_t bl = dm1 ? 64u - (uint32_t)__builtin_clzll(dm1) : 0u;
+            cref.est_dict = d > 65536 ? UINT64_MAX : d * (T / 8) + (uint64_t)nvec * (32 + 128ull * bl);
+        }
+    }
+}
+
+// code of value x: its slot's code (the table holds every value of the chunk)
+__device__ __forceinline__ uint32_t dict_code(const uint64_t *keys, const uint32_t *codes, uint32_t mask,
+                                              uint32_t empty_code, uint64_t x) {
+    if (x == kDictEmpty) return empty_code;
+    uint32_t h = (uint32_t)dict_hash(x) & mask;
+    for (uint32_t probe = 0; probe <= mask && keys[h] != x; ++probe) h = (h + 1) & mask;
+    return codes[h];
+}
+
+__global__ __launch_bounds__(256) void dict_encode_kernel(const EncChunk *__restrict__ chunks) {
+    __shared__ uint64_t U[kDictGpuMax];              // the sorted distinct values (order keys)
+    __shared__ uint32_t Vall[kEncWaves * kVectorSize];
+    __shared__ uint32_t Wv[64];
+    __shared__ int64_t Bv[64];
+    __shared__ uint64_t Ov[67];
+    __shared__ uint32_t fill;
+    const EncChunk c = chunks[blockIdx.x];
+    if (!c.dict_tab || !(c.enc == ENC_DICT || c.enc == ENC_AUTO)) return;
+    const uint64_t lw = *(const FLS_GLOBAL uint64_t *)c.len_out;
+    if ((uint32_t)(lw >> kEncShift) != ENC_DICT || (lw & ((1ull << kEncShift) - 1)) != 0) return;
+    const DictHeader *hdr = (const DictHeader *)c.dict_tab;
+    uint64_t *keys = (uint64_t *)(c.dict_tab + sizeof(DictHeader));
+    const uint32_t n = c.nrows, T = c.T, nvec = (n + kVectorSize - 1) / kVectorSize;
+    const uint32_t cap = enc_dict_cap(n), mask = cap - 1;
+    uint32_t *codes = (uint32_t *)(keys + cap);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(hdr->count);
+    const uint32_t has_empty = __builtin_amdgcn_readfirstlane(hdr->has_empty);
+    const uint32_t d = cnt + has_empty;
+    if (d > kDictGpuMax || d == 0) return;  // the host encodes it (length stays 0)
+    FLS_LDS uint64_t *K = (FLS_LDS uint64_t *)U;
+    // ---- the distinct values, ordered by their signed T-bit value: the sort
+    // key is sext(x) with the sign bit flipped (unsigned order = signed order)
+    const uint64_t flip = 1ull << 63;
+    if (threadIdx.x == 0) fill = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+        const uint64_t x = keys[i];
+        if (x != kDictEmpty) K[atomicAdd(&fill, 1u)] = (uint64_t)sext_d(x, T) ^ flip;
+    }
+    __syncthreads();
+    uint32_t P = 1;
+    while (P < d) P <<= 1;
+    if (threadIdx.x == 0 && has_empty) K[cnt] = (uint64_t)sext_d(kDictEmpty, T) ^ flip;
+    for (uint32_t i = d + threadIdx.x; i < P; i += blockDim.x) K[i] = ~0ull;  // padding sorts last
+    __syncthreads();
+    block_bitonic(K, P);
+    // ---- each value's code = its position; the dictionary (put_word layout)
+    const uint64_t tm = tmask_d(T);
+    const uint64_t packed_off = (sizeof(ChunkHeader) + sizeof(VecMeta) * (uint64_t)nvec + 15) & ~15ull;
+    FLS_GLOBAL uint8_t *out = (FLS_GLOBAL uint8_t *)c.out;
+    __shared__ uint32_t empty_code_s;
+    for (uint32_t i = threadIdx.x; i < d; i += blockDim.x) {
+        const uint64_t x = (K[i] ^ flip) & tm;
+        if (x == kDictEmpty) {
+            empty_code_s = i;
+        } else {
+            uint32_t h = (uint32_t)dict_hash(x) & mask;
+            for (uint32_t probe = 0; probe < cap && keys[h] != x; ++probe) h = (h + 1) & mask;
+            codes[h] = i;
+        }
+    }
+    __syncthreads();  // codes[] written by the block before it reads them
+    const uint32_t empty_code = has_empty ? empty_code_s : 0u;
+    // ---- codes -> FFOR (T = 32) per vector, as encode_chunk<32, false>
+    const uint32_t lane = threadIdx.x & 63, w = wave_index();
+    FLS_LDS uint32_t *V = (FLS_LDS uint32_t *)Vall + w * kVectorSize;
+    FLS_LDS uint32_t *W = (FLS_LDS uint32_t *)Wv;
+    FLS_LDS int64_t *B = (FLS_LDS int64_t *)Bv;
+    FLS_LDS uint64_t *O = (FLS_LDS uint64_t *)Ov;
+    const uint8_t *in = (const uint8_t *)c.in;
+    uint32_t done = 0;
+    for (uint32_t r = 0; r < nvec; r += kEncWaves) {
+        const uint32_t v = r + w;
+        const bool act = v < nvec;
+        VecStat st{0, 0};
+        if (act) {
+            const uint32_t vn = min(kVectorSize, n - v * kVectorSize);
+            for (uint32_t j = lane; j < kVectorSize; j += 64)
+                V[j] = dict_code(keys, codes, mask, empty_code, load_value(in, T, (uint64_t)v * kVectorSize + min(j, vn - 1)));
+            wave_sync();
+            uint32_t x[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) x[k] = V[lane + 64 * k];
+            st = analyze_regs<32>(x);
+            if (lane == 0) {
+                W[v] = st.W;
+                B[v] = st.base;
+            }
+            wave_sync();
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = x[k] - (uint32_t)st.base;
+            wave_sync();
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t off = done;
+            for (uint32_t i = r; i < v; ++i) off += 128u * W[i];
+            pack_vector<32>(V, st.W, out + packed_off + off, lane);
+        }
+        for (uint32_t i = r; i < min(r + (uint32_t)kEncWaves, nvec); ++i) done += 128u * W[i];
+        wave_sync();
+    }
+    __syncthreads();
+    // ---- chunk layout (assemble_chunk): the dictionary is the aux area, padded to 16 B
+    const uint64_t meta_off = sizeof(ChunkHeader);
+    const uint64_t dict_bytes = (uint64_t)d * (T / 8);
+    const uint64_t aux_len = (dict_bytes + 15) & ~15ull;
+    if (w == 0) {
+        const uint32_t pw = lane < nvec ? 128u * W[lane] : 0u;
+        uint32_t incl = pw;
+        for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t y = __shfl_up(incl, dd, 64);
+            if (lane >= dd) incl += y;
+        }
+        const uint64_t packed_total = rl(incl, 63);
+        const uint64_t aux_off = (packed_off + packed_total + 15) & ~15ull;
+        const uint64_t total = (aux_off + aux_len + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
+        if (lane < nvec) {
+            VecMeta m;
+            m.packed_off = incl - pw;
+            m.for_base = B[lane];
+            m.aux_off = 0;
+            m.nvals = (uint16_t)min(kVectorSize, n - lane * kVectorSize);
+            m.bw = (uint8_t)W[lane];
+            m.pad = 0;
+            m.aux_count = 0;
+            const uint32_t *mw = reinterpret_cast<const uint32_t *>(&m);
+            FLS_GLOBAL uint32_t *dm = reinterpret_cast<FLS_GLOBAL uint32_t *>(out + meta_off + sizeof(VecMeta) * lane);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dm[i] = mw[i];
+        }
+        if (lane == 0) {
+            ChunkHeader h;
+            h.magic = kChunkMagic;
+            h.enc = ENC_DICT;
+            h.T = 32;
+            h.vbits = (uint8_t)T;
+            h.is_str = 0;
+            h.nvec = nvec;
+            h.nvals = n;
+            h.meta_off = meta_off;
+            h.packed_off = packed_off;
+            h.aux_off = aux_off;
+            h.aux_len = aux_len;
+            h.dict_count = d;
+            h.reserved0 = 0;
+            h.reserved1 = 0;
+            const uint32_t *hw = reinterpret_cast<const uint32_t *>(&h);
+            FLS_GLOBAL uint32_t *dh = reinterpret_cast<FLS_GLOBAL uint32_t *>(out);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dh[i] = hw[i];
+            O[64] = packed_total;
+            O[65] = aux_off;
+            O[66] = total;
+        }
+    }
+    __syncthreads();
+    const uint64_t packed_total = O[64], aux_off = O[65], total = O[66];
+    // the dictionary, byte by byte in the put_word layout (little-endian T/8 bytes)
+    for (uint32_t i = threadIdx.x; i < d; i += blockDim.x) {
+        const uint64_t x = (K[i] ^ flip) & tm;
+        FLS_GLOBAL uint8_t *dp = out + aux_off + (uint64_t)i * (T / 8);
+        for (uint32_t b = 0; b < T / 8; ++b) dp[b] = (uint8_t)(x >> (8 * b));
+    }
+    {
+        const uint64_t gaps[3][2] = {{meta_off + sizeof(VecMeta) * nvec, packed_off},
+                                     {packed_off + packed_total, aux_off},
+                                     {aux_off + dict_bytes, total}};
+        for (int g = 0; g < 3; ++g)
+            for (uint64_t b = gaps[g][0] + threadIdx.x; b < gaps[g][1]; b += blockDim.x) out[b] = 0;
+    }
+    if (threadIdx.x == 0) *(FLS_GLOBAL uint64_t *)c.len_out = total | (uint64_t)ENC_DICT << kEncShift;
 }
 
 // One lane per string.  The table is staged in LDS; a lane reads its string
@@ -797,11 +1115,19 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
     const uint64_t delta = packed_off + 128ull * T * nvec + (enc == ENC_FFOR ? 0ull : 128ull * nvec);
     // RLE: T = 16 packing, aux = 128 B of bases + up to 1,024 run values per vector
     const uint64_t rle = packed_off + 128ull * 16 * nvec + nvec * ((128ull + 1024ull * (T / 8) + 15) & ~15ull);
-    const uint64_t need = enc == ENC_RLE ? rle : enc == ENC_AUTO ? std::max(delta, rle) : delta;  // AUTO may pick any
+    // DICT: codes of at most 16 bits (65,536 distinct values) FFOR-packed at T = 32, the dictionary
+    const uint64_t dict = packed_off + 128ull * 17 * nvec + (((uint64_t)nrows * (T / 8) + 15) & ~15ull);
+    const uint64_t need = enc == ENC_RLE    ? rle
+                          : enc == ENC_AUTO ? std::max({delta, rle, dict})  // AUTO may pick any
+                          : enc == ENC_DICT ? dict
+                                            : delta;
     return (need + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
 }
 
-hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle) {
+hipError_t launch_encode(EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle,
+                         bool dict) {
+    if (dict && n_wide + n_narrow)
+        hipLaunchKernelGGL(dict_analyze_kernel, dim3(n_wide + n_narrow), dim3(256), 0, stream, d_chunks);
     if (n_wide) hipLaunchKernelGGL(encode_kernel<uint64_t>, dim3(n_wide), dim3(64 * kEncWaves), 0, stream, d_chunks, n_wide);
     if (n_narrow)
         hipLaunchKernelGGL(encode_kernel<uint32_t>, dim3(n_narrow), dim3(64 * kEncWaves), 0, stream, d_chunks + n_wide,
@@ -811,6 +1137,8 @@ hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_n
     if (rle && n_narrow)
         hipLaunchKernelGGL(encode_rle_kernel<uint32_t>, dim3(n_narrow), dim3(64 * kEncWaves), 0, stream,
                            d_chunks + n_wide, n_narrow);
+    if (dict && n_wide + n_narrow)
+        hipLaunchKernelGGL(dict_encode_kernel, dim3(n_wide + n_narrow), dim3(256), 0, stream, d_chunks);
     return hipGetLastError();
 }
 

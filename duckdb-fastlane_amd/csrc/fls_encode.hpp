@@ -13,15 +13,33 @@ struct EncChunk {
     uint64_t len_out;  // device address of a uint64: the chunk's byte length (written)
     uint64_t scratch;  // device address of enc_scratch_bytes() bytes (the DELTA chain bases)
     uint32_t nrows;    // rows of the chunk (1..65536)
-    uint8_t T, enc;    // packing width 8/16/32/64; ENC_FFOR, ENC_DELTA or ENC_AUTO
+    uint8_t T, enc;    // packing width 8/16/32/64; ENC_FFOR, ENC_DELTA, ENC_RLE, ENC_DICT or ENC_AUTO
     uint8_t pad[2];
-    uint64_t est_dict; // ENC_AUTO: the host's DICT size estimate (UINT64_MAX: DICT not worth it)
+    uint64_t est_dict; // ENC_AUTO: the DICT size estimate (UINT64_MAX: DICT not worth it;
+                       // kEstDictGpu: dict_analyze_kernel computes it, as the CPU writer's est_dict)
+    uint64_t dict_tab; // ENC_DICT / ENC_AUTO: device address of enc_dict_tab_bytes(nrows) bytes (the
+                       // chunk's distinct-value hash table), 0 = the host encodes DICT chunks
+    uint64_t reserved;
 };
-// *len_out = chunk bytes | encoding << kEncShift.  ENC_AUTO chunks that choose
-// RLE or DICT are not encoded on the GPU: length 0, the encoding in the top
-// byte, and the host encodes them (fls_writer.cpp GpuEncoder::complete).
+// *len_out = chunk bytes | encoding << kEncShift.  Chunks the GPU does not
+// write (ENC_AUTO picking RLE is written by encode_rle_kernel; a DICT chunk
+// without a table or with more distinct values than dict_encode_kernel sorts
+// in LDS) come back with length 0, the encoding in the top byte, and the host
+// encodes them from the staged values (fls_writer.cpp GpuEncoder::complete).
 constexpr int kEncShift = 56;
-static_assert(sizeof(EncChunk) == 48, "EncChunk is 48 B");
+constexpr uint64_t kEstDictGpu = UINT64_MAX - 1;
+static_assert(sizeof(EncChunk) == 64, "EncChunk is 64 B");
+
+// The DICT hash table of a chunk of nrows values: a 64-byte header (distinct
+// count, ...), keys u64[cap], codes u32[cap], cap = the power of two >= 2 nrows.
+__host__ __device__ inline uint32_t enc_dict_cap(uint32_t nrows) {
+    uint32_t cap = 64;
+    while (cap < 2u * nrows) cap <<= 1;
+    return cap;
+}
+inline uint64_t enc_dict_tab_bytes(uint32_t nrows) { return 64ull + 12ull * enc_dict_cap(nrows); }
+// Distinct values dict_encode_kernel sorts in LDS (more: the host encodes the chunk).
+constexpr uint32_t kDictGpuMax = 16384;
 
 // Scratch bytes per chunk: 64 x 128 B of DELTA chain bases (their place in
 // the chunk follows the packed area, known only once every width is).
@@ -33,7 +51,10 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // Launch over chunks [0, n_wide) of T = 64 and then [n_wide, n_wide + n_narrow)
 // of T <= 32 (one kernel each: u64 or u32 registers and LDS).
 // rle: some chunk is ENC_RLE or ENC_AUTO (encode_rle_kernel follows).
-hipError_t launch_encode(const EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle);
+// dict: some chunk is ENC_DICT or ENC_AUTO with a dict_tab (dict_analyze_kernel
+// runs first, dict_encode_kernel after).  d_chunks is written (est_dict).
+hipError_t launch_encode(EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle,
+                         bool dict = false);
 
 // GPU FSST compression (writer side of ENC_FSST chunks; fls_writer.cpp
 // enc_fsst).  The host builds the chunk's symbol table from its sample

@@ -1487,10 +1487,14 @@ struct GpuEncoder {
         uint64_t in_off, out_off;
         uint32_t nrows;
         uint8_t T, enc;         // enc may be ENC_AUTO: the kernel chooses (fls_encode.hip choose_encoding)
-        uint64_t est_dict = UINT64_MAX;  // ENC_AUTO: the DICT estimate (set by the staging pass)
+        uint64_t est_dict = UINT64_MAX;  // ENC_AUTO: the DICT estimate (set by the staging pass, or kEstDictGpu)
+        uint64_t dict_off = UINT64_MAX;  // ENC_DICT / ENC_AUTO: its DICT table in d_dict (UINT64_MAX: none)
     };
     struct Set {
         uint8_t *h_stage = nullptr, *d_in = nullptr, *d_out = nullptr, *d_scratch = nullptr, *h_out = nullptr;
+        uint8_t *d_dict = nullptr;    // DICT hash tables of the set's ENC_DICT / ENC_AUTO jobs
+        size_t dict_cap = 0;
+        uint64_t dict_used = 0;
         uint64_t *h_lens = nullptr, *d_lens = nullptr;
         EncChunk *h_desc = nullptr, *d_desc = nullptr;
         size_t in_cap = 0, out_cap = 0, job_cap = 0;
@@ -1515,6 +1519,7 @@ struct GpuEncoder {
         hipFree(b.d_lens);
         hipFree(b.d_desc);
         hipFree(b.d_scratch);
+        hipFree(b.d_dict);
         if (b.done) hipEventDestroy(b.done);
         b = Set();
     }
@@ -1537,10 +1542,17 @@ struct GpuEncoder {
         if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-    // Room for a full batch of row groups needing in_rg / out_rg / nj each
-    // (the set is empty and idle here).
-    int ensure(Set &b, uint64_t in_rg, uint64_t out_rg, size_t nj) {
+    // Room for a full batch of row groups needing in_rg / out_rg / nj /
+    // dict_rg each (the set is empty and idle here).
+    int ensure(Set &b, uint64_t in_rg, uint64_t out_rg, size_t nj, uint64_t dict_rg) {
         if (!b.done) WHIP(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+        if (kBatch * dict_rg > b.dict_cap) {
+            hipFree(b.d_dict);
+            b.d_dict = nullptr;
+            b.dict_cap = 0;
+            WHIP(hipMalloc((void **)&b.d_dict, kBatch * dict_rg));
+            b.dict_cap = kBatch * dict_rg;
+        }
         if (kBatch * in_rg > b.in_cap) {
             hipHostFree(b.h_stage);
             hipFree(b.d_in);
@@ -1584,23 +1596,31 @@ struct GpuEncoder {
     }
 
     // Pinned staging / slot bytes columns cols of an nrows row group need.
+    // DICT chunks on the GPU (FLS_WRITER_DICT_GPU=0: DICT estimates and DICT
+    // chunks on the host, the round-3 path)
+    static bool dict_gpu() {
+        const char *e = getenv("FLS_WRITER_DICT_GPU");
+        return !(e && atoi(e) == 0);
+    }
+    static bool dict_job(uint8_t enc) { return (enc == ENC_DICT || enc == ENC_AUTO) && dict_gpu(); }
     static void need(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, uint32_t nrows,
-                     uint64_t &in_rg, uint64_t &out_rg) {
-        in_rg = out_rg = 0;
+                     uint64_t &in_rg, uint64_t &out_rg, uint64_t &dict_rg) {
+        in_rg = out_rg = dict_rg = 0;
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
             in_rg += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
             out_rg += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
+            if (dict_job(specs[c].enc)) dict_rg += (enc_dict_tab_bytes(nrows) + 255) & ~255ull;
         }
     }
     // Whether add() would take this row group into the current set without
     // first submitting it (submitting needs every row group of the set staged).
     bool has_room(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, uint32_t nrows) const {
-        uint64_t in_rg, out_rg;
-        need(specs, cols, nrows, in_rg, out_rg);
+        uint64_t in_rg, out_rg, dict_rg;
+        need(specs, cols, nrows, in_rg, out_rg, dict_rg);
         const Set &b = sets[cur];
         return !b.in_flight && b.in_used + in_rg <= b.in_cap && b.out_used + out_rg <= b.out_cap &&
-               b.jobs.size() + cols.size() <= b.job_cap;
+               b.jobs.size() + cols.size() <= b.job_cap && b.dict_used + dict_rg <= b.dict_cap;
     }
 
     // Reserve the current set's room for columns cols of row group rg (nrows
@@ -1613,27 +1633,33 @@ struct GpuEncoder {
         if (!stream) WHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         // capacity for a full batch of row groups like this one (the first
         // row group is the largest: only the last one may be short)
-        uint64_t in_rg, out_rg;
-        need(specs, cols, nrows, in_rg, out_rg);
+        uint64_t in_rg, out_rg, dict_rg;
+        need(specs, cols, nrows, in_rg, out_rg, dict_rg);
         if (sets[cur].in_flight) {
             const int rc = complete(sets[cur], rgs, nthreads);
             if (rc) return rc;
         }
         Set *b = &sets[cur];
-        if (b->in_used + in_rg > b->in_cap || b->out_used + out_rg > b->out_cap || b->jobs.size() + cols.size() > b->job_cap) {
+        if (b->in_used + in_rg > b->in_cap || b->out_used + out_rg > b->out_cap ||
+            b->jobs.size() + cols.size() > b->job_cap || b->dict_used + dict_rg > b->dict_cap) {
             if (!b->jobs.empty()) {
                 int rc = submit();
                 if (rc) return rc;
                 b = &sets[cur];
                 if (b->in_flight && (rc = complete(*b, rgs, nthreads))) return rc;
             }
-            const int rc = ensure(*b, in_rg, out_rg, cols.size());
+            const int rc = ensure(*b, in_rg, out_rg, cols.size(), dict_rg);
             if (rc) return rc;
         }
         const size_t j0 = b->jobs.size();
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
-            b->jobs.push_back(Job{rg, c, b->in_used, b->out_used, nrows, (uint8_t)T, specs[c].enc});
+            Job jb{rg, c, b->in_used, b->out_used, nrows, (uint8_t)T, specs[c].enc};
+            if (dict_job(specs[c].enc)) {
+                jb.dict_off = b->dict_used;
+                b->dict_used += (enc_dict_tab_bytes(nrows) + 255) & ~255ull;
+            }
+            b->jobs.push_back(jb);
             stage[c] = b->h_stage + b->in_used;
             b->in_used += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
             b->out_used += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
@@ -1661,6 +1687,8 @@ struct GpuEncoder {
             c.enc = jb.enc;
             c.pad[0] = c.pad[1] = 0;
             c.est_dict = jb.est_dict;
+            c.dict_tab = jb.dict_off == UINT64_MAX ? 0 : (uint64_t)(uintptr_t)(b.d_dict + jb.dict_off);
+            c.reserved = 0;
         }
         // T = 64 chunks first (launch_encode); each carries its own addresses
         EncChunk *first = b.h_desc, *last = b.h_desc + b.jobs.size();
@@ -1668,9 +1696,12 @@ struct GpuEncoder {
             (uint32_t)(std::stable_partition(first, last, [](const EncChunk &c) { return c.T == 64; }) - first);
         WHIP(hipMemcpyAsync(b.d_in, b.h_stage, b.in_used, hipMemcpyHostToDevice, stream));
         WHIP(hipMemcpyAsync(b.d_desc, b.h_desc, b.jobs.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
-        bool rle = false;
-        for (const Job &jb : b.jobs) rle |= jb.enc == ENC_RLE || jb.enc == ENC_AUTO;
-        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream, rle));
+        bool rle = false, dict = false;
+        for (const Job &jb : b.jobs) {
+            rle |= jb.enc == ENC_RLE || jb.enc == ENC_AUTO;
+            dict |= jb.dict_off != UINT64_MAX;
+        }
+        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream, rle, dict));
         WHIP(hipMemcpyAsync(b.h_lens, b.d_lens, b.jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         // the slots come back in one pinned copy (slots are sized for W = T,
         // so this moves more than the chunks hold, but one large copy beats
@@ -1714,6 +1745,7 @@ struct GpuEncoder {
         for (auto &t : th) t.join();
         b.jobs.clear();
         b.in_used = b.out_used = 0;
+        b.dict_used = 0;
         b.batched = 0;
         b.in_flight = false;
         if (g_prof.on) {
@@ -1937,7 +1969,8 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
             if (!type_is_string(cs.type) && !type_is_float(cs.type) &&
-                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO))
+                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO ||
+                 (cs.enc == ENC_DICT && GpuEncoder::dict_gpu())))
                 gcols.push_back(c);
         }
     std::vector<uint8_t> on_gpu(ncols, 0);
@@ -1990,9 +2023,13 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             if (nulls) fill_nulls(p.stage[c], vbytes, nrows, vw);
             p.rg.zones[c] = zone_of_typed(cs.type, p.stage[c], nrows);
             null_flags(p.rg.zones[c]);
-            if (cs.enc == ENC_AUTO) {  // the one ENC_AUTO estimate the GPU does not make
-                const size_t d = est_dict_typed(type_value_bits(cs.type), p.stage[c], nrows);
-                *p.est_dict[c] = d == SIZE_MAX ? UINT64_MAX : (uint64_t)d;
+            if (cs.enc == ENC_AUTO) {
+                if (GpuEncoder::dict_gpu()) {  // dict_analyze_kernel makes the DICT estimate
+                    *p.est_dict[c] = kEstDictGpu;
+                } else {                       // the host's (FLS_WRITER_DICT_GPU=0)
+                    const size_t d = est_dict_typed(type_value_bits(cs.type), p.stage[c], nrows);
+                    *p.est_dict[c] = d == SIZE_MAX ? UINT64_MAX : (uint64_t)d;
+                }
             }
             return;
         }

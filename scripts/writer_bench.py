@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--workload", default="lineitem", help="lineitem | lineitem_full (l_comment FSST)")
     ap.add_argument("--gpu", action="store_true", help="also the writer with fls_writer_set_device(0)")
     ap.add_argument("--batch", type=int, default=8, help="row groups per fls_writer_add_rowgroups call (arm)")
+    ap.add_argument("--arms", default="", help="COPY leg: interleaved env arms 'name:VAR=v,VAR2=v;name2:...'")
+    ap.add_argument("--reps", type=int, default=1, help="COPY leg: rounds over the arms")
     a = ap.parse_args()
     import pkgload
     fl = pkgload.load()
@@ -138,20 +140,46 @@ def main():
 
 
 def copy_leg(fl, a, img):
-    if True:
-        from ext_harness import Ext
-        e = Ext()
-        with tempfile.TemporaryDirectory() as d:
-            src, dst = os.path.join(d, "src.fls"), os.path.join(d, "dst.fls")
-            img.write(src)
-            for th in sorted({1, a.threads}):
-                t0 = time.perf_counter()
-                rows = e.copy("read_fastlanes", src, dst, fmt="fls", threads=th)
-                dt = time.perf_counter() - t0
-                what = "ordered, one sink" if th == 1 else f"unordered, {th} sink threads"
-                print(f"COPY (SELECT * FROM read_fastlanes) TO (FORMAT fls), {what}: {rows} rows in {dt:.2f} s = "
-                      f"{rows / dt / 1e6:.2f} M rows/s", flush=True)
-        e.close()
+    """COPY through the executor harness at 1 (ordered) and N (unordered)
+    sink threads; with --arms, the arms' environments interleaved round by
+    round on the same source file (same-box A/B), medians reported."""
+    import statistics
+    from ext_harness import Ext
+    arms = [("default", {})]
+    if a.arms:
+        arms = []
+        for spec in a.arms.split(";"):
+            name, _, kv = spec.partition(":")
+            arms.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+    e = Ext()
+    times = {}
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "src.fls"), os.path.join(d, "dst.fls")
+        img.write(src)
+        for _ in range(max(1, a.reps)):
+            for name, env in arms:
+                saved = {k: os.environ.get(k) for k in env}
+                os.environ.update(env)
+                try:
+                    for th in sorted({1, a.threads}):
+                        t0 = time.perf_counter()
+                        rows = e.copy("read_fastlanes", src, dst, fmt="fls", threads=th)
+                        dt = time.perf_counter() - t0
+                        times.setdefault((name, th), []).append(dt)
+                        what = "ordered, one sink" if th == 1 else f"unordered, {th} sink threads"
+                        print(f"COPY (SELECT * FROM read_fastlanes) TO (FORMAT fls), {what} [{name}]: {rows} rows "
+                              f"in {dt:.2f} s = {rows / dt / 1e6:.2f} M rows/s", flush=True)
+                finally:
+                    for k, v in saved.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
+    e.close()
+    if len(arms) > 1 or a.reps > 1:
+        for (name, th), v in sorted(times.items()):
+            print(f"median [{name}] {th} sink thread(s): {rows / statistics.median(v) / 1e6:.2f} M rows/s "
+                  f"over {len(v)} runs", flush=True)
 
 
 if __name__ == "__main__":

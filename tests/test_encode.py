@@ -340,3 +340,78 @@ def test_gpu_writer_fsst_failure_marks_writer_failed(fl, gpu, monkeypatch):
         assert b"failed earlier" in fl.lib.fls_last_error()
     finally:
         fl.lib.fls_writer_free(w)
+
+
+# ---- DICT chunks of integer columns on the GPU (dict_analyze_kernel /
+# dict_encode_kernel; SURVEY.md 8(f) row 1 "dict analysis";
+# reference writer stub src/writer/write_fastlane_stream.cpp:65-107,294-314) ----
+def _dict_columns(fl, n, rng):
+    """Explicit ENC_DICT and DICT-choosing ENC_AUTO columns of every integer
+    type: a few distinct values over the whole range (the type's min and max,
+    0, and the all-ones value -- for 64-bit types the GPU table's empty marker,
+    kept beside the table), a single value, and, for wide types, more distinct
+    values than dict_encode_kernel sorts in LDS (kDictGpuMax = 16,384: those
+    chunks go back to the host, same bytes)."""
+    cols = []
+    for tn in INT_TYPES:
+        ty = getattr(fl, tn)
+        dt = np.dtype(fl.NP_DTYPE[ty])
+        info = np.iinfo(dt)
+        pool = rng.integers(info.min, info.max, 40, dtype=dt, endpoint=True)
+        pool[:4] = [info.min, info.max, 0, np.array(-1).astype(dt) if info.min < 0 else info.max]
+        few = pool[rng.integers(0, 40, n)]
+        one = np.full(n, pool[7], dtype=dt)
+        cols += [(f"{tn}_dict_few", ty, few, fl.ENC_DICT), (f"{tn}_dict_one", ty, one, fl.ENC_DICT),
+                 (f"{tn}_auto_few", ty, few[::-1].copy(), fl.ENC_AUTO)]
+        if dt.itemsize >= 4:
+            wide = rng.integers(info.min, info.max, 20000, dtype=dt, endpoint=True)
+            cols += [(f"{tn}_dict_many", ty, wide[rng.integers(0, 20000, n)], fl.ENC_DICT)]
+    return cols
+
+
+def test_dict_columns_are_dict_on_cpu(fl):
+    cols = _dict_columns(fl, 20000, np.random.default_rng(3))
+    encs = _chunk_encodings(fl.write_image(cols, rowgroup=4096).tobytes())
+    assert set(encs) == {fl.ENC_DICT}, encs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (1024 * 3 + 5, 1024), (1, 65536)])
+def test_gpu_writer_dict_bytes_identical(fl, ref, gpu, monkeypatch, n, rowgroup):
+    """DICT chunks of every integer type encoded on the GPU -- the distinct
+    values hashed and sorted by signed value, the codes FFOR-packed -- and
+    ENC_AUTO's DICT estimate made on the GPU (the CPU writer's sample rule and
+    size estimate): the file is the CPU writer's, byte for byte, decodes to
+    the input under the oracle, and so is the round-3 path (host estimate and
+    host DICT encoding, FLS_WRITER_DICT_GPU=0)."""
+    cols = _dict_columns(fl, n, np.random.default_rng(n + 3))
+    cpu_img = fl.write_image(cols, rowgroup=rowgroup)
+    cpu = cpu_img.tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0, threads=8).tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+    rf = ref.RefFile(cpu_img)
+    for c, (name, ty, vals, _) in enumerate(cols):
+        got = np.concatenate([rf.decode(c, r) for r in range(rf.nrowgroups)])
+        assert np.array_equal(got.view(vals.dtype), vals), name
+    monkeypatch.setenv("FLS_WRITER_DICT_GPU", "0")
+    assert fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes() == cpu
+
+
+@pytest.mark.gpu
+def test_gpu_writer_auto_dict_estimate_matches_host(fl, gpu, monkeypatch):
+    """ENC_AUTO on the GPU without the host's sample: chunks near the DICT
+    boundaries (sample of 1,024 with ~512 distinct values, distinct counts
+    around the FFOR / DICT break-even) choose exactly what the CPU writer
+    chooses."""
+    rng = np.random.default_rng(77)
+    n = 65536 * 3
+    cols = []
+    for k in (400, 500, 512, 520, 600, 3000, 9000, 30000):
+        pool = rng.integers(-2**62, 2**62, k)
+        cols.append((f"i64_{k}", fl.INT64, pool[rng.integers(0, k, n)], fl.ENC_AUTO))
+        pool32 = rng.integers(-2**30, 2**30, k)
+        cols.append((f"i32_{k}", fl.INT32, pool32[rng.integers(0, k, n)].astype(np.int32), fl.ENC_AUTO))
+    cpu = fl.write_image(cols).tobytes()
+    assert fl.ENC_DICT in _chunk_encodings(cpu) and fl.ENC_FFOR in _chunk_encodings(cpu)
+    assert fl.write_image(cols, device=0, threads=8).tobytes() == cpu
