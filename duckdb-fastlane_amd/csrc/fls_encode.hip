@@ -1047,6 +1047,100 @@ __global__ __launch_bounds__(256) void dict_encode_kernel(const EncChunk *__rest
     if (threadIdx.x == 0) *(FLS_GLOBAL uint64_t *)c.len_out = total | (uint64_t)ENC_DICT << kEncShift;
 }
 
+
+// ---- VARCHAR / BLOB dictionaries (build_str_dict's order: first appearance) ----
+// Rows are hashed into an open-addressing table whose slot holds the row that
+// claimed it (atomicCAS), the smallest row holding its string (atomicMin: the
+// first appearance) and, once sorted, its code; a probe compares the candidate
+// row's bytes with the claiming row's.  The distinct strings, ordered by first
+// row (a bitonic sort in LDS), number the codes.
+__device__ __forceinline__ uint64_t str_hash_d(const uint8_t *p, uint32_t n) {
+    uint64_t h = 0xcbf29ce484222325ull ^ n;
+    for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+    return dict_hash(h);
+}
+__device__ __forceinline__ bool str_eq_d(const uint8_t *bytes, const uint32_t *offs, uint32_t a, uint32_t b) {
+    const uint32_t a0 = offs[a], la = offs[a + 1] - a0, b0 = offs[b], lb = offs[b + 1] - b0;
+    if (la != lb) return false;
+    for (uint32_t i = 0; i < la; ++i)
+        if (bytes[a0 + i] != bytes[b0 + i]) return false;
+    return true;
+}
+constexpr uint32_t kStrEmpty = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(1024) void str_dict_kernel(const uint8_t *__restrict__ bytes, const uint32_t *__restrict__ offs,
+                                                        uint32_t n, uint32_t limit, uint32_t *__restrict__ slots,
+                                                        uint32_t *__restrict__ row_slot, uint32_t *__restrict__ codes,
+                                                        uint32_t *__restrict__ entries, StrDictInfo *__restrict__ info) {
+    __shared__ uint64_t K[kDictGpuMax];
+    __shared__ uint32_t cnt, overflow, fill;
+    __shared__ unsigned long long ebytes;
+    const uint32_t cap = enc_dict_cap(n), mask = cap - 1;
+    uint32_t *srow = slots, *sfirst = slots + cap, *scode = slots + 2 * cap;
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+        srow[i] = kStrEmpty;
+        sfirst[i] = kStrEmpty;
+    }
+    if (threadIdx.x == 0) {
+        cnt = 0;
+        overflow = 0;
+        fill = 0;
+        ebytes = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        if (*(volatile uint32_t *)&overflow) break;
+        uint32_t s = (uint32_t)str_hash_d(bytes + offs[i], offs[i + 1] - offs[i]) & mask;
+        for (uint32_t probe = 0; probe < cap; ++probe) {
+            const uint32_t r = atomicCAS(srow + s, kStrEmpty, i);
+            if (r == kStrEmpty) {
+                if (atomicAdd(&cnt, 1u) >= limit) overflow = 1;
+                break;
+            }
+            if (str_eq_d(bytes, offs, r, i)) break;
+            s = (s + 1) & mask;
+        }
+        atomicMin(sfirst + s, i);
+        row_slot[i] = s;
+    }
+    __syncthreads();
+    const uint32_t d = cnt;
+    if (overflow || d > kDictGpuMax) {
+        if (threadIdx.x == 0) {
+            info->count = d;
+            info->overflow = overflow;
+            info->big = !overflow;
+            info->entry_bytes = 0;
+        }
+        return;
+    }
+    // the distinct strings as (first row << 32 | slot), sorted by first row
+    for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) {
+        const uint32_t r = srow[s];
+        if (r == kStrEmpty) continue;
+        K[atomicAdd(&fill, 1u)] = (uint64_t)sfirst[s] << 32 | s;
+        atomicAdd(&ebytes, (unsigned long long)(offs[r + 1] - offs[r]));
+    }
+    uint32_t P = 1;
+    while (P < d) P <<= 1;
+    __syncthreads();
+    for (uint32_t i = d + threadIdx.x; i < P; i += blockDim.x) K[i] = ~0ull;
+    __syncthreads();
+    block_bitonic((FLS_LDS uint64_t *)K, P);
+    for (uint32_t k = threadIdx.x; k < d; k += blockDim.x) {
+        scode[(uint32_t)K[k]] = k;
+        entries[k] = (uint32_t)(K[k] >> 32);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) codes[i] = scode[row_slot[i]];
+    if (threadIdx.x == 0) {
+        info->count = d;
+        info->overflow = 0;
+        info->big = 0;
+        info->entry_bytes = ebytes;
+    }
+}
+
 // One lane per string.  The table is staged in LDS; a lane reads its string
 // 8 bytes at a time from two aligned qwords (the L1 serves the overlap of
 // consecutive steps) and writes its codes byte by byte into its own region.
@@ -1106,6 +1200,15 @@ hipError_t launch_fsst_compress(const uint8_t *d_bytes, const uint32_t *d_offs, 
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(fsst_compress_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_bytes, d_offs, n, d_tab,
                        d_codes, d_clen);
+    return hipGetLastError();
+}
+
+hipError_t launch_str_dict(const uint8_t *d_bytes, const uint32_t *d_offs, uint32_t n, uint32_t limit,
+                           uint32_t *d_slots, uint32_t *d_row_slot, uint32_t *d_codes, uint32_t *d_entries,
+                           StrDictInfo *d_info, hipStream_t stream) {
+    if (n == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(str_dict_kernel, dim3(1), dim3(1024), 0, stream, d_bytes, d_offs, n, limit, d_slots, d_row_slot,
+                       d_codes, d_entries, d_info);
     return hipGetLastError();
 }
 

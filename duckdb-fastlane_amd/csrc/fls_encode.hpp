@@ -81,4 +81,22 @@ __host__ __device__ inline uint32_t fsst_cbucket(uint32_t two_bytes) { return (t
 hipError_t launch_fsst_compress(const uint8_t *d_bytes, const uint32_t *d_offs, uint32_t n, const FsstCTable *d_tab,
                                 uint8_t *d_codes, uint32_t *d_clen, hipStream_t stream);
 
+// GPU dictionary of a VARCHAR / BLOB chunk (fls_writer.cpp build_str_dict:
+// the distinct strings in order of first appearance, each row's code): one
+// block per chunk.  limit: more distinct strings than this (ENC_AUTO: n / 8)
+// stops the build (info->overflow); more than kDictGpuMax leaves it to the
+// host (info->big).  Tables in device memory: slots u32[3 cap] (cap =
+// enc_dict_cap(n)), row_slot u32[n]; outputs codes u32[n], entries u32[n]
+// (the first row of each distinct string, in code order).
+struct StrDictInfo {
+    uint32_t count;       // distinct strings
+    uint32_t overflow;    // more than limit
+    uint32_t big;         // more than kDictGpuMax (the host builds it)
+    uint32_t pad;
+    uint64_t entry_bytes; // sum of the distinct strings' lengths
+};
+hipError_t launch_str_dict(const uint8_t *d_bytes, const uint32_t *d_offs, uint32_t n, uint32_t limit,
+                           uint32_t *d_slots, uint32_t *d_row_slot, uint32_t *d_codes, uint32_t *d_entries,
+                           StrDictInfo *d_info, hipStream_t stream);
+
 }  // namespace fls

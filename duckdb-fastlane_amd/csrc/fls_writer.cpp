@@ -656,15 +656,36 @@ void fsst_segments(const FsstTable &st, const std::vector<uint8_t> &comp, uint8_
 // greedy longest match as FsstTable::compress, so the same code bytes) and
 // the vectors are assembled here as for the host compressor.  One context per
 // concurrently encoding worker (its own stream and buffers), from a free list.
+// The same context builds VARCHAR / BLOB dictionaries on the GPU (run_dict,
+// launch_str_dict: build_str_dict's first-appearance order and codes).
 struct FsstGpuCtx {
     hipStream_t stream = nullptr;
     uint8_t *h_in = nullptr, *d_in = nullptr, *h_codes = nullptr, *d_codes = nullptr;
     uint32_t *h_offs = nullptr, *d_offs = nullptr, *h_clen = nullptr, *d_clen = nullptr;
     FsstCTable *h_tab = nullptr, *d_tab = nullptr;
     size_t in_cap = 0, n_cap = 0;
+    // string dictionaries: slots u32[3 cap], row slots, codes and entries u32[n]
+    uint32_t *d_slots = nullptr, *d_rows = nullptr, *d_dcodes = nullptr, *d_entries = nullptr;
+    uint32_t *h_dcodes = nullptr, *h_entries = nullptr;
+    StrDictInfo *d_info = nullptr, *h_info = nullptr;
+    size_t dict_n_cap = 0;
 
+    void release_dict() {
+        hipFree(d_slots);
+        hipFree(d_rows);
+        hipFree(d_dcodes);
+        hipFree(d_entries);
+        hipFree(d_info);
+        hipHostFree(h_dcodes);
+        hipHostFree(h_entries);
+        hipHostFree(h_info);
+        d_slots = d_rows = d_dcodes = d_entries = h_dcodes = h_entries = nullptr;
+        d_info = h_info = nullptr;
+        dict_n_cap = 0;
+    }
     void release() {
         if (stream) hipStreamSynchronize(stream);
+        release_dict();
         hipHostFree(h_in);
         hipHostFree(h_codes);
         hipHostFree(h_offs);
@@ -683,12 +704,9 @@ struct FsstGpuCtx {
         const hipError_t e_ = (expr);                                                               \
         if (e_ != hipSuccess) return fail(FLS_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
-    // compress strings [offs[0], offs[n]) of bytes with table st: string i's
-    // codes at h_codes + 2 * (offs[i] - offs[0]), their count h_clen[i]
-    int run(int dev, const FsstTable &st, const uint32_t *offs, const char *bytes, uint32_t n) {
-        // test hook: a failed device compression (the writer's error path)
-        if (const char *f = getenv("FLS_TEST_FAIL_FSST_GPU"); f && atoi(f) != 0)
-            return fail(FLS_ERR_DEVICE, "injected GPU FSST compression failure");
+    // Strings [offs[0], offs[n]) of bytes into d_in (8-aligned, 16 zero bytes
+    // after) and their offsets from 0 into d_offs, on this context's stream.
+    int upload(int dev, const uint32_t *offs, const char *bytes, uint32_t n) {
         FHIP(hipSetDevice(dev));
         if (!stream) FHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         const size_t nb = offs[n] - offs[0];
@@ -726,6 +744,66 @@ struct FsstGpuCtx {
         memcpy(h_in, bytes + offs[0], nb);
         memset(h_in + nb, 0, 16);
         for (uint32_t i = 0; i <= n; ++i) h_offs[i] = offs[i] - offs[0];
+        FHIP(hipMemcpyAsync(d_in, h_in, nb + 16, hipMemcpyHostToDevice, stream));
+        FHIP(hipMemcpyAsync(d_offs, h_offs, 4ull * (n + 1), hipMemcpyHostToDevice, stream));
+        return 0;
+    }
+
+    // The dictionary of the n strings (build_str_dict on the GPU): d.entries
+    // in first-appearance order and d.codes; few = false once more than
+    // `limit` distinct strings occur.  A chunk with more than kDictGpuMax
+    // distinct strings is built on the host (same result).
+    int run_dict(int dev, const uint32_t *offs, const char *bytes, uint32_t n, uint32_t limit, StrDict &d, bool &few) {
+        if (const char *f = getenv("FLS_TEST_FAIL_FSST_GPU"); f && atoi(f) != 0)
+            return fail(FLS_ERR_DEVICE, "injected GPU string dictionary failure");
+        if (int rc = upload(dev, offs, bytes, n)) return rc;
+        if (n > dict_n_cap) {
+            release_dict();
+            FHIP(hipMalloc((void **)&d_slots, 12ull * enc_dict_cap(n)));
+            FHIP(hipMalloc((void **)&d_rows, 4ull * n));
+            FHIP(hipMalloc((void **)&d_dcodes, 4ull * n));
+            FHIP(hipMalloc((void **)&d_entries, 4ull * n));
+            FHIP(hipMalloc((void **)&d_info, sizeof(StrDictInfo)));
+            FHIP(hipHostMalloc((void **)&h_dcodes, 4ull * n, 0));
+            FHIP(hipHostMalloc((void **)&h_entries, 4ull * n, 0));
+            FHIP(hipHostMalloc((void **)&h_info, sizeof(StrDictInfo), 0));
+            dict_n_cap = n;
+        }
+        FHIP(launch_str_dict(d_in, d_offs, n, limit, d_slots, d_rows, d_dcodes, d_entries, d_info, stream));
+        FHIP(hipMemcpyAsync(h_info, d_info, sizeof(StrDictInfo), hipMemcpyDeviceToHost, stream));
+        FHIP(hipStreamSynchronize(stream));
+        const StrDictInfo info = *h_info;
+        if (info.overflow) {
+            few = false;
+            return 0;
+        }
+        if (info.big) {  // more distinct strings than the GPU sorts: the host's build
+            few = build_str_dict(offs, bytes, n, limit, d);
+            return 0;
+        }
+        FHIP(hipMemcpyAsync(h_dcodes, d_dcodes, 4ull * n, hipMemcpyDeviceToHost, stream));
+        FHIP(hipMemcpyAsync(h_entries, d_entries, 4ull * info.count, hipMemcpyDeviceToHost, stream));
+        FHIP(hipStreamSynchronize(stream));
+        d.entries.resize(info.count);
+        for (uint32_t k = 0; k < info.count; ++k) {
+            const uint32_t r = h_entries[k];
+            if (r >= n) return fail(FLS_ERR_DEVICE, "GPU string dictionary: entry %u names row %u of %u", k, r, n);
+            d.entries[k] = std::string_view(bytes + offs[r], offs[r + 1] - offs[r]);
+        }
+        d.codes.assign(h_dcodes, h_dcodes + n);
+        d.entry_bytes = info.entry_bytes;
+        few = true;
+        return 0;
+    }
+
+    // compress strings [offs[0], offs[n]) of bytes with table st: string i's
+    // codes at h_codes + 2 * (offs[i] - offs[0]), their count h_clen[i]
+    int run(int dev, const FsstTable &st, const uint32_t *offs, const char *bytes, uint32_t n) {
+        // test hook: a failed device compression (the writer's error path)
+        if (const char *f = getenv("FLS_TEST_FAIL_FSST_GPU"); f && atoi(f) != 0)
+            return fail(FLS_ERR_DEVICE, "injected GPU FSST compression failure");
+        if (int rc = upload(dev, offs, bytes, n)) return rc;
+        const size_t nb = offs[n] - offs[0];
         // the table: codes of length >= 2 bucketed by their first two bytes in
         // the order the host's two-byte index lists them (by_first order)
         FsstCTable &t = *h_tab;
@@ -742,8 +820,6 @@ struct FsstGpuCtx {
         for (int b = 0; b < 256; ++b)
             for (uint8_t c : st.by_first[b])
                 if (st.len[c] >= 2) t.codes[cnt[fsst_cbucket((uint32_t)(st.sym[c] & 0xFFFF))]++] = c;
-        FHIP(hipMemcpyAsync(d_in, h_in, nb + 16, hipMemcpyHostToDevice, stream));
-        FHIP(hipMemcpyAsync(d_offs, h_offs, 4ull * (n + 1), hipMemcpyHostToDevice, stream));
         FHIP(hipMemcpyAsync(d_tab, h_tab, sizeof(FsstCTable), hipMemcpyHostToDevice, stream));
         FHIP(launch_fsst_compress(d_in, d_offs, n, d_tab, d_codes, d_clen, stream));
         FHIP(hipMemcpyAsync(h_clen, d_clen, 4ull * n, hipMemcpyDeviceToHost, stream));
@@ -864,11 +940,27 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
 // VARCHAR: DICT when the distinct values are few (at most n / 8, and their
 // bytes + 4 each under half the chunk's bytes), else FSST.  ENC_AUTO builds
 // the dictionary once: it is the estimate and, when DICT wins, the encoding.
+// With a device (gpu), the dictionary is built on the GPU (FsstGpuCtx::
+// run_dict; FLS_WRITER_DICT_GPU=0 keeps it on the host): same entries, same
+// codes, so the same bytes.
 std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const char *bytes, uint32_t n,
                                       FsstGpu *gpu = nullptr) {
     if (enc == ENC_FSST) return enc_fsst(offs, bytes, n, gpu);
     StrDict d;
-    const bool few = build_str_dict(offs, bytes, n, enc == ENC_AUTO ? n / 8 : n, d);
+    const uint32_t limit = enc == ENC_AUTO ? n / 8 : n;
+    bool few;
+    const char *dg = getenv("FLS_WRITER_DICT_GPU");
+    if (gpu && n > 0 && !(dg && atoi(dg) == 0)) {
+        FsstGpuCtx *g = gpu->take();
+        const int rc = g->run_dict(gpu->dev, offs, bytes, n, limit, d, few);
+        gpu->give(g);
+        if (rc) {
+            gpu->failed(rc);
+            return {};
+        }
+    } else {
+        few = build_str_dict(offs, bytes, n, limit, d);
+    }
     if (enc == ENC_AUTO &&
         !(few && d.entry_bytes + 4ull * d.entries.size() < (uint64_t)(offs[n] - offs[0]) / 2))
         return enc_fsst(offs, bytes, n, gpu);

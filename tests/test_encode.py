@@ -415,3 +415,53 @@ def test_gpu_writer_auto_dict_estimate_matches_host(fl, gpu, monkeypatch):
     cpu = fl.write_image(cols).tobytes()
     assert fl.ENC_DICT in _chunk_encodings(cpu) and fl.ENC_FFOR in _chunk_encodings(cpu)
     assert fl.write_image(cols, device=0, threads=8).tobytes() == cpu
+
+
+def _str_dict_columns(fl, n, rng):
+    """VARCHAR / BLOB columns for the GPU string dictionary: few distinct
+    strings (l_shipmode-like), empty strings and NULLs, binary bytes (NUL,
+    0xFF), distinct counts around ENC_AUTO's n / 8 limit, more distinct
+    strings than the GPU sorts (kDictGpuMax: the host builds that one) and
+    free text (AUTO: past the limit, FSST)."""
+    modes = [b"AIR", b"FOB", b"MAIL", b"RAIL", b"REG AIR", b"SHIP", b"TRUCK"]
+    few = [modes[k] for k in rng.integers(0, 7, n)]
+    bins = [bytes(rng.integers(0, 256, rng.integers(0, 6), dtype=np.uint8)) for _ in range(23)]
+    binary = [bins[k] for k in rng.integers(0, 23, n)]
+    nulls = [None if i % 7 == 0 else few[i] for i in range(n)]
+    near = max(1, n // 8)
+    around = [b"k%d" % k for k in rng.integers(0, near, n)]          # distinct count just under n / 8
+    over = [b"k%d" % k for k in rng.integers(0, near + near // 2 + 2, n)]
+    many = [b"m%06d" % k for k in rng.integers(0, 20000, n)]
+    text = [b"t%d %s" % (i, b"x" * int(i % 13)) for i in range(n)]
+    return [("few_dict", fl.VARCHAR, few, fl.ENC_DICT), ("few_auto", fl.VARCHAR, few[::-1], fl.ENC_AUTO),
+            ("bin_dict", fl.BLOB, binary, fl.ENC_DICT), ("bin_auto", fl.BLOB, binary, fl.ENC_AUTO),
+            ("nulls_auto", fl.VARCHAR, nulls, fl.ENC_AUTO), ("around_auto", fl.VARCHAR, around, fl.ENC_AUTO),
+            ("over_auto", fl.VARCHAR, over, fl.ENC_AUTO), ("many_dict", fl.VARCHAR, many, fl.ENC_DICT),
+            ("text_auto", fl.VARCHAR, text, fl.ENC_AUTO)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (9, 1024), (1, 65536)])
+def test_gpu_writer_str_dict_bytes_identical(fl, ref, gpu, monkeypatch, n, rowgroup):
+    """VARCHAR / BLOB dictionaries built on the GPU (str_dict_kernel: the
+    distinct strings in order of first appearance, every row's code, ENC_AUTO's
+    limit of n / 8 distinct strings): the file is the CPU writer's, byte for
+    byte, and its strings decode under the oracle; the host build
+    (FLS_WRITER_DICT_GPU=0) writes the same file."""
+    cols = _str_dict_columns(fl, n, np.random.default_rng(n + 11))
+    cpu_img = fl.write_image(cols, rowgroup=rowgroup)
+    cpu = cpu_img.tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0, threads=8).tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+    rf = ref.RefFile(cpu_img)
+    for c, (name, _, vals, _) in enumerate(cols):
+        assert rf.strings_column(c) == [b"" if v is None else v for v in vals], name
+    monkeypatch.setenv("FLS_WRITER_DICT_GPU", "0")
+    assert fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes() == cpu
+
+
+def test_str_dict_columns_cover_dict_and_fsst_cpu(fl):
+    cols = _str_dict_columns(fl, 65536, np.random.default_rng(4))
+    encs = _chunk_encodings(fl.write_image(cols).tobytes())
+    assert encs.get(fl.ENC_DICT, 0) >= 6 and encs.get(fl.ENC_FSST, 0) >= 2, encs
