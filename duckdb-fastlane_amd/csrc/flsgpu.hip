@@ -295,6 +295,7 @@ struct HostBatch {
 struct Slot {                       // one batch of row groups in flight
     uint32_t rg0 = 0, nrg = 0;      // absolute row groups (consecutive, all surviving pruning)
     bool busy = false;              // a batch is enqueued and not yet fully handed out
+    bool filling = false;           // claimed, its work being enqueued (fill_batch, outside s.mu)
     bool starved = false;           // refill deferred: the host-batch pool is at its cap
     HostBatch *hb = nullptr;        // host side of the batch in flight
     std::vector<DevBuf<uint8_t>> d_out;   // per decoded column
@@ -1337,7 +1338,16 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
 
 // enqueue the next batch of device d into slot si: up to s.batch consecutive
 // surviving row groups
-int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
+// A slot's refill in two parts.  claim_batch (with s.mu held) takes the
+// slot's next row groups and a host batch; fill_batch (without s.mu: the
+// staging copy, descriptors, H2D, launches and D2H of a batch take about a
+// millisecond, and every consumer's acquire and release needs s.mu) enqueues
+// its work; the slot turns busy (visible to acquire) only once its event is
+// recorded.  The read_fastlanes profile of round 3's inline refill: of 1.8 s
+// of scan-thread time (16 threads, lineitem_full SF10), 1.2 s was waiting for
+// the claim lock while one thread ran a refill (profiles/r4/).
+int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si);
+int claim_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     Slot &sl = d.slots[si];
     sl.busy = false;
     sl.starved = false;
@@ -1359,7 +1369,6 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         if (f && ++n_enqueue == atol(f)) return fail(FLS_ERR_NOMEM, "injected batch enqueue failure (FLS_TEST_FAIL_ENQUEUE)");
     }
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
-    const bool filtered = !s.terms.empty();
     sl.rg0 = s.rgs[d.next_p];
     sl.nrg = 1;
     while (sl.nrg < s.batch && d.next_p + sl.nrg < d.p1 && s.rgs[d.next_p + sl.nrg] == sl.rg0 + sl.nrg) sl.nrg++;
@@ -1371,6 +1380,23 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     hb.nrg = sl.nrg;
     hb.handed = hb.released = 0;
     hb.h_out.resize(ncols);
+    sl.filling = true;
+    return 1;
+}
+// Both parts (the scan's first batches, a refill a release unblocks).
+int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
+    const int c = claim_batch(t, s, d, si);
+    if (c <= 0) return c;
+    const int rc = fill_batch(t, s, d, si);
+    d.slots[si].filling = false;
+    d.slots[si].busy = rc == 0;
+    return rc;
+}
+int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
+    Slot &sl = d.slots[si];
+    HostBatch &hb = *sl.hb;
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    const bool filtered = !s.terms.empty();
     HIP_TRY(hipSetDevice(d.dev));
     // 1. H2D of the batch's compressed bytes
     uint64_t lo, hi;
@@ -1594,8 +1620,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                 if (col_selected(s.mask, c))
                     hb.col_ptrs[(size_t)r * ncols + c] =
                         hb.h_out[c].p + (t->meta.rgs[sl.rg0 + r].first_row - t->meta.rgs[sl.rg0].first_row) * hb.ob[c];
-    sl.busy = true;
-    return 0;
+    return 0;  // the caller marks the slot busy (under s.mu)
 }
 
 void build_records(const fls_table *t, HostBatch &hb, uint32_t rg) {
@@ -1785,14 +1810,27 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
             if (any_null) hb->valid_ptrs[i0 + c] = w.data();
         }
     }
-    std::lock_guard<std::mutex> lk(s.mu);
-    s.out.emplace_back(rg, hb);
-    if (++hb->handed == hb->nrg) {
-        // a failed refill does not take this row group back: it is delivered,
-        // and the error surfaces at the next acquire
-        set_scan_error(s, enqueue_batch(t, s, d, si));
+    bool refill = false;
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        s.out.emplace_back(rg, hb);
+        if (++hb->handed == hb->nrg) {
+            // a failed refill does not take this row group back: it is delivered,
+            // and the error surfaces at the next acquire
+            const int c = claim_batch(t, s, d, si);
+            set_scan_error(s, c < 0 ? c : 0);
+            refill = c == 1;
+        }
+        s.cv.notify_all();
     }
-    s.cv.notify_all();
+    if (refill) {  // the slot's next batch, outside s.mu (claim_batch)
+        const int rc = fill_batch(t, s, d, si);
+        std::lock_guard<std::mutex> lk(s.mu);
+        sl.filling = false;
+        sl.busy = rc == 0;
+        set_scan_error(s, rc);
+        s.cv.notify_all();
+    }
     return 1;
 }
 

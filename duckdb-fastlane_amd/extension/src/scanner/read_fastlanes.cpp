@@ -412,52 +412,66 @@ unique_ptr<LocalTableFunctionState> ReadInitLocal(ExecutionContext &context, Tab
 }
 
 // give back the local state's row group and claim the next one (in file and
-// row-group order over all threads); false at the end of all files
+// row-group order over all threads); false at the end of all files.  The
+// global lock covers only the file advance: fls_scan_acquire is thread-safe
+// and hands out row groups in order itself, and it may wait for a batch or
+// enqueue the next one (the 16-thread profile showed two thirds of the scan
+// threads' time waiting for this lock while it was held across the acquire).
 bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &l) {
     ReadProfile *prof = g.prof.get();
     {
         PhaseTimer t(prof, ReadProfile::kRelease);
         l.pin.reset();  // released now unless a chunk DuckDB still holds references it
     }
-    const uint64_t tw = prof ? ReadProfile::now() : 0;
-    std::lock_guard<std::mutex> guard(g.lock);
-    if (prof) prof->ns[ReadProfile::kLockWait] += ReadProfile::now() - tw;
     while (true) {
-        if (!g.cur) {
-            if (g.file_idx >= bind.files.size()) return false;
-            auto t = std::move(g.tables[g.file_idx]);  // opened by InitGlobal
-            if (fls_scan_filter(t->table, g.preds.data(), (uint32_t)g.preds.size()) != 0)
-                throw IOException(string("FastLanes scan failed: ") + fls_last_error());
-            // DICT string columns as codes + dictionary (DuckDB dictionary
-            // vectors: 1-2 bytes per row over PCIe instead of a 16-byte
-            // string_t); FLS_READ_DICT=0 delivers string_t (A/B knob)
-            static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
-            // integer columns narrowed to their row groups' ranges (value -
-            // base in 1-4 bytes, widened in EmitColumn), see ReadInitGlobal
-            // narrowed scans deliver FSST columns as lengths; their string_t
-            // records are built by this thread after the lock (ReadFunction)
-            if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 || fls_scan_narrow(t->table, g.narrow ? 1 : 0) != 0 ||
-                fls_scan_defer_records(t->table, 1) != 0 ||
-                fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
-                throw IOException(string("FastLanes scan failed: ") + fls_last_error());
-            g.cur = std::move(t);
+        std::shared_ptr<OpenTable> cur;
+        idx_t fidx;
+        {
+            const uint64_t tw = prof ? ReadProfile::now() : 0;
+            std::lock_guard<std::mutex> guard(g.lock);
+            if (prof) prof->ns[ReadProfile::kLockWait] += ReadProfile::now() - tw;
+            if (!g.cur) {
+                if (g.file_idx >= bind.files.size()) return false;
+                auto t = std::move(g.tables[g.file_idx]);  // opened by InitGlobal
+                if (fls_scan_filter(t->table, g.preds.data(), (uint32_t)g.preds.size()) != 0)
+                    throw IOException(string("FastLanes scan failed: ") + fls_last_error());
+                // DICT string columns as codes + dictionary (DuckDB dictionary
+                // vectors: 1-2 bytes per row over PCIe instead of a 16-byte
+                // string_t); FLS_READ_DICT=0 delivers string_t (A/B knob)
+                static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
+                // integer columns narrowed to their row groups' ranges (value -
+                // base in 1-4 bytes, widened in EmitColumn), see ReadInitGlobal;
+                // narrowed scans deliver FSST columns as lengths, their string_t
+                // records built by the consuming thread (ReadScan)
+                if (fls_scan_dict_codes(t->table, codes ? 1 : 0) != 0 ||
+                    fls_scan_narrow(t->table, g.narrow ? 1 : 0) != 0 || fls_scan_defer_records(t->table, 1) != 0 ||
+                    fls_scan_begin(t->table, g.mask.data(), 0, fls_table_nrowgroups(t->table)) != 0)
+                    throw IOException(string("FastLanes scan failed: ") + fls_last_error());
+                g.cur = std::move(t);
+            }
+            cur = g.cur;
+            fidx = g.file_idx;
         }
         int rc;
         {
             PhaseTimer t(prof, ReadProfile::kAcquire);
-            rc = fls_scan_acquire(g.cur->table, &l.rg);
+            rc = fls_scan_acquire(cur->table, &l.rg);
         }
         if (rc < 0) throw IOException(string("FastLanes scan failed: ") + fls_last_error());
         if (rc == 1) {
             if (prof) prof->rowgroups++;
-            l.table = g.cur->table;
-            l.pin = make_buffer<RowGroupPin>(g.cur, l.rg.rowgroup);
+            l.table = cur->table;
+            l.pin = make_buffer<RowGroupPin>(cur, l.rg.rowgroup);
             l.rg_pos = 0;
-            l.batch_index = g.rg_base[g.file_idx] + l.rg.rowgroup;
+            l.batch_index = g.rg_base[fidx] + l.rg.rowgroup;
             return true;
         }
-        g.cur.reset();  // closed once the last thread holding one of its row groups lets go
-        g.file_idx++;
+        // this file is done: the first thread to see it moves the scan on
+        std::lock_guard<std::mutex> guard(g.lock);
+        if (g.cur == cur) {
+            g.cur.reset();  // closed once the last thread holding one of its row groups lets go
+            g.file_idx++;
+        }
     }
 }
 

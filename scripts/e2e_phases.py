@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--workload", default="lineitem_full")
     ap.add_argument("--scale", type=float, default=10)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--arms", default="", help="interleaved env arms for the N-thread DataChunk scan: "
+                                               "'name:VAR=v,VAR2=v;name2:...' (same file, same box)")
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     import pkgload
     fl = pkgload.load()
@@ -66,6 +69,29 @@ def main():
                 n, sec = e.scan_rows("read_fastlanes", path, threads=th)
                 print(f"DataChunks {th} threads rep {rep}: {n} rows in {sec * 1e3:.1f} ms = {n / sec / 1e6:.1f} M rows/s",
                       flush=True)
+        if a.arms:
+            import statistics
+            arms = []
+            for spec in a.arms.split(";"):
+                name, _, kv = spec.partition(":")
+                arms.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+            res = {name: [] for name, _ in arms}
+            for _ in range(a.reps):
+                for name, env in arms:
+                    saved = {k: os.environ.get(k) for k in env}
+                    os.environ.update(env)
+                    try:
+                        n, sec = e.scan_rows("read_fastlanes", path, threads=a.threads)
+                    finally:
+                        for k, v in saved.items():
+                            if v is None:
+                                os.environ.pop(k, None)
+                            else:
+                                os.environ[k] = v
+                    res[name].append(n / sec)
+            for name, v in res.items():
+                print(f"arm {name}: DataChunks {a.threads} threads median {statistics.median(v) / 1e6:.1f} M rows/s "
+                      f"(best {max(v) / 1e6:.1f}) over {len(v)}", flush=True)
         # the phase profile of the N-thread scan (read_fastlanes.cpp ReadProfile, printed on stderr)
         os.environ["FLS_READ_PROFILE"] = "1"
         sys.stderr.flush()

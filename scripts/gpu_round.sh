@@ -20,6 +20,7 @@
 #               name=ENV=V,ENV2=V2;name2=...)
 #   fsstsq:<kernel>[:<scale>]  SQ counters of an FSST kernel on l_comment (3 PMC passes)
 #   e2e         read_fastlanes DataChunk delivery, 1 and 16 threads, phase profile
+#   e2earms:<arms>  the same with interleaved env arms (name:VAR=v,...;name2:...)
 #   launcher2   bench.py --gpus 2 rehearsal (both ranks on the one GPU)
 # Results go to gpurun_out/<mode>_<tag>.*; copy what is judged to profiles/.
 TAG=${1:?tag}
@@ -90,6 +91,8 @@ for mode in "$@"; do
     python3 scripts/pmc_summary.py "$kern" $O/fsq_${TAG}_1 $O/fsq_${TAG}_2 $O/fsq_${TAG}_3 | tee $O/fsst_sq_$TAG.txt ;;
   e2e)
     step 600 $O/e2e_phases_$TAG.txt python scripts/e2e_phases.py --scale 10 || exit $? ;;
+  e2earms:*)  # e2earms:<arms>: interleaved env arms of the 16-thread DataChunk scan
+    step 600 $O/e2e_arms_$TAG.txt python scripts/e2e_phases.py --scale 10 --arms "${mode#e2earms:}" || exit $? ;;
   launcher2)
     timeout -k 10 600 python bench.py --gpus 2 --scale 1 --steps 5 --cpu-seconds 0 --e2e-scale 0 --no-traffic \
         > $O/bench_gpus2_$TAG.json 2> $O/bench_gpus2_$TAG.log
