@@ -269,11 +269,19 @@ constexpr uint32_t kSegSlack = 2 * 16 * 8 + 16;    // a lane may write past its 
 // else u32 x 1025), the tagged symbol table u64[256], 256 B kept free (the
 // occupancy the kernel was measured at: 16 waves per CU), the ring.  The
 // packed lengths are staged in the ring before the rounds start.
-template <bool SMALL>
+// Experiment bits of the segmented kernel (0 in the product build; the
+// experiment library, make exp, instantiates the others for same-buffer A/B:
+// FLS_FSST_VARIANT = kFsstDefault | x << kSegXShift).
+enum : int {
+    kSegXShift = 20,
+    kSegXInline = 1,   // records read a string's bytes 4..11 only for inline (<= 12-byte) strings
+    kSegXNoPad = 2,    // no 256 B pad in the per-wave LDS (17 waves per CU instead of 16 for SMALL)
+};
+template <bool SMALL, int X = 0>
 struct SegLds {
     static constexpr uint32_t kOffD = 0;
     static constexpr uint32_t kOffSym = SMALL ? 2064 : 4112;
-    static constexpr uint32_t kOffRing = kOffSym + 2048 + 256;
+    static constexpr uint32_t kOffRing = kOffSym + 2048 + ((X & kSegXNoPad) ? 0 : 256);
     static constexpr uint32_t kPackedMax = SMALL ? 128 * 8 + 128 : 128 * 32 + 128;  // W <= 8 | 32, + zero row
     static constexpr uint32_t kRing = kPackedMax > kSegRingCap + kSegSlack ? kPackedMax : kSegRingCap + kSegSlack;
     static constexpr uint32_t kWave = kOffRing + kRing;
@@ -393,10 +401,10 @@ __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in,
     return qw.bytes();
 }
 
-template <bool SMALL>
+template <bool SMALL, int X = 0>
 __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const VecArgs &a, uint32_t lane,
                            uint32_t *err) {
-    using Layout = SegLds<SMALL>;
+    using Layout = SegLds<SMALL, X>;
     lu8 *ring = L + Layout::kOffRing;
     lu32 *D = reinterpret_cast<lu32 *>(L + Layout::kOffD);
     const uint32_t nvals = a.nvals;
@@ -502,8 +510,18 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
             if (lane < n_ok) {
                 const lu32 *r32 = reinterpret_cast<const lu32 *>(ring);
                 const uint32_t x = d0 - ring_base, i0 = x >> 2;
+                uint32_t w2 = 0, w3 = 0;
+                if constexpr ((X & kSegXInline) != 0) {
+                    if (n <= 12) {  // a pointer record needs only the 4-byte prefix
+                        w2 = r32[i0 + 2];
+                        w3 = r32[i0 + 3];
+                    }
+                } else {
+                    w2 = r32[i0 + 2];
+                    w3 = r32[i0 + 3];
+                }
                 *reinterpret_cast<ov4 *>(a.out + 16ull * i) =
-                    make_record(r32[i0], r32[i0 + 1], r32[i0 + 2], r32[i0 + 3], x & 3, n, h.ptr_base + d0);
+                    make_record(r32[i0], r32[i0 + 1], w2, w3, x & 3, n, h.ptr_base + d0);
             }
             if (n_ok > 0) str_base += rl(rel1, n_ok - 1);
             next_str += n_ok;
@@ -922,7 +940,7 @@ __device__ void cp_vector(lu8 *L, const DevChunk &c, const VecArgs &a, uint32_t 
 // ============================================================================
 enum class Kind { Seg, Cp };
 
-template <Kind K, bool SMALL, bool QUEUE>
+template <Kind K, bool SMALL, bool QUEUE, int X = 0>
 __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchunks, uint32_t nitems, uint32_t item0,
                                            uint32_t item1, uint32_t *queue, uint32_t piece, lu8 *L, uint32_t *err) {
     chunks = uni_ptr(chunks);
@@ -944,7 +962,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
     }
     item0 = uni(item0);
     item1 = uni(item1);
-    constexpr uint32_t kOffSym = K == Kind::Seg ? SegLds<SMALL>::kOffSym : CpLds<SMALL>::kOffSym;
+    constexpr uint32_t kOffSym = K == Kind::Seg ? SegLds<SMALL, X>::kOffSym : CpLds<SMALL>::kOffSym;
     lu64 *sym = reinterpret_cast<lu64 *>(L + kOffSym);
     uint32_t ci = chunk_of(chunks, nchunks, item0);
     DevChunk c = load_chunk(chunks, ci);
@@ -969,7 +987,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
             have_table = true;
         }
         const VecArgs a = vec_args(c, v);
-        if constexpr (K == Kind::Seg) seg_vector<SMALL>(L, sym, c, a, lane, err);
+        if constexpr (K == Kind::Seg) seg_vector<SMALL, X>(L, sym, c, a, lane, err);
         else cp_vector<SMALL>(L, c, a, lane, err);
         wave_sync();
         ++item;
@@ -978,7 +996,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
 
 // register budgets: the segmented kernel 5 waves per SIMD (96 VGPRs, no
 // spill; its LDS admits 16 waves per CU), the code-parallel one 6 (80 VGPRs)
-template <Kind K, bool SMALL, bool QUEUE>
+template <Kind K, bool SMALL, bool QUEUE, int X = 0>
 __global__ __launch_bounds__(64, K == Kind::Seg ? 5 : 6) void fsst_kernel(const DevChunk *__restrict__ chunks,
                                                                          uint32_t nchunks, uint32_t nitems,
                                                                          uint32_t *__restrict__ err,
@@ -996,14 +1014,14 @@ __global__ __launch_bounds__(64, K == Kind::Seg ? 5 : 6) void fsst_kernel(const 
         i1 = min(i0 + per, nitems);
         if (i0 >= i1) return;
     }
-    fsst_range<K, SMALL, QUEUE>(chunks, nchunks, nitems, i0, i1, queue, piece, (lu8 *)(size_t)0, err);
+    fsst_range<K, SMALL, QUEUE, X>(chunks, nchunks, nitems, i0, i1, queue, piece, (lu8 *)(size_t)0, err);
 }
 
-template <Kind K, bool SMALL, bool QUEUE>
+template <Kind K, bool SMALL, bool QUEUE, int X = 0>
 hipError_t launch_kind(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err, hipStream_t stream,
                        const FsstLaunch &how) {
-    const uint32_t shmem = K == Kind::Seg ? SegLds<SMALL>::kWave : CpLds<SMALL>::kWave;
-    auto kern = fsst_kernel<K, SMALL, QUEUE>;
+    const uint32_t shmem = K == Kind::Seg ? SegLds<SMALL, X>::kWave : CpLds<SMALL>::kWave;
+    auto kern = fsst_kernel<K, SMALL, QUEUE, X>;
     // the kernel addresses its dynamic LDS from 0, which holds only without
     // static LDS: refuse to launch one that has some
     static const bool lds_at_zero = [kern] {
@@ -1038,13 +1056,13 @@ hipError_t launch_kind(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), shmem, stream, d_chunks, nchunks, nvecs, d_err, how.queue, piece);
     return hipGetLastError();
 }
-template <Kind K>
+template <Kind K, int X = 0>
 hipError_t launch_kind2(const DevChunk *d, uint32_t nchunks, uint32_t nvecs, uint32_t *err, hipStream_t stream,
                         const FsstLaunch &how) {
-    if (how.queue) return how.small ? launch_kind<K, true, true>(d, nchunks, nvecs, err, stream, how)
-                                    : launch_kind<K, false, true>(d, nchunks, nvecs, err, stream, how);
-    return how.small ? launch_kind<K, true, false>(d, nchunks, nvecs, err, stream, how)
-                     : launch_kind<K, false, false>(d, nchunks, nvecs, err, stream, how);
+    if (how.queue) return how.small ? launch_kind<K, true, true, X>(d, nchunks, nvecs, err, stream, how)
+                                    : launch_kind<K, false, true, X>(d, nchunks, nvecs, err, stream, how);
+    return how.small ? launch_kind<K, true, false, X>(d, nchunks, nvecs, err, stream, how)
+                     : launch_kind<K, false, false, X>(d, nchunks, nvecs, err, stream, how);
 }
 
 // ============================================================================
@@ -1309,16 +1327,30 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
 }
 
 bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
-    // the product build has the default of each kernel only
-    return variant == kFsstDefault && (seg || bytes_per_lane == 8);
+    if (seg || bytes_per_lane == 8) {
+        if (variant == kFsstDefault) return true;  // the product build has each kernel's default only
+#ifdef FLS_EXPERIMENTS
+        const int x = variant >> kSegXShift;
+        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && x >= 1 && x <= 3) return true;
+#endif
+    }
+    return false;
 }
 
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, const FsstLaunch &how) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
     if (!fsst_variant_built(how.variant, how.seg, how.bytes_per_lane)) return hipErrorInvalidValue;
-    return how.seg ? launch_kind2<Kind::Seg>(d_chunks, nchunks, nvecs, d_err, stream, how)
-                   : launch_kind2<Kind::Cp>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    if (!how.seg) return launch_kind2<Kind::Cp>(d_chunks, nchunks, nvecs, d_err, stream, how);
+#ifdef FLS_EXPERIMENTS
+    switch (how.variant >> kSegXShift) {
+    case 1: return launch_kind2<Kind::Seg, 1>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 2: return launch_kind2<Kind::Seg, 2>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 3: return launch_kind2<Kind::Seg, 3>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    default: break;
+    }
+#endif
+    return launch_kind2<Kind::Seg>(d_chunks, nchunks, nvecs, d_err, stream, how);
 }
 
 }  // namespace fls
