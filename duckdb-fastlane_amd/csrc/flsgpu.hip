@@ -333,7 +333,9 @@ struct ScanDev {
     uint32_t rg0 = 0, rg1 = 0;      // span of row groups this GPU owns within the scan
     uint32_t p0 = 0, p1 = 0;        // ... as positions in ScanCtx::rgs
     uint32_t next_p = 0;            // next position to enqueue
-    Slot slots[2];
+    // device slots: batches in flight at once (ScanCtx::nslots of them used)
+    static constexpr int kMaxSlots = 4;
+    Slot slots[kMaxSlots];
     std::vector<std::unique_ptr<HostBatch>> batches;  // host-batch pool of this GPU
     std::vector<HostBatch *> free_batches;
     DevBuf<StrT> strtab;
@@ -388,6 +390,7 @@ struct ScanCtx {
     int64_t held = -1;              // row group fls_scan_next handed out last (released on the next call)
     std::vector<std::pair<uint32_t, HostBatch *>> out;  // row groups handed out and not yet released
     uint32_t max_batches = 64;      // host-batch pool cap per GPU (FLS_SCAN_HOST_BATCHES)
+    int nslots = 2;                 // device slots per GPU (FLS_SCAN_SLOTS, 1..ScanDev::kMaxSlots)
     // sticky error of a failed batch refill (scan_release): consumers waiting
     // for a row group of that batch, and every later acquire, return it
     // instead of waiting for a batch that will never be enqueued
@@ -912,7 +915,7 @@ int fsst_config_check(int policy) {
     if (fv) {
         char *end = nullptr;
         const long v = strtol(fv, &end, 10);
-        if (end == fv || *end != 0 || v < 0 || v > 0xFFFF)
+        if (end == fv || *end != 0 || v < 0 || v > 0x7FFFFFFF)
             return fail(FLS_ERR_CONFIG, "FLS_FSST_VARIANT=%s is not a variant number", fv);
         variant = (int)v;
     }
@@ -1006,7 +1009,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
     FsstLaunch how[kFsstGroups];
     for (int g = 0; g < kFsstGroups; ++g) {
         how[g].bytes_per_lane = (policy & POLICY_FSST16) ? 16 : 8;
-        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv) & 0xFFFF;  // fsst_config_check'ed
+        if (const char *fv = getenv("FLS_FSST_VARIANT")) how[g].variant = atoi(fv);  // fsst_config_check'ed
         how[g].small = g == 0 || g == 2;
         how[g].seg = g < 2;
         if (const char *sc = getenv("FLS_FSST_SEG_CAP")) how[g].seg_cap = atoi(sc);
@@ -1201,6 +1204,8 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
     s.batch = b ? (uint32_t)std::max(1, atoi(b)) : 8u;
     const char *mb = getenv("FLS_SCAN_HOST_BATCHES");
     s.max_batches = mb ? (uint32_t)std::max(2, atoi(mb)) : 64u;
+    const char *ns = getenv("FLS_SCAN_SLOTS");
+    s.nslots = ns ? std::max(1, std::min(ScanDev::kMaxSlots, atoi(ns))) : 2;
     for (uint32_t g = 0; g < G; ++g) {
         ScanDev &d = *s.devs[g];
         HIP_TRY(hipSetDevice(d.dev));
@@ -1677,7 +1682,7 @@ void build_records(const fls_table *t, HostBatch &hb, uint32_t rg) {
 int scan_start(fls_table *t, ScanCtx &s) {
     if (s.rgs.empty()) return 0;
     for (auto &d : s.devs)
-        for (int si = 0; si < 2; ++si) {
+        for (int si = 0; si < s.nslots; ++si) {
             int rc = enqueue_batch(t, s, *d, si);
             if (rc) return rc;
         }
@@ -1687,7 +1692,7 @@ int scan_start(fls_table *t, ScanCtx &s) {
 // the (device, slot) holding row group rg, or false if its batch is not enqueued
 bool find_slot(ScanCtx &s, uint32_t rg, int &g, int &si) {
     for (size_t i = 0; i < s.devs.size(); ++i)
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < s.nslots; ++j) {
             const Slot &sl = s.devs[i]->slots[j];
             if (sl.busy && rg >= sl.rg0 && rg < sl.rg0 + sl.nrg) {
                 g = (int)i;
@@ -1850,7 +1855,7 @@ int scan_release(fls_table *t, ScanCtx &s, uint32_t rg) {
         for (auto &b : d.batches) mine = mine || b.get() == hb;
         if (!mine) continue;
         d.free_batches.push_back(hb);
-        for (int si = 0; si < 2 && !rc; ++si)
+        for (int si = 0; si < s.nslots && !rc; ++si)
             if (d.slots[si].starved) {
                 rc = enqueue_batch(t, s, d, si);
                 set_scan_error(s, rc);
