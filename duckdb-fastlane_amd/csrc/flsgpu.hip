@@ -203,6 +203,7 @@ class CopyPool {
 
 }  // namespace
 
+struct DevImage;  // a file's compressed image resident in HBM (defined with MappedFile)
 namespace {
 
 // Device images are allocated this much past their last chunk: kernels read
@@ -303,7 +304,9 @@ struct Slot {                       // one batch of row groups in flight
     std::vector<uint64_t> heap_bytes;     // per column: heap bytes of this batch
     PinBuf<DevChunk> h_chunks;
     DevBuf<DevChunk> d_chunks;
-    DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch
+    DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch (no resident image)
+    const uint8_t *in_dev = nullptr;  // device address of the batch's first compressed byte
+    std::atomic<bool> upload_resident{false};  // the batch uploads into the resident image (marked present once done)
     PinBuf<uint8_t> h_stage;        // pinned bounce buffer when the image cannot be pinned
     DevBuf<uint32_t> queue;         // decode work-queue counter
     uint64_t in_base = 0;
@@ -336,6 +339,7 @@ struct ScanDev {
     // device slots: batches in flight at once (ScanCtx::nslots of them used)
     static constexpr int kMaxSlots = 4;
     Slot slots[kMaxSlots];
+    std::shared_ptr<DevImage> dimg;  // the scanned file's resident image on this GPU (none: per-slot uploads)
     std::vector<std::unique_ptr<HostBatch>> batches;  // host-batch pool of this GPU
     std::vector<HostBatch *> free_batches;
     DevBuf<StrT> strtab;
@@ -587,11 +591,24 @@ struct Resident {
 // keeps the last few in a process-wide cache keyed by (device, inode, size,
 // mtime), so reopening an unchanged file (DuckDB opens files at every query)
 // skips the chunk-header validation (10-30 ms at SF10).
+// A file's compressed image kept in one GPU's HBM by the scan pipeline: the
+// first scan's batches are uploaded into it instead of a per-slot buffer, and
+// later scans of the same (cached, unchanged) file decode its row groups from
+// it with no staging copy and no H2D -- a warm query moves only decoded bytes
+// over PCIe, in one direction.  Lives with the open-file cache entry.
+struct DevImage {
+    DevBuf<uint8_t> buf;                               // the whole file image, + kImagePad
+    std::unique_ptr<std::atomic<uint8_t>[]> present;   // per row group: its chunks are in buf
+    uint32_t nrg = 0;
+};
 struct MappedFile {
     void *map = nullptr;
     size_t len = 0;
     FileMeta meta;
+    std::mutex dev_mu;
+    std::map<int, std::shared_ptr<DevImage>> dev_img;  // per GPU (scan_setup)
     ~MappedFile() {
+        dev_img.clear();
         if (map) munmap(map, len);
     }
 };
@@ -1073,6 +1090,10 @@ fls_table::~fls_table() {
     // copies may read the image or the pinned stage)
     for (ScanCtx *s : {&scan, &mat})
         for (auto &d : s->devs) {
+            if (d) {
+                d->sync();
+                d->dimg.reset();  // the resident image stays with the open-file cache entry
+            }
             if (res) res->give(std::move(d));
             d.reset();
         }
@@ -1143,6 +1164,37 @@ bool rowgroup_may_match(const fls_table *t, uint32_t rg, const std::vector<HostT
         if (!any) return false;
     }
     return true;
+}
+
+// The file's resident image on GPU dev (made on first use), or none: a table
+// not read from a file, FLS_SCAN_RESIDENT_MB=0, a file over that budget
+// (default 65,536 MB) or over half the GPU's free memory.
+std::shared_ptr<DevImage> resident_image(fls_table *t, int dev) {
+    if (!t->mapped) return nullptr;
+    const char *e = getenv("FLS_SCAN_RESIDENT_MB");
+    const uint64_t budget = (uint64_t)(e ? std::max(0L, atol(e)) : 65536L) << 20;
+    const uint64_t need = t->len + kImagePad;
+    if (need > budget) return nullptr;
+    std::lock_guard<std::mutex> lk(t->mapped->dev_mu);
+    auto &p = t->mapped->dev_img[dev];
+    if (p) return p;
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess || need > free_b / 2) {
+        (void)hipGetLastError();
+        t->mapped->dev_img.erase(dev);
+        return nullptr;
+    }
+    auto di = std::make_shared<DevImage>();
+    if (di->buf.alloc(dev, need) != hipSuccess) {
+        (void)hipGetLastError();
+        t->mapped->dev_img.erase(dev);
+        return nullptr;
+    }
+    di->nrg = (uint32_t)t->meta.rgs.size();
+    di->present.reset(new std::atomic<uint8_t>[di->nrg]);
+    for (uint32_t r = 0; r < di->nrg; ++r) di->present[r].store(0);
+    p = di;
+    return p;
 }
 
 int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uint8_t *col_mask, uint32_t rg0,
@@ -1221,6 +1273,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         d.next_p = d.p0;
         d.rg0 = d.p0 < d.p1 ? s.rgs[d.p0] : 0;
         d.rg1 = d.p0 < d.p1 ? s.rgs[d.p1 - 1] + 1 : 0;
+        d.dimg = resident_image(t, d.dev);
         int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off, d.h_strtab);
         if (rc) return rc;
         if (s.dict_codes && !d.ident.p) {
@@ -1281,7 +1334,7 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
             uint64_t *dst = sl.d_valid[c].p + (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) / 64;
             const size_t bytes = (size_t)kValidityVecBytes * ch.hdr.nvec;
             if (chunk_has_validity(ch.hdr))
-                HIP_TRY(hipMemcpyAsync(dst, sl.d_in.p + (ch.off - in_lo) + validity_off(ch.len, ch.hdr.nvec), bytes,
+                HIP_TRY(hipMemcpyAsync(dst, sl.in_dev + (ch.off - in_lo) + validity_off(ch.len, ch.hdr.nvec), bytes,
                                        hipMemcpyDeviceToDevice, sl.stream));
             else
                 HIP_TRY(hipMemsetAsync(dst, 0xFF, bytes, sl.stream));
@@ -1319,7 +1372,7 @@ int enqueue_filter(fls_table *t, ScanCtx &s, ScanDev &d, Slot &sl, uint64_t rows
             } else {  // DICT: long strings point into the file image, uploaded as d_in
                 dt.host_lo = (uint64_t)(uintptr_t)(t->img + in_lo);
                 dt.host_hi = dt.host_lo + in_len;
-                dt.dev_delta = (int64_t)((uintptr_t)sl.d_in.p - (uintptr_t)(t->img + in_lo));
+                dt.dev_delta = (int64_t)((uintptr_t)sl.in_dev - (uintptr_t)(t->img + in_lo));
             }
         }
     }
@@ -1404,17 +1457,37 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     const bool filtered = !s.terms.empty();
     HIP_TRY(hipSetDevice(d.dev));
     // 1. H2D of the batch's compressed bytes
+    // (resident image: nothing when every row group of the batch is there
+    // already, else the upload goes into the image and marks them present)
     uint64_t lo, hi;
     rg_byte_range(t->meta, sl.rg0, sl.rg0 + sl.nrg, lo, hi);
-    HIP_TRY(sl.d_in.alloc(d.dev, hi - lo + kImagePad));
     sl.in_base = lo;
-    const uint8_t *src = t->img + lo;
-    if (!t->registered) {
-        HIP_TRY(sl.h_stage.alloc(hi - lo));
-        t->res->copy.copy(sl.h_stage.p, src, hi - lo);
-        src = sl.h_stage.p;
+    DevImage *di = d.dimg.get();
+    bool have = di != nullptr;
+    for (uint32_t r = sl.rg0; have && r < sl.rg0 + sl.nrg; ++r) have = di->present[r].load(std::memory_order_acquire) != 0;
+    sl.upload_resident.store(di != nullptr && !have);
+    if (have) {
+        sl.in_dev = di->buf.p + lo;
+        if (getenv("FLS_DEBUG"))
+            fprintf(stderr, "DEBUG: scan batch of row groups [%u, %u) decoded from the HBM-resident image\n", sl.rg0,
+                    sl.rg0 + sl.nrg);
+    } else {
+        uint8_t *dst;
+        if (di) {
+            dst = di->buf.p + lo;
+        } else {
+            HIP_TRY(sl.d_in.alloc(d.dev, hi - lo + kImagePad));
+            dst = sl.d_in.p;
+        }
+        const uint8_t *src = t->img + lo;
+        if (!t->registered) {
+            HIP_TRY(sl.h_stage.alloc(hi - lo));
+            t->res->copy.copy(sl.h_stage.p, src, hi - lo);
+            src = sl.h_stage.p;
+        }
+        HIP_TRY(hipMemcpyAsync(dst, src, hi - lo, hipMemcpyHostToDevice, sl.stream));
+        sl.in_dev = dst;
     }
-    HIP_TRY(hipMemcpyAsync(sl.d_in.p, src, hi - lo, hipMemcpyHostToDevice, sl.stream));
     // dictionary-coded delivery: a delivered DICT string column no filter term
     // reads goes over PCIe as 1- or 2-byte codes when every chunk of the batch
     // is DICT (DuckDB dictionary vectors over the host string_t dictionaries)
@@ -1547,7 +1620,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             const uint8_t *dict = so == UINT64_MAX ? nullptr : (const uint8_t *)(d.strtab.p + so);
             uint8_t *out = sl.d_out[c].p + (t->meta.rgs[r].first_row - t->meta.rgs[sl.rg0].first_row) * dob[c];
             const uint64_t ho = hoff[(size_t)(r - sl.rg0) * ncols + c];
-            list.push_back(make_devchunk(t, r, c, sl.d_in.p + (ch.off - lo), dict, out, &bc,
+            list.push_back(make_devchunk(t, r, c, sl.in_dev + (ch.off - lo), dict, out, &bc,
                                          sl.heap_bytes[c] ? sl.d_heap[c].p + ho : nullptr,
                                          sl.heap_bytes[c] ? hb.h_heap[c].p + ho : nullptr, code_w[c], d.ident.p));
         }
@@ -1776,6 +1849,10 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         s.cv.notify_all();
         return rc;
     }
+    // the batch's upload into the resident image is complete (its event covers
+    // the H2D): later scans of this file may decode these row groups from it
+    if (sl.upload_resident.exchange(false) && d.dimg)
+        for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) d.dimg->present[r].store(1, std::memory_order_release);
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     out->rowgroup = rg;
     out->nrows = t->meta.rgs[rg].nrows;
