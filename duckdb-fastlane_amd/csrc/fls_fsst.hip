@@ -149,7 +149,7 @@ __device__ __forceinline__ VecHeap vec_heap(const DevChunk &c, const VecArgs &a)
 // bytes) rides in the top byte of the entry (the segmented kernel: tables of
 // symbols <= 7 bytes only; a longer one is reported as a bad descriptor).
 // Else the byte lengths go to len[256].
-template <bool TAG>
+template <bool TAG, bool SPLIT = false>
 __device__ __forceinline__ void stage_table(gu8 *aux, lu64 *sym, lu8 *len, uint32_t lane, uint32_t *err) {
     wave_sync();
     const FLS_GLOBAL uint64_t *gs = reinterpret_cast<const FLS_GLOBAL uint64_t *>(aux);
@@ -157,7 +157,12 @@ __device__ __forceinline__ void stage_table(gu8 *aux, lu64 *sym, lu8 *len, uint3
     for (uint32_t k = lane; k < 256; k += 64) {
         const uint32_t n = k == kFsstEscape ? 0u : min((uint32_t)aux[8 * 256 + k], 8u);
         const uint64_t sy = n >= 8 ? gs[k] : gs[k] & ((1ull << (8 * n)) - 1);
-        if constexpr (TAG) {
+        if constexpr (TAG && SPLIT) {  // (experiment) low dwords at [0, 256), high at [256, 512)
+            const uint64_t t = sy | (uint64_t)(8 * n) << 56;
+            reinterpret_cast<lu32 *>(sym)[k] = (uint32_t)t;
+            reinterpret_cast<lu32 *>(sym)[256 + k] = (uint32_t)(t >> 32);
+            long8 |= n >= 8;
+        } else if constexpr (TAG) {
             sym[k] = sy | (uint64_t)(8 * n) << 56;
             long8 |= n >= 8;
         } else {
@@ -276,6 +281,7 @@ enum : int {
     kSegXShift = 20,
     kSegXInline = 1,   // records read a string's bytes 4..11 only for inline (<= 12-byte) strings
     kSegXNoPad = 2,    // no 256 B pad in the per-wave LDS (17 waves per CU instead of 16 for SMALL)
+    kSegXSplit = 4,    // symbol table as two u32 arrays (low / high dwords): two b32 gathers per code
 };
 template <bool SMALL, int X = 0>
 struct SegLds {
@@ -342,7 +348,7 @@ struct LeanWriter {
 // check catches).  The fast path (FULL, no escapes) issues all 16 table reads
 // together; the general one keeps each code byte (a literal's value) beside
 // its entry and reads 4 at a time to stay in the fast path's registers.
-template <bool FULL, bool ESC>
+template <bool FULL, bool ESC, bool SPLIT = false>
 __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in, uint32_t nb, uint32_t &st,
                                              LeanWriter &qw) {
     // an opaque copy: the callers' variants would otherwise share (hoist) the
@@ -359,7 +365,12 @@ __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in,
 #pragma unroll
         for (uint32_t k = 0; k < B; ++k) {
             c[k] = byte_of(raw, B * h + k);
-            sy[k] = sym[c[k]];
+            if constexpr (SPLIT) {
+                const lu32 *s32 = reinterpret_cast<const lu32 *>(sym);
+                sy[k] = (uint64_t)s32[256 + c[k]] << 32 | s32[c[k]];
+            } else {
+                sy[k] = sym[c[k]];
+            }
             if constexpr (!kFast) {
                 sl[k] = (uint32_t)(sy[k] >> 56);
                 sy[k] &= 0x00FFFFFFFFFFFFFFull;
@@ -608,9 +619,10 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
             if (lane >= l0 && lane < l1) {
                 LeanWriter qw(ring, p0 + (incl - dl - done));
                 const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, 16u) : 0u;
-                const uint32_t got = !full   ? seg_lane<false, true>(sym, raw, nb, st, qw)
-                                     : vec_esc ? seg_lane<true, true>(sym, raw, nb, st, qw)
-                                               : seg_lane<true, false>(sym, raw, nb, st, qw);
+                constexpr bool kSplit = (X & kSegXSplit) != 0;
+                const uint32_t got = !full   ? seg_lane<false, true, kSplit>(sym, raw, nb, st, qw)
+                                     : vec_esc ? seg_lane<true, true, kSplit>(sym, raw, nb, st, qw)
+                                               : seg_lane<true, false, kSplit>(sym, raw, nb, st, qw);
                 if (got != dl) bad = true;
                 qw.finish();
             }
@@ -982,7 +994,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
         }
         if (!have_table) {
             gu8 *aux = gptr(c.chunk) + c.aux_off;
-            if constexpr (K == Kind::Seg) stage_table<true>(aux, sym, nullptr, lane, err);
+            if constexpr (K == Kind::Seg) stage_table<true, (X & kSegXSplit) != 0>(aux, sym, nullptr, lane, err);
             else stage_table<false>(aux, sym, L + CpLds<SMALL>::kOffLen, lane, err);
             have_table = true;
         }
@@ -1331,7 +1343,7 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
         if (variant == kFsstDefault) return true;  // the product build has each kernel's default only
 #ifdef FLS_EXPERIMENTS
         const int x = variant >> kSegXShift;
-        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && x >= 1 && x <= 3) return true;
+        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && x >= 1 && x <= 7) return true;
 #endif
     }
     return false;
@@ -1347,6 +1359,10 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     case 1: return launch_kind2<Kind::Seg, 1>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 2: return launch_kind2<Kind::Seg, 2>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 3: return launch_kind2<Kind::Seg, 3>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 4: return launch_kind2<Kind::Seg, 4>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 5: return launch_kind2<Kind::Seg, 5>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 6: return launch_kind2<Kind::Seg, 6>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 7: return launch_kind2<Kind::Seg, 7>(d_chunks, nchunks, nvecs, d_err, stream, how);
     default: break;
     }
 #endif

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cols", default="all")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip checking each arm's decoded columns against the generator")
     a = ap.parse_args()
     import torch  # noqa: F401  (same runtime as the bench)
     import pkgload
@@ -40,6 +42,7 @@ def main():
     t.device_upload()
     sels = [None if c == "all" else [int(c)] for c in a.cols.split(",")]
     res = {}
+    any_bad = False
 
     def run(env, sel, reps):
         saved = {k: os.environ.get(k) for k in env}
@@ -69,11 +72,21 @@ def main():
                 algo = st.algo_bytes
         line = {n: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4),
                     "GBps": round(algo / statistics.median(v) / 1e6, 1)} for n, v in times.items()}
+        if not a.no_verify:  # every arm's output, bit-exact against the seeded generator (on the GPU)
+            for n, env in arms:
+                run(env, sel, 1)
+                mism = fl.check_device_table(t, a.workload, a.scale, a.rows)
+                bad = {c: m for c, m in enumerate(mism) if m and (sel is None or c in sel)}
+                line[n]["verified"] = not bad
+                if bad:
+                    any_bad = True
+                    print(f"{key} arm {n}: MISMATCHING rows per column {bad}", flush=True)
         res[key] = line
         print(key, json.dumps(line), flush=True)
     out = ROOT / "gpurun_out" / "ab_env.json"
     out.parent.mkdir(exist_ok=True)
     out.write_text(json.dumps(res, indent=1))
+    sys.exit(3 if any_bad else 0)
 
 
 if __name__ == "__main__":

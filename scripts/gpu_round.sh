@@ -21,6 +21,9 @@
 #   fsstsq:<kernel>[:<scale>]  SQ counters of an FSST kernel on l_comment (3 PMC passes)
 #   e2e         read_fastlanes DataChunk delivery, 1 and 16 threads, phase profile
 #   e2earms:<arms>  the same with interleaved env arms (name:VAR=v,...;name2:...)
+#   copy:<workload>:<scale>:<reps>:<arms>
+#               COPY (read_fastlanes) TO (FORMAT fls), env arms interleaved
+#               (scripts/writer_bench.py --copy-only; arms name:VAR=v,...;name2:...)
 #   launcher2   bench.py --gpus 2 rehearsal (both ranks on the one GPU)
 # Results go to gpurun_out/<mode>_<tag>.*; copy what is judged to profiles/.
 TAG=${1:?tag}
@@ -93,6 +96,11 @@ for mode in "$@"; do
     step 600 $O/e2e_phases_$TAG.txt python scripts/e2e_phases.py --scale 10 || exit $? ;;
   e2earms:*)  # e2earms:<arms>: interleaved env arms of the 16-thread DataChunk scan
     step 600 $O/e2e_arms_$TAG.txt python scripts/e2e_phases.py --scale 10 --arms "${mode#e2earms:}" || exit $? ;;
+  copy:*)  # copy:<workload>:<scale>:<reps>:<arms>: COPY (read_fastlanes) TO fls, env arms interleaved
+    IFS=: read -r _ wl sc reps arms <<< "$mode"
+    step 900 $O/copy_${TAG}_${wl}_${sc}.txt python scripts/writer_bench.py --copy-only --workload "$wl" \
+        --scale "$sc" --reps "$reps" --arms "$arms" || exit $?
+    grep median $O/copy_${TAG}_${wl}_${sc}.txt ;;
   launcher2)
     timeout -k 10 600 python bench.py --gpus 2 --scale 1 --steps 5 --cpu-seconds 0 --e2e-scale 0 --no-traffic \
         > $O/bench_gpus2_$TAG.json 2> $O/bench_gpus2_$TAG.log
