@@ -850,11 +850,15 @@ __global__ __launch_bounds__(256) void dict_analyze_kernel(EncChunk *__restrict_
         }
         uint32_t h = (uint32_t)dict_hash(x) & mask;
         for (uint32_t probe = 0; probe < cap; ++probe) {
-            const uint64_t old = atomicCAS((unsigned long long *)(keys + h), (unsigned long long)kDictEmpty,
-                                           (unsigned long long)x);
+            // a plain read first: a value already in the table (every repeat
+            // of a low-cardinality column) costs no atomic
+            uint64_t old = __hip_atomic_load(keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == kDictEmpty) {
-                atomicAdd(&cnt, 1u);
-                break;
+                old = atomicCAS((unsigned long long *)(keys + h), (unsigned long long)kDictEmpty, (unsigned long long)x);
+                if (old == kDictEmpty) {
+                    atomicAdd(&cnt, 1u);
+                    break;
+                }
             }
             if (old == x) break;
             h = (h + 1) & mask;
@@ -1049,71 +1053,86 @@ __global__ __launch_bounds__(256) void dict_encode_kernel(const EncChunk *__rest
 
 
 // ---- VARCHAR / BLOB dictionaries (build_str_dict's order: first appearance) ----
-// Rows are hashed into an open-addressing table whose slot holds the row that
-// claimed it (atomicCAS), the smallest row holding its string (atomicMin: the
-// first appearance) and, once sorted, its code; a probe compares the candidate
-// row's bytes with the claiming row's.  The distinct strings, ordered by first
-// row (a bitonic sort in LDS), number the codes.
-__device__ __forceinline__ uint64_t str_hash_d(const uint8_t *p, uint32_t n) {
-    uint64_t h = 0xcbf29ce484222325ull ^ n;
-    for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
-    return dict_hash(h);
+// Four steps on the context's stream, no host round trip between them:
+//   insert (a thread per row, the whole grid): the row's bytes hashed a word
+//     at a time, then linear probing of an open-addressing table in HBM whose
+//     slot holds the row that claimed it (atomicCAS on an empty slot; a slot
+//     already held is compared word by word, no atomic), the smallest row
+//     holding its string (atomicMin: the first appearance) and, once sorted,
+//     its code; a global count of distinct strings, and past `limit` an
+//     overflow flag that ends the other rows early;
+//   sort (one block): the distinct strings as (first row, slot) in LDS, a
+//     bitonic sort by first row numbers the codes;
+//   codes (the grid): each row's code through its slot.
+// The bytes are 8-aligned with 16 readable bytes past the last string, so a
+// string is read as aligned qwords whatever its offset.
+__device__ __forceinline__ uint64_t str_word(const uint8_t *bytes, uint32_t p, uint32_t left) {
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(bytes + (p & ~7u));
+    const uint32_t sh = 8 * (p & 7);
+    uint64_t w = q[0] >> sh;
+    if (sh) w |= q[1] << (64 - sh);
+    return left >= 8 ? w : w & ((1ull << (8 * left)) - 1);
+}
+__device__ __forceinline__ uint64_t str_hash_d(const uint8_t *bytes, uint32_t p, uint32_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    for (uint32_t k = 0; k < n; k += 8) h = dict_hash(h ^ str_word(bytes, p + k, n - k));
+    return h;
 }
 __device__ __forceinline__ bool str_eq_d(const uint8_t *bytes, const uint32_t *offs, uint32_t a, uint32_t b) {
     const uint32_t a0 = offs[a], la = offs[a + 1] - a0, b0 = offs[b], lb = offs[b + 1] - b0;
     if (la != lb) return false;
-    for (uint32_t i = 0; i < la; ++i)
-        if (bytes[a0 + i] != bytes[b0 + i]) return false;
+    for (uint32_t k = 0; k < la; k += 8)
+        if (str_word(bytes, a0 + k, la - k) != str_word(bytes, b0 + k, la - k)) return false;
     return true;
 }
 constexpr uint32_t kStrEmpty = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(1024) void str_dict_kernel(const uint8_t *__restrict__ bytes, const uint32_t *__restrict__ offs,
-                                                        uint32_t n, uint32_t limit, uint32_t *__restrict__ slots,
-                                                        uint32_t *__restrict__ row_slot, uint32_t *__restrict__ codes,
-                                                        uint32_t *__restrict__ entries, StrDictInfo *__restrict__ info) {
-    __shared__ uint64_t K[kDictGpuMax];
-    __shared__ uint32_t cnt, overflow, fill;
-    __shared__ unsigned long long ebytes;
+__global__ __launch_bounds__(256) void str_dict_insert_kernel(const uint8_t *__restrict__ bytes,
+                                                              const uint32_t *__restrict__ offs, uint32_t n,
+                                                              uint32_t limit, uint32_t *__restrict__ slots,
+                                                              uint32_t *__restrict__ row_slot, StrDictInfo *info) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (__hip_atomic_load(&info->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const uint32_t cap = enc_dict_cap(n), mask = cap - 1;
-    uint32_t *srow = slots, *sfirst = slots + cap, *scode = slots + 2 * cap;
-    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
-        srow[i] = kStrEmpty;
-        sfirst[i] = kStrEmpty;
+    uint32_t *srow = slots, *sfirst = slots + cap;
+    const uint32_t p = offs[i], len = offs[i + 1] - p;
+    uint32_t s = (uint32_t)str_hash_d(bytes, p, len) & mask;
+    for (uint32_t probe = 0; probe < cap; ++probe) {
+        uint32_t r = __hip_atomic_load(srow + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r == kStrEmpty) {
+            r = atomicCAS(srow + s, kStrEmpty, i);
+            if (r == kStrEmpty) {
+                if (atomicAdd(&info->count, 1u) >= limit) atomicOr(&info->overflow, 1u);
+                break;
+            }
+        }
+        if (str_eq_d(bytes, offs, r, i)) break;
+        s = (s + 1) & mask;
+    }
+    atomicMin(sfirst + s, i);
+    row_slot[i] = s;
+}
+
+__global__ __launch_bounds__(1024) void str_dict_sort_kernel(const uint32_t *__restrict__ offs, uint32_t n,
+                                                             uint32_t *__restrict__ slots, uint32_t *__restrict__ entries,
+                                                             StrDictInfo *__restrict__ info) {
+    __shared__ uint64_t K[kDictGpuMax];
+    __shared__ uint32_t fill;
+    __shared__ unsigned long long ebytes;
+    const uint32_t cap = enc_dict_cap(n);
+    const uint32_t *srow = slots, *sfirst = slots + cap;
+    uint32_t *scode = slots + 2 * cap;
+    const uint32_t d = info->count;
+    if (info->overflow || d > kDictGpuMax) {
+        if (threadIdx.x == 0) info->big = !info->overflow;
+        return;
     }
     if (threadIdx.x == 0) {
-        cnt = 0;
-        overflow = 0;
         fill = 0;
         ebytes = 0;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        if (*(volatile uint32_t *)&overflow) break;
-        uint32_t s = (uint32_t)str_hash_d(bytes + offs[i], offs[i + 1] - offs[i]) & mask;
-        for (uint32_t probe = 0; probe < cap; ++probe) {
-            const uint32_t r = atomicCAS(srow + s, kStrEmpty, i);
-            if (r == kStrEmpty) {
-                if (atomicAdd(&cnt, 1u) >= limit) overflow = 1;
-                break;
-            }
-            if (str_eq_d(bytes, offs, r, i)) break;
-            s = (s + 1) & mask;
-        }
-        atomicMin(sfirst + s, i);
-        row_slot[i] = s;
-    }
-    __syncthreads();
-    const uint32_t d = cnt;
-    if (overflow || d > kDictGpuMax) {
-        if (threadIdx.x == 0) {
-            info->count = d;
-            info->overflow = overflow;
-            info->big = !overflow;
-            info->entry_bytes = 0;
-        }
-        return;
-    }
     // the distinct strings as (first row << 32 | slot), sorted by first row
     for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) {
         const uint32_t r = srow[s];
@@ -1131,14 +1150,18 @@ __global__ __launch_bounds__(1024) void str_dict_kernel(const uint8_t *__restric
         scode[(uint32_t)K[k]] = k;
         entries[k] = (uint32_t)(K[k] >> 32);
     }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) codes[i] = scode[row_slot[i]];
     if (threadIdx.x == 0) {
-        info->count = d;
-        info->overflow = 0;
         info->big = 0;
         info->entry_bytes = ebytes;
     }
+}
+
+__global__ __launch_bounds__(256) void str_dict_codes_kernel(uint32_t n, const uint32_t *__restrict__ slots,
+                                                             const uint32_t *__restrict__ row_slot,
+                                                             uint32_t *__restrict__ codes, const StrDictInfo *info) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || info->overflow || info->big) return;
+    codes[i] = slots[2 * enc_dict_cap(n) + row_slot[i]];
 }
 
 // One lane per string.  The table is staged in LDS; a lane reads its string
@@ -1207,8 +1230,15 @@ hipError_t launch_str_dict(const uint8_t *d_bytes, const uint32_t *d_offs, uint3
                            uint32_t *d_slots, uint32_t *d_row_slot, uint32_t *d_codes, uint32_t *d_entries,
                            StrDictInfo *d_info, hipStream_t stream) {
     if (n == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(str_dict_kernel, dim3(1), dim3(1024), 0, stream, d_bytes, d_offs, n, limit, d_slots, d_row_slot,
-                       d_codes, d_entries, d_info);
+    const uint32_t cap = enc_dict_cap(n), grid = (n + 255) / 256;
+    hipError_t e = hipMemsetAsync(d_slots, 0xFF, 8ull * cap, stream);   // row and first row: empty
+    if (e == hipSuccess) e = hipMemsetAsync(d_info, 0, sizeof(StrDictInfo), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(str_dict_insert_kernel, dim3(grid), dim3(256), 0, stream, d_bytes, d_offs, n, limit, d_slots,
+                       d_row_slot, d_info);
+    hipLaunchKernelGGL(str_dict_sort_kernel, dim3(1), dim3(1024), 0, stream, d_offs, n, d_slots, d_entries, d_info);
+    hipLaunchKernelGGL(str_dict_codes_kernel, dim3(grid), dim3(256), 0, stream, n, d_slots, d_row_slot, d_codes,
+                       d_info);
     return hipGetLastError();
 }
 

@@ -769,8 +769,13 @@ struct FsstGpuCtx {
             FHIP(hipHostMalloc((void **)&h_info, sizeof(StrDictInfo), 0));
             dict_n_cap = n;
         }
+        // one round trip: the codes and entries come back with the outcome
+        // (unused when the build overflowed or is left to the host)
         FHIP(launch_str_dict(d_in, d_offs, n, limit, d_slots, d_rows, d_dcodes, d_entries, d_info, stream));
         FHIP(hipMemcpyAsync(h_info, d_info, sizeof(StrDictInfo), hipMemcpyDeviceToHost, stream));
+        FHIP(hipMemcpyAsync(h_dcodes, d_dcodes, 4ull * n, hipMemcpyDeviceToHost, stream));
+        FHIP(hipMemcpyAsync(h_entries, d_entries, 4ull * std::min<uint32_t>(n, kDictGpuMax), hipMemcpyDeviceToHost,
+                            stream));
         FHIP(hipStreamSynchronize(stream));
         const StrDictInfo info = *h_info;
         if (info.overflow) {
@@ -781,9 +786,8 @@ struct FsstGpuCtx {
             few = build_str_dict(offs, bytes, n, limit, d);
             return 0;
         }
-        FHIP(hipMemcpyAsync(h_dcodes, d_dcodes, 4ull * n, hipMemcpyDeviceToHost, stream));
-        FHIP(hipMemcpyAsync(h_entries, d_entries, 4ull * info.count, hipMemcpyDeviceToHost, stream));
-        FHIP(hipStreamSynchronize(stream));
+        if (info.count > std::min<uint32_t>(n, kDictGpuMax))
+            return fail(FLS_ERR_DEVICE, "GPU string dictionary: %u entries for %u rows", info.count, n);
         d.entries.resize(info.count);
         for (uint32_t k = 0; k < info.count; ++k) {
             const uint32_t r = h_entries[k];
@@ -798,11 +802,13 @@ struct FsstGpuCtx {
 
     // compress strings [offs[0], offs[n]) of bytes with table st: string i's
     // codes at h_codes + 2 * (offs[i] - offs[0]), their count h_clen[i]
-    int run(int dev, const FsstTable &st, const uint32_t *offs, const char *bytes, uint32_t n) {
+    // (uploaded: these strings are already in d_in / d_offs, from run_dict)
+    int run(int dev, const FsstTable &st, const uint32_t *offs, const char *bytes, uint32_t n, bool uploaded = false) {
         // test hook: a failed device compression (the writer's error path)
         if (const char *f = getenv("FLS_TEST_FAIL_FSST_GPU"); f && atoi(f) != 0)
             return fail(FLS_ERR_DEVICE, "injected GPU FSST compression failure");
-        if (int rc = upload(dev, offs, bytes, n)) return rc;
+        if (!uploaded)
+            if (int rc = upload(dev, offs, bytes, n)) return rc;
         const size_t nb = offs[n] - offs[0];
         // the table: codes of length >= 2 bucketed by their first two bytes in
         // the order the host's two-byte index lists them (by_first order)
@@ -874,13 +880,16 @@ struct FsstGpu {
 };
 
 // gpu: compress on that GPU (fls_writer_set_device); a failure is recorded in
-// gpu->err (the caller reports it) and leaves an empty chunk
-std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n, FsstGpu *gpu = nullptr) {
+// gpu->err (the caller reports it) and leaves an empty chunk.  held: a context
+// taken from gpu that already holds these strings (ENC_AUTO's dictionary
+// attempt uploaded them); it is given back here.
+std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n, FsstGpu *gpu = nullptr,
+                              FsstGpuCtx *held = nullptr) {
     const FsstTable st = fsst_build(offs, bytes, n);
     FsstGpuCtx *g = nullptr;
     if (gpu) {
-        g = gpu->take();
-        if (const int rc = g->run(gpu->dev, st, offs, bytes, n)) {
+        g = held ? held : gpu->take();
+        if (const int rc = g->run(gpu->dev, st, offs, bytes, n, held != nullptr)) {
             gpu->give(g);
             gpu->failed(rc);
             return {};
@@ -950,14 +959,19 @@ std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const c
     const uint32_t limit = enc == ENC_AUTO ? n / 8 : n;
     bool few;
     const char *dg = getenv("FLS_WRITER_DICT_GPU");
-    if (gpu && n > 0 && !(dg && atoi(dg) == 0)) {
+    const char *sg = getenv("FLS_WRITER_STRDICT_GPU");   // (A/B: strings only; default follows DICT_GPU)
+    if (gpu && n > 0 && !(dg && atoi(dg) == 0) && !(sg && atoi(sg) == 0)) {
         FsstGpuCtx *g = gpu->take();
         const int rc = g->run_dict(gpu->dev, offs, bytes, n, limit, d, few);
-        gpu->give(g);
         if (rc) {
+            gpu->give(g);
             gpu->failed(rc);
             return {};
         }
+        if (enc == ENC_AUTO &&
+            !(few && d.entry_bytes + 4ull * d.entries.size() < (uint64_t)(offs[n] - offs[0]) / 2))
+            return enc_fsst(offs, bytes, n, gpu, g);   // the strings are on the GPU already
+        gpu->give(g);
     } else {
         few = build_str_dict(offs, bytes, n, limit, d);
     }
