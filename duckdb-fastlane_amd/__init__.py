@@ -258,7 +258,7 @@ def gen_dict_string(workload: str, col: int, code: int) -> str | None:
 
 # --- writer ----------------------------------------------------------------
 def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: int = -1,
-                batch: int = 1, threads: int = 0) -> Image:
+                batch: int = 1, threads: int = 0, path: str | None = None) -> Image | None:
     """columns: list of (name, type, values, encoding[, width, scale]).
     values: numpy int array for integer types, float array for FLOAT/DOUBLE
     (stored bit-exactly), list of str/bytes for VARCHAR.  NULLs: None entries
@@ -266,7 +266,9 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
     goes to fls_writer_add_rowgroups_v).  device >= 0: the
     FFOR / DELTA integer columns are encoded on that GPU (same bytes).
     batch > 1: row groups go in `batch` at a time (fls_writer_add_rowgroups;
-    same bytes).  threads > 0: writer threads (fls_writer_set_threads)."""
+    same bytes).  threads > 0: writer threads (fls_writer_set_threads).
+    path: the file is written there instead (fls_writer_finish_file: the
+    same bytes, chunks written in parallel, no image); returns None."""
     w = _lib.fls_writer_new(row_offset)
     try:
         _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))
@@ -335,6 +337,9 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
                 _check(_lib.fls_writer_add_rowgroups(w, len(grp), rows, data, offs))
             else:
                 _check(_lib.fls_writer_add_rowgroup(w, rows[0], data, offs))
+        if path is not None:
+            _check(_lib.fls_writer_finish_file(w, str(path).encode()))
+            return None
         p, ln = _P(), C.c_uint64()
         rc = _lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln))
         return _take_image(rc, p, ln)

@@ -1110,7 +1110,10 @@ __global__ __launch_bounds__(256) void str_dict_insert_kernel(const uint8_t *__r
         if (str_eq_d(bytes, offs, r, i)) break;
         s = (s + 1) & mask;
     }
-    atomicMin(sfirst + s, i);
+    // first appearance: only a row below the slot's current first row takes
+    // the atomic (a low-cardinality column would otherwise send every row's
+    // atomicMin to the same few addresses)
+    if (__hip_atomic_load(sfirst + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > i) atomicMin(sfirst + s, i);
     row_slot[i] = s;
 }
 

@@ -10,6 +10,7 @@
 #include <cstddef>
 #include <atomic>
 #include <chrono>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -23,6 +24,9 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 #include "../../include/flsgpu.h"
 #include "../../include/flswriter.h"
@@ -879,13 +883,28 @@ struct FsstGpu {
     ~FsstGpu() { release(); }
 };
 
+// FLS_WRITER_PROFILE=1: time in the string chunk steps, summed over worker
+// threads (printed with the writer's phases)
+struct StrProfile {
+    std::atomic<uint64_t> dict_ns{0}, table_ns{0}, compress_ns{0}, chunks{0};
+    static uint64_t now_ns() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+};
+StrProfile g_str_prof;
+bool g_str_prof_on = getenv("FLS_WRITER_PROFILE") != nullptr;  // (re-read by fls_writer_new)
+
 // gpu: compress on that GPU (fls_writer_set_device); a failure is recorded in
 // gpu->err (the caller reports it) and leaves an empty chunk.  held: a context
 // taken from gpu that already holds these strings (ENC_AUTO's dictionary
 // attempt uploaded them); it is given back here.
 std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t n, FsstGpu *gpu = nullptr,
                               FsstGpuCtx *held = nullptr) {
+    const uint64_t t0 = g_str_prof_on ? StrProfile::now_ns() : 0;
     const FsstTable st = fsst_build(offs, bytes, n);
+    const uint64_t t1 = g_str_prof_on ? StrProfile::now_ns() : 0;
+    if (g_str_prof_on) g_str_prof.table_ns += t1 - t0;
     FsstGpuCtx *g = nullptr;
     if (gpu) {
         g = held ? held : gpu->take();
@@ -894,6 +913,7 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
             gpu->failed(rc);
             return {};
         }
+        if (g_str_prof_on) g_str_prof.compress_ns += StrProfile::now_ns() - t1;
     }
     std::vector<uint8_t> table(kFsstTableBytes, 0);
     memcpy(table.data(), st.sym, 8 * 256);
@@ -949,9 +969,8 @@ std::vector<uint8_t> enc_fsst(const uint32_t *offs, const char *bytes, uint32_t 
 // VARCHAR: DICT when the distinct values are few (at most n / 8, and their
 // bytes + 4 each under half the chunk's bytes), else FSST.  ENC_AUTO builds
 // the dictionary once: it is the estimate and, when DICT wins, the encoding.
-// With a device (gpu), the dictionary is built on the GPU (FsstGpuCtx::
-// run_dict; FLS_WRITER_DICT_GPU=0 keeps it on the host): same entries, same
-// codes, so the same bytes.
+// With a device (gpu) and FLS_WRITER_STRDICT_GPU=1 the dictionary is built
+// on the GPU (FsstGpuCtx::run_dict): same entries, same codes, same bytes.
 std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const char *bytes, uint32_t n,
                                       FsstGpu *gpu = nullptr) {
     if (enc == ENC_FSST) return enc_fsst(offs, bytes, n, gpu);
@@ -959,10 +978,17 @@ std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const c
     const uint32_t limit = enc == ENC_AUTO ? n / 8 : n;
     bool few;
     const char *dg = getenv("FLS_WRITER_DICT_GPU");
-    const char *sg = getenv("FLS_WRITER_STRDICT_GPU");   // (A/B: strings only; default follows DICT_GPU)
-    if (gpu && n > 0 && !(dg && atoi(dg) == 0) && !(sg && atoi(sg) == 0)) {
+    // VARCHAR dictionaries on the GPU are opt-in (FLS_WRITER_STRDICT_GPU=1):
+    // a chunk's build is one synchronous round trip (~0.45 ms of copies and
+    // kernels, queued behind the other workers' on the device), slower in
+    // COPY than the host threads' build
+    const char *sg = getenv("FLS_WRITER_STRDICT_GPU");
+    const uint64_t t0 = g_str_prof_on ? StrProfile::now_ns() : 0;
+    if (g_str_prof_on) ++g_str_prof.chunks;
+    if (gpu && n > 0 && !(dg && atoi(dg) == 0) && sg && atoi(sg) != 0) {
         FsstGpuCtx *g = gpu->take();
         const int rc = g->run_dict(gpu->dev, offs, bytes, n, limit, d, few);
+        if (g_str_prof_on) g_str_prof.dict_ns += StrProfile::now_ns() - t0;
         if (rc) {
             gpu->give(g);
             gpu->failed(rc);
@@ -974,6 +1000,7 @@ std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const c
         gpu->give(g);
     } else {
         few = build_str_dict(offs, bytes, n, limit, d);
+        if (g_str_prof_on) g_str_prof.dict_ns += StrProfile::now_ns() - t0;
     }
     if (enc == ENC_AUTO &&
         !(few && d.entry_bytes + 4ull * d.entries.size() < (uint64_t)(offs[n] - offs[0]) / 2))
@@ -1384,6 +1411,81 @@ struct FileBuilder {
         *len = total;
         return 0;
     }
+
+    // The same bytes written straight to a file: every chunk pwrite()n at its
+    // offset by the row group's thread (no image of the whole file in memory,
+    // no single-threaded write of it).  Padding is written, not left as holes.
+    int write_file(const char *path, int nthreads) {
+        std::vector<uint64_t> offs;
+        uint64_t off = 256;
+        for (auto &r : rgs)
+            for (size_t c = 0; c < r.chunks.size(); ++c) {
+                offs.push_back(off);
+                off += (r.chunk_len(c) + 15) & ~15ull;
+            }
+        std::vector<uint8_t> ft = footer(offs);
+        const uint64_t foot_off = off;
+        const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) return fail(FLS_ERR_IO, "cannot create %s: %s", path, strerror(errno));
+        std::atomic<int> bad{0};
+        auto put = [&](const void *p, uint64_t n, uint64_t at) {
+            const uint8_t *b = (const uint8_t *)p;
+            while (n > 0) {
+                const ssize_t k = ::pwrite(fd, b, std::min<uint64_t>(n, 1ull << 30), (off_t)at);
+                if (k < 0 && errno == EINTR) continue;
+                if (k <= 0) {
+                    bad.store(errno ? errno : EIO);
+                    return;
+                }
+                b += k;
+                at += (uint64_t)k;
+                n -= (uint64_t)k;
+            }
+        };
+        uint8_t head[256] = {};
+        memcpy(head, kFileMagic, 8);
+        const uint64_t version = 1;
+        memcpy(head + 8, &version, 8);
+        put(head, sizeof(head), 0);
+        std::atomic<size_t> next{0};
+        std::vector<size_t> rg_first(rgs.size() + 1, 0);
+        for (size_t i = 0; i < rgs.size(); ++i) rg_first[i + 1] = rg_first[i] + rgs[i].chunks.size();
+        static const uint8_t zeros[16] = {};
+        auto work = [&]() {
+            std::vector<uint8_t> tmp;
+            for (size_t r; !bad.load() && (r = next.fetch_add(1)) < rgs.size();) {
+                for (size_t c = 0; c < rgs[r].chunks.size(); ++c) {
+                    auto &ch = rgs[r].chunks[c];
+                    const uint64_t at = offs[rg_first[r] + c], len = rgs[r].chunk_len(c), padded = (len + 15) & ~15ull;
+                    if (c < rgs[r].valid.size() && !rgs[r].valid[c].empty()) {
+                        tmp.assign(padded, 0);
+                        memcpy(tmp.data(), ch.data(), ch.size());
+                        append_validity(tmp.data(), ch.size(), len, rgs[r].valid[c]);
+                        put(tmp.data(), padded, at);
+                    } else {
+                        put(ch.data(), ch.size(), at);
+                        if (padded > ch.size()) put(zeros, padded - ch.size(), at + ch.size());
+                    }
+                    std::vector<uint8_t>().swap(ch);
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+        work();
+        for (auto &t : th) t.join();
+        uint8_t tail[16];
+        const uint32_t flen = (uint32_t)ft.size();
+        memcpy(tail, &foot_off, 8);
+        memcpy(tail + 8, &flen, 4);
+        memcpy(tail + 12, kTailMagic, 4);
+        ft.insert(ft.end(), tail, tail + 16);
+        put(ft.data(), ft.size(), foot_off);
+        const int e = bad.load();
+        if (::close(fd) != 0 && !e) return fail(FLS_ERR_IO, "close %s: %s", path, strerror(errno));
+        if (e) return fail(FLS_ERR_IO, "write to %s: %s", path, strerror(e));
+        return 0;
+    }
 };
 
 // ---- seeded workloads ----------------------------------------------------
@@ -1570,6 +1672,12 @@ struct WriterProfile {
                     "fls_writer profile: CPU columns, GPU staging and zone maps %.3f s, submit %.3f s, gpu wait %.3f s, "
                     "copy out %.3f s (%llu flushes), finish %.3f s\n",
                     cpu, submit, gpu_wait, copy_out, (unsigned long long)flushes, finish);
+        if (on)
+            fprintf(stderr,
+                    "fls_writer profile: string chunks %llu: dictionaries %.3f s, FSST tables %.3f s, "
+                    "FSST compression (GPU round trips) %.3f s (summed over worker threads)\n",
+                    (unsigned long long)g_str_prof.chunks.load(), g_str_prof.dict_ns.load() * 1e-9,
+                    g_str_prof.table_ns.load() * 1e-9, g_str_prof.compress_ns.load() * 1e-9);
     }
 };
 static WriterProfile g_prof;
@@ -1961,6 +2069,7 @@ extern "C" {
 fls_writer *fls_writer_new(uint64_t row_offset) {
     auto *w = new fls_writer();
     w->fb.row_offset = row_offset;
+    g_prof.on = g_str_prof_on = getenv("FLS_WRITER_PROFILE") != nullptr;  // (profiles the writers made from here on)
     return w;
 }
 
@@ -2275,8 +2384,10 @@ int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows) {
     return 0;
 }
 
-int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
-    if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
+namespace {
+// the image (img) or the file (path): the GPU encoder's last batch completed,
+// then the row groups assembled
+int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path) {
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
     if (w->gpu.dev >= 0) {
@@ -2284,27 +2395,25 @@ int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
         if (rc) return rc;
     }
     const double tf = g_prof.on ? WriterProfile::now() : 0;
-    const int rc = w->fb.finish(img, len, w->threads);
+    const int rc = path ? w->fb.write_file(path, w->threads) : w->fb.finish(img, len, w->threads);
     if (g_prof.on) {
         g_prof.finish += WriterProfile::now() - tf;
         g_prof.print();
         g_prof = WriterProfile();
+        g_str_prof.dict_ns = g_str_prof.table_ns = g_str_prof.compress_ns = g_str_prof.chunks = 0;
     }
     return rc;
 }
+}  // namespace
+
+int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
+    if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
+    return finish_writer(w, img, len, nullptr);
+}
 
 int fls_writer_finish_file(fls_writer *w, const char *path) {
-    uint8_t *img = nullptr;
-    uint64_t len = 0;
-    int rc = fls_writer_finish_image(w, &img, &len);
-    if (rc) return rc;
-    FILE *f = fopen(path, "wb");
-    if (!f) { free(img); return fail(FLS_ERR_IO, "cannot create %s", path); }
-    size_t wr = fwrite(img, 1, len, f);
-    fclose(f);
-    free(img);
-    if (wr != len) return fail(FLS_ERR_IO, "short write to %s", path);
-    return 0;
+    if (!w || !path) return fail(FLS_ERR_ARG, "fls_writer_finish_file: NULL argument");
+    return finish_writer(w, nullptr, nullptr, path);
 }
 
 void fls_image_free(uint8_t *img) { free(img); }

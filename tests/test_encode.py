@@ -447,10 +447,13 @@ def test_gpu_writer_str_dict_bytes_identical(fl, ref, gpu, monkeypatch, n, rowgr
     distinct strings in order of first appearance, every row's code, ENC_AUTO's
     limit of n / 8 distinct strings): the file is the CPU writer's, byte for
     byte, and its strings decode under the oracle; the host build
-    (FLS_WRITER_DICT_GPU=0) writes the same file."""
+    (FLS_WRITER_DICT_GPU=0) writes the same file.  FLS_WRITER_STRDICT_GPU=1
+    selects the GPU build (off by default: one round trip per chunk measured
+    slower than the host threads' build in COPY)."""
     cols = _str_dict_columns(fl, n, np.random.default_rng(n + 11))
     cpu_img = fl.write_image(cols, rowgroup=rowgroup)
     cpu = cpu_img.tobytes()
+    monkeypatch.setenv("FLS_WRITER_STRDICT_GPU", "1")   # opt-in (the host build is the default)
     dev = fl.write_image(cols, rowgroup=rowgroup, device=0, threads=8).tobytes()
     assert len(cpu) == len(dev)
     assert cpu == dev

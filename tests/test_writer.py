@@ -227,3 +227,27 @@ def test_add_rowgroups_rejects_short_group_before_the_last(fl):
         assert lib.fls_writer_add_rowgroups(w, 1, (C.c_uint32 * 1)(1024), (C.c_void_p * 1)(b.ctypes.data), None) != 0
     finally:
         lib.fls_writer_free(w)
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_finish_file_writes_the_image_bytes(fl, tmp_path, threads):
+    # fls_writer_finish_file pwrite()s every chunk at its offset from the
+    # writer's threads (no whole-file image): the same bytes as
+    # fls_writer_finish_image, NULL-bearing chunks (validity appended) included
+    n = 5 * 1024 + 300
+    cols = _mixed_columns(fl, n, 7)
+    rng = np.random.default_rng(3)
+    cols.append(("nv", fl.INT32, np.ma.masked_array(rng.integers(0, 100, n), mask=rng.random(n) < 0.1),
+                 fl.ENC_AUTO))
+    cols.append(("ns", fl.VARCHAR, [None if i % 7 == 0 else "v%d" % (i % 13) for i in range(n)], fl.ENC_AUTO))
+    img = fl.write_image(cols, rowgroup=1024, batch=4, threads=threads)
+    path = tmp_path / "t.fls"
+    assert fl.write_image(cols, rowgroup=1024, batch=4, threads=threads, path=path) is None
+    assert path.read_bytes() == bytes(img.view())
+
+
+def test_finish_file_reports_unwritable_path(fl, tmp_path):
+    cols = _mixed_columns(fl, 2000, 1)
+    with pytest.raises(fl.FlsError):
+        fl.write_image(cols, rowgroup=1024, path=tmp_path / "missing_dir" / "t.fls")
+    assert "cannot create" in fl.last_error()
