@@ -270,6 +270,7 @@ __device__ __forceinline__ void flush_ring(lu8 *ring, uint32_t ring_bytes, uint3
 // ============================================================================
 constexpr uint32_t kSegRingCap = 5120;             // decoded bytes per part of a round
 constexpr uint32_t kSegSlack = 2 * 16 * 8 + 16;    // a lane may write past its claimed end on a corrupt table
+
 // Per-wave LDS layout (bytes, 16-aligned): string offsets (SMALL: u16 x 1025;
 // else u32 x 1025), the tagged symbol table u64[256], 256 B kept free (the
 // occupancy the kernel was measured at: 16 waves per CU), the ring.  The
@@ -282,6 +283,7 @@ enum : int {
     kSegXInline = 1,   // records read a string's bytes 4..11 only for inline (<= 12-byte) strings
     kSegXNoPad = 2,    // no 256 B pad in the per-wave LDS (17 waves per CU instead of 16 for SMALL)
     kSegXSplit = 4,    // symbol table as two u32 arrays (low / high dwords): two b32 gathers per code
+    kSegXDouble = 8,   // two consecutive segments (32 code bytes) per lane per round: half the rounds
 };
 template <bool SMALL, int X = 0>
 struct SegLds {
@@ -289,7 +291,8 @@ struct SegLds {
     static constexpr uint32_t kOffSym = SMALL ? 2064 : 4112;
     static constexpr uint32_t kOffRing = kOffSym + 2048 + ((X & kSegXNoPad) ? 0 : 256);
     static constexpr uint32_t kPackedMax = SMALL ? 128 * 8 + 128 : 128 * 32 + 128;  // W <= 8 | 32, + zero row
-    static constexpr uint32_t kRing = kPackedMax > kSegRingCap + kSegSlack ? kPackedMax : kSegRingCap + kSegSlack;
+    static constexpr uint32_t kSlack = (X & kSegXDouble) ? 2 * 32 * 8 + 16 : kSegSlack;  // 32 codes per lane
+    static constexpr uint32_t kRing = kPackedMax > kSegRingCap + kSlack ? kPackedMax : kSegRingCap + kSlack;
     static constexpr uint32_t kWave = kOffRing + kRing;
     static_assert(kOffSym % 16 == 0 && kOffRing % 16 == 0 && kWave % 16 == 0, "LDS layout alignment");
 };
@@ -575,27 +578,39 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
     const bool vec_esc = (uni(shp->flags) & FSST_SEG_HAS_ESCAPE) != 0;
     if (uni(shp->nseg) != nseg) bad = true;
     gu8 *segv = a.vh + soff + sizeof(FsstSegHeader);
-    constexpr uint32_t kRoundCodes = 64 * 16;
+    // (experiment kSegXDouble: lane l decodes segments 2l and 2l + 1 of a round)
+    constexpr uint32_t SEGS = (X & kSegXDouble) ? 2 : 1;
+    constexpr uint32_t kRoundCodes = 64 * 16 * SEGS;
     const uint32_t n16 = (comp_len + 15) >> 4;
-    auto load_seg = [&](uint32_t r0) -> uint32_t {
-        const uint32_t k = (r0 >> 4) + lane;
+    auto load_seg = [&](uint32_t r0, uint32_t j) -> uint32_t {
+        const uint32_t k = (r0 >> 4) + SEGS * lane + j;
         return k < nseg ? (uint32_t)segv[k] : 0u;
     };
-    auto load_codes = [&](uint32_t r0) -> v4u {
-        const uint32_t k = (r0 >> 4) + lane;
+    auto load_codes = [&](uint32_t r0, uint32_t j) -> v4u {
+        const uint32_t k = (r0 >> 4) + SEGS * lane + j;
         return k < n16 ? comp[k] : mk4(0, 0, 0, 0);
     };
-    v4u raw_next = load_codes(0);
-    uint32_t sv_next = load_seg(0);
+    v4u raw_next = load_codes(0, 0), raw_next1 = mk4(0, 0, 0, 0);
+    uint32_t sv_next = load_seg(0, 0), sv_next1 = 0;
+    if constexpr (SEGS == 2) {
+        raw_next1 = load_codes(0, 1);
+        sv_next1 = load_seg(0, 1);
+    }
     for (uint32_t r0 = 0; r0 < comp_len; r0 += kRoundCodes) {
-        const uint32_t idx0 = r0 + 16 * lane;
-        const v4u raw = raw_next;
+        const uint32_t idx0 = r0 + 16 * SEGS * lane;
+        const v4u raw = raw_next, raw1 = raw_next1;
         // segment value: dlen (entry state 0) or 129 + dlen (state 1)
         const uint32_t entry = sv_next > 128 ? 1u : 0u;
-        const uint32_t dl = entry ? sv_next - 129 : sv_next;
+        const uint32_t dl0 = entry ? sv_next - 129 : sv_next;
+        const uint32_t entry1 = sv_next1 > 128 ? 1u : 0u;
+        const uint32_t dl = dl0 + (SEGS == 2 ? (entry1 ? sv_next1 - 129 : sv_next1) : 0u);
         if (r0 + kRoundCodes < comp_len) {
-            raw_next = load_codes(r0 + kRoundCodes);
-            sv_next = load_seg(r0 + kRoundCodes);
+            raw_next = load_codes(r0 + kRoundCodes, 0);
+            sv_next = load_seg(r0 + kRoundCodes, 0);
+            if constexpr (SEGS == 2) {
+                raw_next1 = load_codes(r0 + kRoundCodes, 1);
+                sv_next1 = load_seg(r0 + kRoundCodes, 1);
+            }
         }
         const bool full = r0 + kRoundCodes <= comp_len;
         // the previous round's stores, after this round's loads
@@ -620,9 +635,16 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
                 LeanWriter qw(ring, p0 + (incl - dl - done));
                 const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, 16u) : 0u;
                 constexpr bool kSplit = (X & kSegXSplit) != 0;
-                const uint32_t got = !full   ? seg_lane<false, true, kSplit>(sym, raw, nb, st, qw)
-                                     : vec_esc ? seg_lane<true, true, kSplit>(sym, raw, nb, st, qw)
-                                               : seg_lane<true, false, kSplit>(sym, raw, nb, st, qw);
+                uint32_t got = !full   ? seg_lane<false, true, kSplit>(sym, raw, nb, st, qw)
+                               : vec_esc ? seg_lane<true, true, kSplit>(sym, raw, nb, st, qw)
+                                         : seg_lane<true, false, kSplit>(sym, raw, nb, st, qw);
+                if constexpr (SEGS == 2) {
+                    const uint32_t nb1 = idx0 + 16 < comp_len ? min(comp_len - idx0 - 16, 16u) : 0u;
+                    if (got != dl0 || (nb1 > 0 && st != entry1)) bad = true;
+                    got = !full   ? seg_lane<false, true, kSplit>(sym, raw1, nb1, st, qw)
+                          : vec_esc ? seg_lane<true, true, kSplit>(sym, raw1, nb1, st, qw)
+                                    : seg_lane<true, false, kSplit>(sym, raw1, nb1, st, qw);
+                }
                 if (got != dl) bad = true;
                 qw.finish();
             }
@@ -635,9 +657,9 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
         }
         // a lane's exit state is the entry state of the segment after it
         const uint32_t nxt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 1) & 63) << 2), (int)entry);
-        if (lane < 63 && idx0 + 16 < comp_len && st != nxt) bad = true;
+        if (lane < 63 && idx0 + 16 * SEGS < comp_len && st != nxt) bad = true;
         if (lane == 0 && entry != carry_lit) bad = true;
-        carry_lit = rl(st, min(63u, (comp_len - 1 - r0) / 16));
+        carry_lit = rl(st, min(63u, (comp_len - 1 - r0) / (16 * SEGS)));
     }
     if (carry_lit) bad = true;  // stream ends inside an escape
     retire(true);
@@ -1009,7 +1031,7 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
 // register budgets: the segmented kernel 5 waves per SIMD (96 VGPRs, no
 // spill; its LDS admits 16 waves per CU), the code-parallel one 6 (80 VGPRs)
 template <Kind K, bool SMALL, bool QUEUE, int X = 0>
-__global__ __launch_bounds__(64, K == Kind::Seg ? 5 : 6) void fsst_kernel(const DevChunk *__restrict__ chunks,
+__global__ __launch_bounds__(64, K == Kind::Seg ? ((X & kSegXDouble) ? 4 : 5) : 6) void fsst_kernel(const DevChunk *__restrict__ chunks,
                                                                          uint32_t nchunks, uint32_t nitems,
                                                                          uint32_t *__restrict__ err,
                                                                          uint32_t *__restrict__ queue, uint32_t piece) {
@@ -1343,7 +1365,7 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
         if (variant == kFsstDefault) return true;  // the product build has each kernel's default only
 #ifdef FLS_EXPERIMENTS
         const int x = variant >> kSegXShift;
-        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && x >= 1 && x <= 7) return true;
+        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && (x >= 1 && x <= 9)) return true;
 #endif
     }
     return false;
@@ -1363,6 +1385,8 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     case 5: return launch_kind2<Kind::Seg, 5>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 6: return launch_kind2<Kind::Seg, 6>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 7: return launch_kind2<Kind::Seg, 7>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 8: return launch_kind2<Kind::Seg, 8>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 9: return launch_kind2<Kind::Seg, 9>(d_chunks, nchunks, nvecs, d_err, stream, how);
     default: break;
     }
 #endif
