@@ -312,6 +312,7 @@ struct Slot {                       // one batch of row groups in flight
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
+    PinBuf<uint32_t> h_err;         // the device error flags, copied after the batch's kernels
     // filtered batches (fls_scan_filter)
     DevBuf<uint64_t> d_mask;        // selection bits, 16 words per 1024-row vector
     DevBuf<uint32_t> d_counts;      // selected rows per vector
@@ -1265,6 +1266,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         for (auto &sl : d.slots) {
             if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
             if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+            HIP_TRY(sl.h_err.alloc(1));
             sl.d_out.resize(ncols);
         }
         // contiguous shard of the surviving row groups
@@ -1684,6 +1686,10 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         if (sl.heap_bytes[c])
             HIP_TRY(hipMemcpyAsync(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
     }
+    // the error flags ride along (sticky device flags: a batch sees its own
+    // kernels' and any earlier ones'), so an acquire reads pinned memory
+    // instead of a synchronous 4-byte copy per row group
+    HIP_TRY(hipMemcpyAsync(sl.h_err.p, d.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.stream));
     HIP_TRY(hipEventRecord(sl.done, sl.stream));
     hb.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
     hb.valid_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
@@ -1834,8 +1840,7 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     auto wait_batch = [&]() -> int {
         HIP_TRY(hipSetDevice(d.dev));
         HIP_TRY(hipEventSynchronize(sl.done));
-        uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, d.err.p, sizeof(err), hipMemcpyDeviceToHost));
+        const uint32_t err = *(volatile const uint32_t *)sl.h_err.p;
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
         if (err & KERR_NARROW)
             return fail(FLS_ERR_FORMAT, "corrupt chunk: a value outside its zone map in a narrowed column (flags 0x%x)", err);
