@@ -1840,22 +1840,7 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     Slot &sl = d.slots[si];
     auto wait_batch = [&]() -> int {
         HIP_TRY(hipSetDevice(d.dev));
-        // FLS_SCAN_WAIT (A/B knob): 0 = hipEventSynchronize (the runtime's
-        // wait), 1 = poll and yield, 2 = poll and sleep 20 us -- a waiting
-        // consumer thread then leaves its CPU to the others
-        const char *wm = getenv("FLS_SCAN_WAIT");
-        const int wait_mode = wm ? atoi(wm) : 0;
-        if (wait_mode == 0) {
-            HIP_TRY(hipEventSynchronize(sl.done));
-        } else {
-            for (;;) {
-                const hipError_t q = hipEventQuery(sl.done);
-                if (q == hipSuccess) break;
-                if (q != hipErrorNotReady) HIP_TRY(q);
-                if (wait_mode == 1) std::this_thread::yield();
-                else std::this_thread::sleep_for(std::chrono::microseconds(20));
-            }
-        }
+        HIP_TRY(hipEventSynchronize(sl.done));
         const uint32_t err = *(volatile const uint32_t *)sl.h_err.p;
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
         if (err & KERR_NARROW)
