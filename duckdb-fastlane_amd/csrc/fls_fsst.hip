@@ -199,6 +199,7 @@ __device__ __forceinline__ void stage_packed(lv4 *P, gu8 *packed, uint32_t W, ui
 // selector byte j is sh + j (a byte of the dword pair) while 4k + j < n, else
 // 12 (a zero byte); the bytes at or past the length come from a 64-bit shift
 // of ones by 8 x clamp(n - 4k, 0, 4) (amounts 0..32, no wrap).
+template <bool SEL = false>
 __device__ __forceinline__ v4u make_record(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t sh,
                                            uint32_t n, uint64_t p) {
     const uint32_t base = 0x03020100u + sh * 0x01010101u, t = 8 * n;
@@ -209,6 +210,12 @@ __device__ __forceinline__ v4u make_record(uint32_t w0, uint32_t w1, uint32_t w2
         return __builtin_amdgcn_perm(hi, lo, sel);
     };
     const bool inl = n <= 12;
+    if constexpr (SEL) {  // (experiment kSegXRecSel) both forms computed, picked by bit select: no branch
+        const uint32_t m = 0u - (uint32_t)inl;
+        uint32_t a = word(w2, w1, 1), b = word(w3, w2, 2);
+        asm volatile("" : "+v"(a), "+v"(b));
+        return mk4(n, word(w1, w0, 0), (a & m) | ((uint32_t)p & ~m), (b & m) | ((uint32_t)(p >> 32) & ~m));
+    }
     return mk4(n, word(w1, w0, 0), inl ? word(w2, w1, 1) : (uint32_t)p, inl ? word(w3, w2, 2) : (uint32_t)(p >> 32));
 }
 
@@ -217,12 +224,36 @@ __device__ __forceinline__ v4u make_record(uint32_t w0, uint32_t w1, uint32_t w2
 // ring stays zero past the decoded bytes).  Up to 4 blocks per lane per pass,
 // all ring reads in flight before the zeroing and the heap stores.  A block
 // past the vector's heap window is refused (bad).
+template <bool UNIFORM = false>
 __device__ __forceinline__ void flush_ring(lu8 *ring, uint32_t ring_bytes, uint32_t ring_base, uint32_t upto,
                                            const VecHeap &h, uint32_t lane, bool &bad) {
     // (a ring never holds more than ring_bytes: the clamp bounds the loop
     // whatever a corrupt stream did to the positions)
     const uint32_t nblk = min((upto - ring_base) >> 4, ring_bytes / 16);
     lv4 *r16 = reinterpret_cast<lv4 *>(ring);
+    if constexpr (UNIFORM) {
+        // (experiment kSegXFlush) every block inside the heap window, checked
+        // once for the wave: no per-block bound test
+        if (ring_base + 16 * nblk <= h.hlim) {
+            for (uint32_t q0 = 0; q0 < nblk; q0 += 256) {
+                v4u b[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t q = q0 + 64 * j + lane;
+                    b[j] = q < nblk ? r16[q] : mk4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t q = q0 + 64 * j + lane;
+                    if (q < nblk) {
+                        r16[q] = mk4(0, 0, 0, 0);
+                        *reinterpret_cast<ov4 *>(h.heap + ring_base + 16 * q) = b[j];
+                    }
+                }
+            }
+            return;
+        }
+    }
     for (uint32_t q0 = 0; q0 < nblk; q0 += 256) {
         v4u b[4];
 #pragma unroll
@@ -284,6 +315,8 @@ enum : int {
     kSegXNoPad = 2,    // no 256 B pad in the per-wave LDS (17 waves per CU instead of 16 for SMALL)
     kSegXSplit = 4,    // symbol table as two u32 arrays (low / high dwords): two b32 gathers per code
     kSegXDouble = 8,   // two consecutive segments (32 code bytes) per lane per round: half the rounds
+    kSegXFlush = 16,   // ring flush bound-checked once per wave instead of per block
+    kSegXRecSel = 32,  // string_t records: inline and pointer words both computed, bit-selected (no branch)
 };
 template <bool SMALL, int X = 0>
 struct SegLds {
@@ -535,7 +568,7 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
                     w3 = r32[i0 + 3];
                 }
                 *reinterpret_cast<ov4 *>(a.out + 16ull * i) =
-                    make_record(r32[i0], r32[i0 + 1], w2, w3, x & 3, n, h.ptr_base + d0);
+                    make_record<(X & kSegXRecSel) != 0>(r32[i0], r32[i0 + 1], w2, w3, x & 3, n, h.ptr_base + d0);
             }
             if (n_ok > 0) str_base += rl(rel1, n_ok - 1);
             next_str += n_ok;
@@ -550,7 +583,7 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
         records(force);
         const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
         const uint32_t new_base = keep_from & ~15u;
-        flush_ring(ring, Layout::kRing, ring_base, new_base, h, lane, bad);
+        flush_ring<(X & kSegXFlush) != 0>(ring, Layout::kRing, ring_base, new_base, h, lane, bad);
         wave_sync();
         const uint32_t src = min(new_base - ring_base, Layout::kRing);
         const uint32_t len = min((out_pos - new_base + 15) & ~15u, Layout::kRing - 16);
@@ -1365,7 +1398,7 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
         if (variant == kFsstDefault) return true;  // the product build has each kernel's default only
 #ifdef FLS_EXPERIMENTS
         const int x = variant >> kSegXShift;
-        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && (x >= 1 && x <= 9)) return true;
+        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48)) return true;
 #endif
     }
     return false;
@@ -1387,6 +1420,9 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     case 7: return launch_kind2<Kind::Seg, 7>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 8: return launch_kind2<Kind::Seg, 8>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 9: return launch_kind2<Kind::Seg, 9>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 16: return launch_kind2<Kind::Seg, 16>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 32: return launch_kind2<Kind::Seg, 32>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 48: return launch_kind2<Kind::Seg, 48>(d_chunks, nchunks, nvecs, d_err, stream, how);
     default: break;
     }
 #endif

@@ -40,7 +40,15 @@ def main():
     img = fl.gen_image(a.workload, a.scale, a.rows)
     t = fl.Connection([0]).read_image(img)
     t.device_upload()
-    sels = [None if c == "all" else [int(c)] for c in a.cols.split(",")]
+    # a selection: "all", one column, or columns joined by "+" ("0-14": a range)
+    def parse_sel(c):
+        if c == "all":
+            return None
+        if "-" in c:
+            lo, hi = map(int, c.split("-"))
+            return list(range(lo, hi + 1))
+        return [int(x) for x in c.split("+")]
+    sels = [parse_sel(c) for c in a.cols.split(",")]
     res = {}
     any_bad = False
 
@@ -59,7 +67,7 @@ def main():
                     os.environ[k] = v
 
     for sel in sels:
-        key = "ALL" if sel is None else t.schema()[sel[0]][0]
+        key = "ALL" if sel is None else t.schema()[sel[0]][0] if len(sel) == 1 else f"cols{sel[0]}-{sel[-1]}"
         times = {n: [] for n, _ in arms}
         for n, env in arms:  # warm (and build each arm's descriptor order once)
             run(env, sel, 1)
