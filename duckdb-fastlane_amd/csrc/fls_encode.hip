@@ -46,6 +46,7 @@
 #include "fls_common.hpp"
 #include "fls_decode.hpp"
 #include "fls_encode.hpp"
+#include "fls_alp.hpp"
 #include "fls_format.hpp"
 #include "fls_unpack.hpp"
 
@@ -663,6 +664,7 @@ __global__ __launch_bounds__(256, sizeof(S) == 8 ? 4 : FLS_ENC_NARROW_WAVES) voi
     FLS_LDS int64_t *B = (FLS_LDS int64_t *)Bv;
     FLS_LDS uint64_t *O = (FLS_LDS uint64_t *)Ov;
     uint8_t enc = c.enc;
+    if (enc == ENC_ALP) return;  // alp_encode_kernel
     if (enc == ENC_AUTO) {
         if constexpr (sizeof(S) == 8) {
             enc = choose_encoding<64>(c, V, O);
@@ -733,6 +735,335 @@ __global__ __launch_bounds__(256, 2) void encode_rle_kernel(const EncChunk *__re
     }
 }
 
+
+
+// ============================================================================
+// ALP chunks of FLOAT / DOUBLE columns (fls_writer.cpp enc_alp, byte for
+// byte).  One 256-thread block per chunk:
+//   1. the chunk's (e, f) candidates: min(8, nvec) sampled vectors (32
+//      values each) score every e <= kMaxE, f <= e by the CPU's cost
+//      (bit width of the encoded range x samples + exceptions x (16 + T)),
+//      each votes for its first cheapest; the up to five most-voted (ties to
+//      the lower e (kMaxE + 1) + f, as the CPU's stable sort) are kept;
+//   2. per vector (a wave each): the cheapest candidate on its own sample,
+//      every value encoded (d = rint(n 10^e 10^-f), kept when d 10^f 10^-e
+//      gives n's bits back), exceptions replaced by the first encoded value,
+//      FOR base and width; then the layout (packed rows, 16-aligned aux
+//      blocks of u16 positions + original values), and a second pass that
+//      writes each vector at its place.
+// The arithmetic is the CPU's, operation for operation, in the value's own
+// precision (no contraction: products only), so the same values encode and
+// the file is the CPU writer's.  Compute-light, HBM-bound (T/8 bytes read
+// twice per value, the chunk written once).
+// ============================================================================
+__constant__ double kAlpF10D[kAlpMaxExpD + 1] = {FLS_ALP_F10_D};
+__constant__ double kAlpIF10D[kAlpMaxExpD + 1] = {FLS_ALP_IF10_D};
+__constant__ float kAlpF10F[kAlpMaxExpF + 1] = {FLS_ALP_F10_F};
+__constant__ float kAlpIF10F[kAlpMaxExpF + 1] = {FLS_ALP_IF10_F};
+
+template <class F>
+struct AlpDev;
+template <>
+struct AlpDev<double> {
+    using I = int64_t;
+    using U = uint64_t;
+    static constexpr int T = 64, kMaxE = kAlpMaxExpD;
+    __device__ static double f10(int e) { return kAlpF10D[e]; }
+    __device__ static double if10(int e) { return kAlpIF10D[e]; }
+    __device__ static bool in_range(double x) { return __builtin_fabs(x) < 9.2233720368547748e18; }
+    __device__ static I round(double x) { return (I)__builtin_rint(x); }
+    __device__ static U bits(double x) { return (U)__double_as_longlong(x); }
+    __device__ static double from_bits(U u) { return __longlong_as_double((long long)u); }
+};
+template <>
+struct AlpDev<float> {
+    using I = int32_t;
+    using U = uint32_t;
+    static constexpr int T = 32, kMaxE = kAlpMaxExpF;
+    __device__ static float f10(int e) { return kAlpF10F[e]; }
+    __device__ static float if10(int e) { return kAlpIF10F[e]; }
+    __device__ static bool in_range(float x) { return __builtin_fabsf(x) < 2.1474835e9f; }
+    __device__ static I round(float x) { return (I)__builtin_rintf(x); }
+    __device__ static U bits(float x) { return (U)__float_as_uint(x); }
+    __device__ static float from_bits(U u) { return __uint_as_float(u); }
+};
+// fls_writer.cpp alp_encode_one: n * 10^e * 10^-f rounded, verified bit-exact
+template <class F>
+__device__ __forceinline__ bool alp_enc1(F n, int e, int f, typename AlpDev<F>::I &d) {
+    using A = AlpDev<F>;
+    const F tmp = n * A::f10(e) * A::if10(f);
+    if (!A::in_range(tmp)) return false;  // also NaN / inf
+    d = A::round(tmp);
+    const F back = (F)d * A::f10(f) * A::if10(e);
+    return A::bits(back) == A::bits(n);
+}
+__device__ __forceinline__ uint32_t bitlen_u64(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+// (e, f) of combination index k in the CPU's loop order (e outer, f <= e inner)
+__device__ __forceinline__ void alp_combo(uint32_t k, int &e, int &f) {
+    int x = 0;
+    while ((uint32_t)((x + 1) * (x + 2) / 2) <= k) ++x;
+    e = x;
+    f = (int)k - x * (x + 1) / 2;
+}
+// alp_cost over the wave's lanes < sn (one sample each): every lane gets the cost
+template <class F>
+__device__ __forceinline__ uint64_t alp_cost_wave(F x, bool have, uint32_t sn, int e, int f) {
+    using A = AlpDev<F>;
+    typename A::I d = 0;
+    const bool ok = have && alp_enc1<F>(x, e, f, d);
+    int64_t mn = ok ? (int64_t)d : INT64_MAX, mx = ok ? (int64_t)d : INT64_MIN;
+    wave_minmax_i64(mn, mx);
+    const uint32_t exc = (uint32_t)__popcll(__ballot(have && !ok));
+    const uint64_t range = mn <= mx ? (uint64_t)((typename A::U)(typename A::I)mx - (typename A::U)(typename A::I)mn) : 0u;
+    return (uint64_t)bitlen_u64(range) * sn + (uint64_t)exc * (16u + A::T);
+}
+constexpr uint32_t kAlpSampleVecs = 8, kAlpSamples = 32, kAlpCombos = 5;
+constexpr uint32_t kAlpNcD = (kAlpMaxExpD + 1) * (kAlpMaxExpD + 2) / 2;  // 190 (e, f) pairs
+
+template <class F>
+__device__ void alp_chunk(const EncChunk &c, uint64_t *lds_v, uint64_t *lds_cost, uint32_t *lds_votes,
+                          uint32_t *Wv, int64_t *Bv, uint64_t *Ov, int *combo) {
+    using A = AlpDev<F>;
+    using I = typename A::I;
+    using U = typename A::U;
+    constexpr int T = A::T, M = A::kMaxE;
+    constexpr uint32_t NC = (M + 1) * (M + 2) / 2;
+    using S = Sto<T>;
+    const uint32_t lane = threadIdx.x & 63, w = wave_index();
+    const uint32_t n = c.nrows, nvec = (n + kVectorSize - 1) / kVectorSize;
+    const FLS_GLOBAL U *in = (const FLS_GLOBAL U *)c.in;
+    FLS_GLOBAL uint8_t *out = (FLS_GLOBAL uint8_t *)c.out;
+    // ---- 1. candidates: sampled vectors score every (e, f)
+    const uint32_t nsv = min(kAlpSampleVecs, nvec);
+    for (uint32_t t = threadIdx.x; t < nsv * NC; t += blockDim.x) {
+        const uint32_t k = t / NC, ci = t % NC;
+        const uint32_t v = (uint32_t)((uint64_t)k * nvec / nsv), b = v * kVectorSize;
+        const uint32_t vn = min(kVectorSize, n - b), sn = min(kAlpSamples, vn);
+        int e, f;
+        alp_combo(ci, e, f);
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+        uint32_t exc = 0;
+        for (uint32_t i = 0; i < sn; ++i) {
+            const F x = A::from_bits(in[b + (uint64_t)i * vn / sn]);
+            I d;
+            if (!alp_enc1<F>(x, e, f, d)) { ++exc; continue; }
+            mn = (int64_t)d < mn ? (int64_t)d : mn;
+            mx = (int64_t)d > mx ? (int64_t)d : mx;
+        }
+        const uint64_t range = mn <= mx ? (uint64_t)((U)(I)mx - (U)(I)mn) : 0u;
+        lds_cost[k * kAlpNcD + ci] = (uint64_t)bitlen_u64(range) * sn + (uint64_t)exc * (16u + T);
+    }
+    for (uint32_t i = threadIdx.x; i < (M + 1) * (M + 1); i += blockDim.x) lds_votes[i] = 0;
+    __syncthreads();
+    if (threadIdx.x < nsv) {  // each sampled vector votes for its first cheapest
+        uint64_t best = UINT64_MAX;
+        uint32_t bi = 0;
+        for (uint32_t ci = 0; ci < NC; ++ci) {
+            const uint64_t x = lds_cost[threadIdx.x * kAlpNcD + ci];
+            if (x < best) { best = x; bi = ci; }
+        }
+        int e, f;
+        alp_combo(bi, e, f);
+        atomicAdd(&lds_votes[e * (M + 1) + f], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the most voted, ties to the lower index (stable sort)
+        int nc = 0;
+        for (; nc < (int)kAlpCombos; ++nc) {
+            uint32_t bv = 0, bi = 0;
+            for (uint32_t i = 0; i < (M + 1) * (M + 1); ++i)
+                if (lds_votes[i] > bv) { bv = lds_votes[i]; bi = i; }
+            if (bv == 0) break;
+            combo[1 + nc] = (int)bi;
+            lds_votes[bi] = 0;
+        }
+        if (nc == 0) { combo[1] = 0; nc = 1; }
+        combo[0] = nc;
+    }
+    __syncthreads();
+    const int ncombo = combo[0];
+    FLS_LDS S *V = (FLS_LDS S *)lds_v + w * kVectorSize;
+    // one vector: its (e, f), every value's d in V (exceptions replaced by the
+    // first encoded value, the tail by the last), the exception bits per row k
+    auto encode_vec = [&](uint32_t v, int &e, int &f, uint64_t (&excm)[16]) {
+        const uint32_t b = v * kVectorSize, vn = min(kVectorSize, n - b);
+        e = combo[1] / (M + 1);
+        f = combo[1] % (M + 1);
+        if (ncombo > 1) {  // level 2: the cheapest candidate on this vector's sample
+            const uint32_t sn = min(kAlpSamples, vn);
+            const bool have = lane < sn;
+            const F x = have ? A::from_bits(in[b + (uint64_t)lane * vn / sn]) : (F)0;
+            uint64_t best = UINT64_MAX;
+            for (int k = 0; k < ncombo; ++k) {
+                const int ek = combo[1 + k] / (M + 1), fk = combo[1 + k] % (M + 1);
+                const uint64_t cst = alp_cost_wave<F>(x, have, sn, ek, fk);
+                if (cst < best) { best = cst; e = ek; f = fk; }
+            }
+        }
+        uint32_t first = kVectorSize;  // first encoded index of this lane
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t i = lane + 64 * k;
+            I d = 0;
+            const bool ok = i < vn && alp_enc1<F>(A::from_bits(in[b + i]), e, f, d);
+            excm[k] = __ballot(i < vn && !ok);
+            if (ok && i < first) first = i;
+            V[i] = (S)(U)d;
+        }
+        for (int o = 32; o >= 1; o >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, o, 64));
+        wave_sync();
+        const S fill = first < kVectorSize ? V[first] : (S)0;
+        wave_sync();
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k)
+            if ((excm[k] >> lane) & 1ull) V[lane + 64 * k] = fill;
+        wave_sync();
+        const S last = V[vn - 1];
+        for (uint32_t i = vn + lane; i < kVectorSize; i += 64) V[i] = last;
+        wave_sync();
+    };
+    // ---- 2a. per vector: (e, f), exceptions, FOR base and width
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        int e, f;
+        uint64_t excm[16];
+        encode_vec(v, e, f, excm);
+        S x[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) x[k] = V[lane + 64 * k];
+        const VecStat st = analyze_regs<T>(x);
+        uint32_t npos = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) npos += (uint32_t)__popcll(excm[k]);
+        if (lane == 0) {
+            Wv[v] = st.W;
+            Bv[v] = st.base;
+            Ov[v] = (uint64_t)npos | ((uint64_t)e << 16) | ((uint64_t)f << 24);
+        }
+        wave_sync();
+    }
+    __syncthreads();
+    // ---- layout (assemble_chunk): packed rows back to back; the aux blocks of
+    // vectors with exceptions, each 16-aligned; aux_len ends at the last block
+    const uint64_t meta_off = sizeof(ChunkHeader);
+    const uint64_t packed_off = (meta_off + sizeof(VecMeta) * nvec + 15) & ~15ull;
+    const uint32_t pw = lane < nvec ? 128u * Wv[lane] : 0u;
+    const uint32_t npos_l = lane < nvec ? (uint32_t)(Ov[lane] & 0xFFFF) : 0u;
+    // this vector's aux block (fls_format.hpp alp_aux_bytes)
+    const uint32_t sz = npos_l ? ((2u * npos_l + 15u) & ~15u) + npos_l * (uint32_t)(T / 8) : 0u;
+    const uint32_t va = (sz + 15) & ~15u;
+    uint32_t pincl = pw, aincl = va;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(pincl, d, 64), z = __shfl_up(aincl, d, 64);
+        if (lane >= d) { pincl += y; aincl += z; }
+    }
+    const uint32_t poff = pincl - pw, aoff = aincl - va;
+    const uint64_t packed_total = __shfl(pincl, 63, 64);
+    const uint64_t aux_off = (packed_off + packed_total + 15) & ~15ull;
+    uint32_t aend = npos_l ? aoff + sz : 0u;
+    for (int o = 32; o >= 1; o >>= 1) aend = max(aend, (uint32_t)__shfl_xor((int)aend, o, 64));
+    const uint64_t aux_len = aend;
+    const uint64_t total = (aux_off + aux_len + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
+    if (w == 0) {
+        if (lane < nvec) {
+            VecMeta m;
+            m.packed_off = poff;
+            m.for_base = Bv[lane];
+            m.aux_off = npos_l ? aoff : 0u;
+            m.nvals = (uint16_t)min(kVectorSize, n - lane * kVectorSize);
+            m.bw = (uint8_t)Wv[lane];
+            m.pad = 0;
+            m.aux_count = (uint32_t)Ov[lane];
+            const uint32_t *mw = reinterpret_cast<const uint32_t *>(&m);
+            FLS_GLOBAL uint32_t *dm = reinterpret_cast<FLS_GLOBAL uint32_t *>(out + meta_off + sizeof(VecMeta) * lane);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dm[i] = mw[i];
+        }
+        if (lane == 0) {
+            ChunkHeader h;
+            h.magic = kChunkMagic;
+            h.enc = ENC_ALP;
+            h.T = (uint8_t)T;
+            h.vbits = (uint8_t)T;
+            h.is_str = 0;
+            h.nvec = nvec;
+            h.nvals = n;
+            h.meta_off = meta_off;
+            h.packed_off = packed_off;
+            h.aux_off = aux_off;
+            h.aux_len = aux_len;
+            h.dict_count = 0;
+            h.reserved0 = 0;
+            h.reserved1 = 0;
+            const uint32_t *hw = reinterpret_cast<const uint32_t *>(&h);
+            FLS_GLOBAL uint32_t *dh = reinterpret_cast<FLS_GLOBAL uint32_t *>(out);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dh[i] = hw[i];
+            *(FLS_GLOBAL uint64_t *)c.len_out = total | (uint64_t)ENC_ALP << kEncShift;
+        }
+    }
+    // ---- 2b. every vector at its place: exceptions (positions, original
+    // values), the packed d - base, the zero gaps of its aux block
+    for (uint32_t v = w; v < nvec; v += kEncWaves) {
+        int e, f;
+        uint64_t excm[16];
+        encode_vec(v, e, f, excm);
+        const uint32_t b = v * kVectorSize;
+        const uint32_t p_off = __shfl(poff, v, 64), a_off = __shfl(aoff, v, 64);
+        const uint32_t npos = __shfl(npos_l, v, 64), vsz = __shfl(sz, v, 64);
+        if (npos) {
+            FLS_GLOBAL uint8_t *aux = out + aux_off + a_off;
+            const uint32_t voff = (2u * npos + 15) & ~15u;
+            uint32_t before = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) {
+                const uint64_t m = excm[k];
+                if ((m >> lane) & 1ull) {
+                    const uint32_t r = before + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                    const uint32_t i = lane + 64 * k;
+                    *(FLS_GLOBAL uint16_t *)(aux + 2 * r) = (uint16_t)i;
+                    *(FLS_GLOBAL U *)(aux + voff + (size_t)r * sizeof(F)) = in[b + i];
+                }
+                before += (uint32_t)__popcll(m);
+            }
+            for (uint32_t j = 2 * npos + lane; j < voff; j += 64) aux[j] = 0;   // positions' padding
+            // up to the next vector's aux block (16-aligned)
+            const uint32_t a_next = (a_off + vsz + 15) & ~15u;
+            if (lane < a_next - (a_off + vsz) && a_off + vsz < aux_len) aux[vsz + lane] = 0;
+        }
+        const VecStat st{Bv[v], Wv[v]};
+        S u[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) u[k] = (S)((uint64_t)V[lane + 64 * k] - (uint64_t)st.base) & (S)tmask_d(T);
+        wave_sync();
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) V[lane + 64 * k] = u[k];
+        wave_sync();
+        pack_vector<T>(V, st.W, out + packed_off + p_off, lane);
+        wave_sync();
+    }
+    // header / meta / packed / aux gaps
+    {
+        const uint64_t gaps[3][2] = {{meta_off + sizeof(VecMeta) * nvec, packed_off},
+                                     {packed_off + packed_total, aux_off},
+                                     {aux_off + aux_len, total}};
+        for (int g = 0; g < 3; ++g)
+            for (uint64_t q = gaps[g][0] + threadIdx.x; q < gaps[g][1]; q += blockDim.x) out[q] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void alp_encode_kernel(const EncChunk *__restrict__ chunks) {
+    __shared__ uint64_t Vall[kEncWaves * kVectorSize];
+    __shared__ uint64_t cost[kAlpSampleVecs * kAlpNcD];
+    __shared__ uint32_t votes[(kAlpMaxExpD + 1) * (kAlpMaxExpD + 1)];
+    __shared__ uint32_t Wv[64];
+    __shared__ int64_t Bv[64];
+    __shared__ uint64_t Ov[64];
+    __shared__ int combo[1 + kAlpCombos];
+    const EncChunk c = chunks[blockIdx.x];
+    if (c.enc != ENC_ALP) return;
+    if (c.T == 64) alp_chunk<double>(c, Vall, cost, votes, Wv, Bv, Ov, combo);
+    else alp_chunk<float>(c, Vall, cost, votes, Wv, Bv, Ov, combo);
+}
 
 // ============================================================================
 // DICT chunks of integer columns (fls_writer.cpp enc_dict_int, byte for byte):
@@ -1253,6 +1584,9 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
     const uint64_t rle = packed_off + 128ull * 16 * nvec + nvec * ((128ull + 1024ull * (T / 8) + 15) & ~15ull);
     // DICT: codes of at most 16 bits (65,536 distinct values) FFOR-packed at T = 32, the dictionary
     const uint64_t dict = packed_off + 128ull * 17 * nvec + (((uint64_t)nrows * (T / 8) + 15) & ~15ull);
+    // ALP: W <= T, and at most every value an exception (16-aligned aux blocks)
+    const uint64_t alp = packed_off + 128ull * T * nvec + nvec * ((alp_aux_bytes(kVectorSize, T) + 15) & ~15ull);
+    if (enc == ENC_ALP) return (alp + kChunkAlign - 1) & ~(uint64_t)(kChunkAlign - 1);
     const uint64_t need = enc == ENC_RLE    ? rle
                           : enc == ENC_AUTO ? std::max({delta, rle, dict})  // AUTO may pick any
                           : enc == ENC_DICT ? dict
@@ -1261,7 +1595,9 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc) {
 }
 
 hipError_t launch_encode(EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle,
-                         bool dict) {
+                         bool dict, bool alp) {
+    if (alp && n_wide + n_narrow)
+        hipLaunchKernelGGL(alp_encode_kernel, dim3(n_wide + n_narrow), dim3(256), 0, stream, d_chunks);
     if (dict && n_wide + n_narrow)
         hipLaunchKernelGGL(dict_analyze_kernel, dim3(n_wide + n_narrow), dim3(256), 0, stream, d_chunks);
     if (n_wide) hipLaunchKernelGGL(encode_kernel<uint64_t>, dim3(n_wide), dim3(64 * kEncWaves), 0, stream, d_chunks, n_wide);

@@ -53,8 +53,9 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // rle: some chunk is ENC_RLE or ENC_AUTO (encode_rle_kernel follows).
 // dict: some chunk is ENC_DICT or ENC_AUTO with a dict_tab (dict_analyze_kernel
 // runs first, dict_encode_kernel after).  d_chunks is written (est_dict).
+// alp: some chunk is ENC_ALP (FLOAT T = 32 / DOUBLE T = 64: alp_encode_kernel).
 hipError_t launch_encode(EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle,
-                         bool dict = false);
+                         bool dict = false, bool alp = false);
 
 // GPU FSST compression (writer side of ENC_FSST chunks; fls_writer.cpp
 // enc_fsst).  The host builds the chunk's symbol table from its sample

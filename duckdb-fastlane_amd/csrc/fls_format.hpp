@@ -279,7 +279,24 @@ inline ZoneMap zone_of_ints(const I *v, uint32_t n) {
     return z;
 }
 inline ZoneMap zone_of_typed(uint8_t type, const void *data, uint32_t n) {
-    if (n == 0 || type_is_float(type) || type_value_bits(type) == 0) return ZoneMap{0, 0, 0, 0};
+    if (n == 0 || type_value_bits(type) == 0) return ZoneMap{0, 0, 0, 0};
+    if (type_is_float(type)) {  // zone_of's rule (NaN flags, one canonical zero) over the typed values
+        ZoneMap z{0, 0, ZM_VALID, 0};
+        bool any = false;
+        double mn = 0, mx = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            double d = type_value_bits(type) == 32 ? (double)((const float *)data)[i] : ((const double *)data)[i];
+            if (d != d) { z.flags |= ZM_HAS_NAN; continue; }
+            if (d == 0) d = 0.0;
+            if (!any || d < mn) mn = d;
+            if (!any || d > mx) mx = d;
+            any = true;
+        }
+        if (!any) z.flags |= ZM_ALL_NAN;
+        __builtin_memcpy(&z.min, &mn, 8);
+        __builtin_memcpy(&z.max, &mx, 8);
+        return z;
+    }
     const bool sg = type_is_signed(type);
     switch (type_value_bits(type)) {
     case 8: return sg ? zone_of_ints((const int8_t *)data, n) : zone_of_ints((const uint8_t *)data, n);

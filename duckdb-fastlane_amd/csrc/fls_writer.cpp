@@ -1817,14 +1817,24 @@ struct GpuEncoder {
         return !(e && atoi(e) == 0);
     }
     static bool dict_job(uint8_t enc) { return (enc == ENC_DICT || enc == ENC_AUTO) && dict_gpu(); }
+    // ALP chunks of FLOAT / DOUBLE columns on the GPU (FLS_WRITER_ALP_GPU=0:
+    // on the host threads)
+    static bool alp_gpu() {
+        const char *e = getenv("FLS_WRITER_ALP_GPU");
+        return !(e && atoi(e) == 0);
+    }
+    // the encoding a job asks the kernels for: FLOAT / DOUBLE columns are ALP
+    // (ENC_AUTO included, as encode_int_chunk does)
+    static uint8_t job_enc(const ColSpec &cs) { return type_is_float(cs.type) ? (uint8_t)ENC_ALP : cs.enc; }
     static void need(const std::vector<ColSpec> &specs, const std::vector<size_t> &cols, uint32_t nrows,
                      uint64_t &in_rg, uint64_t &out_rg, uint64_t &dict_rg) {
         in_rg = out_rg = dict_rg = 0;
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
+            const uint8_t enc = job_enc(specs[c]);
             in_rg += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
-            out_rg += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
-            if (dict_job(specs[c].enc)) dict_rg += (enc_dict_tab_bytes(nrows) + 255) & ~255ull;
+            out_rg += enc_slot_bytes((uint32_t)T, nrows, enc);
+            if (dict_job(enc)) dict_rg += (enc_dict_tab_bytes(nrows) + 255) & ~255ull;
         }
     }
     // Whether add() would take this row group into the current set without
@@ -1868,15 +1878,16 @@ struct GpuEncoder {
         const size_t j0 = b->jobs.size();
         for (size_t c : cols) {
             const int T = type_value_bits(specs[c].type);
-            Job jb{rg, c, b->in_used, b->out_used, nrows, (uint8_t)T, specs[c].enc};
-            if (dict_job(specs[c].enc)) {
+            const uint8_t enc = job_enc(specs[c]);
+            Job jb{rg, c, b->in_used, b->out_used, nrows, (uint8_t)T, enc};
+            if (dict_job(enc)) {
                 jb.dict_off = b->dict_used;
                 b->dict_used += (enc_dict_tab_bytes(nrows) + 255) & ~255ull;
             }
             b->jobs.push_back(jb);
             stage[c] = b->h_stage + b->in_used;
             b->in_used += ((uint64_t)nrows * (T / 8) + 15) & ~15ull;
-            b->out_used += enc_slot_bytes((uint32_t)T, nrows, specs[c].enc);
+            b->out_used += enc_slot_bytes((uint32_t)T, nrows, enc);
         }
         for (size_t k = 0; k < cols.size(); ++k) est_dict[cols[k]] = &b->jobs[j0 + k].est_dict;
         ++b->batched;  // the caller submits a full set once this row group is in rgs
@@ -1910,12 +1921,13 @@ struct GpuEncoder {
             (uint32_t)(std::stable_partition(first, last, [](const EncChunk &c) { return c.T == 64; }) - first);
         WHIP(hipMemcpyAsync(b.d_in, b.h_stage, b.in_used, hipMemcpyHostToDevice, stream));
         WHIP(hipMemcpyAsync(b.d_desc, b.h_desc, b.jobs.size() * sizeof(EncChunk), hipMemcpyHostToDevice, stream));
-        bool rle = false, dict = false;
+        bool rle = false, dict = false, alp = false;
         for (const Job &jb : b.jobs) {
             rle |= jb.enc == ENC_RLE || jb.enc == ENC_AUTO;
             dict |= jb.dict_off != UINT64_MAX;
+            alp |= jb.enc == ENC_ALP;
         }
-        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream, rle, dict));
+        WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream, rle, dict, alp));
         WHIP(hipMemcpyAsync(b.h_lens, b.d_lens, b.jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         // the slots come back in one pinned copy (slots are sized for W = T,
         // so this moves more than the chunks hold, but one large copy beats
@@ -2178,15 +2190,19 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             }
         }
     }
-    // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA / RLE / AUTO
+    // GPU-encoded columns (fls_writer_set_device): integer FFOR / DELTA / RLE /
+    // DICT / AUTO, FLOAT / DOUBLE (ALP)
     std::vector<size_t> gcols;
     if (w->gpu.dev >= 0)
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
-            if (!type_is_string(cs.type) && !type_is_float(cs.type) &&
-                (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO ||
-                 (cs.enc == ENC_DICT && GpuEncoder::dict_gpu())))
+            if (type_is_float(cs.type)) {
+                if (GpuEncoder::alp_gpu()) gcols.push_back(c);
+            } else if (!type_is_string(cs.type) &&
+                       (cs.enc == ENC_FFOR || cs.enc == ENC_DELTA || cs.enc == ENC_RLE || cs.enc == ENC_AUTO ||
+                        (cs.enc == ENC_DICT && GpuEncoder::dict_gpu()))) {
                 gcols.push_back(c);
+            }
         }
     std::vector<uint8_t> on_gpu(ncols, 0);
     for (size_t c : gcols) on_gpu[c] = 1;
@@ -2238,7 +2254,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             if (nulls) fill_nulls(p.stage[c], vbytes, nrows, vw);
             p.rg.zones[c] = zone_of_typed(cs.type, p.stage[c], nrows);
             null_flags(p.rg.zones[c]);
-            if (cs.enc == ENC_AUTO) {
+            if (cs.enc == ENC_AUTO && !type_is_float(cs.type)) {
                 if (GpuEncoder::dict_gpu()) {  // dict_analyze_kernel makes the DICT estimate
                     *p.est_dict[c] = kEstDictGpu;
                 } else {                       // the host's (FLS_WRITER_DICT_GPU=0)

@@ -468,3 +468,86 @@ def test_str_dict_columns_cover_dict_and_fsst_cpu(fl):
     cols = _str_dict_columns(fl, 65536, np.random.default_rng(4))
     encs = _chunk_encodings(fl.write_image(cols).tobytes())
     assert encs.get(fl.ENC_DICT, 0) >= 6 and encs.get(fl.ENC_FSST, 0) >= 2, encs
+
+
+def _alp_columns(fl, n, rng):
+    """FLOAT / DOUBLE columns that exercise ALP's choices: decimals (one
+    exponent fits), integers as doubles, values with no decimal form (every
+    value an exception), specials (NaN, +-inf, -0.0, subnormals, huge), a
+    constant, float32 twins, and NULLs (placeholders: the previous value)."""
+    price = np.round(rng.random(n) * 1e5, 2)
+    ints = rng.integers(-10**6, 10**6, n).astype(np.float64)
+    rnd = rng.standard_normal(n)
+    special = np.round(rng.random(n) * 100, 1)
+    k = np.arange(n)
+    for j, x in enumerate([np.nan, np.inf, -np.inf, -0.0, 5e-324, 1e300, 0.0]):
+        special[k % 97 == j] = x
+    const = np.full(n, 3.14)
+    mixed = np.where(rng.random(n) < 0.3, rnd, price)   # some vectors mostly exceptions
+    fprice = np.round(rng.random(n) * 1e3, 2).astype(np.float32)
+    frnd = rng.standard_normal(n).astype(np.float32)
+    with np.errstate(over="ignore"):
+        fspecial = special.astype(np.float32)                # 1e300 -> inf
+    masked = np.ma.masked_array(np.round(rng.random(n) * 50, 3), mask=rng.random(n) < 0.2)
+    return [("price", fl.DOUBLE, price, fl.ENC_ALP), ("ints", fl.DOUBLE, ints, fl.ENC_AUTO),
+            ("rnd", fl.DOUBLE, rnd, fl.ENC_ALP), ("special", fl.DOUBLE, special, fl.ENC_ALP),
+            ("const", fl.DOUBLE, const, fl.ENC_AUTO), ("mixed", fl.DOUBLE, mixed, fl.ENC_ALP),
+            ("fprice", fl.FLOAT, fprice, fl.ENC_ALP), ("frnd", fl.FLOAT, frnd, fl.ENC_AUTO),
+            ("fspecial", fl.FLOAT, fspecial, fl.ENC_ALP), ("masked", fl.DOUBLE, masked, fl.ENC_ALP)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rowgroup", [(65536 * 2 + 777, 65536), (20000, 4096), (1024 * 3 + 5, 1024), (9, 1024),
+                                        (1, 65536)])
+def test_gpu_writer_alp_bytes_identical(fl, ref, gpu, monkeypatch, n, rowgroup):
+    """ALP chunks of FLOAT / DOUBLE columns encoded on the GPU
+    (alp_encode_kernel: the sampled (e, f) votes, each vector's cheapest
+    candidate, exceptions and FFOR packing): the file -- chunks and float zone
+    maps -- is the CPU writer's, byte for byte, its values decode bit-exactly
+    under the oracle, and the host path (FLS_WRITER_ALP_GPU=0) writes the same."""
+    cols = _alp_columns(fl, n, np.random.default_rng(n + 5))
+    cpu_img = fl.write_image(cols, rowgroup=rowgroup)
+    cpu = cpu_img.tobytes()
+    dev = fl.write_image(cols, rowgroup=rowgroup, device=0, threads=8).tobytes()
+    assert len(cpu) == len(dev)
+    assert cpu == dev
+    rf = ref.RefFile(cpu_img)
+    for c, (name, ty, vals, _) in enumerate(cols):
+        got = np.concatenate([rf.decode(c, r) for r in range(rf.nrowgroups)])
+        want = np.ma.getdata(vals)
+        if np.ma.isMaskedArray(vals):  # NULL rows hold the previous valid value
+            m = np.ma.getmaskarray(vals)
+            want = want.copy()
+            for i in np.flatnonzero(m):
+                want[i] = want[i - 1] if i > 0 else 0.0
+            keep = ~m
+            assert np.array_equal(got.view(want.dtype)[keep].view(np.uint8), want[keep].view(np.uint8)), name
+        else:
+            assert np.array_equal(got, want.view(np.uint8)), name
+    monkeypatch.setenv("FLS_WRITER_ALP_GPU", "0")
+    assert fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes() == cpu
+
+
+@pytest.mark.gpu
+def test_gpu_writer_alp_lineitem_dbl_decodes(fl, gpu):
+    """lineitem with the four DECIMAL columns as DOUBLE (the lineitem_dbl
+    workload's shape), written on the GPU: the file is the CPU writer's and the
+    GPU decode of it returns every value's bits."""
+    n = 65536 + 1000
+    rng = np.random.default_rng(11)
+    qty = rng.integers(1, 51, n).astype(np.float64)
+    price = np.round(rng.integers(90000, 10500000, n) / 100.0, 2)
+    disc = rng.integers(0, 11, n) / 100.0
+    tax = rng.integers(0, 9, n) / 100.0
+    cols = [("q", fl.DOUBLE, qty, fl.ENC_ALP), ("p", fl.DOUBLE, price, fl.ENC_ALP),
+            ("d", fl.DOUBLE, disc, fl.ENC_ALP), ("t", fl.DOUBLE, tax, fl.ENC_AUTO)]
+    cpu = fl.write_image(cols).tobytes()
+    img = fl.write_image(cols, device=0, threads=4)
+    assert img.tobytes() == cpu
+    t = fl.Connection([0]).read_image(img)
+    got = {c: [] for c in range(len(cols))}
+    for _, arrs in t.scan(cols=list(range(len(cols)))):
+        for c in got:
+            got[c].append(np.asarray(arrs[c]).view(np.uint8))
+    for c, (_, _, vals, _) in enumerate(cols):
+        assert np.array_equal(np.concatenate(got[c]), vals.view(np.uint8)), c
