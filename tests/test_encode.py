@@ -488,6 +488,8 @@ def _alp_columns(fl, n, rng):
     frnd = rng.standard_normal(n).astype(np.float32)
     with np.errstate(over="ignore"):
         fspecial = special.astype(np.float32)                # 1e300 -> inf
+    fspecial[k % 89 == 3] = np.float32(1e-40)               # float32 subnormals (no flush to zero)
+    fspecial[k % 89 == 4] = np.float32(-3e-42)
     masked = np.ma.masked_array(np.round(rng.random(n) * 50, 3), mask=rng.random(n) < 0.2)
     return [("price", fl.DOUBLE, price, fl.ENC_ALP), ("ints", fl.DOUBLE, ints, fl.ENC_AUTO),
             ("rnd", fl.DOUBLE, rnd, fl.ENC_ALP), ("special", fl.DOUBLE, special, fl.ENC_ALP),
