@@ -1947,6 +1947,7 @@ struct GpuEncoder {
         WHIP(hipEventSynchronize(b.done));
         const double t1 = g_prof.on ? WriterProfile::now() : 0;
         std::atomic<size_t> next{0};
+        std::atomic<size_t> empty{SIZE_MAX};  // a job whose chunk came back empty (a kernel that did not write it)
         auto move_out = [&]() {
             for (size_t i; (i = next.fetch_add(1)) < b.jobs.size();) {
                 const Job &jb = b.jobs[i];
@@ -1961,6 +1962,10 @@ struct GpuEncoder {
                     dst = enc == ENC_RLE ? enc_rle(jb.T, v.data(), jb.nrows) : enc_dict_int(jb.T, v.data(), jb.nrows);
                     continue;
                 }
+                if (len == 0) {
+                    empty.store(i);
+                    continue;
+                }
                 dst.assign(b.h_out + jb.out_off, b.h_out + jb.out_off + len);
             }
         };
@@ -1969,6 +1974,19 @@ struct GpuEncoder {
         for (size_t t = 1; t < nth; ++t) th.emplace_back(move_out);
         move_out();
         for (auto &t : th) t.join();
+        // test hook: a set whose first chunk came back empty (the error path)
+        if (const char *f = getenv("FLS_TEST_FAIL_GPU_ENCODE"); f && atoi(f) != 0 && !b.jobs.empty()) empty.store(0);
+        if (const size_t e = empty.load(); e != SIZE_MAX) {
+            const Job &jb = b.jobs[e];
+            const int rc = fail(FLS_ERR_DEVICE, "GPU encoder: no chunk for row group %zu column %zu (encoding %u)", jb.rg,
+                                jb.col, (unsigned)jb.enc);
+            b.jobs.clear();
+            b.in_used = b.out_used = 0;
+            b.dict_used = 0;
+            b.batched = 0;
+            b.in_flight = false;
+            return rc;
+        }
         b.jobs.clear();
         b.in_used = b.out_used = 0;
         b.dict_used = 0;
@@ -2308,6 +2326,13 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         w->broken_msg = fsst_gpu->err_msg;
         return fail(rc, "%s", fsst_gpu->err_msg.c_str());
     };
+    // a GPU encoder failure (a set that did not come back whole) leaves row
+    // groups without some of their chunks: the writer is failed from here on
+    auto gpu_failed = [&](int rc) -> int {
+        w->broken = rc;
+        w->broken_msg = fls_last_error();
+        return rc;
+    };
     seg.reserve(nrg);
     for (uint32_t k = 0; k < nrg; ++k) {
         Pending p;
@@ -2326,8 +2351,8 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size() + seg.size(), a[k].nrows, w->threads,
                                       w->fb.rgs, p.stage, p.est_dict);
             if (rc) {
-                run_seg();  // the row groups already in the batch stay consistent
-                return rc;
+                run_seg();
+                return gpu_failed(rc);
             }
         }
         seg.push_back(std::move(p));
@@ -2336,7 +2361,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             run_seg();
             if (const int rc = seg_failed()) return rc;
             const int rc = w->gpu.submit();
-            if (rc) return rc;
+            if (rc) return gpu_failed(rc);
         }
     }
     run_seg();
@@ -2408,7 +2433,11 @@ int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path)
     if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
     if (w->gpu.dev >= 0) {
         const int rc = w->gpu.finish(w->fb.rgs, w->threads);
-        if (rc) return rc;
+        if (rc) {  // row groups without some of their chunks: no file from this writer
+            w->broken = rc;
+            w->broken_msg = fls_last_error();
+            return rc;
+        }
     }
     const double tf = g_prof.on ? WriterProfile::now() : 0;
     const int rc = path ? w->fb.write_file(path, w->threads) : w->fb.finish(img, len, w->threads);

@@ -342,6 +342,34 @@ def test_gpu_writer_fsst_failure_marks_writer_failed(fl, gpu, monkeypatch):
         fl.lib.fls_writer_free(w)
 
 
+@pytest.mark.gpu
+def test_gpu_encoder_failure_marks_writer_failed(fl, gpu, monkeypatch):
+    """A GPU encoder set that comes back without one of its chunks (injected:
+    FLS_TEST_FAIL_GPU_ENCODE) fails the call that completes it, names the row
+    group and column, and leaves the writer failed: no later finish writes a
+    file whose row groups miss chunks."""
+    import ctypes as C
+    rng = np.random.default_rng(6)
+    n = 4096
+    strs = [b"x%d" % (i % 7) for i in range(n)]
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_set_rowgroup_size(w, n) == 0
+        assert fl.lib.fls_writer_set_device(w, 0) == 0
+        assert fl.lib.fls_writer_add_column(w, b"i", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_add_column(w, b"s", fl.VARCHAR, 0, 0, fl.ENC_AUTO) == 0
+        assert _add_rg(fl, w, rng.integers(0, 1000, n), strs) == 0
+        monkeypatch.setenv("FLS_TEST_FAIL_GPU_ENCODE", "1")
+        p, ln = C.c_void_p(), C.c_uint64()
+        assert fl.lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)) < 0
+        assert b"no chunk for row group" in fl.lib.fls_last_error()
+        monkeypatch.delenv("FLS_TEST_FAIL_GPU_ENCODE")
+        assert fl.lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)) < 0
+        assert b"failed earlier" in fl.lib.fls_last_error()
+    finally:
+        fl.lib.fls_writer_free(w)
+
+
 # ---- DICT chunks of integer columns on the GPU (dict_analyze_kernel /
 # dict_encode_kernel, VERDICT r3 item 5; SURVEY.md 8(f) row 1 "dict analysis";
 # reference writer stub src/writer/write_fastlane_stream.cpp:65-107,294-314) ----
