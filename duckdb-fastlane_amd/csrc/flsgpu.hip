@@ -1546,13 +1546,15 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     // rebuilt over the copied heap on the consumer's thread (scan_acquire).
     // Unfiltered scans only (a filtered batch compacts its rows, and the heap
     // offsets of the delivered strings need every row's length).
-    // Opt-in (FLS_SCAN_STRLEN=1): measured neutral on the 16-CPU GPU box,
-    // where a narrowed 16-thread read_fastlanes is bound by host work rather
-    // than by the link (lineitem_full SF10: 5.72e8 rows/s with, 5.71e8
-    // without; profiles/r3/bench_e2e_strlen_r3zj.json, bench_r3zc.json).
+    // On by default with narrowing (FLS_SCAN_STRLEN=0: string_t records over
+    // the link).  Round 3 measured it neutral while the scan was bound by host
+    // work (profiles/r3/bench_e2e_strlen_r3zj.json); with the compressed image
+    // resident in HBM the 16-thread read_fastlanes is bound by the D2H link,
+    // and the lengths (15 fewer bytes per lineitem row) measured 7.81e8 rows/s
+    // against 6.78e8 (profiles/r4/e2e_arms_strlen_r4t.txt).
     hb.strlen_w.assign(ncols, 0);
     const char *sle = getenv("FLS_SCAN_STRLEN");
-    const bool strlen_on = sle && atoi(sle) != 0;
+    const bool strlen_on = !(sle && atoi(sle) == 0);
     for (uint32_t c = 0; strlen_on && s.narrow && s.terms.empty() && c < ncols; ++c) {
         if (!col_selected(s.mask, c) || !type_is_string(t->meta.cols[c].type) || hb.ob[c] != 16) continue;
         bool ok = true;

@@ -51,7 +51,20 @@ def _scan_strings(fl, t, narrow, threads_cols):
 
 @pytest.fixture
 def strlen_on(monkeypatch):
-    monkeypatch.setenv("FLS_SCAN_STRLEN", "1")   # FSST-as-lengths delivery is opt-in
+    monkeypatch.setenv("FLS_SCAN_STRLEN", "1")   # FSST-as-lengths delivery (the default since round 4)
+
+
+def test_fsst_records_delivery_when_lengths_off(fl, gpu, monkeypatch):
+    """FLS_SCAN_STRLEN=0: a narrowed scan ships the GPU-built string_t records
+    (round 3's delivery); the strings equal the full-width scan's"""
+    monkeypatch.setenv("FLS_SCAN_STRLEN", "0")
+    t = fl.Connection([0]).read_image(fl.gen_image("lineitem_full", 0.02))
+    sch = t.schema()
+    sc = [c for c in range(t.ncols) if sch[c][0] == "l_comment"]
+    full = _scan_strings(fl, t, False, sc)
+    nar = _scan_strings(fl, t, True, sc)
+    for c in sc:
+        assert len(full[c]) == t.nrows and full[c] == nar[c]
 
 
 @pytest.mark.parametrize("scale", [0.02, 0.25])
