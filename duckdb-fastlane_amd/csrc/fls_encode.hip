@@ -1498,45 +1498,6 @@ __global__ __launch_bounds__(256) void str_dict_codes_kernel(uint32_t n, const u
     codes[i] = slots[2 * enc_dict_cap(n) + row_slot[i]];
 }
 
-// ---- packing a set's chunks for the D2H (fls_writer.cpp GpuEncoder) ----
-// Chunks are written to slots sized for their worst case (W = T, every ALP
-// value an exception); the host needs only their bytes.  pack_offsets_kernel
-// (one block): each job's offset in a dense buffer, an exclusive scan of the
-// lengths (multiples of kChunkAlign), and the total at poff[njobs];
-// pack_copy_kernel (a block per chunk): the chunk's bytes to its offset.
-__global__ __launch_bounds__(1024) void pack_offsets_kernel(const uint64_t *__restrict__ lens, uint32_t njobs,
-                                                            uint64_t *__restrict__ poff) {
-    __shared__ uint64_t part[1024];
-    const uint32_t t = threadIdx.x, per = (njobs + 1023) / 1024;
-    const uint32_t i0 = min(njobs, t * per), i1 = min(njobs, i0 + per);
-    const uint64_t mask = (1ull << kEncShift) - 1;
-    uint64_t sum = 0;
-    for (uint32_t i = i0; i < i1; ++i) sum += lens[i] & mask;
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive scan of the thread sums
-        const uint64_t y = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += y;
-        __syncthreads();
-    }
-    uint64_t run = part[t] - sum;
-    for (uint32_t i = i0; i < i1; ++i) {
-        poff[i] = run;
-        run += lens[i] & mask;
-    }
-    if (t == 1023) poff[njobs] = part[1023];
-}
-__global__ __launch_bounds__(256) void pack_copy_kernel(const EncChunk *__restrict__ desc, const uint64_t *lens,
-                                                        const uint64_t *__restrict__ poff, uint8_t *__restrict__ pack) {
-    const EncChunk c = desc[blockIdx.x];
-    const uint32_t j = (uint32_t)((c.len_out - (uint64_t)(uintptr_t)lens) / sizeof(uint64_t));
-    const uint64_t len = lens[j] & ((1ull << kEncShift) - 1);
-    const FLS_GLOBAL v4u *src = (const FLS_GLOBAL v4u *)(uintptr_t)c.out;
-    FLS_GLOBAL v4u *dst = (FLS_GLOBAL v4u *)(FLS_GLOBAL uint8_t *)(pack + poff[j]);
-    for (uint64_t q = threadIdx.x; q < len / 16; q += blockDim.x) dst[q] = src[q];
-}
-
 // One lane per string.  The table is staged in LDS; a lane reads its string
 // 8 bytes at a time from two aligned qwords (the L1 serves the overlap of
 // consecutive steps) and writes its codes byte by byte into its own region.
@@ -1612,14 +1573,6 @@ hipError_t launch_str_dict(const uint8_t *d_bytes, const uint32_t *d_offs, uint3
     hipLaunchKernelGGL(str_dict_sort_kernel, dim3(1), dim3(1024), 0, stream, d_offs, n, d_slots, d_entries, d_info);
     hipLaunchKernelGGL(str_dict_codes_kernel, dim3(grid), dim3(256), 0, stream, n, d_slots, d_row_slot, d_codes,
                        d_info);
-    return hipGetLastError();
-}
-
-hipError_t launch_pack_chunks(const EncChunk *d_desc, uint32_t njobs, const uint64_t *d_lens, uint64_t *d_poff,
-                              uint8_t *d_pack, hipStream_t stream) {
-    if (njobs == 0) return hipSuccess;
-    hipLaunchKernelGGL(pack_offsets_kernel, dim3(1), dim3(1024), 0, stream, d_lens, njobs, d_poff);
-    hipLaunchKernelGGL(pack_copy_kernel, dim3(njobs), dim3(256), 0, stream, d_desc, d_lens, d_poff, d_pack);
     return hipGetLastError();
 }
 

@@ -53,11 +53,6 @@ uint64_t enc_slot_bytes(uint32_t T, uint32_t nrows, uint8_t enc);
 // rle: some chunk is ENC_RLE or ENC_AUTO (encode_rle_kernel follows).
 // dict: some chunk is ENC_DICT or ENC_AUTO with a dict_tab (dict_analyze_kernel
 // runs first, dict_encode_kernel after).  d_chunks is written (est_dict).
-// Pack a launch's chunks densely for the D2H: poff[i] = the offset of job i
-// (the job whose length word is d_lens[i]), poff[njobs] = the total; the
-// chunks' bytes copied from their slots (d_desc[k].out) into d_pack.
-hipError_t launch_pack_chunks(const EncChunk *d_desc, uint32_t njobs, const uint64_t *d_lens, uint64_t *d_poff,
-                              uint8_t *d_pack, hipStream_t stream);
 // alp: some chunk is ENC_ALP (FLOAT T = 32 / DOUBLE T = 64: alp_encode_kernel).
 hipError_t launch_encode(EncChunk *d_chunks, uint32_t n_wide, uint32_t n_narrow, hipStream_t stream, bool rle,
                          bool dict = false, bool alp = false);

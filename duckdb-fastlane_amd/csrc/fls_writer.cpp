@@ -1710,12 +1710,6 @@ struct GpuEncoder {
         size_t dict_cap = 0;
         uint64_t dict_used = 0;
         uint64_t *h_lens = nullptr, *d_lens = nullptr;
-        // the set's chunks packed densely (launch_pack_chunks): their offsets
-        // (job order, total last) and bytes; h_out holds the packed bytes
-        uint8_t *d_pack = nullptr;
-        uint64_t *h_poff = nullptr, *d_poff = nullptr;
-        uint64_t copied = 0;  // packed bytes already on their way to h_out (submit)
-        bool dense = true;    // packed (else h_out holds the slots as they lie)
         EncChunk *h_desc = nullptr, *d_desc = nullptr;
         size_t in_cap = 0, out_cap = 0, job_cap = 0;
         std::vector<Job> jobs;
@@ -1728,10 +1722,6 @@ struct GpuEncoder {
     hipStream_t stream = nullptr;
     Set sets[2];
     int cur = 0;
-    // packed bytes / slot bytes of the last completed set: the share of a set
-    // copied back asynchronously at submit (the rest, if any, in complete)
-    double pack_ratio = 1.0;
-    hipStream_t rest_stream = nullptr;
 
     static void free_set(Set &b) {
         hipHostFree(b.h_stage);
@@ -1744,9 +1734,6 @@ struct GpuEncoder {
         hipFree(b.d_desc);
         hipFree(b.d_scratch);
         hipFree(b.d_dict);
-        hipFree(b.d_pack);
-        hipFree(b.d_poff);
-        hipHostFree(b.h_poff);
         if (b.done) hipEventDestroy(b.done);
         b = Set();
     }
@@ -1757,8 +1744,7 @@ struct GpuEncoder {
         free_set(sets[0]);
         free_set(sets[1]);
         if (stream) hipStreamDestroy(stream);
-        if (rest_stream) hipStreamDestroy(rest_stream);
-        stream = rest_stream = nullptr;
+        stream = nullptr;
         cur = 0;
     }
     ~GpuEncoder() { release(); }
@@ -1792,12 +1778,10 @@ struct GpuEncoder {
         }
         if (kBatch * out_rg > b.out_cap) {
             hipFree(b.d_out);
-            hipFree(b.d_pack);
             hipHostFree(b.h_out);
-            b.d_out = b.d_pack = b.h_out = nullptr;
+            b.d_out = b.h_out = nullptr;
             b.out_cap = 0;
             WHIP(hipMalloc((void **)&b.d_out, kBatch * out_rg));
-            WHIP(hipMalloc((void **)&b.d_pack, kBatch * out_rg));
             WHIP(hipHostMalloc((void **)&b.h_out, kBatch * out_rg, 0));
             b.out_cap = kBatch * out_rg;
         }
@@ -1807,16 +1791,11 @@ struct GpuEncoder {
             hipHostFree(b.h_lens);
             hipHostFree(b.h_desc);
             hipFree(b.d_scratch);
-            hipFree(b.d_poff);
-            hipHostFree(b.h_poff);
             b.d_desc = b.h_desc = nullptr;
             b.d_lens = b.h_lens = nullptr;
-            b.d_poff = b.h_poff = nullptr;
             b.d_scratch = nullptr;
             b.job_cap = 0;
             const size_t n = kBatch * nj;
-            WHIP(hipMalloc((void **)&b.d_poff, (n + 1) * sizeof(uint64_t)));
-            WHIP(hipHostMalloc((void **)&b.h_poff, (n + 1) * sizeof(uint64_t), 0));
             WHIP(hipMalloc((void **)&b.d_desc, n * sizeof(EncChunk)));
             WHIP(hipHostMalloc((void **)&b.h_desc, n * sizeof(EncChunk), 0));
             WHIP(hipMalloc((void **)&b.d_lens, n * sizeof(uint64_t)));
@@ -1838,10 +1817,6 @@ struct GpuEncoder {
         return !(e && atoi(e) == 0);
     }
     static bool dict_job(uint8_t enc) { return (enc == ENC_DICT || enc == ENC_AUTO) && dict_gpu(); }
-    static bool dense_d2h() {
-        const char *e = getenv("FLS_WRITER_DENSE_D2H");
-        return !(e && atoi(e) == 0);
-    }
     // ALP chunks of FLOAT / DOUBLE columns on the GPU (FLS_WRITER_ALP_GPU=0:
     // on the host threads)
     static bool alp_gpu() {
@@ -1953,24 +1928,11 @@ struct GpuEncoder {
             alp |= jb.enc == ENC_ALP;
         }
         WHIP(launch_encode(b.d_desc, n_wide, (uint32_t)b.jobs.size() - n_wide, stream, rle, dict, alp));
-        // the chunks packed densely on the device, then one pinned copy of
-        // the expected packed bytes (the last set's share of its slot bytes,
-        // +25 %); complete() copies any rest once the total is known.  (Round 3
-        // copied the whole slots: sized for W = T and, for ALP, every value an
-        // exception, they hold 4-6x the chunks' bytes.)
-        const uint32_t nj = (uint32_t)b.jobs.size();
-        WHIP(hipMemcpyAsync(b.h_lens, b.d_lens, nj * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-        b.dense = dense_d2h();
-        if (b.dense) {
-            WHIP(launch_pack_chunks(b.d_desc, nj, b.d_lens, b.d_poff, b.d_pack, stream));
-            WHIP(hipMemcpyAsync(b.h_poff, b.d_poff, (nj + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-            b.copied = std::min<uint64_t>(
-                b.out_used, (uint64_t)((double)b.out_used * std::min(1.0, pack_ratio * 1.25)) + (1u << 20));
-            b.copied &= ~(uint64_t)(kChunkAlign - 1);
-            if (b.copied) WHIP(hipMemcpyAsync(b.h_out, b.d_pack, b.copied, hipMemcpyDeviceToHost, stream));
-        } else {  // (A/B: round 3's copy of every slot, FLS_WRITER_DENSE_D2H=0)
-            WHIP(hipMemcpyAsync(b.h_out, b.d_out, b.out_used, hipMemcpyDeviceToHost, stream));
-        }
+        WHIP(hipMemcpyAsync(b.h_lens, b.d_lens, b.jobs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        // the slots come back in one pinned copy (slots are sized for W = T,
+        // so this moves more than the chunks hold, but one large copy beats
+        // a small copy per chunk); complete() moves each chunk's bytes out
+        WHIP(hipMemcpyAsync(b.h_out, b.d_out, b.out_used, hipMemcpyDeviceToHost, stream));
         WHIP(hipEventRecord(b.done, stream));
         b.in_flight = true;
         cur ^= 1;
@@ -1983,16 +1945,6 @@ struct GpuEncoder {
     int complete(Set &b, std::vector<FileBuilder::RG> &rgs, int nthreads) {
         const double t0 = g_prof.on ? WriterProfile::now() : 0;
         WHIP(hipEventSynchronize(b.done));
-        const uint64_t packed = b.dense ? b.h_poff[b.jobs.size()] : 0;
-        if (packed > b.out_used) return fail(FLS_ERR_DEVICE, "GPU encoder: packed chunks exceed their slots");
-        if (b.dense && packed > b.copied) {  // the rest of the packed bytes, on a stream of its own (the other
-                                  // set may be queued on the encoder's stream behind this one)
-            if (!rest_stream) WHIP(hipStreamCreateWithFlags(&rest_stream, hipStreamNonBlocking));
-            WHIP(hipMemcpyAsync(b.h_out + b.copied, b.d_pack + b.copied, packed - b.copied, hipMemcpyDeviceToHost,
-                                rest_stream));
-            WHIP(hipStreamSynchronize(rest_stream));
-        }
-        if (b.dense && b.out_used) pack_ratio = (double)packed / (double)b.out_used;
         const double t1 = g_prof.on ? WriterProfile::now() : 0;
         std::atomic<size_t> next{0};
         std::atomic<size_t> empty{SIZE_MAX};  // a job whose chunk came back empty (a kernel that did not write it)
@@ -2014,8 +1966,7 @@ struct GpuEncoder {
                     empty.store(i);
                     continue;
                 }
-                const uint64_t at = b.dense ? b.h_poff[i] : jb.out_off;
-                dst.assign(b.h_out + at, b.h_out + at + len);
+                dst.assign(b.h_out + jb.out_off, b.h_out + jb.out_off + len);
             }
         };
         std::vector<std::thread> th;

@@ -581,22 +581,3 @@ def test_gpu_writer_alp_lineitem_dbl_decodes(fl, gpu):
             got[c].append(np.asarray(arrs[c]).view(np.uint8))
     for c, (_, _, vals, _) in enumerate(cols):
         assert np.array_equal(np.concatenate(got[c]), vals.view(np.uint8)), c
-
-
-@pytest.mark.gpu
-def test_gpu_encoder_dense_d2h_rest_copy(fl, gpu, monkeypatch):
-    """The GPU encoder packs a set's chunks densely and copies back the
-    share the last set needed (+25 %) at submit, the rest once the total is
-    known.  A file whose first 32-row-group set compresses to almost nothing
-    and whose next set does not takes the rest path; both, and round 3's
-    whole-slot copy (FLS_WRITER_DENSE_D2H=0), write the CPU writer's bytes."""
-    rng = np.random.default_rng(21)
-    rg = 1024
-    n = 40 * rg
-    a = np.concatenate([np.full(32 * rg, 7, np.int64), rng.integers(-2**62, 2**62, n - 32 * rg)])
-    b = np.concatenate([np.zeros(32 * rg), rng.standard_normal(n - 32 * rg)])
-    cols = [("a", fl.INT64, a, fl.ENC_FFOR), ("b", fl.DOUBLE, b, fl.ENC_ALP), ("c", fl.INT32, (a % 1000).astype(np.int32), fl.ENC_AUTO)]
-    cpu = fl.write_image(cols, rowgroup=rg).tobytes()
-    assert fl.write_image(cols, rowgroup=rg, device=0, batch=8, threads=8).tobytes() == cpu
-    monkeypatch.setenv("FLS_WRITER_DENSE_D2H", "0")
-    assert fl.write_image(cols, rowgroup=rg, device=0, batch=8, threads=8).tobytes() == cpu
