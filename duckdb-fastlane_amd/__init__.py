@@ -102,6 +102,8 @@ _sig("fls_device_count", C.c_int)
 _sig("fls_connect", C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(_P))
 _sig("fls_disconnect", None, _P)
 _sig("fls_connection_trim", C.c_int, _P, C.c_uint64, C.POINTER(C.c_uint64))
+_sig("fls_release_device_memory", C.c_int, C.c_int, C.POINTER(C.c_uint64))
+_sig("fls_resident_info", C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32))
 _sig("fls_read_fls", C.c_int, _P, C.c_char_p, C.POINTER(_P))
 _sig("fls_read_fls_image", C.c_int, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P))
 _sig("fls_table_close", None, _P)
@@ -417,6 +419,21 @@ class Connection:
         left = C.c_uint64()
         _check(_lib.fls_connection_trim(self.h, keep_bytes, C.byref(left)))
         return left.value
+
+    @staticmethod
+    def release_device_memory(device: int = -1) -> int:
+        """Free the HBM-resident file images no running scan uses on device
+        (-1: every GPU); returns the bytes freed (fls_release_device_memory)."""
+        freed = C.c_uint64()
+        _check(_lib.fls_release_device_memory(device, C.byref(freed)))
+        return freed.value
+
+    @staticmethod
+    def resident_info(device: int = -1):
+        """(bytes, images) of the HBM-resident file images on device (-1: all)."""
+        b, n = C.c_uint64(), C.c_uint32()
+        _check(_lib.fls_resident_info(device, C.byref(b), C.byref(n)))
+        return b.value, n.value
 
     def read_fls(self, path: str) -> "Table":
         h = _P()

@@ -702,10 +702,50 @@ __device__ __forceinline__ uint32_t next_chunk(uint32_t *queue, uint32_t prev, u
     return stride + uni(ci);
 }
 
+#ifdef FLS_WAVE_TRACE
+// Timing build (make trace, libflsgpu_trace.so; scripts/wave_trace.py): one
+// record per decode_chunk call -- start / end (s_memrealtime, 100 MHz), the
+// wave, its hardware slot and XCD, the vector range and the chunk's shape.
+struct TraceRec {
+    uint64_t t0, t1;
+    uint32_t wave, vr, hw_id, xcc_id, shape, max_w;
+};
+constexpr uint32_t kTraceCap = 1u << 20;
+__device__ TraceRec g_trace[kTraceCap];
+__device__ uint32_t g_trace_n;
+#endif
+
+__device__ __forceinline__ void decode_chunk_body(const DevChunk *cg, uint32_t lp, uint32_t lv, uint32_t v_bytes,
+                                                  uint32_t *err, uint32_t vr);
 // Decode vectors [vr & 0xFF, vr >> 8) of one chunk: the chunk's (encoding, T,
 // output width) picks the path instantiation.
 __device__ __forceinline__ void decode_chunk(const DevChunk *cg, uint32_t lp, uint32_t lv, uint32_t v_bytes,
                                              uint32_t *err, uint32_t vr) {
+#ifdef FLS_WAVE_TRACE
+    const uint64_t t0 = wall_clock64();
+    decode_chunk_body(cg, lp, lv, v_bytes, err, vr);
+    const uint64_t t1 = wall_clock64();
+    if (__lane_id() == 0) {
+        const uint32_t i = atomicAdd(&g_trace_n, 1u);
+        if (i < kTraceCap) {
+            const FLS_GLOBAL DevChunk *c = gptr(cg);
+            TraceRec &r = g_trace[i];
+            r.t0 = t0;
+            r.t1 = t1;
+            r.wave = blockIdx.x * kWaves + (threadIdx.x >> 6);
+            r.vr = vr;
+            r.hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            r.xcc_id = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+            r.shape = (uint32_t)c->enc | (uint32_t)c->T << 8 | (uint32_t)c->ob << 16 | c->nvec << 24;
+            r.max_w = c->max_w;
+        }
+    }
+#else
+    decode_chunk_body(cg, lp, lv, v_bytes, err, vr);
+#endif
+}
+__device__ __forceinline__ void decode_chunk_body(const DevChunk *cg, uint32_t lp, uint32_t lv, uint32_t v_bytes,
+                                                  uint32_t *err, uint32_t vr) {
     const FLS_GLOBAL DevChunk *c = gptr(cg);
     const uint32_t dc = c->dict_count, mw = c->max_w;
     const uint32_t enc = c->enc, T = c->T, ob = c->ob;
@@ -791,6 +831,21 @@ __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const D
     const uint32_t lp = (uint32_t)(size_t)((lu8 *)lds_raw + w * (p_bytes + v_bytes));
     const uint32_t lv = lp + p_bytes;
     const uint32_t stride = shared_queue ? 0u : gridDim.x * kWaves, first = blockIdx.x * kWaves + w;
+    if (split && shared_queue) {
+        // several grids drain one guided plan: queue value q < nst is static
+        // item q, the rest tail pieces (nst = the plan's waves, flags >> 8)
+        const FLS_GLOBAL uint32_t *sp = gptr(split);
+        const uint32_t nst = flags >> 8;
+        for (;;) {
+            uint32_t q = 0;
+            if (__lane_id() == 0) q = atomicAdd(queue, 1u);
+            q = uni(q);
+            if (q >= nst + npieces) break;
+            const uint32_t i = q < nst ? q : q + 1;  // pieces start one entry past the static boundaries
+            decode_range(chunks, nchunks, uni(sp[i]), uni(sp[i + 1]), lp, lv, v_bytes, err);
+        }
+        return;
+    }
     if (split) {
         const FLS_GLOBAL uint32_t *sp = gptr(split);
         decode_range(chunks, nchunks, uni(sp[first]), uni(sp[first + 1]), lp, lv, v_bytes, err);
@@ -814,6 +869,23 @@ __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const D
 }
 
 }  // namespace
+
+#ifdef FLS_WAVE_TRACE
+extern "C" int fls_trace_reset(void) {
+    const uint32_t z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// copies up to cap records (40 B each) to dst; returns how many were recorded
+extern "C" int64_t fls_trace_read(void *dst, uint32_t cap) {
+    uint32_t n = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_trace_n), sizeof(n)) != hipSuccess)
+        return -1;
+    const uint32_t k = std::min(std::min(n, cap), kTraceCap);
+    if (k && hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_trace), (size_t)k * sizeof(TraceRec)) != hipSuccess) return -1;
+    return n;
+}
+#endif
 
 int decode_grid_size(uint32_t shmem_per_block) {
     int dev = 0, cus = 256, per_cu = 1;
@@ -873,13 +945,52 @@ SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t st
     return plan;
 }
 
+SplitPlan guided_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t factor, uint32_t min_vecs,
+                       std::vector<uint32_t> &pos) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += h[i].nvec * vec_cost(h[i]);
+    factor = std::max(1u, factor);
+    min_vecs = std::max(1u, min_vecs);
+    nw = std::max<uint32_t>(nw, kWaves);
+    // item starts (positions chunk << 7 | vector), one walk in list order
+    std::vector<uint32_t> b;
+    b.reserve(n + n / 4);
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t nv = h[i].nvec;
+        if (nv == 0) continue;
+        const uint64_t vc = vec_cost(h[i]), cc = nv * vc;
+        const uint64_t target = std::max<uint64_t>((total - acc) / ((uint64_t)factor * nw), (uint64_t)min_vecs * vc);
+        uint32_t parts = 1;
+        if (cc > target)
+            parts = (uint32_t)std::min<uint64_t>((cc + target - 1) / target, (nv + min_vecs - 1) / min_vecs);
+        for (uint32_t p = 0; p < parts; ++p) b.push_back(i << 7 | (uint32_t)((uint64_t)nv * p / parts));
+        acc += cc;
+    }
+    const uint32_t items = (uint32_t)b.size();
+    b.push_back(n << 7);
+    SplitPlan plan;
+    plan.guided = true;
+    plan.waves = std::min<uint32_t>(nw, std::max<uint32_t>(kWaves, (items + kWaves - 1) / kWaves * kWaves));
+    plan.pieces = items > plan.waves ? items - plan.waves : 0;
+    pos.clear();
+    pos.reserve(plan.positions());
+    // static: wave w takes item w (an empty range past the last item)
+    for (uint32_t w = 0; w <= plan.waves; ++w) pos.push_back(b[std::min(w, items)]);
+    // tail pieces: items waves .. items - 1 (pieces == 0: one unused entry)
+    for (uint32_t p = 0; p <= plan.pieces; ++p) pos.push_back(b[std::min(plan.waves + p, items)]);
+    return plan;
+}
+
 hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d_err, const DecodeGeom &geom,
                          hipStream_t stream, uint32_t *d_queue, const uint32_t *d_split, SplitPlan plan,
                          bool shared_queue, int prio) {
     if (nchunks == 0) return hipSuccess;
     const uint32_t shmem = kWaves * (geom.p_bytes + geom.v_bytes);
     int grid;
-    if (d_split) {
+    if (d_split && shared_queue) {
+        grid = std::min<int>(geom.grid > 0 ? geom.grid : decode_grid_size(shmem), (int)(plan.waves / kWaves));
+    } else if (d_split) {
         grid = (int)(plan.waves / kWaves);
         if (!plan.pieces) d_queue = nullptr;
     } else {
@@ -891,7 +1002,8 @@ hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d
     }
     hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
                        geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces,
-                       (uint32_t)(shared_queue && d_queue) | (uint32_t)(prio & 3) << 1);
+                       (uint32_t)(shared_queue && d_queue) | (uint32_t)(prio & 3) << 1 |
+                           (d_split && shared_queue ? plan.waves << 8 : 0u));
     return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ struct DecodeGeom {
 // when their static range is done.  waves == 0: no split.
 struct SplitPlan {
     uint32_t waves = 0, pieces = 0;
+    bool guided = false;  // guided_split (whole chunks, then ever smaller pieces), else balanced_split
     size_t positions() const { return waves ? (size_t)waves + pieces + 2 : 0; }
 };
 
@@ -74,6 +75,14 @@ uint32_t decode_waves(const DecodeGeom &geom);
 // equal tail pieces (dynamic: the waves that finish first take them).
 SplitPlan balanced_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t static_pct, uint32_t pieces_per_wave,
                          std::vector<uint32_t> &pos);
+// Guided split of h[0, n) in list order (largest output first) over at most
+// nw waves: work items are whole chunks while a chunk costs at most the
+// remaining work / (factor * nw), then pieces of that size, never below
+// min_vecs vectors, so the launch ends on pieces a few vectors long instead
+// of whole chunks.  Item w < waves is wave w's first (static) item, the rest
+// are tail pieces from the queue.
+SplitPlan guided_split(const DevChunk *h, uint32_t n, uint32_t nw, uint32_t factor, uint32_t min_vecs,
+                       std::vector<uint32_t> &pos);
 // Code-parallel FSST kernel variants (bits): kFsstPlain = escape-free rounds
 // skip the escape-state logic; kFsstTwoQ = each symbol OR-ed into both
 // qwords it spans instead of through a 64-bit accumulator; kFsstZeroFlush =

@@ -34,6 +34,7 @@
 #include "fls_filter.hpp"
 #include "fls_format.hpp"
 #include "fls_reader.hpp"
+#include "fls_resident.hpp"
 
 using namespace fls;
 
@@ -67,6 +68,11 @@ StrT make_string_t(const char *p, uint32_t n) {
     return s;
 }
 
+// Frees every HBM-resident image no running scan uses on GPU dev (defined
+// with the image registry); a device allocation that runs out of memory calls
+// it once and retries, so the image cache never fails a scan's own buffers.
+uint64_t release_idle_images(int dev);
+
 template <typename T>
 struct DevBuf {
     T *p = nullptr;
@@ -92,7 +98,16 @@ struct DevBuf {
         release();
         dev = d;
         n = count;
-        return hipMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)));
+        hipError_t e = hipMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)));
+        if (e == hipErrorOutOfMemory && release_idle_images(d) > 0) {
+            (void)hipGetLastError();
+            e = hipMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)));
+        }
+        if (e != hipSuccess) {
+            p = nullptr;
+            n = 0;
+        }
+        return e;
     }
     ~DevBuf() { release(); }
 };
@@ -561,8 +576,8 @@ struct Resident {
     std::vector<DevChunk> h_chunks;
     std::vector<uint8_t> mask;         // column mask h_chunks was built for
     uint32_t nmain = 0;                // h_chunks[0, nmain) main kernel, the rest FSST
-    int policy = -1;                   // decode_policy() h_chunks was ordered for
-    int lpolicy = 0;                   // ... and the launch policy it resolved to (launch_policy)
+    int64_t policy = -1;               // decode_policy() h_chunks was ordered for
+    int64_t lpolicy = 0;                // ... and the launch policy it resolved to (launch_policy)
     FsstCounts fsst;                   // FSST chunks of h_chunks
     SplitPlan split;                   // balanced split after h_chunks on the device (waves 0: none)
     ByteCount bytes;                   // algorithmic bytes of one launch
@@ -598,22 +613,69 @@ struct Resident {
 // later scans of the same (cached, unchanged) file decode its row groups from
 // it with no staging copy and no H2D -- a warm query moves only decoded bytes
 // over PCIe, in one direction.  Lives with the open-file cache entry.
+// One GPU's image holds the file bytes of that GPU's shard of the whole
+// table (its row groups when the table is split over the connection's GPUs),
+// not the whole file.  Images live in a process-wide registry with one byte
+// budget per GPU (ResidentSet, resident_image).
 struct DevImage {
-    DevBuf<uint8_t> buf;                               // the whole file image, + kImagePad
-    std::unique_ptr<std::atomic<uint8_t>[]> present;   // per row group: its chunks are in buf
+    uint8_t *p = nullptr;                              // file bytes [lo, hi) + kImagePad
+    int dev = -1;
+    uint64_t lo = 0, hi = 0;
+    std::unique_ptr<std::atomic<uint8_t>[]> present;   // per row group of the file: its chunks are in p
     uint32_t nrg = 0;
+    ~DevImage() {
+        if (p) {
+            int cur = 0;
+            hipGetDevice(&cur);
+            hipSetDevice(dev);
+            hipFree(p);
+            hipSetDevice(cur);
+        }
+    }
 };
+void drop_file_images(const void *owner);
 struct MappedFile {
     void *map = nullptr;
     size_t len = 0;
     FileMeta meta;
-    std::mutex dev_mu;
-    std::map<int, std::shared_ptr<DevImage>> dev_img;  // per GPU (scan_setup)
     ~MappedFile() {
-        dev_img.clear();
+        drop_file_images(this);
         if (map) munmap(map, len);
     }
 };
+
+// Every GPU's resident images, under one lock (process lifetime: tables may
+// outlive static destruction order).
+struct ImageRegistry {
+    std::mutex mu;
+    ResidentSet<DevImage> set;
+};
+ImageRegistry &image_registry() {
+    static auto *r = new ImageRegistry();
+    return *r;
+}
+// FLS_SCAN_RESIDENT_MB: the image budget per GPU over every cached file (0 = off)
+uint64_t resident_budget() {
+    const char *e = getenv("FLS_SCAN_RESIDENT_MB");
+    return (uint64_t)(e ? std::max(0L, atol(e)) : 65536L) << 20;
+}
+namespace {
+uint64_t release_idle_images(int dev) {
+    ImageRegistry &R = image_registry();
+    ResidentSet<DevImage>::Evicted ev;
+    std::lock_guard<std::mutex> lk(R.mu);
+    const uint64_t b = R.set.release_idle(dev, ev);
+    ev.clear();
+    return b;
+}
+}  // namespace
+void drop_file_images(const void *owner) {
+    ImageRegistry &R = image_registry();
+    ResidentSet<DevImage>::Evicted ev;
+    std::lock_guard<std::mutex> lk(R.mu);
+    R.set.drop_owner(owner, ev);
+    ev.clear();
+}
 
 struct fls_table {
     std::vector<int> devices;          // the connection's GPUs (row groups shard over them)
@@ -788,7 +850,9 @@ enum : int {
 // cached launch list): FLS_STATIC_PCT = % of the bytes split statically
 // (bits 8-15, default 100), FLS_TAIL_PIECES = tail pieces per wave for the
 // rest (bits 16-23, default 2), FLS_BLOCKS_PER_CU (bits 24-30, 0 = unset).
-int decode_policy() {
+// Guided tail defaults (FLS_GUIDED_MIN_VECS / FLS_GUIDED_FACTOR, guided_split)
+constexpr int kGuidedMinVecs = 0, kGuidedFactor = 2;
+int64_t decode_policy() {
     const char *e = getenv("FLS_DECODE_POLICY");
     const char *sp = getenv("FLS_STATIC_PCT");
     const char *tp = getenv("FLS_TAIL_PIECES");
@@ -802,7 +866,15 @@ int decode_policy() {
     // code-parallel kernel) changes the descriptors: fold it in too
     const char *sg = getenv("FLS_FSST_SEG");
     const int noseg = sg && atoi(sg) == 0 ? POLICY_FSST_NOSEG : 0;
-    return ((e ? (atoi(e) & 0xFF) : 0) | noseg) | pct << 8 | pieces << 16 | bpc << 24;
+    // guided tail (guided_split): FLS_GUIDED_MIN_VECS = smallest piece in
+    // vectors (bits 32-39, 0 = whole chunks only), FLS_GUIDED_FACTOR = pieces
+    // per wave of the remaining work (bits 40-47)
+    const char *gm = getenv("FLS_GUIDED_MIN_VECS");
+    const char *gf = getenv("FLS_GUIDED_FACTOR");
+    const int64_t gmin = gm ? std::min(64, std::max(0, atoi(gm))) : kGuidedMinVecs;
+    const int64_t gfac = gf ? std::min(255, std::max(1, atoi(gf))) : kGuidedFactor;
+    return (int64_t)(((e ? (atoi(e) & 0xFF) : 0) | noseg) | pct << 8 | pieces << 16 | bpc << 24) | gmin << 32 |
+           gfac << 40;
 }
 
 // Policy for one launch: the default (no distribution bits) switches to the
@@ -811,7 +883,7 @@ int decode_policy() {
 // waves), where whole-chunk work items would leave most waves idle.  Large
 // launches keep the work queue: same-buffer A/B on SF100 lineitem, c3 and c4
 // found the split no faster than the queue (profiles/r1/abenv_bal_*.txt).
-int launch_policy(int policy, const std::vector<DevChunk> &v, DecodeGeom &geom) {
+int64_t launch_policy(int64_t policy, const std::vector<DevChunk> &v, DecodeGeom &geom) {
     if (policy & (POLICY_STATIC | POLICY_BALANCED | POLICY_QUEUE)) return policy;
     size_t nmain = 0;
     for (const DevChunk &d : v) nmain += d.enc != ENC_FSST;
@@ -822,7 +894,7 @@ int launch_policy(int policy, const std::vector<DevChunk> &v, DecodeGeom &geom) 
 // FSST chunks go last (their own kernels: string-parallel ones first, then
 // code-parallel ones, each group numbering its vectors through vec_base);
 // returns how many lead (main kernel) and the FSST counts
-uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int policy) {
+uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int64_t policy) {
     auto mid = std::stable_partition(v.begin(), v.end(), [](const DevChunk &d) { return d.enc != ENC_FSST; });
     std::stable_sort(mid, v.end(), [](const DevChunk &a, const DevChunk &b) {
         return fsst_group(a.vbits) < fsst_group(b.vbits);
@@ -852,11 +924,17 @@ uint32_t order_for_launch(std::vector<DevChunk> &v, FsstCounts *fc, int policy) 
 // Append the balanced split of the main chunks to the descriptor list (as
 // extra DevChunk slots, so it uploads with it); plan.waves == 0 when the
 // policy does not split.
-SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const DecodeGeom &geom, int policy) {
-    if (!(policy & POLICY_BALANCED) || nmain == 0) return SplitPlan();
+SplitPlan append_split(std::vector<DevChunk> &list, uint32_t nmain, const DecodeGeom &geom, int64_t policy) {
+    if (nmain == 0) return SplitPlan();
     std::vector<uint32_t> pos;
-    const SplitPlan plan = balanced_split(list.data(), nmain, decode_waves(geom), (policy >> 8) & 0xFF,
-                                          (policy >> 16) & 0xFF, pos);
+    SplitPlan plan;
+    if (policy & POLICY_BALANCED)
+        plan = balanced_split(list.data(), nmain, decode_waves(geom), (policy >> 8) & 0xFF, (policy >> 16) & 0xFF, pos);
+    else if (!(policy & (POLICY_STATIC | POLICY_NO_LPT)) && ((policy >> 32) & 0xFF))
+        plan = guided_split(list.data(), nmain, decode_waves(geom), (uint32_t)((policy >> 40) & 0xFF),
+                            (uint32_t)((policy >> 32) & 0xFF), pos);
+    else
+        return SplitPlan();
     const size_t k = list.size();
     list.resize(k + (pos.size() * 4 + sizeof(DevChunk) - 1) / sizeof(DevChunk));
     memcpy(list.data() + k, pos.data(), pos.size() * 4);
@@ -893,6 +971,9 @@ struct OverlapSplit {
     // index mod 32 is < m, FSST on the others, each kind alone on its CUs
     // (0 = the co-resident split above)
     int cu_split = 0;
+    // FLS_OVERLAP_GUIDED=1: the overlapped decode grids drain the guided plan's
+    // items (whole chunks, then pieces) instead of whole chunks
+    bool guided = false;
 };
 OverlapSplit overlap_split() {
     OverlapSplit o;
@@ -901,6 +982,7 @@ OverlapSplit overlap_split() {
     if (const char *e = getenv("FLS_OVERLAP_FSST_WPC")) o.fsst_wpc = std::max(0, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_MIN_VECS_PER_CU")) o.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
     if (const char *e = getenv("FLS_OVERLAP_DECODE_PRIO")) o.decode_prio = std::min(3, std::max(0, atoi(e)));
+    if (const char *e = getenv("FLS_OVERLAP_GUIDED")) o.guided = atoi(e) != 0;
     return o;
 }
 
@@ -928,7 +1010,7 @@ OverlapSplit overlap_split() {
 // (fls_fsst.hip), the experiment library every variant (make lab).  A stale
 // tuning variable fails the decode with FLS_ERR_CONFIG instead of running a
 // kernel it did not ask for.
-int fsst_config_check(int policy) {
+int fsst_config_check(int64_t policy) {
     int variant = kFsstDefault;
     const char *fv = getenv("FLS_FSST_VARIANT");
     if (fv) {
@@ -1020,9 +1102,12 @@ hipError_t launch_cu_split(const DevChunk *d_chunks, uint32_t nmain, const FsstC
 }
 
 hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal, const FsstCounts &fc,
-                      uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int policy,
+                      uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream, uint32_t *d_queue, int64_t policy,
                       SplitPlan plan, const SideStream *side = nullptr) {
+    // a guided plan only orders the serial launch: the overlapped and
+    // CU-split launches drain whole chunks from a queue several grids share
     const uint32_t *d_split = plan.waves ? reinterpret_cast<const uint32_t *>(d_chunks + ntotal) : nullptr;
+    const bool balanced = d_split && !plan.guided;
     const bool sp = (policy & POLICY_FSST_SP) != 0;
     const OverlapSplit ov = overlap_split();
     FsstLaunch how[kFsstGroups];
@@ -1043,12 +1128,12 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const uint64_t fsst_vecs = fc.total_vecs();
-    if (ov.cu_split > 0 && side && side->stream && nmain > 0 && fsst_vecs > 0 && !d_split && !sp &&
+    if (ov.cu_split > 0 && side && side->stream && nmain > 0 && fsst_vecs > 0 && !balanced && !sp &&
         !(policy & POLICY_STATIC))
         return launch_cu_split(d_chunks, nmain, fc, d_err, geom, stream, d_queue, const_cast<SideStream *>(side),
                                ov, cus, how, launch_group);
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
-                         fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !d_split && !sp &&
+                         fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !balanced && !sp &&
                          !(policy & POLICY_STATIC);
     hipError_t e = hipSuccess;
     if (overlap) {
@@ -1066,12 +1151,15 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
             narrow_how[g].waves_per_cu = ov.fsst_wpc;
         }
         // main stream: narrow decode, then full FSST
+        // (a guided plan: both decode grids drain its items from the shared queue)
+        const uint32_t *gs = d_split && plan.guided && ov.guided ? d_split : nullptr;
+        const SplitPlan gp = gs ? plan : SplitPlan();
         if (e == hipSuccess)
-            e = launch_decode(d_chunks, nmain, d_err, narrow, stream, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
+            e = launch_decode(d_chunks, nmain, d_err, narrow, stream, d_queue, gs, gp, true, ov.decode_prio);
         // side stream: narrow FSST, then full decode
         for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, side->stream, narrow_how[g]);
         if (e == hipSuccess)
-            e = launch_decode(d_chunks, nmain, d_err, geom, side->stream, d_queue, nullptr, SplitPlan(), true, ov.decode_prio);
+            e = launch_decode(d_chunks, nmain, d_err, geom, side->stream, d_queue, gs, gp, true, ov.decode_prio);
         for (int g = 0; g < kFsstGroups && e == hipSuccess; ++g) e = launch_group(g, stream, how[g]);
         if (e == hipSuccess) e = hipEventRecord(side->join, side->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join, 0);
@@ -1169,34 +1257,76 @@ bool rowgroup_may_match(const fls_table *t, uint32_t rg, const std::vector<HostT
 }
 
 // The file's resident image on GPU dev (made on first use), or none: a table
-// not read from a file, FLS_SCAN_RESIDENT_MB=0, a file over that budget
-// (default 65,536 MB) or over half the GPU's free memory.
-std::shared_ptr<DevImage> resident_image(fls_table *t, int dev) {
+// not read from a file, FLS_SCAN_RESIDENT_MB=0, or no room in the GPU's image
+// budget (FLS_SCAN_RESIDENT_MB, default 65,536 MB, over every cached file)
+// after evicting the least recently used images no running scan holds.  The
+// image holds the file bytes of shard g of G: the row groups this GPU owns
+// when the whole table is split over the connection's GPUs.
+std::shared_ptr<DevImage> resident_image(fls_table *t, int dev, uint32_t g, uint32_t G) {
     if (!t->mapped) return nullptr;
-    const char *e = getenv("FLS_SCAN_RESIDENT_MB");
-    const uint64_t budget = (uint64_t)(e ? std::max(0L, atol(e)) : 65536L) << 20;
-    const uint64_t need = t->len + kImagePad;
-    if (need > budget) return nullptr;
-    std::lock_guard<std::mutex> lk(t->mapped->dev_mu);
-    auto &p = t->mapped->dev_img[dev];
-    if (p) return p;
-    size_t free_b = 0, total_b = 0;
-    if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess || need > free_b / 2) {
+    const uint64_t budget = resident_budget();
+    const uint32_t N = (uint32_t)t->meta.rgs.size();
+    G = std::max(1u, G);
+    const uint32_t r0 = (uint32_t)((uint64_t)N * g / G), r1 = (uint32_t)((uint64_t)N * (g + 1) / G);
+    if (budget == 0 || r0 >= r1) return nullptr;
+    uint64_t lo, hi;
+    rg_byte_range(t->meta, r0, r1, lo, hi);
+    if (hi <= lo) return nullptr;
+    const uint64_t need = hi - lo + kImagePad;
+    ImageRegistry &R = image_registry();
+    ResidentSet<DevImage>::Evicted ev;  // freed under the lock: the new image may need their memory
+    std::lock_guard<std::mutex> lk(R.mu);
+    uint64_t flo = 0, fhi = 0;
+    if (auto p = R.set.find(t->mapped.get(), dev, &flo, &fhi)) {
+        // made for another split of the table: batches outside it stream
+        if (flo <= lo && hi <= fhi) return p;
+        if (p.use_count() > 2) return p;  // another scan decodes from it
+        p.reset();
+        R.set.drop_one(t->mapped.get(), dev, ev);
+        ev.clear();
+    }
+    if (!R.set.make_room(dev, need, budget, ev)) return nullptr;
+    ev.clear();
+    if (hipSetDevice(dev) != hipSuccess) {
         (void)hipGetLastError();
-        t->mapped->dev_img.erase(dev);
         return nullptr;
+    }
+    // leave at least half of the free HBM to the scans' own buffers: evict
+    // more idle images (least recent first) while the new one would not
+    for (;;) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        if (need <= free_b / 2) break;
+        if (!R.set.evict_lru(dev, ev)) return nullptr;
+        ev.clear();
     }
     auto di = std::make_shared<DevImage>();
-    if (di->buf.alloc(dev, need) != hipSuccess) {
+    di->dev = dev;
+    hipError_t e = hipMalloc((void **)&di->p, need);
+    if (e == hipErrorOutOfMemory && R.set.release_idle(dev, ev) > 0) {
         (void)hipGetLastError();
-        t->mapped->dev_img.erase(dev);
+        ev.clear();
+        e = hipMalloc((void **)&di->p, need);
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        di->p = nullptr;
         return nullptr;
     }
-    di->nrg = (uint32_t)t->meta.rgs.size();
-    di->present.reset(new std::atomic<uint8_t>[di->nrg]);
-    for (uint32_t r = 0; r < di->nrg; ++r) di->present[r].store(0);
-    p = di;
-    return p;
+    di->lo = lo;
+    di->hi = hi;
+    di->nrg = N;
+    di->present.reset(new std::atomic<uint8_t>[N]);
+    for (uint32_t r = 0; r < N; ++r) di->present[r].store(0);
+    R.set.insert(t->mapped.get(), dev, lo, hi, need, di);
+    if (debug_enabled())
+        fprintf(stderr, "DEBUG: resident image of row groups [%u, %u) on GPU %d: %llu bytes (%llu of %llu MB in use)\n",
+                r0, r1, dev, (unsigned long long)need, (unsigned long long)(R.set.used(dev) >> 20),
+                (unsigned long long)(budget >> 20));
+    return di;
 }
 
 int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uint8_t *col_mask, uint32_t rg0,
@@ -1276,7 +1406,12 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         d.next_p = d.p0;
         d.rg0 = d.p0 < d.p1 ? s.rgs[d.p0] : 0;
         d.rg1 = d.p0 < d.p1 ? s.rgs[d.p1 - 1] + 1 : 0;
-        d.dimg = resident_image(t, d.dev);
+        {   // the image holds this GPU's shard of the table over the connection's GPUs
+            const auto it = std::find(t->devices.begin(), t->devices.end(), d.dev);
+            const bool in = it != t->devices.end();
+            d.dimg = resident_image(t, d.dev, in ? (uint32_t)(it - t->devices.begin()) : 0u,
+                                    in ? (uint32_t)t->devices.size() : 1u);
+        }
         int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off, d.h_strtab);
         if (rc) return rc;
         if (s.dict_codes && !d.ident.p) {
@@ -1466,18 +1601,19 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     rg_byte_range(t->meta, sl.rg0, sl.rg0 + sl.nrg, lo, hi);
     sl.in_base = lo;
     DevImage *di = d.dimg.get();
+    if (di && (lo < di->lo || hi > di->hi)) di = nullptr;  // outside this GPU's image: streamed
     bool have = di != nullptr;
     for (uint32_t r = sl.rg0; have && r < sl.rg0 + sl.nrg; ++r) have = di->present[r].load(std::memory_order_acquire) != 0;
     sl.upload_resident.store(di != nullptr && !have);
     if (have) {
-        sl.in_dev = di->buf.p + lo;
+        sl.in_dev = di->p + (lo - di->lo);
         if (getenv("FLS_DEBUG"))
             fprintf(stderr, "DEBUG: scan batch of row groups [%u, %u) decoded from the HBM-resident image\n", sl.rg0,
                     sl.rg0 + sl.nrg);
     } else {
         uint8_t *dst;
         if (di) {
-            dst = di->buf.p + lo;
+            dst = di->p + (lo - di->lo);
         } else {
             HIP_TRY(sl.d_in.alloc(d.dev, hi - lo + kImagePad));
             dst = sl.d_in.p;
@@ -1631,7 +1767,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         }
     }
     FsstCounts fsst;
-    const int policy = launch_policy(decode_policy(), list, bc.geom);
+    const int64_t policy = launch_policy(decode_policy(), list, bc.geom);
     const uint32_t nmain = order_for_launch(list, &fsst, policy);
     const size_t k = list.size();
     const SplitPlan plan = append_split(list, nmain, bc.geom, policy);
@@ -1901,6 +2037,7 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         }
     }
     bool refill = false;
+    std::shared_ptr<DevImage> done_img;  // dropped outside s.mu
     {
         std::lock_guard<std::mutex> lk(s.mu);
         s.out.emplace_back(rg, hb);
@@ -1910,6 +2047,13 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
             const int c = claim_batch(t, s, d, si);
             set_scan_error(s, c < 0 ? c : 0);
             refill = c == 1;
+            // this GPU's last batch is decoded: the scan no longer holds its
+            // resident image, which becomes evictable (the table may stay open)
+            if (c == 0 && d.next_p >= d.p1 && d.dimg) {
+                bool idle = true;
+                for (int k = 0; k < s.nslots; ++k) idle = idle && !d.slots[k].busy && !d.slots[k].filling;
+                if (idle) done_img = std::move(d.dimg);
+            }
         }
         s.cv.notify_all();
     }
@@ -2071,6 +2215,21 @@ int fls_connect(const int *devices, int ndevices, fls_connection **out) {
 }
 
 void fls_disconnect(fls_connection *conn) { delete conn; }
+
+int fls_release_device_memory(int device, uint64_t *freed_bytes) {
+    const uint64_t b = release_idle_images(device < 0 ? -1 : device);
+    if (freed_bytes) *freed_bytes = b;
+    return 0;
+}
+
+int fls_resident_info(int device, uint64_t *bytes, uint32_t *images) {
+    ImageRegistry &R = image_registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    const int dv = device < 0 ? -1 : device;
+    if (bytes) *bytes = R.set.used(dv);
+    if (images) *images = (uint32_t)R.set.count(dv);
+    return 0;
+}
 
 int fls_connection_trim(fls_connection *conn, uint64_t keep_bytes, uint64_t *idle_bytes) {
     if (!conn) return fail(FLS_ERR_ARG, "fls_connection_trim: NULL connection");
@@ -2389,7 +2548,7 @@ int upload_part(fls_table *t, Resident &r) {
 int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     HIP_TRY(hipSetDevice(r.dev));
-    const int policy = decode_policy();
+    const int64_t policy = decode_policy();
     if (mask != r.mask || r.h_chunks.empty() || policy != r.policy) {
         // (re)build the launch descriptor list: column-major task order, so
         // concurrent waves stream one column's consecutive row groups
@@ -2408,7 +2567,7 @@ int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask) {
                                                r.h_heap[c].p ? r.h_heap[c].p + ho : nullptr));
             }
         }
-        const int lpol = launch_policy(policy, chunks, bc.geom);
+        const int64_t lpol = launch_policy(policy, chunks, bc.geom);
         r.nmain = order_for_launch(chunks, &r.fsst, lpol);
         r.policy = policy;
         r.lpolicy = lpol;

@@ -26,10 +26,11 @@ void FastlaneVersionFn(DataChunk &, ExpressionState &, Vector &result) {
     result.SetVectorType(VectorType::CONSTANT_VECTOR);
 }
 // SELECT fastlane_release_memory(): not in the reference.  Hands the pinned
-// host memory the GPU scan keeps between queries back to the OS; returns the
-// pinned bytes still held (0).
+// host memory the GPU scan keeps between queries back to the OS and frees the
+// HBM-resident file images no running scan uses; returns the bytes of both
+// still held (0 when no scan runs).
 void FastlaneReleaseMemoryFn(DataChunk &, ExpressionState &, Vector &result) {
-    const uint64_t left = ext_fastlane::TrimSharedConnections(0);
+    const uint64_t left = ext_fastlane::ReleaseMemory();
     result.SetValue(0, Value::BIGINT((int64_t)left));
     result.SetVectorType(VectorType::CONSTANT_VECTOR);
 }

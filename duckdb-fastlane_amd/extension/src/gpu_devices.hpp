@@ -72,5 +72,15 @@ inline uint64_t TrimSharedConnections(uint64_t keep_bytes) {
     return left;
 }
 
+// fastlane_release_memory(): the idle pinned host memory (above) and every
+// HBM-resident file image no running scan uses (fls_release_device_memory);
+// returns the bytes of both still held.
+inline uint64_t ReleaseMemory() {
+    uint64_t left = TrimSharedConnections(0), freed = 0, resident = 0;
+    fls_release_device_memory(-1, &freed);
+    if (fls_resident_info(-1, &resident, nullptr) == 0) left += resident;
+    return left;
+}
+
 }  // namespace ext_fastlane
 }  // namespace duckdb

@@ -154,6 +154,17 @@ void fls_disconnect(fls_connection *conn);
  * (FLS_IDLE_PINNED_MB, default 512).  Not in the reference: a long-lived
  * host (DuckDB) uses it to hand page-locked memory back. */
 int fls_connection_trim(fls_connection *conn, uint64_t keep_bytes, uint64_t *idle_bytes);
+/* HBM-resident compressed images (the scan pipeline keeps a scanned file's
+ * bytes in HBM so warm queries skip the H2D): one byte budget per GPU over
+ * every cached file (FLS_SCAN_RESIDENT_MB, default 65,536), least recently
+ * used images evicted first, never one a running scan uses.  Not in the
+ * reference, whose closeFile (src/fastlanes_facade.cpp:202-210) releases
+ * everything it holds.
+ * fls_release_device_memory: free every image no running scan uses on
+ * device (-1: every GPU); freed_bytes (may be NULL) receives the bytes freed.
+ * fls_resident_info: the images' bytes and count on device (-1: every GPU). */
+int fls_release_device_memory(int device, uint64_t *freed_bytes);
+int fls_resident_info(int device, uint64_t *bytes, uint32_t *images);
 
 /* Connection::read_fls(): parse footer + schema (no GPU work). */
 int fls_read_fls(fls_connection *conn, const char *path, fls_table **out);

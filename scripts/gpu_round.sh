@@ -25,6 +25,10 @@
 #               COPY (read_fastlanes) TO (FORMAT fls), env arms interleaved
 #               (scripts/writer_bench.py --copy-only; arms name:VAR=v,...;name2:...)
 #   launcher2   bench.py --gpus 2 rehearsal (both ranks on the one GPU)
+#   build:<t>   make <t> on the box (lab / exp / trace: the experiment and
+#               timing libraries are not pushed, .gpurunignore)
+#   wavetrace:<workload>:<scale>:<cols>[:<env>]  per-wave timeline of one
+#               main decode launch (needs build:trace first)
 # Results go to gpurun_out/<mode>_<tag>.*; copy what is judged to profiles/.
 TAG=${1:?tag}
 shift
@@ -101,6 +105,13 @@ for mode in "$@"; do
     step 900 $O/copy_${TAG}_${wl}_${sc}.txt python scripts/writer_bench.py --copy-only --workload "$wl" \
         --scale "$sc" --reps "$reps" --arms "$arms" || exit $?
     grep median $O/copy_${TAG}_${wl}_${sc}.txt ;;
+  build:*)
+    step 600 $O/build_${mode#build:}_$TAG.log make -C duckdb-fastlane_amd -j16 "${mode#build:}" || exit $? ;;
+  wavetrace:*)
+    IFS=: read -r _ wl sc cols env <<< "$mode"
+    step 300 $O/wave_trace_${TAG}_${wl}_${sc}.txt env FLS_LIB=libflsgpu_trace.so python scripts/wave_trace.py \
+        --workload "$wl" --scale "$sc" --cols "$cols" --env "$env" --out $O/wave_trace_${TAG}.npz || exit $?
+    head -20 $O/wave_trace_${TAG}_${wl}_${sc}.txt ;;
   launcher2)
     timeout -k 10 600 python bench.py --gpus 2 --scale 1 --steps 5 --cpu-seconds 0 --e2e-scale 0 --no-traffic \
         > $O/bench_gpus2_$TAG.json 2> $O/bench_gpus2_$TAG.log

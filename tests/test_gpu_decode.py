@@ -242,8 +242,10 @@ def test_small_rowgroups_decode_and_scan(fl, ref, gpu, monkeypatch, rgsz):
 # default (0: small launches like this one take the balanced split), the work
 # queue of whole chunks (64), static grid-stride (1), the balanced split of
 # vector ranges (32: a chunk may be cut between waves, including inside the
-# ragged last row group) with and without dynamic tail pieces.  Every policy
-# must decode identically.
+# ragged last row group) with and without dynamic tail pieces, and the guided
+# queue (64 + FLS_GUIDED_MIN_VECS: whole chunks, then ever smaller pieces,
+# cut inside chunks and the ragged last row group).  Every policy must decode
+# identically.
 @pytest.mark.parametrize("env", [
     {"FLS_DECODE_POLICY": "0"},
     {"FLS_DECODE_POLICY": "64"},
@@ -252,7 +254,12 @@ def test_small_rowgroups_decode_and_scan(fl, ref, gpu, monkeypatch, rgsz):
     {"FLS_DECODE_POLICY": "32", "FLS_STATIC_PCT": "70", "FLS_TAIL_PIECES": "3"},
     {"FLS_DECODE_POLICY": "32", "FLS_STATIC_PCT": "0", "FLS_TAIL_PIECES": "1"},
     {"FLS_DECODE_POLICY": "32", "FLS_BLOCKS_PER_CU": "1"},
-], ids=["default", "queue", "static", "balanced", "balanced_tail70", "tail_only", "balanced_1blk"])
+    {"FLS_DECODE_POLICY": "64", "FLS_GUIDED_MIN_VECS": "0"},
+    {"FLS_DECODE_POLICY": "64", "FLS_GUIDED_MIN_VECS": "1", "FLS_GUIDED_FACTOR": "8"},
+    {"FLS_DECODE_POLICY": "64", "FLS_GUIDED_MIN_VECS": "8", "FLS_GUIDED_FACTOR": "1"},
+    {"FLS_DECODE_POLICY": "64", "FLS_GUIDED_MIN_VECS": "3", "FLS_GUIDED_FACTOR": "2", "FLS_BLOCKS_PER_CU": "1"},
+], ids=["default", "queue", "static", "balanced", "balanced_tail70", "tail_only", "balanced_1blk", "queue_chunks",
+        "guided_1", "guided_8", "guided_3_1blk"])
 def test_work_distribution_policies(fl, ref, gpu, monkeypatch, env):
     for k, v in env.items():
         monkeypatch.setenv(k, v)

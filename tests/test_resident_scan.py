@@ -56,3 +56,82 @@ def test_rewritten_file_is_not_served_from_a_stale_image(ext, fl, gpu, tmpfile):
     b = ext.scan_count("read_fastlanes", p, threads=2)[:2]
     assert b != a and b[0] == fl.gen_nrows("lineitem", 0.03)
     assert ext.scan_count("read_fastlanes", p, threads=2)[:2] == b
+
+
+def _resident(fl, dev=0):
+    return fl.Connection.resident_info(dev)
+
+
+def test_two_files_over_budget_evict_the_older(ext, fl, gpu, tmpfile, monkeypatch):
+    """One HBM budget per GPU over every cached file: with
+    room for one image, scanning a second file evicts the first one's (the
+    least recently used image no scan holds), and the first file then scans
+    bit-exactly again from its bytes on disk."""
+    a, b = tmpfile("budget_a.fls"), tmpfile("budget_b.fls")
+    fl.gen_image("lineitem_full", 0.1).write(a)
+    fl.gen_image("lineitem_full", 0.11).write(b)
+    import os
+    big = max(os.path.getsize(a), os.path.getsize(b))
+    monkeypatch.setenv("FLS_SCAN_RESIDENT_MB", "0")
+    ref_a = ext.scan_count("read_fastlanes", a, threads=4)[:2]
+    ref_b = ext.scan_count("read_fastlanes", b, threads=4)[:2]
+    fl.Connection.release_device_memory()
+    assert _resident(fl) == (0, 0)
+    # room for the larger file, not for both
+    monkeypatch.setenv("FLS_SCAN_RESIDENT_MB", str(big // (1 << 20) + 2))
+    assert ext.scan_count("read_fastlanes", a, threads=4)[:2] == ref_a
+    bytes_a, n = _resident(fl)
+    assert n == 1 and bytes_a >= os.path.getsize(a) // 2
+    assert ext.scan_count("read_fastlanes", b, threads=4)[:2] == ref_b
+    bytes_b, n = _resident(fl)
+    assert n == 1 and bytes_b != bytes_a          # a's image made room for b's
+    assert ext.scan_count("read_fastlanes", a, threads=4)[:2] == ref_a   # after eviction: from disk again
+    assert _resident(fl) == (bytes_a, 1)
+    assert ext.scan_count("read_fastlanes", a, threads=4)[:2] == ref_a   # warm, from its image
+    # a budget with room for both keeps both
+    monkeypatch.setenv("FLS_SCAN_RESIDENT_MB", str(2 * (big // (1 << 20)) + 4))
+    assert ext.scan_count("read_fastlanes", b, threads=4)[:2] == ref_b
+    assert _resident(fl) == (bytes_a + bytes_b, 2)
+    fl.Connection.release_device_memory()
+
+
+def test_release_returns_the_hbm(ext, fl, gpu, tmpfile):
+    """fastlane_release_memory() frees the resident images as well as the idle
+    pinned host memory: the device's free memory (hipMemGetInfo) grows by
+    the images' bytes, and the next scan is still exact."""
+    import torch
+    p = tmpfile("release.fls")
+    fl.gen_image("lineitem_full", 0.2).write(p)
+    fl.Connection.release_device_memory()
+    first = ext.scan_count("read_fastlanes", p, threads=4)[:2]
+    held, n = _resident(fl)
+    assert n == 1 and held > 0
+    free_before = torch.cuda.mem_get_info(0)[0]
+    assert ext.scalar0("fastlane_release_memory") == "0"
+    assert _resident(fl) == (0, 0)
+    free_after = torch.cuda.mem_get_info(0)[0]
+    assert free_after - free_before >= held - (4 << 20), (free_before, free_after, held)
+    assert ext.scan_count("read_fastlanes", p, threads=4)[:2] == first
+
+
+def test_image_holds_only_this_gpus_shard(ext, fl, gpu, tmpfile, monkeypatch):
+    """A GPU's image holds its shard of the table: with the table
+    split over two devices (GPU 0 listed twice), each image is about half
+    the file, and both decode exactly."""
+    import os
+    p = tmpfile("shard.fls")
+    fl.gen_image("lineitem", 0.2).write(p)
+    fl.Connection.release_device_memory()
+    monkeypatch.setenv("FLS_SCAN_RESIDENT_MB", "0")
+    ref = ext.scan_count("read_fastlanes", p, threads=4)[:2]
+    monkeypatch.delenv("FLS_SCAN_RESIDENT_MB")
+    con = fl.Connection([0, 0])
+    t = con.read_fls(p)
+    sch = t.schema()
+    rows = sum(len(cols[0]) // sch[0][4] for _, cols in t.scan(cols=[0]))
+    assert rows == ref[0]
+    held, n = _resident(fl)
+    size = os.path.getsize(p)
+    assert n == 1 and held < 0.6 * size      # (both parts are GPU 0: one image, its first shard)
+    t.close()
+    fl.Connection.release_device_memory()
