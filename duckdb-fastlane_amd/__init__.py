@@ -156,6 +156,7 @@ _sig("fls_encode_slot_bytes", C.c_uint64, C.c_uint8, C.c_uint8, C.c_uint32)
 _sig("fls_encode_device", C.c_int, C.c_int, C.c_uint8, C.c_uint8, _P, C.c_uint64, C.c_uint32, _P,
      C.POINTER(C.c_uint64), C.POINTER(C.c_float))
 _sig("fls_writer_finish_file", C.c_int, _P, C.c_char_p)
+_sig("fls_writer_set_output", C.c_int, _P, C.c_char_p)
 _sig("fls_writer_finish_image", C.c_int, _P, C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_image_free", None, _P)
 _sig("fls_gen_nrows", C.c_int64, C.c_char_p, C.c_double, C.c_uint64)
@@ -260,7 +261,7 @@ def gen_dict_string(workload: str, col: int, code: int) -> str | None:
 
 # --- writer ----------------------------------------------------------------
 def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: int = -1,
-                batch: int = 1, threads: int = 0, path: str | None = None) -> Image | None:
+                batch: int = 1, threads: int = 0, path: str | None = None, stream: bool = False) -> Image | None:
     """columns: list of (name, type, values, encoding[, width, scale]).
     values: numpy int array for integer types, float array for FLOAT/DOUBLE
     (stored bit-exactly), list of str/bytes for VARCHAR.  NULLs: None entries
@@ -270,7 +271,9 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
     batch > 1: row groups go in `batch` at a time (fls_writer_add_rowgroups;
     same bytes).  threads > 0: writer threads (fls_writer_set_threads).
     path: the file is written there instead (fls_writer_finish_file: the
-    same bytes, chunks written in parallel, no image); returns None."""
+    same bytes, chunks written in parallel, no image); returns None.
+    stream: with path, row groups go to the file as they are encoded
+    (fls_writer_set_output; the same bytes)."""
     w = _lib.fls_writer_new(row_offset)
     try:
         _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))
@@ -278,6 +281,8 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
             _check(_lib.fls_writer_set_threads(w, threads))
         if device >= 0:
             _check(_lib.fls_writer_set_device(w, device))
+        if stream and path is not None:
+            _check(_lib.fls_writer_set_output(w, str(path).encode()))
         n = None
         prepped = []
         for spec in columns:

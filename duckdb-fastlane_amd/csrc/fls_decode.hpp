@@ -151,6 +151,19 @@ struct FsstLaunch {
 // (DevChunk.vec_base numbers them) (fls_fsst.hip).
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                        hipStream_t stream, const FsstLaunch &how);
+// The fused launch (fls_fsst.hip fused_kernel): the main decode of nmain
+// chunks and the segmented FSST decode of nfsst chunks (nfvecs vectors, all
+// of one kind: small = every string <= 255 bytes) in one kernel of 1-wave
+// blocks that pull from two queues (d_queues[0] main chunks, [1] FSST
+// pieces; zeroed by the launch).
+struct FusedLaunch {
+    uint32_t fsst_per16 = 5;   // of every 16 waves, how many start on the FSST queue
+    uint32_t piece = 2;        // FSST vectors per queue item
+    int waves_per_cu = 0;      // 0: as many as fit
+};
+hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
+                        uint32_t nfvecs, bool small, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,
+                        uint32_t *d_queues, const FusedLaunch &how);
 // Whether this build holds the FSST kernel for (variant, segmented, bytes per
 // lane): the product build only each kernel's default (kFsstDefault, 8 bytes
 // per lane for the code-parallel one); the experiment library (`make lab`,

@@ -38,6 +38,7 @@
 #include <cstdlib>
 
 #include "fls_decode.hpp"
+#include "fls_decode_dev.hpp"
 #include "fls_format.hpp"
 #include "fls_unpack.hpp"
 
@@ -1133,6 +1134,82 @@ hipError_t launch_kind2(const DevChunk *d, uint32_t nchunks, uint32_t nvecs, uin
 }
 
 // ============================================================================
+// 4. Fused kernel: the main decode (fls_decode_dev.hpp) and the segmented FSST
+// decode in ONE launch of 1-wave blocks.  The main decode is HBM-bound and
+// the FSST decode VALU / LDS-bound, so they share each CU better than either
+// runs alone; run one after the other, each kernel's tail idles the CUs and
+// the second kernel waits for the first one's drain.  Every wave pulls from
+// two queues: whole main chunks (the host's largest-output-first order) and
+// FSST pieces of `piece` vectors; fsst_per16 of every 16 waves start on the
+// FSST queue, the rest on the main one, and a wave whose queue runs dry
+// moves to the other, so both end together whatever the mix.  LDS per wave:
+// the larger of the two kernels' (dynamic LDS from address 0, as the FSST
+// code addresses it), registers: the main decode's budget (4 waves / SIMD).
+// ============================================================================
+template <bool SMALL>
+__global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict__ mchunks, uint32_t nmain,
+                                                      const DevChunk *__restrict__ fchunks, uint32_t nfsst,
+                                                      uint32_t nfvecs, uint32_t *__restrict__ err,
+                                                      uint32_t *__restrict__ queues, uint32_t p_bytes,
+                                                      uint32_t v_bytes, uint32_t piece, uint32_t fsst_per16) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    if ((uint32_t)(size_t)lds_raw != 0u) {  // LDS addressed from 0 (fsst_kernel)
+        if (threadIdx.x == 0) atomicOr(err, KERR_LDS_BASE);
+        return;
+    }
+    auto main_part = [&]() {
+        for (;;) {
+            uint32_t ci = 0;
+            if (__lane_id() == 0) ci = atomicAdd(queues, 1u);
+            ci = uni(ci);
+            if (ci >= nmain) break;
+            const uint32_t nvec = gptr(mchunks)[ci].nvec;
+            if (nvec) dec::decode_chunk(mchunks + ci, 0u, p_bytes, v_bytes, err, nvec << 8);
+        }
+    };
+    auto fsst_part = [&]() {
+        fsst_range<Kind::Seg, SMALL, true>(fchunks, nfsst, nfvecs, 0, 0, queues + 1, piece, (lu8 *)(size_t)0, err);
+        wave_sync();
+    };
+    if ((blockIdx.x & 15) < fsst_per16) {
+        fsst_part();
+        main_part();
+    } else {
+        main_part();
+        fsst_part();
+    }
+}
+
+template <bool SMALL>
+hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
+                          uint32_t nfvecs, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,
+                          uint32_t *d_queues, const FusedLaunch &how) {
+    auto kern = fused_kernel<SMALL>;
+    const uint32_t shmem = std::max<uint32_t>(geom.p_bytes + geom.v_bytes, SegLds<SMALL>::kWave);
+    static const bool lds_at_zero = [kern] {
+        hipFuncAttributes a{};
+        return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(kern)) == hipSuccess && a.sharedSizeBytes == 0;
+    }();
+    if (!lds_at_zero) return hipErrorInvalidDeviceFunction;
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, shmem) != hipSuccess) per_cu = 1;
+    }
+    if (how.waves_per_cu > 0) per_cu = std::min(per_cu, how.waves_per_cu);
+    const int grid = cus * std::max(1, per_cu);
+    hipError_t e = hipMemsetAsync(d_queues, 0, 2 * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    if (getenv("FLS_DEBUG"))
+        fprintf(stderr, "DEBUG: fused_kernel<%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u main chunks, %u FSST "
+                        "vectors in pieces of %u, %u of 16 waves FSST first\n",
+                SMALL ? "small" : "any", grid, per_cu, shmem, nmain, nfvecs, how.piece, how.fsst_per16);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), shmem, stream, d_main, nmain, d_fsst, nfsst, nfvecs, d_err,
+                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, how.piece), std::min(16u, how.fsst_per16));
+    return hipGetLastError();
+}
+
+// ============================================================================
 // 3. String-parallel kernel (chunks whose strings are all <= 255 bytes, both
 // decompressed and compressed: the host marks them, DevChunk.vbits = 1;
 // FLS_DECODE_POLICY bit 7).  Every string is compressed on its own and the
@@ -1402,6 +1479,14 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
 #endif
     }
     return false;
+}
+
+hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
+                        uint32_t nfvecs, bool small, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,
+                        uint32_t *d_queues, const FusedLaunch &how) {
+    if (nmain == 0 && nfsst == 0) return hipSuccess;
+    return small ? launch_fused_t<true>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream, d_queues, how)
+                 : launch_fused_t<false>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream, d_queues, how);
 }
 
 hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,

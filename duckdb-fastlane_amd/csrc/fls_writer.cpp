@@ -16,6 +16,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -26,6 +27,7 @@
 #include <vector>
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "../../include/flsgpu.h"
@@ -1302,12 +1304,207 @@ struct FileBuilder {
         // per column: the chunk's validity bitmaps (nvec x 128 B) when it has
         // a NULL, else empty; appended to the chunk by finish()
         std::vector<std::vector<uint64_t>> valid;
+        // per column: the chunk's final length once it was handed to the
+        // output stream (its bytes are gone then)
+        std::vector<uint64_t> flen;
         uint64_t chunk_len(size_t c) const {
+            if (!flen.empty()) return flen[c];
             const uint64_t n = chunks[c].size();
             return c < valid.size() && !valid[c].empty() ? ((n + 15) & ~15ull) + 8ull * valid[c].size() : n;
         }
     };
     std::vector<RG> rgs;
+
+    // ---- streamed output (fls_writer_set_output) ------------------------------
+    // Row groups whose chunks are all encoded are handed, in order, to a
+    // thread that pwrite()s them at their final offsets in a temporary file in
+    // the destination's directory, so the file is written while later row
+    // groups encode instead of all at the end; finish writes the footer and
+    // renames the file over the destination (a failed or abandoned write
+    // leaves no partial file there).  Chunk bytes are freed once written.
+    struct Stream {
+        struct Job {
+            uint64_t at = 0, len = 0;
+            std::vector<uint8_t> bytes;
+            std::vector<uint64_t> valid;
+        };
+        int fd = -1;
+        std::string path, tmp;
+        uint64_t off = 256;              // next chunk's offset
+        size_t next_rg = 0;              // first row group not handed over yet
+        std::vector<uint64_t> offs;      // per chunk handed over (footer)
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv, room;
+        std::deque<Job> q;
+        uint64_t queued = 0;             // bytes waiting in q
+        bool stop = false;
+        int err = 0;                     // errno of a failed write
+        static constexpr uint64_t kMaxQueued = 512ull << 20;
+    };
+    std::unique_ptr<Stream> out;
+
+    static int pwrite_all(int fd, const void *p, uint64_t n, uint64_t at) {
+        const uint8_t *b = (const uint8_t *)p;
+        while (n > 0) {
+            const ssize_t k = ::pwrite(fd, b, std::min<uint64_t>(n, 1ull << 30), (off_t)at);
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) return errno ? errno : EIO;
+            b += k;
+            at += (uint64_t)k;
+            n -= (uint64_t)k;
+        }
+        return 0;
+    }
+    static std::string tmp_name(const std::string &path) {
+        return path + ".tmp." + std::to_string((long)getpid()) + "." +
+               std::to_string((unsigned long long)(uintptr_t)&path % 100000);
+    }
+    int open_stream(const char *path) {
+        if (out) return fail(FLS_ERR_STATE, "fls_writer_set_output: output already set");
+        if (!rgs.empty()) return fail(FLS_ERR_STATE, "fls_writer_set_output: after first row group");
+        auto st = std::make_unique<Stream>();
+        st->path = path;
+        st->tmp = tmp_name(st->path);
+        st->fd = ::open(st->tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (st->fd < 0) return fail(FLS_ERR_IO, "cannot create %s: %s", st->tmp.c_str(), strerror(errno));
+        uint8_t head[256] = {};
+        memcpy(head, kFileMagic, 8);
+        const uint64_t version = 1;
+        memcpy(head + 8, &version, 8);
+        if (const int e = pwrite_all(st->fd, head, sizeof(head), 0)) {
+            ::close(st->fd);
+            ::unlink(st->tmp.c_str());
+            return fail(FLS_ERR_IO, "write to %s: %s", st->tmp.c_str(), strerror(e));
+        }
+        Stream *sp = st.get();
+        st->th = std::thread([sp] {
+            static const uint8_t zeros[16] = {};
+            std::vector<uint8_t> tmp;
+            for (;;) {
+                Stream::Job j;
+                {
+                    std::unique_lock<std::mutex> lk(sp->mu);
+                    sp->cv.wait(lk, [&] { return sp->stop || !sp->q.empty(); });
+                    if (sp->q.empty()) return;
+                    j = std::move(sp->q.front());
+                    sp->q.pop_front();
+                }
+                int e = 0;
+                if (!sp->err) {
+                    const uint64_t padded = (j.len + 15) & ~15ull;
+                    if (!j.valid.empty()) {
+                        tmp.assign(padded, 0);
+                        memcpy(tmp.data(), j.bytes.data(), j.bytes.size());
+                        append_validity(tmp.data(), j.bytes.size(), j.len, j.valid);
+                        e = pwrite_all(sp->fd, tmp.data(), padded, j.at);
+                    } else {
+                        e = pwrite_all(sp->fd, j.bytes.data(), j.bytes.size(), j.at);
+                        if (!e && padded > j.bytes.size()) e = pwrite_all(sp->fd, zeros, padded - j.bytes.size(), j.at + j.bytes.size());
+                    }
+                }
+                std::lock_guard<std::mutex> lk(sp->mu);
+                if (e && !sp->err) sp->err = e;
+                sp->queued -= j.bytes.size();
+                sp->room.notify_all();
+            }
+        });
+        out = std::move(st);
+        return 0;
+    }
+    // hand the complete row groups from next_rg on to the stream (all: every
+    // row group must be complete -- after the GPU encoder's last batch)
+    int flush_stream(bool all) {
+        if (!out) return 0;
+        Stream &st = *out;
+        for (; st.next_rg < rgs.size(); ++st.next_rg) {
+            RG &r = rgs[st.next_rg];
+            bool done = true;
+            for (auto &ch : r.chunks) done = done && !ch.empty();
+            if (!done) {
+                if (all) return fail(FLS_ERR_STATE, "row group %zu incomplete at finish", st.next_rg);
+                break;
+            }
+            std::vector<uint64_t> lens(r.chunks.size());
+            for (size_t c = 0; c < r.chunks.size(); ++c) lens[c] = r.chunk_len(c);
+            for (size_t c = 0; c < r.chunks.size(); ++c) {
+                Stream::Job j;
+                j.at = st.off;
+                j.len = lens[c];
+                j.bytes = std::move(r.chunks[c]);
+                if (c < r.valid.size()) j.valid = std::move(r.valid[c]);
+                st.offs.push_back(st.off);
+                st.off += (lens[c] + 15) & ~15ull;
+                std::unique_lock<std::mutex> lk(st.mu);
+                st.room.wait(lk, [&] { return st.queued < Stream::kMaxQueued || st.err; });
+                st.queued += j.bytes.size();
+                st.q.push_back(std::move(j));
+                st.cv.notify_one();
+            }
+            r.flen = std::move(lens);
+            r.chunks.assign(r.chunks.size(), {});
+        }
+        return 0;
+    }
+    // stop the thread after the queue drains; the first write error (0: none)
+    int drain_stream() {
+        if (!out || !out->th.joinable()) return out ? out->err : 0;
+        {
+            std::lock_guard<std::mutex> lk(out->mu);
+            out->stop = true;
+        }
+        out->cv.notify_all();
+        out->th.join();
+        return out->err;
+    }
+    void abandon_stream() {
+        if (!out) return;
+        drain_stream();
+        if (out->fd >= 0) ::close(out->fd);
+        ::unlink(out->tmp.c_str());
+        out.reset();
+    }
+    ~FileBuilder() { abandon_stream(); }
+    FileBuilder() = default;
+    FileBuilder(const FileBuilder &) = delete;
+    FileBuilder &operator=(const FileBuilder &) = delete;
+    // the streamed file: remaining row groups, footer, tail, rename over path
+    int finish_stream(const char *path) {
+        Stream &st = *out;
+        if (st.path != path) {
+            abandon_stream();
+            return fail(FLS_ERR_ARG, "fls_writer_finish_file: the output was set to another path");
+        }
+        if (const int rc = flush_stream(true)) {
+            abandon_stream();
+            return rc;
+        }
+        const int e = drain_stream();
+        if (e) {
+            const std::string t = st.tmp;
+            abandon_stream();
+            return fail(FLS_ERR_IO, "write to %s: %s", t.c_str(), strerror(e));
+        }
+        std::vector<uint8_t> ft = footer(st.offs);
+        uint8_t tail[16];
+        const uint32_t flen = (uint32_t)ft.size();
+        memcpy(tail, &st.off, 8);
+        memcpy(tail + 8, &flen, 4);
+        memcpy(tail + 12, kTailMagic, 4);
+        ft.insert(ft.end(), tail, tail + 16);
+        int rc = pwrite_all(st.fd, ft.data(), ft.size(), st.off);
+        if (!rc && ftruncate(st.fd, (off_t)(st.off + ft.size())) != 0) rc = errno;
+        if (::close(st.fd) != 0 && !rc) rc = errno;
+        st.fd = -1;
+        if (!rc && ::rename(st.tmp.c_str(), st.path.c_str()) != 0) rc = errno;
+        if (rc) {
+            const std::string t = st.tmp;
+            abandon_stream();
+            return fail(FLS_ERR_IO, "write to %s: %s", t.c_str(), strerror(rc));
+        }
+        out.reset();
+        return 0;
+    }
 
     std::vector<uint8_t> footer(const std::vector<uint64_t> &chunk_offs) const {
         std::vector<uint8_t> f;
@@ -1425,8 +1622,12 @@ struct FileBuilder {
             }
         std::vector<uint8_t> ft = footer(offs);
         const uint64_t foot_off = off;
-        const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        if (fd < 0) return fail(FLS_ERR_IO, "cannot create %s: %s", path, strerror(errno));
+        // written beside path and renamed over it once complete: a failed write
+        // leaves no partial file at path, and tables still mapping the old file
+        // keep its inode
+        const std::string tmp = tmp_name(path);
+        const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) return fail(FLS_ERR_IO, "cannot create %s: %s", tmp.c_str(), strerror(errno));
         std::atomic<int> bad{0};
         auto put = [&](const void *p, uint64_t n, uint64_t at) {
             const uint8_t *b = (const uint8_t *)p;
@@ -1481,9 +1682,13 @@ struct FileBuilder {
         memcpy(tail + 12, kTailMagic, 4);
         ft.insert(ft.end(), tail, tail + 16);
         put(ft.data(), ft.size(), foot_off);
-        const int e = bad.load();
-        if (::close(fd) != 0 && !e) return fail(FLS_ERR_IO, "close %s: %s", path, strerror(errno));
-        if (e) return fail(FLS_ERR_IO, "write to %s: %s", path, strerror(e));
+        int e = bad.load();
+        if (::close(fd) != 0 && !e) e = errno ? errno : EIO;
+        if (!e && ::rename(tmp.c_str(), path) != 0) e = errno ? errno : EIO;
+        if (e) {
+            ::unlink(tmp.c_str());
+            return fail(FLS_ERR_IO, "write to %s: %s", path, strerror(e));
+        }
         return 0;
     }
 };
@@ -2365,7 +2570,8 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         }
     }
     run_seg();
-    return seg_failed();
+    if (const int rc = seg_failed()) return rc;
+    return w->fb.flush_stream(false);  // streamed output: the complete row groups go to the file
 }
 }  // namespace
 
@@ -2440,7 +2646,10 @@ int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path)
         }
     }
     const double tf = g_prof.on ? WriterProfile::now() : 0;
-    const int rc = path ? w->fb.write_file(path, w->threads) : w->fb.finish(img, len, w->threads);
+    if (w->fb.out && !path) return fail(FLS_ERR_STATE, "fls_writer_finish_image: the writer streams to a file");
+    const int rc = w->fb.out ? w->fb.finish_stream(path)
+                   : path    ? w->fb.write_file(path, w->threads)
+                             : w->fb.finish(img, len, w->threads);
     if (g_prof.on) {
         g_prof.finish += WriterProfile::now() - tf;
         g_prof.print();
@@ -2454,6 +2663,11 @@ int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path)
 int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
     if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
     return finish_writer(w, img, len, nullptr);
+}
+
+int fls_writer_set_output(fls_writer *w, const char *path) {
+    if (!w || !path) return fail(FLS_ERR_ARG, "fls_writer_set_output: NULL argument");
+    return w->fb.open_stream(path);
 }
 
 int fls_writer_finish_file(fls_writer *w, const char *path) {

@@ -68,6 +68,49 @@ StrT make_string_t(const char *p, uint32_t n) {
     return s;
 }
 
+// Scan set-up profile (FLS_SCAN_PROFILE=1): process-wide time and bytes per
+// phase, printed to stderr when a table that scanned closes -- where a cold
+// query's first milliseconds go (pinned and device allocations, string_t
+// tables, the resident image, staging copies, the consumers' waits).
+enum ProfPhase {
+    PROF_PIN_ALLOC, PROF_DEV_ALLOC, PROF_SETUP, PROF_STRTABS, PROF_IMAGE, PROF_STAGE_COPY, PROF_FILL, PROF_WAIT,
+    PROF_N
+};
+struct ScanProf {
+    std::atomic<uint64_t> ns[PROF_N] = {}, bytes[PROF_N] = {}, calls[PROF_N] = {};
+    static bool on() {
+        static const bool e = getenv("FLS_SCAN_PROFILE") && atoi(getenv("FLS_SCAN_PROFILE")) != 0;
+        return e;
+    }
+    void print() {
+        static const char *names[PROF_N] = {"pinned host alloc", "device alloc", "scan_setup", "string_t tables",
+                                            "resident image", "staging copy", "fill_batch (all)", "consumer wait"};
+        fprintf(stderr, "FLS_SCAN_PROFILE (process, since the last report):\n");
+        for (int i = 0; i < PROF_N; ++i)
+            fprintf(stderr, "  %-20s %9.3f ms  %8llu calls  %10.1f MB\n", names[i], ns[i].exchange(0) / 1e6,
+                    (unsigned long long)calls[i].exchange(0), bytes[i].exchange(0) / 1e6);
+    }
+};
+ScanProf &scan_prof() {
+    static auto *p = new ScanProf();
+    return *p;
+}
+struct ProfTimer {
+    int ph;
+    uint64_t b;
+    std::chrono::steady_clock::time_point t0;
+    explicit ProfTimer(int phase, uint64_t bytes = 0) : ph(ScanProf::on() ? phase : -1), b(bytes) {
+        if (ph >= 0) t0 = std::chrono::steady_clock::now();
+    }
+    ~ProfTimer() {
+        if (ph < 0) return;
+        ScanProf &p = scan_prof();
+        p.ns[ph] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        p.bytes[ph] += b;
+        p.calls[ph] += 1;
+    }
+};
+
 // Frees every HBM-resident image no running scan uses on GPU dev (defined
 // with the image registry); a device allocation that runs out of memory calls
 // it once and retries, so the image cache never fails a scan's own buffers.
@@ -98,6 +141,7 @@ struct DevBuf {
         release();
         dev = d;
         n = count;
+        ProfTimer pt(PROF_DEV_ALLOC, count * sizeof(T));
         hipError_t e = hipMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)));
         if (e == hipErrorOutOfMemory && release_idle_images(d) > 0) {
             (void)hipGetLastError();
@@ -129,6 +173,7 @@ struct PinBuf {
         if (count <= n && p) return hipSuccess;
         release();
         n = count;
+        ProfTimer pt(PROF_PIN_ALLOC, count * sizeof(T));
         return hipHostMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)), hipHostMallocDefault);
     }
     ~PinBuf() { release(); }
@@ -700,6 +745,7 @@ struct fls_table {
     bool dict_codes = false;        // fls_scan_dict_codes: applies to the next fls_scan_begin
     bool narrow = false;            // fls_scan_narrow: applies to the next fls_scan_begin
     bool defer_records = false;     // fls_scan_defer_records: applies to the next fls_scan_begin
+    bool profiled = false;          // scanned with FLS_SCAN_PROFILE=1 (prints the totals at close)
     ~fls_table();
 };
 
@@ -1031,6 +1077,26 @@ int fsst_config_check(int64_t policy) {
 
 constexpr uint32_t kQueueWords = 1 + kFsstGroups;
 
+// Fused launch knobs (launch_all -> launch_fused): FLS_FUSED=1 turns it on,
+// FLS_FUSED_FSST16 = waves of every 16 that start on FSST, FLS_FUSED_PIECE =
+// FSST vectors per queue item, FLS_FUSED_WPC = waves per CU (0: as many as
+// fit), FLS_FUSED_MIN_VECS_PER_CU = the FSST vectors per CU below which the
+// launch stays serial.
+struct FusedCfg {
+    bool on = false;
+    uint32_t min_vecs_per_cu = 0;
+    FusedLaunch how;
+};
+FusedCfg fused_cfg() {
+    FusedCfg f;
+    if (const char *e = getenv("FLS_FUSED")) f.on = atoi(e) != 0;
+    if (const char *e = getenv("FLS_FUSED_FSST16")) f.how.fsst_per16 = (uint32_t)std::min(16, std::max(0, atoi(e)));
+    if (const char *e = getenv("FLS_FUSED_PIECE")) f.how.piece = (uint32_t)std::min(64, std::max(1, atoi(e)));
+    if (const char *e = getenv("FLS_FUSED_WPC")) f.how.waves_per_cu = std::max(0, atoi(e));
+    if (const char *e = getenv("FLS_FUSED_MIN_VECS_PER_CU")) f.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
+    return f;
+}
+
 // CU-partitioned overlap: the main decode (HBM-bound) and the FSST kernels
 // (VALU / LDS-bound) each start alone on their own CU set instead of sharing
 // every CU's LDS and issue slots (the co-resident split lost to running them
@@ -1132,6 +1198,21 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
         !(policy & POLICY_STATIC))
         return launch_cu_split(d_chunks, nmain, fc, d_err, geom, stream, d_queue, const_cast<SideStream *>(side),
                                ov, cus, how, launch_group);
+    // fused: one kernel pulling main chunks and FSST pieces from two queues
+    // (launch_fused), when every FSST chunk is of one segmented kind
+    {
+        const FusedCfg fz = fused_cfg();
+        int g1 = -1, ng = 0;
+        for (int g = 0; g < kFsstGroups; ++g)
+            if (fc.n[g]) {
+                g1 = g;
+                ++ng;
+            }
+        if (fz.on && ng == 1 && g1 < 2 && !balanced && !sp && !(policy & POLICY_STATIC) &&
+            fsst_vecs >= (uint64_t)fz.min_vecs_per_cu * (uint64_t)cus)
+            return launch_fused(d_chunks, nmain, d_chunks + nmain + fc.first(g1), fc.n[g1], fc.vecs[g1], g1 == 0, d_err,
+                                geom, stream, d_queue, fz.how);
+    }
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
                          fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !balanced && !sp &&
                          !(policy & POLICY_STATIC);
@@ -1175,6 +1256,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
 }  // namespace
 
 fls_table::~fls_table() {
+    if (profiled && ScanProf::on()) scan_prof().print();
     resident.clear();
     // the scan pipelines go back to the connection (synchronised first: their
     // copies may read the image or the pinned stage)
@@ -1331,6 +1413,8 @@ std::shared_ptr<DevImage> resident_image(fls_table *t, int dev, uint32_t g, uint
 
 int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uint8_t *col_mask, uint32_t rg0,
                uint32_t rg1, const std::vector<HostTerm> *filter) {
+    ProfTimer prof(PROF_SETUP);
+    t->profiled = t->profiled || ScanProf::on();
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     if (rg1 > t->meta.rgs.size() || rg0 > rg1) return fail(FLS_ERR_ARG, "row-group range [%u,%u) out of bounds", rg0, rg1);
     // tear down a previous scan on this context
@@ -1409,10 +1493,15 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         {   // the image holds this GPU's shard of the table over the connection's GPUs
             const auto it = std::find(t->devices.begin(), t->devices.end(), d.dev);
             const bool in = it != t->devices.end();
+            ProfTimer pi(PROF_IMAGE);
             d.dimg = resident_image(t, d.dev, in ? (uint32_t)(it - t->devices.begin()) : 0u,
                                     in ? (uint32_t)t->devices.size() : 1u);
         }
-        int rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off, d.h_strtab);
+        int rc;
+        {
+            ProfTimer ps(PROF_STRTABS);
+            rc = build_strtabs(t, d.dev, d.rg0, d.rg1, d.strtab, d.strtab_off, d.h_strtab);
+        }
         if (rc) return rc;
         if (s.dict_codes && !d.ident.p) {
             std::vector<uint8_t> id(kIdent16 + 2 * 65536);
@@ -1589,6 +1678,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     return rc;
 }
 int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
+    ProfTimer prof(PROF_FILL);
     Slot &sl = d.slots[si];
     HostBatch &hb = *sl.hb;
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
@@ -1621,6 +1711,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         const uint8_t *src = t->img + lo;
         if (!t->registered) {
             HIP_TRY(sl.h_stage.alloc(hi - lo));
+            ProfTimer pc(PROF_STAGE_COPY, hi - lo);
             t->res->copy.copy(sl.h_stage.p, src, hi - lo);
             src = sl.h_stage.p;
         }
@@ -1978,6 +2069,7 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     Slot &sl = d.slots[si];
     auto wait_batch = [&]() -> int {
         HIP_TRY(hipSetDevice(d.dev));
+        ProfTimer pw(PROF_WAIT);
         HIP_TRY(hipEventSynchronize(sl.done));
         const uint32_t err = *(volatile const uint32_t *)sl.h_err.p;
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);

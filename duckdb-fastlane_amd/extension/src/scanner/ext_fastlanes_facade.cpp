@@ -339,6 +339,16 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
             return false;
         }
     }
+    // the file is written while the COPY runs (row groups stream to a
+    // temporary file renamed over file_path at finalize); FLS_COPY_STREAM=0
+    // writes it all at finalize instead
+    const char *cs = std::getenv("FLS_COPY_STREAM");
+    if ((!cs || std::atoi(cs) != 0) && fls_writer_set_output(s.writer, file_path.c_str()) != 0) {
+        s.error = std::string("FastLanes writer: ") + fls_last_error();
+        fls_writer_free(s.writer);
+        s.writer = nullptr;
+        return false;
+    }
     s.out_path = file_path;
     s.wtypes = types;
     s.wnames = names;

@@ -90,8 +90,16 @@ int fls_writer_add_rowgroups(fls_writer *w, uint32_t nrg, const uint32_t *nrows,
  * reference writer's NULL tracking (src/writer/write_fastlane.cpp:207-208). */
 int fls_writer_add_rowgroups_v(fls_writer *w, uint32_t nrg, const uint32_t *nrows, const void *const *data,
                                const uint32_t *const *str_offsets, const uint64_t *const *validity);
-/* Assemble the file: to `path`, or into a malloc'ed buffer freed with
- * fls_image_free. */
+/* Stream the file to `path` while it is written: row groups whose chunks are
+ * all encoded go to a temporary file beside `path` (their bytes freed once
+ * written), and fls_writer_finish_file(w, path) -- the same path -- adds the
+ * footer and renames the file over `path`.  Before the first row group.
+ * fls_writer_free without a finish removes the temporary file; nothing is
+ * left at `path`.  Not in the reference, whose writer is a stub
+ * (src/writer/write_fastlane_stream.cpp:65-107). */
+int fls_writer_set_output(fls_writer *w, const char *path);
+/* Assemble the file: to `path` (written beside it, then renamed over it), or
+ * into a malloc'ed buffer freed with fls_image_free. */
 int fls_writer_finish_file(fls_writer *w, const char *path);
 int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len);
 void fls_image_free(uint8_t *img);

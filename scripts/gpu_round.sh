@@ -57,14 +57,25 @@ for mode in "$@"; do
     rc=$?; echo "[$TAG] bench rc=$rc"; cat $O/bench_$TAG.json; [ $rc -eq 0 ] || exit $rc
     step 400 $O/prof_$TAG.log rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o kt --output-format csv -- \
         python3 bench.py --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-verify --no-traffic || exit $?
-    find $O/prof_$TAG -name "*kernel_stats.csv" -exec head -4 {} \; ;;
+    find $O/prof_$TAG -name "*kernel_stats.csv" -exec head -4 {} \;
+    # per-step spans of the same trace (a step is several grids: the kernel
+    # averages above are not a step) and the roofline fraction of their mean
+    ab=$(python3 -c "import json;print(json.load(open('$O/bench_$TAG.json'))['roofline']['algo_bytes_per_launch'])")
+    kt=$(find $O/prof_$TAG -name "*kernel_trace.csv" | head -1)
+    python3 scripts/trace_span.py "$kt" --algo-bytes "$ab" > $O/step_spans_$TAG.txt && tail -2 $O/step_spans_$TAG.txt ;;
   shares)
     for sf in 25 12.5; do
       timeout -k 10 400 python bench.py --scale $sf --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-traffic \
           > $O/bench_sf${sf}_$TAG.json 2> $O/bench_sf${sf}_$TAG.log
       rc=$?; python3 -c "import json;d=json.load(open('$O/bench_sf${sf}_$TAG.json'));print('sf$sf', d['ms_per_step'], d['roofline']['frac'])"
       [ $rc -eq 0 ] || exit $rc
-    done ;;
+    done
+    # the 8-GPU share's kernel trace and step spans
+    step 300 $O/prof_sf12_$TAG.log rocprofv3 --kernel-trace --stats -d $O/prof_sf12_$TAG -o kt --output-format csv -- \
+        python3 bench.py --scale 12.5 --steps 20 --cpu-seconds 0 --e2e-scale 0 --no-verify --no-traffic || exit $?
+    ab=$(python3 -c "import json;print(json.load(open('$O/bench_sf12.5_$TAG.json'))['roofline']['algo_bytes_per_launch'])")
+    kt=$(find $O/prof_sf12_$TAG -name "*kernel_trace.csv" | head -1)
+    python3 scripts/trace_span.py "$kt" --algo-bytes "$ab" > $O/step_spans_sf12_$TAG.txt && tail -2 $O/step_spans_sf12_$TAG.txt ;;
   configs)
     for wl in c3 c4 lineitem lineitem_dbl; do
       timeout -k 10 500 python bench.py --workload $wl --steps 10 --cpu-seconds 5 > $O/bench_${wl}_$TAG.json 2> $O/bench_${wl}_$TAG.log

@@ -183,7 +183,9 @@ def test_gpu_alp_fsst_device_resident(fl, ref, gpu, n):
 # FSST kernels: the segmented one (default for files with segment tables,
 # ring cap 4096 or 3072 bytes) and the round-2 code-parallel one (files
 # without them, or FLS_FSST_SEG=0)
-FSST_KERNELS = {"seg": {}, "seg3072": {"FLS_FSST_SEG_CAP": "3072"}, "cp": {"FLS_FSST_SEG": "0"}}
+FSST_KERNELS = {"seg": {}, "seg3072": {"FLS_FSST_SEG_CAP": "3072"}, "cp": {"FLS_FSST_SEG": "0"},
+                # the fused launch (fused_kernel: its FSST part)
+                "fused": {"FLS_FUSED": "1"}}
 
 
 def _use_kernel(monkeypatch, kernel):

@@ -75,3 +75,33 @@ def test_lineitem_variants_sf1_bit_exact(fl, gpu, wl):
         b[0] ^= 0x20
         assert hip.hipMemcpy(at, b, 1, 1) == 0
         assert fl.check_device_table(t, wl, 1.0)[15] == 1
+
+
+@pytest.mark.parametrize("env", [
+    {"FLS_FUSED": "1"},
+    {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "0", "FLS_FUSED_PIECE": "1"},
+    {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "16", "FLS_FUSED_PIECE": "7"},
+    {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "8", "FLS_FUSED_WPC": "3"},
+], ids=["fused", "fused_main_first", "fused_fsst_first", "fused_3wpc"])
+def test_fused_launch_bit_exact(fl, gpu, monkeypatch, capfd, env):
+    """The fused launch (one kernel pulling main chunks and FSST pieces from
+    two queues) decodes all 16 lineitem_full columns like the serial kernels,
+    whatever the mix of waves starting on each queue, the piece size and the
+    grid; then the same table again with the serial launch."""
+    img = fl.gen_image("lineitem_full", 0.3)
+    t = fl.Connection([0]).read_image(img)
+    t.device_upload()
+    # (a launch this small -- 420 main chunks -- would take the balanced split)
+    monkeypatch.setenv("FLS_DECODE_POLICY", "64")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("FLS_DEBUG", "1")
+    capfd.readouterr()
+    t.device_decode()
+    t.device_sync()
+    assert "fused_kernel<small>" in capfd.readouterr().err
+    assert fl.check_device_table(t, "lineitem_full", 0.3) == [0] * 16
+    monkeypatch.setenv("FLS_FUSED", "0")
+    t.device_decode()
+    t.device_sync()
+    assert fl.check_device_table(t, "lineitem_full", 0.3) == [0] * 16

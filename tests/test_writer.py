@@ -1,6 +1,8 @@
 """CPU writer (the .fls producer, reference write path stubs
 src/writer/write_fastlane*.cpp) round-trips through the oracle, for every
 encoding, type and the seeded workloads."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -244,6 +246,60 @@ def test_finish_file_writes_the_image_bytes(fl, tmp_path, threads):
     path = tmp_path / "t.fls"
     assert fl.write_image(cols, rowgroup=1024, batch=4, threads=threads, path=path) is None
     assert path.read_bytes() == bytes(img.view())
+
+
+@pytest.mark.parametrize("batch", [1, 3, 8])
+def test_streamed_output_writes_the_image_bytes(fl, tmp_path, batch):
+    # fls_writer_set_output: complete row groups stream to a temporary file
+    # beside the path while later ones encode, the footer is added and the
+    # file renamed over the path at finish -- the same bytes as the image
+    n = 9 * 1024 + 77
+    cols = _mixed_columns(fl, n, 11)
+    rng = np.random.default_rng(5)
+    cols.append(("nv", fl.INT64, np.ma.masked_array(rng.integers(-9, 9, n), mask=rng.random(n) < 0.2),
+                 fl.ENC_AUTO))
+    cols.append(("ns", fl.VARCHAR, [None if i % 5 == 0 else "s%d" % (i % 31) for i in range(n)], fl.ENC_FSST))
+    img = fl.write_image(cols, rowgroup=1024, batch=batch, threads=4)
+    path = tmp_path / "s.fls"
+    path.write_bytes(b"old contents")  # replaced whole, never partly overwritten
+    assert fl.write_image(cols, rowgroup=1024, batch=batch, threads=4, path=path, stream=True) is None
+    assert path.read_bytes() == bytes(img.view())
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["s.fls"]   # no temporary file left
+
+
+def test_streamed_output_abandoned_leaves_nothing(fl, tmp_path):
+    # a writer freed without its finish (a failed COPY) removes its temporary
+    # file and leaves the destination as it was
+    path = tmp_path / "a.fls"
+    path.write_bytes(b"keep me")
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_add_column(w, b"x", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_set_output(w, str(path).encode()) == 0
+        x = np.arange(3000, dtype=np.int32)
+        data = (ctypes.c_void_p * 1)(x.ctypes.data)
+        assert fl.lib.fls_writer_add_rowgroup(w, 3000, data, None) == 0
+        assert len(list(tmp_path.iterdir())) == 2   # the destination + the temporary file
+        # another path at finish is refused (and the temporary file removed)
+        assert fl.lib.fls_writer_finish_file(w, str(tmp_path / "b.fls").encode()) < 0
+    finally:
+        fl.lib.fls_writer_free(w)
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["a.fls"] and path.read_bytes() == b"keep me"
+
+
+def test_streamed_output_refuses_unwritable_dir_and_late_set(fl, tmp_path):
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_add_column(w, b"x", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_set_output(w, str(tmp_path / "nodir" / "x.fls").encode()) < 0
+        assert "cannot create" in fl.last_error()
+        x = np.arange(100, dtype=np.int32)
+        data = (ctypes.c_void_p * 1)(x.ctypes.data)
+        assert fl.lib.fls_writer_add_rowgroup(w, 100, data, None) == 0
+        assert fl.lib.fls_writer_set_output(w, str(tmp_path / "x.fls").encode()) < 0   # after a row group
+    finally:
+        fl.lib.fls_writer_free(w)
+    assert list(tmp_path.iterdir()) == []
 
 
 def test_finish_file_reports_unwritable_path(fl, tmp_path):
