@@ -159,6 +159,7 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
 struct FusedLaunch {
     uint32_t fsst_per16 = 5;   // of every 16 waves, how many start on the FSST queue
     uint32_t piece = 2;        // FSST vectors per queue item
+    uint32_t fsst_static_pct = 50;  // % of the FSST vectors split statically over the FSST-first waves
     int waves_per_cu = 0;      // 0: as many as fit
 };
 hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,

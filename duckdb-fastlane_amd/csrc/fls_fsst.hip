@@ -97,7 +97,12 @@ __device__ __forceinline__ T *uni_ptr(T *p) {
     return (T *)((uint64_t)uni((uint32_t)(v >> 32)) << 32 | uni((uint32_t)v));
 }
 // Index of the chunk holding launch item `item` (last ci with vec_base <= item).
+// Chunks of full row groups hold 64 vectors, so item / 64 is checked first
+// (one descriptor read); a binary search otherwise.
 __device__ __forceinline__ uint32_t chunk_of(const DevChunk *chunks, uint32_t nchunks, uint32_t item) {
+    const uint32_t g = min(item / 64, nchunks - 1);
+    const uint32_t gb = uni(gptr(chunks + g)->vec_base), gn = uni(gptr(chunks + g)->nvec);
+    if (gb <= item && item - gb < gn) return g;
     uint32_t lo = 0, hi = nchunks;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -225,13 +230,37 @@ __device__ __forceinline__ v4u make_record(uint32_t w0, uint32_t w1, uint32_t w2
 // ring stays zero past the decoded bytes).  Up to 4 blocks per lane per pass,
 // all ring reads in flight before the zeroing and the heap stores.  A block
 // past the vector's heap window is refused (bad).
-template <bool UNIFORM = false>
+template <bool UNIFORM = false, bool CLAMP = false>
 __device__ __forceinline__ void flush_ring(lu8 *ring, uint32_t ring_bytes, uint32_t ring_base, uint32_t upto,
                                            const VecHeap &h, uint32_t lane, bool &bad) {
     // (a ring never holds more than ring_bytes: the clamp bounds the loop
     // whatever a corrupt stream did to the positions)
     const uint32_t nblk = min((upto - ring_base) >> 4, ring_bytes / 16);
     lv4 *r16 = reinterpret_cast<lv4 *>(ring);
+    if constexpr (CLAMP) {
+        // (experiment kSegXClamp) no exec-masked stores: the window is checked
+        // once for the wave, a pass's rows of 64 blocks past the end are
+        // skipped by a wave-uniform test, and in the last row the lanes past
+        // nblk take block nblk - 1 -- they read, zero and store the same bytes
+        // as its own lane, which is harmless
+        if (ring_base + 16 * nblk <= h.hlim) {
+            for (uint32_t q0 = 0; q0 < nblk; q0 += 256) {
+                const uint32_t nj = min(4u, (nblk - q0 + 63) >> 6);
+                v4u b[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (j < nj) b[j] = r16[min(q0 + 64 * j + lane, nblk - 1)];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (j < nj) {
+                        const uint32_t q = min(q0 + 64 * j + lane, nblk - 1);
+                        r16[q] = mk4(0, 0, 0, 0);
+                        *reinterpret_cast<ov4 *>(h.heap + ring_base + 16 * q) = b[j];
+                    }
+            }
+            return;
+        }
+    }
     if constexpr (UNIFORM) {
         // (experiment kSegXFlush) every block inside the heap window, checked
         // once for the wave: no per-block bound test
@@ -318,6 +347,7 @@ enum : int {
     kSegXDouble = 8,   // two consecutive segments (32 code bytes) per lane per round: half the rounds
     kSegXFlush = 16,   // ring flush bound-checked once per wave instead of per block
     kSegXRecSel = 32,  // string_t records: inline and pointer words both computed, bit-selected (no branch)
+    kSegXClamp = 64,   // ring flush without exec-masked stores (clamped block index, uniform row skips)
 };
 template <bool SMALL, int X = 0>
 struct SegLds {
@@ -584,7 +614,7 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
         records(force);
         const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
         const uint32_t new_base = keep_from & ~15u;
-        flush_ring<(X & kSegXFlush) != 0>(ring, Layout::kRing, ring_base, new_base, h, lane, bad);
+        flush_ring<(X & kSegXFlush) != 0, (X & kSegXClamp) != 0>(ring, Layout::kRing, ring_base, new_base, h, lane, bad);
         wave_sync();
         const uint32_t src = min(new_base - ring_base, Layout::kRing);
         const uint32_t len = min((out_pos - new_base + 15) & ~15u, Layout::kRing - 16);
@@ -1008,25 +1038,30 @@ __device__ void cp_vector(lu8 *L, const DevChunk &c, const VecArgs &a, uint32_t 
 // ============================================================================
 enum class Kind { Seg, Cp };
 
+// Items [item0, item1) first, then (QUEUE) pieces of `piece` items from
+// `queue`: piece p = [qbase + p * piece, ...) up to nitems.  A queue launch
+// may pass an empty first range (then the first piece comes from the queue).
 template <Kind K, bool SMALL, bool QUEUE, int X = 0>
 __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchunks, uint32_t nitems, uint32_t item0,
-                                           uint32_t item1, uint32_t *queue, uint32_t piece, lu8 *L, uint32_t *err) {
+                                           uint32_t item1, uint32_t *queue, uint32_t piece, lu8 *L, uint32_t *err,
+                                           uint32_t qbase = 0) {
     chunks = uni_ptr(chunks);
     err = uni_ptr(err);
     nchunks = uni(nchunks);
+    qbase = uni(qbase);
     const uint32_t lane = __lane_id();
     // next piece of the queue into [item0, item1); false when none is left
     auto take = [&]() -> bool {
         uint32_t p = 0;
         if (lane == 0) p = atomicAdd(queue, 1u);
         p = rl(p, 0);
-        if (p >= (nitems + piece - 1) / piece) return false;
-        item0 = p * piece;
+        if (qbase >= nitems || p >= (nitems - qbase + piece - 1) / piece) return false;
+        item0 = qbase + p * piece;
         item1 = min(item0 + piece, nitems);
         return true;
     };
     if constexpr (QUEUE) {
-        if (!take()) return;
+        if (uni(item0) >= uni(item1) && !take()) return;
     }
     item0 = uni(item0);
     item1 = uni(item1);
@@ -1040,6 +1075,13 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
             if constexpr (!QUEUE) break;
             if (!take()) break;
             item = item0;
+            // the next piece is usually far ahead (the other waves took the
+            // ones between): find its chunk instead of walking there
+            if (item - uni(c.vec_base) >= uni(c.nvec)) {
+                ci = chunk_of(chunks, nchunks, item);
+                c = load_chunk(chunks, ci);
+                have_table = false;
+            }
         }
         const uint32_t v = item - uni(c.vec_base);
         if (v >= uni(c.nvec)) {  // next chunk
@@ -1146,37 +1188,66 @@ hipError_t launch_kind2(const DevChunk *d, uint32_t nchunks, uint32_t nvecs, uin
 // the larger of the two kernels' (dynamic LDS from address 0, as the FSST
 // code addresses it), registers: the main decode's budget (4 waves / SIMD).
 // ============================================================================
+// The FSST part out of line: its own register allocation, as the main
+// decode's paths have theirs (run_chunk); arguments arrive in VGPRs and are
+// made uniform again inside (fsst_range).
+template <bool SMALL>
+__device__ __attribute__((noinline)) void fused_fsst_part(const DevChunk *fchunks, uint32_t nfsst, uint32_t nfvecs,
+                                                          uint32_t item0, uint32_t item1, uint32_t *queue,
+                                                          uint32_t piece, uint32_t qbase, uint32_t *err) {
+    fsst_range<Kind::Seg, SMALL, true>(fchunks, nfsst, nfvecs, uni(item0), uni(item1), uni_ptr(queue), uni(piece),
+                                       (lu8 *)(size_t)0, err, uni(qbase));
+}
+
 template <bool SMALL>
 __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict__ mchunks, uint32_t nmain,
                                                       const DevChunk *__restrict__ fchunks, uint32_t nfsst,
                                                       uint32_t nfvecs, uint32_t *__restrict__ err,
                                                       uint32_t *__restrict__ queues, uint32_t p_bytes,
-                                                      uint32_t v_bytes, uint32_t piece, uint32_t fsst_per16) {
+                                                      uint32_t v_bytes, uint32_t piece, uint32_t fsst_per16,
+                                                      uint32_t fsst_static, uint32_t nf_waves) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     if ((uint32_t)(size_t)lds_raw != 0u) {  // LDS addressed from 0 (fsst_kernel)
         if (threadIdx.x == 0) atomicOr(err, KERR_LDS_BASE);
         return;
     }
-    auto main_part = [&]() {
-        for (;;) {
-            uint32_t ci = 0;
-            if (__lane_id() == 0) ci = atomicAdd(queues, 1u);
-            ci = uni(ci);
-            if (ci >= nmain) break;
+    // every wave's first item is static (no burst of same-address atomics at
+    // launch): main-first wave m takes main chunk m (the queue starts past
+    // them), FSST-first wave f the f-th equal share of the first fsst_static
+    // FSST vectors (the queue's pieces start after those)
+    const uint32_t b = blockIdx.x, k = fsst_per16, grp = b >> 4, r = b & 15;
+    const bool fsst_first = r < k;
+    auto main_part = [&](bool first) {
+        uint32_t ci = first ? grp * (16 - k) + (r - k) : 0u;
+        for (;; first = false) {
+            if (!first) {
+                if (__lane_id() == 0) ci = atomicAdd(queues, 1u);
+                ci = uni(ci);
+            }
+            if (ci >= nmain) {
+                if (first) continue;  // (fewer main chunks than waves: the queue is empty too)
+                break;
+            }
             const uint32_t nvec = gptr(mchunks)[ci].nvec;
             if (nvec) dec::decode_chunk(mchunks + ci, 0u, p_bytes, v_bytes, err, nvec << 8);
         }
     };
-    auto fsst_part = [&]() {
-        fsst_range<Kind::Seg, SMALL, true>(fchunks, nfsst, nfvecs, 0, 0, queues + 1, piece, (lu8 *)(size_t)0, err);
+    auto fsst_part = [&](bool first) {
+        uint32_t i0 = 0, i1 = 0;
+        if (first) {
+            const uint32_t f = grp * k + r;
+            i0 = (uint32_t)((uint64_t)fsst_static * f / nf_waves);
+            i1 = (uint32_t)((uint64_t)fsst_static * (f + 1) / nf_waves);
+        }
+        if (nfsst) fused_fsst_part<SMALL>(fchunks, nfsst, nfvecs, i0, i1, queues + 1, piece, fsst_static, err);
         wave_sync();
     };
-    if ((blockIdx.x & 15) < fsst_per16) {
-        fsst_part();
-        main_part();
+    if (fsst_first) {
+        fsst_part(true);
+        main_part(false);
     } else {
-        main_part();
-        fsst_part();
+        main_part(true);
+        fsst_part(false);
     }
 }
 
@@ -1198,14 +1269,23 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
     }
     if (how.waves_per_cu > 0) per_cu = std::min(per_cu, how.waves_per_cu);
     const int grid = cus * std::max(1, per_cu);
-    hipError_t e = hipMemsetAsync(d_queues, 0, 2 * sizeof(uint32_t), stream);
+    // waves starting on each queue (blockIdx & 15 < k: FSST first), and the
+    // static first items: main chunk m of main-first wave m, the first
+    // fsst_static_pct % of the FSST vectors split over the FSST-first waves
+    const uint32_t k = std::min(16u, how.fsst_per16);
+    uint32_t nf = 0;
+    for (int bb = 0; bb < grid; ++bb) nf += (uint32_t)(bb & 15) < k;
+    const uint32_t nm = (uint32_t)grid - nf;
+    const uint32_t fstat = nf ? (uint32_t)((uint64_t)nfvecs * std::min(100u, how.fsst_static_pct) / 100) : 0u;
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)d_queues, std::min(nm, nmain), 1, stream);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(d_queues + 1), 0, 1, stream);
     if (e != hipSuccess) return e;
     if (getenv("FLS_DEBUG"))
         fprintf(stderr, "DEBUG: fused_kernel<%s>: %d blocks of 1 wave (%d per CU, %u B LDS), %u main chunks, %u FSST "
                         "vectors in pieces of %u, %u of 16 waves FSST first\n",
                 SMALL ? "small" : "any", grid, per_cu, shmem, nmain, nfvecs, how.piece, how.fsst_per16);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), shmem, stream, d_main, nmain, d_fsst, nfsst, nfvecs, d_err,
-                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, how.piece), std::min(16u, how.fsst_per16));
+                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, how.piece), k, fstat, std::max(1u, nf));
     return hipGetLastError();
 }
 
@@ -1475,7 +1555,9 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
         if (variant == kFsstDefault) return true;  // the product build has each kernel's default only
 #ifdef FLS_EXPERIMENTS
         const int x = variant >> kSegXShift;
-        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault && ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48)) return true;
+        if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault &&
+            ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48 || x == 64 || x == 96 || x == 112))
+            return true;
 #endif
     }
     return false;
@@ -1508,6 +1590,9 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     case 16: return launch_kind2<Kind::Seg, 16>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 32: return launch_kind2<Kind::Seg, 32>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 48: return launch_kind2<Kind::Seg, 48>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 64: return launch_kind2<Kind::Seg, 64>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 96: return launch_kind2<Kind::Seg, 96>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 112: return launch_kind2<Kind::Seg, 112>(d_chunks, nchunks, nvecs, d_err, stream, how);
     default: break;
     }
 #endif

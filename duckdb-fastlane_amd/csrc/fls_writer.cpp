@@ -37,6 +37,7 @@
 #include "fls_encode.hpp"
 #include "fls_format.hpp"
 #include "fls_gen.hpp"
+#include "fls_pinned.hpp"
 #include "fls_text.hpp"
 
 namespace fls {
@@ -682,9 +683,9 @@ struct FsstGpuCtx {
         hipFree(d_dcodes);
         hipFree(d_entries);
         hipFree(d_info);
-        hipHostFree(h_dcodes);
-        hipHostFree(h_entries);
-        hipHostFree(h_info);
+        pinned_free(h_dcodes);
+        pinned_free(h_entries);
+        pinned_free(h_info);
         d_slots = d_rows = d_dcodes = d_entries = h_dcodes = h_entries = nullptr;
         d_info = h_info = nullptr;
         dict_n_cap = 0;
@@ -692,11 +693,11 @@ struct FsstGpuCtx {
     void release() {
         if (stream) hipStreamSynchronize(stream);
         release_dict();
-        hipHostFree(h_in);
-        hipHostFree(h_codes);
-        hipHostFree(h_offs);
-        hipHostFree(h_clen);
-        hipHostFree(h_tab);
+        pinned_free(h_in);
+        pinned_free(h_codes);
+        pinned_free(h_offs);
+        pinned_free(h_clen);
+        pinned_free(h_tab);
         hipFree(d_in);
         hipFree(d_codes);
         hipFree(d_offs);
@@ -717,34 +718,34 @@ struct FsstGpuCtx {
         if (!stream) FHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         const size_t nb = offs[n] - offs[0];
         if (nb + 16 > in_cap) {
-            hipHostFree(h_in);
-            hipHostFree(h_codes);
+            pinned_free(h_in);
+            pinned_free(h_codes);
             hipFree(d_in);
             hipFree(d_codes);
             h_in = h_codes = d_in = d_codes = nullptr;
             in_cap = 0;
             const size_t cap = std::max<size_t>(nb + 16, 1 << 20) * 5 / 4;
-            FHIP(hipHostMalloc((void **)&h_in, cap, 0));
-            FHIP(hipHostMalloc((void **)&h_codes, 2 * cap, 0));
+            FHIP(pinned_alloc((void **)&h_in, cap));
+            FHIP(pinned_alloc((void **)&h_codes, 2 * cap));
             FHIP(hipMalloc((void **)&d_in, cap));
             FHIP(hipMalloc((void **)&d_codes, 2 * cap));
             in_cap = cap;
         }
         if (n + 1 > n_cap) {
-            hipHostFree(h_offs);
-            hipHostFree(h_clen);
+            pinned_free(h_offs);
+            pinned_free(h_clen);
             hipFree(d_offs);
             hipFree(d_clen);
             h_offs = h_clen = d_offs = d_clen = nullptr;
             n_cap = 0;
-            FHIP(hipHostMalloc((void **)&h_offs, 4ull * (n + 1), 0));
-            FHIP(hipHostMalloc((void **)&h_clen, 4ull * (n + 1), 0));
+            FHIP(pinned_alloc((void **)&h_offs, 4ull * (n + 1)));
+            FHIP(pinned_alloc((void **)&h_clen, 4ull * (n + 1)));
             FHIP(hipMalloc((void **)&d_offs, 4ull * (n + 1)));
             FHIP(hipMalloc((void **)&d_clen, 4ull * (n + 1)));
             n_cap = n + 1;
         }
         if (!h_tab) {
-            FHIP(hipHostMalloc((void **)&h_tab, sizeof(FsstCTable), 0));
+            FHIP(pinned_alloc((void **)&h_tab, sizeof(FsstCTable)));
             FHIP(hipMalloc((void **)&d_tab, sizeof(FsstCTable)));
         }
         memcpy(h_in, bytes + offs[0], nb);
@@ -770,9 +771,9 @@ struct FsstGpuCtx {
             FHIP(hipMalloc((void **)&d_dcodes, 4ull * n));
             FHIP(hipMalloc((void **)&d_entries, 4ull * n));
             FHIP(hipMalloc((void **)&d_info, sizeof(StrDictInfo)));
-            FHIP(hipHostMalloc((void **)&h_dcodes, 4ull * n, 0));
-            FHIP(hipHostMalloc((void **)&h_entries, 4ull * n, 0));
-            FHIP(hipHostMalloc((void **)&h_info, sizeof(StrDictInfo), 0));
+            FHIP(pinned_alloc((void **)&h_dcodes, 4ull * n));
+            FHIP(pinned_alloc((void **)&h_entries, 4ull * n));
+            FHIP(pinned_alloc((void **)&h_info, sizeof(StrDictInfo)));
             dict_n_cap = n;
         }
         // one round trip: the codes and entries come back with the outcome
@@ -1929,10 +1930,10 @@ struct GpuEncoder {
     int cur = 0;
 
     static void free_set(Set &b) {
-        hipHostFree(b.h_stage);
-        hipHostFree(b.h_lens);
-        hipHostFree(b.h_out);
-        hipHostFree(b.h_desc);
+        pinned_free(b.h_stage);
+        pinned_free(b.h_lens);
+        pinned_free(b.h_out);
+        pinned_free(b.h_desc);
         hipFree(b.d_in);
         hipFree(b.d_out);
         hipFree(b.d_lens);
@@ -1973,28 +1974,28 @@ struct GpuEncoder {
             b.dict_cap = kBatch * dict_rg;
         }
         if (kBatch * in_rg > b.in_cap) {
-            hipHostFree(b.h_stage);
+            pinned_free(b.h_stage);
             hipFree(b.d_in);
             b.h_stage = b.d_in = nullptr;
             b.in_cap = 0;
-            WHIP(hipHostMalloc((void **)&b.h_stage, kBatch * in_rg, 0));
+            WHIP(pinned_alloc((void **)&b.h_stage, kBatch * in_rg));
             WHIP(hipMalloc((void **)&b.d_in, kBatch * in_rg));
             b.in_cap = kBatch * in_rg;
         }
         if (kBatch * out_rg > b.out_cap) {
             hipFree(b.d_out);
-            hipHostFree(b.h_out);
+            pinned_free(b.h_out);
             b.d_out = b.h_out = nullptr;
             b.out_cap = 0;
             WHIP(hipMalloc((void **)&b.d_out, kBatch * out_rg));
-            WHIP(hipHostMalloc((void **)&b.h_out, kBatch * out_rg, 0));
+            WHIP(pinned_alloc((void **)&b.h_out, kBatch * out_rg));
             b.out_cap = kBatch * out_rg;
         }
         if (kBatch * nj > b.job_cap) {
             hipFree(b.d_desc);
             hipFree(b.d_lens);
-            hipHostFree(b.h_lens);
-            hipHostFree(b.h_desc);
+            pinned_free(b.h_lens);
+            pinned_free(b.h_desc);
             hipFree(b.d_scratch);
             b.d_desc = b.h_desc = nullptr;
             b.d_lens = b.h_lens = nullptr;
@@ -2002,9 +2003,9 @@ struct GpuEncoder {
             b.job_cap = 0;
             const size_t n = kBatch * nj;
             WHIP(hipMalloc((void **)&b.d_desc, n * sizeof(EncChunk)));
-            WHIP(hipHostMalloc((void **)&b.h_desc, n * sizeof(EncChunk), 0));
+            WHIP(pinned_alloc((void **)&b.h_desc, n * sizeof(EncChunk)));
             WHIP(hipMalloc((void **)&b.d_lens, n * sizeof(uint64_t)));
-            WHIP(hipHostMalloc((void **)&b.h_lens, n * sizeof(uint64_t), 0));
+            WHIP(pinned_alloc((void **)&b.h_lens, n * sizeof(uint64_t)));
             WHIP(hipMalloc((void **)&b.d_scratch, n * enc_scratch_bytes()));
             b.job_cap = n;
         }

@@ -33,6 +33,7 @@
 #include "fls_decode.hpp"
 #include "fls_filter.hpp"
 #include "fls_format.hpp"
+#include "fls_pinned.hpp"
 #include "fls_reader.hpp"
 #include "fls_resident.hpp"
 
@@ -165,7 +166,7 @@ struct PinBuf {
     PinBuf &operator=(const PinBuf &) = delete;
     PinBuf(PinBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
     void release() {
-        if (p) hipHostFree(p);
+        if (p) pinned_free(p);
         p = nullptr;
         n = 0;
     }
@@ -174,7 +175,12 @@ struct PinBuf {
         release();
         n = count;
         ProfTimer pt(PROF_PIN_ALLOC, count * sizeof(T));
-        return hipHostMalloc((void **)&p, std::max<size_t>(1, count * sizeof(T)), hipHostMallocDefault);
+        const hipError_t e = pinned_alloc((void **)&p, std::max<size_t>(1, count * sizeof(T)));
+        if (e != hipSuccess) {
+            p = nullptr;
+            n = 0;
+        }
+        return e;
     }
     ~PinBuf() { release(); }
 };
@@ -1080,8 +1086,9 @@ constexpr uint32_t kQueueWords = 1 + kFsstGroups;
 // Fused launch knobs (launch_all -> launch_fused): FLS_FUSED=1 turns it on,
 // FLS_FUSED_FSST16 = waves of every 16 that start on FSST, FLS_FUSED_PIECE =
 // FSST vectors per queue item, FLS_FUSED_WPC = waves per CU (0: as many as
-// fit), FLS_FUSED_MIN_VECS_PER_CU = the FSST vectors per CU below which the
-// launch stays serial.
+// fit), FLS_FUSED_STATIC_PCT = % of the FSST vectors the FSST-first waves
+// split statically before the queue, FLS_FUSED_MIN_VECS_PER_CU = the FSST
+// vectors per CU below which the launch stays serial.
 struct FusedCfg {
     bool on = false;
     uint32_t min_vecs_per_cu = 0;
@@ -1093,6 +1100,7 @@ FusedCfg fused_cfg() {
     if (const char *e = getenv("FLS_FUSED_FSST16")) f.how.fsst_per16 = (uint32_t)std::min(16, std::max(0, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_PIECE")) f.how.piece = (uint32_t)std::min(64, std::max(1, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_WPC")) f.how.waves_per_cu = std::max(0, atoi(e));
+    if (const char *e = getenv("FLS_FUSED_STATIC_PCT")) f.how.fsst_static_pct = (uint32_t)std::min(100, std::max(0, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_MIN_VECS_PER_CU")) f.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
     return f;
 }
@@ -1208,10 +1216,12 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
                 g1 = g;
                 ++ng;
             }
-        if (fz.on && ng == 1 && g1 < 2 && !balanced && !sp && !(policy & POLICY_STATIC) &&
-            fsst_vecs >= (uint64_t)fz.min_vecs_per_cu * (uint64_t)cus)
-            return launch_fused(d_chunks, nmain, d_chunks + nmain + fc.first(g1), fc.n[g1], fc.vecs[g1], g1 == 0, d_err,
+        if (fz.on && ng <= 1 && g1 < 2 && !balanced && !sp && !(policy & POLICY_STATIC) &&
+            fsst_vecs >= (uint64_t)fz.min_vecs_per_cu * (uint64_t)cus) {
+            const int g = std::max(0, g1);  // (no FSST chunks: the main decode alone, in the fused kernel)
+            return launch_fused(d_chunks, nmain, d_chunks + nmain + fc.first(g), fc.n[g], fc.vecs[g], g == 0, d_err,
                                 geom, stream, d_queue, fz.how);
+        }
     }
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
                          fsst_vecs >= (uint64_t)ov.min_vecs_per_cu * (uint64_t)cus && !balanced && !sp &&
@@ -1868,7 +1878,10 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(sl.queue.alloc(d.dev, kQueueWords));
-    if (const int rc = fsst_config_check(policy)) return rc;
+    // (only batches with FSST work: a stale FLS_FSST_VARIANT must not fail
+    // integer-only scans, nor cost every refill an environment parse)
+    if (fsst.total_vecs() > 0)
+        if (const int rc = fsst_config_check(policy)) return rc;
     HIP_TRY(launch_all(sl.d_chunks.p, nmain, (uint32_t)k, fsst, d.err.p, bc.geom, sl.stream, sl.queue.p, policy,
                        plan));
     const uint64_t rows = t->meta.rgs[sl.rg0 + sl.nrg - 1].first_row + t->meta.rgs[sl.rg0 + sl.nrg - 1].nrows -
@@ -2687,7 +2700,8 @@ int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask) {
         HIP_TRY(hipEventCreateWithFlags(&r.side.fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&r.side.join, hipEventDisableTiming));
     }
-    if (const int rc = fsst_config_check(r.lpolicy)) return rc;
+    if (r.fsst.total_vecs() > 0)
+        if (const int rc = fsst_config_check(r.lpolicy)) return rc;
     hipEvent_t e0 = r.ev_pool[r.ev_used], e1 = r.ev_pool[r.ev_used + 1];
     r.ev_used += 2;
     HIP_TRY(hipEventRecord(e0, r.stream));

@@ -497,3 +497,20 @@ def test_gpu_fsst_unknown_variant_refused(fl, gpu, monkeypatch, variant):
     monkeypatch.delenv("FLS_FSST_VARIANT")
     t.device_decode()
     t.device_sync()   # the default decodes again
+
+
+@pytest.mark.gpu
+def test_gpu_stale_fsst_variant_does_not_fail_integer_tables(fl, gpu, monkeypatch):
+    """the FSST variant check runs only for launches with FSST
+    work, so a stale FLS_FSST_VARIANT cannot fail a table without strings
+    (device-resident decode and the scan pipeline)."""
+    x = np.arange(70000, dtype=np.int64) * 3
+    img = fl.write_image([("x", fl.INT64, x, fl.ENC_DELTA)])
+    monkeypatch.setenv("FLS_FSST_VARIANT", "893")
+    t = fl.Connection().read_image(img)
+    t.device_upload()
+    t.device_decode()
+    t.device_sync()
+    assert np.array_equal(t.device_copy_out(0).view(np.int64), x)
+    got = np.concatenate([cols[0].view(np.int64) for _, cols in t.scan()])
+    assert np.array_equal(got, x)

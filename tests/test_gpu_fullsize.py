@@ -82,7 +82,9 @@ def test_lineitem_variants_sf1_bit_exact(fl, gpu, wl):
     {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "0", "FLS_FUSED_PIECE": "1"},
     {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "16", "FLS_FUSED_PIECE": "7"},
     {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "8", "FLS_FUSED_WPC": "3"},
-], ids=["fused", "fused_main_first", "fused_fsst_first", "fused_3wpc"])
+    {"FLS_FUSED": "1", "FLS_FUSED_STATIC_PCT": "0", "FLS_FUSED_PIECE": "3"},
+    {"FLS_FUSED": "1", "FLS_FUSED_STATIC_PCT": "100", "FLS_FUSED_FSST16": "11"},
+], ids=["fused", "fused_main_first", "fused_fsst_first", "fused_3wpc", "fused_all_queue", "fused_all_static"])
 def test_fused_launch_bit_exact(fl, gpu, monkeypatch, capfd, env):
     """The fused launch (one kernel pulling main chunks and FSST pieces from
     two queues) decodes all 16 lineitem_full columns like the serial kernels,
