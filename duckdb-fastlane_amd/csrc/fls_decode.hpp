@@ -160,6 +160,7 @@ struct FusedLaunch {
     uint32_t fsst_per16 = 5;   // of every 16 waves, how many start on the FSST queue
     uint32_t piece = 2;        // FSST vectors per queue item
     uint32_t fsst_static_pct = 50;  // % of the FSST vectors split statically over the FSST-first waves
+    bool static_first = true;       // every wave's first item static (false: all from the queues)
     int waves_per_cu = 0;      // 0: as many as fit
 };
 hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,

@@ -1242,11 +1242,12 @@ __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict
         if (nfsst) fused_fsst_part<SMALL>(fchunks, nfsst, nfvecs, i0, i1, queues + 1, piece, fsst_static, err);
         wave_sync();
     };
+    const bool stat = nf_waves != 0;  // 0: every item from the queues (FusedLaunch::static_first)
     if (fsst_first) {
-        fsst_part(true);
+        fsst_part(stat);
         main_part(false);
     } else {
-        main_part(true);
+        main_part(stat);
         fsst_part(false);
     }
 }
@@ -1276,8 +1277,9 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
     uint32_t nf = 0;
     for (int bb = 0; bb < grid; ++bb) nf += (uint32_t)(bb & 15) < k;
     const uint32_t nm = (uint32_t)grid - nf;
-    const uint32_t fstat = nf ? (uint32_t)((uint64_t)nfvecs * std::min(100u, how.fsst_static_pct) / 100) : 0u;
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)d_queues, std::min(nm, nmain), 1, stream);
+    const bool stat = how.static_first;
+    const uint32_t fstat = stat && nf ? (uint32_t)((uint64_t)nfvecs * std::min(100u, how.fsst_static_pct) / 100) : 0u;
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)d_queues, stat ? std::min(nm, nmain) : 0u, 1, stream);
     if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(d_queues + 1), 0, 1, stream);
     if (e != hipSuccess) return e;
     if (getenv("FLS_DEBUG"))
@@ -1285,7 +1287,7 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
                         "vectors in pieces of %u, %u of 16 waves FSST first\n",
                 SMALL ? "small" : "any", grid, per_cu, shmem, nmain, nfvecs, how.piece, how.fsst_per16);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), shmem, stream, d_main, nmain, d_fsst, nfsst, nfvecs, d_err,
-                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, how.piece), k, fstat, std::max(1u, nf));
+                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, how.piece), k, fstat, stat ? std::max(1u, nf) : 0u);
     return hipGetLastError();
 }
 
