@@ -4,9 +4,11 @@
 Metric (BASELINE.json): "decoded values/sec + achieved HBM GB/s, TPC-H SF100
 lineitem scan at 1/2/4/8 GPU".  A step is ONE decode launch over every
 resident vector of every column of this rank's row-group shard (compressed
-input resident in HBM, decoded columns written to HBM): the fused
-decode_kernel plus, for l_comment, the FSST kernel overlapped with it.  The
-default workload is the full 16-column lineitem (l_comment FSST-compressed).
+input resident in HBM, decoded columns written to HBM): decode_kernel, or,
+with l_comment's FSST chunks in the table, ONE fused_kernel that decodes the
+main columns and the FSST strings side by side (round 5; FLS_FUSED=0: the
+decode and FSST kernels of earlier rounds).  The default workload is the full
+16-column lineitem (l_comment FSST-compressed).
 Row groups are sharded contiguously over ranks with no data-path collective
 (SURVEY.md 8(e)); torch.distributed over gloo (CPU tensors) only brackets the
 timing (barrier, MAX of times, SUM of values) and gathers the per-rank
@@ -203,16 +205,16 @@ def measure_traffic(args):
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
         except Exception as e:  # noqa: BLE001 - report, never fail the bench on profiling
             return None, f"rocprofv3 {ctr} pass failed: {e}"
-        per = {}  # kernel -> samples (a step is decode_kernel, plus the FSST kernels for FSST columns)
+        per = {}  # kernel -> samples (a step is the fused kernel, or decode_kernel plus the FSST kernels)
         for path in Path(d).rglob("*counter_collection.csv"):
             for r in csv.DictReader(open(path)):
                 k = r.get("Kernel_Name", "")
                 kind = ("fsst_sp" if "fsst_sp_kernel" in k else "fsst_cp" if "fsst_kernel" in k
-                        else "decode" if "decode_kernel" in k else None)
+                        else "fused" if "fused_kernel" in k else "decode" if "decode_kernel" in k else None)
                 if kind and r.get("Counter_Name") == ctr:
                     per.setdefault(kind, []).append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
-        if "decode" not in per:
+        if "decode" not in per and "fused" not in per:
             return None, f"no {ctr} samples"
         # per step: every dispatch of the step's kernels (a table decode with
         # FSST columns runs several grids of each kind), over the child's
@@ -221,6 +223,15 @@ def measure_traffic(args):
     return 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"], \
         f"rocprofv3 --pmc per launch: FETCH_SIZE x2 {2 * vals['FETCH_SIZE'] / 1e9:.3f} GB + " \
         f"WRITE_SIZE {vals['WRITE_SIZE'] / 1e9:.3f} GB"
+
+
+def kernel_name(args) -> str:
+    """the kernel(s) one step launches (launch_all in flsgpu.hip)"""
+    if args.workload != "lineitem_full":
+        return "fls::decode_kernel"
+    if os.environ.get("FLS_FUSED", "") == "0":
+        return "fls::decode_kernel + fls::fsst_kernel"
+    return "fls::fused_kernel (main decode + FSST)"
 
 
 def cpu_baseline(fl, args, nthreads: int, nrows_total: int, cores: dict):
@@ -575,8 +586,7 @@ def main(argv=None):
                          "achievable": HBM_ACHIEVABLE_GBS, "frac_achievable": mean_achieved / HBM_ACHIEVABLE_GBS,
                          "traffic": traffic / 1e9 if traffic else None,
                          "traffic_unit": "GB per launch (HBM, PMC)", "traffic_note": traffic_note,
-                         "kernel": "fls::decode_kernel" + (" + fls::fsst_kernel" if args.workload == "lineitem_full"
-                                                           else ""),
+                         "kernel": kernel_name(args),
                          "kernel_ms": avg_ms,
                          "algo_bytes_per_launch": algo,
                          "algo_bytes_split": {"packed": int(st.packed_bytes), "meta": int(st.meta_bytes),

@@ -157,9 +157,10 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
 // blocks that pull from two queues (d_queues[0] main chunks, [1] FSST
 // pieces; zeroed by the launch).
 struct FusedLaunch {
-    uint32_t fsst_per16 = 5;   // of every 16 waves, how many start on the FSST queue
-    uint32_t piece = 2;        // FSST vectors per queue item
-    uint32_t fsst_static_pct = 50;  // % of the FSST vectors split statically over the FSST-first waves
+    uint32_t fsst_per16 = 6;   // of every 16 waves, how many start on the FSST queue
+    uint32_t piece = 2;        // FSST vectors per queue item (halving: the largest piece)
+    bool halving = false;      // pieces of `piece` vectors over half the queue's items, half that over a quarter, ...
+    uint32_t fsst_static_pct = 0;   // % of the FSST vectors split statically over the FSST-first waves
     bool static_first = true;       // every wave's first item static (false: all from the queues)
     int waves_per_cu = 0;      // 0: as many as fit
 };

@@ -1037,6 +1037,7 @@ __device__ void cp_vector(lu8 *L, const DevChunk &c, const VecArgs &a, uint32_t 
 // profiles/r2/abenv_fsst_abslds.txt).
 // ============================================================================
 enum class Kind { Seg, Cp };
+constexpr uint32_t kHalving = 0x80000000u;  // fsst_range's piece: halving piece sizes
 
 // Items [item0, item1) first, then (QUEUE) pieces of `piece` items from
 // `queue`: piece p = [qbase + p * piece, ...) up to nitems.  A queue launch
@@ -1051,14 +1052,35 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
     qbase = uni(qbase);
     const uint32_t lane = __lane_id();
     // next piece of the queue into [item0, item1); false when none is left
+    // piece & kHalving: pieces of (piece & 0xFFFF) vectors over the first
+    // half of the queue's items, half that over the next quarter, ... down to
+    // single vectors (few table stagings early, a fine-grained end)
     auto take = [&]() -> bool {
         uint32_t p = 0;
         if (lane == 0) p = atomicAdd(queue, 1u);
         p = rl(p, 0);
-        if (qbase >= nitems || p >= (nitems - qbase + piece - 1) / piece) return false;
-        item0 = qbase + p * piece;
-        item1 = min(item0 + piece, nitems);
-        return true;
+        if (qbase >= nitems) return false;
+        if (!(piece & kHalving)) {
+            if (p >= (nitems - qbase + piece - 1) / piece) return false;
+            item0 = qbase + p * piece;
+            item1 = min(item0 + piece, nitems);
+            return true;
+        }
+        uint32_t base = qbase, rem = nitems - qbase, ps = max(1u, piece & 0xFFFFu);
+        for (;;) {
+            const uint32_t span = ps > 1 ? max(1u, rem / 2) : rem;
+            const uint32_t cnt = (span + ps - 1) / ps;
+            if (p < cnt) {
+                item0 = base + p * ps;
+                item1 = min(item0 + ps, base + span);
+                return true;
+            }
+            p -= cnt;
+            base += span;
+            rem -= span;
+            if (ps == 1 || rem == 0) return false;
+            ps >>= 1;
+        }
     };
     if constexpr (QUEUE) {
         if (uni(item0) >= uni(item1) && !take()) return;
@@ -1287,7 +1309,8 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
                         "vectors in pieces of %u, %u of 16 waves FSST first\n",
                 SMALL ? "small" : "any", grid, per_cu, shmem, nmain, nfvecs, how.piece, how.fsst_per16);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), shmem, stream, d_main, nmain, d_fsst, nfsst, nfvecs, d_err,
-                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, how.piece), k, fstat, stat ? std::max(1u, nf) : 0u);
+                       d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, std::min(64u, how.piece)) | (how.halving ? kHalving : 0u),
+                       k, fstat, stat ? std::max(1u, nf) : 0u);
     return hipGetLastError();
 }
 

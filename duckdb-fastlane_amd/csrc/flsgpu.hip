@@ -1083,25 +1083,31 @@ int fsst_config_check(int64_t policy) {
 
 constexpr uint32_t kQueueWords = 1 + kFsstGroups;
 
-// Fused launch knobs (launch_all -> launch_fused): FLS_FUSED=1 turns it on,
+// Fused launch knobs (launch_all -> launch_fused): the default for a table
+// decode whose FSST chunks are of one segmented kind; FLS_FUSED=0 turns it
+// off (serial or overlapped kernels), FLS_FUSED=1 forces it even without FSST
+// chunks (the main decode alone in the fused kernel: 2 % slower, A/B only),
 // FLS_FUSED_FSST16 = waves of every 16 that start on FSST, FLS_FUSED_PIECE =
 // FSST vectors per queue item, FLS_FUSED_WPC = waves per CU (0: as many as
 // fit), FLS_FUSED_STATIC_PCT = % of the FSST vectors the FSST-first waves
 // split statically before the queue, FLS_FUSED_MIN_VECS_PER_CU = the FSST
 // vectors per CU below which the launch stays serial.
 struct FusedCfg {
-    bool on = false;
+    // 0 off; 1 (default) launches with main chunks and FSST chunks of one
+    // segmented kind; 2 (FLS_FUSED=1) also launches with only one of the two
+    int mode = 1;
     uint32_t min_vecs_per_cu = 0;
     FusedLaunch how;
 };
 FusedCfg fused_cfg() {
     FusedCfg f;
-    if (const char *e = getenv("FLS_FUSED")) f.on = atoi(e) != 0;
+    if (const char *e = getenv("FLS_FUSED")) f.mode = std::min(2, std::max(0, atoi(e) == 1 ? 2 : atoi(e)));
     if (const char *e = getenv("FLS_FUSED_FSST16")) f.how.fsst_per16 = (uint32_t)std::min(16, std::max(0, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_PIECE")) f.how.piece = (uint32_t)std::min(64, std::max(1, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_WPC")) f.how.waves_per_cu = std::max(0, atoi(e));
     if (const char *e = getenv("FLS_FUSED_STATIC_PCT")) f.how.fsst_static_pct = (uint32_t)std::min(100, std::max(0, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_STATIC_FIRST")) f.how.static_first = atoi(e) != 0;
+    if (const char *e = getenv("FLS_FUSED_HALVING")) f.how.halving = atoi(e) != 0;
     if (const char *e = getenv("FLS_FUSED_MIN_VECS_PER_CU")) f.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
     return f;
 }
@@ -1217,7 +1223,8 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
                 g1 = g;
                 ++ng;
             }
-        if (fz.on && ng <= 1 && g1 < 2 && !balanced && !sp && !(policy & POLICY_STATIC) &&
+        if (fz.mode > 0 && ((ng == 1 && nmain > 0) || fz.mode == 2) && ng <= 1 && g1 < 2 && !balanced && !sp &&
+            !(policy & POLICY_STATIC) &&
             fsst_vecs >= (uint64_t)fz.min_vecs_per_cu * (uint64_t)cus) {
             const int g = std::max(0, g1);  // (no FSST chunks: the main decode alone, in the fused kernel)
             return launch_fused(d_chunks, nmain, d_chunks + nmain + fc.first(g), fc.n[g], fc.vecs[g], g == 0, d_err,

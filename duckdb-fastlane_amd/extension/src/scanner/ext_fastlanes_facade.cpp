@@ -693,7 +693,12 @@ bool FastLanesFacade::mergeStage(Stage &st) {
         return true;
     }
     const size_t nc = s.wtypes.size();
-    idx_t r0 = 0;
+    // When own sits at a row-group boundary, st's complete row groups go to
+    // the writer as they are (no copy: at the end of an unordered COPY every
+    // sink's stage holds up to a batch of them, a GB in all at 16 sinks) and
+    // only its partial last row group is copied into own.
+    const idx_t full = o.wrows % s.rg_rows == 0 ? st.wrows / s.rg_rows * s.rg_rows : 0;
+    idx_t r0 = full;
     while (r0 < st.wrows) {
         const idx_t n = std::min<idx_t>(st.wrows - r0, s.rg_rows - o.wrows % s.rg_rows);
         for (size_t c = 0; c < nc; ++c) {
@@ -736,6 +741,25 @@ bool FastLanesFacade::mergeStage(Stage &st) {
             return false;
         }
     }
+    if (full == 0) {
+        s.reset_stage(st);
+        s.account(st);
+        return true;
+    }
+    // st keeps its rows [0, full): the copied tail goes, then st is a batch
+    for (size_t c = 0; c < nc; ++c) {
+        if (TypeMapping::IsString(s.wtypes[c])) {
+            st.wrec[c].shrink(st.wrec[c].size() - full * sizeof(string_t));
+        } else {
+            const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(s.wtypes[c]));
+            st.wcols[c].shrink(st.wcols[c].size() - full * w);
+        }
+        if (!st.wvalid[c].empty()) st.wvalid[c].shrink(st.wvalid[c].size() - 8 * ((full + 63) / 64));
+    }
+    st.wbytes.assign(nc, 0);
+    st.wrows = full;
+    s.account(st);
+    if (!s.flush_stage(st)) return false;  // (st.error set)
     s.reset_stage(st);
     s.account(st);
     return true;

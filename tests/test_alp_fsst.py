@@ -251,6 +251,7 @@ def test_gpu_full_fidelity_lineitem(fl, ref, gpu, monkeypatch, wl, split):
     FLS_OVERLAP_MIN_VECS_PER_CU); the overlapped cases lower that threshold."""
     if split != "default":
         monkeypatch.setenv("FLS_OVERLAP_MIN_VECS_PER_CU", "0")
+        monkeypatch.setenv("FLS_FUSED", "0")   # the overlapped kernels, not the fused one
     if split == "0":
         monkeypatch.setenv("FLS_OVERLAP_FSST_WPC", "0")
     elif split and split.startswith("cu"):   # CU-partitioned overlap (FLS_OVERLAP_CU_SPLIT)
