@@ -1097,12 +1097,16 @@ struct FusedCfg {
     // segmented kind; 2 (FLS_FUSED=1) also launches with only one of the two
     int mode = 1;
     uint32_t min_vecs_per_cu = 0;
+    bool per16_set = false;  // FLS_FUSED_FSST16 given (else by launch size, launch_all)
     FusedLaunch how;
 };
 FusedCfg fused_cfg() {
     FusedCfg f;
     if (const char *e = getenv("FLS_FUSED")) f.mode = std::min(2, std::max(0, atoi(e) == 1 ? 2 : atoi(e)));
-    if (const char *e = getenv("FLS_FUSED_FSST16")) f.how.fsst_per16 = (uint32_t)std::min(16, std::max(0, atoi(e)));
+    if (const char *e = getenv("FLS_FUSED_FSST16")) {
+        f.how.fsst_per16 = (uint32_t)std::min(16, std::max(0, atoi(e)));
+        f.per16_set = true;
+    }
     if (const char *e = getenv("FLS_FUSED_PIECE")) f.how.piece = (uint32_t)std::min(64, std::max(1, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_WPC")) f.how.waves_per_cu = std::max(0, atoi(e));
     if (const char *e = getenv("FLS_FUSED_STATIC_PCT")) f.how.fsst_static_pct = (uint32_t)std::min(100, std::max(0, atoi(e)));
@@ -1227,8 +1231,13 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
             !(policy & POLICY_STATIC) &&
             fsst_vecs >= (uint64_t)fz.min_vecs_per_cu * (uint64_t)cus) {
             const int g = std::max(0, g1);  // (no FSST chunks: the main decode alone, in the fused kernel)
+            // waves starting on FSST: 6 of 16 for large launches (SF100:
+            // 21.79 ms against 21.93 with 5), 5 below 1,000 FSST vectors per
+            // CU (SF12.5: 3.115 against 3.133 ms with 6; profiles/r5/)
+            FusedLaunch how = fz.how;
+            if (!fz.per16_set) how.fsst_per16 = fsst_vecs < 1000ull * (uint64_t)cus ? 5u : 6u;
             return launch_fused(d_chunks, nmain, d_chunks + nmain + fc.first(g), fc.n[g], fc.vecs[g], g == 0, d_err,
-                                geom, stream, d_queue, fz.how);
+                                geom, stream, d_queue, how);
         }
     }
     const bool overlap = side && side->stream && ov.fsst_wpc > 0 && nmain > 0 && fsst_vecs > 0 &&
