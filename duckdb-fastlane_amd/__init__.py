@@ -157,6 +157,7 @@ _sig("fls_encode_device", C.c_int, C.c_int, C.c_uint8, C.c_uint8, _P, C.c_uint64
      C.POINTER(C.c_uint64), C.POINTER(C.c_float))
 _sig("fls_writer_finish_file", C.c_int, _P, C.c_char_p)
 _sig("fls_writer_set_output", C.c_int, _P, C.c_char_p)
+_sig("fls_writer_set_pipelined", C.c_int, _P, C.c_int)
 _sig("fls_writer_finish_image", C.c_int, _P, C.POINTER(_P), C.POINTER(C.c_uint64))
 _sig("fls_image_free", None, _P)
 _sig("fls_gen_nrows", C.c_int64, C.c_char_p, C.c_double, C.c_uint64)
@@ -261,7 +262,8 @@ def gen_dict_string(workload: str, col: int, code: int) -> str | None:
 
 # --- writer ----------------------------------------------------------------
 def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: int = -1,
-                batch: int = 1, threads: int = 0, path: str | None = None, stream: bool = False) -> Image | None:
+                batch: int = 1, threads: int = 0, path: str | None = None, stream: bool = False,
+                pipelined: bool = False) -> Image | None:
     """columns: list of (name, type, values, encoding[, width, scale]).
     values: numpy int array for integer types, float array for FLOAT/DOUBLE
     (stored bit-exactly), list of str/bytes for VARCHAR.  NULLs: None entries
@@ -273,7 +275,9 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
     path: the file is written there instead (fls_writer_finish_file: the
     same bytes, chunks written in parallel, no image); returns None.
     stream: with path, row groups go to the file as they are encoded
-    (fls_writer_set_output; the same bytes)."""
+    (fls_writer_set_output; the same bytes).  pipelined: a call returns
+    before its row groups are encoded (fls_writer_set_pipelined; the same
+    bytes), so each batch's buffers are kept until the next call returns."""
     w = _lib.fls_writer_new(row_offset)
     try:
         _check(_lib.fls_writer_set_rowgroup_size(w, rowgroup))
@@ -283,7 +287,10 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
             _check(_lib.fls_writer_set_device(w, device))
         if stream and path is not None:
             _check(_lib.fls_writer_set_output(w, str(path).encode()))
+        if pipelined:
+            _check(_lib.fls_writer_set_pipelined(w, 1))
         n = None
+        held = None  # pipelined: the previous call's buffers
         prepped = []
         for spec in columns:
             name, ty, vals, enc = spec[:4]
@@ -344,6 +351,7 @@ def write_image(columns, rowgroup: int = ROWGROUP, row_offset: int = 0, device: 
                 _check(_lib.fls_writer_add_rowgroups(w, len(grp), rows, data, offs))
             else:
                 _check(_lib.fls_writer_add_rowgroup(w, rows[0], data, offs))
+            held = (keep, data, offs, vmask, rows)
         if path is not None:
             _check(_lib.fls_writer_finish_file(w, str(path).encode()))
             return None

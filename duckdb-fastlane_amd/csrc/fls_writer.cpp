@@ -2216,11 +2216,19 @@ struct GpuEncoder {
 #undef WHIP
 };
 
-// The writer's persistent workers: run(n, fn) calls fn(0..n-1) on the calling
-// thread and the workers and returns when every call is done (threads were
-// created per row group before: 15 thread starts per 65,536-row group).
+// The writer's persistent threads (created per row group before: 15 thread
+// starts per 65,536-row group): a FIFO of jobs, each n independent tasks; workers take
+// the front job's next task.  run() submits and waits; submit() / wait()
+// split it, so a pipelined writer (fls_writer_set_pipelined) lets the next
+// call's tasks start while the previous call's last ones finish.  The caller
+// of wait() runs its own job's remaining tasks before it sleeps.
 class WorkerPool {
 public:
+    struct Job {
+        std::function<void(size_t)> fn;
+        size_t n = 0;
+        std::atomic<size_t> next{0}, done{0};
+    };
     ~WorkerPool() { stop(); }
     // nthreads in total, the calling thread included
     void resize(int nthreads) {
@@ -2230,42 +2238,48 @@ public:
         quit_ = false;
         for (size_t i = 0; i < want; ++i) th_.emplace_back([this] { loop(); });
     }
-    void run(size_t n, const std::function<void(size_t)> &fn) {
-        if (th_.empty() || n <= 1) {
-            for (size_t i = 0; i < n; ++i) fn(i);
-            return;
-        }
-        {
+    std::shared_ptr<Job> submit(size_t n, std::function<void(size_t)> fn) {
+        auto j = std::make_shared<Job>();
+        j->fn = std::move(fn);
+        j->n = n;
+        if (n > 1 && !th_.empty()) {
             std::lock_guard<std::mutex> lk(mu_);
-            fn_ = &fn;
-            n_ = n;
-            next_.store(0);
-            busy_ = th_.size();
-            ++gen_;
+            q_.push_back(j);
+            cv_.notify_all();
         }
-        cv_.notify_all();
-        drain();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return busy_ == 0; });
-        fn_ = nullptr;
+        return j;
     }
+    void wait(const std::shared_ptr<Job> &j) {
+        if (!j) return;
+        for (size_t i; (i = j->next.fetch_add(1)) < j->n;) finish_task(*j, i);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return j->done.load() == j->n; });
+    }
+    void run(size_t n, const std::function<void(size_t)> &fn) { wait(submit(n, fn)); }
 
 private:
-    void drain() {
-        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    void finish_task(Job &j, size_t i) {
+        j.fn(i);
+        if (j.done.fetch_add(1) + 1 == j.n) {
+            std::lock_guard<std::mutex> lk(mu_);
+            done_.notify_all();
+        }
     }
     void loop() {
-        uint64_t seen = 0;
         for (;;) {
+            std::shared_ptr<Job> j;
             {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                cv_.wait(lk, [&] { return quit_ || !q_.empty(); });
                 if (quit_) return;
-                seen = gen_;
+                j = q_.front();
+                if (j->next.load() >= j->n) {  // every task taken: the job leaves the queue
+                    q_.pop_front();
+                    continue;
+                }
             }
-            drain();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--busy_ == 0) done_.notify_one();
+            const size_t i = j->next.fetch_add(1);
+            if (i < j->n) finish_task(*j, i);
         }
     }
     void stop() {
@@ -2276,16 +2290,38 @@ private:
         cv_.notify_all();
         for (auto &t : th_) t.join();
         th_.clear();
+        q_.clear();
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
-    const std::function<void(size_t)> *fn_ = nullptr;
-    size_t n_ = 0, busy_ = 0;
-    std::atomic<size_t> next_{0};
-    uint64_t gen_ = 0;
+    std::deque<std::shared_ptr<Job>> q_;  // jobs with tasks not taken yet
     bool quit_ = false;
 };
+
+namespace {
+struct RgArgs {
+    uint32_t nrows;
+    const void *const *data;
+    const uint32_t *const *offs;
+    const uint64_t *const *valid = nullptr;  // per column: validity words, or NULL (all valid)
+};
+// A row group being encoded: its chunks, zone maps and bitmaps, the caller's
+// columns, and (GPU columns) where its values are staged.
+struct PendingRg {
+    FileBuilder::RG rg;
+    RgArgs in;
+    std::vector<uint8_t *> stage;     // GPU columns: where their values go in pinned memory
+    std::vector<uint64_t *> est_dict; // GPU ENC_AUTO columns: the host's DICT estimate
+};
+// A pipelined writer's segment still encoding on the pool after its call
+// returned (fls_writer_set_pipelined): appended by the next call or finish.
+struct PendingSeg {
+    std::vector<PendingRg> seg;
+    std::shared_ptr<WorkerPool::Job> job;
+    double t0 = 0;
+};
+}  // namespace
 
 struct fls_writer {
     FileBuilder fb;
@@ -2298,7 +2334,34 @@ struct fls_writer {
     // finish fails with this instead of completing those jobs
     int broken = 0;
     std::string broken_msg;
+    bool pipelined = false;                  // fls_writer_set_pipelined
+    std::unique_ptr<PendingSeg> pend;        // pipelined: the last call's segment, still encoding
+    ~fls_writer() {
+        if (pend) pool.wait(pend->job);      // its tasks read the caller's buffers and our row groups
+    }
 };
+
+namespace {
+// a segment's tasks done: its row groups appended in order (none when a GPU
+// FSST compression failed; the caller reports that, seg_failed / finish_writer)
+void append_segment(fls_writer *w, std::unique_ptr<PendingSeg> ps) {
+    if (!ps) return;
+    w->pool.wait(ps->job);
+    if (w->fsst_gpu.err.load()) return;
+    for (PendingRg &p : ps->seg) w->fb.rgs.push_back(std::move(p.rg));
+    if (g_prof.on) g_prof.cpu += WriterProfile::now() - ps->t0;
+}
+// the last call's segment of a pipelined writer, and its FSST failure if any
+int drain_pending(fls_writer *w) {
+    append_segment(w, std::move(w->pend));
+    if (const int rc = w->fsst_gpu.err.exchange(0)) {
+        w->broken = rc;
+        w->broken_msg = w->fsst_gpu.err_msg;
+        return fail(rc, "%s", w->fsst_gpu.err_msg.c_str());
+    }
+    return 0;
+}
+}  // namespace
 
 extern "C" {
 
@@ -2333,12 +2396,6 @@ int fls_writer_add_column(fls_writer *w, const char *name, uint8_t type, uint8_t
 }  // extern "C"
 
 namespace {
-struct RgArgs {
-    uint32_t nrows;
-    const void *const *data;
-    const uint32_t *const *offs;
-    const uint64_t *const *valid = nullptr;  // per column: validity words, or NULL (all valid)
-};
 
 // The chunk bitmaps of n rows from the caller's validity words (bits past n
 // cleared); false when every row is valid.  nnull: NULL rows.
@@ -2387,16 +2444,19 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
     const size_t ncols = w->fb.cols.size();
     const uint32_t rgsz = w->fb.rowgroup_size;
+    // row groups so far, a pipelined writer's pending segment included
+    const size_t nprev = w->fb.rgs.size() + (w->pend ? w->pend->seg.size() : 0);
+    const uint32_t last_rows = w->pend ? w->pend->seg.back().rg.nrows : nprev ? w->fb.rgs.back().nrows : rgsz;
     // validate every row group before any is added
     for (uint32_t k = 0; k < nrg; ++k) {
         const uint32_t nrows = a[k].nrows;
         if (nrows == 0 || nrows > rgsz) return fail(FLS_ERR_ARG, "row group needs 1..%u rows, got %u", rgsz, nrows);
-        const bool prev_short = k == 0 ? !w->fb.rgs.empty() && w->fb.rgs.back().nrows != rgsz : a[k - 1].nrows != rgsz;
+        const bool prev_short = (k == 0 ? last_rows : a[k - 1].nrows) != rgsz;
         if (prev_short) return fail(FLS_ERR_STATE, "only the last row group may be short");
         if (!a[k].data) return fail(FLS_ERR_ARG, "fls_writer_add_rowgroup: NULL argument");
         // test hook: fail the call that would add row group k (error paths of callers)
         if (const char *f = getenv("FLS_TEST_FAIL_WRITER_RG"))
-            if (w->fb.rgs.size() + k == (size_t)atoi(f)) return fail(FLS_ERR_STATE, "injected writer failure at row group %s", f);
+            if (nprev + k == (size_t)atoi(f)) return fail(FLS_ERR_STATE, "injected writer failure at row group %s", f);
         for (size_t c = 0; c < ncols; ++c) {
             const ColSpec &cs = w->fb.cols[c];
             if (!a[k].data[c]) return fail(FLS_ERR_ARG, "column %zu: NULL data", c);
@@ -2435,20 +2495,16 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     const char *fg = getenv("FLS_WRITER_FSST_GPU");
     FsstGpu *fsst_gpu = w->fsst_gpu.dev >= 0 && !(fg && atoi(fg) == 0) ? &w->fsst_gpu : nullptr;
 
-    struct Pending {
-        FileBuilder::RG rg;
-        const RgArgs *in;
-        std::vector<uint8_t *> stage;     // GPU columns: where their values go in pinned memory
-        std::vector<uint64_t *> est_dict; // GPU ENC_AUTO columns: the host's DICT estimate
-    };
+    using Pending = PendingRg;
     std::vector<Pending> seg;
-    auto encode_col = [&](Pending &p, size_t c) {
+    // (by value: a pipelined call's tasks outlive this call)
+    auto encode_col = [w, on_gpu, fsst_gpu](Pending &p, size_t c) {
         const ColSpec &cs = w->fb.cols[c];
-        const uint32_t nrows = p.in->nrows;
-        const void *data = p.in->data[c];
+        const uint32_t nrows = p.in.nrows;
+        const void *data = p.in.data[c];
         // NULLs: the chunk's bitmaps, placeholders at the NULL rows, zone-map flags
         uint32_t nnull = 0;
-        const bool nulls = chunk_validity(p.in->valid ? p.in->valid[c] : nullptr, nrows, p.rg.valid[c], nnull);
+        const bool nulls = chunk_validity(p.in.valid ? p.in.valid[c] : nullptr, nrows, p.rg.valid[c], nnull);
         const std::vector<uint64_t> &vw = p.rg.valid[c];
         auto null_flags = [&](ZoneMap &z) {
             if (!nulls) return;
@@ -2457,11 +2513,11 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         };
         if (type_is_string(cs.type)) {
             if (!nulls) {
-                p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in->offs[c], (const char *)data, nrows, fsst_gpu);
+                p.rg.chunks[c] = encode_str_chunk(cs.enc, p.in.offs[c], (const char *)data, nrows, fsst_gpu);
                 return;
             }
             // NULL rows as empty strings
-            const uint32_t *o = p.in->offs[c];
+            const uint32_t *o = p.in.offs[c];
             std::vector<uint32_t> no(nrows + 1, 0);
             std::string bytes;
             for (uint32_t i = 0; i < nrows; ++i) {
@@ -2501,24 +2557,31 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         p.rg.zones[c] = zone_of(cs.type, v.data(), nrows);
         null_flags(p.rg.zones[c]);
     };
-    // encode the segment's chunks, then append its row groups in order
-    auto run_seg = [&]() {
-        if (seg.empty()) return;
-        const double tc = g_prof.on ? WriterProfile::now() : 0;
+    // encode the segment's chunks (submitted to the pool), then append its
+    // row groups in order; a pipelined writer leaves the call's last segment
+    // encoding (w->pend) and appends it at the start of the next call
+    auto start_seg = [&]() -> std::unique_ptr<PendingSeg> {
+        if (seg.empty()) return nullptr;
+        auto ps = std::make_unique<PendingSeg>();
+        ps->t0 = g_prof.on ? WriterProfile::now() : 0;
+        ps->seg = std::move(seg);
+        seg.clear();
         std::vector<std::pair<uint32_t, uint32_t>> tasks;  // (row group in segment, column)
-        tasks.reserve(seg.size() * ncols);
+        tasks.reserve(ps->seg.size() * ncols);
         for (int pass = 0; pass < 2; ++pass)
-            for (uint32_t k = 0; k < seg.size(); ++k)
+            for (uint32_t k = 0; k < ps->seg.size(); ++k)
                 for (uint32_t c = 0; c < ncols; ++c)
                     if ((type_is_string(w->fb.cols[c].type)) == (pass == 0)) tasks.emplace_back(k, c);
-        w->pool.run(tasks.size(), [&](size_t t) { encode_col(seg[tasks[t].first], tasks[t].second); });
-        if (fsst_gpu && fsst_gpu->err.load()) {  // reported by seg_failed(); no row group of the segment is added
-            seg.clear();
-            return;
-        }
-        for (Pending &p : seg) w->fb.rgs.push_back(std::move(p.rg));
-        seg.clear();
-        if (g_prof.on) g_prof.cpu += WriterProfile::now() - tc;
+        PendingSeg *pp = ps.get();
+        ps->job = w->pool.submit(tasks.size(), [pp, tasks, encode_col](size_t t) {
+            encode_col(pp->seg[tasks[t].first], tasks[t].second);
+        });
+        return ps;
+    };
+    auto finish_pend = [&]() { append_segment(w, std::move(w->pend)); };
+    auto run_seg = [&]() {
+        finish_pend();
+        append_segment(w, start_seg());
     };
     // a GPU FSST compression that failed in the last segment
     // The segment's row groups were dropped, but the GPU encoder's current
@@ -2542,7 +2605,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     seg.reserve(nrg);
     for (uint32_t k = 0; k < nrg; ++k) {
         Pending p;
-        p.in = &a[k];
+        p.in = a[k];
         p.rg.nrows = a[k].nrows;
         p.rg.chunks.resize(ncols);
         p.rg.zones.assign(ncols, ZoneMap{0, 0, 0, 0});
@@ -2554,8 +2617,12 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             // caller's buffers are only valid during this call)
             if (!w->gpu.has_room(w->fb.cols, gcols, a[k].nrows)) run_seg();
             if (const int rc = seg_failed()) return rc;
-            const int rc = w->gpu.add(w->fb.cols, gcols, w->fb.rgs.size() + seg.size(), a[k].nrows, w->threads,
-                                      w->fb.rgs, p.stage, p.est_dict);
+            // (its position in the file: a pending segment's row groups are
+            // appended before any set holding them is submitted -- run_seg
+            // before every submit, drain_pending before gpu.finish -- so a
+            // completing set only touches row groups already in rgs)
+            const size_t at = w->fb.rgs.size() + (w->pend ? w->pend->seg.size() : 0) + seg.size();
+            const int rc = w->gpu.add(w->fb.cols, gcols, at, a[k].nrows, w->threads, w->fb.rgs, p.stage, p.est_dict);
             if (rc) {
                 run_seg();
                 return gpu_failed(rc);
@@ -2570,7 +2637,15 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
             if (rc) return gpu_failed(rc);
         }
     }
-    run_seg();
+    if (w->pipelined) {
+        // the previous call's segment first (row groups stay in call order),
+        // this one's tasks already queued behind it
+        auto mine = start_seg();
+        finish_pend();
+        w->pend = std::move(mine);
+    } else {
+        run_seg();
+    }
     if (const int rc = seg_failed()) return rc;
     return w->fb.flush_stream(false);  // streamed output: the complete row groups go to the file
 }
@@ -2609,6 +2684,7 @@ int fls_writer_set_threads(fls_writer *w, int nthreads) {
 
 int fls_writer_set_device(fls_writer *w, int device) {
     if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_device: NULL writer");
+    if (const int rc = drain_pending(w)) return rc;  // (its FSST chunks may be on the old device)
     w->gpu.release();
     w->gpu.dev = -1;
     w->fsst_gpu.release();
@@ -2627,7 +2703,7 @@ int fls_writer_set_rowgroup_size(fls_writer *w, uint32_t rows) {
     if (rows == 0 || rows > kRowGroupSize || rows % kVectorSize)
         return fail(FLS_ERR_ARG, "row group size must be a multiple of %u in [%u, %u], got %u", kVectorSize, kVectorSize,
                     kRowGroupSize, rows);
-    if (!w->fb.rgs.empty()) return fail(FLS_ERR_STATE, "fls_writer_set_rowgroup_size: after first row group");
+    if (!w->fb.rgs.empty() || w->pend) return fail(FLS_ERR_STATE, "fls_writer_set_rowgroup_size: after first row group");
     w->fb.rowgroup_size = rows;
     return 0;
 }
@@ -2638,6 +2714,7 @@ namespace {
 int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path) {
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
+    if (const int rc = drain_pending(w)) return rc;
     if (w->gpu.dev >= 0) {
         const int rc = w->gpu.finish(w->fb.rgs, w->threads);
         if (rc) {  // row groups without some of their chunks: no file from this writer
@@ -2664,6 +2741,14 @@ int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path)
 int fls_writer_finish_image(fls_writer *w, uint8_t **img, uint64_t *len) {
     if (!w || !img || !len) return fail(FLS_ERR_ARG, "fls_writer_finish_image: NULL argument");
     return finish_writer(w, img, len, nullptr);
+}
+
+int fls_writer_set_pipelined(fls_writer *w, int on) {
+    if (!w) return fail(FLS_ERR_ARG, "fls_writer_set_pipelined: NULL writer");
+    if (!on)
+        if (const int rc = drain_pending(w)) return rc;
+    w->pipelined = on != 0;
+    return 0;
 }
 
 int fls_writer_set_output(fls_writer *w, const char *path) {

@@ -112,7 +112,18 @@ public:
         std::vector<RawBuf> valid;  // per column: validity words of the batch rows, or empty (no NULL)
         std::vector<std::vector<uint32_t>> offs;  // per row group k: rows_k + 1 offsets from k * (rg_rows + 1)
         std::vector<std::vector<uint64_t>> base;  // per row group: its first byte in cols[c]
+        // the writer call's arrays (a pipelined writer reads them after the call)
+        std::vector<uint32_t> nrows;
+        std::vector<const void *> data;
+        std::vector<const uint32_t *> offs_p;
+        std::vector<const uint64_t *> valid_p;
     };
+    // Pipelined writer calls (fls_writer_set_pipelined; FLS_COPY_PIPELINE=0
+    // turns them off): a call returns with its chunks still encoding, so the
+    // batch it was given stays here until the next call (or the finish)
+    // returns.  Touched only by the chained writer calls and after them.
+    bool pipelined = true;
+    std::unique_ptr<Batch> held;
     static constexpr size_t kMaxInflight = 3;
     std::deque<std::shared_future<std::string>> inflight;  // "" or the writer's error (fls_last_error is per thread)
     std::vector<std::unique_ptr<Batch>> spare;
@@ -342,6 +353,9 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     // the file is written while the COPY runs (row groups stream to a
     // temporary file renamed over file_path at finalize); FLS_COPY_STREAM=0
     // writes it all at finalize instead
+    const char *cp = std::getenv("FLS_COPY_PIPELINE");
+    s.pipelined = !(cp && std::atoi(cp) == 0);
+    if (s.pipelined) fls_writer_set_pipelined(s.writer, 1);
     const char *cs = std::getenv("FLS_COPY_STREAM");
     if ((!cs || std::atoi(cs) != 0) && fls_writer_set_output(s.writer, file_path.c_str()) != 0) {
         s.error = std::string("FastLanes writer: ") + fls_last_error();
@@ -481,7 +495,16 @@ bool FastLanesFacade::Impl::flush_stage(Stage &st) {
         const int rc = fls_writer_add_rowgroups_v(writer, nrg, nrows.data(), data.data(), offs.data(), valid.data());
         std::string e = rc == 0 ? std::string() : std::string(fls_last_error());
         if (prof.on) encode_s += CopyProfile::now() - t0;
-        recycle();
+        if (pipelined) {
+            // this call has returned: the previous batch is free, this one
+            // (and the arrays the call was given) stays until the next
+            std::swap(b->nrows, nrows);
+            std::swap(b->data, data);
+            std::swap(b->offs_p, offs);
+            std::swap(b->valid_p, valid);
+            std::swap(held, own_b);
+        }
+        if (own_b) recycle();
         return e;
     }).share());
     return true;
@@ -798,8 +821,9 @@ void FastLanesFacade::finalizeFile() {
                 s.prof.sink, s.prof.prep, s.prof.fixed, s.prof.str, s.prof.wait, s.encode_s, s.prof.finish,
                 (unsigned long long)s.staged_peak.load());
     }
-    fls_writer_free(s.writer);
+    fls_writer_free(s.writer);  // (waits for a pipelined call's chunks)
     s.writer = nullptr;
+    s.held.reset();
     s.finalized_ok = ok;
 }
 

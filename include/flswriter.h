@@ -98,6 +98,14 @@ int fls_writer_add_rowgroups_v(fls_writer *w, uint32_t nrg, const uint32_t *nrow
  * left at `path`.  Not in the reference, whose writer is a stub
  * (src/writer/write_fastlane_stream.cpp:65-107). */
 int fls_writer_set_output(fls_writer *w, const char *path);
+/* Pipelined adds (on != 0): an add call returns once its row groups' chunk
+ * tasks are queued behind the previous call's, not when they are encoded, so
+ * the caller prepares the next batch while the threads encode this one.  The
+ * file is the same.  The buffers of call k (the pointer arrays included) must
+ * stay valid until call k+1, a finish, fls_writer_set_pipelined(w, 0) or
+ * fls_writer_free returns.
+ * on == 0 waits for the pending call's row groups. */
+int fls_writer_set_pipelined(fls_writer *w, int on);
 /* Assemble the file: to `path` (written beside it, then renamed over it), or
  * into a malloc'ed buffer freed with fls_image_free. */
 int fls_writer_finish_file(fls_writer *w, const char *path);

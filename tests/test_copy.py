@@ -150,17 +150,26 @@ def test_copy_background_writer_failure_is_reported(ext, tmpfile, monkeypatch, f
         ext.copy_values([("a", "INTEGER", list(range(n)))], tmpfile("fail.fls"))
 
 
-@pytest.mark.parametrize("batch", ["1", "2", "8"])
-def test_copy_batches_of_row_groups_cpu(ext, ref, tmpfile, monkeypatch, batch):
+@pytest.mark.parametrize("batch,pipeline", [("1", "1"), ("2", "1"), ("8", "1"), ("1", "0"), ("2", "0")])
+def test_copy_batches_of_row_groups_cpu(ext, ref, tmpfile, monkeypatch, batch, pipeline):
     """The sink hands the writer FLS_COPY_BATCH row groups per call
     (fls_writer_add_rowgroups): 4 row groups, the last partial, in batches of
-    1, 2 and 8 decode (oracle) to the source values, VARCHAR offsets included."""
+    1, 2 and 8 decode (oracle) to the source values, VARCHAR offsets included;
+    with the writer calls pipelined (fls_writer_set_pipelined, the default) or
+    not (FLS_COPY_PIPELINE=0) -- the same file."""
     monkeypatch.setenv("FLS_COPY_BATCH", batch)
+    monkeypatch.setenv("FLS_COPY_PIPELINE", pipeline)
     n = 3 * 65536 + 1000
     a = [(i * 7919) % 100003 - 50000 for i in range(n)]
     s = [f"w{i % 7}" * (i % 11) for i in range(n)]  # 0..20 bytes: inlined and pointer string_t
-    dst = tmpfile(f"batch{batch}.fls")
+    dst = tmpfile(f"batch{batch}_{pipeline}.fls")
     assert ext.copy_values([("a", "INTEGER", a), ("s", "VARCHAR", s)], dst) == n
+    if batch == "2":
+        # the same bytes either way
+        other = tmpfile(f"batch{batch}_{pipeline}_other.fls")
+        monkeypatch.setenv("FLS_COPY_PIPELINE", "0" if pipeline == "1" else "1")
+        assert ext.copy_values([("a", "INTEGER", a), ("s", "VARCHAR", s)], other) == n
+        assert open(other, "rb").read() == open(dst, "rb").read()
     rf = ref.RefFile(open(dst, "rb").read())
     assert rf.nrows == n and rf.nrowgroups == 4
     assert np.concatenate([rf.decode(0, g) for g in range(4)]).view(np.int32).tolist() == a

@@ -248,6 +248,10 @@ def test_gpu_writer_batched_rowgroups_bytes_identical(fl, gpu, batch, n, rowgrou
     cpu = fl.write_image(cols, rowgroup=rowgroup).tobytes()
     dev = fl.write_image(cols, rowgroup=rowgroup, device=0, batch=batch, threads=8).tobytes()
     assert cpu == dev
+    # pipelined calls (fls_writer_set_pipelined): a call's last segment is
+    # still staging into the encoder's batch when the next call adds to it
+    piped = fl.write_image(cols, rowgroup=rowgroup, device=0, batch=batch, threads=8, pipelined=True).tobytes()
+    assert cpu == piped
 
 
 def _fsst_columns(fl, n, rng):

@@ -267,6 +267,44 @@ def test_streamed_output_writes_the_image_bytes(fl, tmp_path, batch):
     assert sorted(p.name for p in tmp_path.iterdir()) == ["s.fls"]   # no temporary file left
 
 
+@pytest.mark.parametrize("batch,stream", [(1, False), (3, True), (8, True)])
+def test_pipelined_adds_write_the_same_bytes(fl, tmp_path, batch, stream):
+    # fls_writer_set_pipelined: a call returns with its chunk tasks queued
+    # behind the previous call's; row groups still go in in call order
+    n = 13 * 1024 + 5
+    cols = _mixed_columns(fl, n, 17)
+    cols.append(("ns", fl.VARCHAR, [None if i % 3 == 0 else "p%d" % (i % 23) for i in range(n)], fl.ENC_FSST))
+    img = fl.write_image(cols, rowgroup=1024, batch=batch, threads=4)
+    piped = fl.write_image(cols, rowgroup=1024, batch=batch, threads=4, pipelined=True)
+    assert bytes(piped.view()) == bytes(img.view())
+    path = tmp_path / "p.fls"
+    assert fl.write_image(cols, rowgroup=1024, batch=batch, threads=4, path=path, stream=stream,
+                          pipelined=True) is None
+    assert path.read_bytes() == bytes(img.view())
+
+
+def test_pipelined_short_row_group_rule_sees_the_pending_call(fl):
+    # the previous call's row groups are still encoding, but a short one
+    # among them still ends the file
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_set_rowgroup_size(w, 1024) == 0
+        assert fl.lib.fls_writer_add_column(w, b"x", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_set_pipelined(w, 1) == 0
+        x = np.arange(1024, dtype=np.int32)
+        data = (ctypes.c_void_p * 1)(x.ctypes.data)
+        assert fl.lib.fls_writer_add_rowgroup(w, 1000, data, None) == 0
+        assert fl.lib.fls_writer_add_rowgroup(w, 1024, data, None) < 0
+        assert "only the last row group" in fl.last_error()
+        assert fl.lib.fls_writer_set_rowgroup_size(w, 2048) < 0   # a row group is pending
+        assert fl.lib.fls_writer_set_pipelined(w, 0) == 0
+        p, ln = ctypes.c_void_p(), ctypes.c_uint64()
+        assert fl.lib.fls_writer_finish_image(w, ctypes.byref(p), ctypes.byref(ln)) == 0
+        fl.lib.fls_image_free(p)
+    finally:
+        fl.lib.fls_writer_free(w)
+
+
 def test_streamed_output_abandoned_leaves_nothing(fl, tmp_path):
     # a writer freed without its finish (a failed COPY) removes its temporary
     # file and leaves the destination as it was
