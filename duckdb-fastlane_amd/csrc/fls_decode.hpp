@@ -163,6 +163,7 @@ struct FusedLaunch {
     uint32_t fsst_static_pct = 0;   // % of the FSST vectors split statically over the FSST-first waves
     bool static_first = true;       // every wave's first item static (false: all from the queues)
     int waves_per_cu = 0;      // 0: as many as fit
+    int x = 0;                 // the FSST part's experiment bits (FLS_FUSED_X; the experiment library only)
 };
 hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
                         uint32_t nfvecs, bool small, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,

@@ -216,7 +216,7 @@ __device__ __forceinline__ v4u make_record(uint32_t w0, uint32_t w1, uint32_t w2
         return __builtin_amdgcn_perm(hi, lo, sel);
     };
     const bool inl = n <= 12;
-    if constexpr (SEL) {  // (experiment kSegXRecSel) both forms computed, picked by bit select: no branch
+    if constexpr (SEL) {  // both forms computed, picked by bit select: no branch (kSegXRecSel: the branch)
         const uint32_t m = 0u - (uint32_t)inl;
         uint32_t a = word(w2, w1, 1), b = word(w3, w2, 2);
         asm volatile("" : "+v"(a), "+v"(b));
@@ -262,8 +262,8 @@ __device__ __forceinline__ void flush_ring(lu8 *ring, uint32_t ring_bytes, uint3
         }
     }
     if constexpr (UNIFORM) {
-        // (experiment kSegXFlush) every block inside the heap window, checked
-        // once for the wave: no per-block bound test
+        // every block inside the heap window, checked once for the wave: no
+        // per-block bound test (kSegXFlush: the per-block test below)
         if (ring_base + 16 * nblk <= h.hlim) {
             for (uint32_t q0 = 0; q0 < nblk; q0 += 256) {
                 v4u b[4];
@@ -345,8 +345,13 @@ enum : int {
     kSegXNoPad = 2,    // no 256 B pad in the per-wave LDS (17 waves per CU instead of 16 for SMALL)
     kSegXSplit = 4,    // symbol table as two u32 arrays (low / high dwords): two b32 gathers per code
     kSegXDouble = 8,   // two consecutive segments (32 code bytes) per lane per round: half the rounds
-    kSegXFlush = 16,   // ring flush bound-checked once per wave instead of per block
-    kSegXRecSel = 32,  // string_t records: inline and pointer words both computed, bit-selected (no branch)
+    // round 5: the next two are the default (a ring flush bound-checked once
+    // per wave; string_t records with both forms computed and bit-selected,
+    // no branch), -1.2 % on l_comment SF10 on two boxes
+    // (profiles/r5/abenv_fsst_segx_r5a.txt, abenv_r5n_lineitem_full_10.txt);
+    // the bits now select round 4's forms
+    kSegXFlush = 16,   // ring flush bound-checked per block
+    kSegXRecSel = 32,  // string_t records: a branch between the inline and the pointer form
     kSegXClamp = 64,   // ring flush without exec-masked stores (clamped block index, uniform row skips)
 };
 template <bool SMALL, int X = 0>
@@ -599,7 +604,7 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
                     w3 = r32[i0 + 3];
                 }
                 *reinterpret_cast<ov4 *>(a.out + 16ull * i) =
-                    make_record<(X & kSegXRecSel) != 0>(r32[i0], r32[i0 + 1], w2, w3, x & 3, n, h.ptr_base + d0);
+                    make_record<(X & kSegXRecSel) == 0>(r32[i0], r32[i0 + 1], w2, w3, x & 3, n, h.ptr_base + d0);
             }
             if (n_ok > 0) str_base += rl(rel1, n_ok - 1);
             next_str += n_ok;
@@ -614,7 +619,7 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
         records(force);
         const uint32_t keep_from = next_str < nvals ? min(str_base, out_pos) : out_pos;
         const uint32_t new_base = keep_from & ~15u;
-        flush_ring<(X & kSegXFlush) != 0, (X & kSegXClamp) != 0>(ring, Layout::kRing, ring_base, new_base, h, lane, bad);
+        flush_ring<(X & kSegXFlush) == 0, (X & kSegXClamp) != 0>(ring, Layout::kRing, ring_base, new_base, h, lane, bad);
         wave_sync();
         const uint32_t src = min(new_base - ring_base, Layout::kRing);
         const uint32_t len = min((out_pos - new_base + 15) & ~15u, Layout::kRing - 16);
@@ -1213,15 +1218,15 @@ hipError_t launch_kind2(const DevChunk *d, uint32_t nchunks, uint32_t nvecs, uin
 // The FSST part out of line: its own register allocation, as the main
 // decode's paths have theirs (run_chunk); arguments arrive in VGPRs and are
 // made uniform again inside (fsst_range).
-template <bool SMALL>
+template <bool SMALL, int X>
 __device__ __attribute__((noinline)) void fused_fsst_part(const DevChunk *fchunks, uint32_t nfsst, uint32_t nfvecs,
                                                           uint32_t item0, uint32_t item1, uint32_t *queue,
                                                           uint32_t piece, uint32_t qbase, uint32_t *err) {
-    fsst_range<Kind::Seg, SMALL, true>(fchunks, nfsst, nfvecs, uni(item0), uni(item1), uni_ptr(queue), uni(piece),
-                                       (lu8 *)(size_t)0, err, uni(qbase));
+    fsst_range<Kind::Seg, SMALL, true, X>(fchunks, nfsst, nfvecs, uni(item0), uni(item1), uni_ptr(queue), uni(piece),
+                                          (lu8 *)(size_t)0, err, uni(qbase));
 }
 
-template <bool SMALL>
+template <bool SMALL, int X = 0>
 __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict__ mchunks, uint32_t nmain,
                                                       const DevChunk *__restrict__ fchunks, uint32_t nfsst,
                                                       uint32_t nfvecs, uint32_t *__restrict__ err,
@@ -1261,7 +1266,7 @@ __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict
             i0 = (uint32_t)((uint64_t)fsst_static * f / nf_waves);
             i1 = (uint32_t)((uint64_t)fsst_static * (f + 1) / nf_waves);
         }
-        if (nfsst) fused_fsst_part<SMALL>(fchunks, nfsst, nfvecs, i0, i1, queues + 1, piece, fsst_static, err);
+        if (nfsst) fused_fsst_part<SMALL, X>(fchunks, nfsst, nfvecs, i0, i1, queues + 1, piece, fsst_static, err);
         wave_sync();
     };
     const bool stat = nf_waves != 0;  // 0: every item from the queues (FusedLaunch::static_first)
@@ -1274,11 +1279,11 @@ __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict
     }
 }
 
-template <bool SMALL>
+template <bool SMALL, int X = 0>
 hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
                           uint32_t nfvecs, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,
                           uint32_t *d_queues, const FusedLaunch &how) {
-    auto kern = fused_kernel<SMALL>;
+    auto kern = fused_kernel<SMALL, X>;
     const uint32_t shmem = std::max<uint32_t>(geom.p_bytes + geom.v_bytes, SegLds<SMALL>::kWave);
     static const bool lds_at_zero = [kern] {
         hipFuncAttributes a{};
@@ -1592,6 +1597,15 @@ hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *
                         uint32_t nfvecs, bool small, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,
                         uint32_t *d_queues, const FusedLaunch &how) {
     if (nmain == 0 && nfsst == 0) return hipSuccess;
+#ifdef FLS_EXPERIMENTS
+    // (experiment library) the FSST part's segmented-kernel bits, FusedLaunch::x
+    if (how.x == (kSegXFlush | kSegXRecSel))
+        return small ? launch_fused_t<true, kSegXFlush | kSegXRecSel>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom,
+                                                                       stream, d_queues, how)
+                     : launch_fused_t<false, kSegXFlush | kSegXRecSel>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom,
+                                                                        stream, d_queues, how);
+#endif
+    if (how.x != 0) return hipErrorInvalidValue;
     return small ? launch_fused_t<true>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream, d_queues, how)
                  : launch_fused_t<false>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream, d_queues, how);
 }
