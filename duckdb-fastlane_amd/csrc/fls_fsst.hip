@@ -353,6 +353,7 @@ enum : int {
     kSegXFlush = 16,   // ring flush bound-checked per block
     kSegXRecSel = 32,  // string_t records: a branch between the inline and the pointer form
     kSegXClamp = 64,   // ring flush without exec-masked stores (clamped block index, uniform row skips)
+    kSegXNoBranch = 128,  // escape-free codes: every code ORs (an incomplete qword into a dummy slot), no exec mask
 };
 template <bool SMALL, int X = 0>
 struct SegLds {
@@ -406,6 +407,22 @@ struct LeanWriter {
         if (nb >= 64) complete(v >> (64 - b));
         b = nb & 63;
     }
+    // (experiment kSegXNoBranch) the same without the exec-masked branch:
+    // every code ORs, an incomplete qword into the lane's dummy slot (two
+    // lanes share one) -- two SALU instructions per code fewer
+    __device__ __forceinline__ void put_tagged_nb(uint32_t lo, uint32_t hi, lu64 *dummy) {
+        uint32_t nb = b + (hi >> 24);
+        asm("" : "+v"(hi), "+v"(nb));
+        hi &= 0x00FFFFFFu;
+        const uint64_t v = (uint64_t)hi << 32 | lo;
+        acc |= v << b;
+        const bool c = nb >= 64;
+        lu64 *dst = c ? reinterpret_cast<lu64 *>(ring + a) : dummy;
+        __hip_atomic_fetch_or(dst, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        a += c ? 8u : 0u;
+        acc = c ? v >> ((64u - b) & 63u) : acc;
+        b = nb & 63;
+    }
     __device__ __forceinline__ void finish() {
         if (b) __hip_atomic_fetch_or(reinterpret_cast<lu64 *>(ring + a), acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
@@ -420,9 +437,9 @@ struct LeanWriter {
 // check catches).  The fast path (FULL, no escapes) issues all 16 table reads
 // together; the general one keeps each code byte (a literal's value) beside
 // its entry and reads 4 at a time to stay in the fast path's registers.
-template <bool FULL, bool ESC, bool SPLIT = false>
+template <bool FULL, bool ESC, bool SPLIT = false, bool NOBRANCH = false>
 __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in, uint32_t nb, uint32_t &st,
-                                             LeanWriter &qw) {
+                                             LeanWriter &qw, lu64 *dummy = nullptr) {
     // an opaque copy: the callers' variants would otherwise share (hoist) the
     // byte extraction and table addresses of all 16 codes ahead of their
     // branch, all of them live at once
@@ -451,7 +468,8 @@ __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in,
 #pragma unroll
         for (uint32_t k = 0; k < B; ++k) {
             if constexpr (kFast) {
-                qw.put_tagged((uint32_t)sy[k], (uint32_t)(sy[k] >> 32));
+                if constexpr (NOBRANCH) qw.put_tagged_nb((uint32_t)sy[k], (uint32_t)(sy[k] >> 32), dummy);
+                else qw.put_tagged((uint32_t)sy[k], (uint32_t)(sy[k] >> 32));
                 continue;
             }
             // selects as bit masks (v_bfi), not compares: per-code lane masks
@@ -704,9 +722,12 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
                 LeanWriter qw(ring, p0 + (incl - dl - done));
                 const uint32_t nb = idx0 < comp_len ? min(comp_len - idx0, 16u) : 0u;
                 constexpr bool kSplit = (X & kSegXSplit) != 0;
+                // (kSegXNoBranch) the lane's dummy slot: the 256 B pad before the ring
+                constexpr bool kNoBr = (X & kSegXNoBranch) != 0 && (X & kSegXNoPad) == 0;
+                lu64 *dummy = reinterpret_cast<lu64 *>(ring - 256) + (lane & 31);
                 uint32_t got = !full   ? seg_lane<false, true, kSplit>(sym, raw, nb, st, qw)
                                : vec_esc ? seg_lane<true, true, kSplit>(sym, raw, nb, st, qw)
-                                         : seg_lane<true, false, kSplit>(sym, raw, nb, st, qw);
+                                         : seg_lane<true, false, kSplit, kNoBr>(sym, raw, nb, st, qw, dummy);
                 if constexpr (SEGS == 2) {
                     const uint32_t nb1 = idx0 + 16 < comp_len ? min(comp_len - idx0 - 16, 16u) : 0u;
                     if (got != dl0 || (nb1 > 0 && st != entry1)) bad = true;
@@ -1586,7 +1607,7 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
 #ifdef FLS_EXPERIMENTS
         const int x = variant >> kSegXShift;
         if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault &&
-            ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48 || x == 64 || x == 96 || x == 112))
+            ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48 || x == 64 || x == 128))
             return true;
 #endif
     }
@@ -1604,6 +1625,11 @@ hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *
                                                                        stream, d_queues, how)
                      : launch_fused_t<false, kSegXFlush | kSegXRecSel>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom,
                                                                         stream, d_queues, how);
+    if (how.x == kSegXNoBranch)
+        return small ? launch_fused_t<true, kSegXNoBranch>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream,
+                                                           d_queues, how)
+                     : launch_fused_t<false, kSegXNoBranch>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream,
+                                                            d_queues, how);
 #endif
     if (how.x != 0) return hipErrorInvalidValue;
     return small ? launch_fused_t<true>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream, d_queues, how)
@@ -1630,8 +1656,7 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     case 32: return launch_kind2<Kind::Seg, 32>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 48: return launch_kind2<Kind::Seg, 48>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 64: return launch_kind2<Kind::Seg, 64>(d_chunks, nchunks, nvecs, d_err, stream, how);
-    case 96: return launch_kind2<Kind::Seg, 96>(d_chunks, nchunks, nvecs, d_err, stream, how);
-    case 112: return launch_kind2<Kind::Seg, 112>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 128: return launch_kind2<Kind::Seg, 128>(d_chunks, nchunks, nvecs, d_err, stream, how);
     default: break;
     }
 #endif

@@ -91,7 +91,8 @@ def main():
                     res[name].append(n / sec)
             for name, v in res.items():
                 print(f"arm {name}: DataChunks {a.threads} threads median {statistics.median(v) / 1e6:.1f} M rows/s "
-                      f"(best {max(v) / 1e6:.1f}) over {len(v)}", flush=True)
+                      f"(best {max(v) / 1e6:.1f}, worst {min(v) / 1e6:.1f}) over {len(v)}: "
+                  + " ".join(f"{x / 1e6:.1f}" for x in v), flush=True)
         # the phase profile of the N-thread scan (read_fastlanes.cpp ReadProfile, printed on stderr)
         os.environ["FLS_READ_PROFILE"] = "1"
         sys.stderr.flush()

@@ -111,6 +111,11 @@ for mode in "$@"; do
     step 600 $O/e2e_phases_$TAG.txt python scripts/e2e_phases.py --scale 10 || exit $? ;;
   e2earms:*)  # e2earms:<arms>: interleaved env arms of the 16-thread DataChunk scan
     step 600 $O/e2e_arms_$TAG.txt python scripts/e2e_phases.py --scale 10 --arms "${mode#e2earms:}" || exit $? ;;
+  e2eenv:*)  # e2eenv:<name>:<VAR=val,...>: the e2e phases with the env set for the whole process, 6 warm 16-thread queries
+    IFS=: read -r _ nm kv <<< "$mode"
+    step 600 $O/e2e_env_${TAG}_$nm.txt env FLS_SCAN_PROFILE=1 ${kv//,/ } python scripts/e2e_phases.py --scale 10 \
+        --arms "q:" --reps 6 || exit $?
+    grep "arm q" $O/e2e_env_${TAG}_$nm.txt ;;
   copy:*)  # copy:<workload>:<scale>:<reps>:<arms>: COPY (read_fastlanes) TO fls, env arms interleaved
     IFS=: read -r _ wl sc reps arms <<< "$mode"
     step 900 $O/copy_${TAG}_${wl}_${sc}.txt python scripts/writer_bench.py --copy-only --workload "$wl" \
