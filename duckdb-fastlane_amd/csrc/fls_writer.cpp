@@ -2023,11 +2023,14 @@ struct GpuEncoder {
         return !(e && atoi(e) == 0);
     }
     static bool dict_job(uint8_t enc) { return (enc == ENC_DICT || enc == ENC_AUTO) && dict_gpu(); }
-    // ALP chunks of FLOAT / DOUBLE columns on the GPU (FLS_WRITER_ALP_GPU=0:
-    // on the host threads)
+    // ALP chunks of FLOAT / DOUBLE columns on the GPU only with
+    // FLS_WRITER_ALP_GPU=1: the host threads won every same-box A/B (COPY
+    // lineitem_dbl SF10: 55.2 vs 51.1 M rows/s unordered, 44.2 vs 38.4 ordered,
+    // profiles/r5/copy_r5o_lineitem_dbl_10.txt; r4: ordered -10 %), and the
+    // byte-identical GPU kernel stays as the opt-in
     static bool alp_gpu() {
         const char *e = getenv("FLS_WRITER_ALP_GPU");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }
     // the encoding a job asks the kernels for: FLOAT / DOUBLE columns are ALP
     // (ENC_AUTO included, as encode_int_chunk does)

@@ -538,10 +538,12 @@ def test_gpu_writer_alp_bytes_identical(fl, ref, gpu, monkeypatch, n, rowgroup):
     (alp_encode_kernel: the sampled (e, f) votes, each vector's cheapest
     candidate, exceptions and FFOR packing): the file -- chunks and float zone
     maps -- is the CPU writer's, byte for byte, its values decode bit-exactly
-    under the oracle, and the host path (FLS_WRITER_ALP_GPU=0) writes the same."""
+    under the oracle, and the host path (the default since round 5;
+    FLS_WRITER_ALP_GPU=1 opts into the GPU) writes the same."""
     cols = _alp_columns(fl, n, np.random.default_rng(n + 5))
     cpu_img = fl.write_image(cols, rowgroup=rowgroup)
     cpu = cpu_img.tobytes()
+    monkeypatch.setenv("FLS_WRITER_ALP_GPU", "1")
     dev = fl.write_image(cols, rowgroup=rowgroup, device=0, threads=8).tobytes()
     assert len(cpu) == len(dev)
     assert cpu == dev
@@ -558,15 +560,16 @@ def test_gpu_writer_alp_bytes_identical(fl, ref, gpu, monkeypatch, n, rowgroup):
             assert np.array_equal(got.view(want.dtype)[keep].view(np.uint8), want[keep].view(np.uint8)), name
         else:
             assert np.array_equal(got, want.view(np.uint8)), name
-    monkeypatch.setenv("FLS_WRITER_ALP_GPU", "0")
+    monkeypatch.delenv("FLS_WRITER_ALP_GPU")
     assert fl.write_image(cols, rowgroup=rowgroup, device=0).tobytes() == cpu
 
 
 @pytest.mark.gpu
-def test_gpu_writer_alp_lineitem_dbl_decodes(fl, gpu):
+def test_gpu_writer_alp_lineitem_dbl_decodes(fl, gpu, monkeypatch):
     """lineitem with the four DECIMAL columns as DOUBLE (the lineitem_dbl
-    workload's shape), written on the GPU: the file is the CPU writer's and the
-    GPU decode of it returns every value's bits."""
+    workload's shape), written on the GPU (FLS_WRITER_ALP_GPU=1): the file is
+    the CPU writer's and the GPU decode of it returns every value's bits."""
+    monkeypatch.setenv("FLS_WRITER_ALP_GPU", "1")
     n = 65536 + 1000
     rng = np.random.default_rng(11)
     qty = rng.integers(1, 51, n).astype(np.float64)
