@@ -72,10 +72,13 @@ StrT make_string_t(const char *p, uint32_t n) {
 // Scan set-up profile (FLS_SCAN_PROFILE=1): process-wide time and bytes per
 // phase, printed to stderr when a table that scanned closes -- where a cold
 // query's first milliseconds go (pinned and device allocations, string_t
-// tables, the resident image, staging copies, the consumers' waits).
+// tables, the resident image, staging copies, the consumers' waits), and
+// per batch on the GPU (HIP events on the slot's stream: the decode kernels,
+// then the D2H of its columns; batches of different slots overlap, so these
+// are summed stream time, not wall time).
 enum ProfPhase {
     PROF_PIN_ALLOC, PROF_DEV_ALLOC, PROF_SETUP, PROF_STRTABS, PROF_IMAGE, PROF_STAGE_COPY, PROF_FILL, PROF_WAIT,
-    PROF_N
+    PROF_GPU_DECODE, PROF_D2H, PROF_N
 };
 struct ScanProf {
     std::atomic<uint64_t> ns[PROF_N] = {}, bytes[PROF_N] = {}, calls[PROF_N] = {};
@@ -85,7 +88,8 @@ struct ScanProf {
     }
     void print() {
         static const char *names[PROF_N] = {"pinned host alloc", "device alloc", "scan_setup", "string_t tables",
-                                            "resident image", "staging copy", "fill_batch (all)", "consumer wait"};
+                                            "resident image", "staging copy", "fill_batch (all)", "consumer wait",
+                                            "GPU decode (events)", "D2H (events)"};
         fprintf(stderr, "FLS_SCAN_PROFILE (process, since the last report):\n");
         for (int i = 0; i < PROF_N; ++i)
             fprintf(stderr, "  %-20s %9.3f ms  %8llu calls  %10.1f MB\n", names[i], ns[i].exchange(0) / 1e6,
@@ -378,6 +382,9 @@ struct Slot {                       // one batch of row groups in flight
     DevBuf<uint32_t> queue;         // decode work-queue counter
     uint64_t in_base = 0;
     hipEvent_t done = nullptr;
+    hipEvent_t pt[3] = {};          // FLS_SCAN_PROFILE: decode start, D2H start, end (timing events)
+    uint64_t prof_d2h = 0;          // ... and the batch's D2H bytes
+    std::atomic<bool> prof_pending{false};  // the batch's times not yet counted (its first acquire does)
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
     PinBuf<uint32_t> h_err;         // the device error flags, copied after the batch's kernels
     // filtered batches (fls_scan_filter)
@@ -432,6 +439,8 @@ struct ScanDev {
         sync();
         for (auto &sl : slots) {
             if (sl.done) hipEventDestroy(sl.done);
+            for (hipEvent_t e : sl.pt)
+                if (e) hipEventDestroy(e);
             if (sl.stream) hipStreamDestroy(sl.stream);
         }
         if (stream) hipStreamDestroy(stream);
@@ -1508,6 +1517,9 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         for (auto &sl : d.slots) {
             if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+            if (ScanProf::on())
+                for (hipEvent_t &e : sl.pt)
+                    if (!e) HIP_TRY(hipEventCreate(&e));
             if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
             HIP_TRY(sl.h_err.alloc(1));
             sl.d_out.resize(ncols);
@@ -1894,6 +1906,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     HIP_TRY(sl.h_chunks.alloc(kk));
     HIP_TRY(sl.d_chunks.alloc(d.dev, kk));
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
+    if (sl.pt[0]) HIP_TRY(hipEventRecord(sl.pt[0], sl.stream));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(sl.queue.alloc(d.dev, kQueueWords));
     // (only batches with FSST work: a stale FLS_FSST_VARIANT must not fail
@@ -1939,13 +1952,23 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         if (rc) return rc;
     }
     // 3. D2H into pinned host columns (and string heaps)
+    if (sl.pt[1]) HIP_TRY(hipEventRecord(sl.pt[1], sl.stream));
+    sl.prof_d2h = 0;
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.mask, c)) continue;
-        if (!filtered)
+        if (!filtered) {
             HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, hb.narrowed[c] ? sl.d_narrow[c].p : sl.d_out[c].p, rows * hb.ob[c],
                                    hipMemcpyDeviceToHost, sl.stream));
-        if (sl.heap_bytes[c])
+            sl.prof_d2h += rows * hb.ob[c];
+        }
+        if (sl.heap_bytes[c]) {
             HIP_TRY(hipMemcpyAsync(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
+            sl.prof_d2h += sl.heap_bytes[c];
+        }
+    }
+    if (sl.pt[2]) {
+        HIP_TRY(hipEventRecord(sl.pt[2], sl.stream));
+        sl.prof_pending.store(true);
     }
     // the error flags ride along (sticky device flags: a batch sees its own
     // kernels' and any earlier ones'), so an acquire reads pinned memory
@@ -2102,6 +2125,18 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         HIP_TRY(hipSetDevice(d.dev));
         ProfTimer pw(PROF_WAIT);
         HIP_TRY(hipEventSynchronize(sl.done));
+        if (sl.prof_pending.exchange(false)) {  // the batch's stream times, once
+            float dec = 0, d2h = 0;
+            if (hipEventElapsedTime(&dec, sl.pt[0], sl.pt[1]) == hipSuccess &&
+                hipEventElapsedTime(&d2h, sl.pt[1], sl.pt[2]) == hipSuccess) {
+                ScanProf &p = scan_prof();
+                p.ns[PROF_GPU_DECODE] += (uint64_t)(dec * 1e6);
+                p.calls[PROF_GPU_DECODE] += 1;
+                p.ns[PROF_D2H] += (uint64_t)(d2h * 1e6);
+                p.bytes[PROF_D2H] += sl.prof_d2h;
+                p.calls[PROF_D2H] += 1;
+            }
+        }
         const uint32_t err = *(volatile const uint32_t *)sl.h_err.p;
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
         if (err & KERR_NARROW)
