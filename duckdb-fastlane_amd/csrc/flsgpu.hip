@@ -501,10 +501,14 @@ size_t pinned_bytes(const ScanDev &d) {
 // What a connection keeps between scans: idle per-GPU pipelines (at most
 // kIdlePerDev per GPU) and the staging copy threads.  The idle pipelines'
 // pinned host batches are capped by BYTES per GPU (FLS_IDLE_PINNED_MB, default
-// 512; 0 keeps none): a batch is up to 8 row groups of every delivered column,
+// 1024; 0 keeps none): a batch is up to 8 row groups of every delivered column,
 // about 150 MB at lineitem_full widths, so a count cap alone let a long-lived
-// process (DuckDB) keep ~1 GB of page-locked memory per GPU.  fls_connection_trim
-// frees the idle pipelines on demand.  Tables share ConnRes by reference, so
+// process (DuckDB) keep more page-locked memory than it uses.  512 MB was
+// below a 16-thread scan's working set: every other warm query re-pinned
+// ~100 MB at hipHostMalloc's 4-5 GB/s (profiles/r5/e2e_env_r5p_prof.txt: the
+// 492 M rows/s query of a 660 M median); at 1024 no warm query allocates
+// (e2e_env_r5o_cap1024.txt).  fls_connection_trim frees the idle pipelines on
+// demand.  Tables share ConnRes by reference, so
 // it lives until the connection and every table opened on it are closed.
 struct ConnRes {
     static constexpr size_t kIdlePerDev = 2;
@@ -513,7 +517,7 @@ struct ConnRes {
     CopyPool copy;
     static size_t idle_cap_bytes() {
         const char *e = getenv("FLS_IDLE_PINNED_MB");
-        return (size_t)(e ? std::max(0L, atol(e)) : 512L) << 20;
+        return (size_t)(e ? std::max(0L, atol(e)) : 1024L) << 20;
     }
     // free idle pipelines until the pinned bytes they hold on GPU dev (every
     // GPU: dev < 0) are at most keep (caller holds mu)
