@@ -618,19 +618,27 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
                 // unpredictably in a column like l_shipinstruct), then their bytes
                 uint32_t longs[STANDARD_VECTOR_SIZE];
                 uint32_t nl = 0;
-                uint64_t bytes = 0;
+                uint64_t bytes = 0, lbytes = 0;
                 for (idx_t r = 0; r < n; ++r) {
                     const uint32_t len = str[r].GetSize();
+                    const bool lg = len > string_t::INLINE_LENGTH;
                     bytes += len;
+                    lbytes += lg ? len : 0u;
                     longs[nl] = (uint32_t)r;
-                    nl += len > string_t::INLINE_LENGTH ? 1u : 0u;
+                    nl += lg ? 1u : 0u;
                 }
+                // the slice's arena bytes in one grow (a grow per string cost
+                // the single ordered sink ~20 ns a string: l_comment's are all
+                // non-inlined)
                 RawBuf &ar = st.warena[c];
+                uint64_t off = ar.size();
+                uint8_t *dst = ar.grow(lbytes);
                 for (uint32_t i = 0; i < nl; ++i) {
                     const uint32_t r = longs[i], len = str[r].GetSize();
-                    const uint64_t off = ar.size();
-                    memcpy(ar.grow(len), str[r].GetData(), len);
+                    memcpy(dst, str[r].GetData(), len);
                     memcpy(rec + sizeof(string_t) * r + 8, &off, 8);
+                    dst += len;
+                    off += len;
                 }
                 if (st.wbytes[c] + bytes > StringLimit()) {  // the writer's offsets are 32-bit
                     st.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
