@@ -9,7 +9,9 @@
 // kBatchRowGroups at a time (fls_writer_add_rowgroups encodes their chunks in
 // parallel): a batch is encoded while the sink buffers the next one.
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <functional>
 #include <cstring>
 #include <deque>
 #include <future>
@@ -68,6 +70,107 @@ public:
 private:
     std::unique_ptr<uint8_t[]> p_;
     size_t n_ = 0, cap_ = 0;
+};
+
+// Helper threads for a lone sink (an ordered COPY has one): a DataChunk
+// slice's columns are copied side by side instead of one after another (the
+// one sink thread's copies were 63 % of an ordered COPY, copy_profile_r5k).
+// A slice is ~50 us of work, less than waking a sleeping thread costs, so the
+// helpers spin between slices and sleep after 2 ms without one.  run()
+// publishes a job through a sequence number (odd while the job's fields
+// change; helpers only join an even, new one, and leave the old one before
+// the fields change).
+class ColumnPool {
+public:
+    ~ColumnPool() { stop(); }
+    int size() const { return (int)th_.size(); }
+    void start(int helpers) {
+        if (!th_.empty() || helpers <= 0) return;
+        quit_ = false;
+        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
+    }
+    // fn(0..n-1) on the caller and the helpers; returns when every call is done
+    void run(size_t n, const std::function<void(size_t)> &fn) {
+        if (th_.empty() || n < 2) {
+            for (size_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        const uint64_t g = seq_.load() + 1;
+        seq_.store(g);  // odd: helpers stay out
+        while (active_.load() != 0) spin();
+        fn_ = &fn;
+        n_ = n;
+        next_.store(0);
+        done_.store(0);
+        seq_.store(g + 1);  // even: the job is open
+        if (sleepers_.load() != 0) {
+            std::lock_guard<std::mutex> lk(mu_);
+            cv_.notify_all();
+        }
+        for (size_t i; (i = next_.fetch_add(1)) < n;) {
+            fn(i);
+            done_.fetch_add(1);
+        }
+        while (done_.load() != n) spin();
+    }
+
+private:
+    static void spin() {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    void loop() {
+        uint64_t seen = seq_.load();
+        auto idle = std::chrono::steady_clock::now();
+        for (;;) {
+            if (quit_.load()) return;
+            const uint64_t g = seq_.load();
+            if ((g & 1) == 0 && g != seen) {
+                active_.fetch_add(1);
+                if (seq_.load() == g) {
+                    seen = g;
+                    for (size_t i; (i = next_.fetch_add(1)) < n_;) {
+                        (*fn_)(i);
+                        done_.fetch_add(1);
+                    }
+                }
+                active_.fetch_sub(1);
+                idle = std::chrono::steady_clock::now();
+                continue;
+            }
+            if (std::chrono::steady_clock::now() - idle < std::chrono::milliseconds(2)) {
+                spin();
+                continue;
+            }
+            std::unique_lock<std::mutex> lk(mu_);
+            sleepers_.fetch_add(1);
+            cv_.wait_for(lk, std::chrono::milliseconds(100), [&] {
+                const uint64_t x = seq_.load();
+                return quit_.load() || ((x & 1) == 0 && x != seen);
+            });
+            sleepers_.fetch_sub(1);
+            idle = std::chrono::steady_clock::now();
+        }
+    }
+    void stop() {
+        quit_.store(true);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cv_.notify_all();
+        }
+        for (auto &t : th_) t.join();
+        th_.clear();
+    }
+    std::vector<std::thread> th_;
+    std::atomic<uint64_t> seq_{0};
+    std::atomic<int> active_{0}, sleepers_{0};
+    std::atomic<bool> quit_{false};
+    const std::function<void(size_t)> *fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0}, done_{0};
+    std::mutex mu_;
+    std::condition_variable cv_;
 };
 
 class FastLanesFacade::Impl {
@@ -129,6 +232,11 @@ public:
     std::vector<std::unique_ptr<Batch>> spare;
     std::mutex spare_mu;
     CopyProfile prof;
+    // a lone sink's column helpers (FLS_COPY_SINK_THREADS, default 4; 0 = none),
+    // started at its first chunk; the sink holding cpool_mu uses them
+    ColumnPool cpool;
+    std::mutex cpool_mu;
+    int cpool_threads = 4;
     double encode_s = 0;  // background writer calls (one at a time: the tasks are chained)
     // wait until at most `keep` batches are in flight, the time into *wait
     // (a profiled stage's own counter); false if one failed
@@ -373,6 +481,7 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.staged_peak = 0;
     if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
     if (const char *b = std::getenv("FLS_COPY_STAGED_MB")) s.staged_budget = (uint64_t)std::max(1, std::atoi(b)) << 20;
+    if (const char *b = std::getenv("FLS_COPY_SINK_THREADS")) s.cpool_threads = std::max(0, std::atoi(b));
     return true;
 }
 
@@ -581,13 +690,29 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
         }
     }
     lap(s.prof.prep);
+    // A lone sink (an ordered COPY's, or the serial path's) copies a slice's
+    // columns on the column helpers, VARCHAR columns first (the longest).
+    // Per-column phase laps are taken only without them.
+    std::unique_lock<std::mutex> par;
+    if (s.cpool_threads > 0 && s.nstages.load() <= 1) {
+        par = std::unique_lock<std::mutex>(s.cpool_mu, std::try_to_lock);
+        if (par.owns_lock()) s.cpool.start(s.cpool_threads);
+        else par = std::unique_lock<std::mutex>();
+    }
+    const bool on_pool = par.owns_lock() && s.cpool.size() > 0;
+    std::vector<uint32_t> order;
+    order.reserve(ncol);
+    for (int pass = 0; pass < 2; ++pass)
+        for (size_t c = 0; c < ncol; ++c)
+            if (TypeMapping::IsString(s.wtypes[c]) == (pass == 0)) order.push_back((uint32_t)c);
     // column-major: append each column's slice up to the row-group boundary
     // in bulk; a full batch of row groups goes to the writer
     idx_t r0 = 0;
     while (r0 < chunk.size()) {
         // (a slice is at most one vector: the VARCHAR path's position list)
         const idx_t n = std::min<idx_t>({chunk.size() - r0, s.rg_rows - st.wrows % s.rg_rows, STANDARD_VECTOR_SIZE});
-        for (size_t c = 0; c < s.wtypes.size(); ++c) {
+        std::atomic<int> too_long{-1};  // a VARCHAR column over the writer's 4 GiB per row group
+        auto copy_col = [&](size_t c) {
             Vector &v = chunk.data[c];
             const LogicalType &t = s.wtypes[c];
             RawBuf &col = st.wcols[c];
@@ -641,12 +766,13 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
                     off += len;
                 }
                 if (st.wbytes[c] + bytes > StringLimit()) {  // the writer's offsets are 32-bit
-                    st.error = "column \"" + s.wnames[c] + "\" holds more than 4 GiB of strings in one row group";
-                    return false;
+                    int none = -1;
+                    too_long.compare_exchange_strong(none, (int)c);
+                    return;
                 }
                 st.wbytes[c] += bytes;
-                lap(s.prof.str);
-                continue;
+                if (!on_pool) lap(s.prof.str);
+                return;
             }
             // the physical bytes (FLOAT/DOUBLE bit-exact for ALP); DECIMAL widened to int64
             const idx_t w = TypeMapping::GetFastLanesTypeSize(TypeMapping::DuckDBToFastLanes(t));
@@ -661,7 +787,17 @@ bool FastLanesFacade::Impl::stage_chunk(Stage &st, DataChunk &chunk) {
                     memcpy(dst + 8 * i, &x, 8);
                 }
             }
-            lap(s.prof.fixed);
+            if (!on_pool) lap(s.prof.fixed);
+        };
+        if (on_pool) {
+            s.cpool.run(order.size(), [&](size_t k) { copy_col(order[k]); });
+            lap(s.prof.str);  // (profiled: the helpers' slice time counts as VARCHAR)
+        } else {
+            for (size_t c = 0; c < ncol; ++c) copy_col(c);
+        }
+        if (too_long.load() >= 0) {
+            st.error = "column \"" + s.wnames[too_long.load()] + "\" holds more than 4 GiB of strings in one row group";
+            return false;
         }
         st.wrows += n;
         r0 += n;

@@ -176,6 +176,25 @@ def test_copy_batches_of_row_groups_cpu(ext, ref, tmpfile, monkeypatch, batch, p
     assert rf.strings_column(1) == [x.encode() for x in s]
 
 
+def test_copy_lone_sink_column_helpers_same_bytes(ext, tmpfile, monkeypatch):
+    """A lone sink (an ordered COPY's) copies each slice's columns on helper
+    threads (FLS_COPY_SINK_THREADS, default 4): the file is the one the sink
+    writes alone, NULLs, inlined and pointer strings and a partial row group
+    included."""
+    n = 2 * 65536 + 3000
+    a = [None if i % 97 == 0 else (i * 7919) % 100003 - 50000 for i in range(n)]
+    s = [None if i % 89 == 0 else f"w{i % 7}" * (i % 11) for i in range(n)]
+    d = [i / 4 for i in range(n)]
+    cols = [("a", "INTEGER", a), ("s", "VARCHAR", s), ("d", "DOUBLE", d), ("t", "VARCHAR", [f"x{i % 3}" for i in range(n)])]
+    out = {}
+    for th in ("0", "4"):
+        monkeypatch.setenv("FLS_COPY_SINK_THREADS", th)
+        dst = tmpfile(f"helpers{th}.fls")
+        assert ext.copy_values(cols, dst) == n
+        out[th] = open(dst, "rb").read()
+    assert out["0"] == out["4"]
+
+
 @pytest.mark.parametrize("fmt", ["fls", "fastlane"])
 def test_copy_execution_mode_and_batch_size(ext, fmt):
     """Like the reference's registration (src/writer/write_fastlane_stream.cpp:
