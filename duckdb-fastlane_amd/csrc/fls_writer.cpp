@@ -1323,9 +1323,9 @@ struct FileBuilder {
     // groups encode instead of all at the end; finish writes the footer and
     // renames the file over the destination (a failed or abandoned write
     // leaves no partial file there).  Chunk bytes are freed once written.
-    // Several threads (FLS_WRITER_STREAM_THREADS, default 4): an unordered
-    // COPY completes its last ~1 GB of row groups at once at the end, and one
-    // thread's page-cache writes of that backlog were 0.28 s of a 1.5 s COPY.
+    // FLS_WRITER_STREAM_THREADS (default 1) threads: 4 did not speed up the
+    // end of an unordered COPY, whose last ~1 GB of row groups complete at
+    // once (34.16 vs 34.39 M rows/s, profiles/r5/copy_stream_threads_r5v.txt).
     struct Stream {
         struct Job {
             uint64_t at = 0, len = 0;
@@ -1383,7 +1383,7 @@ struct FileBuilder {
         }
         Stream *sp = st.get();
         const char *nt = getenv("FLS_WRITER_STREAM_THREADS");
-        const int nthreads = std::max(1, std::min(16, nt ? atoi(nt) : 4));
+        const int nthreads = std::max(1, std::min(16, nt ? atoi(nt) : 1));
         for (int t = 0; t < nthreads; ++t) st->th.emplace_back([sp] {
             static const uint8_t zeros[16] = {};
             std::vector<uint8_t> tmp;
