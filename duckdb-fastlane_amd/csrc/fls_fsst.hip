@@ -1145,9 +1145,31 @@ __device__ __forceinline__ void fsst_range(const DevChunk *chunks, uint32_t nchu
             have_table = true;
         }
         const VecArgs a = vec_args(c, v);
+#ifdef FLS_WAVE_TRACE
+        const uint64_t tr0 = wall_clock64();
+#endif
         if constexpr (K == Kind::Seg) seg_vector<SMALL, X>(L, sym, c, a, lane, err);
         else cp_vector<SMALL>(L, c, a, lane, err);
         wave_sync();
+#ifdef FLS_WAVE_TRACE
+        // (timing build) one record per FSST vector: shape enc 0xFE, ob 0,
+        // max_w = its bytes / 128 (records + heap + compressed, estimated)
+        const uint64_t tr1 = wall_clock64();
+        if (lane == 0) {
+            const uint32_t i = atomicAdd(&dec::g_trace_n, 1u);
+            if (i < dec::kTraceCap) {
+                dec::TraceRec &r = dec::g_trace[i];
+                r.t0 = tr0;
+                r.t1 = tr1;
+                r.wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+                r.vr = item;
+                r.hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+                r.xcc_id = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+                r.shape = 0xFEu | 1u << 24;
+                r.max_w = (16u * 1024u + a.dbytes + a.dbytes / 2) / 128u;
+            }
+        }
+#endif
         ++item;
     }
 }
@@ -1662,5 +1684,23 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
 #endif
     return launch_kind2<Kind::Seg>(d_chunks, nchunks, nvecs, d_err, stream, how);
 }
+
+#ifdef FLS_WAVE_TRACE
+// (timing build) this file's trace records: the fused kernel's main chunks
+// and every FSST vector (fls_decode.hip holds decode_kernel's)
+extern "C" int fls_trace_fsst_reset(void) {
+    const uint32_t z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(dec::g_trace_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+extern "C" int64_t fls_trace_fsst_read(void *dst, uint32_t cap) {
+    uint32_t n = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(&n, HIP_SYMBOL(dec::g_trace_n), sizeof(n)) != hipSuccess)
+        return -1;
+    const uint32_t k = std::min(std::min(n, cap), dec::kTraceCap);
+    if (k && hipMemcpyFromSymbol(dst, HIP_SYMBOL(dec::g_trace), k * sizeof(dec::TraceRec)) != hipSuccess) return -1;
+    return n;
+}
+#endif
 
 }  // namespace fls

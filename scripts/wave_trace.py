@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of one main decode launch (the timing build,
+"""Per-wave timeline of one table decode launch (the timing build,
 libflsgpu_trace.so: every decode_chunk call records its start / end from
-s_memrealtime, 100 MHz).  Answers where a launch loses time against its
+s_memrealtime, 100 MHz, and every FSST vector its own -- the fused kernel's
+main chunks and FSST vectors alike, shape enc 0xFE marking FSST).  Answers where a launch loses time against its
 steady-state rate: the ramp at the start, the drain after the queue runs dry,
 and per-chunk durations by column shape.
 
@@ -42,6 +43,9 @@ def main():
     lib.fls_trace_reset.restype = C.c_int
     lib.fls_trace_read.restype = C.c_int64
     lib.fls_trace_read.argtypes = [C.c_void_p, C.c_uint32]
+    lib.fls_trace_fsst_reset.restype = C.c_int
+    lib.fls_trace_fsst_read.restype = C.c_int64
+    lib.fls_trace_fsst_read.argtypes = [C.c_void_p, C.c_uint32]
     lo, hi = map(int, a.cols.split("-")) if "-" in a.cols else (int(a.cols), int(a.cols))
     sel = list(range(lo, hi + 1))
     img = fl.gen_image(a.workload, a.scale)
@@ -51,12 +55,18 @@ def main():
         t.device_decode(sel)
     t.device_sync()
     lib.fls_trace_reset()
+    lib.fls_trace_fsst_reset()
     t.device_decode(sel)
     st = t.device_sync()
     cap = 1 << 20
-    buf = np.zeros(cap, REC)
-    n = lib.fls_trace_read(buf.ctypes.data, cap)
-    r = buf[:min(n, cap)]
+    parts = []
+    n = 0
+    for read in (lib.fls_trace_read, lib.fls_trace_fsst_read):  # fls_decode.hip's records, fls_fsst.hip's
+        buf = np.zeros(cap, REC)
+        k = read(buf.ctypes.data, cap)
+        n += k
+        parts.append(buf[:min(k, cap)])
+    r = np.concatenate(parts)
     kernel_ms = st.kernel_ms_total / max(1, st.timed_launches)
     t0 = r["t0"].min()
     s = (r["t0"] - t0) / 100.0  # us
@@ -100,6 +110,26 @@ def main():
     print(f"timeline ({a.bin_us:.0f} us bins): GB/s, active waves")
     for k in range(nb):
         print(f"  {edges[k]:7.0f} {tl[k] / a.bin_us / 1e3:7.0f} {act[k]:7.0f}")
+    # main chunks against FSST vectors (the fused kernel's two queues)
+    fsst = (r["shape"] & 0xFF) == 0xFE
+    if fsst.any():
+        print("kind: records, bytes (GB), first start, last end (us), wave-us busy, waves")
+        for name, m in (("main", ~fsst), ("fsst", fsst)):
+            if m.any():
+                print(f"  {name}: {m.sum():7d} {byt[m].sum() / 1e9:7.3f} {s[m].min():8.1f} {e[m].max():8.1f} "
+                      f"{(e[m] - s[m]).sum():10.0f} {len(np.unique(r['wave'][m])):5d}")
+        print(f"timeline by kind ({a.bin_us:.0f} us bins): main GB/s, main waves, fsst GB/s, fsst waves")
+        for k in range(nb):
+            row = []
+            for m in (~fsst, fsst):
+                g = 0.0
+                w = 0.0
+                for i in np.flatnonzero(m & (s < edges[k + 1]) & (e > edges[k])):
+                    ov = min(e[i], edges[k + 1]) - max(s[i], edges[k])
+                    g += byt[i] / max(e[i] - s[i], 1e-3) * ov
+                    w += ov / a.bin_us
+                row += [g / a.bin_us / 1e3, w]
+            print(f"  {edges[k]:7.0f} {row[0]:7.0f} {row[1]:7.0f} {row[2]:7.0f} {row[3]:7.0f}")
     # per shape: duration per vector
     keys = np.unique(r["shape"] & 0xFFFFFF)
     print("per chunk shape (enc, T, ob): calls, vectors, us per call mean / p95, us per vector (mean)")
