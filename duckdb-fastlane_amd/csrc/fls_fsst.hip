@@ -354,6 +354,7 @@ enum : int {
     kSegXRecSel = 32,  // string_t records: a branch between the inline and the pointer form
     kSegXClamp = 64,   // ring flush without exec-masked stores (clamped block index, uniform row skips)
     kSegXNoBranch = 128,  // escape-free codes: every code ORs (an incomplete qword into a dummy slot), no exec mask
+    kSegXTwo = 256,       // escape-free segments as two independent 8-code chains (the second's start from the first's lengths)
 };
 template <bool SMALL, int X = 0>
 struct SegLds {
@@ -437,7 +438,7 @@ struct LeanWriter {
 // check catches).  The fast path (FULL, no escapes) issues all 16 table reads
 // together; the general one keeps each code byte (a literal's value) beside
 // its entry and reads 4 at a time to stay in the fast path's registers.
-template <bool FULL, bool ESC, bool SPLIT = false, bool NOBRANCH = false>
+template <bool FULL, bool ESC, bool SPLIT = false, bool NOBRANCH = false, bool TWO = false>
 __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in, uint32_t nb, uint32_t &st,
                                              LeanWriter &qw, lu64 *dummy = nullptr) {
     // an opaque copy: the callers' variants would otherwise share (hoist) the
@@ -464,6 +465,26 @@ __device__ __forceinline__ uint32_t seg_lane(const lu64 *sym, const v4u &raw_in,
                 sl[k] = (uint32_t)(sy[k] >> 56);
                 sy[k] &= 0x00FFFFFFFFFFFFFFull;
             }
+        }
+        if constexpr (kFast && TWO) {
+            // (kSegXTwo) codes 0-7 and 8-15 as two independent chains: the
+            // second starts where the first 8 symbols end (their lengths, in
+            // bits, ride in the entries' top bytes); the chains share at most
+            // the qword at the seam, and OR merges it
+            uint32_t h8 = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) h8 += (uint32_t)(sy[k] >> 56);
+            LeanWriter q2(qw.ring, (8 * qw.a + qw.b + h8) >> 3);
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                qw.put_tagged((uint32_t)sy[k], (uint32_t)(sy[k] >> 32));
+                q2.put_tagged((uint32_t)sy[k + 8], (uint32_t)(sy[k + 8] >> 32));
+            }
+            qw.finish();
+            qw.acc = q2.acc;  // the lane goes on as the second chain (start kept: bytes() counts both)
+            qw.a = q2.a;
+            qw.b = q2.b;
+            return qw.bytes();
         }
 #pragma unroll
         for (uint32_t k = 0; k < B; ++k) {
@@ -724,10 +745,11 @@ __device__ void seg_vector(lu8 *L, const lu64 *sym, const DevChunk &c, const Vec
                 constexpr bool kSplit = (X & kSegXSplit) != 0;
                 // (kSegXNoBranch) the lane's dummy slot: the 256 B pad before the ring
                 constexpr bool kNoBr = (X & kSegXNoBranch) != 0 && (X & kSegXNoPad) == 0;
+                constexpr bool kTwo = (X & kSegXTwo) != 0 && !kNoBr && !kSplit;
                 lu64 *dummy = reinterpret_cast<lu64 *>(ring - 256) + (lane & 31);
                 uint32_t got = !full   ? seg_lane<false, true, kSplit>(sym, raw, nb, st, qw)
                                : vec_esc ? seg_lane<true, true, kSplit>(sym, raw, nb, st, qw)
-                                         : seg_lane<true, false, kSplit, kNoBr>(sym, raw, nb, st, qw, dummy);
+                                         : seg_lane<true, false, kSplit, kNoBr, kTwo>(sym, raw, nb, st, qw, dummy);
                 if constexpr (SEGS == 2) {
                     const uint32_t nb1 = idx0 + 16 < comp_len ? min(comp_len - idx0 - 16, 16u) : 0u;
                     if (got != dl0 || (nb1 > 0 && st != entry1)) bad = true;
@@ -1629,7 +1651,7 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
 #ifdef FLS_EXPERIMENTS
         const int x = variant >> kSegXShift;
         if ((variant & ((1 << kSegXShift) - 1)) == kFsstDefault &&
-            ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48 || x == 64 || x == 128))
+            ((x >= 1 && x <= 9) || x == 16 || x == 32 || x == 48 || x == 64 || x == 128 || x == 256))
             return true;
 #endif
     }
@@ -1647,6 +1669,11 @@ hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *
                                                                        stream, d_queues, how)
                      : launch_fused_t<false, kSegXFlush | kSegXRecSel>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom,
                                                                         stream, d_queues, how);
+    if (how.x == kSegXTwo)
+        return small ? launch_fused_t<true, kSegXTwo>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream,
+                                                      d_queues, how)
+                     : launch_fused_t<false, kSegXTwo>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream,
+                                                       d_queues, how);
     if (how.x == kSegXNoBranch)
         return small ? launch_fused_t<true, kSegXNoBranch>(d_main, nmain, d_fsst, nfsst, nfvecs, d_err, geom, stream,
                                                            d_queues, how)
@@ -1679,6 +1706,7 @@ hipError_t launch_fsst(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
     case 48: return launch_kind2<Kind::Seg, 48>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 64: return launch_kind2<Kind::Seg, 64>(d_chunks, nchunks, nvecs, d_err, stream, how);
     case 128: return launch_kind2<Kind::Seg, 128>(d_chunks, nchunks, nvecs, d_err, stream, how);
+    case 256: return launch_kind2<Kind::Seg, 256>(d_chunks, nchunks, nvecs, d_err, stream, how);
     default: break;
     }
 #endif

@@ -31,7 +31,12 @@ def main():
     ap.add_argument("--bin-us", type=float, default=20.0)
     ap.add_argument("--env", default="", help="VAR=v,VAR2=v set for the traced launch")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "wave_trace.npz"))
+    ap.add_argument("--from-npz", default="", help="analyse a saved trace (no GPU)")
     a = ap.parse_args()
+    if a.from_npz:
+        z = np.load(a.from_npz)
+        analyse(a, z["rec"], float(z["kernel_ms"]), len(z["rec"]))
+        return
     os.environ.setdefault("FLS_LIB", "libflsgpu_trace.so")
     for kv in filter(None, a.env.split(",")):
         k, v = kv.split("=", 1)
@@ -68,13 +73,20 @@ def main():
         parts.append(buf[:min(k, cap)])
     r = np.concatenate(parts)
     kernel_ms = st.kernel_ms_total / max(1, st.timed_launches)
+    analyse(a, r, kernel_ms, n)
+    Path(a.out).parent.mkdir(exist_ok=True)
+    np.savez_compressed(a.out, rec=r, kernel_ms=kernel_ms)
+
+
+def analyse(a, r, kernel_ms, n):
     t0 = r["t0"].min()
     s = (r["t0"] - t0) / 100.0  # us
     e = (r["t1"] - t0) / 100.0
     span = e.max()
     vb = r["vr"] & 0xFF
     ve = r["vr"] >> 8
-    nv = np.minimum(ve, r["shape"] >> 24) - vb
+    fsst = (r["shape"] & 0xFF) == 0xFE  # one FSST vector per record (vr = its index)
+    nv = np.where(fsst, 1, np.minimum(ve, r["shape"] >> 24) - vb)
     ob = (r["shape"] >> 16) & 0xFF
     byt = nv * (1024.0 * ob + 128.0 * r["max_w"])
     waves = np.unique(r["wave"])
@@ -111,7 +123,6 @@ def main():
     for k in range(nb):
         print(f"  {edges[k]:7.0f} {tl[k] / a.bin_us / 1e3:7.0f} {act[k]:7.0f}")
     # main chunks against FSST vectors (the fused kernel's two queues)
-    fsst = (r["shape"] & 0xFF) == 0xFE
     if fsst.any():
         print("kind: records, bytes (GB), first start, last end (us), wave-us busy, waves")
         for name, m in (("main", ~fsst), ("fsst", fsst)):
@@ -146,8 +157,6 @@ def main():
     for x in np.unique(r["xcc"] & 0xF):
         m = (r["xcc"] & 0xF) == x
         print(f"  xcc {x}: calls {m.sum()}, bytes {byt[m].sum() / 1e9:.3f} GB, last end {e[m].max():.1f} us")
-    Path(a.out).parent.mkdir(exist_ok=True)
-    np.savez_compressed(a.out, rec=r, kernel_ms=kernel_ms)
 
 
 if __name__ == "__main__":
