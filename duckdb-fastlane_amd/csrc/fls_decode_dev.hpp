@@ -111,12 +111,15 @@ __device__ __forceinline__ VecInfo vec_info(const ChunkMetas &m, uint32_t v) {
 // instruction i is issued only when some lane needs it (a wave-uniform
 // branch on W); inside it, lanes past the end re-read a safe dummy line.  The
 // waits stay exact: what follows the prefetch (the stores) is fixed per path.
-template <int L>
+// ALL: every one of the L loads is issued (past the end: the dummy line), so
+// the number of memory operations between a load and its use is fixed and
+// the compiler's vmcnt waits can leave a second vector's loads in flight
+template <int L, bool ALL = false>
 __device__ __forceinline__ void prefetch(gv4 *__restrict__ src, uint32_t n16, gv4 *__restrict__ dummy,
                                          uint32_t lane, v4u (&r)[L]) {
 #pragma unroll
     for (int i = 0; i < L; ++i) {
-        if (64 * i < n16) {
+        if (ALL || 64 * i < n16) {
             const uint32_t idx = lane + 64 * i;
             r[i] = ld16(idx < n16 ? src + idx : dummy);
         }
@@ -590,6 +593,69 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
     const uint32_t last_nvals = rl(m.nvbw, nvec - 1) & 0xFFFF;
     const uint32_t nfull = (ve == nvec && last_nvals != kVectorSize) ? ve - 1 : ve;
 
+#ifndef FLS_PREFETCH1
+    // Two vectors ahead: the packed bits of v + 1 and v + 2 are in flight
+    // while v decodes (two register sets, the loop unrolled by two so each
+    // set keeps its registers; every prefetch issues all L loads, so the
+    // compiler's vmcnt waits leave the second set in flight).  A wave's bytes
+    // in flight bound the main decode: its rate per wave was the same alone
+    // and beside the FSST waves of the fused kernel.
+    // Measured against one vector ahead (FLS_PREFETCH1, interleaved builds,
+    // profiles/r5/ab_prefetch2_*_r5z.txt): lineitem_full SF12.5 2.846 vs
+    // 3.104 ms, SF100 20.98 vs 21.10 ms.
+    if (vb < ve) {
+        v4u ra[L], rb[L];
+        VecInfo xa = vec_info(m, vb);
+        Aux aa, ab;
+        aa.load(path.aux_ptr(c, xa), lane);
+        prefetch<L, true>(packed + xa.poff16, 8 * xa.W, dummy, lane, ra);
+        VecInfo xb = vec_info(m, min(vb + 1, ve - 1));
+        ab.load(path.aux_ptr(c, xb), lane);
+        prefetch<L, true>(packed + xb.poff16, 8 * xb.W, dummy, lane, rb);
+        uint32_t v = vb;
+        for (;;) {
+            if (v >= nfull) break;
+            wave_sync();
+            stage<L>(s.P, ra, 8 * xa.W, lane);
+            {
+                const VecInfo xn = vec_info(m, min(v + 2, ve - 1));
+                Aux an;
+                an.load(path.aux_ptr(c, xn), lane);
+                prefetch<L, true>(packed + xn.poff16, 8 * xn.W, dummy, lane, ra);
+                wave_sync();
+                path.template vec<true>(s, xa, aa, out + (size_t)v * kVectorSize * ob, lane);
+                xa = xn;
+                aa = an;
+            }
+            ++v;
+            if (v >= nfull) break;
+            wave_sync();
+            stage<L>(s.P, rb, 8 * xb.W, lane);
+            {
+                const VecInfo xn = vec_info(m, min(v + 2, ve - 1));
+                Aux an;
+                an.load(path.aux_ptr(c, xn), lane);
+                prefetch<L, true>(packed + xn.poff16, 8 * xn.W, dummy, lane, rb);
+                wave_sync();
+                path.template vec<true>(s, xb, ab, out + (size_t)v * kVectorSize * ob, lane);
+                xb = xn;
+                ab = an;
+            }
+            ++v;
+        }
+        if (nfull < ve) {  // partial tail vector: in ra after an even number of full ones
+            wave_sync();
+            const bool in_a = ((v - vb) & 1) == 0;
+            if (in_a) stage<L>(s.P, ra, 8 * xa.W, lane);
+            else stage<L>(s.P, rb, 8 * xb.W, lane);
+            wave_sync();
+            if (in_a) path.template vec<false>(s, xa, aa, out + (size_t)v * kVectorSize * ob, lane);
+            else path.template vec<false>(s, xb, ab, out + (size_t)v * kVectorSize * ob, lane);
+        }
+    }
+    return;
+#endif
+    // (FLS_PREFETCH1 builds) one vector ahead
     v4u r[L];
     Aux aux, aux_next;
     // aux (DELTA / RLE bases) is loaded before the packed bits of the same
