@@ -593,16 +593,15 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
     const uint32_t last_nvals = rl(m.nvbw, nvec - 1) & 0xFFFF;
     const uint32_t nfull = (ve == nvec && last_nvals != kVectorSize) ? ve - 1 : ve;
 
-#ifndef FLS_PREFETCH1
-    // Two vectors ahead: the packed bits of v + 1 and v + 2 are in flight
-    // while v decodes (two register sets, the loop unrolled by two so each
-    // set keeps its registers; every prefetch issues all L loads, so the
-    // compiler's vmcnt waits leave the second set in flight).  A wave's bytes
-    // in flight bound the main decode: its rate per wave was the same alone
-    // and beside the FSST waves of the fused kernel.
-    // Measured against one vector ahead (FLS_PREFETCH1, interleaved builds,
-    // profiles/r5/ab_prefetch2_*_r5z.txt): lineitem_full SF12.5 2.846 vs
-    // 3.104 ms, SF100 20.98 vs 21.10 ms.
+#ifdef FLS_PREFETCH2
+    // (experiment build) two vectors ahead: the packed bits of v + 1 and v + 2
+    // in flight while v decodes (two register sets, the loop unrolled by two
+    // so each set keeps its registers; every prefetch issues all L loads, so
+    // the compiler's vmcnt waits leave the second set in flight).  Not a
+    // gain: with the load order of the two builds in one process swapped,
+    // each build measured the same when loaded first (3.109 / 3.109 ms,
+    // lineitem_full SF12.5) -- the 2.85 ms first seen was the second-loaded
+    // build's advantage (profiles/r5/ab_prefetch_order_r6b.txt).
     if (vb < ve) {
         v4u ra[L], rb[L];
         VecInfo xa = vec_info(m, vb);
@@ -655,7 +654,6 @@ __device__ __attribute__((noinline)) void run_chunk(const DevChunk *chunk_generi
     }
     return;
 #endif
-    // (FLS_PREFETCH1 builds) one vector ahead
     v4u r[L];
     Aux aux, aux_next;
     // aux (DELTA / RLE bases) is loaded before the packed bits of the same
