@@ -6,6 +6,12 @@ side by side; the same SF image is uploaded once per variant and launches
 alternate A, B, A, B ...  Kernel time from HIP events per launch.
 
     python scripts/ab.py --variants base,noseq [--scale 100] [--rounds 7] [--cols all,0,8]
+
+Caveat (round 5, profiles/r5/ab_prefetch_order_r6b.txt): of two DIFFERENT
+builds in one process, the one loaded second decoded lineitem_full SF12.5
+~10 % faster whatever its code (3.109 ms first, 2.74-2.81 ms second, in both
+orders), while one build loaded twice measured the same (ab_same_build_twice_
+r6c.txt).  Compare builds in both orders, each at the same load position.
 """
 import argparse
 import importlib.util
