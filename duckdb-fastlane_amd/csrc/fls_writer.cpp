@@ -2449,6 +2449,15 @@ void fill_nulls(uint8_t *vals, uint32_t w, uint32_t n, const std::vector<uint64_
 // that end where the batch is full or out of room, since a batch is only
 // submitted once every row group in it is staged.
 int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
+    // a pipelined writer's previous call is done when this one returns with
+    // an error (its caller may then free that call's buffers)
+    struct SettleOnError {
+        fls_writer *w;
+        bool ok = false;
+        ~SettleOnError() {
+            if (!ok && w->pend) append_segment(w, std::move(w->pend));
+        }
+    } settle{w};
     if (w->fb.cols.empty()) return fail(FLS_ERR_STATE, "no columns");
     if (w->broken) return fail(FLS_ERR_STATE, "writer failed earlier: %s", w->broken_msg.c_str());
     const size_t ncols = w->fb.cols.size();
@@ -2656,7 +2665,9 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
         run_seg();
     }
     if (const int rc = seg_failed()) return rc;
-    return w->fb.flush_stream(false);  // streamed output: the complete row groups go to the file
+    const int rc = w->fb.flush_stream(false);  // streamed output: the complete row groups go to the file
+    settle.ok = rc == 0;
+    return rc;
 }
 }  // namespace
 

@@ -296,13 +296,19 @@ def test_pipelined_short_row_group_rule_sees_the_pending_call(fl):
         assert fl.lib.fls_writer_add_rowgroup(w, 1000, data, None) == 0
         assert fl.lib.fls_writer_add_rowgroup(w, 1024, data, None) < 0
         assert "only the last row group" in fl.last_error()
+        # the failed call settled the pending one: its buffers are free now
+        x[:] = -1
         assert fl.lib.fls_writer_set_rowgroup_size(w, 2048) < 0   # a row group is pending
         assert fl.lib.fls_writer_set_pipelined(w, 0) == 0
         p, ln = ctypes.c_void_p(), ctypes.c_uint64()
         assert fl.lib.fls_writer_finish_image(w, ctypes.byref(p), ctypes.byref(ln)) == 0
+        img = ctypes.string_at(p, ln.value)
         fl.lib.fls_image_free(p)
     finally:
         fl.lib.fls_writer_free(w)
+    # the one row group holds 0..999 (written before x was overwritten)
+    ref = fl.write_image([("x", fl.INT32, np.arange(1000, dtype=np.int32), fl.ENC_FFOR)], rowgroup=1024)
+    assert img == bytes(ref.view())
 
 
 def test_streamed_output_abandoned_leaves_nothing(fl, tmp_path):
