@@ -104,7 +104,10 @@ int fls_writer_set_output(fls_writer *w, const char *path);
  * file is the same.  The buffers of call k (the pointer arrays included) must
  * stay valid until call k+1, a finish, fls_writer_set_pipelined(w, 0) or
  * fls_writer_free returns.
- * on == 0 waits for the pending call's row groups. */
+ * on == 0 waits for the pending call's row groups.  No reference counterpart
+ * (the reference's COPY writer is a stub, src/writer/write_fastlane_stream.cpp:
+ * 65-107); the COPY sink of extension/src/scanner/ext_fastlanes_facade.cpp
+ * uses it. */
 int fls_writer_set_pipelined(fls_writer *w, int on);
 /* Assemble the file: to `path` (written beside it, then renamed over it), or
  * into a malloc'ed buffer freed with fls_image_free. */
