@@ -11,6 +11,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <exception>
 #include <functional>
 #include <cstring>
 #include <deque>
@@ -89,7 +90,9 @@ public:
         quit_ = false;
         for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
     }
-    // fn(0..n-1) on the caller and the helpers; returns when every call is done
+    // fn(0..n-1) on the caller and the helpers; returns when every call is
+    // done, rethrowing on the caller the first exception a call threw (a
+    // helper's bad_alloc must not end the process)
     void run(size_t n, const std::function<void(size_t)> &fn) {
         if (th_.empty() || n < 2) {
             for (size_t i = 0; i < n; ++i) fn(i);
@@ -107,14 +110,26 @@ public:
             std::lock_guard<std::mutex> lk(mu_);
             cv_.notify_all();
         }
-        for (size_t i; (i = next_.fetch_add(1)) < n;) {
-            fn(i);
-            done_.fetch_add(1);
-        }
+        for (size_t i; (i = next_.fetch_add(1)) < n;) call(i);
         while (done_.load() != n) spin();
+        if (failed_.load()) {
+            failed_.store(false);
+            std::exception_ptr e = std::move(error_);
+            error_ = nullptr;
+            std::rethrow_exception(e);
+        }
     }
 
 private:
+    void call(size_t i) {
+        try {
+            (*fn_)(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!failed_.exchange(true)) error_ = std::current_exception();
+        }
+        done_.fetch_add(1);
+    }
     static void spin() {
 #if defined(__x86_64__)
         __builtin_ia32_pause();
@@ -130,10 +145,7 @@ private:
                 active_.fetch_add(1);
                 if (seq_.load() == g) {
                     seen = g;
-                    for (size_t i; (i = next_.fetch_add(1)) < n_;) {
-                        (*fn_)(i);
-                        done_.fetch_add(1);
-                    }
+                    for (size_t i; (i = next_.fetch_add(1)) < n_;) call(i);
                 }
                 active_.fetch_sub(1);
                 idle = std::chrono::steady_clock::now();
@@ -169,6 +181,8 @@ private:
     const std::function<void(size_t)> *fn_ = nullptr;
     size_t n_ = 0;
     std::atomic<size_t> next_{0}, done_{0};
+    std::atomic<bool> failed_{false};
+    std::exception_ptr error_;
     std::mutex mu_;
     std::condition_variable cv_;
 };
