@@ -311,6 +311,39 @@ def test_pipelined_short_row_group_rule_sees_the_pending_call(fl):
     assert img == bytes(ref.view())
 
 
+def test_pipelined_free_without_finish_waits_for_pending(fl):
+    # freeing a pipelined writer whose last call is still encoding waits for
+    # it (its tasks read the caller's buffers) -- no crash, nothing leaks
+    for _ in range(3):
+        w = fl.lib.fls_writer_new(0)
+        try:
+            assert fl.lib.fls_writer_set_rowgroup_size(w, 1024) == 0
+            assert fl.lib.fls_writer_add_column(w, b"s", fl.VARCHAR, 0, 0, fl.ENC_AUTO) == 0
+            assert fl.lib.fls_writer_set_threads(w, 4) == 0
+            assert fl.lib.fls_writer_set_pipelined(w, 1) == 0
+            strs = [b"pending row %d" % i for i in range(8 * 1024)]
+            buf = np.frombuffer(b"".join(strs), dtype=np.uint8).copy()
+            offs = np.zeros(len(strs) + 1, dtype=np.uint32)
+            offs[1:] = np.cumsum([len(x) for x in strs])
+            nrows = (ctypes.c_uint32 * 8)(*([1024] * 8))
+            data = (ctypes.c_void_p * 8)(*[buf.ctypes.data] * 8)
+            op = (ctypes.c_void_p * 8)(*[offs.ctypes.data + 4 * 1024 * k for k in range(8)])
+            # row group k: strings [1024 k, 1024 k + 1024), offsets relative to buf
+            assert fl.lib.fls_writer_add_rowgroups(w, 8, nrows, data, op) == 0
+        finally:
+            fl.lib.fls_writer_free(w)
+
+
+def test_pipelined_image_matches_across_thread_counts(fl):
+    # any thread count, pipelined, writes the unpipelined image's bytes
+    n = 9 * 1024 + 11
+    cols = _mixed_columns(fl, n, 23)
+    ref = fl.write_image(cols, rowgroup=1024, batch=2, threads=3).tobytes()
+    for threads in (1, 2, 7):
+        got = fl.write_image(cols, rowgroup=1024, batch=2, threads=threads, pipelined=True).tobytes()
+        assert got == ref
+
+
 def test_streamed_output_abandoned_leaves_nothing(fl, tmp_path):
     # a writer freed without its finish (a failed COPY) removes its temporary
     # file and leaves the destination as it was
