@@ -14,12 +14,13 @@ def main():
     ap.add_argument("--scale", type=float, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cols", default="15")
+    ap.add_argument("--workload", default="lineitem_full")
     a = ap.parse_args()
     lo, hi = map(int, a.cols.split("-")) if "-" in a.cols else (int(a.cols), int(a.cols))
     cols = list(range(lo, hi + 1))
     import pkgload
     fl = pkgload.load()
-    t = fl.Connection([0]).read_image(fl.gen_image("lineitem_full", a.scale))
+    t = fl.Connection([0]).read_image(fl.gen_image(a.workload, a.scale))
     t.device_upload()
     for _ in range(a.reps):
         t.device_decode(cols)

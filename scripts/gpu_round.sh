@@ -94,8 +94,8 @@ for mode in "$@"; do
     step 600 $O/abenv_${TAG}_${wl}_${sc}.txt python scripts/ab_env.py --workload "$wl" --scale "$sc" --cols "$cols" \
         --arms $(echo "$arms" | tr ';' ' ') || exit $?
     grep -v amdgpu.ids $O/abenv_${TAG}_${wl}_${sc}.txt ;;
-  fsstsq:*)   # fsstsq:<kernel substring>[:<scale>[:<cols>]]: SQ counters of a kernel on l_comment (or cols), 3 PMC passes
-    IFS=: read -r _ kern sc cols <<< "$mode"
+  fsstsq:*)   # fsstsq:<kernel substring>[:<scale>[:<cols>[:<workload>]]]: SQ counters of a kernel on l_comment (or cols), 3 PMC passes
+    IFS=: read -r _ kern sc cols wl <<< "$mode"
     P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU"
     P2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_WAVES"
     P3="SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU"
@@ -103,7 +103,7 @@ for mode in "$@"; do
     for P in "$P1" "$P2" "$P3"; do
       i=$((i+1))
       timeout -k 10 -s KILL 120 rocprofv3 --pmc $P -d $O/fsq_${TAG}_$i -o pmc --output-format csv -- \
-          python3 scripts/fsst_prof.py --scale "${sc:-10}" --cols "${cols:-15}" > $O/fsq_${TAG}_$i.log 2>&1
+          python3 scripts/fsst_prof.py --scale "${sc:-10}" --cols "${cols:-15}" --workload "${wl:-lineitem_full}" > $O/fsq_${TAG}_$i.log 2>&1
       rc=$?; echo "[$TAG] pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/fsq_${TAG}_$i.log; exit $rc; }
     done
     python3 scripts/pmc_summary.py "$kern" $O/fsq_${TAG}_1 $O/fsq_${TAG}_2 $O/fsq_${TAG}_3 | tee $O/fsst_sq_$TAG.txt ;;
