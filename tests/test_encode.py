@@ -347,11 +347,13 @@ def test_gpu_writer_fsst_failure_marks_writer_failed(fl, gpu, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_encoder_failure_marks_writer_failed(fl, gpu, monkeypatch):
+@pytest.mark.parametrize("pipelined", [0, 1])
+def test_gpu_encoder_failure_marks_writer_failed(fl, gpu, monkeypatch, pipelined):
     """A GPU encoder set that comes back without one of its chunks (injected:
     FLS_TEST_FAIL_GPU_ENCODE) fails the call that completes it, names the row
     group and column, and leaves the writer failed: no later finish writes a
-    file whose row groups miss chunks."""
+    file whose row groups miss chunks -- also with pipelined calls (the
+    pending row group is appended before the set completes)."""
     import ctypes as C
     rng = np.random.default_rng(6)
     n = 4096
@@ -362,7 +364,15 @@ def test_gpu_encoder_failure_marks_writer_failed(fl, gpu, monkeypatch):
         assert fl.lib.fls_writer_set_device(w, 0) == 0
         assert fl.lib.fls_writer_add_column(w, b"i", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
         assert fl.lib.fls_writer_add_column(w, b"s", fl.VARCHAR, 0, 0, fl.ENC_AUTO) == 0
-        assert _add_rg(fl, w, rng.integers(0, 1000, n), strs) == 0
+        assert fl.lib.fls_writer_set_pipelined(w, pipelined) == 0
+        # (the buffers live to the end: a pipelined call's tasks read them later)
+        ints = np.ascontiguousarray(rng.integers(0, 1000, n), dtype=np.int32)
+        o = np.zeros(n + 1, dtype=np.uint32)
+        o[1:] = np.cumsum([len(x) for x in strs])
+        buf = np.frombuffer(b"".join(strs), dtype=np.uint8).copy()
+        data = (C.c_void_p * 2)(ints.ctypes.data, buf.ctypes.data)
+        offs = (C.c_void_p * 2)(None, o.ctypes.data)
+        assert fl.lib.fls_writer_add_rowgroup(w, n, data, offs) == 0
         monkeypatch.setenv("FLS_TEST_FAIL_GPU_ENCODE", "1")
         p, ln = C.c_void_p(), C.c_uint64()
         assert fl.lib.fls_writer_finish_image(w, C.byref(p), C.byref(ln)) < 0
