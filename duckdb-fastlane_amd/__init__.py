@@ -98,6 +98,10 @@ def _sig(name, res, *args):
 _P = C.c_void_p
 _sig("fls_last_error", C.c_char_p)
 _sig("fls_version", C.c_char_p)
+_sig("fls_config_default", C.c_int, C.c_char_p, C.POINTER(C.c_int64))
+_sig("fls_config_value", C.c_int, C.c_char_p, C.POINTER(C.c_int64))
+_sig("fls_config_count", C.c_int)
+_sig("fls_config_name", C.c_char_p, C.c_int)
 _sig("fls_device_count", C.c_int)
 _sig("fls_connect", C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(_P))
 _sig("fls_disconnect", None, _P)
@@ -184,6 +188,18 @@ def last_error() -> str:
 
 def version() -> str:
     return _lib.fls_version().decode()
+
+
+def config() -> dict[str, tuple[int, int]]:
+    """The deployment knobs: name -> (compiled default, value in effect)."""
+    out = {}
+    for i in range(_lib.fls_config_count()):
+        name = _lib.fls_config_name(i)
+        d, v = C.c_int64(), C.c_int64()
+        _check(_lib.fls_config_default(name, C.byref(d)))
+        _check(_lib.fls_config_value(name, C.byref(v)))
+        out[name.decode()] = (d.value, v.value)
+    return out
 
 
 def device_count() -> int:

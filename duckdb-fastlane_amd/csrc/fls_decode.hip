@@ -254,4 +254,66 @@ hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d
     return hipGetLastError();
 }
 
+// ---- HBM placement probe ---------------------------------------
+namespace {
+// the decode's write stream without the decode: wave w writes regions w, w+NW,
+// ... front to back, 1 KiB per store instruction
+__global__ __launch_bounds__(64) void probe_regions_kernel(const ProbeRegion *__restrict__ r, uint32_t n) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint64_t p = (uint64_t)r[i].out, nb = r[i].bytes >> 10;
+        // uni() returns the readfirstlane value as uint32_t: the builtin's int
+        // would sign-extend a low word >= 2^31 across the high word
+        FLS_GLOBAL v4u *o = (FLS_GLOBAL v4u *)((uint64_t)uni((uint32_t)(p >> 32)) << 32 | (uint64_t)uni((uint32_t)p));
+        const v4u z = {0u, 0u, 0u, 0u};
+        for (uint64_t b = 0; b < nb; ++b) o[b * 64 + lane] = z;
+    }
+}
+// a linear fill: one 4 KiB block per 256-thread workgroup, dispatch order =
+// address order (placement-insensitive in every measurement)
+__global__ __launch_bounds__(256) void probe_fill_kernel(v4u *__restrict__ out) {
+    ((FLS_GLOBAL v4u *)out)[(size_t)blockIdx.x * 256 + threadIdx.x] = v4u{0u, 0u, 0u, 0u};
+}
+}  // namespace
+
+hipError_t probe_placement(const ProbeRegion *d_regions, uint32_t nregions, uint8_t *const *bufs,
+                           const uint64_t *buf_bytes, uint32_t nbuf, int reps, hipStream_t stream, float *chunk_ms,
+                           float *fill_ms) {
+    int dev = 0, cus = 256;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    hipEvent_t a, b;
+    if ((e = hipEventCreate(&a)) != hipSuccess) return e;
+    if ((e = hipEventCreate(&b)) != hipSuccess) {
+        hipEventDestroy(a);
+        return e;
+    }
+    float best_c = 1e30f, best_f = 1e30f;
+    for (int r = 0; r <= reps && e == hipSuccess; ++r) {  // r == 0 warms up
+        float ms = 0;
+        hipEventRecord(a, stream);
+        hipLaunchKernelGGL(probe_regions_kernel, dim3(cus * 16), dim3(64), 0, stream, d_regions, nregions);
+        hipEventRecord(b, stream);
+        if ((e = hipEventSynchronize(b)) != hipSuccess) break;
+        hipEventElapsedTime(&ms, a, b);
+        if (r) best_c = std::min(best_c, ms);
+        hipEventRecord(a, stream);
+        for (uint32_t i = 0; i < nbuf; ++i)
+            if (buf_bytes[i] >= 4096)
+                hipLaunchKernelGGL(probe_fill_kernel, dim3((uint32_t)(buf_bytes[i] >> 12)), dim3(256), 0, stream,
+                                   (v4u *)bufs[i]);
+        hipEventRecord(b, stream);
+        if ((e = hipEventSynchronize(b)) != hipSuccess) break;
+        hipEventElapsedTime(&ms, a, b);
+        if (r) best_f = std::min(best_f, ms);
+    }
+    if (e == hipSuccess) e = hipGetLastError();
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    *chunk_ms = best_c;
+    *fill_ms = best_f;
+    return e;
+}
+
 }  // namespace fls

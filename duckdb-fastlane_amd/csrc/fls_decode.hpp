@@ -173,6 +173,10 @@ hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *
 // per lane for the code-parallel one); the experiment library (`make lab`,
 // fls_fsst_lab.hip) every variant.  launch_fsst refuses the others.
 bool fsst_variant_built(int variant, bool seg, int bytes_per_lane);
+// Whether this build holds the fused kernel's FSST-part bits x
+// (FusedLaunch::x, FLS_FUSED_X): 0 always, the others in the experiment
+// library only.
+bool fused_x_built(int x);
 // Launch the string-parallel FSST decode over nchunks FSST chunks whose
 // strings are all <= 255 bytes (DevChunk.vbits = 1), nvecs vectors numbered
 // through DevChunk.vec_base (fls_fsst.hip).
@@ -180,6 +184,24 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
                           hipStream_t stream);
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
+
+// HBM placement probe (round 6).  How fast the decode's write
+// stream runs depends on where the driver placed the output buffers: the same
+// pure write of the decode's output shape ran 5.66-6.89 TB/s from one
+// allocation to the next at identical virtual addresses, while a linear fill
+// (one 4 KiB block per 256-thread workgroup) ran 6.82-6.94 TB/s on every one
+// (profiles/r6/membw7_*.txt, membw8_*.txt, membw9_*.txt).  The probe times
+// both on a candidate set of output buffers; their ratio rates the placement.
+struct ProbeRegion {  // 16 B: one output chunk, written front to back by one wave
+    uint8_t *out;
+    uint64_t bytes;   // a multiple of 1 KiB
+};
+// Time (ms, HIP events, best of `reps`) of the chunk-order write over the
+// regions (persistent 1-wave blocks, wave w takes regions w, w + NW, ...) and
+// of a linear fill of each of the `nbuf` buffers.
+hipError_t probe_placement(const ProbeRegion *d_regions, uint32_t nregions, uint8_t *const *bufs,
+                           const uint64_t *buf_bytes, uint32_t nbuf, int reps, hipStream_t stream, float *chunk_ms,
+                           float *fill_ms);
 // LDS bytes per wave the v2 kernel needs for one chunk (given its max width)
 inline void chunk_lds_need(uint8_t enc, uint8_t T, uint8_t ob, uint32_t dict_count, uint32_t max_w,
                            uint32_t &p_bytes, uint32_t &v_bytes) {

@@ -1658,6 +1658,15 @@ bool fsst_variant_built(int variant, bool seg, int bytes_per_lane) {
     return false;
 }
 
+bool fused_x_built(int x) {
+    if (x == 0) return true;
+#ifdef FLS_EXPERIMENTS
+    return x == (kSegXFlush | kSegXRecSel) || x == kSegXTwo || x == kSegXNoBranch;
+#else
+    return false;
+#endif
+}
+
 hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
                         uint32_t nfvecs, bool small, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,
                         uint32_t *d_queues, const FusedLaunch &how) {

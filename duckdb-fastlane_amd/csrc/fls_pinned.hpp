@@ -7,8 +7,8 @@
 // hipHostRegister'ed pins at 22 GB/s on one thread (76 GB/s on four), but
 // with every pinned buffer of the engine allocated that way the GPU test
 // suite faulted twice ("illegal memory access" in a later pageable D2H copy,
-// profiles/r5/pytest_gpu_r5h.log, _r5j.log; the same suite passed with
-// hipHostMalloc, _r5i.log), although the registration's device pointer was
+// profiles/r5/pytest_gpu_r5h_fault.log, _r5j_fault.log; the same suite passed with
+// hipHostMalloc, pytest_gpu_hostmalloc_r5i.log), although the registration's device pointer was
 // checked and the GPUs were synchronised before every unregister -- most
 // likely a freed registration's address range reused by the allocator while
 // the runtime still mapped it.  So hipHostMalloc it is; the finding is in

@@ -34,6 +34,7 @@
 #include "../../include/flswriter.h"
 #include "fls_alp.hpp"
 #include "fls_common.hpp"
+#include "fls_config.hpp"
 #include "fls_encode.hpp"
 #include "fls_format.hpp"
 #include "fls_gen.hpp"
@@ -980,15 +981,13 @@ std::vector<uint8_t> encode_str_chunk(uint8_t enc, const uint32_t *offs, const c
     StrDict d;
     const uint32_t limit = enc == ENC_AUTO ? n / 8 : n;
     bool few;
-    const char *dg = getenv("FLS_WRITER_DICT_GPU");
     // VARCHAR dictionaries on the GPU are opt-in (FLS_WRITER_STRDICT_GPU=1):
     // a chunk's build is one synchronous round trip (~0.45 ms of copies and
     // kernels, queued behind the other workers' on the device), slower in
     // COPY than the host threads' build
-    const char *sg = getenv("FLS_WRITER_STRDICT_GPU");
     const uint64_t t0 = g_str_prof_on ? StrProfile::now_ns() : 0;
     if (g_str_prof_on) ++g_str_prof.chunks;
-    if (gpu && n > 0 && !(dg && atoi(dg) == 0) && sg && atoi(sg) != 0) {
+    if (gpu && n > 0 && knob_value("FLS_WRITER_DICT_GPU") != 0 && knob_value("FLS_WRITER_STRDICT_GPU") != 0) {
         FsstGpuCtx *g = gpu->take();
         const int rc = g->run_dict(gpu->dev, offs, bytes, n, limit, d, few);
         if (g_str_prof_on) g_str_prof.dict_ns += StrProfile::now_ns() - t0;
@@ -1343,7 +1342,7 @@ struct FileBuilder {
         std::deque<Job> q;
         uint64_t queued = 0;             // bytes waiting in q
         bool stop = false;
-        int err = 0;                     // errno of a failed write
+        std::atomic<int> err{0};         // errno of a failed write (read by writer threads without mu)
         static constexpr uint64_t kMaxQueued = 512ull << 20;
     };
     std::unique_ptr<Stream> out;
@@ -1382,8 +1381,7 @@ struct FileBuilder {
             return fail(FLS_ERR_IO, "write to %s: %s", st->tmp.c_str(), strerror(e));
         }
         Stream *sp = st.get();
-        const char *nt = getenv("FLS_WRITER_STREAM_THREADS");
-        const int nthreads = std::max(1, std::min(16, nt ? atoi(nt) : 1));
+        const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(16, knob_value("FLS_WRITER_STREAM_THREADS")));
         for (int t = 0; t < nthreads; ++t) st->th.emplace_back([sp] {
             static const uint8_t zeros[16] = {};
             std::vector<uint8_t> tmp;
@@ -1454,7 +1452,7 @@ struct FileBuilder {
     }
     // stop the thread after the queue drains; the first write error (0: none)
     int drain_stream() {
-        if (!out || out->th.empty()) return out ? out->err : 0;
+        if (!out || out->th.empty()) return out ? out->err.load() : 0;
         {
             std::lock_guard<std::mutex> lk(out->mu);
             out->stop = true;
@@ -1462,7 +1460,7 @@ struct FileBuilder {
         out->cv.notify_all();
         for (auto &t : out->th) t.join();
         out->th.clear();
-        return out->err;
+        return out->err.load();
     }
     void abandon_stream() {
         if (!out) return;
@@ -2025,8 +2023,7 @@ struct GpuEncoder {
     // DICT chunks on the GPU (FLS_WRITER_DICT_GPU=0: DICT estimates and DICT
     // chunks on the host, the round-3 path)
     static bool dict_gpu() {
-        const char *e = getenv("FLS_WRITER_DICT_GPU");
-        return !(e && atoi(e) == 0);
+        return knob_value("FLS_WRITER_DICT_GPU") != 0;
     }
     static bool dict_job(uint8_t enc) { return (enc == ENC_DICT || enc == ENC_AUTO) && dict_gpu(); }
     // ALP chunks of FLOAT / DOUBLE columns on the GPU only with
@@ -2035,8 +2032,7 @@ struct GpuEncoder {
     // profiles/r5/copy_r5o_lineitem_dbl_10.txt; r4: ordered -10 %), and the
     // byte-identical GPU kernel stays as the opt-in
     static bool alp_gpu() {
-        const char *e = getenv("FLS_WRITER_ALP_GPU");
-        return e && atoi(e) != 0;
+        return knob_value("FLS_WRITER_ALP_GPU") != 0;
     }
     // the encoding a job asks the kernels for: FLOAT / DOUBLE columns are ALP
     // (ENC_AUTO included, as encode_int_chunk does)
@@ -2510,8 +2506,7 @@ int add_rowgroups_impl(fls_writer *w, uint32_t nrg, const RgArgs *a) {
     for (size_t c : gcols) on_gpu[c] = 1;
     w->pool.resize(w->threads);
     // FSST chunks compressed on the GPU (FLS_WRITER_FSST_GPU=0: on the host)
-    const char *fg = getenv("FLS_WRITER_FSST_GPU");
-    FsstGpu *fsst_gpu = w->fsst_gpu.dev >= 0 && !(fg && atoi(fg) == 0) ? &w->fsst_gpu : nullptr;
+    FsstGpu *fsst_gpu = w->fsst_gpu.dev >= 0 && knob_value("FLS_WRITER_FSST_GPU") != 0 ? &w->fsst_gpu : nullptr;
 
     using Pending = PendingRg;
     std::vector<Pending> seg;
@@ -2745,9 +2740,21 @@ int finish_writer(fls_writer *w, uint8_t **img, uint64_t *len, const char *path)
     }
     const double tf = g_prof.on ? WriterProfile::now() : 0;
     if (w->fb.out && !path) return fail(FLS_ERR_STATE, "fls_writer_finish_image: the writer streams to a file");
-    const int rc = w->fb.out ? w->fb.finish_stream(path)
+    const bool streaming = w->fb.out != nullptr;
+    const int rc = streaming ? w->fb.finish_stream(path)
                    : path    ? w->fb.write_file(path, w->threads)
                              : w->fb.finish(img, len, w->threads);
+    if (rc && streaming) {
+        // row groups handed to the stream gave their chunk bytes away (flen
+        // set, chunks empty): a later finish would write blank chunks under a
+        // valid footer, so this writer makes no file any more
+        bool handed = false;
+        for (const auto &r : w->fb.rgs) handed = handed || !r.flen.empty();
+        if (handed) {
+            w->broken = rc;
+            w->broken_msg = fls_last_error();
+        }
+    }
     if (g_prof.on) {
         g_prof.finish += WriterProfile::now() - tf;
         g_prof.print();

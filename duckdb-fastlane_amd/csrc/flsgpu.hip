@@ -30,6 +30,7 @@
 
 #include "../../include/flsgpu.h"
 #include "fls_common.hpp"
+#include "fls_config.hpp"
 #include "fls_decode.hpp"
 #include "fls_filter.hpp"
 #include "fls_format.hpp"
@@ -246,8 +247,7 @@ class CopyPool {
         std::lock_guard<std::mutex> lk(mu_);
         if (started_) return;
         started_ = true;
-        int n = 4;
-        if (const char *e = getenv("FLS_COPY_THREADS")) n = std::max(0, std::min(64, atoi(e)));
+        const int n = (int)std::max<int64_t>(0, std::min<int64_t>(64, knob_value("FLS_COPY_THREADS")));
         for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
     }
     void run() {
@@ -516,8 +516,7 @@ struct ConnRes {
     std::vector<std::unique_ptr<ScanDev>> idle;
     CopyPool copy;
     static size_t idle_cap_bytes() {
-        const char *e = getenv("FLS_IDLE_PINNED_MB");
-        return (size_t)(e ? std::max(0L, atol(e)) : 1024L) << 20;
+        return (size_t)std::max<int64_t>(0, knob_value("FLS_IDLE_PINNED_MB")) << 20;
     }
     // free idle pipelines until the pinned bytes they hold on GPU dev (every
     // GPU: dev < 0) are at most keep (caller holds mu)
@@ -636,6 +635,7 @@ struct Resident {
     std::vector<PinBuf<uint8_t>> h_heap;   // per FSST column: host copy string_t points into
     std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
     std::vector<DevBuf<uint8_t>> d_out;    // per column, rows of [rg0, rg1)
+    double placement_q = 0;                // rating of d_out's placement (choose_placement; 0: not rated)
     DevBuf<DevChunk> d_chunks;
     std::vector<DevChunk> h_chunks;
     std::vector<uint8_t> mask;         // column mask h_chunks was built for
@@ -720,8 +720,7 @@ ImageRegistry &image_registry() {
 }
 // FLS_SCAN_RESIDENT_MB: the image budget per GPU over every cached file (0 = off)
 uint64_t resident_budget() {
-    const char *e = getenv("FLS_SCAN_RESIDENT_MB");
-    return (uint64_t)(e ? std::max(0L, atol(e)) : 65536L) << 20;
+    return (uint64_t)std::max<int64_t>(0, knob_value("FLS_SCAN_RESIDENT_MB")) << 20;
 }
 namespace {
 uint64_t release_idle_images(int dev) {
@@ -1085,6 +1084,15 @@ int fsst_config_check(int64_t policy) {
             return fail(FLS_ERR_CONFIG, "FLS_FSST_VARIANT=%s is not a variant number", fv);
         variant = (int)v;
     }
+    if (const char *fx = getenv("FLS_FUSED_X")) {  // the fused kernel's FSST-part bits (experiments)
+        char *end = nullptr;
+        const long x = strtol(fx, &end, 10);
+        if (end == fx || *end != 0 || x < 0 || x > 0x7FFFFFFF || !fused_x_built((int)x))
+            return fail(FLS_ERR_CONFIG,
+                        "FLS_FUSED_X=%s is not in this build: the product library holds the default fused kernel "
+                        "only; experiments need FLS_LIB=libflsgpu_lab.so (make lab) -- unset FLS_FUSED_X",
+                        fx);
+    }
     const int bpl = (policy & POLICY_FSST16) ? 16 : 8;
     if (!fsst_variant_built(variant, true, bpl) || !fsst_variant_built(variant, false, bpl))
         return fail(FLS_ERR_CONFIG,
@@ -1111,6 +1119,7 @@ struct FusedCfg {
     int mode = 1;
     uint32_t min_vecs_per_cu = 0;
     bool per16_set = false;  // FLS_FUSED_FSST16 given (else by launch size, launch_all)
+    bool variant = false;    // a non-default FLS_FSST_VARIANT: no fused launch
     FusedLaunch how;
 };
 FusedCfg fused_cfg() {
@@ -1127,6 +1136,11 @@ FusedCfg fused_cfg() {
     if (const char *e = getenv("FLS_FUSED_HALVING")) f.how.halving = atoi(e) != 0;
     if (const char *e = getenv("FLS_FUSED_X")) f.how.x = atoi(e);
     if (const char *e = getenv("FLS_FUSED_MIN_VECS_PER_CU")) f.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
+    // an FSST kernel variant A/B (FLS_FSST_VARIANT, experiment library) runs
+    // the standalone FSST kernels: the fused kernel holds only the default's
+    // FSST part, so fusing would measure the default instead
+    if (const char *e = getenv("FLS_FSST_VARIANT"))
+        if (atoi(e) != kFsstDefault) f.variant = true;
     return f;
 }
 
@@ -1241,7 +1255,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
                 g1 = g;
                 ++ng;
             }
-        if (fz.mode > 0 && ((ng == 1 && nmain > 0) || fz.mode == 2) && ng <= 1 && g1 < 2 && !balanced && !sp &&
+        if (fz.mode > 0 && !fz.variant && ((ng == 1 && nmain > 0) || fz.mode == 2) && ng <= 1 && g1 < 2 && !balanced && !sp &&
             !(policy & POLICY_STATIC) &&
             fsst_vecs >= (uint64_t)fz.min_vecs_per_cu * (uint64_t)cus) {
             const int g = std::max(0, g1);  // (no FSST chunks: the main decode alone, in the fused kernel)
@@ -1509,12 +1523,9 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         s.devs.clear();
         for (uint32_t g = 0; g < G; ++g) s.devs.push_back(t->res->take(devs[g]));
     }
-    const char *b = getenv("FLS_SCAN_BATCH");
-    s.batch = b ? (uint32_t)std::max(1, atoi(b)) : 8u;
-    const char *mb = getenv("FLS_SCAN_HOST_BATCHES");
-    s.max_batches = mb ? (uint32_t)std::max(2, atoi(mb)) : 64u;
-    const char *ns = getenv("FLS_SCAN_SLOTS");
-    s.nslots = ns ? std::max(1, std::min(ScanDev::kMaxSlots, atoi(ns))) : 2;
+    s.batch = (uint32_t)std::max<int64_t>(1, knob_value("FLS_SCAN_BATCH"));
+    s.max_batches = (uint32_t)std::max<int64_t>(2, knob_value("FLS_SCAN_HOST_BATCHES"));
+    s.nslots = (int)std::max<int64_t>(1, std::min<int64_t>(ScanDev::kMaxSlots, knob_value("FLS_SCAN_SLOTS")));
     for (uint32_t g = 0; g < G; ++g) {
         ScanDev &d = *s.devs[g];
         HIP_TRY(hipSetDevice(d.dev));
@@ -1824,8 +1835,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     // and the lengths (15 fewer bytes per lineitem row) measured 7.81e8 rows/s
     // against 6.78e8 (profiles/r4/e2e_arms_strlen_r4t.txt).
     hb.strlen_w.assign(ncols, 0);
-    const char *sle = getenv("FLS_SCAN_STRLEN");
-    const bool strlen_on = !(sle && atoi(sle) == 0);
+    const bool strlen_on = knob_value("FLS_SCAN_STRLEN") != 0;
     for (uint32_t c = 0; strlen_on && s.narrow && s.terms.empty() && c < ncols; ++c) {
         if (!col_selected(s.mask, c) || !type_is_string(t->meta.cols[c].type) || hb.ob[c] != 16) continue;
         bool ok = true;
@@ -2336,6 +2346,25 @@ const char *fls_last_error(void) { return last_error().c_str(); }
 
 const char *fls_version(void) { return "fastlanes-mi355x 0.1.0 (gfx950)"; }
 
+int fls_config_default(const char *name, int64_t *value) {
+    const Knob *k = find_knob(name);
+    if (!k || !value) return fail(FLS_ERR_ARG, "fls_config_default: '%s' is not a knob", name ? name : "(null)");
+    *value = k->def;
+    return 0;
+}
+
+int fls_config_value(const char *name, int64_t *value) {
+    if (!find_knob(name) || !value) return fail(FLS_ERR_ARG, "fls_config_value: '%s' is not a knob", name ? name : "(null)");
+    *value = knob_value(name);
+    return 0;
+}
+
+int fls_config_count(void) { return (int)(sizeof(kKnobs) / sizeof(kKnobs[0])); }
+
+const char *fls_config_name(int i) {
+    return i >= 0 && i < fls_config_count() ? kKnobs[i].name : nullptr;
+}
+
 int fls_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -2421,7 +2450,7 @@ struct FileCache {
     std::mutex mu;
     std::vector<std::pair<FileKey, std::shared_ptr<MappedFile>>> lru;  // most recent last
     static size_t capacity() {
-        static const size_t cap = getenv("FLS_OPEN_CACHE") ? (size_t)std::max(0, atoi(getenv("FLS_OPEN_CACHE"))) : 16;
+        static const size_t cap = (size_t)std::max<int64_t>(0, knob_value("FLS_OPEN_CACHE"));
         return cap;
     }
     std::shared_ptr<MappedFile> find(const FileKey &k) {
@@ -2663,6 +2692,99 @@ int fls_scan_release(fls_table *t, uint32_t rowgroup) {
 
 namespace {
 
+// ---- HBM placement of the resident output columns --------------
+// The decode's write stream runs at a speed set by where the driver placed
+// the output buffers (the same decode at the same virtual addresses: 2.63-3.13
+// ms on lineitem_full SF12.5 from one allocation to the next,
+// profiles/r6/placement_*.txt).  A candidate set of output columns is rated by
+// probe_placement: the decode's chunk-order write stream against a linear fill
+// of the same buffers (the fill runs at the same speed on every placement, so
+// the ratio q rates the placement on this box).  Up to FLS_PLACEMENT_TRIES
+// sets (default 4) are tried, the best kept, the search ending early once
+// q >= FLS_PLACEMENT_GOOD / 1000 (default 930).
+int placement_tries() { return (int)std::max<int64_t>(1, knob_value("FLS_PLACEMENT_TRIES")); }
+
+struct PlacementRating {
+    float chunk_ms = 0, fill_ms = 0;
+    double q = 0;
+};
+
+int rate_outputs(const fls_table *t, const Resident &r, const std::vector<DevBuf<uint8_t>> &outs,
+                 PlacementRating &pr) {
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    std::vector<ProbeRegion> reg;
+    for (uint32_t c = 0; c < ncols; ++c)
+        for (uint32_t g = r.rg0; g < r.rg1; ++g) {
+            const uint64_t ob = out_bytes_of(t, c);
+            const uint64_t bytes = (t->meta.rgs[g].nrows * ob) & ~1023ull;
+            if (bytes) reg.push_back({outs[c].p + (t->meta.rgs[g].first_row - r.first_row) * ob, bytes});
+        }
+    // the decode's queue order: largest output first
+    std::stable_sort(reg.begin(), reg.end(), [](const ProbeRegion &a, const ProbeRegion &b) { return a.bytes > b.bytes; });
+    DevBuf<ProbeRegion> d;
+    HIP_TRY(d.alloc(r.dev, reg.size()));
+    HIP_TRY(hipMemcpy(d.p, reg.data(), reg.size() * sizeof(ProbeRegion), hipMemcpyHostToDevice));
+    std::vector<uint8_t *> bufs(ncols);
+    std::vector<uint64_t> sizes(ncols);
+    for (uint32_t c = 0; c < ncols; ++c) {
+        bufs[c] = outs[c].p;
+        sizes[c] = (r.rows * out_bytes_of(t, c)) & ~4095ull;
+    }
+    HIP_TRY(probe_placement(d.p, (uint32_t)reg.size(), bufs.data(), sizes.data(), ncols, 2, r.stream, &pr.chunk_ms,
+                            &pr.fill_ms));
+    pr.q = pr.chunk_ms > 0 ? pr.fill_ms / pr.chunk_ms : 0;
+    return 0;
+}
+
+int choose_placement(const fls_table *t, Resident &r) {
+    const int tries = placement_tries();
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    uint64_t set_bytes = 0;
+    for (uint32_t c = 0; c < ncols; ++c) set_bytes += r.rows * out_bytes_of(t, c);
+    if (tries <= 1 || set_bytes < (256ull << 20)) return 0;  // small outputs: nothing to gain
+    const double good = knob_value("FLS_PLACEMENT_GOOD") / 1000.0;  // per mille
+    const bool dbg = getenv("FLS_DEBUG") != nullptr;
+    PlacementRating best;
+    if (const int rc = rate_outputs(t, r, r.d_out, best)) return rc;
+    if (dbg)
+        fprintf(stderr, "DEBUG: placement dev %d set 0: chunk order %.3f ms, fill %.3f ms, q %.3f\n", r.dev,
+                best.chunk_ms, best.fill_ms, best.q);
+    int kept = 0;
+    for (int k = 1; k < tries && best.q < good; ++k) {
+        size_t fr = 0, tot = 0;
+        HIP_TRY(hipMemGetInfo(&fr, &tot));
+        if (fr < set_bytes + set_bytes / 8 + (1ull << 30)) break;  // no room for a second set
+        std::vector<DevBuf<uint8_t>> cand(ncols);
+        bool ok = true;
+        for (uint32_t c = 0; c < ncols && ok; ++c) {
+            // plain hipMalloc: a speculative set must not evict cached images
+            const size_t n = std::max<size_t>(1, r.rows * out_bytes_of(t, c));
+            if (hipMalloc((void **)&cand[c].p, n) != hipSuccess) {
+                (void)hipGetLastError();
+                cand[c].p = nullptr;
+                ok = false;
+                break;
+            }
+            cand[c].n = n;
+            cand[c].dev = r.dev;
+        }
+        if (!ok) break;
+        PlacementRating pr;
+        if (const int rc = rate_outputs(t, r, cand, pr)) return rc;
+        if (dbg)
+            fprintf(stderr, "DEBUG: placement dev %d set %d: chunk order %.3f ms, fill %.3f ms, q %.3f\n", r.dev, k,
+                    pr.chunk_ms, pr.fill_ms, pr.q);
+        if (pr.q > best.q) {
+            std::swap(r.d_out, cand);  // the previous set is freed with cand
+            best = pr;
+            kept = k;
+        }
+    }
+    r.placement_q = best.q;
+    if (dbg) fprintf(stderr, "DEBUG: placement dev %d kept set %d (q %.3f)\n", r.dev, kept, best.q);
+    return 0;
+}
+
 // Upload one GPU's part: row groups [rg0, rg1) verbatim, their string_t
 // tables, HBM output columns and FSST heaps.
 int upload_part(fls_table *t, Resident &r) {
@@ -2683,6 +2805,7 @@ int upload_part(fls_table *t, Resident &r) {
     r.rows = t->meta.rgs[r.rg1 - 1].first_row + t->meta.rgs[r.rg1 - 1].nrows - r.first_row;
     r.d_out.resize(ncols);
     for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(r.d_out[c].alloc(r.dev, r.rows * out_bytes_of(t, c)));
+    if (const int prc = choose_placement(t, r)) return prc;
     // FSST heaps: chunk heaps back to back per column, host copy for string_t
     r.heap_off.assign((size_t)(r.rg1 - r.rg0) * ncols, 0);
     r.d_heap.resize(ncols);
@@ -2703,6 +2826,13 @@ int upload_part(fls_table *t, Resident &r) {
     }
     r.h_chunks.clear();
     r.mask.clear();
+    if (getenv("FLS_DEBUG")) {  // buffer placement (decode speed by buffer address)
+        fprintf(stderr, "DEBUG: part dev %d rg [%u, %u) image %p %llu B\n", r.dev, r.rg0, r.rg1, (void *)r.img.p,
+                (unsigned long long)(hi - lo));
+        for (uint32_t c = 0; c < ncols; ++c)
+            fprintf(stderr, "DEBUG:   col %u out %p %llu B heap %p\n", c, (void *)r.d_out[c].p,
+                    (unsigned long long)(r.rows * out_bytes_of(t, c)), (void *)r.d_heap[c].p);
+    }
     return 0;
 }
 

@@ -12,6 +12,14 @@
 namespace duckdb {
 namespace ext_fastlane {
 
+// A deployment knob's value in effect (the environment's, else the default
+// from the engine's one table, fls_config_value in flsgpu.h).
+inline int64_t KnobValue(const char *name) {
+    int64_t v = 0;
+    if (fls_config_value(name, &v) != 0) std::abort();  // not a knob: a programming error
+    return v;
+}
+
 inline std::vector<int> GpuDevices() {
     std::vector<int> d;
     if (const char *e = std::getenv("FLS_GPU_DEVICES")) {

@@ -461,8 +461,7 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     // integer columns are chosen (ENC_AUTO) and encoded on the first GPU of
     // the extension's set when one is visible -- the file is byte-identical
     // to the CPU writer's (FLS_COPY_GPU=0 keeps the CPU)
-    const char *cg = std::getenv("FLS_COPY_GPU");
-    if ((!cg || std::atoi(cg) != 0) && fls_device_count() > 0) fls_writer_set_device(s.writer, GpuDevices()[0]);
+    if (KnobValue("FLS_COPY_GPU") != 0 && fls_device_count() > 0) fls_writer_set_device(s.writer, GpuDevices()[0]);
     for (size_t c = 0; c < types.size(); ++c) {
         const uint8_t ft = TypeMapping::DuckDBToFastLanes(types[c]);
         if (!ft || fls_writer_add_column(s.writer, names[c].c_str(), ft, types[c].Width(), types[c].Scale(),
@@ -475,11 +474,9 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     // the file is written while the COPY runs (row groups stream to a
     // temporary file renamed over file_path at finalize); FLS_COPY_STREAM=0
     // writes it all at finalize instead
-    const char *cp = std::getenv("FLS_COPY_PIPELINE");
-    s.pipelined = !(cp && std::atoi(cp) == 0);
+    s.pipelined = KnobValue("FLS_COPY_PIPELINE") != 0;
     if (s.pipelined) fls_writer_set_pipelined(s.writer, 1);
-    const char *cs = std::getenv("FLS_COPY_STREAM");
-    if ((!cs || std::atoi(cs) != 0) && fls_writer_set_output(s.writer, file_path.c_str()) != 0) {
+    if (KnobValue("FLS_COPY_STREAM") != 0 && fls_writer_set_output(s.writer, file_path.c_str()) != 0) {
         s.error = std::string("FastLanes writer: ") + fls_last_error();
         fls_writer_free(s.writer);
         s.writer = nullptr;
@@ -493,9 +490,9 @@ bool FastLanesFacade::createFile(const std::string &file_path, const std::vector
     s.own->accounted = 0;
     s.staged = 0;
     s.staged_peak = 0;
-    if (const char *b = std::getenv("FLS_COPY_BATCH")) s.batch_rgs = (idx_t)std::max(1, std::atoi(b));
-    if (const char *b = std::getenv("FLS_COPY_STAGED_MB")) s.staged_budget = (uint64_t)std::max(1, std::atoi(b)) << 20;
-    if (const char *b = std::getenv("FLS_COPY_SINK_THREADS")) s.cpool_threads = std::max(0, std::atoi(b));
+    s.batch_rgs = (idx_t)std::max<int64_t>(1, KnobValue("FLS_COPY_BATCH"));
+    s.staged_budget = (uint64_t)std::max<int64_t>(1, KnobValue("FLS_COPY_STAGED_MB")) << 20;
+    s.cpool_threads = (int)std::max<int64_t>(0, KnobValue("FLS_COPY_SINK_THREADS"));
     return true;
 }
 

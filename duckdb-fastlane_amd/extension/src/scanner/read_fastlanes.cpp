@@ -438,7 +438,7 @@ bool NextRowGroup(const ReadBindData &bind, ReadGlobalState &g, ReadLocalState &
                 // DICT string columns as codes + dictionary (DuckDB dictionary
                 // vectors: 1-2 bytes per row over PCIe instead of a 16-byte
                 // string_t); FLS_READ_DICT=0 delivers string_t (A/B knob)
-                static const bool codes = !(std::getenv("FLS_READ_DICT") && std::atoi(std::getenv("FLS_READ_DICT")) == 0);
+                static const bool codes = KnobValue("FLS_READ_DICT") != 0;
                 // integer columns narrowed to their row groups' ranges (value -
                 // base in 1-4 bytes, widened in EmitColumn), see ReadInitGlobal;
                 // narrowed scans deliver FSST columns as lengths, their string_t

@@ -134,6 +134,18 @@ typedef struct fls_decode_stats {
 
 const char *fls_last_error(void);
 const char *fls_version(void);
+/* Deployment knobs: the environment variables the library and the extension
+ * read (FLS_IDLE_PINNED_MB, FLS_SCAN_RESIDENT_MB, FLS_COPY_BATCH, ...; the
+ * list with each meaning is in INTEGRATION.md), defaults kept in one table
+ * (csrc/fls_config.hpp).  fls_config_default: the compiled default;
+ * fls_config_value: the value in effect (the environment's, else the
+ * default); FLS_ERR_ARG for a name that is not a knob.  fls_config_count /
+ * fls_config_name enumerate the knobs (NULL past the end).  Not in the
+ * reference, which reads no environment. */
+int fls_config_default(const char *name, int64_t *value);
+int fls_config_value(const char *name, int64_t *value);
+int fls_config_count(void);
+const char *fls_config_name(int i);
 /* Number of HIP devices visible (0 when there is no GPU). */
 int fls_device_count(void);
 /* Raw device buffers and copies on GPU `device`, for callers that hold no HIP
@@ -151,7 +163,7 @@ void fls_disconnect(fls_connection *conn);
  * host batches kept for the next scan) down to keep_bytes of pinned memory
  * per GPU (0: all of them); idle_bytes (may be NULL) receives what stays.
  * Idle pinned memory is also capped per GPU when a scan ends
- * (FLS_IDLE_PINNED_MB, default 512).  Not in the reference: a long-lived
+ * (FLS_IDLE_PINNED_MB, default 1024).  Not in the reference: a long-lived
  * host (DuckDB) uses it to hand page-locked memory back. */
 int fls_connection_trim(fls_connection *conn, uint64_t keep_bytes, uint64_t *idle_bytes);
 /* HBM-resident compressed images (the scan pipeline keeps a scanned file's
@@ -218,9 +230,10 @@ int fls_scan_dict_codes(fls_table *t, int enable);
  * narrow_base); the consumer adds the base back while filling its vectors.
  * Off by default. */
 int fls_scan_narrow(fls_table *t, int enable);
-/* With fls_scan_narrow and FLS_SCAN_STRLEN=1 in the environment (opt-in:
- * measured neutral where the consumer, not the link, is the bound), an
- * unfiltered scan also delivers FSST string columns
+/* With fls_scan_narrow (FLS_SCAN_STRLEN, default 1; 0 ships string_t
+ * records instead: the lengths measured 7.81e8 against 6.78e8 rows/s on the
+ * link-bound 16-thread read_fastlanes, profiles/r4/e2e_arms_strlen_r4t.txt),
+ * an unfiltered scan also delivers FSST string columns
  * as their lengths (1, 2 or 4 bytes per row) plus the string heap, and the
  * string_t records are rebuilt on the host; fls_rowgroup shows them as
  * ordinary string_t columns.  fls_scan_acquire builds them unless

@@ -501,6 +501,28 @@ def test_gpu_fsst_unknown_variant_refused(fl, gpu, monkeypatch, variant):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("x", ["3", "5", "-1", "junk"])
+def test_gpu_fused_x_refused_with_config_error(fl, gpu, monkeypatch, x):
+    """a leftover FLS_FUSED_X (the fused kernel's experiment bits)
+    fails a product-library decode with FLS_ERR_CONFIG, not a HIP error."""
+    n = 70000
+    rng = np.random.default_rng(4)
+    img = fl.write_image([("k", fl.INT64, np.arange(n, dtype=np.int64), fl.ENC_DELTA),
+                          ("s", fl.VARCHAR, fsst_text(n, rng), fl.ENC_FSST)])
+    t = fl.Connection().read_image(img)
+    t.device_upload()
+    monkeypatch.setenv("FLS_FUSED_X", x)
+    with pytest.raises(fl.FlsError, match="FLS_FUSED_X") as ei:
+        t.device_decode()
+        t.device_sync()
+    assert ei.value.code == -7
+    monkeypatch.delenv("FLS_FUSED_X")
+    t.device_decode()
+    t.device_sync()
+    assert np.array_equal(t.device_copy_out(0).view(np.int64), np.arange(n, dtype=np.int64))
+
+
+@pytest.mark.gpu
 def test_gpu_stale_fsst_variant_does_not_fail_integer_tables(fl, gpu, monkeypatch):
     """the FSST variant check runs only for launches with FSST
     work, so a stale FLS_FSST_VARIANT cannot fail a table without strings

@@ -364,6 +364,49 @@ def test_streamed_output_abandoned_leaves_nothing(fl, tmp_path):
     assert sorted(p.name for p in tmp_path.iterdir()) == ["a.fls"] and path.read_bytes() == b"keep me"
 
 
+def test_streamed_output_failed_finish_breaks_the_writer(fl, tmp_path):
+    # row groups handed to the stream gave their chunk bytes away;
+    # after a failed finish (wrong path) a retry must not build a file or an
+    # image from the emptied chunks under a valid footer
+    path = tmp_path / "r.fls"
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_set_rowgroup_size(w, 1024) == 0
+        assert fl.lib.fls_writer_add_column(w, b"x", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_set_output(w, str(path).encode()) == 0
+        x = np.arange(1024, dtype=np.int32)
+        data = (ctypes.c_void_p * 1)(x.ctypes.data)
+        for _ in range(3):
+            assert fl.lib.fls_writer_add_rowgroup(w, 1024, data, None) == 0
+        assert fl.lib.fls_writer_finish_file(w, str(tmp_path / "other.fls").encode()) < 0
+        assert fl.lib.fls_writer_finish_file(w, str(path).encode()) < 0
+        assert "failed earlier" in fl.last_error()
+        p, ln = ctypes.c_void_p(), ctypes.c_uint64()
+        assert fl.lib.fls_writer_finish_image(w, ctypes.byref(p), ctypes.byref(ln)) < 0
+    finally:
+        fl.lib.fls_writer_free(w)
+    assert list(tmp_path.iterdir()) == []
+
+
+def test_streamed_output_wrong_path_before_any_row_group_can_retry(fl, tmp_path):
+    # nothing was handed to the stream yet: the data is intact, and a finish
+    # with a path (the stream abandoned) writes the whole file
+    path = tmp_path / "ok.fls"
+    w = fl.lib.fls_writer_new(0)
+    try:
+        assert fl.lib.fls_writer_add_column(w, b"x", fl.INT32, 0, 0, fl.ENC_FFOR) == 0
+        assert fl.lib.fls_writer_set_output(w, str(path).encode()) == 0
+        assert fl.lib.fls_writer_finish_file(w, str(tmp_path / "other.fls").encode()) < 0
+        x = np.arange(100, dtype=np.int32)
+        data = (ctypes.c_void_p * 1)(x.ctypes.data)
+        assert fl.lib.fls_writer_add_rowgroup(w, 100, data, None) == 0
+        assert fl.lib.fls_writer_finish_file(w, str(path).encode()) == 0
+    finally:
+        fl.lib.fls_writer_free(w)
+    ref = fl.write_image([("x", fl.INT32, np.arange(100, dtype=np.int32), fl.ENC_FFOR)])
+    assert path.read_bytes() == bytes(ref.view())
+
+
 def test_streamed_output_refuses_unwritable_dir_and_late_set(fl, tmp_path):
     w = fl.lib.fls_writer_new(0)
     try:
