@@ -30,6 +30,7 @@ inline constexpr Knob kKnobs[] = {
     {"FLS_SCAN_STRLEN", 1},           // narrowed scans ship FSST columns as lengths + heap
     {"FLS_OPEN_CACHE", 16},           // opened files kept mapped with their metadata (0: off)
     {"FLS_COPY_THREADS", 4},          // staging copy threads per connection
+    {"FLS_PIN_ARENA_MB", 0},          // registered pinned arena cap (fls_pinned.hpp; 0: hipHostMalloc only)
     {"FLS_PLACEMENT_TRIES", 4},       // output-buffer placements tried per resident part
     {"FLS_PLACEMENT_GOOD", 930},      // placement rating (per mille) that ends the search
     // writer (fls_writer.cpp)

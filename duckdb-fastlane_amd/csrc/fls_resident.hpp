@@ -35,13 +35,34 @@ class ResidentSet {
     };
     using Evicted = std::vector<std::shared_ptr<Img>>;
 
-    // the image of owner on dev, if any (a use: it becomes the most recent)
-    std::shared_ptr<Img> find(const void *owner, int dev, uint64_t *lo = nullptr, uint64_t *hi = nullptr) {
+    // owner's image on dev that holds the file bytes [lo, hi), if any (a use:
+    // it becomes the most recent).  One file may have several images on one
+    // GPU: one per shard when a connection lists the GPU more than once (the
+    // 8-way split rehearsed on one GPU).
+    std::shared_ptr<Img> find(const void *owner, int dev, uint64_t lo, uint64_t hi) {
+        for (Entry &e : e_)
+            if (e.owner == owner && e.dev == dev && e.lo <= lo && hi <= e.hi) {
+                e.tick = ++tick_;
+                return e.img;
+            }
+        return nullptr;
+    }
+    // any image of owner on dev (a scan's hold in the CPU driver)
+    std::shared_ptr<Img> find_any(const void *owner, int dev) {
         for (Entry &e : e_)
             if (e.owner == owner && e.dev == dev) {
                 e.tick = ++tick_;
-                if (lo) *lo = e.lo;
-                if (hi) *hi = e.hi;
+                return e.img;
+            }
+        return nullptr;
+    }
+    // an image of owner on dev overlapping [lo, hi) that a scan holds (made
+    // for another split of the table: the caller decodes what it covers and
+    // streams the rest), or none
+    std::shared_ptr<Img> find_held_overlap(const void *owner, int dev, uint64_t lo, uint64_t hi) {
+        for (Entry &e : e_)
+            if (e.owner == owner && e.dev == dev && e.lo < hi && lo < e.hi && !idle(e)) {
+                e.tick = ++tick_;
                 return e.img;
             }
         return nullptr;
@@ -90,10 +111,11 @@ class ResidentSet {
                 e_.erase(e_.begin() + (long)i);
             }
     }
-    // owner's image on dev (replaced: made for another split of the table)
-    void drop_one(const void *owner, int dev, Evicted &out) {
+    // owner's idle images on dev overlapping [lo, hi) (replaced: made for
+    // another split of the table)
+    void drop_overlap(const void *owner, int dev, uint64_t lo, uint64_t hi, Evicted &out) {
         for (size_t i = e_.size(); i-- > 0;)
-            if (e_[i].owner == owner && e_[i].dev == dev) {
+            if (e_[i].owner == owner && e_[i].dev == dev && e_[i].lo < hi && lo < e_[i].hi && idle(e_[i])) {
                 out.push_back(std::move(e_[i].img));
                 e_.erase(e_.begin() + (long)i);
             }

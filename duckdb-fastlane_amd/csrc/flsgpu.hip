@@ -1413,15 +1413,13 @@ std::shared_ptr<DevImage> resident_image(fls_table *t, int dev, uint32_t g, uint
     ImageRegistry &R = image_registry();
     ResidentSet<DevImage>::Evicted ev;  // freed under the lock: the new image may need their memory
     std::lock_guard<std::mutex> lk(R.mu);
-    uint64_t flo = 0, fhi = 0;
-    if (auto p = R.set.find(t->mapped.get(), dev, &flo, &fhi)) {
-        // made for another split of the table: batches outside it stream
-        if (flo <= lo && hi <= fhi) return p;
-        if (p.use_count() > 2) return p;  // another scan decodes from it
-        p.reset();
-        R.set.drop_one(t->mapped.get(), dev, ev);
-        ev.clear();
-    }
+    if (auto p = R.set.find(t->mapped.get(), dev, lo, hi)) return p;
+    // an image made for another split of the table that another scan decodes
+    // from: use it (batches outside it stream); idle ones overlapping this
+    // shard are replaced
+    if (auto p = R.set.find_held_overlap(t->mapped.get(), dev, lo, hi)) return p;
+    R.set.drop_overlap(t->mapped.get(), dev, lo, hi, ev);
+    ev.clear();
     if (!R.set.make_room(dev, need, budget, ev)) return nullptr;
     ev.clear();
     if (hipSetDevice(dev) != hipSuccess) {
@@ -1545,12 +1543,20 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         d.next_p = d.p0;
         d.rg0 = d.p0 < d.p1 ? s.rgs[d.p0] : 0;
         d.rg1 = d.p0 < d.p1 ? s.rgs[d.p1 - 1] + 1 : 0;
-        {   // the image holds this GPU's shard of the table over the connection's GPUs
-            const auto it = std::find(t->devices.begin(), t->devices.end(), d.dev);
-            const bool in = it != t->devices.end();
+        {   // the image holds this GPU's shard of the table over the connection's GPUs;
+            // a GPU the connection lists k times holds k shards: pipeline g
+            // takes the shard of the listing that is its own occurrence
+            uint32_t occ = 0;
+            for (uint32_t h = 0; h < g; ++h) occ += s.devs[h]->dev == d.dev;
+            uint32_t shard = 0, seen = 0;
+            bool in = false;
+            for (uint32_t k = 0; k < (uint32_t)t->devices.size() && !in; ++k)
+                if (t->devices[k] == d.dev && seen++ == occ) {
+                    shard = k;
+                    in = true;
+                }
             ProfTimer pi(PROF_IMAGE);
-            d.dimg = resident_image(t, d.dev, in ? (uint32_t)(it - t->devices.begin()) : 0u,
-                                    in ? (uint32_t)t->devices.size() : 1u);
+            d.dimg = resident_image(t, d.dev, in ? shard : 0u, in ? (uint32_t)t->devices.size() : 1u);
         }
         int rc;
         {

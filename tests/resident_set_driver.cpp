@@ -1,6 +1,9 @@
 // Drives fls::ResidentSet (csrc/fls_resident.hpp, the HBM image budget policy)
 // from a script on stdin, for tests/test_resident_budget.py (CPU only):
 //   get <file> <dev> <bytes> <budget>   find or make room + insert; prints hit|new|none
+//   shard <file> <dev> <lo> <hi> <budget>  the same for file bytes [lo, hi) (one
+//                                        image per shard; idle overlapping ones replaced,
+//                                        a held overlapping one returned: prints held)
 //   hold <file> <dev> / drop <file> <dev>   a scan takes / gives back the image
 //   release <dev>                        release_idle; prints the bytes freed
 //   close <file>                         drop_owner (the file left the open cache)
@@ -39,7 +42,7 @@ int main() {
             uint64_t bytes = 0, budget = 0;
             in >> file >> dev >> bytes >> budget;
             owner = key(file);
-            if (set.find(owner, dev)) {
+            if (set.find(owner, dev, 0, bytes)) {
                 std::cout << "hit\n";
             } else if (set.make_room(dev, bytes, budget, ev)) {
                 set.insert(owner, dev, 0, bytes, bytes, std::make_shared<Img>(file));
@@ -49,9 +52,28 @@ int main() {
             } else {
                 std::cout << "none\n";
             }
+        } else if (op == "shard") {
+            uint64_t lo = 0, hi = 0, budget = 0;
+            in >> file >> dev >> lo >> hi >> budget;
+            owner = key(file);
+            if (set.find(owner, dev, lo, hi)) {
+                std::cout << "hit\n";
+            } else if (set.find_held_overlap(owner, dev, lo, hi)) {
+                std::cout << "held\n";
+            } else {
+                set.drop_overlap(owner, dev, lo, hi, ev);
+                const size_t dropped = ev.size();
+                ev.clear();
+                if (set.make_room(dev, hi - lo, budget, ev)) {
+                    set.insert(owner, dev, lo, hi, hi - lo, std::make_shared<Img>(file));
+                    std::cout << "new replaced " << dropped << "\n";
+                } else {
+                    std::cout << "none\n";
+                }
+            }
         } else if (op == "hold") {
             in >> file >> dev;
-            held[{file, dev}] = set.find(key(file), dev);
+            held[{file, dev}] = set.find_any(key(file), dev);
             std::cout << (held[{file, dev}] ? "held\n" : "absent\n");
         } else if (op == "drop") {
             in >> file >> dev;

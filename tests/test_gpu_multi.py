@@ -89,3 +89,44 @@ def test_lineitem_full_sf100_bit_exact(fl, gpu):
     st = t.device_sync()
     assert st.values == 16 * t.nrows
     assert fl.check_device_table(t, "lineitem_full", 100.0) == [0] * 16
+
+
+def test_eight_way_split_on_one_gpu(fl, gpu, tmp_path):
+    """the 8-way engine split, rehearsed on one GPU
+    (Connection([0] * 8): eight pipelines, eight resident parts, eight shard
+    images, all on GPU 0).  lineitem_full SF1 has 92 row groups: shards of
+    11 / 12, not multiples of the scan batch (8).  Checked: row-group order
+    through scan(), every value of two columns vs the generator, the eight
+    shard images, the device parts' boundaries, and every value of all 16
+    columns of the device-resident decode.  A correctness rehearsal only:
+    one physical GPU measures no scaling."""
+    img = fl.gen_image("lineitem_full", 1.0)
+    path = tmp_path / "l8.fls"
+    img.write(str(path))
+    fl.Connection.release_device_memory()
+    t = fl.Connection([0] * 8).read_fls(str(path))
+    N, n = t.nrowgroups, t.nrows
+    assert N == 92 and n == 6001215
+    names = [s[0] for s in t.schema()]
+    ck, cd = names.index("l_orderkey"), names.index("l_shipdate")
+    got = list(t.scan(cols=[ck, cd]))
+    assert [first // 65536 for first, _ in got] == list(range(N))
+    keys = np.concatenate([cols[ck].view(np.int64) for _, cols in got])
+    days = np.concatenate([cols[cd].view(np.int32) for _, cols in got])
+    assert np.array_equal(keys, fl.gen_values("lineitem_full", ck, 0, n, np.int64))
+    assert np.array_equal(days, fl.gen_values("lineitem_full", cd, 0, n, np.int32))
+    held, images = fl.Connection.resident_info(0)
+    assert images == 8, (held, images)
+    assert 0.9 * path.stat().st_size < held < 1.05 * path.stat().st_size
+    t.device_upload()
+    parts = t.device_parts()
+    bounds = [N * g // 8 for g in range(9)]
+    assert [(p.rg_begin, p.rg_end) for p in parts] == list(zip(bounds[:-1], bounds[1:]))
+    assert sorted({p.rg_end - p.rg_begin for p in parts}) == [11, 12]
+    assert [p.device for p in parts] == [0] * 8 and sum(p.nrows for p in parts) == n
+    t.device_decode()
+    st = t.device_sync()
+    assert st.values == 16 * n
+    assert fl.check_device_table(t, "lineitem_full", 1.0) == [0] * 16
+    t.close()
+    fl.Connection.release_device_memory()

@@ -111,3 +111,30 @@ lru 0
 lru 0
 state 0""")
     assert out == ["new", "new", "held", "2", "-1", "10 1 live 1"]
+
+
+def test_shards_of_one_file_share_a_gpu(driver):
+    """a connection listing one GPU several times (the
+    8-way split rehearsed on one GPU) keeps one image per shard there."""
+    script = "\n".join(f"shard 1 0 {100 * g} {100 * (g + 1)} 10000" for g in range(8)) + "\nstate 0"
+    out = driver(script)
+    assert out == ["new replaced 0"] * 8 + ["800 8 live 8"]
+    # the same shards again: all hits
+    again = driver(script + "\n" + "\n".join(f"shard 1 0 {100 * g} {100 * (g + 1)} 10000" for g in range(8)))
+    assert again[9:] == ["hit"] * 8
+
+
+def test_other_split_replaces_idle_overlapping_shards_only(driver):
+    out = driver("""shard 1 0 0 100 10000
+shard 1 0 100 200 10000
+shard 1 0 200 300 10000
+hold 1 0
+shard 1 0 0 300 10000
+drop 1 0
+shard 1 0 0 300 10000
+state 0""")
+    # a held shard (the first: hold takes any image of the file) overlapping
+    # the new range is used as it is; once released, the whole-file request
+    # replaces all three idle shards with one image
+    assert out == ["new replaced 0", "new replaced 0", "new replaced 0", "held", "held", "ok",
+                   "new replaced 3", "300 1 live 1"]

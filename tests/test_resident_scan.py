@@ -116,8 +116,11 @@ def test_release_returns_the_hbm(ext, fl, gpu, tmpfile):
 
 def test_image_holds_only_this_gpus_shard(ext, fl, gpu, tmpfile, monkeypatch):
     """A GPU's image holds its shard of the table: with the table
-    split over two devices (GPU 0 listed twice), each image is about half
-    the file, and both decode exactly."""
+    split over two devices (GPU 0 listed twice), GPU 0 holds one image per
+    shard (round 6: the registry keys images by shard, so the split rehearsed
+    on one GPU keeps both), together about the file, and both decode
+    exactly; a later unsplit scan replaces the two idle shards with one
+    image."""
     import os
     p = tmpfile("shard.fls")
     fl.gen_image("lineitem", 0.2).write(p)
@@ -132,6 +135,12 @@ def test_image_holds_only_this_gpus_shard(ext, fl, gpu, tmpfile, monkeypatch):
     assert rows == ref[0]
     held, n = _resident(fl)
     size = os.path.getsize(p)
-    assert n == 1 and held < 0.6 * size      # (both parts are GPU 0: one image, its first shard)
+    assert n == 2 and 0.9 * size < held < 1.05 * size   # two half-size shard images on GPU 0
     t.close()
+    t1 = fl.Connection([0]).read_fls(p)
+    rows1 = sum(len(cols[0]) // sch[0][4] for _, cols in t1.scan(cols=[0]))
+    assert rows1 == ref[0]
+    held1, n1 = _resident(fl)
+    assert n1 == 1 and 0.9 * size < held1 < 1.05 * size   # one whole-file image replaced the shards
+    t1.close()
     fl.Connection.release_device_memory()
