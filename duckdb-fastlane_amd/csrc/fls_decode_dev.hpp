@@ -45,12 +45,22 @@ __constant__ float kF10F[kAlpMaxExpF + 1] = {FLS_ALP_F10_F};
 __constant__ float kIF10F[kAlpMaxExpF + 1] = {FLS_ALP_IF10_F};
 // keep unrolled iterations in program order: bounds register pressure to one
 // iteration (the occupancy, not the ILP of one wave, hides latency here)
-// full 16-byte output store (FLS_NT_STORE: non-temporal streaming store)
-__device__ __forceinline__ void st16(FLS_GLOBAL v4u *p, v4u v) {
-#ifdef FLS_NT_STORE
-    __builtin_nontemporal_store(v, p);
+// full 16-byte output store at byte off of the vector's (wave-uniform) output
+// out.  FLS_STORE_CPOL (experiment builds): a buffer store with that cache
+// policy (16 = sc1: the line leaves the XCD's L2 once written, 2 = nt, 17 =
+// sc0 sc1; the write microbenchmark ran 512 KiB-chunk writes with a 1/8 read
+// share 6.8 % faster with sc1 than plain, profiles/r6/membw6_*.txt);
+// FLS_NT_STORE: non-temporal global store.
+__device__ __forceinline__ void st16(ou8 *out, uint32_t off, v4u v) {
+#if defined(FLS_STORE_CPOL)
+    const uint64_t b = (uint64_t)out;
+    void *ub = (void *)((uint64_t)uni((uint32_t)(b >> 32)) << 32 | (uint64_t)uni((uint32_t)b));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, FLS_STORE_CPOL);
+#elif defined(FLS_NT_STORE)
+    __builtin_nontemporal_store(v, reinterpret_cast<ov4 *>(out + off));
 #else
-    *p = v;
+    *reinterpret_cast<ov4 *>(out + off) = v;
 #endif
 }
 // packed-bit load (FLS_NT_LOAD: non-temporal, read-once stream)
@@ -153,7 +163,7 @@ __device__ __forceinline__ void ffor_vec(const lv4 *__restrict__ P, uint32_t W, 
     for (uint32_t j = 0; j < T / 8; ++j) {
         const uint32_t ci = lane + 64 * j;
         const v4u v = add_base<T>(unpack_chunk<T>(P, W, ci), base);
-        if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, v);
+        if (FULL) st16(out, 16 * ci, v);
         else store16<T / 8>(out, 16 * ci, limit, v);
         seq();
     }
@@ -208,7 +218,7 @@ __device__ __forceinline__ void delta64_vec(const lv4 *__restrict__ P, uint32_t 
         const uint64_t v0 = p0 + a0[j], v1 = p1 + a1[j];
         const v4u v = mk4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
         const uint32_t off = 128 * (8 * s + j) + 16 * q;
-        if (FULL) st16(reinterpret_cast<ov4 *>(out + off), v);
+        if (FULL) st16(out, off, v);
         else store16<8>(out, off, limit, v);
     }
 }
@@ -292,7 +302,7 @@ __device__ __forceinline__ void copy_out(const lu8 *__restrict__ V, ou8 *__restr
     for (uint32_t j = 0; j < EB; ++j) {
         const uint32_t ci = lane + 64 * j;
         const v4u x = *reinterpret_cast<const lv4 *>(V + 16 * ci);
-        if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, x);
+        if (FULL) st16(out, 16 * ci, x);
         else store16<EB>(out, 16 * ci, limit, x);
         seq();
     }
@@ -328,7 +338,7 @@ __device__ __forceinline__ void gather_out(TabF tab, ou8 *__restrict__ out, uint
             }
         }
         const v4u v = mk4(w[0], w[1], w[2], w[3]);
-        if (FULL) st16(reinterpret_cast<ov4 *>(out) + oc, v);
+        if (FULL) st16(out, 16 * oc, v);
         else store16<OB == 16 ? 8 : OB>(out, 16 * oc, limit, v);
         seq();
     }
@@ -524,7 +534,7 @@ struct PathAlp {
         for (uint32_t j = 0; j < T / 8; ++j) {
             const uint32_t ci = lane + 64 * j;
             const v4u v = sc.apply(add_base<T>(unpack_chunk<T>(s.P, x.W, ci), x.base));
-            if (FULL) st16(reinterpret_cast<ov4 *>(out) + ci, v);
+            if (FULL) st16(out, 16 * ci, v);
             else store16<T / 8>(out, 16 * ci, limit, v);
             seq();
         }
