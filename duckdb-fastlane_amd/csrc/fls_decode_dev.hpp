@@ -46,22 +46,30 @@ __constant__ float kIF10F[kAlpMaxExpF + 1] = {FLS_ALP_IF10_F};
 // keep unrolled iterations in program order: bounds register pressure to one
 // iteration (the occupancy, not the ILP of one wave, hides latency here)
 // full 16-byte output store at byte off of the vector's (wave-uniform) output
-// out.  FLS_STORE_CPOL (experiment builds): a buffer store with that cache
-// policy (16 = sc1: the line leaves the XCD's L2 once written, 2 = nt, 17 =
-// sc0 sc1; the write microbenchmark ran 512 KiB-chunk writes with a 1/8 read
-// share 6.8 % faster with sc1 than plain, profiles/r6/membw6_*.txt);
-// FLS_NT_STORE: non-temporal global store.
-__device__ __forceinline__ void st16(ou8 *out, uint32_t off, v4u v) {
-#if defined(FLS_STORE_CPOL)
-    const uint64_t b = (uint64_t)out;
-    void *ub = (void *)((uint64_t)uni((uint32_t)(b >> 32)) << 32 | (uint64_t)uni((uint32_t)b));
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7FFFFFFF, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, FLS_STORE_CPOL);
-#elif defined(FLS_NT_STORE)
-    __builtin_nontemporal_store(v, reinterpret_cast<ov4 *>(out + off));
+// out.  CPOL != 0: a buffer store with that cache policy (2 = nt, 16 = sc1,
+// 17 = sc0 sc1).  Chosen per path by build A/B over re-drawn placements
+// (scripts/ab_builds.py, profiles/r6/ab_builds_*): nt stores made DELTA64
+// (c3, 1e9 INT64 keys) 5.0-7.2 % faster and sc1 4.4 %, while nt cost the
+// FFOR / DICT paths 1.8-2.9 % (c4, lineitem SF10) and nothing at SF100; so
+// only the DELTA64 path stores nt.  FLS_STORE_CPOL (experiment builds, make
+// cpol) overrides every path's policy.
+#ifdef FLS_STORE_CPOL
+constexpr int kCpolAll = FLS_STORE_CPOL;
 #else
-    *reinterpret_cast<ov4 *>(out + off) = v;
+constexpr int kCpolAll = -1;
 #endif
+constexpr int kCpolDelta64 = 2;  // nt
+template <int CPOL = 0>
+__device__ __forceinline__ void st16(ou8 *out, uint32_t off, v4u v) {
+    constexpr int cp = kCpolAll >= 0 ? kCpolAll : CPOL;
+    if constexpr (cp != 0) {
+        const uint64_t b = (uint64_t)out;
+        void *ub = (void *)((uint64_t)uni((uint32_t)(b >> 32)) << 32 | (uint64_t)uni((uint32_t)b));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, cp);
+    } else {
+        *reinterpret_cast<ov4 *>(out + off) = v;
+    }
 }
 // packed-bit load (FLS_NT_LOAD: non-temporal, read-once stream)
 __device__ __forceinline__ v4u ld16(const FLS_GLOBAL v4u *p) {
@@ -218,7 +226,7 @@ __device__ __forceinline__ void delta64_vec(const lv4 *__restrict__ P, uint32_t 
         const uint64_t v0 = p0 + a0[j], v1 = p1 + a1[j];
         const v4u v = mk4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
         const uint32_t off = 128 * (8 * s + j) + 16 * q;
-        if (FULL) st16(out, off, v);
+        if (FULL) st16<kCpolDelta64>(out, off, v);
         else store16<8>(out, off, limit, v);
     }
 }
