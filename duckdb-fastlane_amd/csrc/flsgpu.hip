@@ -2706,8 +2706,9 @@ namespace {
 // probe_placement: the decode's chunk-order write stream against a linear fill
 // of the same buffers (the fill runs at the same speed on every placement, so
 // the ratio q rates the placement on this box).  Up to FLS_PLACEMENT_TRIES
-// sets (default 4) are tried, the best kept, the search ending early once
-// q >= FLS_PLACEMENT_GOOD / 1000 (default 930).
+// sets (default 8) are tried, the best kept, the search ending early once
+// q >= FLS_PLACEMENT_GOOD / 1000 (default 990: at 0.93-0.97 some placements
+// still decoded slowly, profiles/r6/placement_q_sf25_r6q.txt).
 int placement_tries() { return (int)std::max<int64_t>(1, knob_value("FLS_PLACEMENT_TRIES")); }
 
 struct PlacementRating {
