@@ -51,14 +51,16 @@ __constant__ float kIF10F[kAlpMaxExpF + 1] = {FLS_ALP_IF10_F};
 // (scripts/ab_builds.py, profiles/r6/ab_builds_*): nt stores made DELTA64
 // (c3, 1e9 INT64 keys) 5.0-7.2 % faster and sc1 4.4 %, while nt cost the
 // FFOR / DICT paths 1.8-2.9 % (c4, lineitem SF10) and nothing at SF100; so
-// only the DELTA64 path stores nt.  FLS_STORE_CPOL (experiment builds, make
-// cpol) overrides every path's policy.
+// only the DELTA64 path leaves the default, with sc1 | nt (c3 1.671 ms
+// against 1.720 with nt alone, sc0 sc1 nt 1.684, sc0 nt 1.705,
+// profiles/r6/ab_builds_c3_cpol_r6s.txt).  FLS_STORE_CPOL (experiment
+// builds, make cpol) overrides every path's policy.
 #ifdef FLS_STORE_CPOL
 constexpr int kCpolAll = FLS_STORE_CPOL;
 #else
 constexpr int kCpolAll = -1;
 #endif
-constexpr int kCpolDelta64 = 2;  // nt
+constexpr int kCpolDelta64 = 18;  // sc1 | nt
 template <int CPOL = 0>
 __device__ __forceinline__ void st16(ou8 *out, uint32_t off, v4u v) {
     constexpr int cp = kCpolAll >= 0 ? kCpolAll : CPOL;
