@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--warm", type=int, default=3)
     ap.add_argument("--child", default="")
+    ap.add_argument("--profile", action="store_true",
+                    help="FLS_SCAN_PROFILE / FLS_READ_PROFILE in the children; their phase tables are printed")
     a = ap.parse_args()
     if a.child:
         child(a.child, a.threads, a.warm)
@@ -60,9 +62,14 @@ def main():
     try:
         for r in range(a.runs):
             for name, env in arms:
+                penv = {**os.environ, **env}
+                if a.profile:
+                    penv.update({"FLS_SCAN_PROFILE": "1", "FLS_READ_PROFILE": "1"})
                 p = subprocess.run([sys.executable, __file__, "--child", path, "--threads", str(a.threads),
-                                    "--warm", str(a.warm)], env={**os.environ, **env}, capture_output=True,
-                                   text=True, timeout=300)
+                                    "--warm", str(a.warm)], env=penv, capture_output=True, text=True, timeout=300)
+                if a.profile:
+                    print(f"--- run {r} {name}: profile (stderr)\n" + "\n".join(
+                        ln for ln in p.stderr.splitlines() if "amdgpu.ids" not in ln)[-6000:], flush=True)
                 if p.returncode != 0:
                     print(p.stderr[-2000:], file=sys.stderr)
                     sys.exit(p.returncode)
