@@ -635,7 +635,8 @@ struct Resident {
     std::vector<PinBuf<uint8_t>> h_heap;   // per FSST column: host copy string_t points into
     std::vector<uint64_t> heap_off;        // per (rg - rg0) * ncols + col: chunk heap offset
     std::vector<DevBuf<uint8_t>> d_out;    // per column, rows of [rg0, rg1)
-    double placement_q = 0;                // rating of d_out's placement (choose_placement; 0: not rated)
+    double placement_q = 0;                // write-probe rating of d_out's placement (choose_placement; 0: not rated)
+    float placement_ms = 0;                // decode-time rating of d_out's placement (0: not rated)
     DevBuf<DevChunk> d_chunks;
     std::vector<DevChunk> h_chunks;
     std::vector<uint8_t> mask;         // column mask h_chunks was built for
@@ -2743,39 +2744,100 @@ int rate_outputs(const fls_table *t, const Resident &r, const std::vector<DevBuf
     return 0;
 }
 
-int choose_placement(const fls_table *t, Resident &r) {
-    const int tries = placement_tries();
+int decode_part(fls_table *t, Resident &r, const std::vector<uint8_t> &mask);
+
+// A candidate set rated by one real decode launch of every column (the
+// launch after a warm-up one, HIP events): at SF100 the write probe rated every
+// set >= 0.99 while the main columns still decoded up to 5 % slower on some
+// sets (profiles/r6/placement_sels_sf100_r6w.txt), and four sets rated by
+// their decode differed by 3-4 % within one upload, the kept one decoding
+// within 0.3 % of its rating afterwards (placement_dec_sf100_r6x.txt).  The
+// launch's errors are not the upload's: a failure (ms < 0) falls back to the
+// write probe.
+float decode_rating(fls_table *t, Resident &r) {
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    const std::vector<uint8_t> mask(ncols, 1);
+    r.h_chunks.clear();  // descriptors point at the current outputs
+    const uint32_t ev0 = r.ev_used;
+    float ms = -1;
+    bool ok = decode_part(t, r, mask) == 0 && decode_part(t, r, mask) == 0;
+    ok = ok && hipStreamSynchronize(r.stream) == hipSuccess;
+    ok = ok && hipEventElapsedTime(&ms, r.ev_pool[ev0 + 2], r.ev_pool[ev0 + 3]) == hipSuccess;
+    uint32_t e = 0;
+    ok = ok && hipMemcpy(&e, r.err.p, sizeof(e), hipMemcpyDeviceToHost) == hipSuccess && e == 0;
+    (void)hipGetLastError();
+    (void)hipMemset(r.err.p, 0, sizeof(uint32_t));
+    r.ev_used = ev0;
+    r.h_chunks.clear();
+    return ok ? ms : -1.0f;
+}
+
+// a new candidate set of output columns (plain hipMalloc: a speculative set
+// must not evict cached images), or false when it does not fit
+bool alloc_candidate(const fls_table *t, const Resident &r, uint64_t set_bytes, std::vector<DevBuf<uint8_t>> &cand) {
+    const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < set_bytes + set_bytes / 8 + (1ull << 30)) {
+        (void)hipGetLastError();
+        return false;  // no room for a second set
+    }
+    cand.clear();
+    cand.resize(ncols);
+    for (uint32_t c = 0; c < ncols; ++c) {
+        const size_t n = std::max<size_t>(1, r.rows * out_bytes_of(t, c));
+        if (hipMalloc((void **)&cand[c].p, n) != hipSuccess) {
+            (void)hipGetLastError();
+            cand[c].p = nullptr;
+            cand.clear();  // frees the ones made
+            return false;
+        }
+        cand[c].n = n;
+        cand[c].dev = r.dev;
+    }
+    return true;
+}
+
+int choose_placement(fls_table *t, Resident &r) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     uint64_t set_bytes = 0;
     for (uint32_t c = 0; c < ncols; ++c) set_bytes += r.rows * out_bytes_of(t, c);
-    if (tries <= 1 || set_bytes < (256ull << 20)) return 0;  // small outputs: nothing to gain
-    const double good = knob_value("FLS_PLACEMENT_GOOD") / 1000.0;  // per mille
+    if (set_bytes < (256ull << 20)) return 0;  // small outputs: nothing to gain
     const bool dbg = getenv("FLS_DEBUG") != nullptr;
+    // 1. by decode time: FLS_PLACEMENT_DECODE sets (default 4), the fastest kept
+    const int ndec = (int)std::max<int64_t>(0, knob_value("FLS_PLACEMENT_DECODE"));
+    float best_ms = ndec > 1 ? decode_rating(t, r) : -1.0f;
+    if (best_ms > 0) {
+        if (dbg) fprintf(stderr, "DEBUG: placement dev %d set 0: decode %.3f ms\n", r.dev, best_ms);
+        int kept = 0;
+        std::vector<DevBuf<uint8_t>> cand;
+        for (int k = 1; k < ndec && alloc_candidate(t, r, set_bytes, cand); ++k) {
+            std::swap(r.d_out, cand);  // the candidate decodes in place of the current set
+            const float ms = decode_rating(t, r);
+            if (dbg) fprintf(stderr, "DEBUG: placement dev %d set %d: decode %.3f ms\n", r.dev, k, ms);
+            if (ms > 0 && ms < best_ms) {
+                best_ms = ms;  // keep it: the previous set is freed with cand
+                kept = k;
+            } else {
+                std::swap(r.d_out, cand);  // back to the current set; the candidate goes
+            }
+            cand.clear();
+        }
+        r.placement_ms = best_ms;
+        if (dbg) fprintf(stderr, "DEBUG: placement dev %d kept set %d (decode %.3f ms)\n", r.dev, kept, best_ms);
+        return 0;
+    }
+    // 2. by the write probe: up to FLS_PLACEMENT_TRIES sets, stop at q >= good
+    const int tries = placement_tries();
+    if (tries <= 1) return 0;
+    const double good = knob_value("FLS_PLACEMENT_GOOD") / 1000.0;  // per mille
     PlacementRating best;
     if (const int rc = rate_outputs(t, r, r.d_out, best)) return rc;
     if (dbg)
         fprintf(stderr, "DEBUG: placement dev %d set 0: chunk order %.3f ms, fill %.3f ms, q %.3f\n", r.dev,
                 best.chunk_ms, best.fill_ms, best.q);
     int kept = 0;
-    for (int k = 1; k < tries && best.q < good; ++k) {
-        size_t fr = 0, tot = 0;
-        HIP_TRY(hipMemGetInfo(&fr, &tot));
-        if (fr < set_bytes + set_bytes / 8 + (1ull << 30)) break;  // no room for a second set
-        std::vector<DevBuf<uint8_t>> cand(ncols);
-        bool ok = true;
-        for (uint32_t c = 0; c < ncols && ok; ++c) {
-            // plain hipMalloc: a speculative set must not evict cached images
-            const size_t n = std::max<size_t>(1, r.rows * out_bytes_of(t, c));
-            if (hipMalloc((void **)&cand[c].p, n) != hipSuccess) {
-                (void)hipGetLastError();
-                cand[c].p = nullptr;
-                ok = false;
-                break;
-            }
-            cand[c].n = n;
-            cand[c].dev = r.dev;
-        }
-        if (!ok) break;
+    std::vector<DevBuf<uint8_t>> cand;
+    for (int k = 1; k < tries && best.q < good && alloc_candidate(t, r, set_bytes, cand); ++k) {
         PlacementRating pr;
         if (const int rc = rate_outputs(t, r, cand, pr)) return rc;
         if (dbg)
@@ -2786,6 +2848,7 @@ int choose_placement(const fls_table *t, Resident &r) {
             best = pr;
             kept = k;
         }
+        cand.clear();
     }
     r.placement_q = best.q;
     if (dbg) fprintf(stderr, "DEBUG: placement dev %d kept set %d (q %.3f)\n", r.dev, kept, best.q);
@@ -2812,7 +2875,6 @@ int upload_part(fls_table *t, Resident &r) {
     r.rows = t->meta.rgs[r.rg1 - 1].first_row + t->meta.rgs[r.rg1 - 1].nrows - r.first_row;
     r.d_out.resize(ncols);
     for (uint32_t c = 0; c < ncols; ++c) HIP_TRY(r.d_out[c].alloc(r.dev, r.rows * out_bytes_of(t, c)));
-    if (const int prc = choose_placement(t, r)) return prc;
     // FSST heaps: chunk heaps back to back per column, host copy for string_t
     r.heap_off.assign((size_t)(r.rg1 - r.rg0) * ncols, 0);
     r.d_heap.resize(ncols);
@@ -2833,6 +2895,7 @@ int upload_part(fls_table *t, Resident &r) {
     }
     r.h_chunks.clear();
     r.mask.clear();
+    if (const int prc = choose_placement(t, r)) return prc;
     if (getenv("FLS_DEBUG")) {  // buffer placement (decode speed by buffer address)
         fprintf(stderr, "DEBUG: part dev %d rg [%u, %u) image %p %llu B\n", r.dev, r.rg0, r.rg1, (void *)r.img.p,
                 (unsigned long long)(hi - lo));

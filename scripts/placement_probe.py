@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--sleep", type=float, default=0.0, help="idle seconds before each trial")
+    ap.add_argument("--sels", default="all", help="column selections timed per trial: all, a-b ranges, c+d lists "
+                    "(comma separated); e.g. all,0-14,15 splits lineitem_full into its main and FSST parts")
     ap.add_argument("--clock-files", default="", help="glob of sysfs files sampled every 2 ms during a trial "
                     "(e.g. /sys/class/drm/card*/device/pp_dpm_[msf]clk); their distinct values per trial are printed")
     a = ap.parse_args()
@@ -85,18 +87,28 @@ def main():
         addrs = [int(x, 16) for x in re.findall(r"(?:image|out) (0x[0-9a-f]+)", txt)]
         qs = [float(x) for x in re.findall(r"placement dev \d+ set \d+: .* q ([0-9.]+)", txt)]
         kept = re.findall(r"kept set (\d+)", txt)
-        upload.last = f"placement q {qs} kept {kept[0] if kept else '-'}"
+        dms = [float(x) for x in re.findall(r"placement dev \d+ set \d+: .* decode ([0-9.-]+) ms", txt)]
+        upload.last = f"placement q {qs} decode {dms} kept {kept[0] if kept else '-'}"
         return t, addrs
 
-    def timeit(tabs):
+    def parse_sel(c):
+        if c == "all":
+            return None
+        if "-" in c:
+            lo, hi = map(int, c.split("-"))
+            return list(range(lo, hi + 1))
+        return [int(x) for x in c.split("+")]
+    sels = [parse_sel(c) for c in a.sels.split(",")]
+
+    def timeit(tabs, sel=None):
         times = [[] for _ in tabs]
         for t in tabs:
-            t.device_decode()
+            t.device_decode(sel)
             t.device_sync()
         for _ in range(a.rounds):
             for i, t in enumerate(tabs):
                 for _ in range(a.reps):
-                    t.device_decode()
+                    t.device_decode(sel)
                 st = t.device_sync()
                 times[i].append(st.kernel_ms_total / st.timed_launches)
         return times
@@ -151,9 +163,10 @@ def main():
         if mb:
             fl._check(fl.lib.fls_device_alloc(0, mb << 20, C.byref(pad)))
         t, ad = upload()
-        v = timeit([t])[0]
-        print(f"{trial:10s} median {statistics.median(v):.4f} ms min {min(v):.4f} rounds {[round(x, 3) for x in v]} "
-              f"| {upload.last} | pad {pad.value or 0:#x} | {desc(ad)}", flush=True)
+        for sname, sel in zip(a.sels.split(","), sels):
+            v = timeit([t], sel)[0]
+            print(f"{trial:10s} [{sname}] median {statistics.median(v):.4f} ms min {min(v):.4f} rounds "
+                  f"{[round(x, 3) for x in v]} | {upload.last} | pad {pad.value or 0:#x} | {desc(ad)}", flush=True)
         if cfiles:
             print("   clocks:", clocks(), flush=True)
         t.close()

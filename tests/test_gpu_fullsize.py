@@ -109,18 +109,20 @@ def test_fused_launch_bit_exact(fl, gpu, monkeypatch, capfd, env):
     assert fl.check_device_table(t, "lineitem_full", 0.3) == [0] * 16
 
 
-@pytest.mark.parametrize("tries", ["1", "3"])
-def test_placement_search_bit_exact(fl, gpu, monkeypatch, capfd, tries):
-    """the resident upload rates FLS_PLACEMENT_TRIES candidate sets
-    of output columns (FLS_PLACEMENT_GOOD=2000 never ends the search early)
-    and keeps the best; the table then decodes every value of all 16
-    lineitem_full SF1 columns bit-exactly into the kept set, and the rejected
-    sets' HBM is returned."""
+@pytest.mark.parametrize("mode", ["decode3", "probe3", "off"])
+def test_placement_search_bit_exact(fl, gpu, monkeypatch, capfd, mode):
+    """the resident upload rates candidate sets of output columns
+    -- by one decode launch each (FLS_PLACEMENT_DECODE, the default) or by the
+    write probe (FLS_PLACEMENT_TRIES; FLS_PLACEMENT_GOOD=2000 never ends that
+    search early) -- and keeps the best; the table then decodes every value of
+    all 16 lineitem_full SF1 columns bit-exactly into the kept set, and the
+    rejected sets' HBM is returned."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so.7")
     free0, tot = ctypes.c_size_t(), ctypes.c_size_t()
     img = fl.gen_image("lineitem_full", 1.0)
-    monkeypatch.setenv("FLS_PLACEMENT_TRIES", tries)
+    monkeypatch.setenv("FLS_PLACEMENT_DECODE", "3" if mode == "decode3" else "0")
+    monkeypatch.setenv("FLS_PLACEMENT_TRIES", "1" if mode == "off" else "3")
     monkeypatch.setenv("FLS_PLACEMENT_GOOD", "2000")
     monkeypatch.setenv("FLS_DEBUG", "1")
     capfd.readouterr()
@@ -129,9 +131,10 @@ def test_placement_search_bit_exact(fl, gpu, monkeypatch, capfd, tries):
     t.device_upload()
     err = capfd.readouterr().err
     rated = [ln for ln in err.splitlines() if "placement dev 0 set" in ln]
-    assert len(rated) == (int(tries) if tries != "1" else 0), err[-2000:]
-    if tries != "1":
+    assert len(rated) == (0 if mode == "off" else 3), err[-2000:]
+    if mode != "off":
         assert "kept set" in err
+        assert all(("decode" in ln) == (mode == "decode3") for ln in rated), rated
     free1 = ctypes.c_size_t()
     assert hip.hipMemGetInfo(ctypes.byref(free1), ctypes.byref(tot)) == 0
     out_bytes = sum(t.device_column(c)[1] for c in range(t.ncols))
