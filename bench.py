@@ -201,8 +201,12 @@ def measure_traffic(args):
                sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--steps", "2", "--warmup", "1",
                "--workload", args.workload, "--scale", str(args.scale), "--rows", str(args.rows),
                "--cpu-seconds", "0", "--e2e-scale", "0", "--no-verify", "--no-traffic"]
+        # the child's upload rates no output placements: its rating launches
+        # would be counted as decode dispatches (bytes per launch do not
+        # depend on the placement)
+        env = {**os.environ, "FLS_PLACEMENT_DECODE": "0", "FLS_PLACEMENT_TRIES": "1"}
         try:
-            subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
+            subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600, env=env)
         except Exception as e:  # noqa: BLE001 - report, never fail the bench on profiling
             return None, f"rocprofv3 {ctr} pass failed: {e}"
         per = {}  # kernel -> samples (a step is the fused kernel, or decode_kernel plus the FSST kernels)

@@ -2759,10 +2759,18 @@ float decode_rating(fls_table *t, Resident &r) {
     const std::vector<uint8_t> mask(ncols, 1);
     r.h_chunks.clear();  // descriptors point at the current outputs
     const uint32_t ev0 = r.ev_used;
-    float ms = -1;
-    bool ok = decode_part(t, r, mask) == 0 && decode_part(t, r, mask) == 0;
+    // two warm-up launches (a fresh set decodes ~4 % slower at first), then
+    // the fastest of three
+    constexpr int kWarm = 2, kTimed = 3;
+    bool ok = true;
+    for (int i = 0; i < kWarm + kTimed && ok; ++i) ok = decode_part(t, r, mask) == 0;
     ok = ok && hipStreamSynchronize(r.stream) == hipSuccess;
-    ok = ok && hipEventElapsedTime(&ms, r.ev_pool[ev0 + 2], r.ev_pool[ev0 + 3]) == hipSuccess;
+    float ms = -1;
+    for (int i = kWarm; i < kWarm + kTimed && ok; ++i) {
+        float x = 0;
+        ok = hipEventElapsedTime(&x, r.ev_pool[ev0 + 2 * i], r.ev_pool[ev0 + 2 * i + 1]) == hipSuccess;
+        if (ok && (ms < 0 || x < ms)) ms = x;
+    }
     uint32_t e = 0;
     ok = ok && hipMemcpy(&e, r.err.p, sizeof(e), hipMemcpyDeviceToHost) == hipSuccess && e == 0;
     (void)hipGetLastError();

@@ -87,7 +87,7 @@ def main():
         addrs = [int(x, 16) for x in re.findall(r"(?:image|out) (0x[0-9a-f]+)", txt)]
         qs = [float(x) for x in re.findall(r"placement dev \d+ set \d+: .* q ([0-9.]+)", txt)]
         kept = re.findall(r"kept set (\d+)", txt)
-        dms = [float(x) for x in re.findall(r"placement dev \d+ set \d+: .* decode ([0-9.-]+) ms", txt)]
+        dms = [float(x) for x in re.findall(r"placement dev \d+ set \d+: .*?decode ([0-9.-]+) ms", txt)]
         upload.last = f"placement q {qs} decode {dms} kept {kept[0] if kept else '-'}"
         return t, addrs
 
