@@ -2811,7 +2811,7 @@ int choose_placement(fls_table *t, Resident &r) {
     for (uint32_t c = 0; c < ncols; ++c) set_bytes += r.rows * out_bytes_of(t, c);
     if (set_bytes < (256ull << 20)) return 0;  // small outputs: nothing to gain
     const bool dbg = getenv("FLS_DEBUG") != nullptr;
-    // 1. by decode time: FLS_PLACEMENT_DECODE sets (default 4), the fastest kept
+    // 1. by decode time: FLS_PLACEMENT_DECODE sets (default 6), the fastest kept
     const int ndec = (int)std::max<int64_t>(0, knob_value("FLS_PLACEMENT_DECODE"));
     float best_ms = ndec > 1 ? decode_rating(t, r) : -1.0f;
     if (best_ms > 0) {
