@@ -62,6 +62,10 @@ namespace {
 //     shared by several waves;
 //   queue != NULL: whole chunks, the first static, then from the work queue;
 //   neither: whole chunks, grid-stride.
+// RATING: the same kernel under another name, for the upload's placement
+// rating launches (rating_launch(), flsgpu.hip decode_rating), so a profile
+// tells them from the decode's own launches
+template <bool RATING>
 __global__ __launch_bounds__(256, FLS_WAVES_PER_SIMD) void decode_kernel(const DevChunk *__restrict__ chunks, uint32_t nchunks,
                                                         uint32_t *__restrict__ err, uint32_t p_bytes,
                                                         uint32_t v_bytes, uint32_t *__restrict__ queue,
@@ -138,7 +142,7 @@ int decode_grid_size(uint32_t shmem_per_block) {
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel, 64 * kWaves, shmem_per_block) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel<false>, 64 * kWaves, shmem_per_block) !=
             hipSuccess)
             per_cu = 1;
         // A/B knob: blocks per CU below what the occupancy query reports
@@ -247,11 +251,17 @@ hipError_t launch_decode(const DevChunk *d_chunks, uint32_t nchunks, uint32_t *d
         const hipError_t e = hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(64 * kWaves), shmem, stream, d_chunks, nchunks, d_err,
+    hipLaunchKernelGGL(rating_launch() ? decode_kernel<true> : decode_kernel<false>, dim3(grid), dim3(64 * kWaves), shmem,
+                       stream, d_chunks, nchunks, d_err,
                        geom.p_bytes, geom.v_bytes, d_queue, d_split, plan.pieces,
                        (uint32_t)(shared_queue && d_queue) | (uint32_t)(prio & 3) << 1 |
                            (d_split && shared_queue ? plan.waves << 8 : 0u));
     return hipGetLastError();
+}
+
+bool &rating_launch() {
+    static thread_local bool f = false;
+    return f;
 }
 
 // ---- HBM placement probe ---------------------------------------

@@ -185,6 +185,13 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
 
+// Placement rating (flsgpu.hip decode_rating): decode launches made by this
+// thread while it is set use the kernels' RATING instantiations -- the same
+// code under another name (decode_kernel<true>, fused_kernel<.., .., true>),
+// so profiles and step spans tell the upload's rating launches from the
+// decode's own.
+bool &rating_launch();
+
 // HBM placement probe (round 6).  How fast the decode's write
 // stream runs depends on where the driver placed the output buffers: the same
 // pure write of the decode's output shape ran 5.66-6.89 TB/s from one

@@ -2759,6 +2759,10 @@ float decode_rating(fls_table *t, Resident &r) {
     const std::vector<uint8_t> mask(ncols, 1);
     r.h_chunks.clear();  // descriptors point at the current outputs
     const uint32_t ev0 = r.ev_used;
+    struct RatingScope {
+        RatingScope() { rating_launch() = true; }
+        ~RatingScope() { rating_launch() = false; }
+    } scope;
     // two warm-up launches (a fresh set decodes ~4 % slower at first), then
     // the fastest of three
     constexpr int kWarm = 2, kTimed = 3;

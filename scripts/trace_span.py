@@ -18,13 +18,18 @@ import csv
 import re
 import statistics
 
-DECODE = re.compile(r"(fused_kernel<[^>]*>|fsst_sp_kernel|fsst_kernel<[^>]*>|decode_kernel)")
+DECODE = re.compile(r"(fused_kernel<[^>]*>|fsst_sp_kernel|fsst_kernel<[^>]*>|decode_kernel(?:<[^>]*>)?)")
+# the upload's placement-rating launches (the same kernels under their RATING
+# instantiation): not steps
+RATING = re.compile(r"(decode_kernel<true>|fused_kernel<[^>]*,\s*true>)")
 
 
 def events(path):
     ev = []
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
+        if RATING.search(k):
+            continue
         m = DECODE.search(k)
         if m:
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1) + f" g{r['Grid_Size_X']}"))
