@@ -164,6 +164,10 @@ struct FusedLaunch {
     bool static_first = true;       // every wave's first item static (false: all from the queues)
     int waves_per_cu = 0;      // 0: as many as fit
     int x = 0;                 // the FSST part's experiment bits (FLS_FUSED_X; the experiment library only)
+    // main-queue tail: the last tail_chunks main chunks (the smallest: the
+    // host orders largest output first) are queued as tail_split pieces of
+    // about nvec / tail_split vectors each, so the launch ends on short items
+    uint32_t tail_chunks = 0, tail_split = 1;
 };
 hipError_t launch_fused(const DevChunk *d_main, uint32_t nmain, const DevChunk *d_fsst, uint32_t nfsst,
                         uint32_t nfvecs, bool small, uint32_t *d_err, const DecodeGeom &geom, hipStream_t stream,

@@ -1297,7 +1297,8 @@ __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict
                                                       uint32_t nfvecs, uint32_t *__restrict__ err,
                                                       uint32_t *__restrict__ queues, uint32_t p_bytes,
                                                       uint32_t v_bytes, uint32_t piece, uint32_t fsst_per16,
-                                                      uint32_t fsst_static, uint32_t nf_waves) {
+                                                      uint32_t fsst_static, uint32_t nf_waves, uint32_t nwhole,
+                                                      uint32_t tsplit) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     if ((uint32_t)(size_t)lds_raw != 0u) {  // LDS addressed from 0 (fsst_kernel)
         if (threadIdx.x == 0) atomicOr(err, KERR_LDS_BASE);
@@ -1309,19 +1310,28 @@ __global__ __launch_bounds__(64, 4) void fused_kernel(const DevChunk *__restrict
     // FSST vectors (the queue's pieces start after those)
     const uint32_t b = blockIdx.x, k = fsst_per16, grp = b >> 4, r = b & 15;
     const bool fsst_first = r < k;
+    // main items: chunks [0, nwhole) whole, then each later chunk as tsplit
+    // pieces (FusedLaunch::tail_chunks / tail_split)
+    const uint32_t nitems = nwhole + (nmain - nwhole) * tsplit;
     auto main_part = [&](bool first) {
-        uint32_t ci = first ? grp * (16 - k) + (r - k) : 0u;
+        uint32_t it = first ? grp * (16 - k) + (r - k) : 0u;
         for (;; first = false) {
             if (!first) {
-                if (__lane_id() == 0) ci = atomicAdd(queues, 1u);
-                ci = uni(ci);
+                if (__lane_id() == 0) it = atomicAdd(queues, 1u);
+                it = uni(it);
             }
-            if (ci >= nmain) {
-                if (first) continue;  // (fewer main chunks than waves: the queue is empty too)
+            if (it >= nitems) {
+                if (first) continue;  // (fewer main items than waves: the queue is empty too)
                 break;
             }
+            uint32_t ci = it, p = 0;
+            if (it >= nwhole) {
+                ci = nwhole + (it - nwhole) / tsplit;
+                p = (it - nwhole) % tsplit;
+            }
             const uint32_t nvec = gptr(mchunks)[ci].nvec;
-            if (nvec) dec::decode_chunk(mchunks + ci, 0u, p_bytes, v_bytes, err, nvec << 8);
+            const uint32_t vb = it >= nwhole ? nvec * p / tsplit : 0u, ve = it >= nwhole ? nvec * (p + 1) / tsplit : nvec;
+            if (vb < ve) dec::decode_chunk(mchunks + ci, 0u, p_bytes, v_bytes, err, vb | ve << 8);
         }
     };
     auto fsst_part = [&](bool first) {
@@ -1374,8 +1384,11 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
     for (int bb = 0; bb < grid; ++bb) nf += (uint32_t)(bb & 15) < k;
     const uint32_t nm = (uint32_t)grid - nf;
     const bool stat = how.static_first;
+    const uint32_t tsplit = std::max(1u, std::min(64u, how.tail_split));
+    const uint32_t nwhole = tsplit > 1 ? nmain - std::min(nmain, how.tail_chunks) : nmain;
+    const uint32_t nitems = nwhole + (nmain - nwhole) * tsplit;
     const uint32_t fstat = stat && nf ? (uint32_t)((uint64_t)nfvecs * std::min(100u, how.fsst_static_pct) / 100) : 0u;
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)d_queues, stat ? std::min(nm, nmain) : 0u, 1, stream);
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)d_queues, stat ? std::min(nm, nitems) : 0u, 1, stream);
     if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(d_queues + 1), 0, 1, stream);
     if (e != hipSuccess) return e;
     if (getenv("FLS_DEBUG"))
@@ -1384,7 +1397,7 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
                 SMALL ? "small" : "any", grid, per_cu, shmem, nmain, nfvecs, how.piece, how.fsst_per16);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), shmem, stream, d_main, nmain, d_fsst, nfsst, nfvecs, d_err,
                        d_queues, geom.p_bytes, geom.v_bytes, std::max(1u, std::min(64u, how.piece)) | (how.halving ? kHalving : 0u),
-                       k, fstat, stat ? std::max(1u, nf) : 0u);
+                       k, fstat, stat ? std::max(1u, nf) : 0u, nwhole, tsplit);
     return hipGetLastError();
 }
 

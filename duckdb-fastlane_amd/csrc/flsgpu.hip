@@ -1135,6 +1135,8 @@ FusedCfg fused_cfg() {
     if (const char *e = getenv("FLS_FUSED_STATIC_PCT")) f.how.fsst_static_pct = (uint32_t)std::min(100, std::max(0, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_STATIC_FIRST")) f.how.static_first = atoi(e) != 0;
     if (const char *e = getenv("FLS_FUSED_HALVING")) f.how.halving = atoi(e) != 0;
+    if (const char *e = getenv("FLS_FUSED_TAIL")) f.how.tail_chunks = (uint32_t)std::max(0, atoi(e));
+    if (const char *e = getenv("FLS_FUSED_TAIL_SPLIT")) f.how.tail_split = (uint32_t)std::min(64, std::max(1, atoi(e)));
     if (const char *e = getenv("FLS_FUSED_X")) f.how.x = atoi(e);
     if (const char *e = getenv("FLS_FUSED_MIN_VECS_PER_CU")) f.min_vecs_per_cu = (uint32_t)std::max(0, atoi(e));
     // an FSST kernel variant A/B (FLS_FSST_VARIANT, experiment library) runs

@@ -84,7 +84,10 @@ def test_lineitem_variants_sf1_bit_exact(fl, gpu, wl):
     {"FLS_FUSED": "1", "FLS_FUSED_FSST16": "8", "FLS_FUSED_WPC": "3"},
     {"FLS_FUSED": "1", "FLS_FUSED_STATIC_PCT": "0", "FLS_FUSED_PIECE": "3"},
     {"FLS_FUSED": "1", "FLS_FUSED_STATIC_PCT": "100", "FLS_FUSED_FSST16": "11"},
-], ids=["fused", "fused_main_first", "fused_fsst_first", "fused_3wpc", "fused_all_queue", "fused_all_static"])
+    {"FLS_FUSED": "1", "FLS_FUSED_TAIL": "300", "FLS_FUSED_TAIL_SPLIT": "3"},
+    {"FLS_FUSED": "1", "FLS_FUSED_TAIL": "1000000", "FLS_FUSED_TAIL_SPLIT": "64"},
+], ids=["fused", "fused_main_first", "fused_fsst_first", "fused_3wpc", "fused_all_queue", "fused_all_static",
+        "fused_tail_thirds", "fused_every_vector_an_item"])
 def test_fused_launch_bit_exact(fl, gpu, monkeypatch, capfd, env):
     """The fused launch (one kernel pulling main chunks and FSST pieces from
     two queues) decodes all 16 lineitem_full columns like the serial kernels,
