@@ -32,6 +32,8 @@ inline constexpr Knob kKnobs[] = {
     {"FLS_COPY_THREADS", 4},          // staging copy threads per connection
     {"FLS_PIN_ARENA_MB", 0},          // registered pinned arena cap (fls_pinned.hpp; 0: hipHostMalloc only)
     {"FLS_PLACEMENT_DECODE", 6},      // output-buffer sets rated by decode launches per resident part (0/1: write probe)
+    {"FLS_PLACEMENT_HEAPS", 1},       // candidate sets include new FSST heaps
+    {"FLS_PLACEMENT_IMAGE", 1},       // candidate sets include a new copy of the compressed image
     {"FLS_PLACEMENT_TRIES", 8},       // write-probe mode: output-buffer sets tried per resident part
     {"FLS_PLACEMENT_GOOD", 990},      // placement rating (per mille) that ends the search
     // writer (fls_writer.cpp)

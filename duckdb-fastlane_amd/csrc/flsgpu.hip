@@ -2786,29 +2786,69 @@ float decode_rating(fls_table *t, Resident &r) {
     return ok ? ms : -1.0f;
 }
 
-// a new candidate set of output columns (plain hipMalloc: a speculative set
-// must not evict cached images), or false when it does not fit
-bool alloc_candidate(const fls_table *t, const Resident &r, uint64_t set_bytes, std::vector<DevBuf<uint8_t>> &cand) {
+// A candidate placement: a new set of output columns, new FSST heaps
+// (FLS_PLACEMENT_HEAPS, default 1) and a new copy of the compressed image
+// (FLS_PLACEMENT_IMAGE, default 1): with all three re-drawn the decode-rated
+// SF100 step ran 20.65-20.75 ms against 20.91-21.05 for outputs alone, four
+// interleaved bench runs each (profiles/r6/ab_placement_candidates_r6af.txt).
+// swap_into exchanges it with the part's current buffers.
+struct Candidate {
+    std::vector<DevBuf<uint8_t>> out, heap;
+    DevBuf<uint8_t> img;
+    void clear() {
+        out.clear();
+        heap.clear();
+        img.release();
+    }
+    void swap_into(Resident &r) {
+        std::swap(r.d_out, out);
+        if (!heap.empty()) std::swap(r.d_heap, heap);
+        if (img.p) {
+            std::swap(r.img.p, img.p);
+            std::swap(r.img.n, img.n);
+            std::swap(r.img.dev, img.dev);
+        }
+    }
+};
+bool placement_flag(const char *name) { return knob_value(name) != 0; }
+
+// a new candidate (plain hipMalloc: a speculative set must not evict cached
+// images), or false when it does not fit
+bool alloc_candidate(const fls_table *t, const Resident &r, uint64_t set_bytes, Candidate &cand) {
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
+    const bool heaps = placement_flag("FLS_PLACEMENT_HEAPS"), image = placement_flag("FLS_PLACEMENT_IMAGE");
+    uint64_t extra = image ? r.img.n : 0;
+    for (uint32_t c = 0; heaps && c < ncols; ++c) extra += r.d_heap[c].p ? r.d_heap[c].n : 0;
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < set_bytes + set_bytes / 8 + (1ull << 30)) {
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < set_bytes + extra + (set_bytes + extra) / 8 + (1ull << 30)) {
         (void)hipGetLastError();
         return false;  // no room for a second set
     }
     cand.clear();
-    cand.resize(ncols);
-    for (uint32_t c = 0; c < ncols; ++c) {
-        const size_t n = std::max<size_t>(1, r.rows * out_bytes_of(t, c));
-        if (hipMalloc((void **)&cand[c].p, n) != hipSuccess) {
+    auto make = [&](DevBuf<uint8_t> &b, size_t n) {
+        if (hipMalloc((void **)&b.p, std::max<size_t>(1, n)) != hipSuccess) {
             (void)hipGetLastError();
-            cand[c].p = nullptr;
-            cand.clear();  // frees the ones made
+            b.p = nullptr;
             return false;
         }
-        cand[c].n = n;
-        cand[c].dev = r.dev;
+        b.n = n;
+        b.dev = r.dev;
+        return true;
+    };
+    cand.out.resize(ncols);
+    bool ok = true;
+    for (uint32_t c = 0; c < ncols && ok; ++c) ok = make(cand.out[c], r.rows * out_bytes_of(t, c));
+    if (ok && heaps) {
+        cand.heap.resize(ncols);
+        for (uint32_t c = 0; c < ncols && ok; ++c)
+            if (r.d_heap[c].p) ok = make(cand.heap[c], r.d_heap[c].n);
     }
-    return true;
+    if (ok && image) ok = make(cand.img, r.img.n) && hipMemcpy(cand.img.p, r.img.p, r.img.n, hipMemcpyDeviceToDevice) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        cand.clear();  // frees the ones made
+    }
+    return ok;
 }
 
 int choose_placement(fls_table *t, Resident &r) {
@@ -2823,16 +2863,16 @@ int choose_placement(fls_table *t, Resident &r) {
     if (best_ms > 0) {
         if (dbg) fprintf(stderr, "DEBUG: placement dev %d set 0: decode %.3f ms\n", r.dev, best_ms);
         int kept = 0;
-        std::vector<DevBuf<uint8_t>> cand;
+        Candidate cand;
         for (int k = 1; k < ndec && alloc_candidate(t, r, set_bytes, cand); ++k) {
-            std::swap(r.d_out, cand);  // the candidate decodes in place of the current set
+            cand.swap_into(r);  // the candidate decodes in place of the current set
             const float ms = decode_rating(t, r);
             if (dbg) fprintf(stderr, "DEBUG: placement dev %d set %d: decode %.3f ms\n", r.dev, k, ms);
             if (ms > 0 && ms < best_ms) {
                 best_ms = ms;  // keep it: the previous set is freed with cand
                 kept = k;
             } else {
-                std::swap(r.d_out, cand);  // back to the current set; the candidate goes
+                cand.swap_into(r);  // back to the current set; the candidate goes
             }
             cand.clear();
         }
@@ -2850,15 +2890,15 @@ int choose_placement(fls_table *t, Resident &r) {
         fprintf(stderr, "DEBUG: placement dev %d set 0: chunk order %.3f ms, fill %.3f ms, q %.3f\n", r.dev,
                 best.chunk_ms, best.fill_ms, best.q);
     int kept = 0;
-    std::vector<DevBuf<uint8_t>> cand;
+    Candidate cand;
     for (int k = 1; k < tries && best.q < good && alloc_candidate(t, r, set_bytes, cand); ++k) {
         PlacementRating pr;
-        if (const int rc = rate_outputs(t, r, cand, pr)) return rc;
+        if (const int rc = rate_outputs(t, r, cand.out, pr)) return rc;
         if (dbg)
             fprintf(stderr, "DEBUG: placement dev %d set %d: chunk order %.3f ms, fill %.3f ms, q %.3f\n", r.dev, k,
                     pr.chunk_ms, pr.fill_ms, pr.q);
         if (pr.q > best.q) {
-            std::swap(r.d_out, cand);  // the previous set is freed with cand
+            cand.swap_into(r);  // the previous set is freed with cand
             best = pr;
             kept = k;
         }
