@@ -69,6 +69,7 @@ def parse(argv=None):
     p.add_argument("--no-traffic", action="store_true",
                    help="skip the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--e2e-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal on CPU: ranks, shards and the cross-rank reduction over gloo; "
                         "no GPU, no decode (tests/test_bench_launcher.py)")
@@ -183,6 +184,18 @@ def wait_ranks(procs, poll_s: float = 0.2, grace_s: float = 30.0) -> int:
 
 
 # ---- measurement pieces -----------------------------------------------------
+def e2e_child(args):
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--e2e-child", "--no-traffic", "--workload", args.workload,
+           "--e2e-scale", str(args.e2e_scale), "--threads", str(args.threads)]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        if p.returncode != 0:
+            return {"error": f"e2e child exited {p.returncode}: {p.stderr[-500:]}"}
+        return json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 - the e2e numbers are reported beside the metric
+        return {"error": repr(e)}
+
+
 def measure_traffic(args):
     """HBM bytes per decode launch from rocprofv3 PMC counters, each counter in
     its own pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950).
@@ -469,6 +482,17 @@ def main(argv=None):
     if world == 1 and not args.no_traffic and not args.pmc_child and not under_profiler:
         traffic, traffic_note = measure_traffic(args)
         log(f"[traffic] {traffic_note}")
+    if args.e2e_child:
+        import pkgload
+        print(json.dumps(e2e_rates(pkgload.load(), args, host_threads(args, 1))), flush=True)
+        return
+    # the PCIe-inclusive e2e block (never `value`) in its own process, before
+    # this one touches the GPU: its scans' buffers land where a fresh process's
+    # would, not among the HBM the metric's upload allocated and rated
+    # 
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_scale > 0 and not args.pmc_child:
+        e2e = e2e_child(args)
 
     import torch  # torch first: its HIP runtime is the one the engine binds to
     import torch.distributed as dist
@@ -544,12 +568,7 @@ def main(argv=None):
     dt, total_vals, bad_total, checked_total = red["dt"], red["values"], red["mismatches"], red["checked"]
     mean_achieved = red["mean_achieved"]
 
-    e2e = None
-    if rank == 0 and world == 1 and args.e2e_scale > 0 and not args.pmc_child:
-        try:
-            e2e = e2e_rates(fl, args, nthreads)
-        except Exception as e:  # noqa: BLE001 - the e2e numbers are reported beside the metric
-            e2e = {"error": repr(e)}
+    ncols_main = t.ncols
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(fl, args, nthreads, nrows, cores)
@@ -557,7 +576,7 @@ def main(argv=None):
     if rank == 0:
         big = args.workload.startswith("lineitem")
         cfg = {"workload": args.workload + (f" SF{args.scale:g}" if big else ""),
-               "rows": nrows, "columns": t.ncols, "rowgroups": nrg,
+               "rows": nrows, "columns": ncols_main, "rowgroups": nrg,
                "rowgroups_per_gpu": red["rowgroups"], "parallelism": f"rowgroup-shard x{world}",
                "ranks_per_gpu": rpg, "physical_gpus": len(set(gpu_ids)),
                "step": "one decode launch over all resident vectors of the shard (HBM -> HBM)",
