@@ -12,6 +12,9 @@
 // coalesced wave access and a word's selection is one ballot.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
+
 #include "fls_filter.hpp"
 
 namespace fls {
@@ -190,7 +193,54 @@ __global__ __launch_bounds__(256) void narrow_kernel(const DevNarrow *__restrict
     if (__ballot(bad) != 0 && __lane_id() == 0) atomicOr(err, KERR_NARROW);
 }
 
+// 64 KiB pieces of the copies over a grid-stride block loop: 256 lanes x 16 B
+// per iteration (a 4 KiB contiguous write burst per block), the copy's last
+// (bytes mod 16) bytes one per lane
+__global__ __launch_bounds__(256) void host_copy_kernel(const HostCopyList l) {
+    const uint32_t total = l.first[l.n];
+    uint32_t i = 0;
+    for (uint32_t p = blockIdx.x; p < total; p += gridDim.x) {
+        while (p >= l.first[i + 1]) ++i;  // pieces ascend with p
+        const HostCopy c = l.c[i];
+        const uint64_t base = (uint64_t)(p - l.first[i]) * kHostCopyPiece;
+        const uint32_t len = (uint32_t)min<uint64_t>(kHostCopyPiece, c.bytes - base);
+        const v4u *__restrict__ s = (const v4u *)(c.src + base);
+        v4u *__restrict__ d = (v4u *)(c.dst + base);
+        const uint32_t nv = len / 16;
+#pragma unroll 4
+        for (uint32_t v = threadIdx.x; v < nv; v += 256) d[v] = s[v];
+        for (uint32_t b = nv * 16 + threadIdx.x; b < len; b += 256) c.dst[base + b] = c.src[base + b];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_host_copy(const HostCopy *copies, uint32_t n, hipStream_t stream) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
+        return hipErrorInvalidDevice;
+    uint32_t k = 0;
+    while (k < n) {
+        HostCopyList l;
+        memset(&l, 0, sizeof(l));
+        uint64_t pieces = 0;
+        for (; k < n && l.n < kHostCopyMax; ++k) {
+            if (!copies[k].bytes) continue;
+            if (((uintptr_t)copies[k].src | (uintptr_t)copies[k].dst) & 15) return hipErrorInvalidValue;
+            l.first[l.n] = (uint32_t)pieces;
+            l.c[l.n++] = copies[k];
+            pieces += (copies[k].bytes + kHostCopyPiece - 1) / kHostCopyPiece;
+            if (pieces >= (1ull << 31)) return hipErrorInvalidValue;
+        }
+        if (!l.n) continue;
+        l.first[l.n] = (uint32_t)pieces;
+        // 2 blocks per CU keep the link busy (256-4096 blocks measured equal)
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(pieces, 2ull * cus);
+        hipLaunchKernelGGL(host_copy_kernel, dim3(grid), dim3(256), 0, stream, l);
+        if (const hipError_t e = hipGetLastError()) return e;
+    }
+    return hipSuccess;
+}
 
 hipError_t launch_narrow(const DevNarrow *d_cols, uint32_t ncols, uint32_t nrows, uint32_t rg_rows,
                          uint32_t *d_err, hipStream_t stream) {

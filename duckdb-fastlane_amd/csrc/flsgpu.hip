@@ -1977,17 +1977,26 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     // 3. D2H into pinned host columns (and string heaps)
     if (sl.pt[1]) HIP_TRY(hipEventRecord(sl.pt[1], sl.stream));
     sl.prof_d2h = 0;
-    for (uint32_t c = 0; c < ncols; ++c) {
-        if (!col_selected(s.mask, c)) continue;
-        if (!filtered) {
-            HIP_TRY(hipMemcpyAsync(hb.h_out[c].p, hb.narrowed[c] ? sl.d_narrow[c].p : sl.d_out[c].p, rows * hb.ob[c],
-                                   hipMemcpyDeviceToHost, sl.stream));
-            sl.prof_d2h += rows * hb.ob[c];
+    {
+        // by the copy kernel (FLS_SCAN_COPY_KERNEL; fls_filter.hpp), or the
+        // DMA engines for a misaligned pair and with the knob at 0
+        const bool by_kernel = knob_value("FLS_SCAN_COPY_KERNEL") != 0;
+        std::vector<HostCopy> copies;
+        auto d2h = [&](uint8_t *dst, const uint8_t *src, uint64_t bytes) -> hipError_t {
+            sl.prof_d2h += bytes;
+            if (by_kernel && !(((uintptr_t)dst | (uintptr_t)src) & 15)) {
+                copies.push_back({src, dst, bytes});
+                return hipSuccess;
+            }
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, sl.stream);
+        };
+        for (uint32_t c = 0; c < ncols; ++c) {
+            if (!col_selected(s.mask, c)) continue;
+            if (!filtered)
+                HIP_TRY(d2h(hb.h_out[c].p, hb.narrowed[c] ? sl.d_narrow[c].p : sl.d_out[c].p, rows * hb.ob[c]));
+            if (sl.heap_bytes[c]) HIP_TRY(d2h(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c]));
         }
-        if (sl.heap_bytes[c]) {
-            HIP_TRY(hipMemcpyAsync(hb.h_heap[c].p, sl.d_heap[c].p, sl.heap_bytes[c], hipMemcpyDeviceToHost, sl.stream));
-            sl.prof_d2h += sl.heap_bytes[c];
-        }
+        HIP_TRY(launch_host_copy(copies.data(), (uint32_t)copies.size(), sl.stream));
     }
     if (sl.pt[2]) {
         HIP_TRY(hipEventRecord(sl.pt[2], sl.stream));
