@@ -125,15 +125,14 @@ hipError_t launch_narrow(const DevNarrow *d_cols, uint32_t ncols, uint32_t nrows
                          uint32_t *d_err, hipStream_t stream);
 
 // Delivery of a batch's decoded columns and string heaps into pinned host
-// memory by a copy kernel (FLS_SCAN_COPY_KERNEL, default 1) instead of the
-// DMA engines: a hipMemcpy D2H ran 57.1 GB/s in some processes and 30.2 in
-// others on one box (link at 32 GT/s x16 throughout), a copy kernel 54.7 in
+// memory by a copy kernel (FLS_SCAN_COPY_KERNEL, default 1) instead of the DMA engines: a
+// hipMemcpy D2H ran 57.1 GB/s in some processes and 30.2 in others on one box (link at 32 GT/s x16 throughout), a copy kernel 54.7 in
 // every process (profiles/r6/d2h_probe_r6an.txt).  Both pointers of a copy
 // are 16-byte aligned (the caller sends the others through hipMemcpyAsync);
 // up to kHostCopyMax copies per launch, passed by value.
 struct HostCopy {
-    const uint8_t *src;  // HBM
-    uint8_t *dst;        // pinned host memory
+    const uint8_t *src;  // HBM or pinned host memory
+    uint8_t *dst;        // the other
     uint64_t bytes;
 };
 constexpr uint32_t kHostCopyMax = 40;

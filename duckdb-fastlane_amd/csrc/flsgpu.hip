@@ -1779,6 +1779,9 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
             t->res->copy.copy(sl.h_stage.p, src, hi - lo);
             src = sl.h_stage.p;
         }
+        // (by the DMA engines: a copy kernel here, 57.4 GB/s alone, waits for
+        // CUs behind the other slot's decode and lost the overlap: the cold
+        // 16-thread query ran 135 against 156 M rows/s, cold_copy_ab_r6ap.txt)
         HIP_TRY(hipMemcpyAsync(dst, src, hi - lo, hipMemcpyHostToDevice, sl.stream));
         sl.in_dev = dst;
     }
