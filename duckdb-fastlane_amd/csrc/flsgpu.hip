@@ -1887,7 +1887,11 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         if (!col_selected(s.dmask, c)) continue;
         const uint64_t nb = max_rows * out_bytes_of(t, c);
         HIP_TRY(sl.d_out[c].alloc(d.dev, nb));
-        if (col_selected(s.mask, c)) HIP_TRY(hb.h_out[c].alloc(nb));
+        // the host column at the width that crosses PCIe (narrowed values,
+        // dictionary codes, string lengths): pinned memory comes at ~6 GB/s
+        // whatever the thread count (pin_alloc_r6ar.txt), and a cold query
+        // allocates every host batch it holds
+        if (col_selected(s.mask, c)) HIP_TRY(hb.h_out[c].alloc(max_rows * hb.ob[c]));
         for (uint32_t r = 0; r < sl.nrg; ++r) {
             hoff[(size_t)r * ncols + c] = sl.heap_bytes[c];
             if (is_fsst(t, sl.rg0 + r, c)) sl.heap_bytes[c] += t->meta.rgs[sl.rg0 + r].chunks[c].hdr.reserved1;
