@@ -29,6 +29,7 @@ inline constexpr Knob kKnobs[] = {
     {"FLS_SCAN_BATCH", 8},            // row groups per scan batch
     {"FLS_SCAN_STRLEN", 1},           // narrowed scans ship FSST columns as lengths + heap
     {"FLS_SCAN_COPY_KERNEL", 1},      // batches reach pinned host memory by a copy kernel (0: DMA engines)
+    {"FLS_SCAN_EARLY_REFILL", 1},     // a slot refills once its batch's D2H is seen complete (0: once handed out)
     {"FLS_OPEN_CACHE", 16},           // opened files kept mapped with their metadata (0: off)
     {"FLS_COPY_THREADS", 4},          // staging copy threads per connection
     {"FLS_PIN_ARENA_MB", 0},          // registered pinned arena cap (fls_pinned.hpp; 0: hipHostMalloc only)

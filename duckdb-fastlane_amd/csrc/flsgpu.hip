@@ -362,11 +362,28 @@ struct HostBatch {
     std::vector<uint64_t> heap_off;
     std::vector<std::unique_ptr<uint8_t[]>> h_rec;
     std::vector<uint64_t> h_rec_cap;      // rows h_rec[c] holds
+    // completion of the batch's device work, per batch rather than per slot:
+    // the slot takes its next batch as soon as this one's D2H is complete (its
+    // first acquire), while consumers still take this one's row groups
+    hipEvent_t done = nullptr;            // recorded after the D2H (fill_batch)
+    hipEvent_t pt[3] = {};                // FLS_SCAN_PROFILE: decode start, D2H start, end (timing events)
+    uint64_t prof_d2h = 0;                // ... and the batch's D2H bytes
+    std::atomic<bool> prof_pending{false};  // the batch's times not yet counted (its first acquire does)
+    std::atomic<bool> upload_resident{false};  // the batch uploads into the resident image (marked present once done)
+    PinBuf<uint32_t> h_err;               // the device error flags, copied after the batch's kernels
+    HostBatch() = default;
+    HostBatch(const HostBatch &) = delete;
+    HostBatch &operator=(const HostBatch &) = delete;
+    ~HostBatch() {
+        if (done) hipEventDestroy(done);
+        for (hipEvent_t e : pt)
+            if (e) hipEventDestroy(e);
+    }
 };
 
 struct Slot {                       // one batch of row groups in flight
     uint32_t rg0 = 0, nrg = 0;      // absolute row groups (consecutive, all surviving pruning)
-    bool busy = false;              // a batch is enqueued and not yet fully handed out
+    bool busy = false;              // a batch is enqueued and its D2H not yet seen complete by an acquire
     bool filling = false;           // claimed, its work being enqueued (fill_batch, outside s.mu)
     bool starved = false;           // refill deferred: the host-batch pool is at its cap
     HostBatch *hb = nullptr;        // host side of the batch in flight
@@ -377,16 +394,10 @@ struct Slot {                       // one batch of row groups in flight
     DevBuf<DevChunk> d_chunks;
     DevBuf<uint8_t> d_in;           // streamed compressed bytes of the batch (no resident image)
     const uint8_t *in_dev = nullptr;  // device address of the batch's first compressed byte
-    std::atomic<bool> upload_resident{false};  // the batch uploads into the resident image (marked present once done)
     PinBuf<uint8_t> h_stage;        // pinned bounce buffer when the image cannot be pinned
     DevBuf<uint32_t> queue;         // decode work-queue counter
     uint64_t in_base = 0;
-    hipEvent_t done = nullptr;
-    hipEvent_t pt[3] = {};          // FLS_SCAN_PROFILE: decode start, D2H start, end (timing events)
-    uint64_t prof_d2h = 0;          // ... and the batch's D2H bytes
-    std::atomic<bool> prof_pending{false};  // the batch's times not yet counted (its first acquire does)
     hipStream_t stream = nullptr;   // one stream per slot: slot b's H2D+decode overlap slot a's D2H
-    PinBuf<uint32_t> h_err;         // the device error flags, copied after the batch's kernels
     // filtered batches (fls_scan_filter)
     DevBuf<uint64_t> d_mask;        // selection bits, 16 words per 1024-row vector
     DevBuf<uint32_t> d_counts;      // selected rows per vector
@@ -437,12 +448,8 @@ struct ScanDev {
     }
     ~ScanDev() {
         sync();
-        for (auto &sl : slots) {
-            if (sl.done) hipEventDestroy(sl.done);
-            for (hipEvent_t e : sl.pt)
-                if (e) hipEventDestroy(e);
+        for (auto &sl : slots)
             if (sl.stream) hipStreamDestroy(sl.stream);
-        }
         if (stream) hipStreamDestroy(stream);
     }
 };
@@ -470,6 +477,10 @@ struct ScanCtx {
     std::vector<std::unique_ptr<ScanDev>> devs;  // borrowed from the connection (ConnRes)
     int64_t held = -1;              // row group fls_scan_next handed out last (released on the next call)
     std::vector<std::pair<uint32_t, HostBatch *>> out;  // row groups handed out and not yet released
+    // batches whose D2H an acquire saw complete and whose slot took its next
+    // batch: (device index, batch) until their last row group is handed out
+    std::vector<std::pair<int, HostBatch *>> ready;
+    bool early_refill = true;       // FLS_SCAN_EARLY_REFILL
     uint32_t max_batches = 64;      // host-batch pool cap per GPU (FLS_SCAN_HOST_BATCHES)
     int nslots = 2;                 // device slots per GPU (FLS_SCAN_SLOTS, 1..ScanDev::kMaxSlots)
     // sticky error of a failed batch refill (scan_release): consumers waiting
@@ -1488,6 +1499,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         for (auto &b : d.batches) d.free_batches.push_back(b.get());
     }
     s.out.clear();
+    s.ready.clear();
     s.mask.assign(ncols, 1);
     if (col_mask)
         for (uint32_t c = 0; c < ncols; ++c) s.mask[c] = col_mask[c] ? 1 : 0;
@@ -1525,6 +1537,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         for (uint32_t g = 0; g < G; ++g) s.devs.push_back(t->res->take(devs[g]));
     }
     s.batch = (uint32_t)std::max<int64_t>(1, knob_value("FLS_SCAN_BATCH"));
+    s.early_refill = knob_value("FLS_SCAN_EARLY_REFILL") != 0;
     s.max_batches = (uint32_t)std::max<int64_t>(2, knob_value("FLS_SCAN_HOST_BATCHES"));
     s.nslots = (int)std::max<int64_t>(1, std::min<int64_t>(ScanDev::kMaxSlots, knob_value("FLS_SCAN_SLOTS")));
     for (uint32_t g = 0; g < G; ++g) {
@@ -1532,12 +1545,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
         HIP_TRY(hipSetDevice(d.dev));
         if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         for (auto &sl : d.slots) {
-            if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-            if (ScanProf::on())
-                for (hipEvent_t &e : sl.pt)
-                    if (!e) HIP_TRY(hipEventCreate(&e));
             if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-            HIP_TRY(sl.h_err.alloc(1));
             sl.d_out.resize(ncols);
         }
         // contiguous shard of the surviving row groups
@@ -1758,7 +1766,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     if (di && (lo < di->lo || hi > di->hi)) di = nullptr;  // outside this GPU's image: streamed
     bool have = di != nullptr;
     for (uint32_t r = sl.rg0; have && r < sl.rg0 + sl.nrg; ++r) have = di->present[r].load(std::memory_order_acquire) != 0;
-    sl.upload_resident.store(di != nullptr && !have);
+    hb.upload_resident.store(di != nullptr && !have);
     if (have) {
         sl.in_dev = di->p + (lo - di->lo);
         if (getenv("FLS_DEBUG"))
@@ -1936,7 +1944,12 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     HIP_TRY(sl.h_chunks.alloc(kk));
     HIP_TRY(sl.d_chunks.alloc(d.dev, kk));
     if (kk) memcpy(sl.h_chunks.p, list.data(), kk * sizeof(DevChunk));
-    if (sl.pt[0]) HIP_TRY(hipEventRecord(sl.pt[0], sl.stream));
+    if (!hb.done) HIP_TRY(hipEventCreateWithFlags(&hb.done, hipEventDisableTiming));
+    if (ScanProf::on())
+        for (hipEvent_t &e : hb.pt)
+            if (!e) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hb.h_err.alloc(1));
+    if (hb.pt[0]) HIP_TRY(hipEventRecord(hb.pt[0], sl.stream));
     HIP_TRY(hipMemcpyAsync(sl.d_chunks.p, sl.h_chunks.p, kk * sizeof(DevChunk), hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(sl.queue.alloc(d.dev, kQueueWords));
     // (only batches with FSST work: a stale FLS_FSST_VARIANT must not fail
@@ -1982,15 +1995,15 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         if (rc) return rc;
     }
     // 3. D2H into pinned host columns (and string heaps)
-    if (sl.pt[1]) HIP_TRY(hipEventRecord(sl.pt[1], sl.stream));
-    sl.prof_d2h = 0;
+    if (hb.pt[1]) HIP_TRY(hipEventRecord(hb.pt[1], sl.stream));
+    hb.prof_d2h = 0;
     {
         // by the copy kernel (FLS_SCAN_COPY_KERNEL; fls_filter.hpp), or the
         // DMA engines for a misaligned pair and with the knob at 0
         const bool by_kernel = knob_value("FLS_SCAN_COPY_KERNEL") != 0;
         std::vector<HostCopy> copies;
         auto d2h = [&](uint8_t *dst, const uint8_t *src, uint64_t bytes) -> hipError_t {
-            sl.prof_d2h += bytes;
+            hb.prof_d2h += bytes;
             if (by_kernel && !(((uintptr_t)dst | (uintptr_t)src) & 15)) {
                 copies.push_back({src, dst, bytes});
                 return hipSuccess;
@@ -2005,15 +2018,15 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         }
         HIP_TRY(launch_host_copy(copies.data(), (uint32_t)copies.size(), sl.stream));
     }
-    if (sl.pt[2]) {
-        HIP_TRY(hipEventRecord(sl.pt[2], sl.stream));
-        sl.prof_pending.store(true);
+    if (hb.pt[2]) {
+        HIP_TRY(hipEventRecord(hb.pt[2], sl.stream));
+        hb.prof_pending.store(true);
     }
     // the error flags ride along (sticky device flags: a batch sees its own
     // kernels' and any earlier ones'), so an acquire reads pinned memory
     // instead of a synchronous 4-byte copy per row group
-    HIP_TRY(hipMemcpyAsync(sl.h_err.p, d.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.stream));
-    HIP_TRY(hipEventRecord(sl.done, sl.stream));
+    HIP_TRY(hipMemcpyAsync(hb.h_err.p, d.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.stream));
+    HIP_TRY(hipEventRecord(hb.done, sl.stream));
     hb.col_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
     hb.valid_ptrs.assign((size_t)sl.nrg * ncols, nullptr);
     hb.vbits.resize((size_t)sl.nrg * ncols);
@@ -2091,14 +2104,21 @@ int scan_start(fls_table *t, ScanCtx &s) {
     return 0;
 }
 
-// the (device, slot) holding row group rg, or false if its batch is not enqueued
-bool find_slot(ScanCtx &s, uint32_t rg, int &g, int &si) {
+// the device and host batch holding row group rg (a batch already released by
+// its slot, or one a slot holds), or false if its batch is not enqueued
+bool find_batch(ScanCtx &s, uint32_t rg, int &g, HostBatch *&hb) {
+    for (auto &[dg, b] : s.ready)
+        if (rg >= b->rg0 && rg < b->rg0 + b->nrg) {
+            g = dg;
+            hb = b;
+            return true;
+        }
     for (size_t i = 0; i < s.devs.size(); ++i)
         for (int j = 0; j < s.nslots; ++j) {
             const Slot &sl = s.devs[i]->slots[j];
             if (sl.busy && rg >= sl.rg0 && rg < sl.rg0 + sl.nrg) {
                 g = (int)i;
-                si = j;
+                hb = sl.hb;
                 return true;
             }
         }
@@ -2136,12 +2156,15 @@ void set_scan_error(ScanCtx &s, int rc) {
 }
 
 // Claim the next row group in order and wait until its batch is decoded and
-// copied back.  Its buffers stay valid until scan_release(rg).  Handing out a
-// batch's last row group refills its slot (the device side is idle once the
-// batch's D2H completed), so no consumer waits on another one's release.
+// copied back.  Its buffers stay valid until scan_release(rg).  The first
+// acquire that sees a batch's D2H complete refills the batch's slot (the
+// device side is idle from then on; the batch's host side, its events and
+// error flags are the HostBatch's), and the batch's other row groups are found
+// on s.ready: the next batch's fill, decode and D2H overlap the hand-out of
+// this one's, and no consumer waits on another one's release.
 int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     if (!s.active) return fail(FLS_ERR_STATE, "scan not started");
-    int g = -1, si = -1;
+    int g = -1;
     uint32_t rg;
     HostBatch *hb = nullptr;
     {
@@ -2149,34 +2172,32 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         if (s.err_rc) return fail(s.err_rc, "%s", s.err_msg.c_str());
         if (s.cur >= s.rgs.size()) return 0;
         rg = s.rgs[s.cur++];
-        // the batch holding rg is enqueued once the slot's previous batch has
-        // been handed out (or, at the host-batch cap, once one is released)
-        s.cv.wait(lk, [&] { return find_slot(s, rg, g, si) || !s.active || s.err_rc != 0; });
+        // the batch holding rg is enqueued once its slot's previous batch has
+        // completed (or, at the host-batch cap, once a batch is released)
+        s.cv.wait(lk, [&] { return find_batch(s, rg, g, hb) || !s.active || s.err_rc != 0; });
         if (g < 0) {
             if (!s.active) return fail(FLS_ERR_STATE, "scan ended while waiting for row group %u", rg);
             return fail(s.err_rc, "%s", s.err_msg.c_str());
         }
-        hb = s.devs[g]->slots[si].hb;
     }
     ScanDev &d = *s.devs[g];
-    Slot &sl = d.slots[si];
     auto wait_batch = [&]() -> int {
         HIP_TRY(hipSetDevice(d.dev));
         ProfTimer pw(PROF_WAIT);
-        HIP_TRY(hipEventSynchronize(sl.done));
-        if (sl.prof_pending.exchange(false)) {  // the batch's stream times, once
+        HIP_TRY(hipEventSynchronize(hb->done));
+        if (hb->prof_pending.exchange(false)) {  // the batch's stream times, once
             float dec = 0, d2h = 0;
-            if (hipEventElapsedTime(&dec, sl.pt[0], sl.pt[1]) == hipSuccess &&
-                hipEventElapsedTime(&d2h, sl.pt[1], sl.pt[2]) == hipSuccess) {
+            if (hipEventElapsedTime(&dec, hb->pt[0], hb->pt[1]) == hipSuccess &&
+                hipEventElapsedTime(&d2h, hb->pt[1], hb->pt[2]) == hipSuccess) {
                 ScanProf &p = scan_prof();
                 p.ns[PROF_GPU_DECODE] += (uint64_t)(dec * 1e6);
                 p.calls[PROF_GPU_DECODE] += 1;
                 p.ns[PROF_D2H] += (uint64_t)(d2h * 1e6);
-                p.bytes[PROF_D2H] += sl.prof_d2h;
+                p.bytes[PROF_D2H] += hb->prof_d2h;
                 p.calls[PROF_D2H] += 1;
             }
         }
-        const uint32_t err = *(volatile const uint32_t *)sl.h_err.p;
+        const uint32_t err = *(volatile const uint32_t *)hb->h_err.p;
         if (err & KERR_FILTER_STR) return fail(FLS_ERR_FORMAT, "filter: string outside its batch heap (flags 0x%x)", err);
         if (err & KERR_NARROW)
             return fail(FLS_ERR_FORMAT, "corrupt chunk: a value outside its zone map in a narrowed column (flags 0x%x)", err);
@@ -2192,8 +2213,8 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     }
     // the batch's upload into the resident image is complete (its event covers
     // the H2D): later scans of this file may decode these row groups from it
-    if (sl.upload_resident.exchange(false) && d.dimg)
-        for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) d.dimg->present[r].store(1, std::memory_order_release);
+    if (hb->upload_resident.exchange(false) && d.dimg)
+        for (uint32_t r = hb->rg0; r < hb->rg0 + hb->nrg; ++r) d.dimg->present[r].store(1, std::memory_order_release);
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
     out->rowgroup = rg;
     out->nrows = t->meta.rgs[rg].nrows;
@@ -2234,11 +2255,20 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         }
     }
     bool refill = false;
+    int si = -1;
     std::shared_ptr<DevImage> done_img;  // dropped outside s.mu
     {
         std::lock_guard<std::mutex> lk(s.mu);
         s.out.emplace_back(rg, hb);
-        if (++hb->handed == hb->nrg) {
+        const bool last = ++hb->handed == hb->nrg;
+        // the batch's D2H is complete: if its slot still holds it, the slot
+        // takes its next batch now (FLS_SCAN_EARLY_REFILL=0: once the batch's
+        // last row group is handed out) and the batch moves to s.ready
+        if (last || s.early_refill)
+            for (int k = 0; k < s.nslots && si < 0; ++k)
+                if (d.slots[k].busy && d.slots[k].hb == hb) si = k;
+        if (si >= 0) {
+            s.ready.emplace_back(g, hb);
             // a failed refill does not take this row group back: it is delivered,
             // and the error surfaces at the next acquire
             const int c = claim_batch(t, s, d, si);
@@ -2252,9 +2282,16 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
                 if (idle) done_img = std::move(d.dimg);
             }
         }
+        if (last)  // every row group of the batch handed out
+            for (size_t i = 0; i < s.ready.size(); ++i)
+                if (s.ready[i].second == hb) {
+                    s.ready.erase(s.ready.begin() + (long)i);
+                    break;
+                }
         s.cv.notify_all();
     }
     if (refill) {  // the slot's next batch, outside s.mu (claim_batch)
+        Slot &sl = d.slots[si];
         const int rc = fill_batch(t, s, d, si);
         std::lock_guard<std::mutex> lk(s.mu);
         sl.filling = false;
