@@ -1710,9 +1710,12 @@ int claim_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     sl.starved = false;
     sl.hb = nullptr;
     if (d.next_p >= d.p1) return 0;
-    // host side from the pool; at the cap the refill waits for a release
+    // host side from the pool; at the cap the refill waits for a release.
+    // Slots past the first two never grow the pool: they run on host batches
+    // consumers have handed back (a cold query's first batches would otherwise
+    // wait for one more pinned allocation each; slots_r6az.txt)
     if (d.free_batches.empty()) {
-        if (d.batches.size() >= s.max_batches) {
+        if (d.batches.size() >= s.max_batches || si >= 2) {
             sl.starved = true;
             return 0;
         }

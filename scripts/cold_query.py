@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--warm", type=int, default=3)
     ap.add_argument("--child", default="")
+    ap.add_argument("--gen-only", default="", help="write the workload's file to this path and exit")
     ap.add_argument("--profile", action="store_true",
                     help="FLS_SCAN_PROFILE / FLS_READ_PROFILE in the children; their phase tables are printed")
     a = ap.parse_args()
@@ -50,6 +51,10 @@ def main():
     import pkgload
     fl = pkgload.load()
     img = fl.gen_image(a.workload, a.scale, 0, 0, None, a.threads)
+    if a.gen_only:
+        img.write(a.gen_only)
+        img.close()
+        return
     fd, path = tempfile.mkstemp(suffix=".fls", dir=os.environ.get("TMPDIR", "/tmp"))
     os.close(fd)
     img.write(path)
