@@ -40,6 +40,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "fls_alp.hpp"
 #include "fls_decode.hpp"
@@ -138,16 +141,44 @@ extern "C" int64_t fls_trace_read(void *dst, uint32_t cap) {
 }
 #endif
 
-int decode_grid_size(uint32_t shmem_per_block) {
-    int dev = 0, cus = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel<false>, 64 * kWaves, shmem_per_block) !=
-            hipSuccess)
-            per_cu = 1;
-        // A/B knob: blocks per CU below what the occupancy query reports
-        if (const char *e = getenv("FLS_BLOCKS_PER_CU")) per_cu = std::min(per_cu, std::max(1, atoi(e)));
+namespace {
+std::mutex g_occ_mu;
+std::map<int, int> g_cus;
+std::map<std::tuple<int, const void *, int, size_t>, int> g_occ;
+}  // namespace
+
+int device_cus() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    {
+        std::lock_guard<std::mutex> lk(g_occ_mu);
+        if (auto it = g_cus.find(dev); it != g_cus.end()) return it->second;
     }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    g_cus[dev] = cus;
+    return cus;
+}
+
+int occupancy(const void *kernel, int block, size_t shmem) {
+    int dev = 0, per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess) return 1;
+    const auto key = std::make_tuple(dev, kernel, block, shmem);
+    {
+        std::lock_guard<std::mutex> lk(g_occ_mu);
+        if (auto it = g_occ.find(key); it != g_occ.end()) return it->second;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, shmem) != hipSuccess) return 1;
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    g_occ[key] = per_cu;
+    return per_cu;
+}
+
+int decode_grid_size(uint32_t shmem_per_block) {
+    const int cus = device_cus();
+    int per_cu = occupancy(reinterpret_cast<const void *>(decode_kernel<false>), 64 * kWaves, shmem_per_block);
+    // A/B knob: blocks per CU below what the occupancy query reports
+    if (const char *e = getenv("FLS_BLOCKS_PER_CU")) per_cu = std::min(per_cu, std::max(1, atoi(e)));
     return cus * std::max(1, per_cu);
 }
 

@@ -188,6 +188,13 @@ hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t n
                           hipStream_t stream);
 // Resident-grid size of the v2 kernel for the given dynamic LDS per block.
 int decode_grid_size(uint32_t shmem_per_block);
+// The current device's CU count and a kernel's resident blocks per CU
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor), cached per device / (device,
+// kernel, block size, dynamic LDS bytes): the scan's refill sizes several
+// grids per batch, and these queries cost more host time than the launches.
+// A failed query returns the fallback (256 CUs, 1 block) uncached.
+int device_cus();
+int occupancy(const void *kernel, int block, size_t shmem);
 
 // Placement rating (flsgpu.hip decode_rating): decode launches made by this
 // thread while it is set use the kernels' RATING instantiations -- the same

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "fls_decode.hpp"
 #include "fls_filter.hpp"
 
 namespace fls {
@@ -216,9 +217,7 @@ __global__ __launch_bounds__(256) void host_copy_kernel(const HostCopyList l) {
 }  // namespace
 
 hipError_t launch_host_copy(const HostCopy *copies, uint32_t n, hipStream_t stream) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
-        return hipErrorInvalidDevice;
+    const int cus = device_cus();
     uint32_t k = 0;
     while (k < n) {
         HostCopyList l;

@@ -1234,11 +1234,7 @@ hipError_t launch_kind(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvec
         fprintf(stderr, "fsst_kernel: static LDS present or attributes unavailable; cannot address LDS from 0\n");
         return hipErrorInvalidDeviceFunction;
     }
-    int dev = 0, cus = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, shmem) != hipSuccess) per_cu = 1;
-    }
+    int cus = device_cus(), per_cu = occupancy(reinterpret_cast<const void *>(kern), 64, shmem);
     if (how.grid_cus > 0) cus = std::min(cus, how.grid_cus);   // a CU-masked stream
     const int full = cus * std::max(1, per_cu);
     int wpc = how.waves_per_cu;
@@ -1369,11 +1365,8 @@ hipError_t launch_fused_t(const DevChunk *d_main, uint32_t nmain, const DevChunk
         return zero(fused_kernel<SMALL, X, false>) && zero(fused_kernel<SMALL, X, true>);
     }();
     if (!lds_at_zero) return hipErrorInvalidDeviceFunction;
-    int dev = 0, cus = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, shmem) != hipSuccess) per_cu = 1;
-    }
+    const int cus = device_cus();
+    int per_cu = occupancy(reinterpret_cast<const void *>(kern), 64, shmem);
     if (how.waves_per_cu > 0) per_cu = std::min(per_cu, how.waves_per_cu);
     const int grid = cus * std::max(1, per_cu);
     // waves starting on each queue (blockIdx & 15 < k: FSST first), and the
@@ -1648,12 +1641,7 @@ __global__ __launch_bounds__(64) void fsst_sp_kernel(const DevChunk *__restrict_
 hipError_t launch_fsst_sp(const DevChunk *d_chunks, uint32_t nchunks, uint32_t nvecs, uint32_t *d_err,
                           hipStream_t stream) {
     if (nchunks == 0 || nvecs == 0) return hipSuccess;
-    int dev = 0, cus = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fsst_sp_kernel, 64, kSpWave) != hipSuccess)
-            per_cu = 1;
-    }
+    const int cus = device_cus(), per_cu = occupancy(reinterpret_cast<const void *>(fsst_sp_kernel), 64, kSpWave);
     const int grid = std::min<int>(cus * std::max(1, per_cu), (int)nvecs);
     if (getenv("FLS_DEBUG"))
         fprintf(stderr, "DEBUG: fsst_sp_kernel: %d blocks of 1 wave (%d per CU, %u B LDS), %u vectors\n", grid, per_cu,

@@ -78,8 +78,8 @@ StrT make_string_t(const char *p, uint32_t n) {
 // then the D2H of its columns; batches of different slots overlap, so these
 // are summed stream time, not wall time).
 enum ProfPhase {
-    PROF_PIN_ALLOC, PROF_DEV_ALLOC, PROF_SETUP, PROF_STRTABS, PROF_IMAGE, PROF_STAGE_COPY, PROF_FILL, PROF_WAIT,
-    PROF_GPU_DECODE, PROF_D2H, PROF_N
+    PROF_PIN_ALLOC, PROF_DEV_ALLOC, PROF_SETUP, PROF_STRTABS, PROF_IMAGE, PROF_STAGE_COPY, PROF_FILL, PROF_FILL_DESC,
+    PROF_REFILL_LAT, PROF_WAIT, PROF_GPU_DECODE, PROF_D2H, PROF_N
 };
 struct ScanProf {
     std::atomic<uint64_t> ns[PROF_N] = {}, bytes[PROF_N] = {}, calls[PROF_N] = {};
@@ -89,7 +89,8 @@ struct ScanProf {
     }
     void print() {
         static const char *names[PROF_N] = {"pinned host alloc", "device alloc", "scan_setup", "string_t tables",
-                                            "resident image", "staging copy", "fill_batch (all)", "consumer wait",
+                                            "resident image", "staging copy", "fill_batch (all)",
+                                            "fill: descriptors", "batch seen -> refill", "consumer wait",
                                             "GPU decode (events)", "D2H (events)"};
         fprintf(stderr, "FLS_SCAN_PROFILE (process, since the last report):\n");
         for (int i = 0; i < PROF_N; ++i)
@@ -108,13 +109,16 @@ struct ProfTimer {
     explicit ProfTimer(int phase, uint64_t bytes = 0) : ph(ScanProf::on() ? phase : -1), b(bytes) {
         if (ph >= 0) t0 = std::chrono::steady_clock::now();
     }
-    ~ProfTimer() {
+    void stop() {  // record now (once)
         if (ph < 0) return;
         ScanProf &p = scan_prof();
         p.ns[ph] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         p.bytes[ph] += b;
         p.calls[ph] += 1;
+        ph = -1;
     }
+    void cancel() { ph = -1; }
+    ~ProfTimer() { stop(); }
 };
 
 // Frees every HBM-resident image no running scan uses on GPU dev (defined
@@ -481,6 +485,7 @@ struct ScanCtx {
     // batch: (device index, batch) until their last row group is handed out
     std::vector<std::pair<int, HostBatch *>> ready;
     bool early_refill = true;       // FLS_SCAN_EARLY_REFILL
+    bool spin_wait = false;         // FLS_SCAN_SPIN_WAIT (A/B): acquires poll the batch event
     uint32_t max_batches = 64;      // host-batch pool cap per GPU (FLS_SCAN_HOST_BATCHES)
     int nslots = 2;                 // device slots per GPU (FLS_SCAN_SLOTS, 1..ScanDev::kMaxSlots)
     // sticky error of a failed batch refill (scan_release): consumers waiting
@@ -1250,10 +1255,7 @@ hipError_t launch_all(const DevChunk *d_chunks, uint32_t nmain, uint32_t ntotal,
         if (g == 2 && sp && !h.queue) return launch_fsst_sp(dc, fc.n[g], fc.vecs[g], d_err, st);
         return launch_fsst(dc, fc.n[g], fc.vecs[g], d_err, st, h);
     };
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
+    const int cus = device_cus();
     const uint64_t fsst_vecs = fc.total_vecs();
     if (ov.cu_split > 0 && side && side->stream && nmain > 0 && fsst_vecs > 0 && !balanced && !sp &&
         !(policy & POLICY_STATIC))
@@ -1538,6 +1540,7 @@ int scan_setup(fls_table *t, ScanCtx &s, const std::vector<int> &devs, const uin
     }
     s.batch = (uint32_t)std::max<int64_t>(1, knob_value("FLS_SCAN_BATCH"));
     s.early_refill = knob_value("FLS_SCAN_EARLY_REFILL") != 0;
+    s.spin_wait = getenv("FLS_SCAN_SPIN_WAIT") && atoi(getenv("FLS_SCAN_SPIN_WAIT")) != 0;
     s.max_batches = (uint32_t)std::max<int64_t>(2, knob_value("FLS_SCAN_HOST_BATCHES"));
     s.nslots = (int)std::max<int64_t>(1, std::min<int64_t>(ScanDev::kMaxSlots, knob_value("FLS_SCAN_SLOTS")));
     for (uint32_t g = 0; g < G; ++g) {
@@ -1753,7 +1756,7 @@ int enqueue_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     return rc;
 }
 int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
-    ProfTimer prof(PROF_FILL);
+    ProfTimer prof(PROF_FILL), pdesc(PROF_FILL_DESC);
     Slot &sl = d.slots[si];
     HostBatch &hb = *sl.hb;
     const uint32_t ncols = (uint32_t)t->meta.cols.size();
@@ -1943,6 +1946,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
     const uint32_t nmain = order_for_launch(list, &fsst, policy);
     const size_t k = list.size();
     const SplitPlan plan = append_split(list, nmain, bc.geom, policy);
+    pdesc.stop();
     const size_t kk = list.size();
     HIP_TRY(sl.h_chunks.alloc(kk));
     HIP_TRY(sl.d_chunks.alloc(d.dev, kk));
@@ -2187,7 +2191,13 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
     auto wait_batch = [&]() -> int {
         HIP_TRY(hipSetDevice(d.dev));
         ProfTimer pw(PROF_WAIT);
-        HIP_TRY(hipEventSynchronize(hb->done));
+        if (s.spin_wait) {  // poll the event (A/B knob FLS_SCAN_SPIN_WAIT: the blocking wait's wake-up latency)
+            hipError_t q;
+            while ((q = hipEventQuery(hb->done)) == hipErrorNotReady) std::this_thread::yield();
+            HIP_TRY(q);
+        } else {
+            HIP_TRY(hipEventSynchronize(hb->done));
+        }
         if (hb->prof_pending.exchange(false)) {  // the batch's stream times, once
             float dec = 0, d2h = 0;
             if (hipEventElapsedTime(&dec, hb->pt[0], hb->pt[1]) == hipSuccess &&
@@ -2214,6 +2224,7 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
         s.cv.notify_all();
         return rc;
     }
+    ProfTimer seen(PROF_REFILL_LAT);  // this acquire saw the batch complete: until its refill starts
     // the batch's upload into the resident image is complete (its event covers
     // the H2D): later scans of this file may decode these row groups from it
     if (hb->upload_resident.exchange(false) && d.dimg)
@@ -2293,6 +2304,8 @@ int scan_acquire(fls_table *t, ScanCtx &s, fls_rowgroup *out) {
                 }
         s.cv.notify_all();
     }
+    if (!refill) seen.cancel();
+    seen.stop();
     if (refill) {  // the slot's next batch, outside s.mu (claim_batch)
         Slot &sl = d.slots[si];
         const int rc = fill_batch(t, s, d, si);
