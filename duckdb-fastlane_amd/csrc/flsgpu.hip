@@ -79,7 +79,7 @@ StrT make_string_t(const char *p, uint32_t n) {
 // are summed stream time, not wall time).
 enum ProfPhase {
     PROF_PIN_ALLOC, PROF_DEV_ALLOC, PROF_SETUP, PROF_STRTABS, PROF_IMAGE, PROF_STAGE_COPY, PROF_FILL, PROF_FILL_DESC,
-    PROF_REFILL_LAT, PROF_WAIT, PROF_GPU_DECODE, PROF_D2H, PROF_N
+    PROF_FILL_LIST, PROF_REFILL_LAT, PROF_WAIT, PROF_GPU_DECODE, PROF_D2H, PROF_N
 };
 struct ScanProf {
     std::atomic<uint64_t> ns[PROF_N] = {}, bytes[PROF_N] = {}, calls[PROF_N] = {};
@@ -90,7 +90,8 @@ struct ScanProf {
     void print() {
         static const char *names[PROF_N] = {"pinned host alloc", "device alloc", "scan_setup", "string_t tables",
                                             "resident image", "staging copy", "fill_batch (all)",
-                                            "fill: descriptors", "batch seen -> refill", "consumer wait",
+                                            "fill: descriptors", "fill: chunk list", "batch seen -> refill",
+                                            "consumer wait",
                                             "GPU decode (events)", "D2H (events)"};
         fprintf(stderr, "FLS_SCAN_PROFILE (process, since the last report):\n");
         for (int i = 0; i < PROF_N; ++i)
@@ -1928,6 +1929,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
         }
     std::vector<DevChunk> list;
     ByteCount bc;
+    ProfTimer plist(PROF_FILL_LIST);
     for (uint32_t c = 0; c < ncols; ++c) {
         if (!col_selected(s.dmask, c)) continue;
         for (uint32_t r = sl.rg0; r < sl.rg0 + sl.nrg; ++r) {
@@ -1941,6 +1943,7 @@ int fill_batch(fls_table *t, ScanCtx &s, ScanDev &d, int si) {
                                          sl.heap_bytes[c] ? hb.h_heap[c].p + ho : nullptr, code_w[c], d.ident.p));
         }
     }
+    plist.stop();
     FsstCounts fsst;
     const int64_t policy = launch_policy(decode_policy(), list, bc.geom);
     const uint32_t nmain = order_for_launch(list, &fsst, policy);
